@@ -1,0 +1,172 @@
+// Context, workspace, profiling and device-memory entry points of the C ABI.
+#include <cstring>
+
+#include "ctx.h"
+
+int ctx_ws(bpp_ctx* ctx, const char* name, size_t bytes, void** out) {
+  auto& b = ctx->ws[name];
+  if (b.bytes < bytes) {
+    if (b.p) BPP_HIP(hipFree(b.p));
+    b.p = nullptr;
+    b.bytes = 0;
+    size_t want = bytes + bytes / 8 + 256;
+    BPP_HIP(hipMalloc(&b.p, want));
+    b.bytes = want;
+  }
+  *out = b.p;
+  return BPP_OK;
+}
+
+int ctx_pinned(bpp_ctx* ctx, size_t bytes, void** out) {
+  if (ctx->pinned_bytes < bytes) {
+    if (ctx->pinned) BPP_HIP(hipHostFree(ctx->pinned));
+    ctx->pinned = nullptr;
+    ctx->pinned_bytes = 0;
+    BPP_HIP(hipHostMalloc(&ctx->pinned, bytes));
+    ctx->pinned_bytes = bytes;
+  }
+  *out = ctx->pinned;
+  return BPP_OK;
+}
+
+int ctx_check_launch(bpp_ctx* ctx, const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    ctx->err = std::string(what) + ": " + hipGetErrorString(e);
+    return BPP_ERR_DEVICE;
+  }
+  return BPP_OK;
+}
+
+static hipEvent_t ev_get(bpp_ctx* ctx) {
+  if (!ctx->ev_pool.empty()) {
+    hipEvent_t e = ctx->ev_pool.back();
+    ctx->ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  hipEventCreate(&e);
+  return e;
+}
+
+ProfScope::ProfScope(bpp_ctx* c, const char* n) : ctx(c), name(n) {
+  if (!ctx->prof) return;
+  a = ev_get(ctx);
+  b = ev_get(ctx);
+  hipEventRecord(a, ctx->stream);
+}
+
+ProfScope::~ProfScope() {
+  if (!ctx->prof || !a) return;
+  hipEventRecord(b, ctx->stream);
+  ctx->pending.push_back({name, a, b});
+}
+
+static void prof_resolve(bpp_ctx* ctx) {
+  if (ctx->pending.empty()) return;
+  hipStreamSynchronize(ctx->stream);
+  for (auto& p : ctx->pending) {
+    float ms = 0;
+    hipEventElapsedTime(&ms, p.a, p.b);
+    auto& acc = ctx->prof_acc[p.name];
+    acc.first += ms;
+    acc.second += 1;
+    ctx->ev_pool.push_back(p.a);
+    ctx->ev_pool.push_back(p.b);
+  }
+  ctx->pending.clear();
+}
+
+extern "C" {
+
+int bpp_ctx_create(int device, bpp_ctx** out) {
+  if (!out) return BPP_ERR_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return BPP_ERR_DEVICE;
+  if (hipSetDevice(device) != hipSuccess) return BPP_ERR_DEVICE;
+  bpp_ctx* ctx = new bpp_ctx();
+  ctx->device = device;
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    return BPP_ERR_DEVICE;
+  }
+  *out = ctx;
+  return BPP_OK;
+}
+
+void bpp_ctx_destroy(bpp_ctx* ctx) {
+  if (!ctx) return;
+  hipSetDevice(ctx->device);
+  hipStreamSynchronize(ctx->stream);
+  for (auto& kv : ctx->ws)
+    if (kv.second.p) hipFree(kv.second.p);
+  if (ctx->pinned) hipHostFree(ctx->pinned);
+  for (auto& p : ctx->pending) {
+    hipEventDestroy(p.a);
+    hipEventDestroy(p.b);
+  }
+  for (auto e : ctx->ev_pool) hipEventDestroy(e);
+  hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+const char* bpp_ctx_last_error(const bpp_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+void* bpp_ctx_stream(bpp_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int bpp_ctx_profile(bpp_ctx* ctx, int enable) {
+  if (!ctx) return BPP_ERR_ARG;
+  ctx->prof = enable != 0;
+  return BPP_OK;
+}
+
+int bpp_ctx_profile_get(bpp_ctx* ctx, const char* stage, double* ms, uint64_t* launches) {
+  if (!ctx || !stage) return BPP_ERR_ARG;
+  prof_resolve(ctx);
+  auto it = ctx->prof_acc.find(stage);
+  if (ms) *ms = it == ctx->prof_acc.end() ? 0.0 : it->second.first;
+  if (launches) *launches = it == ctx->prof_acc.end() ? 0 : it->second.second;
+  return BPP_OK;
+}
+
+void bpp_ctx_profile_reset(bpp_ctx* ctx) {
+  if (!ctx) return;
+  prof_resolve(ctx);
+  ctx->prof_acc.clear();
+}
+
+int bpp_dev_alloc(bpp_ctx* ctx, size_t bytes, void** dptr) {
+  if (!ctx || !dptr) return BPP_ERR_ARG;
+  BPP_HIP(hipSetDevice(ctx->device));
+  BPP_HIP(hipMalloc(dptr, bytes ? bytes : 1));
+  return BPP_OK;
+}
+
+int bpp_dev_free(bpp_ctx* ctx, void* dptr) {
+  if (!ctx) return BPP_ERR_ARG;
+  BPP_HIP(hipFree(dptr));
+  return BPP_OK;
+}
+
+int bpp_memcpy_htod(bpp_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  if (!ctx) return BPP_ERR_ARG;
+  BPP_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  BPP_HIP(hipStreamSynchronize(ctx->stream));
+  return BPP_OK;
+}
+
+int bpp_memcpy_dtoh(bpp_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  if (!ctx) return BPP_ERR_ARG;
+  BPP_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  BPP_HIP(hipStreamSynchronize(ctx->stream));
+  return BPP_OK;
+}
+
+int bpp_synchronize(bpp_ctx* ctx) {
+  if (!ctx) return BPP_ERR_ARG;
+  BPP_HIP(hipStreamSynchronize(ctx->stream));
+  return BPP_OK;
+}
+
+}  // extern "C"

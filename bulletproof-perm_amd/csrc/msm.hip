@@ -1,0 +1,251 @@
+// MSM engine (host orchestration of msm_kernels.cuh) and its C-ABI entry
+// points: bpp_msm, bpp_msm_table, bpp_msm_table_dev, bpp_msm_batch and the
+// window-partitioned variants used for multi-GPU.
+#include <cstring>
+
+#include "ctx.h"
+#include "host/fe64.h"
+#include "msm_kernels.cuh"
+#include "msm_engine.h"
+
+// Scalar field order l, little-endian 32-bit words.
+static const uint32_t L_WORDS[8] = {0x5cf5d3edu, 0x5812631au, 0xa2f79cd6u, 0x14def9deu,
+                                    0x00000000u, 0x00000000u, 0x00000000u, 0x10000000u};
+
+bool scalar_is_canonical(const uint8_t* s) {
+  uint32_t w[8];
+  memcpy(w, s, 32);
+  for (int i = 7; i >= 0; --i) {
+    if (w[i] < L_WORDS[i]) return true;
+    if (w[i] > L_WORDS[i]) return false;
+  }
+  return false;  // == l
+}
+
+uint32_t msm_choose_c(double n_per_msm) {
+  uint32_t best = 4;
+  double bestc = 1e300;
+  for (uint32_t c = 2; c <= 20; ++c) {
+    const uint32_t W = (254 + c - 1) / c;
+    const double cost = (double)W * (7.0 * n_per_msm + 9.0 * (double)(1u << c)) + 8.0 * c * (W - 1);
+    if (cost < bestc) {
+      bestc = cost;
+      best = c;
+    }
+  }
+  return best;
+}
+
+static unsigned grid_for(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
+
+int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const uint32_t* d_off, uint32_t M,
+               uint32_t T, uint32_t c, uint32_t wb, uint32_t Wn, const uint32_t* d_tbl, uint32_t** d_wsum_out) {
+  MsmGeom g;
+  g.M = M;
+  g.T = T;
+  g.c = c;
+  g.W = (254 + c - 1) / c;
+  g.wb = wb;
+  g.Wn = Wn;
+  g.B = 1u << (c - 1);
+  const size_t nseg = (size_t)M * Wn;
+  const size_t NB = nseg * g.B;
+  void *cnt, *cur, *boff, *entries, *bsum, *wsum;
+  BPP_TRY(ctx_ws(ctx, "msm_cnt", (NB + 1) * 4, &cnt));
+  BPP_TRY(ctx_ws(ctx, "msm_cur", NB * 4, &cur));
+  BPP_TRY(ctx_ws(ctx, "msm_boff", (NB + 1) * 4, &boff));
+  BPP_TRY(ctx_ws(ctx, "msm_entries", (size_t)T * Wn * 4 + 4, &entries));
+  BPP_TRY(ctx_ws(ctx, "msm_bsum", NB * 128, &bsum));
+  BPP_TRY(ctx_ws(ctx, "msm_wsum", nseg * 128, &wsum));
+  BPP_HIP(hipMemsetAsync(cnt, 0, (NB + 1) * 4, ctx->stream));
+  BPP_HIP(hipMemsetAsync(cur, 0, NB * 4, ctx->stream));
+  if (T) {
+    ProfScope ps(ctx, "msm_count");
+    hipLaunchKernelGGL(k_msm_count, dim3(grid_for(T, 256)), dim3(256), 0, ctx->stream, d_scal, d_off, g,
+                       (uint32_t*)cnt);
+  }
+  BPP_TRY(ctx_check_launch(ctx, "k_msm_count"));
+  {
+    ProfScope ps(ctx, "msm_scan");
+    BPP_TRY(scan_exclusive_u32(ctx, (const uint32_t*)cnt, (uint32_t*)boff, NB + 1));
+  }
+  if (T) {
+    ProfScope ps(ctx, "msm_scatter");
+    hipLaunchKernelGGL(k_msm_scatter, dim3(grid_for(T, 256)), dim3(256), 0, ctx->stream, d_scal, d_off, d_pidx, g,
+                       (const uint32_t*)boff, (uint32_t*)cur, (uint32_t*)entries);
+  }
+  BPP_TRY(ctx_check_launch(ctx, "k_msm_scatter"));
+  {
+    ProfScope ps(ctx, "msm_accumulate");
+    hipLaunchKernelGGL(k_msm_accumulate, dim3(grid_for(NB, 256)), dim3(256), 0, ctx->stream, d_tbl,
+                       (const uint32_t*)entries, (const uint32_t*)boff, (uint32_t)NB, (uint32_t*)bsum);
+  }
+  BPP_TRY(ctx_check_launch(ctx, "k_msm_accumulate"));
+  {
+    ProfScope ps(ctx, "msm_reduce");
+    if (g.B >= 256)
+      hipLaunchKernelGGL(k_msm_reduce<256>, dim3((unsigned)nseg), dim3(256), 0, ctx->stream, (const uint32_t*)bsum, g,
+                         (uint32_t*)wsum);
+    else if (g.B >= 64)
+      hipLaunchKernelGGL(k_msm_reduce<64>, dim3((unsigned)nseg), dim3(64), 0, ctx->stream, (const uint32_t*)bsum, g,
+                         (uint32_t*)wsum);
+    else
+      hipLaunchKernelGGL(k_msm_reduce<8>, dim3((unsigned)nseg), dim3(8), 0, ctx->stream, (const uint32_t*)bsum, g,
+                         (uint32_t*)wsum);
+  }
+  BPP_TRY(ctx_check_launch(ctx, "k_msm_reduce"));
+  *d_wsum_out = (uint32_t*)wsum;
+  return BPP_OK;
+}
+
+// Host Horner: sum_j 2^(c*(wb+j)) * ws[j], j < Wn.
+static h25519::ge horner_host(const uint32_t* ws_words, uint32_t Wn, uint32_t c, uint32_t wb) {
+  using namespace h25519;
+  ge acc = ge_from_words(ws_words + (size_t)(Wn - 1) * 32);
+  for (int j = (int)Wn - 2; j >= 0; --j) {
+    for (uint32_t k = 0; k < c; ++k) acc = ge_dbl(acc);
+    acc = ge_add(acc, ge_from_words(ws_words + (size_t)j * 32));
+  }
+  for (uint32_t k = 0; k < c * wb; ++k) acc = ge_dbl(acc);
+  return acc;
+}
+
+// Single MSM over device scalars + resident table, windows [wb, wb+Wn).
+int msm_single_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const uint32_t* d_tbl, size_t n,
+                   uint32_t c, uint32_t wb, uint32_t Wn, h25519::ge* out) {
+  if (n == 0 || Wn == 0) {
+    *out = h25519::ge_identity();
+    return BPP_OK;
+  }
+  uint32_t* d_ws = nullptr;
+  BPP_TRY(msm_engine(ctx, d_scal, d_pidx, nullptr, 1, (uint32_t)n, c, wb, Wn, d_tbl, &d_ws));
+  void* h = nullptr;
+  BPP_TRY(ctx_pinned(ctx, (size_t)Wn * 128, &h));
+  BPP_HIP(hipMemcpyAsync(h, d_ws, (size_t)Wn * 128, hipMemcpyDeviceToHost, ctx->stream));
+  BPP_HIP(hipStreamSynchronize(ctx->stream));
+  *out = horner_host((const uint32_t*)h, Wn, c, wb);
+  return BPP_OK;
+}
+
+int upload_scalars(bpp_ctx* ctx, const uint8_t* scalars, size_t n, const char* name, uint32_t** d_out) {
+  for (size_t i = 0; i < n; ++i)
+    if (!scalar_is_canonical(scalars + 32 * i)) {
+      ctx->err = "non-canonical scalar at index " + std::to_string(i);
+      return BPP_ERR_NONCANONICAL;
+    }
+  void* d = nullptr;
+  BPP_TRY(ctx_ws(ctx, name, n * 32 + 32, &d));
+  if (n) BPP_HIP(hipMemcpyAsync(d, scalars, n * 32, hipMemcpyHostToDevice, ctx->stream));
+  *d_out = (uint32_t*)d;
+  return BPP_OK;
+}
+
+extern "C" {
+
+int bpp_msm_windows(size_t n, uint32_t* c, uint32_t* windows) {
+  uint32_t cc = msm_choose_c((double)(n ? n : 1));
+  if (c) *c = cc;
+  if (windows) *windows = (254 + cc - 1) / cc;
+  return BPP_OK;
+}
+
+int bpp_msm_table_dev(bpp_ctx* ctx, const void* d_scalars, const bpp_points* tbl, size_t n, uint8_t out[32]) {
+  if (!ctx || !tbl || !out || (!d_scalars && n)) return BPP_ERR_ARG;
+  if (n > tbl->n || n >= 0x80000000ull) return BPP_ERR_LEN;
+  BPP_HIP(hipSetDevice(ctx->device));
+  const uint32_t c = msm_choose_c((double)n);
+  const uint32_t W = (254 + c - 1) / c;
+  h25519::ge r;
+  BPP_TRY(msm_single_dev(ctx, (const uint32_t*)d_scalars, nullptr, tbl->d, n, c, 0, W, &r));
+  h25519::encode(out, r);
+  return BPP_OK;
+}
+
+int bpp_msm_table_dev_partial(bpp_ctx* ctx, const void* d_scalars, const bpp_points* tbl, size_t n, uint32_t w_begin,
+                              uint32_t w_end, uint8_t partial[128]) {
+  if (!ctx || !tbl || !partial || (!d_scalars && n)) return BPP_ERR_ARG;
+  if (n > tbl->n || n >= 0x80000000ull) return BPP_ERR_LEN;
+  const uint32_t c = msm_choose_c((double)n);
+  const uint32_t W = (254 + c - 1) / c;
+  if (w_begin > w_end || w_end > W) return BPP_ERR_ARG;
+  BPP_HIP(hipSetDevice(ctx->device));
+  h25519::ge r;
+  BPP_TRY(msm_single_dev(ctx, (const uint32_t*)d_scalars, nullptr, tbl->d, n, c, w_begin, w_end - w_begin, &r));
+  h25519::ge_to_words((uint32_t*)partial, r);
+  return BPP_OK;
+}
+
+int bpp_partials_finish(const uint8_t* partials, size_t count, uint8_t out[32]) {
+  if (!out || (!partials && count)) return BPP_ERR_ARG;
+  h25519::ge acc = h25519::ge_identity();
+  for (size_t i = 0; i < count; ++i) {
+    uint32_t w[32];
+    memcpy(w, partials + 128 * i, 128);
+    acc = h25519::ge_add(acc, h25519::ge_from_words(w));
+  }
+  h25519::encode(out, acc);
+  return BPP_OK;
+}
+
+int bpp_msm_table(bpp_ctx* ctx, const uint8_t* scalars, const bpp_points* tbl, size_t n, uint8_t out[32]) {
+  if (!ctx || !tbl || !out || (!scalars && n)) return BPP_ERR_ARG;
+  if (n > tbl->n) return BPP_ERR_LEN;
+  BPP_HIP(hipSetDevice(ctx->device));
+  uint32_t* d_s = nullptr;
+  BPP_TRY(upload_scalars(ctx, scalars, n, "msm_scal", &d_s));
+  return bpp_msm_table_dev(ctx, d_s, tbl, n, out);
+}
+
+int bpp_msm(bpp_ctx* ctx, const uint8_t* scalars, const uint8_t* points, size_t n, uint8_t out[32]) {
+  if (!ctx || !out || ((!scalars || !points) && n)) return BPP_ERR_ARG;
+  bpp_points* tbl = nullptr;
+  size_t bad = 0;
+  BPP_TRY(bpp_points_decompress(ctx, points, n, &tbl, &bad));
+  int rc = bpp_msm_table(ctx, scalars, tbl, n, out);
+  bpp_points_destroy(tbl);
+  return rc;
+}
+
+int bpp_msm_batch(bpp_ctx* ctx, size_t count, const uint64_t* offsets, const uint8_t* scalars,
+                  const uint32_t* point_idx, const bpp_points* tbl, uint8_t* out) {
+  if (!ctx || !offsets || !tbl || (!out && count)) return BPP_ERR_ARG;
+  if (count == 0) return BPP_OK;
+  const uint64_t T = offsets[count];
+  if (offsets[0] != 0 || T >= 0x80000000ull) return BPP_ERR_LEN;
+  for (size_t j = 0; j < count; ++j)
+    if (offsets[j + 1] < offsets[j]) return BPP_ERR_LEN;
+  for (uint64_t t = 0; t < T; ++t)
+    if (point_idx[t] >= tbl->n) return BPP_ERR_LEN;
+  BPP_HIP(hipSetDevice(ctx->device));
+  uint32_t* d_s = nullptr;
+  BPP_TRY(upload_scalars(ctx, scalars, T, "msmb_scal", &d_s));
+  void *d_idx, *d_off, *d_res;
+  BPP_TRY(ctx_ws(ctx, "msmb_idx", T * 4 + 4, &d_idx));
+  BPP_TRY(ctx_ws(ctx, "msmb_off", (count + 1) * 4, &d_off));
+  BPP_TRY(ctx_ws(ctx, "msmb_res", count * 128, &d_res));
+  std::vector<uint32_t> off32(count + 1);
+  for (size_t j = 0; j <= count; ++j) off32[j] = (uint32_t)offsets[j];
+  if (T) BPP_HIP(hipMemcpyAsync(d_idx, point_idx, T * 4, hipMemcpyHostToDevice, ctx->stream));
+  BPP_HIP(hipMemcpyAsync(d_off, off32.data(), (count + 1) * 4, hipMemcpyHostToDevice, ctx->stream));
+  const uint32_t c = msm_choose_c((double)T / (double)count);
+  const uint32_t W = (254 + c - 1) / c;
+  MsmGeom g;
+  g.M = (uint32_t)count;
+  g.T = (uint32_t)T;
+  g.c = c;
+  g.W = W;
+  g.wb = 0;
+  g.Wn = W;
+  g.B = 1u << (c - 1);
+  uint32_t* d_ws = nullptr;
+  BPP_TRY(msm_engine(ctx, d_s, (const uint32_t*)d_idx, (const uint32_t*)d_off, g.M, g.T, c, 0, W, tbl->d, &d_ws));
+  {
+    ProfScope ps(ctx, "msm_horner");
+    hipLaunchKernelGGL(k_msm_horner, dim3(grid_for(count, 64)), dim3(64), 0, ctx->stream, (const uint32_t*)d_ws, g,
+                       (uint32_t*)d_res);
+  }
+  BPP_TRY(ctx_check_launch(ctx, "k_msm_horner"));
+  return points_compress_p3(ctx, (const uint32_t*)d_res, count, out);
+}
+
+}  // extern "C"

@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""bench.py — Ristretto MSM pairs/s on MI355X (+ CPU baseline, roofline).
+
+Metric (BASELINE.json): "permutation proofs/sec + Ristretto MSM pairs/sec at
+1/2/4/8 MI355X".  `value` is MSM scalar-point pairs/s of one step = one full
+multiscalar multiplication over synthetic uniform scalars and distinct
+hash-to-group points already resident in HBM (2^20
+pairs on one GPU).  At N GPUs the MSM has 2^20*N pairs and its bucket
+windows are partitioned across the ranks (config 5 shape: 2^22 at N=4); each
+rank computes the partial sum of its windows and the 128-byte partial points
+are all-gathered over RCCL and added (RCCL cannot add curve points), so
+per-GPU work is fixed: "scaling": "weak".
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--log2n 20]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "bulletproof-perm_amd"))
+
+L = 2**252 + 27742317777372353535851937790883648493
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def synth_scalars(n: int, seed: int) -> bytes:
+    """Uniform scalars = from_bytes_mod_order_wide(SHAKE256 bytes) (dalek
+    Scalar::random shape), serialized canonical little-endian."""
+    raw = hashlib.shake_256(b"bench-scalars" + seed.to_bytes(8, "little")).digest(64 * n)
+    out = bytearray(32 * n)
+    for i in range(n):
+        s = int.from_bytes(raw[64 * i: 64 * i + 64], "little") % L
+        out[32 * i: 32 * i + 32] = s.to_bytes(32, "little")
+    return bytes(out)
+
+
+def synth_point_bytes(n: int, seed: int) -> bytes:
+    """64 uniform bytes per point -> RistrettoPoint::from_uniform_bytes (on GPU)."""
+    return hashlib.shake_256(b"bench-points" + seed.to_bytes(8, "little")).digest(64 * n)
+
+
+def load_traffic(stage: str, log2n: int):
+    """HBM bytes per launch from the committed rocprofv3 --pmc summary."""
+    p = ROOT / "profiles" / "pmc_summary.json"
+    if not p.exists():
+        return None
+    try:
+        d = json.loads(p.read_text())
+        return d.get(f"{stage}@2^{log2n}", {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(seconds: float = 15.0):
+    """Serial C restatement of dalek-ng's Pippenger (oracle/c, 'port') timed
+    on a bounded sample of the same workload: one 2^16-pair MSM, repeated
+    until ~`seconds` of CPU time, 1 thread."""
+    try:
+        sys.path.insert(0, str(ROOT))
+        from oracle import cport
+    except Exception as e:  # pragma: no cover
+        return {"value": None, "unit": "pairs/s", "cores": 1, "kind": "port", "sample": f"unavailable: {e}"}
+    return cport.bench_msm(log2n=16, seconds=seconds)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--log2n", type=int, default=20, help="pairs per GPU = 2^log2n")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--verify", action="store_true", help="also recompute via a second window split")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    import bpperm
+
+    n = (1 << args.log2n) * world
+    ctx = bpperm.Context(local)
+
+    # ---- inputs resident in HBM before the timed region
+    t0 = time.time()
+    pts = ctx.from_uniform(synth_point_bytes(n, 3))
+    sc = synth_scalars(n, 2)
+    d_sc = ctx.dev_alloc(len(sc))
+    ctx.htod(d_sc, sc)
+    setup_s = time.time() - t0
+
+    c, W = bpperm.msm_windows(n)
+    # contiguous window ranges per rank
+    cuts = [(W * r) // world for r in range(world + 1)]
+    wb, we = cuts[rank], cuts[rank + 1]
+
+    def step():
+        if world == 1:
+            return ctx.msm_table_dev(d_sc, pts, n)
+        part = ctx.msm_table_dev_partial(d_sc, pts, n, wb, we)
+        t = torch.frombuffer(bytearray(part), dtype=torch.uint8).cuda()
+        gathered = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(gathered, t)
+        return bpperm.partials_finish([g.cpu().numpy().tobytes() for g in gathered])
+
+    for _ in range(args.warmup):
+        res = step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = tt.item()
+
+    # ---- per-kernel timing (HIP events on the library stream), separate pass
+    ctx.profile(True)
+    ctx.profile_reset()
+    prof_steps = max(2, min(args.steps, 5))
+    for _ in range(prof_steps):
+        if world == 1:
+            ctx.msm_table_dev(d_sc, pts, n)
+        else:
+            ctx.msm_table_dev_partial(d_sc, pts, n, wb, we)
+    stages = {}
+    for st in ("msm_count", "msm_scan", "msm_scatter", "msm_accumulate", "msm_reduce"):
+        ms, k = ctx.profile_get(st)
+        stages[st] = ms / max(k, 1)
+    ctx.profile(False)
+
+    ms_step = el / args.steps * 1e3
+    value = n * args.steps / el
+    acc_ms = stages["msm_accumulate"]
+    algo_bytes = 96 * n  # 32 B scalar + 64 B affine point per pair
+    achieved = algo_bytes / (acc_ms * 1e-3) / 1e9 if acc_ms > 0 else None
+
+    line = {
+        "metric": "Ristretto MSM scalar-point pairs/sec",
+        "value": value,
+        "unit": "pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32 limbs (GF(2^255-19) integer)",
+        "data": "synthetic: uniform scalars (SHAKE256 -> mod l), hash-to-group points (from_uniform_bytes on GPU)",
+        "config": {"workload": f"ristretto255 Pippenger MSM, 2^{args.log2n} pairs per GPU (config 3; config 5 shape at N=4)",
+                   "pairs": n, "window_bits": c, "windows": W, "parallelism": f"window-partition x{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                     "traffic": load_traffic("msm_accumulate", args.log2n),
+                     "kernel": "k_msm_accumulate", "kernel_ms": acc_ms,
+                     "algo_bytes_per_launch": algo_bytes},
+        "stage_ms": stages,
+        "setup_s": setup_s,
+        "result_prefix": res.hex()[:16],
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    ctx.dev_free(d_sc)
+    pts.close()
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

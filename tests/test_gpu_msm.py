@@ -107,3 +107,15 @@ def test_msm_window_partials(ctx):
     assert bpperm.partials_finish(parts) == full
     assert full == r255.encode(r255.msm_pippenger(sc, pts, 6))
     ctx.dev_free(d)
+
+
+def test_msm_golden_vectors(ctx):
+    import json
+    from pathlib import Path
+    cases = json.loads((Path(__file__).parent / "golden" / "msm.json").read_text())["cases"]
+    for case in cases:
+        pts = bytes.fromhex(case["points"])
+        tbl = ctx.from_uniform(bytes.fromhex(case["uniform"]))
+        assert b"".join(tbl.compress()) == pts
+        assert ctx.msm(bytes.fromhex(case["scalars"]), pts).hex() == case["result"], case["n"]
+        assert ctx.msm_table(bytes.fromhex(case["scalars"]), tbl).hex() == case["result"], case["n"]

@@ -217,3 +217,187 @@ def default_context() -> Context:
 def vartime_multiscalar_mul(scalars, points) -> bytes:
     """`RistrettoPoint::vartime_multiscalar_mul(scalars, points).compress()`."""
     return default_context().msm(scalars, points)
+
+
+# ------------------------------------------------------------------ protocol
+class Transcript:
+    """merlin 3.0.0 `Transcript` on the host side of libbpperm (byte-exact;
+    transcript_protocol.rs TranscriptProtocol helpers included)."""
+
+    def __init__(self, label: bytes = b"", _handle=None):
+        self.lib = _lib.load()
+        self.h = C.c_void_p(_handle) if _handle else C.c_void_p(self.lib.bpp_transcript_new(_buf(label), len(label)))
+
+    def clone(self) -> "Transcript":
+        return Transcript(_handle=self.lib.bpp_transcript_clone(self.h))
+
+    def close(self):
+        if self.h:
+            self.lib.bpp_transcript_destroy(self.h)
+            self.h = C.c_void_p(0)
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def append_message(self, label: bytes, msg: bytes):
+        check(self.lib.bpp_transcript_append_message(self.h, _buf(label), len(label), _buf(msg), len(msg)),
+              "append_message")
+
+    def append_u64(self, label: bytes, x: int):
+        check(self.lib.bpp_transcript_append_u64(self.h, _buf(label), len(label), x), "append_u64")
+
+    def challenge_bytes(self, label: bytes, n: int) -> bytes:
+        out = C.create_string_buffer(n)
+        check(self.lib.bpp_transcript_challenge_bytes(self.h, _buf(label), len(label), out, n), "challenge_bytes")
+        return out.raw
+
+    def challenge_scalar(self, label: bytes) -> bytes:
+        out = C.create_string_buffer(32)
+        check(self.lib.bpp_transcript_challenge_scalar(self.h, _buf(label), len(label), out), "challenge_scalar")
+        return out.raw
+
+    # TranscriptProtocol (transcript_protocol.rs)
+    def arithmetic_domain_sep(self, n: int):
+        self.append_message(b"dom-sep", b"acp v1")
+        self.append_u64(b"n", n)
+
+    def append_scalar(self, label: bytes, s: bytes):
+        self.append_message(label, s)
+
+    def append_point(self, label: bytes, p: bytes):
+        self.append_message(label, p)
+
+
+class Gens:
+    """BulletproofGens(n, 1) + PedersenGens resident on the GPU (bpp_gens)."""
+
+    def __init__(self, ctx: Context, n: int | None = None, points=None):
+        self.ctx = ctx
+        h = C.c_void_p()
+        if points is None:
+            check(ctx.lib.bpp_gens_create(ctx.h, n, C.byref(h)), "bpp_gens_create", ctx.h)
+        else:
+            G, H, B, Bb = points
+            g = _join(G, 32, "G")
+            hh = _join(H, 32, "H")
+            check(ctx.lib.bpp_gens_from_points(ctx.h, _buf(g), _buf(hh), len(g) // 32, _buf(B), _buf(Bb),
+                                               C.byref(h)), "bpp_gens_from_points", ctx.h)
+        self.h = h
+
+    def __len__(self):
+        return int(self.ctx.lib.bpp_gens_len(self.h))
+
+    def export(self):
+        n = len(self)
+        out = C.create_string_buffer(32 * (2 * n + 2))
+        check(self.ctx.lib.bpp_gens_export(self.ctx.h, self.h, out), "bpp_gens_export", self.ctx.h)
+        raw = out.raw
+        pts = [raw[32 * i: 32 * i + 32] for i in range(2 * n + 2)]
+        return pts[:n], pts[n: 2 * n], pts[2 * n], pts[2 * n + 1]
+
+    def close(self):
+        if self.h:
+            self.ctx.lib.bpp_gens_destroy(self.h)
+            self.h = C.c_void_p(0)
+
+    def pedersen_commit(self, v, gamma) -> list[bytes]:
+        """PedersenGens::commit over a batch (weights.rs:58-61)."""
+        vb = _join(v, 32, "v")
+        gb = _join(gamma, 32, "gamma")
+        m = len(vb) // 32
+        if len(gb) // 32 != m:
+            raise BppError(2, "bpp_pedersen_commit_batch", "length mismatch")
+        out = C.create_string_buffer(32 * max(m, 1))
+        check(self.ctx.lib.bpp_pedersen_commit_batch(self.ctx.h, self.h, _buf(vb), _buf(gb), m, out),
+              "bpp_pedersen_commit_batch", self.ctx.h)
+        return [out.raw[32 * i: 32 * i + 32] for i in range(m)]
+
+    def vec_commit(self, blind: bytes, a, b=None) -> bytes:
+        ab = _join(a, 32, "a")
+        bb = _join(b, 32, "b") if b is not None else None
+        out = C.create_string_buffer(32)
+        check(self.ctx.lib.bpp_vec_commit(self.ctx.h, self.h, _buf(blind), _buf(ab), _buf(bb) if bb else None,
+                                          len(ab) // 32, out), "bpp_vec_commit", self.ctx.h)
+        return out.raw
+
+    def ipa_prove(self, tr: Transcript, Q: bytes, G_factors, H_factors, a, b):
+        """InnerProductProof::create -> (L list, R list, a, b)."""
+        ab, bb = _join(a, 32, "a"), _join(b, 32, "b")
+        n = len(ab) // 32
+        gf = _join(G_factors, 32, "G_factors") if G_factors is not None else None
+        hf = _join(H_factors, 32, "H_factors") if H_factors is not None else None
+        lg = max(n.bit_length() - 1, 0)
+        Lo = C.create_string_buffer(32 * max(lg, 1))
+        Ro = C.create_string_buffer(32 * max(lg, 1))
+        ao, bo = C.create_string_buffer(32), C.create_string_buffer(32)
+        check(self.ctx.lib.bpp_ipa_prove(self.ctx.h, self.h, tr.h, _buf(Q), _buf(gf) if gf else None,
+                                         _buf(hf) if hf else None, _buf(ab), _buf(bb), n, Lo, Ro, ao, bo),
+              "bpp_ipa_prove", self.ctx.h)
+        return ([Lo.raw[32 * i: 32 * i + 32] for i in range(lg)], [Ro.raw[32 * i: 32 * i + 32] for i in range(lg)],
+                ao.raw, bo.raw)
+
+    def ipa_verify(self, tr: Transcript, n: int, G_factors, H_factors, P: bytes, Q: bytes, L, R, a: bytes,
+                   b: bytes) -> bool:
+        gf = _join(G_factors, 32, "G_factors") if G_factors is not None else None
+        hf = _join(H_factors, 32, "H_factors") if H_factors is not None else None
+        rc = self.ctx.lib.bpp_ipa_verify(self.ctx.h, self.h, tr.h, n, _buf(gf) if gf else None,
+                                         _buf(hf) if hf else None, _buf(P), _buf(Q), _buf(b"".join(L)),
+                                         _buf(b"".join(R)), _buf(a), _buf(b))
+        if rc == 6:
+            return False
+        check(rc, "bpp_ipa_verify", self.ctx.h)
+        return True
+
+
+class PermProver:
+    """Permutation proof over resident generators — the sound-mode restatement
+    of ACProof::ArithmeticCircuitProof (circuit_lib.rs:139-585)."""
+
+    def __init__(self, gens: Gens, k: int, label: bytes = b"bp-perm"):
+        self.gens = gens
+        self.ctx = gens.ctx
+        self.k = k
+        self.label = label
+        self.proof_len = int(self.ctx.lib.bpp_perm_proof_len(k))
+        self.m = 2 * k + 1
+
+    def prove(self, seed: int):
+        """-> (proof bytes, [V_j], permutation)"""
+        pf = C.create_string_buffer(self.proof_len)
+        V = C.create_string_buffer(32 * self.m)
+        perm = (C.c_uint32 * self.k)()
+        check(self.ctx.lib.bpp_perm_prove(self.ctx.h, self.gens.h, self.k, seed, _buf(self.label), len(self.label),
+                                          pf, V, perm), "bpp_perm_prove", self.ctx.h)
+        return pf.raw, [V.raw[32 * j: 32 * j + 32] for j in range(self.m)], list(perm)
+
+    def prove_batch(self, seeds: Sequence[int]):
+        cnt = len(seeds)
+        pf = C.create_string_buffer(self.proof_len * cnt)
+        V = C.create_string_buffer(32 * self.m * cnt)
+        sd = (C.c_uint64 * cnt)(*seeds)
+        check(self.ctx.lib.bpp_perm_prove_batch(self.ctx.h, self.gens.h, self.k, cnt, sd, _buf(self.label),
+                                                len(self.label), pf, V), "bpp_perm_prove_batch", self.ctx.h)
+        return ([pf.raw[i * self.proof_len:(i + 1) * self.proof_len] for i in range(cnt)],
+                [V.raw[i * 32 * self.m:(i + 1) * 32 * self.m] for i in range(cnt)])
+
+    def verify(self, proof: bytes, V) -> bool:
+        vb = _join(V, 32, "V")
+        rc = self.ctx.lib.bpp_perm_verify(self.ctx.h, self.gens.h, self.k, _buf(self.label), len(self.label),
+                                          _buf(proof), len(proof), _buf(vb))
+        if rc == 6:
+            return False
+        check(rc, "bpp_perm_verify", self.ctx.h)
+        return True
+
+    def verify_batch(self, proofs: Sequence[bytes], Vs: Sequence[bytes]) -> bool:
+        pb = b"".join(proofs)
+        vb = b"".join(Vs)
+        rc = self.ctx.lib.bpp_perm_verify_batch(self.ctx.h, self.gens.h, self.k, len(proofs), _buf(self.label),
+                                                len(self.label), _buf(pb), _buf(vb))
+        if rc == 6:
+            return False
+        check(rc, "bpp_perm_verify_batch", self.ctx.h)
+        return True

@@ -55,6 +55,27 @@ SIGNATURES = {
     "bpp_msm_table_dev_partial": (i32, [vp, vp, vp, sz, u32, u32, vp]),
     "bpp_partials_finish": (i32, [vp, sz, vp]),
     "bpp_msm_batch": (i32, [vp, sz, vp, vp, vp, vp, vp]),
+    "bpp_gens_create": (i32, [vp, sz, C.POINTER(vp)]),
+    "bpp_gens_from_points": (i32, [vp, vp, vp, sz, vp, vp, C.POINTER(vp)]),
+    "bpp_gens_len": (sz, [vp]),
+    "bpp_gens_export": (i32, [vp, vp, vp]),
+    "bpp_gens_destroy": (None, [vp]),
+    "bpp_pedersen_commit_batch": (i32, [vp, vp, vp, vp, sz, vp]),
+    "bpp_vec_commit": (i32, [vp, vp, vp, vp, vp, sz, vp]),
+    "bpp_transcript_new": (vp, [vp, sz]),
+    "bpp_transcript_clone": (vp, [vp]),
+    "bpp_transcript_destroy": (None, [vp]),
+    "bpp_transcript_append_message": (i32, [vp, vp, sz, vp, sz]),
+    "bpp_transcript_append_u64": (i32, [vp, vp, sz, u64]),
+    "bpp_transcript_challenge_bytes": (i32, [vp, vp, sz, vp, sz]),
+    "bpp_transcript_challenge_scalar": (i32, [vp, vp, sz, vp]),
+    "bpp_ipa_prove": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, vp]),
+    "bpp_ipa_verify": (i32, [vp, vp, vp, sz, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "bpp_perm_proof_len": (sz, [u32]),
+    "bpp_perm_prove": (i32, [vp, vp, u32, u64, vp, sz, vp, vp, vp]),
+    "bpp_perm_prove_batch": (i32, [vp, vp, u32, sz, vp, vp, sz, vp, vp]),
+    "bpp_perm_verify": (i32, [vp, vp, u32, vp, sz, vp, sz, vp]),
+    "bpp_perm_verify_batch": (i32, [vp, vp, u32, sz, vp, sz, vp, vp]),
 }
 
 _lib = None

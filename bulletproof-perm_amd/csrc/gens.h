@@ -1,0 +1,24 @@
+// Internal view of bpp_gens (see gens.hip).
+#pragma once
+#include <stdint.h>
+
+#include <vector>
+
+#include "ctx.h"
+#include "msm_engine.h"
+
+#define FB_POS 64  // radix-16 positions per fixed base
+
+struct bpp_gens {
+  bpp_ctx* ctx = nullptr;
+  size_t n = 0;
+  uint32_t* d_tbl = nullptr;  // (2n+2) affine Niels: G[0..n) H[n..2n) B[2n] Bb[2n+1]
+  uint32_t* d_fb = nullptr;   // fixed-base tables for B and Bb: 2 x 64 x 8 Niels
+  uint32_t gidx(size_t i) const { return (uint32_t)i; }
+  uint32_t hidx(size_t i) const { return (uint32_t)(n + i); }
+  uint32_t bidx() const { return (uint32_t)(2 * n); }
+  uint32_t bbidx() const { return (uint32_t)(2 * n + 1); }
+};
+
+int pedersen_dev(bpp_ctx* ctx, const bpp_gens* g, const uint32_t* d_v, const uint32_t* d_gam, size_t m,
+                 uint32_t* d_out_enc, uint32_t* d_out_p3);

@@ -1,0 +1,252 @@
+// Generators resident in HBM + fixed-base Pedersen commitments.
+//
+// bpp_gens = BulletproofGens::new(n, 1) (G_vec, H_vec from SHAKE256
+// GeneratorsChain "G"||0u32 / "H"||0u32) + PedersenGens::default() (B, B_blinding
+// = hash_from_bytes::<Sha3_512>(B.compress())), or explicit points as the
+// reference's test builds them (lib.rs:163-180, random G/H and a random
+// PedersenGens).  Table layout (affine Niels): G[0..n) H[n..2n) B[2n] Bb[2n+1].
+//
+// Pedersen commitments V = v*B + gamma*Bb (weights.rs:58-61,
+// PedersenGens::commit) and T_i = t_i*g + tau_i*h (circuit_lib.rs:363-413) are
+// fixed-base: per base a table of d*16^i*P (i < 64, d = 1..8) turns each
+// commitment into 2 x 64 mixed additions with signed radix-16 digits and no
+// doublings; one lane per commitment.
+#include <cstring>
+
+#include "ctx.h"
+#include "gens.h"
+#include "ge_io.cuh"
+#include "host/merlin.h"
+
+static unsigned grid_for(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
+
+// declared in points.hip
+__global__ void k_decompress(const uint32_t* __restrict__ enc, size_t n, uint32_t* __restrict__ tbl,
+                             unsigned long long* __restrict__ bad);
+__global__ void k_from_uniform(const uint32_t* __restrict__ bytes, size_t n, uint32_t* __restrict__ tbl);
+
+// thread t: base = t / 512, pos = (t / 8) % 64, d = t % 8 + 1 -> d * 16^pos * P_base
+__global__ void k_fb_tables(const uint32_t* __restrict__ tbl, uint32_t b0, uint32_t b1, uint32_t* __restrict__ fb) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 2 * FB_POS * 8) return;
+  const uint32_t base = t / (FB_POS * 8), pos = (t / 8) % FB_POS, d = t % 8 + 1;
+  const ge_niels P = load_niels(tbl, base ? b1 : b0);
+  ge_p3 acc = ge_identity();
+  for (uint32_t i = 0; i < d; ++i) acc = ge_madd(acc, P);
+  for (uint32_t i = 0; i < 4 * pos; ++i) acc = ge_dbl(acc);
+  store_niels(fb, t, ge_to_niels(acc));
+}
+
+FE_INLINE void radix16(const uint32_t s[8], int8_t e[64]) {
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) {
+    _Pragma("unroll") for (int j = 0; j < 8; ++j) e[8 * i + j] = (int8_t)((s[i] >> (4 * j)) & 15u);
+  }
+  int carry = 0;
+  _Pragma("unroll") for (int i = 0; i < 63; ++i) {
+    int v = e[i] + carry;
+    carry = (v + 8) >> 4;
+    e[i] = (int8_t)(v - (carry << 4));
+  }
+  e[63] = (int8_t)(e[63] + carry);
+}
+
+FE_INLINE ge_p3 fb_mul_add(ge_p3 acc, const uint32_t* __restrict__ fb, uint32_t base, const int8_t e[64]) {
+  for (int i = 0; i < 64; ++i) {
+    const int d = e[i];
+    if (d == 0) continue;
+    const uint32_t idx = base * FB_POS * 8 + (uint32_t)i * 8 + (uint32_t)((d < 0 ? -d : d) - 1);
+    const ge_niels q = load_niels(fb, idx);
+    acc = d < 0 ? ge_msub(acc, q) : ge_madd(acc, q);
+  }
+  return acc;
+}
+
+// out[j] = compress(v_j * B + g_j * Bb); scalars canonical (8 words each)
+__global__ void __launch_bounds__(256) k_pedersen(const uint32_t* __restrict__ fb, const uint32_t* __restrict__ v,
+                                                 const uint32_t* __restrict__ gam, size_t m,
+                                                 uint32_t* __restrict__ out_enc, uint32_t* __restrict__ out_p3) {
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  uint32_t s[8];
+  int8_t e[64];
+  ge_p3 acc = ge_identity();
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) s[i] = v[8 * j + i];
+  radix16(s, e);
+  acc = fb_mul_add(acc, fb, 0, e);
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) s[i] = gam[8 * j + i];
+  radix16(s, e);
+  acc = fb_mul_add(acc, fb, 1, e);
+  if (out_p3) store_p3(out_p3, j, acc);
+  if (out_enc) {
+    uint32_t w[8];
+    ge_ristretto_encode(acc, w);
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) out_enc[8 * j + i] = w[i];
+  }
+}
+
+static int gens_alloc(bpp_ctx* ctx, size_t n, bpp_gens** out) {
+  bpp_gens* g = new bpp_gens();
+  g->ctx = ctx;
+  g->n = n;
+  if (hipMalloc(&g->d_tbl, (2 * n + 2) * MSM_NIELS_WORDS * 4) != hipSuccess ||
+      hipMalloc(&g->d_fb, 2 * FB_POS * 8 * MSM_NIELS_WORDS * 4) != hipSuccess) {
+    if (g->d_tbl) hipFree(g->d_tbl);
+    delete g;
+    ctx->err = "hipMalloc generators";
+    return BPP_ERR_NOMEM;
+  }
+  *out = g;
+  return BPP_OK;
+}
+
+static int gens_finish(bpp_ctx* ctx, bpp_gens* g) {
+  {
+    ProfScope ps(ctx, "fb_tables");
+    hipLaunchKernelGGL(k_fb_tables, dim3(grid_for(2 * FB_POS * 8, 64)), dim3(64), 0, ctx->stream, g->d_tbl,
+                       (uint32_t)(2 * g->n), (uint32_t)(2 * g->n + 1), g->d_fb);
+  }
+  BPP_TRY(ctx_check_launch(ctx, "k_fb_tables"));
+  BPP_HIP(hipStreamSynchronize(ctx->stream));
+  return BPP_OK;
+}
+
+int pedersen_dev(bpp_ctx* ctx, const bpp_gens* g, const uint32_t* d_v, const uint32_t* d_gam, size_t m,
+                 uint32_t* d_out_enc, uint32_t* d_out_p3) {
+  if (!m) return BPP_OK;
+  {
+    ProfScope ps(ctx, "pedersen");
+    hipLaunchKernelGGL(k_pedersen, dim3(grid_for(m, 64)), dim3(64), 0, ctx->stream, g->d_fb, d_v, d_gam, m, d_out_enc,
+                       d_out_p3);
+  }
+  return ctx_check_launch(ctx, "k_pedersen");
+}
+
+void gens_chain_bytes(const char* label, uint32_t party, size_t n, uint8_t* out64) {
+  merlin::Shake256 sh;
+  sh.update((const uint8_t*)"GeneratorsChain", 15);
+  uint8_t lab[5] = {(uint8_t)label[0], 0, 0, 0, 0};
+  memcpy(lab + 1, &party, 4);
+  sh.update(lab, 5);
+  sh.read(out64, 64 * n);
+}
+
+extern "C" {
+
+int bpp_gens_create(bpp_ctx* ctx, size_t n, bpp_gens** out) {
+  if (!ctx || !out || n == 0 || n >= (1u << 28)) return BPP_ERR_ARG;
+  *out = nullptr;
+  BPP_HIP(hipSetDevice(ctx->device));
+  bpp_gens* g = nullptr;
+  BPP_TRY(gens_alloc(ctx, n, &g));
+  // uniform bytes: G chain, H chain, then B_blinding's SHA3-512(B) (as 64 B)
+  std::vector<uint8_t> uni((2 * n + 1) * 64);
+  gens_chain_bytes("G", 0, n, uni.data());
+  gens_chain_bytes("H", 0, n, uni.data() + 64 * n);
+  static const uint8_t B_ENC[32] = {0xe2, 0xf2, 0xae, 0x0a, 0x6a, 0xbc, 0x4e, 0x71, 0xa8, 0x84, 0xa9,
+                                    0x61, 0xc5, 0x00, 0x51, 0x5f, 0x58, 0xe3, 0x0b, 0x6a, 0xa5, 0x82,
+                                    0xdd, 0x8d, 0xb6, 0xa6, 0x59, 0x45, 0xe0, 0x8d, 0x2d, 0x76};
+  merlin::sha3_512(B_ENC, 32, uni.data() + 64 * 2 * n);
+  void *d_uni, *d_b, *d_bad;
+  int rc = ctx_ws(ctx, "gens_uni", uni.size(), &d_uni);
+  if (!rc) rc = ctx_ws(ctx, "gens_b", 32, &d_b);
+  if (!rc) rc = ctx_ws(ctx, "gens_bad", 8, &d_bad);
+  if (rc) {
+    bpp_gens_destroy(g);
+    return rc;
+  }
+  unsigned long long init = ~0ull;
+  BPP_HIP(hipMemcpyAsync(d_uni, uni.data(), uni.size(), hipMemcpyHostToDevice, ctx->stream));
+  BPP_HIP(hipMemcpyAsync(d_b, B_ENC, 32, hipMemcpyHostToDevice, ctx->stream));
+  BPP_HIP(hipMemcpyAsync(d_bad, &init, 8, hipMemcpyHostToDevice, ctx->stream));
+  hipLaunchKernelGGL(k_from_uniform, dim3(grid_for(2 * n, 64)), dim3(64), 0, ctx->stream, (const uint32_t*)d_uni, 2 * n,
+                     g->d_tbl);
+  hipLaunchKernelGGL(k_from_uniform, dim3(1), dim3(64), 0, ctx->stream, (const uint32_t*)d_uni + 16 * 2 * n, (size_t)1,
+                     g->d_tbl + (2 * n + 1) * MSM_NIELS_WORDS);
+  hipLaunchKernelGGL(k_decompress, dim3(1), dim3(64), 0, ctx->stream, (const uint32_t*)d_b, (size_t)1,
+                     g->d_tbl + 2 * n * MSM_NIELS_WORDS, (unsigned long long*)d_bad);
+  rc = ctx_check_launch(ctx, "gens kernels");
+  if (!rc) rc = gens_finish(ctx, g);
+  if (rc) {
+    bpp_gens_destroy(g);
+    return rc;
+  }
+  *out = g;
+  return BPP_OK;
+}
+
+int bpp_gens_from_points(bpp_ctx* ctx, const uint8_t* G_enc, const uint8_t* H_enc, size_t n, const uint8_t B_enc[32],
+                         const uint8_t Bb_enc[32], bpp_gens** out) {
+  if (!ctx || !out || !G_enc || !H_enc || !B_enc || !Bb_enc || n == 0) return BPP_ERR_ARG;
+  *out = nullptr;
+  BPP_HIP(hipSetDevice(ctx->device));
+  bpp_gens* g = nullptr;
+  BPP_TRY(gens_alloc(ctx, n, &g));
+  std::vector<uint8_t> enc((2 * n + 2) * 32);
+  memcpy(enc.data(), G_enc, 32 * n);
+  memcpy(enc.data() + 32 * n, H_enc, 32 * n);
+  memcpy(enc.data() + 64 * n, B_enc, 32);
+  memcpy(enc.data() + 64 * n + 32, Bb_enc, 32);
+  void *d_enc, *d_bad;
+  int rc = ctx_ws(ctx, "gens_enc", enc.size(), &d_enc);
+  if (!rc) rc = ctx_ws(ctx, "gens_bad", 8, &d_bad);
+  if (rc) {
+    bpp_gens_destroy(g);
+    return rc;
+  }
+  unsigned long long bad = ~0ull;
+  BPP_HIP(hipMemcpyAsync(d_enc, enc.data(), enc.size(), hipMemcpyHostToDevice, ctx->stream));
+  BPP_HIP(hipMemcpyAsync(d_bad, &bad, 8, hipMemcpyHostToDevice, ctx->stream));
+  hipLaunchKernelGGL(k_decompress, dim3(grid_for(2 * n + 2, 64)), dim3(64), 0, ctx->stream, (const uint32_t*)d_enc,
+                     2 * n + 2, g->d_tbl, (unsigned long long*)d_bad);
+  BPP_HIP(hipMemcpyAsync(&bad, d_bad, 8, hipMemcpyDeviceToHost, ctx->stream));
+  BPP_HIP(hipStreamSynchronize(ctx->stream));
+  if (bad != ~0ull) {
+    ctx->err = "invalid generator encoding at index " + std::to_string(bad);
+    bpp_gens_destroy(g);
+    return BPP_ERR_DECOMPRESS;
+  }
+  rc = gens_finish(ctx, g);
+  if (rc) {
+    bpp_gens_destroy(g);
+    return rc;
+  }
+  *out = g;
+  return BPP_OK;
+}
+
+size_t bpp_gens_len(const bpp_gens* g) { return g ? g->n : 0; }
+
+int bpp_gens_export(bpp_ctx* ctx, const bpp_gens* g, uint8_t* out) {
+  if (!ctx || !g || !out) return BPP_ERR_ARG;
+  bpp_points view;
+  view.ctx = ctx;
+  view.d = g->d_tbl;
+  view.n = 2 * g->n + 2;
+  return bpp_points_compress(ctx, &view, out);
+}
+
+void bpp_gens_destroy(bpp_gens* g) {
+  if (!g) return;
+  hipSetDevice(g->ctx->device);
+  if (g->d_tbl) hipFree(g->d_tbl);
+  if (g->d_fb) hipFree(g->d_fb);
+  delete g;
+}
+
+int bpp_pedersen_commit_batch(bpp_ctx* ctx, const bpp_gens* g, const uint8_t* v, const uint8_t* gamma, size_t m,
+                              uint8_t* out) {
+  if (!ctx || !g || ((!v || !gamma || !out) && m)) return BPP_ERR_ARG;
+  if (!m) return BPP_OK;
+  BPP_HIP(hipSetDevice(ctx->device));
+  uint32_t *d_v, *d_g;
+  BPP_TRY(upload_scalars(ctx, v, m, "ped_v", &d_v));
+  BPP_TRY(upload_scalars(ctx, gamma, m, "ped_g", &d_g));
+  void* d_out = nullptr;
+  BPP_TRY(ctx_ws(ctx, "ped_out", m * 32, &d_out));
+  BPP_TRY(pedersen_dev(ctx, g, d_v, d_g, m, (uint32_t*)d_out, nullptr));
+  BPP_HIP(hipMemcpyAsync(out, d_out, m * 32, hipMemcpyDeviceToHost, ctx->stream));
+  BPP_HIP(hipStreamSynchronize(ctx->stream));
+  return BPP_OK;
+}
+
+}  // extern "C"

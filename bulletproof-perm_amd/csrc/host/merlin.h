@@ -1,0 +1,245 @@
+// Merlin transcript (STROBE-128 over Keccak-f[1600]) for the host side.
+//
+// Byte-exact with merlin 3.0.0 (not vendored; bp-perm/Cargo.lock), which
+// the reference drives through its TranscriptProtocol trait
+// (bp-perm/src/transcript_protocol.rs:26-67):
+//   arithmetic_domain_sep  :27-30   append_scalar :32-34
+//   append_point           :45-47   validate_and_append_point :48-60
+//   challenge_scalar       :62-67 (64 bytes -> from_bytes_mod_order_wide)
+// plus bulletproofs 4.0.0's innerproduct_domain_sep ("ipp v1").
+// Fiat-Shamir is sequential, so this stays on the host.
+#pragma once
+#include <stdint.h>
+#include <string.h>
+
+#include "scalar.h"
+
+namespace merlin {
+
+static inline uint64_t rol(uint64_t x, int n) { return n ? (x << n) | (x >> (64 - n)) : x; }
+
+static inline void keccak_f1600(uint64_t s[25]) {
+  static const uint64_t RC[24] = {
+      0x0000000000000001ULL, 0x0000000000008082ULL, 0x800000000000808AULL, 0x8000000080008000ULL,
+      0x000000000000808BULL, 0x0000000080000001ULL, 0x8000000080008081ULL, 0x8000000000008009ULL,
+      0x000000000000008AULL, 0x0000000000000088ULL, 0x0000000080008009ULL, 0x000000008000000AULL,
+      0x000000008000808BULL, 0x800000000000008BULL, 0x8000000000008089ULL, 0x8000000000008003ULL,
+      0x8000000000008002ULL, 0x8000000000000080ULL, 0x000000000000800AULL, 0x800000008000000AULL,
+      0x8000000080008081ULL, 0x8000000000008080ULL, 0x0000000080000001ULL, 0x8000000080008008ULL};
+  // rotation offsets r[x + 5y]
+  static const int R[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43, 25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
+  for (int round = 0; round < 24; ++round) {
+    uint64_t C[5], D[5], B[25];
+    for (int x = 0; x < 5; ++x) C[x] = s[x] ^ s[x + 5] ^ s[x + 10] ^ s[x + 15] ^ s[x + 20];
+    for (int x = 0; x < 5; ++x) D[x] = C[(x + 4) % 5] ^ rol(C[(x + 1) % 5], 1);
+    for (int i = 0; i < 25; ++i) s[i] ^= D[i % 5];
+    for (int x = 0; x < 5; ++x)
+      for (int y = 0; y < 5; ++y) B[y + 5 * ((2 * x + 3 * y) % 5)] = rol(s[x + 5 * y], R[x + 5 * y]);
+    for (int x = 0; x < 5; ++x)
+      for (int y = 0; y < 5; ++y) s[x + 5 * y] = B[x + 5 * y] ^ ((~B[(x + 1) % 5 + 5 * y]) & B[(x + 2) % 5 + 5 * y]);
+    s[0] ^= RC[round];
+  }
+}
+
+// SHAKE256 XOF (rate 136, domain 0x1F): bulletproofs' GeneratorsChain and
+// PedersenGens::default's SHA3-512 hash-to-point need it.
+struct Shake256 {
+  uint64_t s[25];
+  uint8_t buf[136];
+  size_t n = 0;
+  bool squeezing = false;
+  size_t rpos = 0;
+  Shake256() { memset(s, 0, sizeof s); }
+  void absorb_block(const uint8_t* b) {
+    for (int i = 0; i < 17; ++i) {
+      uint64_t w;
+      memcpy(&w, b + 8 * i, 8);
+      s[i] ^= w;
+    }
+    keccak_f1600(s);
+  }
+  void update(const uint8_t* d, size_t len) {
+    for (size_t i = 0; i < len; ++i) {
+      buf[n++] = d[i];
+      if (n == 136) {
+        absorb_block(buf);
+        n = 0;
+      }
+    }
+  }
+  void finish() {
+    memset(buf + n, 0, 136 - n);
+    buf[n] ^= 0x1F;
+    buf[135] ^= 0x80;
+    absorb_block(buf);
+    squeezing = true;
+    rpos = 0;
+  }
+  void read(uint8_t* out, size_t len) {
+    if (!squeezing) finish();
+    for (size_t i = 0; i < len; ++i) {
+      if (rpos == 136) {
+        keccak_f1600(s);
+        rpos = 0;
+      }
+      out[i] = (uint8_t)(s[rpos / 8] >> (8 * (rpos % 8)));
+      ++rpos;
+    }
+  }
+};
+
+// SHA3-512 (rate 72, domain 0x06)
+static inline void sha3_512(const uint8_t* d, size_t len, uint8_t out[64]) {
+  uint64_t s[25];
+  memset(s, 0, sizeof s);
+  uint8_t block[72];
+  size_t off = 0;
+  while (len - off >= 72) {
+    for (int i = 0; i < 9; ++i) {
+      uint64_t w;
+      memcpy(&w, d + off + 8 * i, 8);
+      s[i] ^= w;
+    }
+    keccak_f1600(s);
+    off += 72;
+  }
+  memset(block, 0, 72);
+  memcpy(block, d + off, len - off);
+  block[len - off] ^= 0x06;
+  block[71] ^= 0x80;
+  for (int i = 0; i < 9; ++i) {
+    uint64_t w;
+    memcpy(&w, block + 8 * i, 8);
+    s[i] ^= w;
+  }
+  keccak_f1600(s);
+  memcpy(out, s, 64);
+}
+
+enum : uint8_t { FLAG_I = 1, FLAG_A = 2, FLAG_C = 4, FLAG_T = 8, FLAG_M = 16, FLAG_K = 32 };
+static const int STROBE_R = 166;
+
+struct Strobe128 {
+  uint8_t st[200];
+  uint8_t pos = 0, pos_begin = 0, cur_flags = 0;
+
+  void run_f() {
+    st[pos] ^= pos_begin;
+    st[pos + 1] ^= 0x04;
+    st[STROBE_R + 1] ^= 0x80;
+    uint64_t lanes[25];
+    memcpy(lanes, st, 200);  // little-endian host
+    keccak_f1600(lanes);
+    memcpy(st, lanes, 200);
+    pos = 0;
+    pos_begin = 0;
+  }
+  void absorb(const uint8_t* d, size_t n) {
+    for (size_t i = 0; i < n; ++i) {
+      st[pos] ^= d[i];
+      if (++pos == STROBE_R) run_f();
+    }
+  }
+  void squeeze(uint8_t* d, size_t n) {
+    for (size_t i = 0; i < n; ++i) {
+      d[i] = st[pos];
+      st[pos] = 0;
+      if (++pos == STROBE_R) run_f();
+    }
+  }
+  void begin_op(uint8_t flags, bool more) {
+    if (more) return;  // continuation of the same op (flags equal by construction)
+    const uint8_t old_begin = pos_begin;
+    pos_begin = pos + 1;
+    cur_flags = flags;
+    const uint8_t hdr[2] = {old_begin, flags};
+    absorb(hdr, 2);
+    if ((flags & (FLAG_C | FLAG_K)) && pos != 0) run_f();
+  }
+  void meta_ad(const uint8_t* d, size_t n, bool more) {
+    begin_op(FLAG_M | FLAG_A, more);
+    absorb(d, n);
+  }
+  void ad(const uint8_t* d, size_t n, bool more) {
+    begin_op(FLAG_A, more);
+    absorb(d, n);
+  }
+  void prf(uint8_t* d, size_t n, bool more) {
+    begin_op(FLAG_I | FLAG_A | FLAG_C, more);
+    squeeze(d, n);
+  }
+  void init(const uint8_t* label, size_t n) {
+    memset(st, 0, sizeof st);
+    const uint8_t hdr[6] = {1, STROBE_R + 2, 1, 0, 1, 96};
+    memcpy(st, hdr, 6);
+    memcpy(st + 6, "STROBEv1.0.2", 12);
+    uint64_t lanes[25];
+    memcpy(lanes, st, 200);
+    keccak_f1600(lanes);
+    memcpy(st, lanes, 200);
+    pos = pos_begin = cur_flags = 0;
+    meta_ad(label, n, false);
+  }
+};
+
+struct Transcript {
+  Strobe128 s;
+
+  explicit Transcript(const uint8_t* label = nullptr, size_t n = 0) {
+    static const char kMerlin[] = "Merlin v1.0";
+    s.init((const uint8_t*)kMerlin, sizeof(kMerlin) - 1);
+    append_message((const uint8_t*)"dom-sep", 7, label, n);
+  }
+  void append_message(const uint8_t* label, size_t ln, const uint8_t* msg, size_t n) {
+    const uint32_t len = (uint32_t)n;
+    uint8_t le[4];
+    memcpy(le, &len, 4);
+    s.meta_ad(label, ln, false);
+    s.meta_ad(le, 4, true);
+    s.ad(msg, n, false);
+  }
+  void append(const char* label, const uint8_t* msg, size_t n) {
+    append_message((const uint8_t*)label, strlen(label), msg, n);
+  }
+  void append_u64(const char* label, uint64_t x) {
+    uint8_t b[8];
+    memcpy(b, &x, 8);
+    append(label, b, 8);
+  }
+  void challenge_bytes(const char* label, uint8_t* out, size_t n) {
+    const uint32_t len = (uint32_t)n;
+    uint8_t le[4];
+    memcpy(le, &len, 4);
+    s.meta_ad((const uint8_t*)label, strlen(label), false);
+    s.meta_ad(le, 4, true);
+    s.prf(out, n, false);
+  }
+  // --- TranscriptProtocol (transcript_protocol.rs)
+  void arithmetic_domain_sep(uint64_t n) {
+    append("dom-sep", (const uint8_t*)"acp v1", 6);
+    append_u64("n", n);
+  }
+  void innerproduct_domain_sep(uint64_t n) {
+    append("dom-sep", (const uint8_t*)"ipp v1", 6);
+    append_u64("n", n);
+  }
+  void append_scalar(const char* label, const hsc::Sc& x) {
+    uint8_t b[32];
+    hsc::to_bytes(b, x);
+    append(label, b, 32);
+  }
+  void append_point(const char* label, const uint8_t p[32]) { append(label, p, 32); }
+  bool validate_and_append_point(const char* label, const uint8_t p[32]) {
+    static const uint8_t zero[32] = {0};
+    if (!memcmp(p, zero, 32)) return false;  // identity -> VerificationError
+    append(label, p, 32);
+    return true;
+  }
+  hsc::Sc challenge_scalar(const char* label) {
+    uint8_t buf[64];
+    challenge_bytes(label, buf, 64);
+    return hsc::from_wide(buf);
+  }
+};
+
+}  // namespace merlin

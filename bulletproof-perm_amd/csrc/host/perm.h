@@ -1,0 +1,68 @@
+// Permutation circuit + arithmetic-circuit proof (sound mode) — host side.
+//
+// Restates the reference's ACProof::ArithmeticCircuitProof
+// (bp-perm/src/circuit_lib.rs:139-585) and the permutation circuit of
+// weights.rs:26-204 in their sound form (SURVEY.md §2.2 defects Q1-Q10
+// fixed; DESIGN.md "Protocol"), with every group operation dropped through
+// the GPU (MSM engine, fixed-base Pedersen, IPA).  Matrices are sparse
+// (the reference's dense Q x n matrices are 99.4 % zeros).
+#pragma once
+#include <stdint.h>
+
+#include <array>
+#include <vector>
+
+#include "merlin.h"
+#include "scalar.h"
+
+namespace perm {
+
+struct Entry {
+  uint32_t q, col;
+  hsc::Sc val;
+};
+
+struct Circuit {
+  uint32_t k = 0, n = 0, n_p = 0, lg = 0, Q = 0, m = 0;
+  std::vector<Entry> WL, WR, WO, WV;
+  std::vector<hsc::Sc> c;  // c[Q-1] = -x set per proof
+};
+
+Circuit build(uint32_t k);
+
+// v = [1..k, pi(1..k), x]; gate values (sound create_a)
+void witness(const Circuit& C, const std::vector<uint32_t>& pi, const hsc::Sc& x, std::vector<hsc::Sc>& v,
+             std::vector<hsc::Sc>& aL, std::vector<hsc::Sc>& aR, std::vector<hsc::Sc>& aO);
+
+// (z^Q)^T W as a dense vector of length ncols
+std::vector<hsc::Sc> zW(const std::vector<Entry>& W, const std::vector<hsc::Sc>& zq, uint32_t ncols);
+
+// SHAKE256(domain || seed_le64) byte stream (oracle/merlin.py Rng)
+struct Rng {
+  merlin::Shake256 sh;
+  Rng(const char* domain, uint64_t seed) {
+    sh.update((const uint8_t*)domain, strlen(domain));
+    uint8_t b[8];
+    memcpy(b, &seed, 8);
+    sh.update(b, 8);
+  }
+  void bytes(uint8_t* out, size_t n) { sh.read(out, n); }
+  uint64_t u64() {
+    uint8_t b[8];
+    bytes(b, 8);
+    uint64_t x;
+    memcpy(&x, b, 8);
+    return x;
+  }
+  hsc::Sc scalar() {
+    uint8_t b[64];
+    bytes(b, 64);
+    return hsc::from_wide(b);
+  }
+};
+
+std::vector<uint32_t> fisher_yates(uint32_t k, Rng& rng);
+
+size_t proof_len(uint32_t k);
+
+}  // namespace perm

@@ -1,0 +1,187 @@
+// Host scalar field Z/lZ, l = 2^252 + 27742317777372353535851937790883648493.
+//
+// Product code for the host-side protocol logic (challenges, circuit
+// linear algebra, batch inversion) that the reference performs with dalek's
+// `Scalar` (circuit_lib.rs:256-302 compute_per_challenges, util.rs:6-94,
+// poly.rs:5-77).  Values are kept canonical (< l) in 4 x u64 limbs;
+// multiplication is two Montgomery (CIOS, R = 2^256) steps.
+#pragma once
+#include <stdint.h>
+#include <string.h>
+
+#include <vector>
+
+namespace hsc {
+
+typedef unsigned __int128 u128;
+
+struct Sc {
+  uint64_t v[4];
+  bool operator==(const Sc& o) const { return !memcmp(v, o.v, 32); }
+  bool operator!=(const Sc& o) const { return !(*this == o); }
+};
+
+static const Sc L = {{0x5812631a5cf5d3edULL, 0x14def9dea2f79cd6ULL, 0x0ULL, 0x1000000000000000ULL}};
+static const Sc R2 = {{0xa40611e3449c0f01ULL, 0xd00e1ba768859347ULL, 0xceec73d217f5be65ULL, 0x0399411b7c309a3dULL}};
+static const Sc R3 = {{0x2a9e49687b83a2dbULL, 0x278324e6aef7f3ecULL, 0x8065dc6c04ec5b65ULL, 0x0e530b773599cec7ULL}};
+static const uint64_t LINV = 0xd2b51da312547e1bULL;  // -l^-1 mod 2^64
+
+static inline Sc zero() { return Sc{{0, 0, 0, 0}}; }
+static inline Sc one() { return Sc{{1, 0, 0, 0}}; }
+static inline Sc from_u64(uint64_t x) { return Sc{{x, 0, 0, 0}}; }
+
+static inline bool geq(const Sc& a, const Sc& b) {
+  for (int i = 3; i >= 0; --i) {
+    if (a.v[i] != b.v[i]) return a.v[i] > b.v[i];
+  }
+  return true;
+}
+
+static inline Sc sub_raw(const Sc& a, const Sc& b, uint64_t* borrow_out) {
+  Sc r;
+  uint64_t br = 0;
+  for (int i = 0; i < 4; ++i) {
+    u128 d = (u128)a.v[i] - b.v[i] - br;
+    r.v[i] = (uint64_t)d;
+    br = (uint64_t)(d >> 64) & 1;
+  }
+  if (borrow_out) *borrow_out = br;
+  return r;
+}
+
+static inline Sc add(const Sc& a, const Sc& b) {
+  Sc r;
+  u128 c = 0;
+  for (int i = 0; i < 4; ++i) {
+    c = (u128)a.v[i] + b.v[i] + (uint64_t)(c >> 64);
+    r.v[i] = (uint64_t)c;
+  }
+  // a, b < l < 2^253: no 256-bit overflow
+  if (geq(r, L)) r = sub_raw(r, L, nullptr);
+  return r;
+}
+
+static inline Sc sub(const Sc& a, const Sc& b) {
+  uint64_t br;
+  Sc r = sub_raw(a, b, &br);
+  if (br) {
+    u128 c = 0;
+    for (int i = 0; i < 4; ++i) {
+      c = (u128)r.v[i] + L.v[i] + (uint64_t)(c >> 64);
+      r.v[i] = (uint64_t)c;
+    }
+  }
+  return r;
+}
+
+static inline Sc neg(const Sc& a) { return sub(zero(), a); }
+
+// Montgomery product a*b*R^-1 mod l (a*b < l*R required)
+static inline Sc mont(const Sc& a, const Sc& b) {
+  uint64_t t[6] = {0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < 4; ++i) {
+    u128 c = 0;
+    for (int j = 0; j < 4; ++j) {
+      c = (u128)a.v[i] * b.v[j] + t[j] + (uint64_t)(c >> 64);
+      t[j] = (uint64_t)c;
+    }
+    c = (u128)t[4] + (uint64_t)(c >> 64);
+    t[4] = (uint64_t)c;
+    t[5] = (uint64_t)(c >> 64);
+    const uint64_t m = t[0] * LINV;
+    c = (u128)m * L.v[0] + t[0];
+    for (int j = 1; j < 4; ++j) {
+      c = (u128)m * L.v[j] + t[j] + (uint64_t)(c >> 64);
+      t[j - 1] = (uint64_t)c;
+    }
+    c = (u128)t[4] + (uint64_t)(c >> 64);
+    t[3] = (uint64_t)c;
+    t[4] = t[5] + (uint64_t)(c >> 64);
+  }
+  Sc r = {{t[0], t[1], t[2], t[3]}};
+  if (t[4] || geq(r, L)) r = sub_raw(r, L, nullptr);
+  return r;
+}
+
+static inline Sc mul(const Sc& a, const Sc& b) { return mont(mont(a, b), R2); }
+static inline Sc sq(const Sc& a) { return mul(a, a); }
+
+// from 32 canonical little-endian bytes; false if >= l
+static inline bool from_canonical(Sc& out, const uint8_t b[32]) {
+  memcpy(out.v, b, 32);
+  return !geq(out, L);
+}
+
+// dalek Scalar::from_bytes_mod_order_wide (64 bytes)
+static inline Sc from_wide(const uint8_t b[64]) {
+  Sc lo, hi;
+  memcpy(lo.v, b, 32);
+  memcpy(hi.v, b + 32, 32);
+  // lo*R*R^-1... : mont(lo, R2) = lo*R mod l (Montgomery form of lo)
+  Sc a = mont(lo, R2);
+  Sc c = mont(hi, R3);  // hi*R^2 mod l = Montgomery form of hi*2^256
+  Sc s = add(a, c);
+  return mont(s, one());  // leave Montgomery form
+}
+
+// dalek Scalar::from_bytes_mod_order (32 bytes, any value)
+static inline Sc from_bytes_mod(const uint8_t b[32]) {
+  uint8_t w[64] = {0};
+  memcpy(w, b, 32);
+  return from_wide(w);
+}
+
+static inline void to_bytes(uint8_t out[32], const Sc& a) { memcpy(out, a.v, 32); }
+
+static inline Sc pow(const Sc& a, const Sc& e) {
+  Sc r = one();
+  for (int i = 255; i >= 0; --i) {
+    r = sq(r);
+    if ((e.v[i >> 6] >> (i & 63)) & 1) r = mul(r, a);
+  }
+  return r;
+}
+
+static inline Sc invert(const Sc& a) {
+  Sc e = sub_raw(L, from_u64(2), nullptr);
+  return pow(a, e);
+}
+
+// Montgomery's trick; returns the inverse of the product.  Zero inputs
+// are not allowed (dalek batch_invert has the same precondition).
+static inline Sc batch_invert(std::vector<Sc>& xs) {
+  const size_t n = xs.size();
+  std::vector<Sc> pref(n);
+  Sc acc = one();
+  for (size_t i = 0; i < n; ++i) {
+    pref[i] = acc;
+    acc = mul(acc, xs[i]);
+  }
+  Sc inv_all = invert(acc);
+  Sc allinv = inv_all;
+  for (size_t i = n; i-- > 0;) {
+    Sc t = mul(inv_all, pref[i]);
+    inv_all = mul(inv_all, xs[i]);
+    xs[i] = t;
+  }
+  return allinv;
+}
+
+static inline Sc inner_product(const std::vector<Sc>& a, const std::vector<Sc>& b) {
+  Sc r = zero();
+  for (size_t i = 0; i < a.size(); ++i) r = add(r, mul(a[i], b[i]));
+  return r;
+}
+
+// (1, x, x^2, ..., x^{n-1})
+static inline std::vector<Sc> powers(const Sc& x, size_t n) {
+  std::vector<Sc> r(n);
+  Sc c = one();
+  for (size_t i = 0; i < n; ++i) {
+    r[i] = c;
+    c = mul(c, x);
+  }
+  return r;
+}
+
+}  // namespace hsc

@@ -1,0 +1,39 @@
+// Inner-product argument (bulletproofs 4.0.0 InnerProductProof) — internal API.
+#pragma once
+#include <array>
+#include <vector>
+
+#include "ctx.h"
+#include "host/merlin.h"
+#include "host/scalar.h"
+
+struct IpaGens {
+  const uint32_t* d_tbl = nullptr;   // points with index < n0
+  const uint32_t* d_tbl1 = nullptr;  // points with index >= n0 (at idx - n0)
+  uint32_t n0 = 0xffffffffu;
+  uint32_t gbase = 0, hbase = 0;     // G_i at gbase + i, H_i at hbase + i
+  uint32_t qidx = 0;                 // Q = qmul * P[qidx]
+  hsc::Sc qmul = hsc::one();
+};
+
+typedef std::array<uint8_t, 32> Enc32;
+
+struct IpaProofHost {
+  std::vector<Enc32> L, R;
+  hsc::Sc a, b;
+};
+
+// a, b, Gf, Hf: device arrays of n canonical scalars (Gf/Hf may be null =
+// all ones).  a and b are consumed.
+int ipa_prove_dev(bpp_ctx* ctx, merlin::Transcript& tr, const IpaGens& g, uint32_t n, const uint32_t* d_Gf,
+                  const uint32_t* d_Hf, const uint32_t* d_a, const uint32_t* d_b, IpaProofHost& out);
+
+// Replays the verifier side of the transcript; returns false on malformed
+// proof (identity L/R, wrong length).  Fills u^2, u^-2 and s (bulletproofs
+// verification_scalars).
+bool ipa_verification_scalars(merlin::Transcript& tr, uint32_t n, const std::vector<Enc32>& L,
+                              const std::vector<Enc32>& R, std::vector<hsc::Sc>& u_sq,
+                              std::vector<hsc::Sc>& uinv_sq, std::vector<hsc::Sc>& s);
+
+static const hsc::Sc SC_R_MOD_L = {{0xd6ec31748d98951dULL, 0xc6ef5bf4737dcf70ULL, 0xfffffffffffffffeULL,
+                                    0x0fffffffffffffffULL}};

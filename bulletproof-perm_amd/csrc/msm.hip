@@ -39,7 +39,8 @@ uint32_t msm_choose_c(double n_per_msm) {
 static unsigned grid_for(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
 int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const uint32_t* d_off, uint32_t M,
-               uint32_t T, uint32_t c, uint32_t wb, uint32_t Wn, const uint32_t* d_tbl, uint32_t** d_wsum_out) {
+               uint32_t T, uint32_t c, uint32_t wb, uint32_t Wn, const uint32_t* d_tbl, uint32_t** d_wsum_out,
+               const uint32_t* d_tbl1, uint32_t n0) {
   MsmGeom g;
   g.M = M;
   g.T = T;
@@ -77,7 +78,7 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
   BPP_TRY(ctx_check_launch(ctx, "k_msm_scatter"));
   {
     ProfScope ps(ctx, "msm_accumulate");
-    hipLaunchKernelGGL(k_msm_accumulate, dim3(grid_for(NB, 256)), dim3(256), 0, ctx->stream, d_tbl,
+    hipLaunchKernelGGL(k_msm_accumulate, dim3(grid_for(NB, 256)), dim3(256), 0, ctx->stream, d_tbl, d_tbl1, n0,
                        (const uint32_t*)entries, (const uint32_t*)boff, (uint32_t)NB, (uint32_t*)bsum);
   }
   BPP_TRY(ctx_check_launch(ctx, "k_msm_accumulate"));
@@ -249,3 +250,50 @@ int bpp_msm_batch(bpp_ctx* ctx, size_t count, const uint64_t* offsets, const uin
 }
 
 }  // extern "C"
+
+// M independent MSMs (host offsets, M+1 entries) over device scalars and
+// point indices; results returned as host points.  Few MSMs: window sums are
+// combined on the host; many: one GPU lane per MSM runs the Horner chain.
+int msm_multi(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const std::vector<uint32_t>& off,
+              const uint32_t* d_tbl, const uint32_t* d_tbl1, uint32_t n0, std::vector<h25519::ge>& out) {
+  const uint32_t M = (uint32_t)off.size() - 1;
+  const uint32_t T = off[M];
+  out.assign(M, h25519::ge_identity());
+  if (M == 0 || T == 0) return BPP_OK;
+  void* d_off = nullptr;
+  BPP_TRY(ctx_ws(ctx, "multi_off", (M + 1) * 4, &d_off));
+  BPP_HIP(hipMemcpyAsync(d_off, off.data(), (M + 1) * 4, hipMemcpyHostToDevice, ctx->stream));
+  const uint32_t c = msm_choose_c((double)T / (double)M);
+  const uint32_t W = (254 + c - 1) / c;
+  uint32_t* d_ws = nullptr;
+  BPP_TRY(msm_engine(ctx, d_scal, d_pidx, (const uint32_t*)d_off, M, T, c, 0, W, d_tbl, &d_ws, d_tbl1, n0));
+  if (M <= 8) {
+    void* h = nullptr;
+    BPP_TRY(ctx_pinned(ctx, (size_t)M * W * 128, &h));
+    BPP_HIP(hipMemcpyAsync(h, d_ws, (size_t)M * W * 128, hipMemcpyDeviceToHost, ctx->stream));
+    BPP_HIP(hipStreamSynchronize(ctx->stream));
+    for (uint32_t m = 0; m < M; ++m) out[m] = horner_host((const uint32_t*)h + (size_t)m * W * 32, W, c, 0);
+    return BPP_OK;
+  }
+  MsmGeom g;
+  g.M = M;
+  g.T = T;
+  g.c = c;
+  g.W = W;
+  g.wb = 0;
+  g.Wn = W;
+  g.B = 1u << (c - 1);
+  void* d_res = nullptr;
+  BPP_TRY(ctx_ws(ctx, "multi_res", (size_t)M * 128, &d_res));
+  {
+    ProfScope ps(ctx, "msm_horner");
+    hipLaunchKernelGGL(k_msm_horner, dim3(grid_for(M, 64)), dim3(64), 0, ctx->stream, (const uint32_t*)d_ws, g,
+                       (uint32_t*)d_res);
+  }
+  BPP_TRY(ctx_check_launch(ctx, "k_msm_horner"));
+  std::vector<uint32_t> h((size_t)M * 32);
+  BPP_HIP(hipMemcpyAsync(h.data(), d_res, (size_t)M * 128, hipMemcpyDeviceToHost, ctx->stream));
+  BPP_HIP(hipStreamSynchronize(ctx->stream));
+  for (uint32_t m = 0; m < M; ++m) out[m] = h25519::ge_from_words(h.data() + (size_t)m * 32);
+  return BPP_OK;
+}

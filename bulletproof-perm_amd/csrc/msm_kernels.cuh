@@ -116,7 +116,10 @@ __global__ void k_msm_scatter(const uint32_t* __restrict__ scalars, const uint32
 }
 
 // One lane per bucket.
+// Points with index < n0 come from tbl, the rest from tbl1[idx - n0] (so a
+// proof's own points can join the resident generators without a copy).
 __global__ void __launch_bounds__(256) k_msm_accumulate(const uint32_t* __restrict__ tbl,
+                                                       const uint32_t* __restrict__ tbl1, uint32_t n0,
                                                        const uint32_t* __restrict__ entries,
                                                        const uint32_t* __restrict__ boff, uint32_t nbuckets,
                                                        uint32_t* __restrict__ bsum) {
@@ -126,7 +129,8 @@ __global__ void __launch_bounds__(256) k_msm_accumulate(const uint32_t* __restri
   ge_p3 acc = ge_identity();
   for (uint32_t i = lo; i < hi; ++i) {
     const uint32_t e = entries[i];
-    ge_niels q = load_niels(tbl, e & 0x7fffffffu);
+    const uint32_t pi = e & 0x7fffffffu;
+    ge_niels q = pi < n0 ? load_niels(tbl, pi) : load_niels(tbl1, pi - n0);
     if (e & 0x80000000u) q = ge_niels_neg(q);
     acc = ge_madd(acc, q);
   }

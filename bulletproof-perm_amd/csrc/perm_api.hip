@@ -1,0 +1,463 @@
+// Permutation proof: sound-mode arithmetic-circuit prover / verifier over
+// the GPU primitives (C ABI bpp_perm_*).
+//
+// Restates ACProof::ArithmeticCircuitProof (bp-perm/src/circuit_lib.rs):
+//   create                 :139-253  -> V (fixed-base Pedersen), A_I/A_O/S
+//                                       (one 3-MSM batch)
+//   challenge_wit_and_const:133-138  -> y, z
+//   compute_per_challenges :256-302  -> y^n, y^-n (batch inversion), z^Q W
+//                                       (sparse, host)
+//   commit_Ts              :304-423  -> t_1..t_6 (host), T_i (fixed-base)
+//   random_chall_x         :425-432  -> x
+//   blinding_values        :434-476  -> l, r, t_hat, tau_x, mu; the clear
+//                                       l, r of :466-467 replaced by an IPA
+//   verify                 :478-585  -> ONE GPU MSM (t-check weighted by a
+//                                       verifier challenge + the IPA check,
+//                                       generator scalars merged)
+// Transcript order and RNG draw order match oracle/bulletproofs.py
+// ac_prove / ac_verify exactly (tests compare proof bytes).
+#include <cstring>
+
+#include "ctx.h"
+#include "gens.h"
+#include "host/perm.h"
+#include "ipa.h"
+#include "msm_engine.h"
+
+using hsc::Sc;
+
+int decompress_ws(bpp_ctx* ctx, const uint8_t* enc, size_t count, const char* name, uint32_t** d_out);
+
+namespace {
+
+struct Proof {
+  std::vector<Enc32> V;
+  Enc32 AI, AO, S, T[5];
+  Sc tau_x, mu, t_hat;
+  IpaProofHost ipa;
+};
+
+void put_sc(std::vector<uint8_t>& buf, const Sc& s) {
+  uint8_t b[32];
+  hsc::to_bytes(b, s);
+  buf.insert(buf.end(), b, b + 32);
+}
+
+void serialize(const perm::Circuit& C, const Proof& P, uint8_t* out) {
+  std::vector<uint8_t> b;
+  b.reserve(perm::proof_len(C.k));
+  for (const Enc32* e : {&P.AI, &P.AO, &P.S, &P.T[0], &P.T[1], &P.T[2], &P.T[3], &P.T[4]})
+    b.insert(b.end(), e->begin(), e->end());
+  put_sc(b, P.tau_x);
+  put_sc(b, P.mu);
+  put_sc(b, P.t_hat);
+  for (uint32_t j = 0; j < C.lg; ++j) {
+    b.insert(b.end(), P.ipa.L[j].begin(), P.ipa.L[j].end());
+    b.insert(b.end(), P.ipa.R[j].begin(), P.ipa.R[j].end());
+  }
+  put_sc(b, P.ipa.a);
+  put_sc(b, P.ipa.b);
+  memcpy(out, b.data(), b.size());
+}
+
+bool deserialize(const perm::Circuit& C, const uint8_t* in, size_t len, const uint8_t* V, Proof& P) {
+  if (len != perm::proof_len(C.k)) return false;
+  size_t o = 0;
+  auto pt = [&](Enc32& e) {
+    memcpy(e.data(), in + o, 32);
+    o += 32;
+  };
+  auto sc = [&](Sc& s) {
+    bool ok = hsc::from_canonical(s, in + o);
+    o += 32;
+    return ok;
+  };
+  pt(P.AI);
+  pt(P.AO);
+  pt(P.S);
+  for (int i = 0; i < 5; ++i) pt(P.T[i]);
+  if (!sc(P.tau_x) || !sc(P.mu) || !sc(P.t_hat)) return false;
+  P.ipa.L.resize(C.lg);
+  P.ipa.R.resize(C.lg);
+  for (uint32_t j = 0; j < C.lg; ++j) {
+    pt(P.ipa.L[j]);
+    pt(P.ipa.R[j]);
+  }
+  if (!sc(P.ipa.a) || !sc(P.ipa.b)) return false;
+  P.V.resize(C.m);
+  for (uint32_t j = 0; j < C.m; ++j) memcpy(P.V[j].data(), V + 32 * j, 32);
+  return true;
+}
+
+std::vector<uint8_t> to_bytes(const std::vector<Sc>& v) {
+  std::vector<uint8_t> b(v.size() * 32);
+  for (size_t i = 0; i < v.size(); ++i) hsc::to_bytes(b.data() + 32 * i, v[i]);
+  return b;
+}
+
+int upload_sc(bpp_ctx* ctx, const std::vector<Sc>& v, const char* name, uint32_t** d) {
+  void* p = nullptr;
+  BPP_TRY(ctx_ws(ctx, name, v.size() * 32 + 32, &p));
+  std::vector<uint8_t> b = to_bytes(v);
+  if (!b.empty()) BPP_HIP(hipMemcpyAsync(p, b.data(), b.size(), hipMemcpyHostToDevice, ctx->stream));
+  BPP_HIP(hipStreamSynchronize(ctx->stream));
+  *d = (uint32_t*)p;
+  return BPP_OK;
+}
+
+// Fixed-base commitments v_i*B + g_i*Bb, returned compressed.
+int pedersen_host(bpp_ctx* ctx, const bpp_gens* g, const std::vector<Sc>& v, const std::vector<Sc>& gam,
+                  std::vector<Enc32>& out) {
+  uint32_t *d_v, *d_g;
+  BPP_TRY(upload_sc(ctx, v, "pp_v", &d_v));
+  BPP_TRY(upload_sc(ctx, gam, "pp_g", &d_g));
+  void* d_out = nullptr;
+  BPP_TRY(ctx_ws(ctx, "pp_out", v.size() * 32, &d_out));
+  BPP_TRY(pedersen_dev(ctx, g, d_v, d_g, v.size(), (uint32_t*)d_out, nullptr));
+  out.resize(v.size());
+  BPP_HIP(hipMemcpyAsync(out.data(), d_out, v.size() * 32, hipMemcpyDeviceToHost, ctx->stream));
+  BPP_HIP(hipStreamSynchronize(ctx->stream));
+  return BPP_OK;
+}
+
+int msm_terms(bpp_ctx* ctx, const std::vector<Sc>& sc, const std::vector<uint32_t>& idx,
+              const std::vector<uint32_t>& off, const uint32_t* tbl, const uint32_t* tbl1, uint32_t n0,
+              std::vector<h25519::ge>& res) {
+  uint32_t* d_s = nullptr;
+  BPP_TRY(upload_sc(ctx, sc, "mt_s", &d_s));
+  void* d_i = nullptr;
+  BPP_TRY(ctx_ws(ctx, "mt_i", idx.size() * 4 + 4, &d_i));
+  BPP_HIP(hipMemcpyAsync(d_i, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+  return msm_multi(ctx, d_s, (const uint32_t*)d_i, off, tbl, tbl1, n0, res);
+}
+
+struct Challenges {
+  Sc x_perm, y, z, x, w;
+};
+
+int prove_one(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, uint64_t seed, merlin::Transcript& tr,
+              Proof& P, std::vector<uint32_t>* pi_out) {
+  const uint32_t k = C.k, n_p = C.n_p, m = C.m;
+  perm::Rng rng("bpperm-prove", seed);
+  std::vector<uint32_t> pi = perm::fisher_yates(k, rng);
+  if (pi_out) *pi_out = pi;
+  std::vector<Sc> gamma(m);
+  for (auto& g : gamma) g = rng.scalar();
+  const Sc alpha = rng.scalar(), beta = rng.scalar(), rho = rng.scalar();
+  std::vector<Sc> sL(n_p), sR(n_p), taus(5);
+  for (auto& s : sL) s = rng.scalar();
+  for (auto& s : sR) s = rng.scalar();
+  for (auto& s : taus) s = rng.scalar();
+
+  tr.arithmetic_domain_sep(n_p);
+  // V_0..V_2k-1, then x_perm, then V_2k = commit(x_perm)
+  std::vector<Sc> vals(2 * k);
+  for (uint32_t i = 0; i < k; ++i) {
+    vals[i] = hsc::from_u64(i + 1);
+    vals[k + i] = hsc::from_u64(pi[i] + 1);
+  }
+  std::vector<Enc32> V;
+  BPP_TRY(pedersen_host(ctx, G, vals, std::vector<Sc>(gamma.begin(), gamma.begin() + 2 * k), V));
+  for (auto& e : V) tr.append_point("V", e.data());
+  const Sc x_perm = tr.challenge_scalar("x_perm");
+  std::vector<Enc32> Vx;
+  BPP_TRY(pedersen_host(ctx, G, {x_perm}, {gamma[2 * k]}, Vx));
+  V.push_back(Vx[0]);
+  tr.append_point("V", Vx[0].data());
+  P.V = V;
+
+  std::vector<Sc> v, aL, aR, aO;
+  perm::witness(C, pi, x_perm, v, aL, aR, aO);
+
+  // A_I, A_O, S: one batch of three MSMs over the resident generators
+  {
+    std::vector<Sc> sc;
+    std::vector<uint32_t> idx;
+    auto add = [&](const Sc& s, uint32_t i) {
+      sc.push_back(s);
+      idx.push_back(i);
+    };
+    add(alpha, G->bbidx());
+    for (uint32_t i = 0; i < n_p; ++i) add(aL[i], G->gidx(i));
+    for (uint32_t i = 0; i < n_p; ++i) add(aR[i], G->hidx(i));
+    const uint32_t o1 = (uint32_t)sc.size();
+    add(beta, G->bbidx());
+    for (uint32_t i = 0; i < n_p; ++i) add(aO[i], G->gidx(i));
+    const uint32_t o2 = (uint32_t)sc.size();
+    add(rho, G->bbidx());
+    for (uint32_t i = 0; i < n_p; ++i) add(sL[i], G->gidx(i));
+    for (uint32_t i = 0; i < n_p; ++i) add(sR[i], G->hidx(i));
+    std::vector<h25519::ge> res;
+    BPP_TRY(msm_terms(ctx, sc, idx, {0, o1, o2, (uint32_t)sc.size()}, G->d_tbl, nullptr, 0xffffffffu, res));
+    h25519::encode(P.AI.data(), res[0]);
+    h25519::encode(P.AO.data(), res[1]);
+    h25519::encode(P.S.data(), res[2]);
+  }
+  tr.append_point("A_I", P.AI.data());
+  tr.append_point("A_O", P.AO.data());
+  tr.append_point("S", P.S.data());
+  const Sc y = tr.challenge_scalar("y");
+  const Sc z = tr.challenge_scalar("z");
+
+  std::vector<Sc> y_n = hsc::powers(y, n_p);
+  std::vector<Sc> y_inv_n = hsc::powers(hsc::invert(y), n_p);
+  std::vector<Sc> zq = hsc::powers(z, C.Q + 1);
+  zq.erase(zq.begin());
+  const std::vector<Sc> zWL = perm::zW(C.WL, zq, n_p), zWR = perm::zW(C.WR, zq, n_p), zWO = perm::zW(C.WO, zq, n_p),
+                        zWV = perm::zW(C.WV, zq, m);
+  // l(X) = l1 X + l2 X^2 + l3 X^3 ; r(X) = r0 + r1 X + r3 X^3
+  std::vector<Sc> l1(n_p), r0(n_p), r1(n_p), r3(n_p);
+  for (uint32_t i = 0; i < n_p; ++i) {
+    l1[i] = hsc::add(aL[i], hsc::mul(y_inv_n[i], zWR[i]));
+    r0[i] = hsc::sub(zWO[i], y_n[i]);
+    r1[i] = hsc::add(hsc::mul(y_n[i], aR[i]), zWL[i]);
+    r3[i] = hsc::mul(y_n[i], sR[i]);
+  }
+  const std::vector<Sc>& l2 = aO;
+  const std::vector<Sc>& l3 = sL;
+  using hsc::add;
+  using hsc::inner_product;
+  Sc t[7];
+  t[1] = inner_product(l1, r0);
+  t[2] = add(inner_product(l1, r1), inner_product(l2, r0));
+  t[3] = add(inner_product(l2, r1), inner_product(l3, r0));
+  t[4] = add(inner_product(l1, r3), inner_product(l3, r1));
+  t[5] = inner_product(l2, r3);
+  t[6] = inner_product(l3, r3);
+  {
+    std::vector<Enc32> T;
+    BPP_TRY(pedersen_host(ctx, G, {t[1], t[3], t[4], t[5], t[6]}, taus, T));
+    static const char* lab[5] = {"T1", "T3", "T4", "T5", "T6"};
+    for (int i = 0; i < 5; ++i) {
+      P.T[i] = T[i];
+      tr.append_point(lab[i], T[i].data());
+    }
+  }
+  const Sc x = tr.challenge_scalar("x");
+  std::vector<Sc> xp = hsc::powers(x, 7);
+  const int tidx[5] = {1, 3, 4, 5, 6};
+  Sc tau_x = hsc::mul(xp[2], inner_product(zWV, gamma));
+  for (int i = 0; i < 5; ++i) tau_x = add(tau_x, hsc::mul(taus[i], xp[tidx[i]]));
+  const Sc mu = add(add(hsc::mul(alpha, x), hsc::mul(beta, xp[2])), hsc::mul(rho, xp[3]));
+  std::vector<Sc> l(n_p), r(n_p);
+  for (uint32_t i = 0; i < n_p; ++i) {
+    l[i] = hsc::mul(x, add(l1[i], hsc::mul(x, add(l2[i], hsc::mul(x, l3[i])))));
+    r[i] = add(r0[i], hsc::mul(x, add(r1[i], hsc::mul(xp[2], r3[i]))));
+  }
+  const Sc t_hat = inner_product(l, r);
+  tr.append_scalar("TX", tau_x);
+  tr.append_scalar("mu", mu);
+  tr.append_scalar("t", t_hat);
+  P.tau_x = tau_x;
+  P.mu = mu;
+  P.t_hat = t_hat;
+  const Sc w = tr.challenge_scalar("w");
+
+  uint32_t *d_l, *d_r, *d_hf;
+  BPP_TRY(upload_sc(ctx, l, "pf_l", &d_l));
+  BPP_TRY(upload_sc(ctx, r, "pf_r", &d_r));
+  BPP_TRY(upload_sc(ctx, y_inv_n, "pf_hf", &d_hf));
+  IpaGens ig;
+  ig.d_tbl = G->d_tbl;
+  ig.gbase = 0;
+  ig.hbase = (uint32_t)G->n;
+  ig.qidx = G->bidx();
+  ig.qmul = w;
+  BPP_TRY(ipa_prove_dev(ctx, tr, ig, n_p, nullptr, d_hf, d_l, d_r, P.ipa));
+  return BPP_OK;
+}
+
+// Verifier: host scalars for one proof.  gen_sc (2n_p + 2: G, H, B, Bb) is
+// ACCUMULATED with weight `wt`; proof-point scalars (m + 8 + 2lg, order
+// V, A_I, A_O, S, T1..T6, L.., R..) are appended to pt_sc.
+bool verify_scalars(const perm::Circuit& C, const Proof& P, merlin::Transcript& tr, const Sc& wt,
+                    std::vector<Sc>& gen_sc, std::vector<Sc>& pt_sc, Sc* weight_challenge) {
+  const uint32_t k = C.k, n_p = C.n_p, m = C.m;
+  if (P.V.size() != m) return false;
+  tr.arithmetic_domain_sep(n_p);
+  for (uint32_t j = 0; j < 2 * k; ++j) tr.append_point("V", P.V[j].data());
+  const Sc x_perm = tr.challenge_scalar("x_perm");
+  tr.append_point("V", P.V[2 * k].data());
+  if (!tr.validate_and_append_point("A_I", P.AI.data())) return false;
+  if (!tr.validate_and_append_point("A_O", P.AO.data())) return false;
+  if (!tr.validate_and_append_point("S", P.S.data())) return false;
+  const Sc y = tr.challenge_scalar("y");
+  const Sc z = tr.challenge_scalar("z");
+  static const char* lab[5] = {"T1", "T3", "T4", "T5", "T6"};
+  for (int i = 0; i < 5; ++i)
+    if (!tr.validate_and_append_point(lab[i], P.T[i].data())) return false;
+  const Sc x = tr.challenge_scalar("x");
+  tr.append_scalar("TX", P.tau_x);
+  tr.append_scalar("mu", P.mu);
+  tr.append_scalar("t", P.t_hat);
+  const Sc w = tr.challenge_scalar("w");
+  std::vector<Sc> u_sq, uinv_sq, s;
+  if (!ipa_verification_scalars(tr, n_p, P.ipa.L, P.ipa.R, u_sq, uinv_sq, s)) return false;
+  const Sc r = tr.challenge_scalar("t-check-weight");
+  if (weight_challenge) *weight_challenge = r;
+
+  std::vector<Sc> xp = hsc::powers(x, 7);
+  std::vector<Sc> y_inv_n = hsc::powers(hsc::invert(y), n_p);
+  std::vector<Sc> zq = hsc::powers(z, C.Q + 1);
+  zq.erase(zq.begin());
+  const std::vector<Sc> zWL = perm::zW(C.WL, zq, n_p), zWR = perm::zW(C.WR, zq, n_p), zWO = perm::zW(C.WO, zq, n_p),
+                        zWV = perm::zW(C.WV, zq, m);
+  std::vector<Sc> c = C.c;
+  c[C.Q - 1] = hsc::neg(x_perm);
+  using hsc::add;
+  using hsc::mul;
+  using hsc::neg;
+  using hsc::sub;
+  Sc delta = hsc::zero();
+  for (uint32_t i = 0; i < n_p; ++i) delta = add(delta, mul(mul(y_inv_n[i], zWR[i]), zWL[i]));
+  const Sc zc = hsc::inner_product(zq, c);
+  const Sc a = P.ipa.a, b = P.ipa.b;
+  // generators (merged t-check and IPA-check scalars)
+  for (uint32_t i = 0; i < n_p; ++i) {
+    const Sc gi = sub(mul(a, s[i]), mul(mul(x, y_inv_n[i]), zWR[i]));
+    const Sc hi = add(sub(mul(mul(b, s[n_p - 1 - i]), y_inv_n[i]), mul(y_inv_n[i], add(mul(x, zWL[i]), zWO[i]))),
+                      hsc::one());
+    gen_sc[i] = add(gen_sc[i], mul(wt, gi));
+    gen_sc[n_p + i] = add(gen_sc[n_p + i], mul(wt, hi));
+  }
+  const Sc tcheck_B = mul(r, sub(P.t_hat, mul(xp[2], add(delta, zc))));
+  const Sc ipa_B = mul(w, sub(mul(a, b), P.t_hat));
+  gen_sc[2 * n_p] = add(gen_sc[2 * n_p], mul(wt, add(tcheck_B, ipa_B)));
+  gen_sc[2 * n_p + 1] = add(gen_sc[2 * n_p + 1], mul(wt, add(mul(r, P.tau_x), P.mu)));
+  // proof points
+  for (uint32_t j = 0; j < m; ++j) pt_sc.push_back(mul(wt, neg(mul(mul(r, xp[2]), zWV[j]))));
+  pt_sc.push_back(mul(wt, neg(x)));
+  pt_sc.push_back(mul(wt, neg(xp[2])));
+  pt_sc.push_back(mul(wt, neg(xp[3])));
+  const int tidx[5] = {1, 3, 4, 5, 6};
+  for (int i = 0; i < 5; ++i) pt_sc.push_back(mul(wt, neg(mul(r, xp[tidx[i]]))));
+  for (uint32_t j = 0; j < C.lg; ++j) pt_sc.push_back(mul(wt, neg(u_sq[j])));
+  for (uint32_t j = 0; j < C.lg; ++j) pt_sc.push_back(mul(wt, neg(uinv_sq[j])));
+  return true;
+}
+
+void proof_points(const Proof& P, std::vector<uint8_t>& enc) {
+  auto add = [&](const Enc32& e) { enc.insert(enc.end(), e.begin(), e.end()); };
+  for (auto& v : P.V) add(v);
+  add(P.AI);
+  add(P.AO);
+  add(P.S);
+  for (int i = 0; i < 5; ++i) add(P.T[i]);
+  for (auto& l : P.ipa.L) add(l);
+  for (auto& r : P.ipa.R) add(r);
+}
+
+// Verify `count` proofs with ONE MSM: generator scalars summed across proofs
+// with per-proof weights from a batch transcript.
+int verify_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const uint8_t* label, size_t llen,
+                 size_t count, const uint8_t* proofs, size_t proof_stride, const uint8_t* V) {
+  const uint32_t n_p = C.n_p;
+  if (G->n < n_p) {
+    ctx->err = "generators shorter than the padded circuit";
+    return BPP_ERR_LEN;
+  }
+  std::vector<Sc> gen_sc(2 * n_p + 2, hsc::zero());
+  std::vector<Sc> pt_sc;
+  std::vector<uint8_t> enc;
+  merlin::Transcript batch((const uint8_t*)"bp-perm-batch-verify", 20);
+  std::vector<Proof> Ps(count);
+  std::vector<Sc> rs(count);
+  // pass 1: parse and replay transcripts to get each proof's weight challenge
+  for (size_t p = 0; p < count; ++p) {
+    if (!deserialize(C, proofs + p * proof_stride, perm::proof_len(C.k), V + p * 32 * C.m, Ps[p])) return BPP_ERR_VERIFY;
+    merlin::Transcript tr(label, llen);
+    std::vector<Sc> g_tmp(2 * n_p + 2, hsc::zero()), p_tmp;
+    if (!verify_scalars(C, Ps[p], tr, hsc::one(), g_tmp, p_tmp, &rs[p])) return BPP_ERR_VERIFY;
+    batch.append_scalar("r", rs[p]);
+  }
+  for (size_t p = 0; p < count; ++p) {
+    const Sc wt = count == 1 ? hsc::one() : batch.challenge_scalar("proof-weight");
+    merlin::Transcript tr(label, llen);
+    if (!verify_scalars(C, Ps[p], tr, wt, gen_sc, pt_sc, nullptr)) return BPP_ERR_VERIFY;
+    proof_points(Ps[p], enc);
+  }
+  uint32_t* d_x = nullptr;
+  int rc = decompress_ws(ctx, enc.data(), enc.size() / 32, "pv_x", &d_x);
+  if (rc == BPP_ERR_DECOMPRESS) return BPP_ERR_VERIFY;
+  BPP_TRY(rc);
+  const uint32_t n0 = (uint32_t)(2 * G->n + 2);
+  std::vector<Sc> sc;
+  std::vector<uint32_t> idx;
+  for (uint32_t i = 0; i < n_p; ++i) {
+    sc.push_back(gen_sc[i]);
+    idx.push_back(G->gidx(i));
+  }
+  for (uint32_t i = 0; i < n_p; ++i) {
+    sc.push_back(gen_sc[n_p + i]);
+    idx.push_back(G->hidx(i));
+  }
+  sc.push_back(gen_sc[2 * n_p]);
+  idx.push_back(G->bidx());
+  sc.push_back(gen_sc[2 * n_p + 1]);
+  idx.push_back(G->bbidx());
+  for (size_t j = 0; j < pt_sc.size(); ++j) {
+    sc.push_back(pt_sc[j]);
+    idx.push_back(n0 + (uint32_t)j);
+  }
+  std::vector<h25519::ge> res;
+  BPP_TRY(msm_terms(ctx, sc, idx, {0, (uint32_t)sc.size()}, G->d_tbl, d_x, n0, res));
+  uint8_t e[32];
+  h25519::encode(e, res[0]);
+  static const uint8_t zero[32] = {0};
+  return memcmp(e, zero, 32) == 0 ? BPP_OK : BPP_ERR_VERIFY;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t bpp_perm_proof_len(uint32_t k) { return k >= 2 ? perm::proof_len(k) : 0; }
+
+int bpp_perm_prove(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, uint64_t seed, const uint8_t* label, size_t llen,
+                   uint8_t* proof_out, uint8_t* V_out, uint32_t* perm_out) {
+  if (!ctx || !G || !proof_out || !V_out || (!label && llen) || k < 2 || k > (1u << 20)) return BPP_ERR_ARG;
+  const perm::Circuit C = perm::build(k);
+  if (G->n < C.n_p) {
+    ctx->err = "generators shorter than the padded circuit";
+    return BPP_ERR_LEN;
+  }
+  BPP_HIP(hipSetDevice(ctx->device));
+  merlin::Transcript tr(label, llen);
+  Proof P;
+  std::vector<uint32_t> pi;
+  BPP_TRY(prove_one(ctx, G, C, seed, tr, P, &pi));
+  serialize(C, P, proof_out);
+  for (uint32_t j = 0; j < C.m; ++j) memcpy(V_out + 32 * j, P.V[j].data(), 32);
+  if (perm_out) memcpy(perm_out, pi.data(), 4 * k);
+  return BPP_OK;
+}
+
+int bpp_perm_prove_batch(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, size_t count, const uint64_t* seeds,
+                         const uint8_t* label, size_t llen, uint8_t* proofs_out, uint8_t* V_out) {
+  if (!ctx || !G || !seeds || ((!proofs_out || !V_out) && count)) return BPP_ERR_ARG;
+  const size_t pl = bpp_perm_proof_len(k);
+  for (size_t p = 0; p < count; ++p)
+    BPP_TRY(bpp_perm_prove(ctx, G, k, seeds[p], label, llen, proofs_out + p * pl, V_out + p * 32 * (2 * k + 1),
+                           nullptr));
+  return BPP_OK;
+}
+
+int bpp_perm_verify(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, const uint8_t* label, size_t llen,
+                    const uint8_t* proof, size_t proof_len, const uint8_t* V) {
+  if (!ctx || !G || !proof || !V || (!label && llen) || k < 2) return BPP_ERR_ARG;
+  if (proof_len != perm::proof_len(k)) return BPP_ERR_VERIFY;
+  BPP_HIP(hipSetDevice(ctx->device));
+  const perm::Circuit C = perm::build(k);
+  return verify_batch(ctx, G, C, label, llen, 1, proof, proof_len, V);
+}
+
+int bpp_perm_verify_batch(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, size_t count, const uint8_t* label, size_t llen,
+                          const uint8_t* proofs, const uint8_t* V) {
+  if (!ctx || !G || ((!proofs || !V) && count) || (!label && llen) || k < 2) return BPP_ERR_ARG;
+  if (!count) return BPP_OK;
+  BPP_HIP(hipSetDevice(ctx->device));
+  const perm::Circuit C = perm::build(k);
+  return verify_batch(ctx, G, C, label, llen, count, proofs, perm::proof_len(k), V);
+}
+
+}  // extern "C"

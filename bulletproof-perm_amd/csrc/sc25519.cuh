@@ -1,0 +1,134 @@
+// Scalar field Z/lZ on gfx950: Montgomery (CIOS, R = 2^256), 8 x 32-bit.
+//
+// Device counterpart of dalek's `Scalar` for the data-parallel scalar work
+// of the inner-product argument (bulletproofs 4.0.0 InnerProductProof: the
+// a/b folds a' = a_lo*u + u^-1*a_hi, b' = b_lo*u^-1 + u*b_hi and the cross
+// inner products c_L, c_R) and of the proof's vector polynomials.
+// Values in Montgomery form (x*R mod l) unless a name says otherwise.
+#pragma once
+#include "fe25519.cuh"
+
+struct sc {
+  uint32_t v[8];
+};
+
+__device__ __constant__ static const uint32_t SC_L[8] = {0x5cf5d3edu, 0x5812631au, 0xa2f79cd6u, 0x14def9deu,
+                                                          0x00000000u, 0x00000000u, 0x00000000u, 0x10000000u};
+__device__ __constant__ static const uint32_t SC_R2[8] = {0x449c0f01u, 0xa40611e3u, 0x68859347u, 0xd00e1ba7u,
+                                                           0x17f5be65u, 0xceec73d2u, 0x7c309a3du, 0x0399411bu};
+#define SC_LINV 0x12547e1bu
+
+FE_INLINE sc sc_zero() { sc r; _Pragma("unroll") for (int i = 0; i < 8; ++i) r.v[i] = 0; return r; }
+
+FE_INLINE bool sc_geq_l(const uint32_t a[8]) {
+  _Pragma("unroll") for (int i = 7; i >= 0; --i) {
+    if (a[i] != SC_L[i]) return a[i] > SC_L[i];
+  }
+  return true;
+}
+
+FE_INLINE void sc_sub_l(uint32_t a[8]) {
+  int64_t br = 0;
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) {
+    int64_t d = (int64_t)a[i] - (int64_t)SC_L[i] + br;
+    a[i] = (uint32_t)d;
+    br = d >> 32;
+  }
+}
+
+FE_INLINE sc sc_add(const sc& a, const sc& b) {
+  sc r;
+  uint64_t c = 0;
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) {
+    c = (uint64_t)a.v[i] + b.v[i] + (c >> 32);
+    r.v[i] = (uint32_t)c;
+  }
+  if (sc_geq_l(r.v)) sc_sub_l(r.v);
+  return r;
+}
+
+FE_INLINE sc sc_sub(const sc& a, const sc& b) {
+  sc r;
+  int64_t br = 0;
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) {
+    int64_t d = (int64_t)a.v[i] - (int64_t)b.v[i] + br;
+    r.v[i] = (uint32_t)d;
+    br = d >> 32;
+  }
+  if (br) {
+    uint64_t c = 0;
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) {
+      c = (uint64_t)r.v[i] + SC_L[i] + (c >> 32);
+      r.v[i] = (uint32_t)c;
+    }
+  }
+  return r;
+}
+
+FE_INLINE sc sc_neg(const sc& a) { return sc_sub(sc_zero(), a); }
+
+// a*b*R^-1 mod l; requires a*b < l*R (true for a, b < 2^256 when one is < l)
+FE_INLINE sc sc_mont(const sc& a, const sc& b) {
+  uint32_t t[10];
+  _Pragma("unroll") for (int i = 0; i < 10; ++i) t[i] = 0;
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) {
+    uint64_t c = 0;
+    _Pragma("unroll") for (int j = 0; j < 8; ++j) {
+      c = (uint64_t)a.v[i] * b.v[j] + t[j] + (c >> 32);
+      t[j] = (uint32_t)c;
+    }
+    c = (uint64_t)t[8] + (c >> 32);
+    t[8] = (uint32_t)c;
+    t[9] = (uint32_t)(c >> 32);
+    const uint32_t m = t[0] * SC_LINV;
+    c = (uint64_t)m * SC_L[0] + t[0];
+    _Pragma("unroll") for (int j = 1; j < 8; ++j) {
+      c = (uint64_t)m * SC_L[j] + t[j] + (c >> 32);
+      t[j - 1] = (uint32_t)c;
+    }
+    c = (uint64_t)t[8] + (c >> 32);
+    t[7] = (uint32_t)c;
+    t[8] = t[9] + (uint32_t)(c >> 32);
+  }
+  sc r;
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) r.v[i] = t[i];
+  if (t[8] || sc_geq_l(r.v)) sc_sub_l(r.v);
+  return r;
+}
+
+FE_INLINE sc sc_load(const uint32_t* p) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  uint4 a = q[0], b = q[1];
+  sc r;
+  r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
+  r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
+  return r;
+}
+
+FE_INLINE void sc_store(uint32_t* p, const sc& a) {
+  uint4* q = reinterpret_cast<uint4*>(p);
+  q[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
+  q[1] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+}
+
+// canonical -> Montgomery and back
+FE_INLINE sc sc_to_mont(const sc& a) {
+  sc r2;
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) r2.v[i] = SC_R2[i];
+  return sc_mont(a, r2);
+}
+FE_INLINE sc sc_from_mont(const sc& a) {
+  sc one = sc_zero();
+  one.v[0] = 1;
+  return sc_mont(a, one);
+}
+
+// 64-lane wave reduction of a Montgomery scalar sum (result valid in lane 0)
+FE_INLINE sc sc_wave_sum(sc a) {
+  _Pragma("unroll") for (int d = 32; d >= 1; d >>= 1) {
+    sc o;
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) o.v[i] = __shfl_down(a.v[i], d, 64);
+    a = sc_add(a, o);
+  }
+  return a;
+}

@@ -115,6 +115,84 @@ int bpp_partials_finish(const uint8_t* partials, size_t count, uint8_t out[32]);
 int bpp_msm_batch(bpp_ctx* ctx, size_t count, const uint64_t* offsets, const uint8_t* scalars,
                   const uint32_t* point_idx, const bpp_points* tbl, uint8_t* out);
 
+/* ----------------------------------------------------------- generators */
+typedef struct bpp_gens bpp_gens;
+/* BulletproofGens::new(n, 1) (G, H from the SHAKE256 GeneratorsChain) plus
+ * PedersenGens::default() (B, B_blinding), generated on the GPU and kept
+ * resident with fixed-base tables for B and B_blinding.
+ * Reference: lib.rs:163 (BulletproofGens::new), weights.rs:58 (PedersenGens). */
+int bpp_gens_create(bpp_ctx* ctx, size_t n, bpp_gens** out);
+/* Explicit generators (the reference's test draws random G, H and a random
+ * PedersenGens, lib.rs:164-180).  G_enc, H_enc: n x 32 bytes. */
+int bpp_gens_from_points(bpp_ctx* ctx, const uint8_t* G_enc, const uint8_t* H_enc, size_t n,
+                         const uint8_t B_enc[32], const uint8_t Bb_enc[32], bpp_gens** out);
+size_t bpp_gens_len(const bpp_gens* g);
+/* Compressed G[0..n), H[0..n), B, B_blinding: (2n + 2) x 32 bytes. */
+int bpp_gens_export(bpp_ctx* ctx, const bpp_gens* g, uint8_t* out);
+void bpp_gens_destroy(bpp_gens* g);
+
+/* ------------------------------------------------- Pedersen commitments */
+/* V_j = v_j * B + gamma_j * B_blinding for j < m (PedersenGens::commit,
+ * weights.rs:58-61), fixed-base on the GPU. */
+int bpp_pedersen_commit_batch(bpp_ctx* ctx, const bpp_gens* g, const uint8_t* v, const uint8_t* gamma, size_t m,
+                              uint8_t* out);
+/* blind * B_blinding + <a, G[0..n)> (+ <b, H[0..n)> when b != NULL):
+ * A_I / A_O / S of circuit_lib.rs:187-229. */
+int bpp_vec_commit(bpp_ctx* ctx, const bpp_gens* g, const uint8_t blind[32], const uint8_t* a, const uint8_t* b,
+                   size_t n, uint8_t out[32]);
+
+/* ------------------------------------------------------ Merlin transcript */
+typedef struct bpp_transcript bpp_transcript;
+/* merlin 3.0.0 Transcript::new(label); byte-exact (transcript_protocol.rs). */
+bpp_transcript* bpp_transcript_new(const uint8_t* label, size_t len);
+bpp_transcript* bpp_transcript_clone(const bpp_transcript* t);
+void bpp_transcript_destroy(bpp_transcript* t);
+int bpp_transcript_append_message(bpp_transcript* t, const uint8_t* label, size_t llen, const uint8_t* msg,
+                                  size_t mlen);
+int bpp_transcript_append_u64(bpp_transcript* t, const uint8_t* label, size_t llen, uint64_t x);
+int bpp_transcript_challenge_bytes(bpp_transcript* t, const uint8_t* label, size_t llen, uint8_t* out, size_t n);
+/* challenge_scalar: 64 challenge bytes -> Scalar::from_bytes_mod_order_wide
+ * (transcript_protocol.rs:62-67). */
+int bpp_transcript_challenge_scalar(bpp_transcript* t, const uint8_t* label, size_t llen, uint8_t out[32]);
+
+/* ------------------------------------------------ inner-product argument */
+/* bulletproofs 4.0.0 InnerProductProof::create over G[0..n), H[0..n) of g
+ * (n a power of two, n <= bpp_gens_len): L_out, R_out receive log2(n)
+ * compressed points each; G_factors / H_factors may be NULL (all ones). */
+int bpp_ipa_prove(bpp_ctx* ctx, const bpp_gens* g, bpp_transcript* tr, const uint8_t Q[32], const uint8_t* G_factors,
+                  const uint8_t* H_factors, const uint8_t* a, const uint8_t* b, size_t n, uint8_t* L_out,
+                  uint8_t* R_out, uint8_t a_out[32], uint8_t b_out[32]);
+/* InnerProductProof::verify: BPP_OK or BPP_ERR_VERIFY.  One GPU MSM of
+ * 2n + 2log2(n) + 2 terms checked against the identity. */
+int bpp_ipa_verify(bpp_ctx* ctx, const bpp_gens* g, bpp_transcript* tr, size_t n, const uint8_t* G_factors,
+                   const uint8_t* H_factors, const uint8_t P[32], const uint8_t Q[32], const uint8_t* L,
+                   const uint8_t* R, const uint8_t a[32], const uint8_t b[32]);
+
+/* ------------------------------------------- permutation proof (sound) */
+/* Arithmetic-circuit proof that the second half of v = [1..k, pi(1..k), x]
+ * is a permutation of the first (ACProof::ArithmeticCircuitProof,
+ * circuit_lib.rs:139-585 over the circuit of weights.rs:26-204), in sound
+ * form (SURVEY.md §2.2 defects fixed; DESIGN.md "Protocol").  Gates are
+ * padded to n_p = next_pow2(2k) <= bpp_gens_len(g).
+ *
+ * Proof bytes (bpp_perm_proof_len(k)): A_I A_O S T1 T3 T4 T5 T6 | tau_x mu
+ * t_hat | L_0 R_0 .. L_{lg-1} R_{lg-1} | a b.  The 2k+1 Pedersen
+ * commitments V go to V_out (public inputs, 32 bytes each).  All prover
+ * randomness (pi, blindings) comes from SHAKE256("bpperm-prove" || seed),
+ * the injected stand-in for the reference's thread_rng (circuit_lib.rs:175). */
+size_t bpp_perm_proof_len(uint32_t k);
+int bpp_perm_prove(bpp_ctx* ctx, const bpp_gens* g, uint32_t k, uint64_t seed, const uint8_t* label, size_t llen,
+                   uint8_t* proof_out, uint8_t* V_out, uint32_t* perm_out);
+int bpp_perm_prove_batch(bpp_ctx* ctx, const bpp_gens* g, uint32_t k, size_t count, const uint64_t* seeds,
+                         const uint8_t* label, size_t llen, uint8_t* proofs_out, uint8_t* V_out);
+/* BPP_OK or BPP_ERR_VERIFY (ProofError::VerificationError). One GPU MSM. */
+int bpp_perm_verify(bpp_ctx* ctx, const bpp_gens* g, uint32_t k, const uint8_t* label, size_t llen,
+                    const uint8_t* proof, size_t proof_len, const uint8_t* V);
+/* Batch verification: all proofs' checks folded with transcript-derived
+ * weights into ONE MSM (generator scalars merged across proofs). */
+int bpp_perm_verify_batch(bpp_ctx* ctx, const bpp_gens* g, uint32_t k, size_t count, const uint8_t* label,
+                          size_t llen, const uint8_t* proofs, const uint8_t* V);
+
 #ifdef __cplusplus
 }
 #endif

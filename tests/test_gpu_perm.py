@@ -1,0 +1,57 @@
+"""GPU parity for the permutation proof (sound mode): proof bytes and V
+commitments bit-exact vs the oracle (oracle/bulletproofs.py ac_prove) for the
+same seed; verification accepts valid proofs and rejects tampered ones."""
+import pytest
+
+from oracle import bulletproofs as bp, ristretto as r255
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gens(ctx):
+    import bpperm
+    g = bpperm.Gens(ctx, 128)
+    yield g
+    g.close()
+
+
+@pytest.mark.parametrize("k,seed", [(2, 1), (3, 2), (4, 3), (5, 4), (8, 5)])
+def test_perm_proof_bit_exact_vs_oracle(gens, k, seed):
+    import bpperm
+    want, perm = bp.ac_prove(k, seed)
+    pr = bpperm.PermProver(gens, k)
+    proof, V, gperm = pr.prove(seed)
+    assert gperm == perm
+    assert V == want.V
+    assert proof == want.to_bytes()
+    assert pr.verify(proof, V)
+    assert bp.ac_verify(k, want)
+
+
+def test_perm_verify_rejects_tampering(gens):
+    import bpperm
+    pr = bpperm.PermProver(gens, 4)
+    proof, V, _ = pr.prove(7)
+    assert pr.verify(proof, V)
+    for off in (0, 100, 8 * 32 + 5, 9 * 32, 11 * 32 + 3, len(proof) - 40, len(proof) - 1):
+        bad = bytearray(proof)
+        bad[off] ^= 1
+        assert not pr.verify(bytes(bad), V), off
+    badV = list(V)
+    badV[1], badV[2] = badV[2], badV[1]
+    assert not pr.verify(proof, badV)
+    other = bpperm.PermProver(gens, 4, label=b"other")
+    assert not other.verify(proof, V)
+
+
+def test_perm_batch_verify(gens):
+    import bpperm
+    pr = bpperm.PermProver(gens, 6)
+    proofs, Vs = pr.prove_batch([11, 12, 13, 14])
+    assert pr.verify_batch(proofs, Vs)
+    bad = list(proofs)
+    b = bytearray(bad[2])
+    b[40] ^= 1
+    bad[2] = bytes(b)
+    assert not pr.verify_batch(bad, Vs)

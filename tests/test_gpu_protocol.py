@@ -1,0 +1,95 @@
+"""GPU parity for the protocol rows: generators, Pedersen commitments,
+vector commitments, Merlin transcript, inner-product argument."""
+import pytest
+
+from oracle import bulletproofs as bp, merlin, ristretto as r255
+from oracle.merlin import Rng
+
+pytestmark = pytest.mark.gpu
+
+
+def sb(s):
+    return r255.scalar_bytes(s)
+
+
+@pytest.fixture(scope="module")
+def gens16(ctx):
+    import bpperm
+    g = bpperm.Gens(ctx, 16)
+    yield g
+    g.close()
+
+
+def test_gens_match_bulletproofs_spec(gens16):
+    G, H, B, Bb = gens16.export()
+    oG, oH = merlin.bulletproof_gens(16)
+    ob, obb = merlin.pedersen_gens_default()
+    assert G == [r255.encode(p) for p in oG]
+    assert H == [r255.encode(p) for p in oH]
+    assert B == r255.encode(ob) and Bb == r255.encode(obb)
+
+
+def test_pedersen_commit_batch(gens16):
+    rng = Rng(5)
+    L = r255.L
+    v = [rng.scalar() for _ in range(50)] + [0, 1, L - 1, 2**252]
+    g = [rng.scalar() for _ in range(50)] + [L - 1, 0, 7, 2**252 - 1]
+    got = gens16.pedersen_commit([sb(x) for x in v], [sb(x) for x in g])
+    B, Bb = merlin.pedersen_gens_default()
+    want = [r255.encode(r255.msm([a, c], [B, Bb])) for a, c in zip(v, g)]
+    assert got == want
+
+
+def test_vec_commit(gens16):
+    rng = Rng(6)
+    oG, oH = merlin.bulletproof_gens(16)
+    _, Bb = merlin.pedersen_gens_default()
+    a = [rng.scalar() for _ in range(16)]
+    b = [rng.scalar() for _ in range(16)]
+    blind = rng.scalar()
+    assert gens16.vec_commit(sb(blind), [sb(x) for x in a], [sb(x) for x in b]) == \
+        r255.encode(bp.msm([blind] + a + b, [Bb] + oG + oH))
+    assert gens16.vec_commit(sb(blind), [sb(x) for x in a[:9]]) == \
+        r255.encode(bp.msm([blind] + a[:9], [Bb] + oG[:9]))
+
+
+def test_transcript_matches_merlin_kat():
+    import bpperm
+    t = bpperm.Transcript(b"test protocol")
+    t.append_message(b"some label", b"some data")
+    assert t.challenge_bytes(b"challenge", 32).hex() == \
+        "d5a21972d0d5fe320c0d263fac7fffb8145aa640af6e9bca177c03c7efcf0615"
+    o = merlin.Transcript(b"x")
+    t = bpperm.Transcript(b"x")
+    for i in range(5):
+        o.append_u64(b"n", i)
+        t.append_u64(b"n", i)
+        o.append_message(b"m" * i, bytes(range(i * 40)))
+        t.append_message(b"m" * i, bytes(range(i * 40)))
+        assert t.challenge_scalar(b"c") == sb(o.challenge_scalar(b"c"))
+
+
+@pytest.mark.parametrize("n", [1, 2, 8, 16])
+def test_ipa_prove_matches_oracle_and_verifies(ctx, gens16, n):
+    import bpperm
+    rng = Rng(100 + n)
+    oG, oH = merlin.bulletproof_gens(16)
+    G, H = oG[:n], oH[:n]
+    Q = rng.point()
+    a = [rng.scalar() for _ in range(n)]
+    b = [rng.scalar() for _ in range(n)]
+    gf = [rng.scalar() for _ in range(n)]
+    hf = [rng.scalar() for _ in range(n)]
+    want = bp.ipa_create(merlin.Transcript(b"ipa-test"), Q, gf, hf, G, H, a, b)
+    L, R, ga, gb = gens16.ipa_prove(bpperm.Transcript(b"ipa-test"), r255.encode(Q), [sb(x) for x in gf],
+                                    [sb(x) for x in hf], [sb(x) for x in a], [sb(x) for x in b])
+    assert L == want.L and R == want.R
+    assert ga == sb(want.a) and gb == sb(want.b)
+    P = bp.msm([x * f for x, f in zip(a, gf)] + [x * f for x, f in zip(b, hf)] + [bp.inner(a, b)], G + H + [Q])
+    args = (n, [sb(x) for x in gf], [sb(x) for x in hf], r255.encode(P), r255.encode(Q), L, R, ga, gb)
+    assert gens16.ipa_verify(bpperm.Transcript(b"ipa-test"), *args)
+    if n > 1:  # with no rounds the transcript never reaches a challenge
+        assert not gens16.ipa_verify(bpperm.Transcript(b"other"), *args)
+    bad = list(args)
+    bad[7] = sb((want.a + 1) % r255.L)
+    assert not gens16.ipa_verify(bpperm.Transcript(b"ipa-test"), *bad)

@@ -26,7 +26,7 @@ __global__ void k_decompress(const uint32_t* __restrict__ enc, size_t n, uint32_
 __global__ void k_from_uniform(const uint32_t* __restrict__ bytes, size_t n, uint32_t* __restrict__ tbl);
 
 // thread t: base = t / 512, pos = (t / 8) % 64, d = t % 8 + 1 -> d * 16^pos * P_base
-__global__ void k_fb_tables(const uint32_t* __restrict__ tbl, uint32_t b0, uint32_t b1, uint32_t* __restrict__ fb) {
+__global__ void __launch_bounds__(64) k_fb_tables(const uint32_t* __restrict__ tbl, uint32_t b0, uint32_t b1, uint32_t* __restrict__ fb) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= 2 * FB_POS * 8) return;
   const uint32_t base = t / (FB_POS * 8), pos = (t / 8) % FB_POS, d = t % 8 + 1;
@@ -62,7 +62,7 @@ FE_INLINE ge_p3 fb_mul_add(ge_p3 acc, const uint32_t* __restrict__ fb, uint32_t 
 }
 
 // out[j] = compress(v_j * B + g_j * Bb); scalars canonical (8 words each)
-__global__ void __launch_bounds__(256) k_pedersen(const uint32_t* __restrict__ fb, const uint32_t* __restrict__ v,
+__global__ void __launch_bounds__(64) k_pedersen(const uint32_t* __restrict__ fb, const uint32_t* __restrict__ v,
                                                  const uint32_t* __restrict__ gam, size_t m,
                                                  uint32_t* __restrict__ out_enc, uint32_t* __restrict__ out_p3) {
   const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -24,7 +24,7 @@
 
 static unsigned grid_for(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
-__global__ void k_ipa_init(uint32_t n, const uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
+__global__ void __launch_bounds__(256) k_ipa_init(uint32_t n, const uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
                            const uint32_t* __restrict__ gf, const uint32_t* __restrict__ hf, uint32_t* __restrict__ am,
                            uint32_t* __restrict__ bm, uint32_t* __restrict__ fG, uint32_t* __restrict__ fH) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -39,7 +39,7 @@ __global__ void k_ipa_init(uint32_t n, const uint32_t* __restrict__ a, const uin
 
 // terms of L at [0, n+1), of R at [n+1, 2n+2); slots n and 2n+1 (Q) are
 // written by k_ipa_cross_final.
-__global__ void k_ipa_terms(uint32_t n, uint32_t m, uint32_t lg_h, const uint32_t* __restrict__ am,
+__global__ void __launch_bounds__(256) k_ipa_terms(uint32_t n, uint32_t m, uint32_t lg_h, const uint32_t* __restrict__ am,
                             const uint32_t* __restrict__ bm, const uint32_t* __restrict__ fG,
                             const uint32_t* __restrict__ fH, uint32_t gbase, uint32_t hbase,
                             uint32_t* __restrict__ scal, uint32_t* __restrict__ pidx) {
@@ -95,7 +95,7 @@ __global__ void __launch_bounds__(CROSS_T) k_ipa_cross(uint32_t h, const uint32_
   }
 }
 
-__global__ void k_ipa_cross_final(uint32_t nblk, const uint32_t* __restrict__ part, sc qmul, uint32_t qidx, uint32_t n,
+__global__ void __launch_bounds__(64) k_ipa_cross_final(uint32_t nblk, const uint32_t* __restrict__ part, sc qmul, uint32_t qidx, uint32_t n,
                                   uint32_t* __restrict__ scal, uint32_t* __restrict__ pidx) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   sc sl = sc_zero(), sr = sc_zero();
@@ -110,7 +110,7 @@ __global__ void k_ipa_cross_final(uint32_t nblk, const uint32_t* __restrict__ pa
   pidx[2 * n + 1] = qidx;
 }
 
-__global__ void k_ipa_fold(uint32_t n, uint32_t m, uint32_t* __restrict__ am, uint32_t* __restrict__ bm,
+__global__ void __launch_bounds__(256) k_ipa_fold(uint32_t n, uint32_t m, uint32_t* __restrict__ am, uint32_t* __restrict__ bm,
                            uint32_t* __restrict__ fG, uint32_t* __restrict__ fH, sc um, sc uim) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;

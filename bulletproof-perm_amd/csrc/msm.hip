@@ -1,6 +1,7 @@
 // MSM engine (host orchestration of msm_kernels.cuh) and its C-ABI entry
 // points: bpp_msm, bpp_msm_table, bpp_msm_table_dev, bpp_msm_batch and the
 // window-partitioned variants used for multi-GPU.
+#include <algorithm>
 #include <cstring>
 
 #include "ctx.h"
@@ -25,7 +26,9 @@ bool scalar_is_canonical(const uint8_t* s) {
 uint32_t msm_choose_c(double n_per_msm) {
   uint32_t best = 4;
   double bestc = 1e300;
-  for (uint32_t c = 2; c <= 20; ++c) {
+  // c <= 15: keeps |digit| - 1 in 14 bits (16-bit digit codes) and a
+  // window's bucket histogram (2^(c-1) x 4 B) within 64 KB of LDS.
+  for (uint32_t c = 2; c <= 15; ++c) {
     const uint32_t W = (254 + c - 1) / c;
     const double cost = (double)W * (7.0 * n_per_msm + 9.0 * (double)(1u << c)) + 8.0 * c * (W - 1);
     if (cost < bestc) {
@@ -60,39 +63,87 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
   BPP_TRY(ctx_ws(ctx, "msm_wsum", nseg * 128, &wsum));
   BPP_HIP(hipMemsetAsync(cnt, 0, (NB + 1) * 4, ctx->stream));
   BPP_HIP(hipMemsetAsync(cur, 0, NB * 4, ctx->stream));
-  if (T) {
-    ProfScope ps(ctx, "msm_count");
-    hipLaunchKernelGGL(k_msm_count, dim3(grid_for(T, 256)), dim3(256), 0, ctx->stream, d_scal, d_off, g,
-                       (uint32_t*)cnt);
+  const bool lds_sort = (M == 1) && (c <= 15) && (T >= 16384);
+  if (lds_sort && T) {
+    void* dig = nullptr;
+    BPP_TRY(ctx_ws(ctx, "msm_dig", (size_t)T * Wn * 2 + 16, &dig));
+    {
+      ProfScope ps(ctx, "msm_digits");
+      hipLaunchKernelGGL(k_msm_digits, dim3(grid_for(T, 256)), dim3(256), 0, ctx->stream, d_scal, g, (uint16_t*)dig);
+    }
+    BPP_TRY(ctx_check_launch(ctx, "k_msm_digits"));
+    // ~2 blocks per CU in total
+    uint32_t nchunk = std::max<uint32_t>(1, (512 + Wn - 1) / Wn);
+    nchunk = std::min<uint32_t>(nchunk, std::max<uint32_t>(1, T / 4096));
+    const uint32_t chunk = (T + nchunk - 1) / nchunk;
+    const size_t lds = (size_t)g.B * 4;
+    {
+      ProfScope ps(ctx, "msm_count");
+      hipLaunchKernelGGL(k_msm_count_lds, dim3(Wn * nchunk), dim3(SORT_T), lds, ctx->stream, (const uint16_t*)dig, g,
+                         chunk, nchunk, (uint32_t*)cnt);
+    }
+    BPP_TRY(ctx_check_launch(ctx, "k_msm_count_lds"));
+    {
+      ProfScope ps(ctx, "msm_scan");
+      BPP_TRY(scan_exclusive_u32(ctx, (const uint32_t*)cnt, (uint32_t*)boff, NB + 1));
+    }
+    {
+      ProfScope ps(ctx, "msm_scatter");
+      hipLaunchKernelGGL(k_msm_scatter_lds, dim3(Wn * nchunk), dim3(SORT_T), lds, ctx->stream, (const uint16_t*)dig,
+                         d_pidx, g, chunk, nchunk, (const uint32_t*)boff, (uint32_t*)cur, (uint32_t*)entries);
+    }
+    BPP_TRY(ctx_check_launch(ctx, "k_msm_scatter_lds"));
+  } else {
+    if (T) {
+      ProfScope ps(ctx, "msm_count");
+      hipLaunchKernelGGL(k_msm_count, dim3(grid_for(T, 256)), dim3(256), 0, ctx->stream, d_scal, d_off, g,
+                         (uint32_t*)cnt);
+    }
+    BPP_TRY(ctx_check_launch(ctx, "k_msm_count"));
+    {
+      ProfScope ps(ctx, "msm_scan");
+      BPP_TRY(scan_exclusive_u32(ctx, (const uint32_t*)cnt, (uint32_t*)boff, NB + 1));
+    }
+    if (T) {
+      ProfScope ps(ctx, "msm_scatter");
+      hipLaunchKernelGGL(k_msm_scatter, dim3(grid_for(T, 256)), dim3(256), 0, ctx->stream, d_scal, d_off, d_pidx, g,
+                         (const uint32_t*)boff, (uint32_t*)cur, (uint32_t*)entries);
+    }
+    BPP_TRY(ctx_check_launch(ctx, "k_msm_scatter"));
   }
-  BPP_TRY(ctx_check_launch(ctx, "k_msm_count"));
   {
-    ProfScope ps(ctx, "msm_scan");
-    BPP_TRY(scan_exclusive_u32(ctx, (const uint32_t*)cnt, (uint32_t*)boff, NB + 1));
+    // entries per lane: enough lanes to fill the chip several times over
+    const uint32_t E_max = T * Wn;
+    uint32_t K = 32;
+    while (K > 4 && (E_max / K) < 256u * 1024u) K >>= 1;
+    const size_t lanes = (E_max + K - 1) / K + 1;
+    void *head, *tail;
+    BPP_TRY(ctx_ws(ctx, "msm_head", lanes * 128, &head));
+    BPP_TRY(ctx_ws(ctx, "msm_tail", lanes * 128, &tail));
+    {
+      ProfScope ps(ctx, "msm_accumulate");
+      hipLaunchKernelGGL(k_msm_accumulate, dim3(grid_for(lanes, 256)), dim3(256), 0, ctx->stream, d_tbl, d_tbl1, n0,
+                         (const uint32_t*)entries, (const uint32_t*)boff, (uint32_t)NB, K, (uint32_t*)bsum,
+                         (uint32_t*)head, (uint32_t*)tail);
+    }
+    BPP_TRY(ctx_check_launch(ctx, "k_msm_accumulate"));
+    {
+      ProfScope ps(ctx, "msm_fixup");
+      hipLaunchKernelGGL(k_msm_fixup, dim3(grid_for(NB, 256)), dim3(256), 0, ctx->stream, (const uint32_t*)boff,
+                         (uint32_t)NB, K, (const uint32_t*)head, (const uint32_t*)tail, (uint32_t*)bsum);
+    }
+    BPP_TRY(ctx_check_launch(ctx, "k_msm_fixup"));
   }
-  if (T) {
-    ProfScope ps(ctx, "msm_scatter");
-    hipLaunchKernelGGL(k_msm_scatter, dim3(grid_for(T, 256)), dim3(256), 0, ctx->stream, d_scal, d_off, d_pidx, g,
-                       (const uint32_t*)boff, (uint32_t*)cur, (uint32_t*)entries);
-  }
-  BPP_TRY(ctx_check_launch(ctx, "k_msm_scatter"));
   {
-    ProfScope ps(ctx, "msm_accumulate");
-    hipLaunchKernelGGL(k_msm_accumulate, dim3(grid_for(NB, 256)), dim3(256), 0, ctx->stream, d_tbl, d_tbl1, n0,
-                       (const uint32_t*)entries, (const uint32_t*)boff, (uint32_t)NB, (uint32_t*)bsum);
-  }
-  BPP_TRY(ctx_check_launch(ctx, "k_msm_accumulate"));
-  {
+    const uint32_t L = g.B >= 512 ? 8 : (g.B >= 64 ? 4 : (g.B >= 8 ? 2 : 1));
+    const uint32_t BPS = (g.B + RED_T * L - 1) / (RED_T * L);
+    void* part = nullptr;
+    BPP_TRY(ctx_ws(ctx, "msm_rpart", nseg * BPS * 128, &part));
     ProfScope ps(ctx, "msm_reduce");
-    if (g.B >= 256)
-      hipLaunchKernelGGL(k_msm_reduce<256>, dim3((unsigned)nseg), dim3(256), 0, ctx->stream, (const uint32_t*)bsum, g,
-                         (uint32_t*)wsum);
-    else if (g.B >= 64)
-      hipLaunchKernelGGL(k_msm_reduce<64>, dim3((unsigned)nseg), dim3(64), 0, ctx->stream, (const uint32_t*)bsum, g,
-                         (uint32_t*)wsum);
-    else
-      hipLaunchKernelGGL(k_msm_reduce<8>, dim3((unsigned)nseg), dim3(8), 0, ctx->stream, (const uint32_t*)bsum, g,
-                         (uint32_t*)wsum);
+    hipLaunchKernelGGL(k_msm_reduce_partial, dim3((unsigned)(nseg * BPS)), dim3(RED_T), 0, ctx->stream,
+                       (const uint32_t*)bsum, g, L, BPS, (uint32_t*)part);
+    hipLaunchKernelGGL(k_msm_reduce_final, dim3((unsigned)nseg), dim3(RED_T), 0, ctx->stream, (const uint32_t*)part,
+                       BPS, (uint32_t*)wsum);
   }
   BPP_TRY(ctx_check_launch(ctx, "k_msm_reduce"));
   *d_wsum_out = (uint32_t*)wsum;

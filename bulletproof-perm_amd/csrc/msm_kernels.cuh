@@ -115,37 +115,109 @@ __global__ void k_msm_scatter(const uint32_t* __restrict__ scalars, const uint32
   });
 }
 
-// One lane per bucket.
+// Largest b with boff[b] <= i (boff non-decreasing, boff[0] = 0, i < boff[nb]).
+FE_INLINE uint32_t bucket_of(const uint32_t* __restrict__ boff, uint32_t nb, uint32_t i) {
+  uint32_t lo = 0, hi = nb;  // boff[lo] <= i < boff[hi]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (boff[mid] <= i) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+FE_INLINE ge_niels fetch_entry(const uint32_t* __restrict__ tbl, const uint32_t* __restrict__ tbl1, uint32_t n0,
+                               uint32_t e) {
+  const uint32_t pi = e & 0x7fffffffu;
+  ge_niels q = pi < n0 ? load_niels(tbl, pi) : load_niels(tbl1, pi - n0);
+  if (e & 0x80000000u) q = ge_niels_neg(q);
+  return q;
+}
+
+// Balanced bucket accumulation: lane l owns entries [l*K, (l+1)*K) of the
+// bucket-sorted entry array, so every lane does exactly K mixed additions
+// whatever the bucket-size distribution (the top window of a 253-bit scalar
+// is 8x denser than the others at c = 16).  A run (a bucket's entries inside
+// one chunk) that covers its whole bucket is written to bsum directly; the
+// first / last run of a chunk whose bucket crosses the chunk border goes to
+// head[l] / tail[l] and k_msm_fixup adds the pieces.
 // Points with index < n0 come from tbl, the rest from tbl1[idx - n0] (so a
 // proof's own points can join the resident generators without a copy).
 __global__ void __launch_bounds__(256) k_msm_accumulate(const uint32_t* __restrict__ tbl,
                                                        const uint32_t* __restrict__ tbl1, uint32_t n0,
                                                        const uint32_t* __restrict__ entries,
                                                        const uint32_t* __restrict__ boff, uint32_t nbuckets,
-                                                       uint32_t* __restrict__ bsum) {
+                                                       uint32_t K, uint32_t* __restrict__ bsum,
+                                                       uint32_t* __restrict__ head, uint32_t* __restrict__ tail) {
+  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t E = boff[nbuckets];
+  const uint32_t i0 = l * K;
+  if (i0 >= E) return;
+  const uint32_t i1 = min(i0 + K, E);
+  uint32_t b = bucket_of(boff, nbuckets, i0);
+  uint32_t bstart = boff[b], bend = boff[b + 1];
+  bool first = true;
+  ge_p3 acc = ge_identity();
+  for (uint32_t i = i0; i < i1; ++i) {
+    if (i == bend) {  // close the run of bucket b
+      if (bstart >= i0) store_p3(bsum, b, acc);  // whole bucket inside the chunk
+      else store_p3(head, l, acc);               // first run, bucket started earlier
+      first = false;
+      do { ++b; } while (boff[b + 1] <= i);
+      bstart = boff[b];
+      bend = boff[b + 1];
+      acc = ge_identity();
+    }
+    acc = ge_madd(acc, fetch_entry(tbl, tbl1, n0, entries[i]));
+  }
+  // last run [max(bstart, i0), i1)
+  if (bstart >= i0 && bend <= i1) store_p3(bsum, b, acc);
+  else if (first) store_p3(head, l, acc);  // single run crossing a border
+  else store_p3(tail, l, acc);
+}
+
+// One lane per bucket: identity for empty buckets, and the sum of the
+// pieces for buckets that cross chunk borders.
+__global__ void __launch_bounds__(256) k_msm_fixup(const uint32_t* __restrict__ boff, uint32_t nbuckets, uint32_t K,
+                            const uint32_t* __restrict__ head, const uint32_t* __restrict__ tail,
+                            uint32_t* __restrict__ bsum) {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= nbuckets) return;
-  const uint32_t lo = boff[b], hi = boff[b + 1];
-  ge_p3 acc = ge_identity();
-  for (uint32_t i = lo; i < hi; ++i) {
-    const uint32_t e = entries[i];
-    const uint32_t pi = e & 0x7fffffffu;
-    ge_niels q = pi < n0 ? load_niels(tbl, pi) : load_niels(tbl1, pi - n0);
-    if (e & 0x80000000u) q = ge_niels_neg(q);
-    acc = ge_madd(acc, q);
+  const uint32_t s = boff[b], e = boff[b + 1];
+  if (s == e) {
+    store_p3(bsum, b, ge_identity());
+    return;
   }
+  const uint32_t l0 = s / K, l1 = (e - 1) / K;
+  if (l0 == l1) return;  // written by the accumulate lane
+  ge_p3 acc = (s == l0 * K) ? load_p3(head, l0) : load_p3(tail, l0);
+  for (uint32_t l = l0 + 1; l <= l1; ++l) acc = ge_add(acc, load_p3(head, l));
   store_p3(bsum, b, acc);
 }
 
-// One workgroup (RT lanes) per segment (msm, window): sum_b (b+1) * bsum[b].
-template <int RT>
-__global__ void __launch_bounds__(RT) k_msm_reduce(const uint32_t* __restrict__ bsum, MsmGeom g,
-                                                  uint32_t* __restrict__ wsum) {
-  __shared__ uint32_t lds[RT * 32];
-  const uint32_t seg = blockIdx.x;
-  const uint32_t per = (g.B + RT - 1) / RT;
-  const uint32_t lo = threadIdx.x * per;
-  const uint32_t hi = min(lo + per, g.B);
+// Bucket reduction sum_b (b+1) * bsum[b] per segment (msm, window), in two
+// launches so that enough lanes are in flight (the work is ~1/16 of the
+// accumulation but latency-bound if given few lanes):
+//   k_msm_reduce_partial: block (seg, j) of 64 lanes; lane t owns L buckets
+//     [lo, lo+L): running sum from the top gives sum (b-lo+1) B_b and
+//     run = sum B_b, plus lo*run by double-and-add; LDS tree over the wave.
+//   k_msm_reduce_final: one 64-lane block per segment sums its BPS partials.
+#define RED_T 64
+FE_INLINE ge_p3 lds_tree_sum(uint32_t* lds, ge_p3 v) {
+  store_p3(lds, threadIdx.x, v);
+  __syncthreads();
+  for (uint32_t s = RED_T / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) store_p3(lds, threadIdx.x, ge_add(load_p3(lds, threadIdx.x), load_p3(lds, threadIdx.x + s)));
+    __syncthreads();
+  }
+  return load_p3(lds, 0);
+}
+
+__global__ void __launch_bounds__(RED_T) k_msm_reduce_partial(const uint32_t* __restrict__ bsum, MsmGeom g,
+                                                             uint32_t L, uint32_t BPS, uint32_t* __restrict__ part) {
+  __shared__ uint32_t lds[RED_T * 32];
+  const uint32_t seg = blockIdx.x / BPS, j = blockIdx.x % BPS;
+  const uint32_t lo = (j * RED_T + threadIdx.x) * L;
+  const uint32_t hi = min(lo + L, g.B);
   const size_t base = (size_t)seg * g.B;
   ge_p3 run = ge_identity();
   ge_p3 acc = ge_identity();
@@ -153,34 +225,31 @@ __global__ void __launch_bounds__(RT) k_msm_reduce(const uint32_t* __restrict__ 
     run = ge_add(run, load_p3(bsum, base + b - 1));
     acc = ge_add(acc, run);
   }
-  // acc = sum (b - lo + 1) B_b ; need + lo * run
-  if (lo < hi && lo > 0) {
-    ge_p3 m = ge_identity();
-    bool started = false;
-    for (int bit = 31; bit >= 0; --bit) {
-      if (started) m = ge_dbl(m);
-      if ((lo >> bit) & 1u) {
-        m = started ? ge_add(m, run) : run;
-        started = true;
-      }
+  if (lo < hi && lo > 0) {  // + lo * run
+    ge_p3 m = run;
+    const int top = 31 - __clz(lo);
+    for (int bit = top - 1; bit >= 0; --bit) {
+      m = ge_dbl(m);
+      if ((lo >> bit) & 1u) m = ge_add(m, run);
     }
     acc = ge_add(acc, m);
   }
-  store_p3(lds, threadIdx.x, acc);
-  __syncthreads();
-  for (uint32_t s = RT / 2; s > 0; s >>= 1) {
-    if (threadIdx.x < s) {
-      ge_p3 a = load_p3(lds, threadIdx.x);
-      ge_p3 b = load_p3(lds, threadIdx.x + s);
-      store_p3(lds, threadIdx.x, ge_add(a, b));
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) store_p3(wsum, seg, load_p3(lds, 0));
+  const ge_p3 tot = lds_tree_sum(lds, acc);
+  if (threadIdx.x == 0) store_p3(part, blockIdx.x, tot);
+}
+
+__global__ void __launch_bounds__(RED_T) k_msm_reduce_final(const uint32_t* __restrict__ part, uint32_t BPS,
+                                                           uint32_t* __restrict__ wsum) {
+  __shared__ uint32_t lds[RED_T * 32];
+  const uint32_t seg = blockIdx.x;
+  ge_p3 acc = ge_identity();
+  for (uint32_t j = threadIdx.x; j < BPS; j += RED_T) acc = ge_add(acc, load_p3(part, (size_t)seg * BPS + j));
+  const ge_p3 tot = lds_tree_sum(lds, acc);
+  if (threadIdx.x == 0) store_p3(wsum, seg, tot);
 }
 
 // One lane per MSM: Horner over its W window sums.
-__global__ void k_msm_horner(const uint32_t* __restrict__ wsum, MsmGeom g, uint32_t* __restrict__ out) {
+__global__ void __launch_bounds__(64) k_msm_horner(const uint32_t* __restrict__ wsum, MsmGeom g, uint32_t* __restrict__ out) {
   const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= g.M) return;
   const size_t base = (size_t)m * g.Wn;
@@ -190,4 +259,80 @@ __global__ void k_msm_horner(const uint32_t* __restrict__ wsum, MsmGeom g, uint3
     acc = ge_add(acc, load_p3(wsum, base + w));
   }
   store_p3(out, m, acc);
+}
+
+// ---------------------------------------------------------------------------
+// Single large MSM sort path (M == 1, c <= 15): digits are recoded once into
+// a window-major uint16 array (code = sign << 15 | (|d| - 1), 0xFFFF = zero
+// digit), then one workgroup per (window, chunk of terms) builds the bucket
+// histogram in LDS.  Global memory then sees one coalesced atomic per
+// (block, bucket) instead of one scattered memory-side atomic per
+// (term, window) — the global-atomic kernels above ran at ~26 G atomics/s.
+#define DIG_ZERO 0xFFFFu
+#define SORT_T 1024
+
+__global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __restrict__ scalars, MsmGeom g,
+                                                   uint16_t* __restrict__ dig) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= g.T) return;
+  uint32_t s[8];
+  load_scalar(scalars, t, s);
+  for (uint32_t w = 0; w < g.Wn; ++w) dig[(size_t)w * g.T + t] = (uint16_t)DIG_ZERO;
+  for_each_digit(s, g, [&](uint32_t w, int d) {
+    const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u;
+    dig[(size_t)w * g.T + t] = (uint16_t)(b | (d < 0 ? 0x8000u : 0u));
+  });
+}
+
+// grid = Wn * nchunk blocks; dynamic LDS = B * 4 bytes
+__global__ void __launch_bounds__(SORT_T) k_msm_count_lds(const uint16_t* __restrict__ dig, MsmGeom g, uint32_t chunk,
+                                                         uint32_t nchunk, uint32_t* __restrict__ cnt) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
+  const uint32_t w = blockIdx.x / nchunk, ch = blockIdx.x % nchunk;
+  for (uint32_t b = threadIdx.x; b < g.B; b += SORT_T) hist[b] = 0;
+  __syncthreads();
+  const uint32_t t0 = ch * chunk, t1 = min(t0 + chunk, g.T);
+  const uint16_t* dw = dig + (size_t)w * g.T;
+  for (uint32_t t = t0 + threadIdx.x; t < t1; t += SORT_T) {
+    const uint32_t code = dw[t];
+    if (code != DIG_ZERO) atomicAdd(&hist[code & 0x7FFFu], 1u);
+  }
+  __syncthreads();
+  uint32_t* cw = cnt + ((size_t)w << (g.c - 1));
+  for (uint32_t b = threadIdx.x; b < g.B; b += SORT_T) {
+    const uint32_t h = hist[b];
+    if (h) atomicAdd(&cw[b], h);
+  }
+}
+
+__global__ void __launch_bounds__(SORT_T) k_msm_scatter_lds(const uint16_t* __restrict__ dig,
+                                                           const uint32_t* __restrict__ pidx, MsmGeom g,
+                                                           uint32_t chunk, uint32_t nchunk,
+                                                           const uint32_t* __restrict__ boff,
+                                                           uint32_t* __restrict__ cursor,
+                                                           uint32_t* __restrict__ entries) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
+  const uint32_t w = blockIdx.x / nchunk, ch = blockIdx.x % nchunk;
+  for (uint32_t b = threadIdx.x; b < g.B; b += SORT_T) hist[b] = 0;
+  __syncthreads();
+  const uint32_t t0 = ch * chunk, t1 = min(t0 + chunk, g.T);
+  const uint16_t* dw = dig + (size_t)w * g.T;
+  for (uint32_t t = t0 + threadIdx.x; t < t1; t += SORT_T) {
+    const uint32_t code = dw[t];
+    if (code != DIG_ZERO) atomicAdd(&hist[code & 0x7FFFu], 1u);
+  }
+  __syncthreads();
+  // reserve this block's slice of every bucket: hist[b] becomes a cursor
+  const size_t gb0 = (size_t)w << (g.c - 1);
+  for (uint32_t b = threadIdx.x; b < g.B; b += SORT_T) {
+    const uint32_t h = hist[b];
+    hist[b] = h ? boff[gb0 + b] + atomicAdd(&cursor[gb0 + b], h) : 0u;
+  }
+  __syncthreads();
+  for (uint32_t t = t0 + threadIdx.x; t < t1; t += SORT_T) {
+    const uint32_t code = dw[t];
+    if (code == DIG_ZERO) continue;
+    const uint32_t pos = atomicAdd(&hist[code & 0x7FFFu], 1u);
+    entries[pos] = (pidx ? pidx[t] : t) | (code & 0x8000u ? 0x80000000u : 0u);
+  }
 }

@@ -10,7 +10,7 @@
 #include "ctx.h"
 #include "ge_io.cuh"
 
-__global__ void k_decompress(const uint32_t* __restrict__ enc, size_t n, uint32_t* __restrict__ tbl,
+__global__ void __launch_bounds__(64) k_decompress(const uint32_t* __restrict__ enc, size_t n, uint32_t* __restrict__ tbl,
                              unsigned long long* __restrict__ bad) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -28,7 +28,7 @@ __global__ void k_decompress(const uint32_t* __restrict__ enc, size_t n, uint32_
   store_niels(tbl, (uint32_t)i, ge_niels_from_affine(P.X, P.Y));
 }
 
-__global__ void k_from_uniform(const uint32_t* __restrict__ bytes, size_t n, uint32_t* __restrict__ tbl) {
+__global__ void __launch_bounds__(64) k_from_uniform(const uint32_t* __restrict__ bytes, size_t n, uint32_t* __restrict__ tbl) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t w[16];
@@ -42,7 +42,7 @@ __global__ void k_from_uniform(const uint32_t* __restrict__ bytes, size_t n, uin
   store_niels(tbl, (uint32_t)i, ge_to_niels(P));
 }
 
-__global__ void k_compress_niels(const uint32_t* __restrict__ tbl, size_t n, uint32_t* __restrict__ out) {
+__global__ void __launch_bounds__(64) k_compress_niels(const uint32_t* __restrict__ tbl, size_t n, uint32_t* __restrict__ out) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   ge_p3 P = ge_from_niels(load_niels(tbl, (uint32_t)i));
@@ -53,7 +53,7 @@ __global__ void k_compress_niels(const uint32_t* __restrict__ tbl, size_t n, uin
   o[1] = make_uint4(w[4], w[5], w[6], w[7]);
 }
 
-__global__ void k_compress_p3(const uint32_t* __restrict__ pts, size_t n, uint32_t* __restrict__ out) {
+__global__ void __launch_bounds__(64) k_compress_p3(const uint32_t* __restrict__ pts, size_t n, uint32_t* __restrict__ out) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   ge_p3 P = load_p3(pts, i);

@@ -283,3 +283,33 @@ def signed_digits(s: int, w: int):
             carry = 0
     assert sum(dg << (w * i) for i, dg in enumerate(out)) == s
     return out
+
+
+def msm_window_partial(scalars, points, c: int, W: int, wb: int, we: int):
+    """sum_{w in [wb, we)} 2^(c w) sum_i d_{i,w} P_i for the signed radix-2^c
+    recoding the GPU engine uses (msm_kernels.cuh for_each_digit: digit
+    v >= 2^(c-1) becomes v - 2^c with a carry, except in the last of W
+    windows).  Summing the partials of a partition of [0, W) gives the MSM."""
+    half = 1 << (c - 1)
+    mask = (1 << c) - 1
+    acc = IDENTITY
+    for s, P in zip(scalars, points):
+        carry = 0
+        k = 0
+        for w in range(we):
+            v = ((s >> (c * w)) & mask) + carry
+            if v >= half and w + 1 < W:
+                d, carry = v - (1 << c), 1
+            else:
+                d, carry = v, 0
+            if w >= wb:
+                k += d << (c * w)
+        if k:
+            acc = ed_add(acc, ed_mul(k, P) if k > 0 else ed_neg(ed_mul(-k, P)))
+    return acc
+
+
+def raw_point_bytes(p) -> bytes:
+    """128-byte raw extended form (X, Y, Z, T little-endian) exchanged between
+    ranks; the same layout bpp_msm_table_dev_partial emits."""
+    return b"".join((c % P).to_bytes(32, "little") for c in p)

@@ -47,6 +47,64 @@ def msm_cases():
     return cases
 
 
+
+
+def config2_inputs(n=1024, seed=1):
+    """n = 2^10 Pedersen vector commitment + IPA.
+    A = alpha*B_blinding + <a_L, G> + <a_R, H>; transcript "config2" absorbs A,
+    y = challenge; IPA on (a_L, a_R) with G_factors = 1, H_factors = y^-i and
+    Q = from_uniform_bytes(rng 64 bytes)."""
+    from oracle.merlin import bulletproof_gens, pedersen_gens_default
+    rng = Rng(seed, b"config2")
+    aL = [rng.scalar() for _ in range(n)]
+    aR = [rng.scalar() for _ in range(n)]
+    alpha = rng.scalar()
+    Qraw = rng.bytes(64)
+    G, H = bulletproof_gens(n)
+    _, Bb = pedersen_gens_default()
+    return aL, aR, alpha, Qraw, G, H, Bb
+
+
+def config2_golden(n=1024, seed=1):
+    from oracle import bulletproofs as bp
+    from oracle.merlin import Transcript
+    aL, aR, alpha, Qraw, G, H, Bb = config2_inputs(n, seed)
+    A = r255.encode(bp.msm([alpha] + aL + aR, [Bb] + G + H))
+    tr = Transcript(b"config2")
+    tr.append_point(b"A", A)
+    y = tr.challenge_scalar(b"y")
+    yinv = bp.powers(r255.scalar_inv(y), n)
+    Q = r255.from_uniform_bytes(Qraw)
+    pf = bp.ipa_create(tr, Q, [1] * n, yinv, G, H, aL, aR)
+    return {"n": n, "seed": seed, "A": A.hex(), "L": [x.hex() for x in pf.L], "R": [x.hex() for x in pf.R],
+            "a": r255.scalar_bytes(pf.a).hex(), "b": r255.scalar_bytes(pf.b).hex()}
+
+
+def config1_golden(k=52, seed=0):
+    """52-card permutation proof (sound mode), seed 0."""
+    from oracle import bulletproofs as bp
+    pf, perm = bp.ac_prove(k, seed)
+    assert bp.ac_verify(k, pf)
+    return {"k": k, "seed": seed, "label": "bp-perm", "perm": perm, "V": [v.hex() for v in pf.V],
+            "proof": pf.to_bytes().hex()}
+
+
+def write_protocol():
+    import time
+    t = time.time()
+    c1 = config1_golden()
+    t1 = time.time() - t
+    c2 = config2_golden()
+    out = {"generator": "tests/golden/make_golden.py write_protocol()", "config1": c1, "config2": c2,
+           "oracle_seconds": {"config1": t1, "config2": time.time() - t - t1}}
+    (HERE / "protocol.json").write_text(json.dumps(out, indent=1))
+    print("wrote", HERE / "protocol.json", out["oracle_seconds"])
+
+
 if __name__ == "__main__":
-    (HERE / "msm.json").write_text(json.dumps({"generator": "tests/golden/make_golden.py", "cases": msm_cases()}))
-    print("wrote", HERE / "msm.json")
+    which = sys.argv[1:] or ["msm", "protocol"]
+    if "msm" in which:
+        (HERE / "msm.json").write_text(json.dumps({"generator": "tests/golden/make_golden.py", "cases": msm_cases()}))
+        print("wrote", HERE / "msm.json")
+    if "protocol" in which:
+        write_protocol()

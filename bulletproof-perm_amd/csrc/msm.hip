@@ -26,9 +26,10 @@ bool scalar_is_canonical(const uint8_t* s) {
 uint32_t msm_choose_c(double n_per_msm) {
   uint32_t best = 4;
   double bestc = 1e300;
-  // c <= 15: keeps |digit| - 1 in 14 bits (16-bit digit codes) and a
-  // window's bucket histogram (2^(c-1) x 4 B) within 64 KB of LDS.
-  for (uint32_t c = 2; c <= 15; ++c) {
+  // c <= 16: a window's bucket histogram (2^(c-1) x 4 B) fits in LDS
+  // (128 KB at c = 16, which also gives W = 16 windows: an even split over
+  // 1, 2, 4 and 8 GPUs).
+  for (uint32_t c = 2; c <= 16; ++c) {
     const uint32_t W = (254 + c - 1) / c;
     const double cost = (double)W * (7.0 * n_per_msm + 9.0 * (double)(1u << c)) + 8.0 * c * (W - 1);
     if (cost < bestc) {
@@ -63,13 +64,13 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
   BPP_TRY(ctx_ws(ctx, "msm_wsum", nseg * 128, &wsum));
   BPP_HIP(hipMemsetAsync(cnt, 0, (NB + 1) * 4, ctx->stream));
   BPP_HIP(hipMemsetAsync(cur, 0, NB * 4, ctx->stream));
-  const bool lds_sort = (M == 1) && (c <= 15) && (T >= 16384);
+  const bool lds_sort = (M == 1) && (c <= 16) && (T >= 16384);
   if (lds_sort && T) {
     void* dig = nullptr;
-    BPP_TRY(ctx_ws(ctx, "msm_dig", (size_t)T * Wn * 2 + 16, &dig));
+    BPP_TRY(ctx_ws(ctx, "msm_dig", (size_t)T * Wn * 4 + 16, &dig));
     {
       ProfScope ps(ctx, "msm_digits");
-      hipLaunchKernelGGL(k_msm_digits, dim3(grid_for(T, 256)), dim3(256), 0, ctx->stream, d_scal, g, (uint16_t*)dig);
+      hipLaunchKernelGGL(k_msm_digits, dim3(grid_for(T, 256)), dim3(256), 0, ctx->stream, d_scal, g, (uint32_t*)dig);
     }
     BPP_TRY(ctx_check_launch(ctx, "k_msm_digits"));
     // ~2 blocks per CU in total
@@ -77,9 +78,15 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
     nchunk = std::min<uint32_t>(nchunk, std::max<uint32_t>(1, T / 4096));
     const uint32_t chunk = (T + nchunk - 1) / nchunk;
     const size_t lds = (size_t)g.B * 4;
+    static bool lds_attr = false;
+    if (!lds_attr) {  // > 64 KB dynamic LDS (128 KB at c = 16; 160 KB per CU on gfx950)
+      BPP_HIP(hipFuncSetAttribute((const void*)k_msm_count_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 131072));
+      BPP_HIP(hipFuncSetAttribute((const void*)k_msm_scatter_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 131072));
+      lds_attr = true;
+    }
     {
       ProfScope ps(ctx, "msm_count");
-      hipLaunchKernelGGL(k_msm_count_lds, dim3(Wn * nchunk), dim3(SORT_T), lds, ctx->stream, (const uint16_t*)dig, g,
+      hipLaunchKernelGGL(k_msm_count_lds, dim3(Wn * nchunk), dim3(SORT_T), lds, ctx->stream, (const uint32_t*)dig, g,
                          chunk, nchunk, (uint32_t*)cnt);
     }
     BPP_TRY(ctx_check_launch(ctx, "k_msm_count_lds"));
@@ -89,7 +96,7 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
     }
     {
       ProfScope ps(ctx, "msm_scatter");
-      hipLaunchKernelGGL(k_msm_scatter_lds, dim3(Wn * nchunk), dim3(SORT_T), lds, ctx->stream, (const uint16_t*)dig,
+      hipLaunchKernelGGL(k_msm_scatter_lds, dim3(Wn * nchunk), dim3(SORT_T), lds, ctx->stream, (const uint32_t*)dig,
                          d_pidx, g, chunk, nchunk, (const uint32_t*)boff, (uint32_t*)cur, (uint32_t*)entries);
     }
     BPP_TRY(ctx_check_launch(ctx, "k_msm_scatter_lds"));

@@ -262,40 +262,41 @@ __global__ void __launch_bounds__(64) k_msm_horner(const uint32_t* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
-// Single large MSM sort path (M == 1, c <= 15): digits are recoded once into
-// a window-major uint16 array (code = sign << 15 | (|d| - 1), 0xFFFF = zero
+// Single large MSM sort path (M == 1, c <= 16): digits are recoded once into
+// a window-major uint32 array (code = sign << 31 | (|d| - 1), ~0 = zero
 // digit), then one workgroup per (window, chunk of terms) builds the bucket
 // histogram in LDS.  Global memory then sees one coalesced atomic per
 // (block, bucket) instead of one scattered memory-side atomic per
 // (term, window) — the global-atomic kernels above ran at ~26 G atomics/s.
-#define DIG_ZERO 0xFFFFu
+#define DIG_ZERO 0xFFFFFFFFu
+#define DIG_SIGN 0x80000000u
 #define SORT_T 1024
 
 __global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __restrict__ scalars, MsmGeom g,
-                                                   uint16_t* __restrict__ dig) {
+                                                   uint32_t* __restrict__ dig) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= g.T) return;
   uint32_t s[8];
   load_scalar(scalars, t, s);
-  for (uint32_t w = 0; w < g.Wn; ++w) dig[(size_t)w * g.T + t] = (uint16_t)DIG_ZERO;
+  for (uint32_t w = 0; w < g.Wn; ++w) dig[(size_t)w * g.T + t] = DIG_ZERO;
   for_each_digit(s, g, [&](uint32_t w, int d) {
     const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u;
-    dig[(size_t)w * g.T + t] = (uint16_t)(b | (d < 0 ? 0x8000u : 0u));
+    dig[(size_t)w * g.T + t] = b | (d < 0 ? DIG_SIGN : 0u);
   });
 }
 
 // grid = Wn * nchunk blocks; dynamic LDS = B * 4 bytes
-__global__ void __launch_bounds__(SORT_T) k_msm_count_lds(const uint16_t* __restrict__ dig, MsmGeom g, uint32_t chunk,
+__global__ void __launch_bounds__(SORT_T) k_msm_count_lds(const uint32_t* __restrict__ dig, MsmGeom g, uint32_t chunk,
                                                          uint32_t nchunk, uint32_t* __restrict__ cnt) {
   extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
   const uint32_t w = blockIdx.x / nchunk, ch = blockIdx.x % nchunk;
   for (uint32_t b = threadIdx.x; b < g.B; b += SORT_T) hist[b] = 0;
   __syncthreads();
   const uint32_t t0 = ch * chunk, t1 = min(t0 + chunk, g.T);
-  const uint16_t* dw = dig + (size_t)w * g.T;
+  const uint32_t* dw = dig + (size_t)w * g.T;
   for (uint32_t t = t0 + threadIdx.x; t < t1; t += SORT_T) {
     const uint32_t code = dw[t];
-    if (code != DIG_ZERO) atomicAdd(&hist[code & 0x7FFFu], 1u);
+    if (code != DIG_ZERO) atomicAdd(&hist[code & ~DIG_SIGN], 1u);
   }
   __syncthreads();
   uint32_t* cw = cnt + ((size_t)w << (g.c - 1));
@@ -305,7 +306,7 @@ __global__ void __launch_bounds__(SORT_T) k_msm_count_lds(const uint16_t* __rest
   }
 }
 
-__global__ void __launch_bounds__(SORT_T) k_msm_scatter_lds(const uint16_t* __restrict__ dig,
+__global__ void __launch_bounds__(SORT_T) k_msm_scatter_lds(const uint32_t* __restrict__ dig,
                                                            const uint32_t* __restrict__ pidx, MsmGeom g,
                                                            uint32_t chunk, uint32_t nchunk,
                                                            const uint32_t* __restrict__ boff,
@@ -316,10 +317,10 @@ __global__ void __launch_bounds__(SORT_T) k_msm_scatter_lds(const uint16_t* __re
   for (uint32_t b = threadIdx.x; b < g.B; b += SORT_T) hist[b] = 0;
   __syncthreads();
   const uint32_t t0 = ch * chunk, t1 = min(t0 + chunk, g.T);
-  const uint16_t* dw = dig + (size_t)w * g.T;
+  const uint32_t* dw = dig + (size_t)w * g.T;
   for (uint32_t t = t0 + threadIdx.x; t < t1; t += SORT_T) {
     const uint32_t code = dw[t];
-    if (code != DIG_ZERO) atomicAdd(&hist[code & 0x7FFFu], 1u);
+    if (code != DIG_ZERO) atomicAdd(&hist[code & ~DIG_SIGN], 1u);
   }
   __syncthreads();
   // reserve this block's slice of every bucket: hist[b] becomes a cursor
@@ -332,7 +333,7 @@ __global__ void __launch_bounds__(SORT_T) k_msm_scatter_lds(const uint16_t* __re
   for (uint32_t t = t0 + threadIdx.x; t < t1; t += SORT_T) {
     const uint32_t code = dw[t];
     if (code == DIG_ZERO) continue;
-    const uint32_t pos = atomicAdd(&hist[code & 0x7FFFu], 1u);
-    entries[pos] = (pidx ? pidx[t] : t) | (code & 0x8000u ? 0x80000000u : 0u);
+    const uint32_t pos = atomicAdd(&hist[code & ~DIG_SIGN], 1u);
+    entries[pos] = (pidx ? pidx[t] : t) | (code & DIG_SIGN);
   }
 }

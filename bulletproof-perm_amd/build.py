@@ -43,14 +43,14 @@ def _compile(src: Path, flags) -> Path:
 def build(debug: bool = False, jobs: int | None = None) -> Path:
     BUILD.mkdir(exist_ok=True)
     flags = ["-O1", "-g"] if debug else ["-O3"]
-    flags += ["-Wno-unused-result", "-Wno-pass-failed"]
+    flags += ["-Wno-unused-result", "-Wno-pass-failed", "-pthread"]
     srcs = sources()
     jobs = jobs or min(8, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(lambda s: _compile(s, flags), srcs))
     if OUT.exists() and OUT.stat().st_mtime >= max(o.stat().st_mtime for o in objs):
         return OUT
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(OUT), *map(str, objs)]
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", str(OUT), *map(str, objs)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

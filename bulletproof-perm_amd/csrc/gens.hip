@@ -121,6 +121,27 @@ int pedersen_dev(bpp_ctx* ctx, const bpp_gens* g, const uint32_t* d_v, const uin
   return ctx_check_launch(ctx, "k_pedersen");
 }
 
+int gens_points(bpp_ctx* ctx, const bpp_gens* g, MsmPoints* out) {
+  const uint32_t np = (uint32_t)(2 * g->n + 2);
+  if (!g->d_wt) {
+    uint32_t* d = nullptr;
+    if (hipMalloc(&d, (size_t)np * FBW_W * MSM_NIELS_WORDS * 4) != hipSuccess) {
+      ctx->err = "hipMalloc generator window tables";
+      return BPP_ERR_NOMEM;
+    }
+    const int rc = fbw_build(ctx, g->d_tbl, np, d);
+    if (rc) {
+      hipFree(d);
+      return rc;
+    }
+    g->d_wt = d;
+  }
+  *out = MsmPoints();
+  out->tbl = g->d_tbl;
+  out->wt = g->d_wt;
+  return BPP_OK;
+}
+
 void gens_chain_bytes(const char* label, uint32_t party, size_t n, uint8_t* out64) {
   merlin::Shake256 sh;
   sh.update((const uint8_t*)"GeneratorsChain", 15);
@@ -230,6 +251,7 @@ void bpp_gens_destroy(bpp_gens* g) {
   hipSetDevice(g->ctx->device);
   if (g->d_tbl) hipFree(g->d_tbl);
   if (g->d_fb) hipFree(g->d_fb);
+  if (g->d_wt) hipFree(g->d_wt);
   delete g;
 }
 

@@ -6,11 +6,10 @@
 #include "ctx.h"
 #include "host/merlin.h"
 #include "host/scalar.h"
+#include "msm_engine.h"
 
 struct IpaGens {
-  const uint32_t* d_tbl = nullptr;   // points with index < n0
-  const uint32_t* d_tbl1 = nullptr;  // points with index >= n0 (at idx - n0)
-  uint32_t n0 = 0xffffffffu;
+  MsmPoints pts;                      // generators (+ window tables), extra points from n0
   uint32_t gbase = 0, hbase = 0;     // G_i at gbase + i, H_i at hbase + i
   uint32_t qidx = 0;                 // Q = qmul * P[qidx]
   hsc::Sc qmul = hsc::one();
@@ -27,6 +26,12 @@ struct IpaProofHost {
 // all ones).  a and b are consumed.
 int ipa_prove_dev(bpp_ctx* ctx, merlin::Transcript& tr, const IpaGens& g, uint32_t n, const uint32_t* d_Gf,
                   const uint32_t* d_Hf, const uint32_t* d_a, const uint32_t* d_b, IpaProofHost& out);
+
+// P instances in lockstep (one per transcript): d_a, d_b, d_Gf, d_Hf are
+// [P][n] (Gf/Hf may be null); Q_p = qmul[p] * P[g.qidx].
+int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& trs, const IpaGens& g, uint32_t n,
+                        const uint32_t* d_Gf, const uint32_t* d_Hf, const uint32_t* d_a, const uint32_t* d_b,
+                        const std::vector<hsc::Sc>& qmul, std::vector<IpaProofHost>& out);
 
 // Replays the verifier side of the transcript; returns false on malformed
 // proof (identity L/R, wrong length).  Fills u^2, u^-2 and s (bulletproofs

@@ -20,15 +20,21 @@
 #include "ctx.h"
 #include "ipa.h"
 #include "msm_engine.h"
+#include "host/par.h"
 #include "sc25519.cuh"
 
 static unsigned grid_for(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
-__global__ void __launch_bounds__(256) k_ipa_init(uint32_t n, const uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
-                           const uint32_t* __restrict__ gf, const uint32_t* __restrict__ hf, uint32_t* __restrict__ am,
-                           uint32_t* __restrict__ bm, uint32_t* __restrict__ fG, uint32_t* __restrict__ fH) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n) return;
+// All kernels run P independent instances of the same length n in lockstep
+// (a batch of proofs); per-instance arrays are [P][n] scalars, the MSM term
+// arrays [P][2n+2] (L terms then R terms of each instance).
+__global__ void __launch_bounds__(256) k_ipa_init(uint32_t n, uint32_t P, const uint32_t* __restrict__ a,
+                                                 const uint32_t* __restrict__ b, const uint32_t* __restrict__ gf,
+                                                 const uint32_t* __restrict__ hf, uint32_t* __restrict__ am,
+                                                 uint32_t* __restrict__ bm, uint32_t* __restrict__ fG,
+                                                 uint32_t* __restrict__ fH) {
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= (size_t)n * P) return;
   sc_store(am + 8 * k, sc_to_mont(sc_load(a + 8 * k)));
   sc_store(bm + 8 * k, sc_to_mont(sc_load(b + 8 * k)));
   sc one = sc_zero();
@@ -37,37 +43,45 @@ __global__ void __launch_bounds__(256) k_ipa_init(uint32_t n, const uint32_t* __
   sc_store(fH + 8 * k, hf ? sc_load(hf + 8 * k) : one);
 }
 
-// terms of L at [0, n+1), of R at [n+1, 2n+2); slots n and 2n+1 (Q) are
-// written by k_ipa_cross_final.
-__global__ void __launch_bounds__(256) k_ipa_terms(uint32_t n, uint32_t m, uint32_t lg_h, const uint32_t* __restrict__ am,
-                            const uint32_t* __restrict__ bm, const uint32_t* __restrict__ fG,
-                            const uint32_t* __restrict__ fH, uint32_t gbase, uint32_t hbase,
-                            uint32_t* __restrict__ scal, uint32_t* __restrict__ pidx) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n) return;
+// terms of L at [0, n+1), of R at [n+1, 2n+2) of each instance; slots n and
+// 2n+1 (Q) are written by k_ipa_cross_final.
+__global__ void __launch_bounds__(256) k_ipa_terms(uint32_t n, uint32_t lg_n, uint32_t P, uint32_t m, uint32_t lg_h,
+                                                  const uint32_t* __restrict__ am, const uint32_t* __restrict__ bm,
+                                                  const uint32_t* __restrict__ fG, const uint32_t* __restrict__ fH,
+                                                  uint32_t gbase, uint32_t hbase, uint32_t* __restrict__ scal,
+                                                  uint32_t* __restrict__ pidx) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (size_t)n * P) return;
+  const size_t inst = t >> lg_n;
+  const uint32_t k = (uint32_t)(t & (n - 1));
   const uint32_t h = m >> 1;
   const uint32_t r = k & (m - 1);
   const bool hi = (r & h) != 0;
   const uint32_t p = r ^ h;
   const uint32_t cidx = ((k >> (lg_h + 1)) << lg_h) | (k & (h - 1));
-  const sc sG = sc_mont(sc_load(am + 8 * p), sc_load(fG + 8 * k));  // canonical a_p * fG_k
-  const sc sH = sc_mont(sc_load(bm + 8 * p), sc_load(fH + 8 * k));
-  const uint32_t posG = hi ? cidx : (n + 1) + cidx;
-  const uint32_t posH = hi ? (n + 1) + (n >> 1) + cidx : (n >> 1) + cidx;
+  const size_t ib = inst << lg_n;  // instance base in [P][n]
+  const sc sG = sc_mont(sc_load(am + 8 * (ib + p)), sc_load(fG + 8 * t));  // canonical a_p * fG_k
+  const sc sH = sc_mont(sc_load(bm + 8 * (ib + p)), sc_load(fH + 8 * t));
+  const size_t tb = inst * (2 * (size_t)n + 2);
+  const size_t posG = tb + (hi ? cidx : (n + 1) + cidx);
+  const size_t posH = tb + (hi ? (n + 1) + (n >> 1) + cidx : (n >> 1) + cidx);
   sc_store(scal + 8 * posG, sG);
   sc_store(scal + 8 * posH, sH);
   pidx[posG] = gbase + k;
   pidx[posH] = hbase + k;
 }
 
+// grid (nb, P): block x of instance y sums its stride of
+// <a_lo, b_hi> and <a_hi, b_lo> -> part[y][x] (16 words).
 #define CROSS_T 256
-__global__ void __launch_bounds__(CROSS_T) k_ipa_cross(uint32_t h, const uint32_t* __restrict__ am,
+__global__ void __launch_bounds__(CROSS_T) k_ipa_cross(uint32_t n, uint32_t h, const uint32_t* __restrict__ am,
                                                       const uint32_t* __restrict__ bm, uint32_t* __restrict__ part) {
   __shared__ uint32_t lds[2][CROSS_T / 64][8];
+  const size_t ib = (size_t)blockIdx.y * n;
   sc cl = sc_zero(), cr = sc_zero();
   for (uint32_t i = blockIdx.x * CROSS_T + threadIdx.x; i < h; i += gridDim.x * CROSS_T) {
-    const sc a0 = sc_load(am + 8 * i), a1 = sc_load(am + 8 * (i + h));
-    const sc b0 = sc_load(bm + 8 * i), b1 = sc_load(bm + 8 * (i + h));
+    const sc a0 = sc_load(am + 8 * (ib + i)), a1 = sc_load(am + 8 * (ib + i + h));
+    const sc b0 = sc_load(bm + 8 * (ib + i)), b1 = sc_load(bm + 8 * (ib + i + h));
     cl = sc_add(cl, sc_mont(a0, b1));
     cr = sc_add(cr, sc_mont(a1, b0));
   }
@@ -90,40 +104,53 @@ __global__ void __launch_bounds__(CROSS_T) k_ipa_cross(uint32_t h, const uint32_
       _Pragma("unroll") for (int i = 0; i < 8; ++i) t.v[i] = lds[1][w][i];
       sr = sc_add(sr, t);
     }
-    sc_store(part + 16 * blockIdx.x, sl);
-    sc_store(part + 16 * blockIdx.x + 8, sr);
+    const size_t o = 16 * ((size_t)blockIdx.y * gridDim.x + blockIdx.x);
+    sc_store(part + o, sl);
+    sc_store(part + o + 8, sr);
   }
 }
 
-__global__ void __launch_bounds__(64) k_ipa_cross_final(uint32_t nblk, const uint32_t* __restrict__ part, sc qmul, uint32_t qidx, uint32_t n,
-                                  uint32_t* __restrict__ scal, uint32_t* __restrict__ pidx) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// one lane per instance: c_L * qmul, c_R * qmul into the Q slots
+__global__ void __launch_bounds__(64) k_ipa_cross_final(uint32_t nblk, uint32_t P, const uint32_t* __restrict__ part,
+                                                       const uint32_t* __restrict__ qmul, uint32_t qidx, uint32_t n,
+                                                       uint32_t* __restrict__ scal, uint32_t* __restrict__ pidx) {
+  const uint32_t inst = blockIdx.x * blockDim.x + threadIdx.x;
+  if (inst >= P) return;
   sc sl = sc_zero(), sr = sc_zero();
   for (uint32_t b = 0; b < nblk; ++b) {
-    sl = sc_add(sl, sc_load(part + 16 * b));
-    sr = sc_add(sr, sc_load(part + 16 * b + 8));
+    sl = sc_add(sl, sc_load(part + 16 * ((size_t)inst * nblk + b)));
+    sr = sc_add(sr, sc_load(part + 16 * ((size_t)inst * nblk + b) + 8));
   }
   // Montgomery c * canonical qmul -> canonical c*qmul
-  sc_store(scal + 8 * n, sc_mont(sl, qmul));
-  sc_store(scal + 8 * (2 * n + 1), sc_mont(sr, qmul));
-  pidx[n] = qidx;
-  pidx[2 * n + 1] = qidx;
+  const sc q = sc_load(qmul + 8 * inst);
+  const size_t tb = (size_t)inst * (2 * (size_t)n + 2);
+  sc_store(scal + 8 * (tb + n), sc_mont(sl, q));
+  sc_store(scal + 8 * (tb + 2 * n + 1), sc_mont(sr, q));
+  pidx[tb + n] = qidx;
+  pidx[tb + 2 * n + 1] = qidx;
 }
 
-__global__ void __launch_bounds__(256) k_ipa_fold(uint32_t n, uint32_t m, uint32_t* __restrict__ am, uint32_t* __restrict__ bm,
-                           uint32_t* __restrict__ fG, uint32_t* __restrict__ fH, sc um, sc uim) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n) return;
+// u: [P][16] = (u * R, u^-1 * R) per instance (Montgomery form)
+__global__ void __launch_bounds__(256) k_ipa_fold(uint32_t n, uint32_t lg_n, uint32_t P, uint32_t m,
+                                                 uint32_t* __restrict__ am, uint32_t* __restrict__ bm,
+                                                 uint32_t* __restrict__ fG, uint32_t* __restrict__ fH,
+                                                 const uint32_t* __restrict__ u) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (size_t)n * P) return;
+  const size_t inst = t >> lg_n;
+  const uint32_t k = (uint32_t)(t & (n - 1));
+  const sc um = sc_load(u + 16 * inst), uim = sc_load(u + 16 * inst + 8);
   const uint32_t h = m >> 1;
   const bool hi = ((k & (m - 1)) & h) != 0;
   // G' = u^-1 G_lo + u G_hi ; H' = u H_lo + u^-1 H_hi
-  sc_store(fG + 8 * k, sc_mont(sc_load(fG + 8 * k), hi ? um : uim));
-  sc_store(fH + 8 * k, sc_mont(sc_load(fH + 8 * k), hi ? uim : um));
+  sc_store(fG + 8 * t, sc_mont(sc_load(fG + 8 * t), hi ? um : uim));
+  sc_store(fH + 8 * t, sc_mont(sc_load(fH + 8 * t), hi ? uim : um));
   if (k < h) {
-    const sc a0 = sc_load(am + 8 * k), a1 = sc_load(am + 8 * (k + h));
-    const sc b0 = sc_load(bm + 8 * k), b1 = sc_load(bm + 8 * (k + h));
-    sc_store(am + 8 * k, sc_add(sc_mont(a0, um), sc_mont(a1, uim)));
-    sc_store(bm + 8 * k, sc_add(sc_mont(b0, uim), sc_mont(b1, um)));
+    const size_t ib = inst << lg_n;
+    const sc a0 = sc_load(am + 8 * (ib + k)), a1 = sc_load(am + 8 * (ib + k + h));
+    const sc b0 = sc_load(bm + 8 * (ib + k)), b1 = sc_load(bm + 8 * (ib + k + h));
+    sc_store(am + 8 * (ib + k), sc_add(sc_mont(a0, um), sc_mont(a1, uim)));
+    sc_store(bm + 8 * (ib + k), sc_add(sc_mont(b0, uim), sc_mont(b1, um)));
   }
 }
 
@@ -142,74 +169,119 @@ static hsc::Sc from_dev_words(const uint32_t w[8]) {
   return r;
 }
 
-int ipa_prove_dev(bpp_ctx* ctx, merlin::Transcript& tr, const IpaGens& g, uint32_t n, const uint32_t* d_Gf,
-                  const uint32_t* d_Hf, const uint32_t* d_a, const uint32_t* d_b, IpaProofHost& out) {
+int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& trs, const IpaGens& g, uint32_t n,
+                        const uint32_t* d_Gf, const uint32_t* d_Hf, const uint32_t* d_a, const uint32_t* d_b,
+                        const std::vector<hsc::Sc>& qmul, std::vector<IpaProofHost>& out) {
+  const uint32_t P = (uint32_t)trs.size();
   if (n == 0 || (n & (n - 1))) {
     ctx->err = "ipa: n must be a power of two";
     return BPP_ERR_LEN;
   }
-  tr.innerproduct_domain_sep(n);
-  out.L.clear();
-  out.R.clear();
-  void *am, *bm, *fG, *fH, *scal, *pidx, *part;
-  BPP_TRY(ctx_ws(ctx, "ipa_am", (size_t)n * 32, &am));
-  BPP_TRY(ctx_ws(ctx, "ipa_bm", (size_t)n * 32, &bm));
-  BPP_TRY(ctx_ws(ctx, "ipa_fG", (size_t)n * 32, &fG));
-  BPP_TRY(ctx_ws(ctx, "ipa_fH", (size_t)n * 32, &fH));
-  BPP_TRY(ctx_ws(ctx, "ipa_scal", (size_t)(2 * n + 2) * 32, &scal));
-  BPP_TRY(ctx_ws(ctx, "ipa_pidx", (size_t)(2 * n + 2) * 4, &pidx));
-  const uint32_t cross_blocks = std::min<uint32_t>(64, grid_for(std::max<uint32_t>(n / 2, 1), CROSS_T));
-  BPP_TRY(ctx_ws(ctx, "ipa_part", (size_t)cross_blocks * 64, &part));
-  hipLaunchKernelGGL(k_ipa_init, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, n, d_a, d_b, d_Gf, d_Hf,
-                     (uint32_t*)am, (uint32_t*)bm, (uint32_t*)fG, (uint32_t*)fH);
-  BPP_TRY(ctx_check_launch(ctx, "k_ipa_init"));
-  const sc qmul = to_dev_sc(g.qmul);
+  if (qmul.size() != P) return BPP_ERR_ARG;
+  out.assign(P, IpaProofHost());
+  if (!P) return BPP_OK;
+  uint32_t lg_n = 0;
+  while ((1u << lg_n) < n) ++lg_n;
+  par::for_each(P, [&](size_t p) { trs[p]->innerproduct_domain_sep(n); });
+  const size_t PN = (size_t)P * n, PT = (size_t)P * (2 * n + 2);
+  void *am, *bm, *fG, *fH, *scal, *pidx, *part, *d_q, *d_u;
+  BPP_TRY(ctx_ws(ctx, "ipa_am", PN * 32, &am));
+  BPP_TRY(ctx_ws(ctx, "ipa_bm", PN * 32, &bm));
+  BPP_TRY(ctx_ws(ctx, "ipa_fG", PN * 32, &fG));
+  BPP_TRY(ctx_ws(ctx, "ipa_fH", PN * 32, &fH));
+  BPP_TRY(ctx_ws(ctx, "ipa_scal", PT * 32, &scal));
+  BPP_TRY(ctx_ws(ctx, "ipa_pidx", PT * 4, &pidx));
+  BPP_TRY(ctx_ws(ctx, "ipa_qmul", (size_t)P * 32, &d_q));
+  BPP_TRY(ctx_ws(ctx, "ipa_u", (size_t)P * 64, &d_u));
+  // cross blocks per instance: enough lanes overall, at most 64
+  const uint32_t cross_blocks =
+      std::max<uint32_t>(1, std::min<uint32_t>({64u, grid_for(std::max<uint32_t>(n / 2, 1), CROSS_T),
+                                                 std::max<uint32_t>(1, 512 / P)}));
+  BPP_TRY(ctx_ws(ctx, "ipa_part", (size_t)P * cross_blocks * 64, &part));
+  {
+    std::vector<uint32_t> qw((size_t)P * 8);
+    for (uint32_t p = 0; p < P; ++p) {
+      const sc q = to_dev_sc(qmul[p]);
+      memcpy(&qw[8 * (size_t)p], q.v, 32);
+    }
+    BPP_HIP(hipMemcpyAsync(d_q, qw.data(), qw.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_ipa_init, dim3(grid_for(PN, 256)), dim3(256), 0, ctx->stream, n, P, d_a, d_b, d_Gf, d_Hf,
+                       (uint32_t*)am, (uint32_t*)bm, (uint32_t*)fG, (uint32_t*)fH);
+    BPP_TRY(ctx_check_launch(ctx, "k_ipa_init"));
+    BPP_HIP(hipStreamSynchronize(ctx->stream));  // qw goes out of scope
+  }
+  std::vector<uint32_t> off(2 * (size_t)P + 1);
+  for (uint32_t p = 0; p < P; ++p) {
+    off[2 * p] = (uint32_t)(p * (2 * (size_t)n + 2));
+    off[2 * p + 1] = off[2 * p] + n + 1;
+  }
+  off[2 * P] = (uint32_t)PT;
+  std::vector<uint8_t> enc((size_t)2 * P * 32);
+  std::vector<hsc::Sc> u(P), ui(P);
+  std::vector<uint32_t> uw((size_t)P * 16);
   uint32_t m = n;
-  uint32_t lg_h = 0;
-  while ((1u << (lg_h + 1)) < n) ++lg_h;  // log2(n/2)
-  std::vector<h25519::ge> res;
+  uint32_t lg_h = lg_n ? lg_n - 1 : 0;  // log2(n/2)
   while (m > 1) {
     const uint32_t h = m >> 1;
     {
       ProfScope ps(ctx, "ipa_terms");
-      hipLaunchKernelGGL(k_ipa_terms, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, n, m, lg_h,
+      hipLaunchKernelGGL(k_ipa_terms, dim3(grid_for(PN, 256)), dim3(256), 0, ctx->stream, n, lg_n, P, m, lg_h,
                          (const uint32_t*)am, (const uint32_t*)bm, (const uint32_t*)fG, (const uint32_t*)fH, g.gbase,
                          g.hbase, (uint32_t*)scal, (uint32_t*)pidx);
       const uint32_t nb = std::min<uint32_t>(cross_blocks, grid_for(h, CROSS_T));
-      hipLaunchKernelGGL(k_ipa_cross, dim3(nb), dim3(CROSS_T), 0, ctx->stream, h, (const uint32_t*)am,
+      hipLaunchKernelGGL(k_ipa_cross, dim3(nb, P), dim3(CROSS_T), 0, ctx->stream, n, h, (const uint32_t*)am,
                          (const uint32_t*)bm, (uint32_t*)part);
-      hipLaunchKernelGGL(k_ipa_cross_final, dim3(1), dim3(64), 0, ctx->stream, nb, (const uint32_t*)part, qmul, g.qidx,
-                         n, (uint32_t*)scal, (uint32_t*)pidx);
+      hipLaunchKernelGGL(k_ipa_cross_final, dim3(grid_for(P, 64)), dim3(64), 0, ctx->stream, nb, P,
+                         (const uint32_t*)part, (const uint32_t*)d_q, g.qidx, n, (uint32_t*)scal, (uint32_t*)pidx);
     }
     BPP_TRY(ctx_check_launch(ctx, "ipa round kernels"));
-    const std::vector<uint32_t> off = {0, n + 1, 2 * n + 2};
-    BPP_TRY(msm_multi(ctx, (const uint32_t*)scal, (const uint32_t*)pidx, off, g.d_tbl, g.d_tbl1, g.n0, res));
-    Enc32 Le, Re;
-    h25519::encode(Le.data(), res[0]);
-    h25519::encode(Re.data(), res[1]);
-    out.L.push_back(Le);
-    out.R.push_back(Re);
-    tr.append_point("L", Le.data());
-    tr.append_point("R", Re.data());
-    const hsc::Sc u = tr.challenge_scalar("u");
-    const hsc::Sc ui = hsc::invert(u);
-    const sc um = to_dev_sc(hsc::mul(u, SC_R_MOD_L));
-    const sc uim = to_dev_sc(hsc::mul(ui, SC_R_MOD_L));
+    BPP_TRY(msm_multi_enc(ctx, (const uint32_t*)scal, (const uint32_t*)pidx, off, g.pts, enc.data()));
+    par::for_each(P, [&](size_t p) {
+      Enc32 Le, Re;
+      memcpy(Le.data(), enc.data() + 64 * p, 32);
+      memcpy(Re.data(), enc.data() + 64 * p + 32, 32);
+      out[p].L.push_back(Le);
+      out[p].R.push_back(Re);
+      trs[p]->append_point("L", Le.data());
+      trs[p]->append_point("R", Re.data());
+      u[p] = trs[p]->challenge_scalar("u");
+    });
+    ui = u;
+    hsc::batch_invert(ui);
+    for (uint32_t p = 0; p < P; ++p) {
+      const sc um = to_dev_sc(hsc::mul(u[p], SC_R_MOD_L));
+      const sc uim = to_dev_sc(hsc::mul(ui[p], SC_R_MOD_L));
+      memcpy(&uw[16 * (size_t)p], um.v, 32);
+      memcpy(&uw[16 * (size_t)p + 8], uim.v, 32);
+    }
+    BPP_HIP(hipMemcpyAsync(d_u, uw.data(), uw.size() * 4, hipMemcpyHostToDevice, ctx->stream));
     {
       ProfScope ps(ctx, "ipa_fold");
-      hipLaunchKernelGGL(k_ipa_fold, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, n, m, (uint32_t*)am,
-                         (uint32_t*)bm, (uint32_t*)fG, (uint32_t*)fH, um, uim);
+      hipLaunchKernelGGL(k_ipa_fold, dim3(grid_for(PN, 256)), dim3(256), 0, ctx->stream, n, lg_n, P, m, (uint32_t*)am,
+                         (uint32_t*)bm, (uint32_t*)fG, (uint32_t*)fH, (const uint32_t*)d_u);
     }
     BPP_TRY(ctx_check_launch(ctx, "k_ipa_fold"));
+    BPP_HIP(hipStreamSynchronize(ctx->stream));  // uw reused next round
     m = h;
     if (lg_h) --lg_h;
   }
-  uint32_t ab[16];
-  BPP_HIP(hipMemcpyAsync(ab, am, 32, hipMemcpyDeviceToHost, ctx->stream));
-  BPP_HIP(hipMemcpyAsync(ab + 8, bm, 32, hipMemcpyDeviceToHost, ctx->stream));
+  // a, b = element 0 of each instance
+  std::vector<uint32_t> ab((size_t)P * 16);
+  BPP_HIP(hipMemcpy2DAsync(ab.data(), 64, am, (size_t)n * 32, 32, P, hipMemcpyDeviceToHost, ctx->stream));
+  BPP_HIP(hipMemcpy2DAsync(ab.data() + 8, 64, bm, (size_t)n * 32, 32, P, hipMemcpyDeviceToHost, ctx->stream));
   BPP_HIP(hipStreamSynchronize(ctx->stream));
-  out.a = hsc::mont(from_dev_words(ab), hsc::one());
-  out.b = hsc::mont(from_dev_words(ab + 8), hsc::one());
+  for (uint32_t p = 0; p < P; ++p) {
+    out[p].a = hsc::mont(from_dev_words(&ab[16 * (size_t)p]), hsc::one());
+    out[p].b = hsc::mont(from_dev_words(&ab[16 * (size_t)p + 8]), hsc::one());
+  }
+  return BPP_OK;
+}
+
+int ipa_prove_dev(bpp_ctx* ctx, merlin::Transcript& tr, const IpaGens& g, uint32_t n, const uint32_t* d_Gf,
+                  const uint32_t* d_Hf, const uint32_t* d_a, const uint32_t* d_b, IpaProofHost& out) {
+  std::vector<IpaProofHost> o;
+  BPP_TRY(ipa_prove_batch_dev(ctx, {&tr}, g, n, d_Gf, d_Hf, d_a, d_b, {g.qmul}, o));
+  out = std::move(o[0]);
   return BPP_OK;
 }
 

@@ -106,7 +106,9 @@ int bpp_vec_commit(bpp_ctx* ctx, const bpp_gens* g, const uint8_t blind[32], con
   BPP_TRY(ctx_ws(ctx, "vc_i", T * 4, &d_i));
   BPP_HIP(hipMemcpyAsync(d_i, idx.data(), T * 4, hipMemcpyHostToDevice, ctx->stream));
   std::vector<h25519::ge> res;
-  BPP_TRY(msm_multi(ctx, d_s, (const uint32_t*)d_i, {0, (uint32_t)T}, g->d_tbl, nullptr, 0xffffffffu, res));
+  MsmPoints pts;
+  BPP_TRY(gens_points(ctx, g, &pts));
+  BPP_TRY(msm_multi(ctx, d_s, (const uint32_t*)d_i, {0, (uint32_t)T}, pts, res));
   h25519::encode(out, res[0]);
   return BPP_OK;
 }
@@ -124,12 +126,11 @@ int bpp_ipa_prove(bpp_ctx* ctx, const bpp_gens* g, bpp_transcript* tr, const uin
   BPP_TRY(upload_opt(ctx, H_factors, n, "ipa_in_hf", &d_hf));
   BPP_TRY(decompress_ws(ctx, Q, 1, "ipa_q", &d_q));
   IpaGens ig;
-  ig.d_tbl = g->d_tbl;
-  ig.d_tbl1 = d_q;
-  ig.n0 = (uint32_t)(2 * g->n + 2);
+  BPP_TRY(gens_points(ctx, g, &ig.pts));
+  BPP_TRY(msm_points_extra(ctx, &ig.pts, d_q, 1, (uint32_t)(2 * g->n + 2), "ipa_q_wt", (double)(n + 1)));
   ig.gbase = 0;
   ig.hbase = (uint32_t)g->n;
-  ig.qidx = ig.n0;
+  ig.qidx = ig.pts.n0;
   IpaProofHost pf;
   BPP_TRY(ipa_prove_dev(ctx, tr->t, ig, (uint32_t)n, d_gf, d_hf, d_a, d_b, pf));
   for (size_t j = 0; j < pf.L.size(); ++j) {
@@ -194,7 +195,10 @@ int bpp_ipa_verify(bpp_ctx* ctx, const bpp_gens* g, bpp_transcript* tr, size_t n
   BPP_TRY(ctx_ws(ctx, "ipav_i", T * 4, &d_i));
   BPP_HIP(hipMemcpyAsync(d_i, idx.data(), T * 4, hipMemcpyHostToDevice, ctx->stream));
   std::vector<h25519::ge> res;
-  BPP_TRY(msm_multi(ctx, d_s, (const uint32_t*)d_i, {0, (uint32_t)T}, g->d_tbl, d_x, n0, res));
+  MsmPoints pts;
+  BPP_TRY(gens_points(ctx, g, &pts));
+  BPP_TRY(msm_points_extra(ctx, &pts, d_x, (uint32_t)(2 + 2 * lg), n0, "ipav_x_wt", (double)T));
+  BPP_TRY(msm_multi(ctx, d_s, (const uint32_t*)d_i, {0, (uint32_t)T}, pts, res));
   uint8_t e[32];
   h25519::encode(e, res[0]);
   static const uint8_t zero[32] = {0};

@@ -2,6 +2,7 @@
 // points: bpp_msm, bpp_msm_table, bpp_msm_table_dev, bpp_msm_batch and the
 // window-partitioned variants used for multi-GPU.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "ctx.h"
@@ -44,7 +45,7 @@ static unsigned grid_for(size_t n, unsigned t) { return (unsigned)((n + t - 1) /
 
 int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const uint32_t* d_off, uint32_t M,
                uint32_t T, uint32_t c, uint32_t wb, uint32_t Wn, const uint32_t* d_tbl, uint32_t** d_wsum_out,
-               const uint32_t* d_tbl1, uint32_t n0) {
+               const uint32_t* d_tbl1, uint32_t n0, bool fb) {
   MsmGeom g;
   g.M = M;
   g.T = T;
@@ -53,7 +54,8 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
   g.wb = wb;
   g.Wn = Wn;
   g.B = 1u << (c - 1);
-  const size_t nseg = (size_t)M * Wn;
+  g.fb = fb ? 1u : 0u;
+  const size_t nseg = fb ? (size_t)M : (size_t)M * Wn;
   const size_t NB = nseg * g.B;
   void *cnt, *cur, *boff, *entries, *bsum, *wsum;
   BPP_TRY(ctx_ws(ctx, "msm_cnt", (NB + 1) * 4, &cnt));
@@ -64,7 +66,7 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
   BPP_TRY(ctx_ws(ctx, "msm_wsum", nseg * 128, &wsum));
   BPP_HIP(hipMemsetAsync(cnt, 0, (NB + 1) * 4, ctx->stream));
   BPP_HIP(hipMemsetAsync(cur, 0, NB * 4, ctx->stream));
-  const bool lds_sort = (M == 1) && (c <= 16) && (T >= 16384);
+  const bool lds_sort = !fb && (M == 1) && (c <= 16) && (T >= 16384);
   if (lds_sort && T) {
     void* dig = nullptr;
     BPP_TRY(ctx_ws(ctx, "msm_dig", (size_t)T * Wn * 4 + 16, &dig));
@@ -296,6 +298,7 @@ int bpp_msm_batch(bpp_ctx* ctx, size_t count, const uint64_t* offsets, const uin
   g.wb = 0;
   g.Wn = W;
   g.B = 1u << (c - 1);
+  g.fb = 0;
   uint32_t* d_ws = nullptr;
   BPP_TRY(msm_engine(ctx, d_s, (const uint32_t*)d_idx, (const uint32_t*)d_off, g.M, g.T, c, 0, W, tbl->d, &d_ws));
   {
@@ -308,6 +311,125 @@ int bpp_msm_batch(bpp_ctx* ctx, size_t count, const uint64_t* offsets, const uin
 }
 
 }  // extern "C"
+
+// thread t: w = t / npts, k = t % npts (a wave shares w, so every lane does
+// the same c*w doublings) -> dst[k*W + w] = 2^(c*w) * src[k].
+__global__ void __launch_bounds__(64) k_fbw_tables(const uint32_t* __restrict__ src, uint32_t npts,
+                                                   uint32_t* __restrict__ dst) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (size_t)npts * FBW_W) return;
+  const uint32_t w = (uint32_t)(t / npts), k = (uint32_t)(t % npts);
+  const ge_niels P = load_niels(src, k);
+  if (w == 0) {
+    store_niels(dst, (size_t)k * FBW_W, P);
+    return;
+  }
+  ge_p3 a = ge_from_niels(P);
+  for (uint32_t i = 0; i < FBW_C * w; ++i) a = ge_dbl(a);
+  store_niels(dst, (size_t)k * FBW_W + w, ge_to_niels(a));
+}
+
+int fbw_build(bpp_ctx* ctx, const uint32_t* d_src, uint32_t npts, uint32_t* d_dst) {
+  if (!npts) return BPP_OK;
+  {
+    ProfScope ps(ctx, "fbw_tables");
+    hipLaunchKernelGGL(k_fbw_tables, dim3(grid_for((size_t)npts * FBW_W, 64)), dim3(64), 0, ctx->stream, d_src, npts,
+                       d_dst);
+  }
+  return ctx_check_launch(ctx, "k_fbw_tables");
+}
+
+static int fb_policy();
+static bool fb_wins(double terms_per_msm);
+
+int msm_points_extra(bpp_ctx* ctx, MsmPoints* pts, const uint32_t* d_x, uint32_t nx, uint32_t n0,
+                     const char* ws_name, double terms_per_msm) {
+  pts->tbl1 = d_x;
+  pts->n0 = n0;
+  pts->wt1 = nullptr;
+  // Building a window table is a ~250-doubling chain per point plus an
+  // inversion: it pays for resident generators, not for points used once
+  // (measured: verify 1.1 ms without, 1.7 ms with), so only BPP_MSM_FB=1
+  // builds them.
+  if (!pts->wt || !nx || fb_policy() != 1 || !fb_wins(terms_per_msm)) return BPP_OK;
+  void* d = nullptr;
+  BPP_TRY(ctx_ws(ctx, ws_name, (size_t)nx * FBW_W * MSM_NIELS_WORDS * 4, &d));
+  BPP_TRY(fbw_build(ctx, d_x, nx, (uint32_t*)d));
+  pts->wt1 = (const uint32_t*)d;
+  return BPP_OK;
+}
+
+// BPP_MSM_FB: unset = cost model, 0 = never, 1 = always (tests cover both)
+static int fb_policy() {
+  const char* e = getenv("BPP_MSM_FB");
+  return e ? atoi(e) : -1;
+}
+
+// Fixed-base costs FBW_W = 32 mixed additions per term against ~W = 254/c
+// for the variable-base engine plus its per-window bucket reduction and
+// Horner combine; below ~16K terms per MSM the fixed cost dominates.
+static bool fb_wins(double terms_per_msm) {
+  const int pol = fb_policy();
+  return pol == 1 || (pol == -1 && terms_per_msm <= 16384.0);
+}
+
+static bool use_fb(const MsmPoints& pts, uint32_t M, uint32_t T) {
+  const bool have_fb = pts.wt && (!pts.tbl1 || pts.wt1);
+  return have_fb && M > 0 && fb_wins((double)T / (double)M);
+}
+
+// Fixed-base engine: device array of the M results (extended, 32 words each).
+static int msm_multi_fb_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx,
+                            const std::vector<uint32_t>& off, const MsmPoints& pts, uint32_t** d_res) {
+  const uint32_t M = (uint32_t)off.size() - 1;
+  const uint32_t T = off[M];
+  if ((uint64_t)(pts.n0 == 0xffffffffu ? 0 : pts.n0) * FBW_W >= 0x80000000ull ||
+      (uint64_t)T * FBW_W >= 0x80000000ull) {
+    ctx->err = "fixed-base MSM too large";
+    return BPP_ERR_LEN;
+  }
+  void* d_off = nullptr;
+  BPP_TRY(ctx_ws(ctx, "multi_off", (M + 1) * 4, &d_off));
+  BPP_HIP(hipMemcpyAsync(d_off, off.data(), (M + 1) * 4, hipMemcpyHostToDevice, ctx->stream));
+  const uint32_t n0w = pts.n0 == 0xffffffffu ? 0xffffffffu : pts.n0 * FBW_W;
+  return msm_engine(ctx, d_scal, d_pidx, (const uint32_t*)d_off, M, T, FBW_C, 0, FBW_W, pts.wt, d_res, pts.wt1, n0w,
+                    true);
+}
+
+int msm_multi(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const std::vector<uint32_t>& off,
+              const MsmPoints& pts, std::vector<h25519::ge>& out) {
+  const uint32_t M = (uint32_t)off.size() - 1;
+  const uint32_t T = off[M];
+  if (!use_fb(pts, M, T)) return msm_multi(ctx, d_scal, d_pidx, off, pts.tbl, pts.tbl1, pts.n0, out);
+  out.assign(M, h25519::ge_identity());
+  if (M == 0 || T == 0) return BPP_OK;
+  uint32_t* d_ws = nullptr;
+  BPP_TRY(msm_multi_fb_dev(ctx, d_scal, d_pidx, off, pts, &d_ws));
+  void* h = nullptr;
+  BPP_TRY(ctx_pinned(ctx, (size_t)M * 128, &h));
+  BPP_HIP(hipMemcpyAsync(h, d_ws, (size_t)M * 128, hipMemcpyDeviceToHost, ctx->stream));
+  BPP_HIP(hipStreamSynchronize(ctx->stream));
+  for (uint32_t m = 0; m < M; ++m) out[m] = h25519::ge_from_words((const uint32_t*)h + (size_t)m * 32);
+  return BPP_OK;
+}
+
+int msm_multi_enc(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const std::vector<uint32_t>& off,
+                  const MsmPoints& pts, uint8_t* out_enc) {
+  const uint32_t M = (uint32_t)off.size() - 1;
+  const uint32_t T = off[M];
+  if (M == 0) return BPP_OK;
+  // Few results: host encoding (~10 us each) beats a latency-bound GPU
+  // launch; many: one GPU lane per result.
+  if (M > 16 && T > 0 && use_fb(pts, M, T)) {
+    uint32_t* d_ws = nullptr;
+    BPP_TRY(msm_multi_fb_dev(ctx, d_scal, d_pidx, off, pts, &d_ws));
+    return points_compress_p3(ctx, d_ws, M, out_enc);
+  }
+  std::vector<h25519::ge> res;
+  BPP_TRY(msm_multi(ctx, d_scal, d_pidx, off, pts, res));
+  for (uint32_t m = 0; m < M; ++m) h25519::encode(out_enc + 32 * (size_t)m, res[m]);
+  return BPP_OK;
+}
 
 // M independent MSMs (host offsets, M+1 entries) over device scalars and
 // point indices; results returned as host points.  Few MSMs: window sums are
@@ -341,6 +463,7 @@ int msm_multi(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, cons
   g.wb = 0;
   g.Wn = W;
   g.B = 1u << (c - 1);
+  g.fb = 0;
   void* d_res = nullptr;
   BPP_TRY(ctx_ws(ctx, "multi_res", (size_t)M * 128, &d_res));
   {

@@ -11,11 +11,38 @@ uint32_t msm_choose_c(double n_per_msm);
 // window sums (extended points, 32 words each).
 int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const uint32_t* d_off, uint32_t M,
                uint32_t T, uint32_t c, uint32_t wb, uint32_t Wn, const uint32_t* d_tbl, uint32_t** d_wsum_out,
-               const uint32_t* d_tbl1 = nullptr, uint32_t n0 = 0xffffffffu);
+               const uint32_t* d_tbl1 = nullptr, uint32_t n0 = 0xffffffffu, bool fb = false);
 int msm_single_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const uint32_t* d_tbl, size_t n,
                    uint32_t c, uint32_t wb, uint32_t Wn, h25519::ge* out);
 int upload_scalars(bpp_ctx* ctx, const uint8_t* scalars, size_t n, const char* name, uint32_t** d_out);
 int points_compress_p3(bpp_ctx* ctx, const uint32_t* d_p3, size_t n, uint8_t* out_host);
 #include <vector>
+// Fixed-base window tables: entry k*FBW_W + w = 2^(FBW_C*w) * P_k (affine
+// Niels).  An MSM over such points needs no per-window Horner combine: all
+// windows share one bucket set.
+#define FBW_C 8
+#define FBW_W 32
+int fbw_build(bpp_ctx* ctx, const uint32_t* d_src, uint32_t npts, uint32_t* d_dst);
+// Point sources of an MSM: index < n0 -> tbl, else tbl1[idx - n0]; wt / wt1
+// are the matching window tables (null: not available).
+struct MsmPoints {
+  const uint32_t* tbl = nullptr;
+  const uint32_t* tbl1 = nullptr;
+  uint32_t n0 = 0xffffffffu;
+  const uint32_t* wt = nullptr;
+  const uint32_t* wt1 = nullptr;
+};
+// Adds nx extra points (device Niels table d_x) at indices n0.. to *pts,
+// building their window tables in workspace `ws_name` when pts has tables
+// and MSMs of `terms_per_msm` terms would take the fixed-base engine.
+int msm_points_extra(bpp_ctx* ctx, MsmPoints* pts, const uint32_t* d_x, uint32_t nx, uint32_t n0, const char* ws_name,
+                     double terms_per_msm);
+// M independent MSMs; picks the fixed-base engine when window tables exist
+// and the MSMs are small enough for it to win (BPP_MSM_FB=0/1 forces).
+int msm_multi(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const std::vector<uint32_t>& off,
+              const MsmPoints& pts, std::vector<h25519::ge>& out);
+// Same, results compressed (M x 32 B).
+int msm_multi_enc(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const std::vector<uint32_t>& off,
+                  const MsmPoints& pts, uint8_t* out_enc);
 int msm_multi(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const std::vector<uint32_t>& off,
               const uint32_t* d_tbl, const uint32_t* d_tbl1, uint32_t n0, std::vector<h25519::ge>& out);

@@ -58,6 +58,9 @@ struct MsmGeom {
   uint32_t wb;      // first window handled by this launch (multi-GPU split)
   uint32_t Wn;      // windows handled by this launch
   uint32_t B;       // buckets per window = 2^(c-1)
+  uint32_t fb;      // fixed-base mode: point idx -> idx*W + w in a table of
+                    // precomputed 2^(c*w) multiples; all windows of an MSM
+                    // share one bucket set (no Horner combine)
 };
 
 // Signed digit loop: calls f(w - wb, digit) for every window in
@@ -92,7 +95,8 @@ __global__ void k_msm_count(const uint32_t* __restrict__ scalars, const uint32_t
   const uint32_t base = m * g.Wn;
   for_each_digit(s, g, [&](uint32_t w, int d) {
     const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u;
-    atomicAdd(&cnt[((base + w) << (g.c - 1)) + b], 1u);
+    const uint32_t seg = g.fb ? m : base + w;
+    atomicAdd(&cnt[(seg << (g.c - 1)) + b], 1u);
   });
 }
 
@@ -109,9 +113,10 @@ __global__ void k_msm_scatter(const uint32_t* __restrict__ scalars, const uint32
   const uint32_t pi = pidx ? pidx[t] : t;
   for_each_digit(s, g, [&](uint32_t w, int d) {
     const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u;
-    const uint32_t gb = ((base + w) << (g.c - 1)) + b;
+    const uint32_t seg = g.fb ? m : base + w;
+    const uint32_t gb = (seg << (g.c - 1)) + b;
     const uint32_t pos = boff[gb] + atomicAdd(&cursor[gb], 1u);
-    entries[pos] = pi | (d < 0 ? 0x80000000u : 0u);
+    entries[pos] = (g.fb ? pi * g.W + w : pi) | (d < 0 ? 0x80000000u : 0u);
   });
 }
 

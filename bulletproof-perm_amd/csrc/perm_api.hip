@@ -17,9 +17,11 @@
 // Transcript order and RNG draw order match oracle/bulletproofs.py
 // ac_prove / ac_verify exactly (tests compare proof bytes).
 #include <cstring>
+#include <memory>
 
 #include "ctx.h"
 #include "gens.h"
+#include "host/par.h"
 #include "host/perm.h"
 #include "ipa.h"
 #include "msm_engine.h"
@@ -35,6 +37,7 @@ struct Proof {
   Enc32 AI, AO, S, T[5];
   Sc tau_x, mu, t_hat;
   IpaProofHost ipa;
+  std::vector<uint32_t> pi;  // prover side only
 };
 
 void put_sc(std::vector<uint8_t>& buf, const Sc& s) {
@@ -121,149 +124,244 @@ int pedersen_host(bpp_ctx* ctx, const bpp_gens* g, const std::vector<Sc>& v, con
 }
 
 int msm_terms(bpp_ctx* ctx, const std::vector<Sc>& sc, const std::vector<uint32_t>& idx,
-              const std::vector<uint32_t>& off, const uint32_t* tbl, const uint32_t* tbl1, uint32_t n0,
-              std::vector<h25519::ge>& res) {
+              const std::vector<uint32_t>& off, const MsmPoints& pts, std::vector<h25519::ge>& res) {
   uint32_t* d_s = nullptr;
   BPP_TRY(upload_sc(ctx, sc, "mt_s", &d_s));
   void* d_i = nullptr;
   BPP_TRY(ctx_ws(ctx, "mt_i", idx.size() * 4 + 4, &d_i));
   BPP_HIP(hipMemcpyAsync(d_i, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, ctx->stream));
-  return msm_multi(ctx, d_s, (const uint32_t*)d_i, off, tbl, tbl1, n0, res);
+  return msm_multi(ctx, d_s, (const uint32_t*)d_i, off, pts, res);
 }
 
-struct Challenges {
-  Sc x_perm, y, z, x, w;
+// Per-proof prover state carried between the lockstep phases.
+struct ProverState {
+  merlin::Transcript tr;
+  std::vector<uint32_t> pi;
+  std::vector<Sc> gamma, sL, sR, taus, vals, aL, aR, aO, y_inv_n, l, r;
+  Sc alpha, beta, rho, x_perm, w;
+  Sc t[7];
+  explicit ProverState(const uint8_t* label, size_t llen) : tr(label, llen) {}
 };
 
-int prove_one(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, uint64_t seed, merlin::Transcript& tr,
-              Proof& P, std::vector<uint32_t>* pi_out) {
+// Proves `seeds.size()` permutation proofs in lockstep: every GPU step
+// (Pedersen V, Pedersen V_2k, the A_I/A_O/S MSMs, Pedersen T, each IPA
+// round) is ONE launch sequence for the whole batch, and the per-proof host
+// work between them (transcripts, challenges, polynomial coefficients) runs
+// on a thread pool.  Outputs are identical to proving one at a time.
+int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const std::vector<uint64_t>& seeds,
+                const uint8_t* label, size_t llen, std::vector<Proof>& Ps) {
   const uint32_t k = C.k, n_p = C.n_p, m = C.m;
-  perm::Rng rng("bpperm-prove", seed);
-  std::vector<uint32_t> pi = perm::fisher_yates(k, rng);
-  if (pi_out) *pi_out = pi;
-  std::vector<Sc> gamma(m);
-  for (auto& g : gamma) g = rng.scalar();
-  const Sc alpha = rng.scalar(), beta = rng.scalar(), rho = rng.scalar();
-  std::vector<Sc> sL(n_p), sR(n_p), taus(5);
-  for (auto& s : sL) s = rng.scalar();
-  for (auto& s : sR) s = rng.scalar();
-  for (auto& s : taus) s = rng.scalar();
+  const size_t P = seeds.size();
+  Ps.assign(P, Proof());
+  if (!P) return BPP_OK;
+  std::vector<std::unique_ptr<ProverState>> S(P);
+  for (size_t p = 0; p < P; ++p) S[p].reset(new ProverState(label, llen));
 
-  tr.arithmetic_domain_sep(n_p);
-  // V_0..V_2k-1, then x_perm, then V_2k = commit(x_perm)
-  std::vector<Sc> vals(2 * k);
-  for (uint32_t i = 0; i < k; ++i) {
-    vals[i] = hsc::from_u64(i + 1);
-    vals[k + i] = hsc::from_u64(pi[i] + 1);
-  }
-  std::vector<Enc32> V;
-  BPP_TRY(pedersen_host(ctx, G, vals, std::vector<Sc>(gamma.begin(), gamma.begin() + 2 * k), V));
-  for (auto& e : V) tr.append_point("V", e.data());
-  const Sc x_perm = tr.challenge_scalar("x_perm");
-  std::vector<Enc32> Vx;
-  BPP_TRY(pedersen_host(ctx, G, {x_perm}, {gamma[2 * k]}, Vx));
-  V.push_back(Vx[0]);
-  tr.append_point("V", Vx[0].data());
-  P.V = V;
+  // RNG draws (order fixed: pi, gamma, alpha beta rho, s_L, s_R, tau x5)
+  par::for_each(P, [&](size_t p) {
+    ProverState& st = *S[p];
+    perm::Rng rng("bpperm-prove", seeds[p]);
+    st.pi = perm::fisher_yates(k, rng);
+    st.gamma.resize(m);
+    for (auto& g : st.gamma) g = rng.scalar();
+    st.alpha = rng.scalar();
+    st.beta = rng.scalar();
+    st.rho = rng.scalar();
+    st.sL.resize(n_p);
+    st.sR.resize(n_p);
+    st.taus.resize(5);
+    for (auto& x : st.sL) x = rng.scalar();
+    for (auto& x : st.sR) x = rng.scalar();
+    for (auto& x : st.taus) x = rng.scalar();
+    st.tr.arithmetic_domain_sep(n_p);
+  });
 
-  std::vector<Sc> v, aL, aR, aO;
-  perm::witness(C, pi, x_perm, v, aL, aR, aO);
-
-  // A_I, A_O, S: one batch of three MSMs over the resident generators
+  // V_0..V_2k-1 of every proof: one fixed-base launch
   {
-    std::vector<Sc> sc;
-    std::vector<uint32_t> idx;
-    auto add = [&](const Sc& s, uint32_t i) {
-      sc.push_back(s);
-      idx.push_back(i);
-    };
-    add(alpha, G->bbidx());
-    for (uint32_t i = 0; i < n_p; ++i) add(aL[i], G->gidx(i));
-    for (uint32_t i = 0; i < n_p; ++i) add(aR[i], G->hidx(i));
-    const uint32_t o1 = (uint32_t)sc.size();
-    add(beta, G->bbidx());
-    for (uint32_t i = 0; i < n_p; ++i) add(aO[i], G->gidx(i));
-    const uint32_t o2 = (uint32_t)sc.size();
-    add(rho, G->bbidx());
-    for (uint32_t i = 0; i < n_p; ++i) add(sL[i], G->gidx(i));
-    for (uint32_t i = 0; i < n_p; ++i) add(sR[i], G->hidx(i));
-    std::vector<h25519::ge> res;
-    BPP_TRY(msm_terms(ctx, sc, idx, {0, o1, o2, (uint32_t)sc.size()}, G->d_tbl, nullptr, 0xffffffffu, res));
-    h25519::encode(P.AI.data(), res[0]);
-    h25519::encode(P.AO.data(), res[1]);
-    h25519::encode(P.S.data(), res[2]);
+    std::vector<Sc> v((size_t)P * 2 * k), g((size_t)P * 2 * k);
+    par::for_each(P, [&](size_t p) {
+      for (uint32_t i = 0; i < k; ++i) {
+        v[p * 2 * k + i] = hsc::from_u64(i + 1);
+        v[p * 2 * k + k + i] = hsc::from_u64(S[p]->pi[i] + 1);
+      }
+      for (uint32_t i = 0; i < 2 * k; ++i) g[p * 2 * k + i] = S[p]->gamma[i];
+    });
+    std::vector<Enc32> V;
+    BPP_TRY(pedersen_host(ctx, G, v, g, V));
+    par::for_each(P, [&](size_t p) {
+      Ps[p].V.assign(V.begin() + p * 2 * k, V.begin() + (p + 1) * 2 * k);
+      for (auto& e : Ps[p].V) S[p]->tr.append_point("V", e.data());
+      S[p]->x_perm = S[p]->tr.challenge_scalar("x_perm");
+    });
   }
-  tr.append_point("A_I", P.AI.data());
-  tr.append_point("A_O", P.AO.data());
-  tr.append_point("S", P.S.data());
-  const Sc y = tr.challenge_scalar("y");
-  const Sc z = tr.challenge_scalar("z");
-
-  std::vector<Sc> y_n = hsc::powers(y, n_p);
-  std::vector<Sc> y_inv_n = hsc::powers(hsc::invert(y), n_p);
-  std::vector<Sc> zq = hsc::powers(z, C.Q + 1);
-  zq.erase(zq.begin());
-  const std::vector<Sc> zWL = perm::zW(C.WL, zq, n_p), zWR = perm::zW(C.WR, zq, n_p), zWO = perm::zW(C.WO, zq, n_p),
-                        zWV = perm::zW(C.WV, zq, m);
-  // l(X) = l1 X + l2 X^2 + l3 X^3 ; r(X) = r0 + r1 X + r3 X^3
-  std::vector<Sc> l1(n_p), r0(n_p), r1(n_p), r3(n_p);
-  for (uint32_t i = 0; i < n_p; ++i) {
-    l1[i] = hsc::add(aL[i], hsc::mul(y_inv_n[i], zWR[i]));
-    r0[i] = hsc::sub(zWO[i], y_n[i]);
-    r1[i] = hsc::add(hsc::mul(y_n[i], aR[i]), zWL[i]);
-    r3[i] = hsc::mul(y_n[i], sR[i]);
-  }
-  const std::vector<Sc>& l2 = aO;
-  const std::vector<Sc>& l3 = sL;
-  using hsc::add;
-  using hsc::inner_product;
-  Sc t[7];
-  t[1] = inner_product(l1, r0);
-  t[2] = add(inner_product(l1, r1), inner_product(l2, r0));
-  t[3] = add(inner_product(l2, r1), inner_product(l3, r0));
-  t[4] = add(inner_product(l1, r3), inner_product(l3, r1));
-  t[5] = inner_product(l2, r3);
-  t[6] = inner_product(l3, r3);
+  // V_2k = commit(x_perm, gamma_2k)
   {
-    std::vector<Enc32> T;
-    BPP_TRY(pedersen_host(ctx, G, {t[1], t[3], t[4], t[5], t[6]}, taus, T));
-    static const char* lab[5] = {"T1", "T3", "T4", "T5", "T6"};
-    for (int i = 0; i < 5; ++i) {
-      P.T[i] = T[i];
-      tr.append_point(lab[i], T[i].data());
+    std::vector<Sc> v(P), g(P);
+    for (size_t p = 0; p < P; ++p) {
+      v[p] = S[p]->x_perm;
+      g[p] = S[p]->gamma[2 * k];
     }
+    std::vector<Enc32> Vx;
+    BPP_TRY(pedersen_host(ctx, G, v, g, Vx));
+    par::for_each(P, [&](size_t p) {
+      Ps[p].V.push_back(Vx[p]);
+      S[p]->tr.append_point("V", Vx[p].data());
+      perm::witness(C, S[p]->pi, S[p]->x_perm, S[p]->vals, S[p]->aL, S[p]->aR, S[p]->aO);
+    });
   }
-  const Sc x = tr.challenge_scalar("x");
-  std::vector<Sc> xp = hsc::powers(x, 7);
-  const int tidx[5] = {1, 3, 4, 5, 6};
-  Sc tau_x = hsc::mul(xp[2], inner_product(zWV, gamma));
-  for (int i = 0; i < 5; ++i) tau_x = add(tau_x, hsc::mul(taus[i], xp[tidx[i]]));
-  const Sc mu = add(add(hsc::mul(alpha, x), hsc::mul(beta, xp[2])), hsc::mul(rho, xp[3]));
-  std::vector<Sc> l(n_p), r(n_p);
-  for (uint32_t i = 0; i < n_p; ++i) {
-    l[i] = hsc::mul(x, add(l1[i], hsc::mul(x, add(l2[i], hsc::mul(x, l3[i])))));
-    r[i] = add(r0[i], hsc::mul(x, add(r1[i], hsc::mul(xp[2], r3[i]))));
+  MsmPoints pts;
+  BPP_TRY(gens_points(ctx, G, &pts));
+  // A_I, A_O, S of every proof: one batch of 3P MSMs
+  {
+    const uint32_t per = 3 + 5 * n_p;  // terms per proof
+    std::vector<Sc> sc((size_t)P * per);
+    std::vector<uint32_t> idx((size_t)P * per), off(3 * P + 1);
+    par::for_each(P, [&](size_t p) {
+      ProverState& st = *S[p];
+      size_t t = p * per;
+      auto add = [&](const Sc& s, uint32_t i) {
+        sc[t] = s;
+        idx[t++] = i;
+      };
+      add(st.alpha, G->bbidx());
+      for (uint32_t i = 0; i < n_p; ++i) add(st.aL[i], G->gidx(i));
+      for (uint32_t i = 0; i < n_p; ++i) add(st.aR[i], G->hidx(i));
+      add(st.beta, G->bbidx());
+      for (uint32_t i = 0; i < n_p; ++i) add(st.aO[i], G->gidx(i));
+      add(st.rho, G->bbidx());
+      for (uint32_t i = 0; i < n_p; ++i) add(st.sL[i], G->gidx(i));
+      for (uint32_t i = 0; i < n_p; ++i) add(st.sR[i], G->hidx(i));
+    });
+    for (size_t p = 0; p < P; ++p) {
+      off[3 * p] = (uint32_t)(p * per);
+      off[3 * p + 1] = (uint32_t)(p * per + 1 + 2 * n_p);
+      off[3 * p + 2] = (uint32_t)(p * per + 2 + 3 * n_p);
+    }
+    off[3 * P] = (uint32_t)(P * per);
+    uint32_t* d_s = nullptr;
+    BPP_TRY(upload_sc(ctx, sc, "mt_s", &d_s));
+    void* d_i = nullptr;
+    BPP_TRY(ctx_ws(ctx, "mt_i", idx.size() * 4 + 4, &d_i));
+    BPP_HIP(hipMemcpyAsync(d_i, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    std::vector<uint8_t> enc(3 * P * 32);
+    BPP_TRY(msm_multi_enc(ctx, d_s, (const uint32_t*)d_i, off, pts, enc.data()));
+    par::for_each(P, [&](size_t p) {
+      memcpy(Ps[p].AI.data(), &enc[96 * p], 32);
+      memcpy(Ps[p].AO.data(), &enc[96 * p + 32], 32);
+      memcpy(Ps[p].S.data(), &enc[96 * p + 64], 32);
+    });
   }
-  const Sc t_hat = inner_product(l, r);
-  tr.append_scalar("TX", tau_x);
-  tr.append_scalar("mu", mu);
-  tr.append_scalar("t", t_hat);
-  P.tau_x = tau_x;
-  P.mu = mu;
-  P.t_hat = t_hat;
-  const Sc w = tr.challenge_scalar("w");
-
-  uint32_t *d_l, *d_r, *d_hf;
-  BPP_TRY(upload_sc(ctx, l, "pf_l", &d_l));
-  BPP_TRY(upload_sc(ctx, r, "pf_r", &d_r));
-  BPP_TRY(upload_sc(ctx, y_inv_n, "pf_hf", &d_hf));
-  IpaGens ig;
-  ig.d_tbl = G->d_tbl;
-  ig.gbase = 0;
-  ig.hbase = (uint32_t)G->n;
-  ig.qidx = G->bidx();
-  ig.qmul = w;
-  BPP_TRY(ipa_prove_dev(ctx, tr, ig, n_p, nullptr, d_hf, d_l, d_r, P.ipa));
+  // challenges y, z and the t(X) coefficients (host, per proof)
+  std::vector<std::vector<Sc>> l1s(P), r0s(P), r1s(P), r3s(P), zWVs(P);
+  par::for_each(P, [&](size_t p) {
+    ProverState& st = *S[p];
+    Proof& Pf = Ps[p];
+    st.tr.append_point("A_I", Pf.AI.data());
+    st.tr.append_point("A_O", Pf.AO.data());
+    st.tr.append_point("S", Pf.S.data());
+    const Sc y = st.tr.challenge_scalar("y");
+    const Sc z = st.tr.challenge_scalar("z");
+    std::vector<Sc> y_n = hsc::powers(y, n_p);
+    st.y_inv_n = hsc::powers(hsc::invert(y), n_p);
+    std::vector<Sc> zq = hsc::powers(z, C.Q + 1);
+    zq.erase(zq.begin());
+    const std::vector<Sc> zWL = perm::zW(C.WL, zq, n_p), zWR = perm::zW(C.WR, zq, n_p),
+                          zWO = perm::zW(C.WO, zq, n_p);
+    zWVs[p] = perm::zW(C.WV, zq, m);
+    // l(X) = l1 X + l2 X^2 + l3 X^3 ; r(X) = r0 + r1 X + r3 X^3
+    std::vector<Sc>&l1 = l1s[p], &r0 = r0s[p], &r1 = r1s[p], &r3 = r3s[p];
+    l1.resize(n_p);
+    r0.resize(n_p);
+    r1.resize(n_p);
+    r3.resize(n_p);
+    for (uint32_t i = 0; i < n_p; ++i) {
+      l1[i] = hsc::add(st.aL[i], hsc::mul(st.y_inv_n[i], zWR[i]));
+      r0[i] = hsc::sub(zWO[i], y_n[i]);
+      r1[i] = hsc::add(hsc::mul(y_n[i], st.aR[i]), zWL[i]);
+      r3[i] = hsc::mul(y_n[i], st.sR[i]);
+    }
+    const std::vector<Sc>& l2 = st.aO;
+    const std::vector<Sc>& l3 = st.sL;
+    using hsc::add;
+    using hsc::inner_product;
+    st.t[1] = inner_product(l1, r0);
+    st.t[2] = add(inner_product(l1, r1), inner_product(l2, r0));
+    st.t[3] = add(inner_product(l2, r1), inner_product(l3, r0));
+    st.t[4] = add(inner_product(l1, r3), inner_product(l3, r1));
+    st.t[5] = inner_product(l2, r3);
+    st.t[6] = inner_product(l3, r3);
+  });
+  // T1, T3..T6 of every proof: one fixed-base launch
+  {
+    std::vector<Sc> v(5 * P), g(5 * P);
+    static const int ti[5] = {1, 3, 4, 5, 6};
+    for (size_t p = 0; p < P; ++p)
+      for (int i = 0; i < 5; ++i) {
+        v[5 * p + i] = S[p]->t[ti[i]];
+        g[5 * p + i] = S[p]->taus[i];
+      }
+    std::vector<Enc32> T;
+    BPP_TRY(pedersen_host(ctx, G, v, g, T));
+    par::for_each(P, [&](size_t p) {
+      ProverState& st = *S[p];
+      Proof& Pf = Ps[p];
+      static const char* lab[5] = {"T1", "T3", "T4", "T5", "T6"};
+      for (int i = 0; i < 5; ++i) {
+        Pf.T[i] = T[5 * p + i];
+        st.tr.append_point(lab[i], Pf.T[i].data());
+      }
+      const Sc x = st.tr.challenge_scalar("x");
+      std::vector<Sc> xp = hsc::powers(x, 7);
+      const int tidx[5] = {1, 3, 4, 5, 6};
+      using hsc::add;
+      Sc tau_x = hsc::mul(xp[2], hsc::inner_product(zWVs[p], st.gamma));
+      for (int i = 0; i < 5; ++i) tau_x = add(tau_x, hsc::mul(st.taus[i], xp[tidx[i]]));
+      const Sc mu = add(add(hsc::mul(st.alpha, x), hsc::mul(st.beta, xp[2])), hsc::mul(st.rho, xp[3]));
+      const std::vector<Sc>&l1 = l1s[p], &r0 = r0s[p], &r1 = r1s[p], &r3 = r3s[p];
+      const std::vector<Sc>& l2 = st.aO;
+      const std::vector<Sc>& l3 = st.sL;
+      st.l.resize(n_p);
+      st.r.resize(n_p);
+      for (uint32_t i = 0; i < n_p; ++i) {
+        st.l[i] = hsc::mul(x, add(l1[i], hsc::mul(x, add(l2[i], hsc::mul(x, l3[i])))));
+        st.r[i] = add(r0[i], hsc::mul(x, add(r1[i], hsc::mul(xp[2], r3[i]))));
+      }
+      const Sc t_hat = hsc::inner_product(st.l, st.r);
+      st.tr.append_scalar("TX", tau_x);
+      st.tr.append_scalar("mu", mu);
+      st.tr.append_scalar("t", t_hat);
+      Pf.tau_x = tau_x;
+      Pf.mu = mu;
+      Pf.t_hat = t_hat;
+      st.w = st.tr.challenge_scalar("w");
+    });
+  }
+  // IPA of every proof in lockstep
+  {
+    std::vector<Sc> L((size_t)P * n_p), R((size_t)P * n_p), HF((size_t)P * n_p);
+    std::vector<Sc> qmul(P);
+    std::vector<merlin::Transcript*> trs(P);
+    par::for_each(P, [&](size_t p) {
+      std::copy(S[p]->l.begin(), S[p]->l.end(), L.begin() + p * n_p);
+      std::copy(S[p]->r.begin(), S[p]->r.end(), R.begin() + p * n_p);
+      std::copy(S[p]->y_inv_n.begin(), S[p]->y_inv_n.end(), HF.begin() + p * n_p);
+      qmul[p] = S[p]->w;
+      trs[p] = &S[p]->tr;
+    });
+    uint32_t *d_l, *d_r, *d_hf;
+    BPP_TRY(upload_sc(ctx, L, "pf_l", &d_l));
+    BPP_TRY(upload_sc(ctx, R, "pf_r", &d_r));
+    BPP_TRY(upload_sc(ctx, HF, "pf_hf", &d_hf));
+    IpaGens ig;
+    ig.pts = pts;
+    ig.gbase = 0;
+    ig.hbase = (uint32_t)G->n;
+    ig.qidx = G->bidx();
+    std::vector<IpaProofHost> ipas;
+    BPP_TRY(ipa_prove_batch_dev(ctx, trs, ig, n_p, nullptr, d_hf, d_l, d_r, qmul, ipas));
+    for (size_t p = 0; p < P; ++p) Ps[p].ipa = std::move(ipas[p]);
+  }
+  for (size_t p = 0; p < P; ++p) Ps[p].pi = S[p]->pi;
   return BPP_OK;
 }
 
@@ -356,26 +454,50 @@ int verify_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const 
     ctx->err = "generators shorter than the padded circuit";
     return BPP_ERR_LEN;
   }
-  std::vector<Sc> gen_sc(2 * n_p + 2, hsc::zero());
-  std::vector<Sc> pt_sc;
-  std::vector<uint8_t> enc;
-  merlin::Transcript batch((const uint8_t*)"bp-perm-batch-verify", 20);
+  // pass 1 (parallel over proofs): parse, replay each transcript, and
+  // collect the unweighted generator / proof-point scalars and the proof's
+  // weight challenge r
   std::vector<Proof> Ps(count);
   std::vector<Sc> rs(count);
-  // pass 1: parse and replay transcripts to get each proof's weight challenge
-  for (size_t p = 0; p < count; ++p) {
-    if (!deserialize(C, proofs + p * proof_stride, perm::proof_len(C.k), V + p * 32 * C.m, Ps[p])) return BPP_ERR_VERIFY;
+  std::vector<std::vector<Sc>> gen_p(count), pt_p(count);
+  std::vector<uint8_t> ok(count, 0);
+  par::for_each(count, [&](size_t p) {
+    if (!deserialize(C, proofs + p * proof_stride, perm::proof_len(C.k), V + p * 32 * C.m, Ps[p])) return;
     merlin::Transcript tr(label, llen);
-    std::vector<Sc> g_tmp(2 * n_p + 2, hsc::zero()), p_tmp;
-    if (!verify_scalars(C, Ps[p], tr, hsc::one(), g_tmp, p_tmp, &rs[p])) return BPP_ERR_VERIFY;
-    batch.append_scalar("r", rs[p]);
+    gen_p[p].assign(2 * n_p + 2, hsc::zero());
+    ok[p] = verify_scalars(C, Ps[p], tr, hsc::one(), gen_p[p], pt_p[p], &rs[p]) ? 1 : 0;
+  });
+  for (size_t p = 0; p < count; ++p)
+    if (!ok[p]) return BPP_ERR_VERIFY;
+  // per-proof weights from a batch transcript over all r (serial, cheap)
+  std::vector<Sc> wts(count, hsc::one());
+  if (count > 1) {
+    merlin::Transcript batch((const uint8_t*)"bp-perm-batch-verify", 20);
+    for (size_t p = 0; p < count; ++p) batch.append_scalar("r", rs[p]);
+    for (size_t p = 0; p < count; ++p) wts[p] = batch.challenge_scalar("proof-weight");
   }
-  for (size_t p = 0; p < count; ++p) {
-    const Sc wt = count == 1 ? hsc::one() : batch.challenge_scalar("proof-weight");
-    merlin::Transcript tr(label, llen);
-    if (!verify_scalars(C, Ps[p], tr, wt, gen_sc, pt_sc, nullptr)) return BPP_ERR_VERIFY;
-    proof_points(Ps[p], enc);
-  }
+  // pass 2: weighted sums (generators merged across proofs; proof points
+  // each weighted by their proof's weight)
+  const size_t npt = pt_p[0].size();
+  std::vector<Sc> gen_sc(2 * n_p + 2, hsc::zero());
+  std::vector<Sc> pt_sc(count * npt);
+  const size_t NG = 2 * (size_t)n_p + 2;
+  const size_t gchunks = std::min<size_t>(NG, 64);
+  par::for_each(gchunks, [&](size_t c) {
+    for (size_t i = c * NG / gchunks; i < (c + 1) * NG / gchunks; ++i) {
+      Sc acc = hsc::zero();
+      for (size_t p = 0; p < count; ++p) acc = hsc::add(acc, hsc::mul(wts[p], gen_p[p][i]));
+      gen_sc[i] = acc;
+    }
+  });
+  std::vector<uint8_t> enc(count * (npt * 32));
+  par::for_each(count, [&](size_t p) {
+    for (size_t j = 0; j < npt; ++j) pt_sc[p * npt + j] = hsc::mul(wts[p], pt_p[p][j]);
+    std::vector<uint8_t> e;
+    e.reserve(npt * 32);
+    proof_points(Ps[p], e);
+    memcpy(&enc[p * npt * 32], e.data(), npt * 32);
+  });
   uint32_t* d_x = nullptr;
   int rc = decompress_ws(ctx, enc.data(), enc.size() / 32, "pv_x", &d_x);
   if (rc == BPP_ERR_DECOMPRESS) return BPP_ERR_VERIFY;
@@ -400,7 +522,10 @@ int verify_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const 
     idx.push_back(n0 + (uint32_t)j);
   }
   std::vector<h25519::ge> res;
-  BPP_TRY(msm_terms(ctx, sc, idx, {0, (uint32_t)sc.size()}, G->d_tbl, d_x, n0, res));
+  MsmPoints pts;
+  BPP_TRY(gens_points(ctx, G, &pts));
+  BPP_TRY(msm_points_extra(ctx, &pts, d_x, (uint32_t)(enc.size() / 32), n0, "pv_x_wt", (double)sc.size()));
+  BPP_TRY(msm_terms(ctx, sc, idx, {0, (uint32_t)sc.size()}, pts, res));
   uint8_t e[32];
   h25519::encode(e, res[0]);
   static const uint8_t zero[32] = {0};
@@ -422,23 +547,33 @@ int bpp_perm_prove(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, uint64_t seed, c
     return BPP_ERR_LEN;
   }
   BPP_HIP(hipSetDevice(ctx->device));
-  merlin::Transcript tr(label, llen);
-  Proof P;
-  std::vector<uint32_t> pi;
-  BPP_TRY(prove_one(ctx, G, C, seed, tr, P, &pi));
-  serialize(C, P, proof_out);
-  for (uint32_t j = 0; j < C.m; ++j) memcpy(V_out + 32 * j, P.V[j].data(), 32);
-  if (perm_out) memcpy(perm_out, pi.data(), 4 * k);
+  std::vector<Proof> Ps;
+  BPP_TRY(prove_batch(ctx, G, C, {seed}, label, llen, Ps));
+  serialize(C, Ps[0], proof_out);
+  for (uint32_t j = 0; j < C.m; ++j) memcpy(V_out + 32 * j, Ps[0].V[j].data(), 32);
+  if (perm_out) memcpy(perm_out, Ps[0].pi.data(), 4 * k);
   return BPP_OK;
 }
 
 int bpp_perm_prove_batch(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, size_t count, const uint64_t* seeds,
                          const uint8_t* label, size_t llen, uint8_t* proofs_out, uint8_t* V_out) {
-  if (!ctx || !G || !seeds || ((!proofs_out || !V_out) && count)) return BPP_ERR_ARG;
-  const size_t pl = bpp_perm_proof_len(k);
-  for (size_t p = 0; p < count; ++p)
-    BPP_TRY(bpp_perm_prove(ctx, G, k, seeds[p], label, llen, proofs_out + p * pl, V_out + p * 32 * (2 * k + 1),
-                           nullptr));
+  if (!ctx || !G || (!seeds && count) || ((!proofs_out || !V_out) && count) || (!label && llen) || k < 2 ||
+      k > (1u << 20))
+    return BPP_ERR_ARG;
+  if (!count) return BPP_OK;
+  const perm::Circuit C = perm::build(k);
+  if (G->n < C.n_p) {
+    ctx->err = "generators shorter than the padded circuit";
+    return BPP_ERR_LEN;
+  }
+  BPP_HIP(hipSetDevice(ctx->device));
+  const size_t pl = perm::proof_len(k);
+  std::vector<Proof> Ps;
+  BPP_TRY(prove_batch(ctx, G, C, std::vector<uint64_t>(seeds, seeds + count), label, llen, Ps));
+  par::for_each(count, [&](size_t p) {
+    serialize(C, Ps[p], proofs_out + p * pl);
+    for (uint32_t j = 0; j < C.m; ++j) memcpy(V_out + (p * C.m + j) * 32, Ps[p].V[j].data(), 32);
+  });
   return BPP_OK;
 }
 

@@ -55,3 +55,43 @@ def test_perm_batch_verify(gens):
     b[40] ^= 1
     bad[2] = bytes(b)
     assert not pr.verify_batch(bad, Vs)
+
+
+@pytest.mark.parametrize("mode", ["0", "1"])
+def test_perm_proof_both_msm_engines(gens, monkeypatch, mode):
+    """BPP_MSM_FB=0 forces the variable-base (per-window Horner) engine,
+    =1 the fixed-base window-table engine; both must give the oracle's bytes
+    and verify (the verifier's proof points take the window-table path too)."""
+    import bpperm
+    monkeypatch.setenv("BPP_MSM_FB", mode)
+    want, perm = bp.ac_prove(6, 21)
+    pr = bpperm.PermProver(gens, 6)
+    proof, V, gperm = pr.prove(21)
+    assert gperm == perm and V == want.V and proof == want.to_bytes()
+    assert pr.verify(proof, V)
+    proofs, Vs = pr.prove_batch([31, 32, 33])
+    assert pr.verify_batch(proofs, Vs)
+    bad = bytearray(proofs[1])
+    bad[3] ^= 4
+    assert not pr.verify_batch([proofs[0], bytes(bad), proofs[2]], Vs)
+
+
+def test_prove_batch_lockstep_bit_exact(gens):
+    """The lockstep batch prover (one launch sequence for all proofs) gives
+    the oracle's bytes for every seed, and the same bytes as proving one at a
+    time for a larger batch (52 cards, more proofs than host threads)."""
+    import bpperm
+    pr = bpperm.PermProver(gens, 5)
+    seeds = [41, 42, 43]
+    proofs, Vs = pr.prove_batch(seeds)
+    for s, pf, V in zip(seeds, proofs, Vs):
+        want, _ = bp.ac_prove(5, s)
+        assert pf == want.to_bytes()
+        assert V == b"".join(want.V)
+    pr52 = bpperm.PermProver(gens, 52)
+    seeds = list(range(100, 140))
+    proofs, Vs = pr52.prove_batch(seeds)
+    for i in (0, 17, 39):
+        pf, V, _ = pr52.prove(seeds[i])
+        assert proofs[i] == pf and Vs[i] == b"".join(V)
+    assert pr52.verify_batch(proofs, Vs)

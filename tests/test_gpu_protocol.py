@@ -93,3 +93,27 @@ def test_ipa_prove_matches_oracle_and_verifies(ctx, gens16, n):
     bad = list(args)
     bad[7] = sb((want.a + 1) % r255.L)
     assert not gens16.ipa_verify(bpperm.Transcript(b"ipa-test"), *bad)
+
+
+@pytest.mark.parametrize("mode", ["0", "1"])
+def test_ipa_and_vec_commit_both_msm_engines(ctx, gens16, monkeypatch, mode):
+    import bpperm
+    monkeypatch.setenv("BPP_MSM_FB", mode)
+    rng = Rng(300)
+    oG, oH = merlin.bulletproof_gens(16)
+    _, Bb = merlin.pedersen_gens_default()
+    n = 16
+    Q = rng.point()
+    a = [rng.scalar() for _ in range(n)]
+    b = [rng.scalar() for _ in range(n)]
+    blind = rng.scalar()
+    assert gens16.vec_commit(sb(blind), [sb(x) for x in a], [sb(x) for x in b]) == \
+        r255.encode(bp.msm([blind] + a + b, [Bb] + oG + oH))
+    ones = [1] * n
+    want = bp.ipa_create(merlin.Transcript(b"ipa-fb"), Q, ones, ones, oG, oH, a, b)
+    L, R, ga, gb = gens16.ipa_prove(bpperm.Transcript(b"ipa-fb"), r255.encode(Q), None, None,
+                                    [sb(x) for x in a], [sb(x) for x in b])
+    assert L == want.L and R == want.R and ga == sb(want.a) and gb == sb(want.b)
+    P = bp.msm(a + b + [bp.inner(a, b)], oG + oH + [Q])
+    assert gens16.ipa_verify(bpperm.Transcript(b"ipa-fb"), n, None, None, r255.encode(P), r255.encode(Q),
+                             L, R, ga, gb)

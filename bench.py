@@ -29,6 +29,10 @@ sys.path.insert(0, str(ROOT / "bulletproof-perm_amd"))
 
 L = 2**252 + 27742317777372353535851937790883648493
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+# Integer-ALU roofline: dependent-free GF(2^255-19) multiplies per second on
+# the whole chip, measured by tools/ubench/felat (profiles/r01_felat.txt,
+# 16 waves/SIMD).  One mixed addition (ge_madd) = 7 field multiplies.
+FE_MUL_PEAK_GOPS = 230.0
 
 
 def synth_scalars(n: int, seed: int) -> bytes:
@@ -71,6 +75,58 @@ def cpu_baseline(seconds: float = 15.0):
     return cport.bench_msm(log2n=16, seconds=seconds)
 
 
+def bench_proofs(ctx, args, world, rank, torch, dist):
+    """Config 4: batches of 52-card permutation proofs, sharded one batch per
+    GPU (independent proofs: no collective on the data path), proved in
+    lockstep on each GPU; then the same proofs batch-verified (one MSM per
+    GPU's batch).  Returns whole-job proofs/s (max time over ranks)."""
+    import bpperm
+    B = args.proofs_per_gpu
+    gens = bpperm.Gens(ctx, 128)
+    pr = bpperm.PermProver(gens, 52)
+    seeds = lambda step: [((step * world + rank) * B + i) for i in range(B)]  # noqa: E731
+    pr.prove_batch(seeds(10_000))  # warmup (window tables, workspaces)
+
+    def timed(fn):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = fn()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([el], dtype=torch.float64, device="cuda")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = tt.item()
+        return out, el
+
+    batches = []
+
+    def prove_all():
+        for st in range(args.proof_steps):
+            batches.append(pr.prove_batch(seeds(st)))
+
+    _, el_p = timed(prove_all)
+
+    def verify_all():
+        ok = True
+        for proofs, Vs in batches:
+            ok &= pr.verify_batch(proofs, Vs)
+        return ok
+
+    ok, el_v = timed(verify_all)
+    total = B * world * args.proof_steps
+    gens.close()
+    return {"metric": "52-card permutation proofs/sec (prove)", "value": total / el_p, "unit": "proofs/s",
+            "ms_per_batch": el_p / args.proof_steps * 1e3, "proofs_per_gpu_per_batch": B, "batches": args.proof_steps,
+            "verify_batch_proofs_per_sec": total / el_v, "verify_ms_per_batch": el_v / args.proof_steps * 1e3,
+            "all_verified": bool(ok), "n_gpus": world, "scaling": "weak",
+            "config": "config 4: 52-card sound-mode permutation proofs, one lockstep batch per GPU per step"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -80,6 +136,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--verify", action="store_true", help="also recompute via a second window split")
+    ap.add_argument("--proofs-per-gpu", type=int, default=128,
+                    help="52-card proofs per GPU per batch (config 4: 1024 over 8 GPUs); 0 = skip")
+    ap.add_argument("--proof-steps", type=int, default=3)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -145,10 +204,14 @@ def main():
         else:
             ctx.msm_table_dev_partial(d_sc, pts, n, wb, we)
     stages = {}
-    for st in ("msm_count", "msm_scan", "msm_scatter", "msm_accumulate", "msm_reduce"):
+    for st in ("msm_digits", "msm_count", "msm_scan", "msm_scatter", "msm_accumulate", "msm_fixup", "msm_reduce"):
         ms, k = ctx.profile_get(st)
         stages[st] = ms / max(k, 1)
     ctx.profile(False)
+
+    proofs = None
+    if args.proofs_per_gpu > 0:
+        proofs = bench_proofs(ctx, args, world, rank, torch, dist)
 
     ms_step = el / args.steps * 1e3
     value = n * args.steps / el
@@ -176,7 +239,12 @@ def main():
                      "traffic": load_traffic("msm_accumulate", args.log2n),
                      "kernel": "k_msm_accumulate", "kernel_ms": acc_ms,
                      "algo_bytes_per_launch": algo_bytes},
+        "alu_roofline": {"achieved": (7 * n * W / (acc_ms * 1e-3) / 1e9) if acc_ms > 0 else None,
+                         "peak": FE_MUL_PEAK_GOPS, "unit": "G field-mul/s",
+                         "frac": (7 * n * W / (acc_ms * 1e-3) / 1e9 / FE_MUL_PEAK_GOPS) if acc_ms > 0 else None,
+                         "note": "k_msm_accumulate: n*W mixed additions x 7 field multiplies"},
         "stage_ms": stages,
+        "proofs": proofs,
         "setup_s": setup_s,
         "result_prefix": res.hex()[:16],
     }

@@ -1,4 +1,5 @@
 // Context, workspace, profiling and device-memory entry points of the C ABI.
+#include <algorithm>
 #include <cstring>
 
 #include "ctx.h"
@@ -26,6 +27,63 @@ int ctx_pinned(bpp_ctx* ctx, size_t bytes, void** out) {
     ctx->pinned_bytes = bytes;
   }
   *out = ctx->pinned;
+  return BPP_OK;
+}
+
+int ctx_sync(bpp_ctx* ctx) {
+  BPP_HIP(hipStreamSynchronize(ctx->stream));
+  ctx->stage_used = 0;
+  return BPP_OK;
+}
+
+static int stage_take(bpp_ctx* ctx, size_t bytes, uint8_t** out) {
+  const size_t need = (bytes + 255) & ~(size_t)255;
+  if (ctx->stage_used + need > ctx->stage_cap) {
+    BPP_TRY(ctx_sync(ctx));  // every staged copy has completed
+    if (need > ctx->stage_cap) {
+      if (ctx->stage) BPP_HIP(hipHostFree(ctx->stage));
+      ctx->stage = nullptr;
+      ctx->stage_cap = 0;
+      const size_t cap = std::max<size_t>(need, 16u << 20);
+      BPP_HIP(hipHostMalloc((void**)&ctx->stage, cap));
+      ctx->stage_cap = cap;
+    }
+  }
+  *out = ctx->stage + ctx->stage_used;
+  ctx->stage_used += need;
+  return BPP_OK;
+}
+
+int ctx_h2d(bpp_ctx* ctx, void* d, const void* h, size_t bytes) {
+  if (!bytes) return BPP_OK;
+  uint8_t* p = nullptr;
+  BPP_TRY(stage_take(ctx, bytes, &p));
+  memcpy(p, h, bytes);
+  BPP_HIP(hipMemcpyAsync(d, p, bytes, hipMemcpyHostToDevice, ctx->stream));
+  return BPP_OK;
+}
+
+int ctx_d2h(bpp_ctx* ctx, void* h, const void* d, size_t bytes) {
+  if (!bytes) return ctx_sync(ctx);
+  uint8_t* p = nullptr;
+  BPP_TRY(stage_take(ctx, bytes, &p));
+  BPP_HIP(hipMemcpyAsync(p, d, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  BPP_TRY(ctx_sync(ctx));
+  memcpy(h, p, bytes);
+  return BPP_OK;
+}
+
+int ctx_child(bpp_ctx* ctx, size_t i, bpp_ctx** out) {
+  while (ctx->children.size() <= i) {
+    bpp_ctx* c = nullptr;
+    const int rc = bpp_ctx_create(ctx->device, &c);
+    if (rc) {
+      ctx->err = "creating a child context failed";
+      return rc;
+    }
+    ctx->children.push_back(c);
+  }
+  *out = ctx->children[i];
   return BPP_OK;
 }
 
@@ -97,11 +155,13 @@ int bpp_ctx_create(int device, bpp_ctx** out) {
 
 void bpp_ctx_destroy(bpp_ctx* ctx) {
   if (!ctx) return;
+  for (bpp_ctx* c : ctx->children) bpp_ctx_destroy(c);
   hipSetDevice(ctx->device);
   hipStreamSynchronize(ctx->stream);
   for (auto& kv : ctx->ws)
     if (kv.second.p) hipFree(kv.second.p);
   if (ctx->pinned) hipHostFree(ctx->pinned);
+  if (ctx->stage) hipHostFree(ctx->stage);
   for (auto& p : ctx->pending) {
     hipEventDestroy(p.a);
     hipEventDestroy(p.b);

@@ -50,39 +50,54 @@ FE_INLINE void radix16(const uint32_t s[8], int8_t e[64]) {
   e[63] = (int8_t)(e[63] + carry);
 }
 
-FE_INLINE ge_p3 fb_mul_add(ge_p3 acc, const uint32_t* __restrict__ fb, uint32_t base, const int8_t e[64]) {
-  for (int i = 0; i < 64; ++i) {
-    const int d = e[i];
-    if (d == 0) continue;
-    const uint32_t idx = base * FB_POS * 8 + (uint32_t)i * 8 + (uint32_t)((d < 0 ? -d : d) - 1);
-    const ge_niels q = load_niels(fb, idx);
-    acc = d < 0 ? ge_msub(acc, q) : ge_madd(acc, q);
+// P_j = v_j * B + g_j * Bb, PED_G lanes per commitment: lane q adds the
+// table entries of radix-16 positions [4q, 4q+4) of both scalars (8 mixed
+// additions), then the 16 partial sums are combined with 4 xor-shuffle
+// levels.  A one-lane-per-commitment kernel would chain 128 additions (the
+// GPU's per-lane field-multiply latency is ~0.3 us, profiles/r01_felat.txt).
+#define PED_G 16
+__global__ void __launch_bounds__(256) k_pedersen(const uint32_t* __restrict__ fb, const uint32_t* __restrict__ v,
+                                                  const uint32_t* __restrict__ gam, size_t m,
+                                                  uint32_t* __restrict__ out_p3) {
+  const size_t gt = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t j = gt / PED_G;
+  const uint32_t q = (uint32_t)(gt % PED_G);
+  ge_p3 acc = ge_identity();
+  if (j < m) {
+    uint32_t s[8];
+    int8_t e[64];
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) s[i] = v[8 * j + i];
+    radix16(s, e);
+    for (uint32_t i = 4 * q; i < 4 * q + 4; ++i) {
+      const int d = e[i];
+      if (d == 0) continue;
+      const ge_niels t = load_niels(fb, i * 8 + (uint32_t)((d < 0 ? -d : d) - 1));
+      acc = d < 0 ? ge_msub(acc, t) : ge_madd(acc, t);
+    }
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) s[i] = gam[8 * j + i];
+    radix16(s, e);
+    for (uint32_t i = 4 * q; i < 4 * q + 4; ++i) {
+      const int d = e[i];
+      if (d == 0) continue;
+      const ge_niels t = load_niels(fb, FB_POS * 8 + i * 8 + (uint32_t)((d < 0 ? -d : d) - 1));
+      acc = d < 0 ? ge_msub(acc, t) : ge_madd(acc, t);
+    }
   }
-  return acc;
+  _Pragma("unroll") for (int off = 1; off < PED_G; off <<= 1) {
+    ge_p3 o;
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) {
+      o.X.v[i] = __shfl_xor(acc.X.v[i], off, 64);
+      o.Y.v[i] = __shfl_xor(acc.Y.v[i], off, 64);
+      o.Z.v[i] = __shfl_xor(acc.Z.v[i], off, 64);
+      o.T.v[i] = __shfl_xor(acc.T.v[i], off, 64);
+    }
+    acc = ge_add(acc, o);
+  }
+  if (j < m && q == 0) store_p3(out_p3, j, acc);
 }
 
-// out[j] = compress(v_j * B + g_j * Bb); scalars canonical (8 words each)
-__global__ void __launch_bounds__(64) k_pedersen(const uint32_t* __restrict__ fb, const uint32_t* __restrict__ v,
-                                                 const uint32_t* __restrict__ gam, size_t m,
-                                                 uint32_t* __restrict__ out_enc, uint32_t* __restrict__ out_p3) {
-  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= m) return;
-  uint32_t s[8];
-  int8_t e[64];
-  ge_p3 acc = ge_identity();
-  _Pragma("unroll") for (int i = 0; i < 8; ++i) s[i] = v[8 * j + i];
-  radix16(s, e);
-  acc = fb_mul_add(acc, fb, 0, e);
-  _Pragma("unroll") for (int i = 0; i < 8; ++i) s[i] = gam[8 * j + i];
-  radix16(s, e);
-  acc = fb_mul_add(acc, fb, 1, e);
-  if (out_p3) store_p3(out_p3, j, acc);
-  if (out_enc) {
-    uint32_t w[8];
-    ge_ristretto_encode(acc, w);
-    _Pragma("unroll") for (int i = 0; i < 8; ++i) out_enc[8 * j + i] = w[i];
-  }
-}
+// declared in points.hip
+__global__ void k_compress_p3(const uint32_t* __restrict__ pts, size_t n, uint32_t* __restrict__ out);
 
 static int gens_alloc(bpp_ctx* ctx, size_t n, bpp_gens** out) {
   bpp_gens* g = new bpp_gens();
@@ -113,12 +128,27 @@ static int gens_finish(bpp_ctx* ctx, bpp_gens* g) {
 int pedersen_dev(bpp_ctx* ctx, const bpp_gens* g, const uint32_t* d_v, const uint32_t* d_gam, size_t m,
                  uint32_t* d_out_enc, uint32_t* d_out_p3) {
   if (!m) return BPP_OK;
+  uint32_t* p3 = d_out_p3;
+  if (!p3) {
+    void* w = nullptr;
+    BPP_TRY(ctx_ws(ctx, "ped_p3", m * 128, &w));
+    p3 = (uint32_t*)w;
+  }
   {
     ProfScope ps(ctx, "pedersen");
-    hipLaunchKernelGGL(k_pedersen, dim3(grid_for(m, 64)), dim3(64), 0, ctx->stream, g->d_fb, d_v, d_gam, m, d_out_enc,
-                       d_out_p3);
+    hipLaunchKernelGGL(k_pedersen, dim3(grid_for(m * PED_G, 256)), dim3(256), 0, ctx->stream, g->d_fb, d_v, d_gam, m,
+                       p3);
   }
-  return ctx_check_launch(ctx, "k_pedersen");
+  BPP_TRY(ctx_check_launch(ctx, "k_pedersen"));
+  if (d_out_enc) {
+    {
+      ProfScope ps(ctx, "compress");
+      hipLaunchKernelGGL(k_compress_p3, dim3(grid_for(m, 64)), dim3(64), 0, ctx->stream, (const uint32_t*)p3, m,
+                         d_out_enc);
+    }
+    BPP_TRY(ctx_check_launch(ctx, "k_compress_p3"));
+  }
+  return BPP_OK;
 }
 
 int gens_points(bpp_ctx* ctx, const bpp_gens* g, MsmPoints* out) {
@@ -266,8 +296,7 @@ int bpp_pedersen_commit_batch(bpp_ctx* ctx, const bpp_gens* g, const uint8_t* v,
   void* d_out = nullptr;
   BPP_TRY(ctx_ws(ctx, "ped_out", m * 32, &d_out));
   BPP_TRY(pedersen_dev(ctx, g, d_v, d_g, m, (uint32_t*)d_out, nullptr));
-  BPP_HIP(hipMemcpyAsync(out, d_out, m * 32, hipMemcpyDeviceToHost, ctx->stream));
-  BPP_HIP(hipStreamSynchronize(ctx->stream));
+  BPP_TRY(ctx_d2h(ctx, out, d_out, m * 32));
   return BPP_OK;
 }
 

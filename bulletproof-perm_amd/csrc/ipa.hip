@@ -204,11 +204,10 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
       const sc q = to_dev_sc(qmul[p]);
       memcpy(&qw[8 * (size_t)p], q.v, 32);
     }
-    BPP_HIP(hipMemcpyAsync(d_q, qw.data(), qw.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    BPP_TRY(ctx_h2d(ctx, d_q, qw.data(), qw.size() * 4));
     hipLaunchKernelGGL(k_ipa_init, dim3(grid_for(PN, 256)), dim3(256), 0, ctx->stream, n, P, d_a, d_b, d_Gf, d_Hf,
                        (uint32_t*)am, (uint32_t*)bm, (uint32_t*)fG, (uint32_t*)fH);
     BPP_TRY(ctx_check_launch(ctx, "k_ipa_init"));
-    BPP_HIP(hipStreamSynchronize(ctx->stream));  // qw goes out of scope
   }
   std::vector<uint32_t> off(2 * (size_t)P + 1);
   for (uint32_t p = 0; p < P; ++p) {
@@ -235,7 +234,11 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
                          (const uint32_t*)part, (const uint32_t*)d_q, g.qidx, n, (uint32_t*)scal, (uint32_t*)pidx);
     }
     BPP_TRY(ctx_check_launch(ctx, "ipa round kernels"));
-    BPP_TRY(msm_multi_enc(ctx, (const uint32_t*)scal, (const uint32_t*)pidx, off, g.pts, enc.data()));
+    {
+      HostScope hs(ctx, "ipa_msm");
+      BPP_TRY(msm_multi_enc(ctx, (const uint32_t*)scal, (const uint32_t*)pidx, off, g.pts, enc.data()));
+    }
+    HostScope hs(ctx, "ipa_host");
     par::for_each(P, [&](size_t p) {
       Enc32 Le, Re;
       memcpy(Le.data(), enc.data() + 64 * p, 32);
@@ -254,22 +257,26 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
       memcpy(&uw[16 * (size_t)p], um.v, 32);
       memcpy(&uw[16 * (size_t)p + 8], uim.v, 32);
     }
-    BPP_HIP(hipMemcpyAsync(d_u, uw.data(), uw.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    BPP_TRY(ctx_h2d(ctx, d_u, uw.data(), uw.size() * 4));
     {
       ProfScope ps(ctx, "ipa_fold");
       hipLaunchKernelGGL(k_ipa_fold, dim3(grid_for(PN, 256)), dim3(256), 0, ctx->stream, n, lg_n, P, m, (uint32_t*)am,
                          (uint32_t*)bm, (uint32_t*)fG, (uint32_t*)fH, (const uint32_t*)d_u);
     }
     BPP_TRY(ctx_check_launch(ctx, "k_ipa_fold"));
-    BPP_HIP(hipStreamSynchronize(ctx->stream));  // uw reused next round
     m = h;
     if (lg_h) --lg_h;
   }
   // a, b = element 0 of each instance
   std::vector<uint32_t> ab((size_t)P * 16);
-  BPP_HIP(hipMemcpy2DAsync(ab.data(), 64, am, (size_t)n * 32, 32, P, hipMemcpyDeviceToHost, ctx->stream));
-  BPP_HIP(hipMemcpy2DAsync(ab.data() + 8, 64, bm, (size_t)n * 32, 32, P, hipMemcpyDeviceToHost, ctx->stream));
-  BPP_HIP(hipStreamSynchronize(ctx->stream));
+  {
+    void* h = nullptr;
+    BPP_TRY(ctx_pinned(ctx, ab.size() * 4, &h));
+    BPP_HIP(hipMemcpy2DAsync(h, 64, am, (size_t)n * 32, 32, P, hipMemcpyDeviceToHost, ctx->stream));
+    BPP_HIP(hipMemcpy2DAsync((uint8_t*)h + 32, 64, bm, (size_t)n * 32, 32, P, hipMemcpyDeviceToHost, ctx->stream));
+    BPP_TRY(ctx_sync(ctx));
+    memcpy(ab.data(), h, ab.size() * 4);
+  }
   for (uint32_t p = 0; p < P; ++p) {
     out[p].a = hsc::mont(from_dev_words(&ab[16 * (size_t)p]), hsc::one());
     out[p].b = hsc::mont(from_dev_words(&ab[16 * (size_t)p + 8]), hsc::one());

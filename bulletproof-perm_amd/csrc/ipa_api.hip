@@ -27,13 +27,12 @@ int decompress_ws(bpp_ctx* ctx, const uint8_t* enc, size_t count, const char* na
   BPP_TRY(ctx_ws(ctx, "dws_enc", count * 32, &d_enc));
   BPP_TRY(ctx_ws(ctx, "dws_bad", 8, &d_bad));
   unsigned long long bad = ~0ull;
-  BPP_HIP(hipMemcpyAsync(d_enc, enc, count * 32, hipMemcpyHostToDevice, ctx->stream));
-  BPP_HIP(hipMemcpyAsync(d_bad, &bad, 8, hipMemcpyHostToDevice, ctx->stream));
+  BPP_TRY(ctx_h2d(ctx, d_enc, enc, count * 32));
+  BPP_TRY(ctx_h2d(ctx, d_bad, &bad, 8));
   hipLaunchKernelGGL(k_decompress, dim3(grid_for(count, 64)), dim3(64), 0, ctx->stream, (const uint32_t*)d_enc, count,
                      (uint32_t*)d_tbl, (unsigned long long*)d_bad);
   BPP_TRY(ctx_check_launch(ctx, "k_decompress"));
-  BPP_HIP(hipMemcpyAsync(&bad, d_bad, 8, hipMemcpyDeviceToHost, ctx->stream));
-  BPP_HIP(hipStreamSynchronize(ctx->stream));
+  BPP_TRY(ctx_d2h(ctx, &bad, d_bad, 8));
   if (bad != ~0ull) {
     ctx->err = "invalid point encoding at index " + std::to_string(bad);
     return BPP_ERR_DECOMPRESS;
@@ -104,7 +103,7 @@ int bpp_vec_commit(bpp_ctx* ctx, const bpp_gens* g, const uint8_t blind[32], con
   BPP_TRY(upload_scalars(ctx, sc.data(), T, "vc_s", &d_s));
   void* d_i = nullptr;
   BPP_TRY(ctx_ws(ctx, "vc_i", T * 4, &d_i));
-  BPP_HIP(hipMemcpyAsync(d_i, idx.data(), T * 4, hipMemcpyHostToDevice, ctx->stream));
+  BPP_TRY(ctx_h2d(ctx, d_i, idx.data(), T * 4));
   std::vector<h25519::ge> res;
   MsmPoints pts;
   BPP_TRY(gens_points(ctx, g, &pts));
@@ -193,7 +192,7 @@ int bpp_ipa_verify(bpp_ctx* ctx, const bpp_gens* g, bpp_transcript* tr, size_t n
   BPP_TRY(upload_scalars(ctx, sc.data(), T, "ipav_s", &d_s));
   void* d_i = nullptr;
   BPP_TRY(ctx_ws(ctx, "ipav_i", T * 4, &d_i));
-  BPP_HIP(hipMemcpyAsync(d_i, idx.data(), T * 4, hipMemcpyHostToDevice, ctx->stream));
+  BPP_TRY(ctx_h2d(ctx, d_i, idx.data(), T * 4));
   std::vector<h25519::ge> res;
   MsmPoints pts;
   BPP_TRY(gens_points(ctx, g, &pts));

@@ -146,13 +146,14 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
   {
     const uint32_t L = g.B >= 512 ? 8 : (g.B >= 64 ? 4 : (g.B >= 8 ? 2 : 1));
     const uint32_t BPS = (g.B + RED_T * L - 1) / (RED_T * L);
-    void* part = nullptr;
-    BPP_TRY(ctx_ws(ctx, "msm_rpart", nseg * BPS * 128, &part));
+    void* part = wsum;  // one block per segment: its partial is the sum
+    if (BPS > 1) BPP_TRY(ctx_ws(ctx, "msm_rpart", nseg * BPS * 128, &part));
     ProfScope ps(ctx, "msm_reduce");
     hipLaunchKernelGGL(k_msm_reduce_partial, dim3((unsigned)(nseg * BPS)), dim3(RED_T), 0, ctx->stream,
                        (const uint32_t*)bsum, g, L, BPS, (uint32_t*)part);
-    hipLaunchKernelGGL(k_msm_reduce_final, dim3((unsigned)nseg), dim3(RED_T), 0, ctx->stream, (const uint32_t*)part,
-                       BPS, (uint32_t*)wsum);
+    if (BPS > 1)
+      hipLaunchKernelGGL(k_msm_reduce_final, dim3((unsigned)nseg), dim3(RED_T), 0, ctx->stream,
+                         (const uint32_t*)part, BPS, (uint32_t*)wsum);
   }
   BPP_TRY(ctx_check_launch(ctx, "k_msm_reduce"));
   *d_wsum_out = (uint32_t*)wsum;
@@ -196,7 +197,7 @@ int upload_scalars(bpp_ctx* ctx, const uint8_t* scalars, size_t n, const char* n
     }
   void* d = nullptr;
   BPP_TRY(ctx_ws(ctx, name, n * 32 + 32, &d));
-  if (n) BPP_HIP(hipMemcpyAsync(d, scalars, n * 32, hipMemcpyHostToDevice, ctx->stream));
+  BPP_TRY(ctx_h2d(ctx, d, scalars, n * 32));
   *d_out = (uint32_t*)d;
   return BPP_OK;
 }
@@ -390,7 +391,7 @@ static int msm_multi_fb_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t
   }
   void* d_off = nullptr;
   BPP_TRY(ctx_ws(ctx, "multi_off", (M + 1) * 4, &d_off));
-  BPP_HIP(hipMemcpyAsync(d_off, off.data(), (M + 1) * 4, hipMemcpyHostToDevice, ctx->stream));
+  BPP_TRY(ctx_h2d(ctx, d_off, off.data(), (M + 1) * 4));
   const uint32_t n0w = pts.n0 == 0xffffffffu ? 0xffffffffu : pts.n0 * FBW_W;
   return msm_engine(ctx, d_scal, d_pidx, (const uint32_t*)d_off, M, T, FBW_C, 0, FBW_W, pts.wt, d_res, pts.wt1, n0w,
                     true);
@@ -442,7 +443,7 @@ int msm_multi(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, cons
   if (M == 0 || T == 0) return BPP_OK;
   void* d_off = nullptr;
   BPP_TRY(ctx_ws(ctx, "multi_off", (M + 1) * 4, &d_off));
-  BPP_HIP(hipMemcpyAsync(d_off, off.data(), (M + 1) * 4, hipMemcpyHostToDevice, ctx->stream));
+  BPP_TRY(ctx_h2d(ctx, d_off, off.data(), (M + 1) * 4));
   const uint32_t c = msm_choose_c((double)T / (double)M);
   const uint32_t W = (254 + c - 1) / c;
   uint32_t* d_ws = nullptr;
@@ -473,8 +474,7 @@ int msm_multi(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, cons
   }
   BPP_TRY(ctx_check_launch(ctx, "k_msm_horner"));
   std::vector<uint32_t> h((size_t)M * 32);
-  BPP_HIP(hipMemcpyAsync(h.data(), d_res, (size_t)M * 128, hipMemcpyDeviceToHost, ctx->stream));
-  BPP_HIP(hipStreamSynchronize(ctx->stream));
+  BPP_TRY(ctx_d2h(ctx, h.data(), d_res, (size_t)M * 128));
   for (uint32_t m = 0; m < M; ++m) out[m] = h25519::ge_from_words(h.data() + (size_t)m * 32);
   return BPP_OK;
 }

@@ -17,7 +17,9 @@
 // Transcript order and RNG draw order match oracle/bulletproofs.py
 // ac_prove / ac_verify exactly (tests compare proof bytes).
 #include <cstring>
+#include <cstdlib>
 #include <memory>
+#include <thread>
 
 #include "ctx.h"
 #include "gens.h"
@@ -102,8 +104,7 @@ int upload_sc(bpp_ctx* ctx, const std::vector<Sc>& v, const char* name, uint32_t
   void* p = nullptr;
   BPP_TRY(ctx_ws(ctx, name, v.size() * 32 + 32, &p));
   std::vector<uint8_t> b = to_bytes(v);
-  if (!b.empty()) BPP_HIP(hipMemcpyAsync(p, b.data(), b.size(), hipMemcpyHostToDevice, ctx->stream));
-  BPP_HIP(hipStreamSynchronize(ctx->stream));
+  BPP_TRY(ctx_h2d(ctx, p, b.data(), b.size()));
   *d = (uint32_t*)p;
   return BPP_OK;
 }
@@ -112,14 +113,20 @@ int upload_sc(bpp_ctx* ctx, const std::vector<Sc>& v, const char* name, uint32_t
 int pedersen_host(bpp_ctx* ctx, const bpp_gens* g, const std::vector<Sc>& v, const std::vector<Sc>& gam,
                   std::vector<Enc32>& out) {
   uint32_t *d_v, *d_g;
-  BPP_TRY(upload_sc(ctx, v, "pp_v", &d_v));
-  BPP_TRY(upload_sc(ctx, gam, "pp_g", &d_g));
+  {
+    HostScope hs(ctx, "ped_upload");
+    BPP_TRY(upload_sc(ctx, v, "pp_v", &d_v));
+    BPP_TRY(upload_sc(ctx, gam, "pp_g", &d_g));
+  }
   void* d_out = nullptr;
   BPP_TRY(ctx_ws(ctx, "pp_out", v.size() * 32, &d_out));
-  BPP_TRY(pedersen_dev(ctx, g, d_v, d_g, v.size(), (uint32_t*)d_out, nullptr));
+  {
+    HostScope hs(ctx, "ped_kernels");
+    BPP_TRY(pedersen_dev(ctx, g, d_v, d_g, v.size(), (uint32_t*)d_out, nullptr));
+  }
+  HostScope hs(ctx, "ped_d2h");
   out.resize(v.size());
-  BPP_HIP(hipMemcpyAsync(out.data(), d_out, v.size() * 32, hipMemcpyDeviceToHost, ctx->stream));
-  BPP_HIP(hipStreamSynchronize(ctx->stream));
+  BPP_TRY(ctx_d2h(ctx, out.data(), d_out, v.size() * 32));
   return BPP_OK;
 }
 
@@ -129,7 +136,7 @@ int msm_terms(bpp_ctx* ctx, const std::vector<Sc>& sc, const std::vector<uint32_
   BPP_TRY(upload_sc(ctx, sc, "mt_s", &d_s));
   void* d_i = nullptr;
   BPP_TRY(ctx_ws(ctx, "mt_i", idx.size() * 4 + 4, &d_i));
-  BPP_HIP(hipMemcpyAsync(d_i, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+  BPP_TRY(ctx_h2d(ctx, d_i, idx.data(), idx.size() * 4));
   return msm_multi(ctx, d_s, (const uint32_t*)d_i, off, pts, res);
 }
 
@@ -158,6 +165,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
   for (size_t p = 0; p < P; ++p) S[p].reset(new ProverState(label, llen));
 
   // RNG draws (order fixed: pi, gamma, alpha beta rho, s_L, s_R, tau x5)
+  std::unique_ptr<HostScope> hs(new HostScope(ctx, "pb_rng"));
   par::for_each(P, [&](size_t p) {
     ProverState& st = *S[p];
     perm::Rng rng("bpperm-prove", seeds[p]);
@@ -177,6 +185,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
   });
 
   // V_0..V_2k-1 of every proof: one fixed-base launch
+  hs.reset(new HostScope(ctx, "pb_pedersen_V"));
   {
     std::vector<Sc> v((size_t)P * 2 * k), g((size_t)P * 2 * k);
     par::for_each(P, [&](size_t p) {
@@ -195,6 +204,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     });
   }
   // V_2k = commit(x_perm, gamma_2k)
+  hs.reset(new HostScope(ctx, "pb_pedersen_Vx_witness"));
   {
     std::vector<Sc> v(P), g(P);
     for (size_t p = 0; p < P; ++p) {
@@ -212,6 +222,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
   MsmPoints pts;
   BPP_TRY(gens_points(ctx, G, &pts));
   // A_I, A_O, S of every proof: one batch of 3P MSMs
+  hs.reset(new HostScope(ctx, "pb_msm_AI_AO_S"));
   {
     const uint32_t per = 3 + 5 * n_p;  // terms per proof
     std::vector<Sc> sc((size_t)P * per);
@@ -242,7 +253,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     BPP_TRY(upload_sc(ctx, sc, "mt_s", &d_s));
     void* d_i = nullptr;
     BPP_TRY(ctx_ws(ctx, "mt_i", idx.size() * 4 + 4, &d_i));
-    BPP_HIP(hipMemcpyAsync(d_i, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    BPP_TRY(ctx_h2d(ctx, d_i, idx.data(), idx.size() * 4));
     std::vector<uint8_t> enc(3 * P * 32);
     BPP_TRY(msm_multi_enc(ctx, d_s, (const uint32_t*)d_i, off, pts, enc.data()));
     par::for_each(P, [&](size_t p) {
@@ -252,6 +263,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     });
   }
   // challenges y, z and the t(X) coefficients (host, per proof)
+  hs.reset(new HostScope(ctx, "pb_host_poly"));
   std::vector<std::vector<Sc>> l1s(P), r0s(P), r1s(P), r3s(P), zWVs(P);
   par::for_each(P, [&](size_t p) {
     ProverState& st = *S[p];
@@ -292,6 +304,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     st.t[6] = inner_product(l3, r3);
   });
   // T1, T3..T6 of every proof: one fixed-base launch
+  hs.reset(new HostScope(ctx, "pb_pedersen_T_lr"));
   {
     std::vector<Sc> v(5 * P), g(5 * P);
     static const int ti[5] = {1, 3, 4, 5, 6};
@@ -301,11 +314,15 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
         g[5 * p + i] = S[p]->taus[i];
       }
     std::vector<Enc32> T;
-    BPP_TRY(pedersen_host(ctx, G, v, g, T));
+    {
+      HostScope hs2(ctx, "pbT_pedersen");
+      BPP_TRY(pedersen_host(ctx, G, v, g, T));
+    }
+    HostScope hs3(ctx, "pbT_host");
     par::for_each(P, [&](size_t p) {
       ProverState& st = *S[p];
       Proof& Pf = Ps[p];
-      static const char* lab[5] = {"T1", "T3", "T4", "T5", "T6"};
+      const char* lab[5] = {"T1", "T3", "T4", "T5", "T6"};
       for (int i = 0; i < 5; ++i) {
         Pf.T[i] = T[5 * p + i];
         st.tr.append_point(lab[i], Pf.T[i].data());
@@ -337,6 +354,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     });
   }
   // IPA of every proof in lockstep
+  hs.reset(new HostScope(ctx, "pb_ipa"));
   {
     std::vector<Sc> L((size_t)P * n_p), R((size_t)P * n_p), HF((size_t)P * n_p);
     std::vector<Sc> qmul(P);
@@ -568,8 +586,58 @@ int bpp_perm_prove_batch(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, size_t cou
   }
   BPP_HIP(hipSetDevice(ctx->device));
   const size_t pl = perm::proof_len(k);
-  std::vector<Proof> Ps;
-  BPP_TRY(prove_batch(ctx, G, C, std::vector<uint64_t>(seeds, seeds + count), label, llen, Ps));
+  std::vector<Proof> Ps(count);
+  // Sub-batches in flight on S streams (child contexts), one host thread
+  // each: while one sub-batch waits on transcripts / challenges on the host,
+  // the others' MSM and Pedersen kernels fill the GPU (a lockstep batch of
+  // 128 proofs leaves most SIMDs idle in its latency-bound launch tails).
+  // (default 1 until the concurrent path measures faster)
+  size_t S = 1;
+  if (const char* e = getenv("BPP_PROVE_STREAMS")) S = std::max<size_t>(1, std::min<size_t>(count, atoi(e)));
+  {
+    MsmPoints warm;  // build the window tables once, before the threads
+    BPP_TRY(gens_points(ctx, G, &warm));
+  }
+  if (S <= 1) {
+    BPP_TRY(prove_batch(ctx, G, C, std::vector<uint64_t>(seeds, seeds + count), label, llen, Ps));
+  } else {
+    std::vector<bpp_ctx*> kids(S);
+    for (size_t s = 0; s < S; ++s) BPP_TRY(ctx_child(ctx, s, &kids[s]));
+    std::vector<int> rcs(S, BPP_OK);
+    std::vector<std::thread> th;
+    for (size_t s = 0; s < S; ++s)
+      th.emplace_back([&, s] {
+        const size_t b = count * s / S, e = count * (s + 1) / S;
+        bpp_ctx* kc = kids[s];
+        kc->prof = ctx->prof;
+        if (hipSetDevice(ctx->device) != hipSuccess) {
+          rcs[s] = BPP_ERR_DEVICE;
+          return;
+        }
+        std::vector<Proof> sub;
+        rcs[s] = prove_batch(kc, G, C, std::vector<uint64_t>(seeds + b, seeds + e), label, llen, sub);
+        if (rcs[s] == BPP_OK)
+          for (size_t i = b; i < e; ++i) Ps[i] = std::move(sub[i - b]);
+      });
+    for (auto& t : th) t.join();
+    if (ctx->prof)  // fold the children's stage times into this context's
+      for (bpp_ctx* kc : kids) {
+        double ms;
+        uint64_t n;
+        bpp_ctx_profile_get(kc, "", &ms, &n);  // resolves pending events
+        for (auto& kv : kc->prof_acc) {
+          auto& acc = ctx->prof_acc[kv.first];
+          acc.first += kv.second.first;
+          acc.second += kv.second.second;
+        }
+        bpp_ctx_profile_reset(kc);
+      }
+    for (size_t s = 0; s < S; ++s)
+      if (rcs[s] != BPP_OK) {
+        ctx->err = kids[s]->err;
+        return rcs[s];
+      }
+  }
   par::for_each(count, [&](size_t p) {
     serialize(C, Ps[p], proofs_out + p * pl);
     for (uint32_t j = 0; j < C.m; ++j) memcpy(V_out + (p * C.m + j) * 32, Ps[p].V[j].data(), 32);

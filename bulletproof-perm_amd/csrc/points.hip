@@ -74,8 +74,7 @@ int points_compress_p3(bpp_ctx* ctx, const uint32_t* d_p3, size_t n, uint8_t* ou
     hipLaunchKernelGGL(k_compress_p3, dim3(grid_for(n, 64)), dim3(64), 0, ctx->stream, d_p3, n, (uint32_t*)d_out);
   }
   BPP_TRY(ctx_check_launch(ctx, "k_compress_p3"));
-  BPP_HIP(hipMemcpyAsync(out_host, d_out, n * 32, hipMemcpyDeviceToHost, ctx->stream));
-  BPP_HIP(hipStreamSynchronize(ctx->stream));
+  BPP_TRY(ctx_d2h(ctx, out_host, d_out, n * 32));
   return BPP_OK;
 }
 

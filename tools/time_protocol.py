@@ -35,29 +35,31 @@ for mode in ("0", "1", None):
     assert pr.verify_batch(proofs, Vs)
     print(f"batch verify 64: {(time.perf_counter() - t) * 1e3:.2f} ms total")
 os.environ.pop("BPP_MSM_FB", None)
-for B in (16, 128, 512):
+for B, S in ((16, "1"), (128, "1"), (256, "1"), (512, "1")):
+    os.environ["BPP_PROVE_STREAMS"] = S
+    print(f"-- streams {S}")
     pr.prove_batch(list(range(B)))
+    tp, tv = [], []
+    for rep in range(3):
+        t = time.perf_counter()
+        proofs, Vs = pr.prove_batch(list(range(1000 * (rep + 1), 1000 * (rep + 1) + B)))
+        tp.append(time.perf_counter() - t)
+        t = time.perf_counter()
+        assert pr.verify_batch(proofs, Vs)
+        tv.append(time.perf_counter() - t)
+    print(f"prove_batch {B}: {[round(x * 1e3, 2) for x in tp]} ms  -> {B / min(tp):.0f} proofs/s (best)")
+    print(f"verify_batch {B}: {[round(x * 1e3, 2) for x in tv]} ms  -> {B / min(tv):.0f} proofs/s (best)")
+for S, B in (("1", 128), ("1", 512), ("2", 512)):
+    os.environ["BPP_PROVE_STREAMS"] = S
+    pr.prove_batch(list(range(B)))
+    ctx.profile(True)
+    ctx.profile_reset()
     t = time.perf_counter()
-    proofs, Vs = pr.prove_batch(list(range(1000, 1000 + B)))
-    dt = time.perf_counter() - t
-    print(f"prove_batch {B}: {dt * 1e3:.2f} ms  -> {B / dt:.0f} proofs/s")
-    t = time.perf_counter()
-    assert pr.verify_batch(proofs, Vs)
-    dt = time.perf_counter() - t
-    print(f"verify_batch {B}: {dt * 1e3:.2f} ms  -> {B / dt:.0f} proofs/s")
-ctx.profile(True)
-ctx.profile_reset()
-pr.prove_batch(list(range(128)))
-print("profile of prove_batch(128):")
-for st in ("fbw_tables", "pedersen", "msm_count", "msm_scatter", "msm_accumulate", "msm_fixup", "msm_reduce",
-           "msm_scan", "msm_horner", "compress", "ipa_terms", "ipa_fold"):
-    ms, k = ctx.profile_get(st)
-    print(f"  {st:16s} {ms:8.3f} ms over {k} launches")
-ctx.profile(True)
-ctx.profile_reset()
-pr.prove(1)
-for st in ("fbw_tables", "pedersen", "msm_count", "msm_scatter", "msm_accumulate", "msm_fixup", "msm_reduce", "msm_scan",
-           "msm_horner", "ipa_terms", "ipa_fold"):
-    ms, k = ctx.profile_get(st)
-    print(f"  {st:16s} {ms:8.3f} ms over {k} launches")
-ctx.profile(False)
+    pr.prove_batch(list(range(B)))
+    print(f"profile of prove_batch({B}), streams {S}: wall {(time.perf_counter() - t) * 1e3:.2f} ms")
+    for st in ("pedersen", "msm_count", "msm_scatter", "msm_accumulate", "msm_fixup", "msm_reduce", "msm_scan",
+               "compress", "ipa_terms", "ipa_fold", "ipa_msm", "ipa_host", "pb_rng", "pb_pedersen_V",
+               "pb_pedersen_Vx_witness", "pb_msm_AI_AO_S", "pb_host_poly", "pb_pedersen_T_lr", "pb_ipa"):
+        ms, k = ctx.profile_get(st)
+        print(f"  {st:22s} {ms:8.3f} ms over {k} launches")
+    ctx.profile(False)

@@ -3,7 +3,11 @@
 #pragma once
 #include "ge25519.cuh"
 
-#define MSM_NIELS_WORDS 24  // 96 bytes per table point
+// A table point is 96 bytes of affine Niels (y+x, y-x, 2dxy) stored at a
+// 128-byte stride: one 128-B memory request per gather instead of 1.5 on
+// average for packed 96-B rows (tools/ubench/gather_cal: 184 B fetched per
+// packed row).
+#define MSM_NIELS_WORDS 32
 
 FE_INLINE ge_niels load_niels(const uint32_t* __restrict__ tbl, uint32_t idx) {
   const uint4* p = reinterpret_cast<const uint4*>(tbl + (size_t)idx * MSM_NIELS_WORDS);

@@ -14,7 +14,7 @@ struct bpp_gens {
   size_t n = 0;
   uint32_t* d_tbl = nullptr;  // (2n+2) affine Niels: G[0..n) H[n..2n) B[2n] Bb[2n+1]
   uint32_t* d_fb = nullptr;   // fixed-base tables for B and Bb: 2 x 64 x 8 Niels
-  // window tables of every generator (FBW_W x 96 B each), built on first use
+  // window tables of every generator (FBW_W x 128 B each), built on first use
   mutable uint32_t* d_wt = nullptr;
   uint32_t gidx(size_t i) const { return (uint32_t)i; }
   uint32_t hidx(size_t i) const { return (uint32_t)(n + i); }

@@ -4,6 +4,7 @@
 
 #include "ctx.h"
 #include "gens.h"
+#include "ge_io.cuh"
 #include "ipa.h"
 #include "msm_engine.h"
 
@@ -21,7 +22,7 @@ static unsigned grid_for(size_t n, unsigned t) { return (unsigned)((n + t - 1) /
 // on any invalid encoding.
 int decompress_ws(bpp_ctx* ctx, const uint8_t* enc, size_t count, const char* name, uint32_t** d_out) {
   void *d_tbl, *d_enc, *d_bad;
-  BPP_TRY(ctx_ws(ctx, name, (count ? count : 1) * 96, &d_tbl));
+  BPP_TRY(ctx_ws(ctx, name, (count ? count : 1) * MSM_NIELS_WORDS * 4, &d_tbl));
   *d_out = (uint32_t*)d_tbl;
   if (!count) return BPP_OK;
   BPP_TRY(ctx_ws(ctx, "dws_enc", count * 32, &d_enc));

@@ -162,7 +162,15 @@ __global__ void __launch_bounds__(256) k_msm_accumulate(const uint32_t* __restri
   uint32_t bstart = boff[b], bend = boff[b + 1];
   bool first = true;
   ge_p3 acc = ge_identity();
+  // entries are read 4 at a time (one 16-B load; K is a multiple of 4 and
+  // the array is padded): a lane's chunk is contiguous, so per-entry 4-B
+  // loads touch the same 128-B line K times across a long loop and
+  // re-fetch it once the table gathers have evicted it
+  uint4 e4 = make_uint4(0, 0, 0, 0);
   for (uint32_t i = i0; i < i1; ++i) {
+    if (((i - i0) & 3u) == 0) e4 = *reinterpret_cast<const uint4*>(entries + i);
+    const uint32_t q = (i - i0) & 3u;
+    const uint32_t e = q == 0 ? e4.x : q == 1 ? e4.y : q == 2 ? e4.z : e4.w;
     if (i == bend) {  // close the run of bucket b
       if (bstart >= i0) store_p3(bsum, b, acc);  // whole bucket inside the chunk
       else store_p3(head, l, acc);               // first run, bucket started earlier
@@ -172,7 +180,7 @@ __global__ void __launch_bounds__(256) k_msm_accumulate(const uint32_t* __restri
       bend = boff[b + 1];
       acc = ge_identity();
     }
-    acc = ge_madd(acc, fetch_entry(tbl, tbl1, n0, entries[i]));
+    acc = ge_madd(acc, fetch_entry(tbl, tbl1, n0, e));
   }
   // last run [max(bstart, i0), i1)
   if (bstart >= i0 && bend <= i1) store_p3(bsum, b, acc);

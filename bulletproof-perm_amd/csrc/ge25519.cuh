@@ -198,12 +198,9 @@ FE_INLINE bool fe_sqrt_ratio_m1(const fe& u, const fe& v, fe& r_out) {
 
 // Decode 32 bytes (as 8 LE words).  Returns false on invalid encoding.
 FE_INLINE bool ge_ristretto_decode(const uint32_t w[8], ge_p3& out) {
-  fe s = fe_load_words(w);
   // canonical: s < p and s non-negative (even)
-  fe sc = fe_canon(s);
-  bool canonical = true;
-  _Pragma("unroll") for (int i = 0; i < 8; ++i) canonical &= (sc.v[i] == s.v[i]);
-  if (!canonical || (s.v[0] & 1)) return false;
+  if (!fe_words_canonical(w) || (w[0] & 1)) return false;
+  fe s = fe_load_words(w);
   fe ss = fe_sq(s);
   fe u1 = fe_sub(fe_one(), ss);
   fe u2 = fe_add(fe_one(), ss);
@@ -272,9 +269,14 @@ FE_INLINE ge_p3 ge_elligator(const fe& t) {
 
 // dalek RistrettoPoint::from_uniform_bytes (64 bytes as 16 LE words)
 FE_INLINE ge_p3 ge_from_uniform(const uint32_t w[16]) {
-  fe t1 = fe_load_words(w);
-  fe t2 = fe_load_words(w + 8);
-  t1.v[7] &= 0x7fffffffu;
-  t2.v[7] &= 0x7fffffffu;
+  uint32_t a[8], b[8];  // bit 255 of each half is dropped
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) {
+    a[i] = w[i];
+    b[i] = w[8 + i];
+  }
+  a[7] &= 0x7fffffffu;
+  b[7] &= 0x7fffffffu;
+  fe t1 = fe_load_words(a);
+  fe t2 = fe_load_words(b);
   return ge_add(ge_elligator(t1), ge_elligator(t2));
 }

@@ -85,7 +85,7 @@ __global__ void __launch_bounds__(256) k_pedersen(const uint32_t* __restrict__ f
   }
   _Pragma("unroll") for (int off = 1; off < PED_G; off <<= 1) {
     ge_p3 o;
-    _Pragma("unroll") for (int i = 0; i < 8; ++i) {
+    _Pragma("unroll") for (int i = 0; i < FE_LIMBS; ++i) {
       o.X.v[i] = __shfl_xor(acc.X.v[i], off, 64);
       o.Y.v[i] = __shfl_xor(acc.Y.v[i], off, 64);
       o.Z.v[i] = __shfl_xor(acc.Z.v[i], off, 64);
@@ -131,7 +131,7 @@ int pedersen_dev(bpp_ctx* ctx, const bpp_gens* g, const uint32_t* d_v, const uin
   uint32_t* p3 = d_out_p3;
   if (!p3) {
     void* w = nullptr;
-    BPP_TRY(ctx_ws(ctx, "ped_p3", m * 128, &w));
+    BPP_TRY(ctx_ws(ctx, "ped_p3", m * P3_BYTES, &w));
     p3 = (uint32_t*)w;
   }
   {

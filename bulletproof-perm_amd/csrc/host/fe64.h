@@ -249,6 +249,30 @@ static inline bool decode(ge& out, const uint8_t in[32]) {
   return true;
 }
 
+// Device element: 10 u32 limbs at bit offsets ceil(25.5 i) (limbs may
+// exceed their nominal width; see csrc/fe25519.cuh) -> loose fe.
+static inline fe fe_from_dev(const uint32_t w[10]) {
+  static const int OFF[10] = {0, 26, 51, 77, 102, 128, 153, 179, 204, 230};
+  uint64_t t[5] = {0, 0, 0, 0, 0};
+  for (int i = 0; i < 10; ++i) {
+    const int q = OFF[i] >> 6, s = OFF[i] & 63;
+    const u128 x = (u128)w[i] << s;
+    u128 c = (u128)t[q] + (uint64_t)x;
+    t[q] = (uint64_t)c;
+    c = (u128)t[q + 1] + (uint64_t)(x >> 64) + (uint64_t)(c >> 64);
+    t[q + 1] = (uint64_t)c;
+    for (int k = q + 2; k < 5 && (c >> 64); ++k) {
+      c = (u128)t[k] + (uint64_t)(c >> 64);
+      t[k] = (uint64_t)c;
+    }
+  }
+  return fe_fold(fe{{t[0], t[1], t[2], t[3]}}, t[4]);
+}
+// device extended point (40 words, csrc/layout.h P3_WORDS) -> host point
+static inline ge ge_from_dev(const uint32_t* w) {
+  return ge{fe_from_dev(w), fe_from_dev(w + 10), fe_from_dev(w + 20), fe_from_dev(w + 30)};
+}
+
 static inline ge ge_from_words(const uint32_t w[32]) {
   return ge{fe_from_words(w), fe_from_words(w + 8), fe_from_words(w + 16), fe_from_words(w + 24)};
 }

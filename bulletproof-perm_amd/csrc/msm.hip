@@ -62,8 +62,8 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
   BPP_TRY(ctx_ws(ctx, "msm_cur", NB * 4, &cur));
   BPP_TRY(ctx_ws(ctx, "msm_boff", (NB + 1) * 4, &boff));
   BPP_TRY(ctx_ws(ctx, "msm_entries", (size_t)T * Wn * 4 + 16, &entries));  // +16: 16-B reads past the end
-  BPP_TRY(ctx_ws(ctx, "msm_bsum", NB * 128, &bsum));
-  BPP_TRY(ctx_ws(ctx, "msm_wsum", nseg * 128, &wsum));
+  BPP_TRY(ctx_ws(ctx, "msm_bsum", NB * P3_BYTES, &bsum));
+  BPP_TRY(ctx_ws(ctx, "msm_wsum", nseg * P3_BYTES, &wsum));
   BPP_HIP(hipMemsetAsync(cnt, 0, (NB + 1) * 4, ctx->stream));
   BPP_HIP(hipMemsetAsync(cur, 0, NB * 4, ctx->stream));
   const bool lds_sort = !fb && (M == 1) && (c <= 16) && (T >= 16384);
@@ -127,8 +127,8 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
     while (K > 4 && (E_max / K) < 256u * 1024u) K >>= 1;
     const size_t lanes = (E_max + K - 1) / K + 1;
     void *head, *tail;
-    BPP_TRY(ctx_ws(ctx, "msm_head", lanes * 128, &head));
-    BPP_TRY(ctx_ws(ctx, "msm_tail", lanes * 128, &tail));
+    BPP_TRY(ctx_ws(ctx, "msm_head", lanes * P3_BYTES, &head));
+    BPP_TRY(ctx_ws(ctx, "msm_tail", lanes * P3_BYTES, &tail));
     {
       ProfScope ps(ctx, "msm_accumulate");
       hipLaunchKernelGGL(k_msm_accumulate, dim3(grid_for(lanes, 256)), dim3(256), 0, ctx->stream, d_tbl, d_tbl1, n0,
@@ -147,7 +147,7 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
     const uint32_t L = g.B >= 512 ? 8 : (g.B >= 64 ? 4 : (g.B >= 8 ? 2 : 1));
     const uint32_t BPS = (g.B + RED_T * L - 1) / (RED_T * L);
     void* part = wsum;  // one block per segment: its partial is the sum
-    if (BPS > 1) BPP_TRY(ctx_ws(ctx, "msm_rpart", nseg * BPS * 128, &part));
+    if (BPS > 1) BPP_TRY(ctx_ws(ctx, "msm_rpart", nseg * BPS * P3_BYTES, &part));
     ProfScope ps(ctx, "msm_reduce");
     hipLaunchKernelGGL(k_msm_reduce_partial, dim3((unsigned)(nseg * BPS)), dim3(RED_T), 0, ctx->stream,
                        (const uint32_t*)bsum, g, L, BPS, (uint32_t*)part);
@@ -163,10 +163,10 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
 // Host Horner: sum_j 2^(c*(wb+j)) * ws[j], j < Wn.
 static h25519::ge horner_host(const uint32_t* ws_words, uint32_t Wn, uint32_t c, uint32_t wb) {
   using namespace h25519;
-  ge acc = ge_from_words(ws_words + (size_t)(Wn - 1) * 32);
+  ge acc = ge_from_dev(ws_words + (size_t)(Wn - 1) * P3_WORDS);
   for (int j = (int)Wn - 2; j >= 0; --j) {
     for (uint32_t k = 0; k < c; ++k) acc = ge_dbl(acc);
-    acc = ge_add(acc, ge_from_words(ws_words + (size_t)j * 32));
+    acc = ge_add(acc, ge_from_dev(ws_words + (size_t)j * P3_WORDS));
   }
   for (uint32_t k = 0; k < c * wb; ++k) acc = ge_dbl(acc);
   return acc;
@@ -182,8 +182,8 @@ int msm_single_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx,
   uint32_t* d_ws = nullptr;
   BPP_TRY(msm_engine(ctx, d_scal, d_pidx, nullptr, 1, (uint32_t)n, c, wb, Wn, d_tbl, &d_ws));
   void* h = nullptr;
-  BPP_TRY(ctx_pinned(ctx, (size_t)Wn * 128, &h));
-  BPP_HIP(hipMemcpyAsync(h, d_ws, (size_t)Wn * 128, hipMemcpyDeviceToHost, ctx->stream));
+  BPP_TRY(ctx_pinned(ctx, (size_t)Wn * P3_BYTES, &h));
+  BPP_HIP(hipMemcpyAsync(h, d_ws, (size_t)Wn * P3_BYTES, hipMemcpyDeviceToHost, ctx->stream));
   BPP_HIP(hipStreamSynchronize(ctx->stream));
   *out = horner_host((const uint32_t*)h, Wn, c, wb);
   return BPP_OK;
@@ -284,7 +284,7 @@ int bpp_msm_batch(bpp_ctx* ctx, size_t count, const uint64_t* offsets, const uin
   void *d_idx, *d_off, *d_res;
   BPP_TRY(ctx_ws(ctx, "msmb_idx", T * 4 + 4, &d_idx));
   BPP_TRY(ctx_ws(ctx, "msmb_off", (count + 1) * 4, &d_off));
-  BPP_TRY(ctx_ws(ctx, "msmb_res", count * 128, &d_res));
+  BPP_TRY(ctx_ws(ctx, "msmb_res", count * P3_BYTES, &d_res));
   std::vector<uint32_t> off32(count + 1);
   for (size_t j = 0; j <= count; ++j) off32[j] = (uint32_t)offsets[j];
   if (T) BPP_HIP(hipMemcpyAsync(d_idx, point_idx, T * 4, hipMemcpyHostToDevice, ctx->stream));
@@ -407,10 +407,10 @@ int msm_multi(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, cons
   uint32_t* d_ws = nullptr;
   BPP_TRY(msm_multi_fb_dev(ctx, d_scal, d_pidx, off, pts, &d_ws));
   void* h = nullptr;
-  BPP_TRY(ctx_pinned(ctx, (size_t)M * 128, &h));
-  BPP_HIP(hipMemcpyAsync(h, d_ws, (size_t)M * 128, hipMemcpyDeviceToHost, ctx->stream));
+  BPP_TRY(ctx_pinned(ctx, (size_t)M * P3_BYTES, &h));
+  BPP_HIP(hipMemcpyAsync(h, d_ws, (size_t)M * P3_BYTES, hipMemcpyDeviceToHost, ctx->stream));
   BPP_HIP(hipStreamSynchronize(ctx->stream));
-  for (uint32_t m = 0; m < M; ++m) out[m] = h25519::ge_from_words((const uint32_t*)h + (size_t)m * 32);
+  for (uint32_t m = 0; m < M; ++m) out[m] = h25519::ge_from_dev((const uint32_t*)h + (size_t)m * P3_WORDS);
   return BPP_OK;
 }
 
@@ -450,10 +450,10 @@ int msm_multi(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, cons
   BPP_TRY(msm_engine(ctx, d_scal, d_pidx, (const uint32_t*)d_off, M, T, c, 0, W, d_tbl, &d_ws, d_tbl1, n0));
   if (M <= 8) {
     void* h = nullptr;
-    BPP_TRY(ctx_pinned(ctx, (size_t)M * W * 128, &h));
-    BPP_HIP(hipMemcpyAsync(h, d_ws, (size_t)M * W * 128, hipMemcpyDeviceToHost, ctx->stream));
+    BPP_TRY(ctx_pinned(ctx, (size_t)M * W * P3_BYTES, &h));
+    BPP_HIP(hipMemcpyAsync(h, d_ws, (size_t)M * W * P3_BYTES, hipMemcpyDeviceToHost, ctx->stream));
     BPP_HIP(hipStreamSynchronize(ctx->stream));
-    for (uint32_t m = 0; m < M; ++m) out[m] = horner_host((const uint32_t*)h + (size_t)m * W * 32, W, c, 0);
+    for (uint32_t m = 0; m < M; ++m) out[m] = horner_host((const uint32_t*)h + (size_t)m * W * P3_WORDS, W, c, 0);
     return BPP_OK;
   }
   MsmGeom g;
@@ -466,15 +466,15 @@ int msm_multi(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, cons
   g.B = 1u << (c - 1);
   g.fb = 0;
   void* d_res = nullptr;
-  BPP_TRY(ctx_ws(ctx, "multi_res", (size_t)M * 128, &d_res));
+  BPP_TRY(ctx_ws(ctx, "multi_res", (size_t)M * P3_BYTES, &d_res));
   {
     ProfScope ps(ctx, "msm_horner");
     hipLaunchKernelGGL(k_msm_horner, dim3(grid_for(M, 64)), dim3(64), 0, ctx->stream, (const uint32_t*)d_ws, g,
                        (uint32_t*)d_res);
   }
   BPP_TRY(ctx_check_launch(ctx, "k_msm_horner"));
-  std::vector<uint32_t> h((size_t)M * 32);
-  BPP_TRY(ctx_d2h(ctx, h.data(), d_res, (size_t)M * 128));
-  for (uint32_t m = 0; m < M; ++m) out[m] = h25519::ge_from_words(h.data() + (size_t)m * 32);
+  std::vector<uint32_t> h((size_t)M * P3_WORDS);
+  BPP_TRY(ctx_d2h(ctx, h.data(), d_res, (size_t)M * P3_BYTES));
+  for (uint32_t m = 0; m < M; ++m) out[m] = h25519::ge_from_dev(h.data() + (size_t)m * P3_WORDS);
   return BPP_OK;
 }

@@ -227,7 +227,7 @@ FE_INLINE ge_p3 lds_tree_sum(uint32_t* lds, ge_p3 v) {
 
 __global__ void __launch_bounds__(RED_T) k_msm_reduce_partial(const uint32_t* __restrict__ bsum, MsmGeom g,
                                                              uint32_t L, uint32_t BPS, uint32_t* __restrict__ part) {
-  __shared__ uint32_t lds[RED_T * 32];
+  __shared__ uint32_t lds[RED_T * P3_WORDS];
   const uint32_t seg = blockIdx.x / BPS, j = blockIdx.x % BPS;
   const uint32_t lo = (j * RED_T + threadIdx.x) * L;
   const uint32_t hi = min(lo + L, g.B);
@@ -253,7 +253,7 @@ __global__ void __launch_bounds__(RED_T) k_msm_reduce_partial(const uint32_t* __
 
 __global__ void __launch_bounds__(RED_T) k_msm_reduce_final(const uint32_t* __restrict__ part, uint32_t BPS,
                                                            uint32_t* __restrict__ wsum) {
-  __shared__ uint32_t lds[RED_T * 32];
+  __shared__ uint32_t lds[RED_T * P3_WORDS];
   const uint32_t seg = blockIdx.x;
   ge_p3 acc = ge_identity();
   for (uint32_t j = threadIdx.x; j < BPS; j += RED_T) acc = ge_add(acc, load_p3(part, (size_t)seg * BPS + j));

@@ -9,7 +9,9 @@ import ctypes as C
 import os
 from pathlib import Path
 
-LIB_PATH = Path(__file__).resolve().parent / "libbpperm.so"
+# BPP_LIB selects an alternative build (A/B kernel experiments, build.py --variant)
+LIB_PATH = Path(os.environ["BPP_LIB"]) if os.environ.get("BPP_LIB") else \
+    Path(__file__).resolve().parent / "libbpperm.so"
 
 BPP_OK = 0
 ERRORS = {

@@ -26,8 +26,8 @@ def sources():
     return sorted(list(CSRC.glob("*.hip")) + list(CSRC.glob("host/*.cpp")))
 
 
-def _compile(src: Path, flags) -> Path:
-    obj = BUILD / (src.relative_to(CSRC).as_posix().replace("/", "_") + ".o")
+def _compile(src: Path, flags, bdir: Path = BUILD) -> Path:
+    obj = bdir / (src.relative_to(CSRC).as_posix().replace("/", "_") + ".o")
     deps = [src] + list(CSRC.glob("*.cuh")) + list(CSRC.glob("*.h")) + list(CSRC.glob("host/*.h")) + \
         [ROOT.parent / "include" / "bpperm.h"]
     if obj.exists() and obj.stat().st_mtime >= max(d.stat().st_mtime for d in deps):
@@ -40,22 +40,34 @@ def _compile(src: Path, flags) -> Path:
     return obj
 
 
-def build(debug: bool = False, jobs: int | None = None) -> Path:
-    BUILD.mkdir(exist_ok=True)
+def build(debug: bool = False, jobs: int | None = None, variant: str = "", defines=()) -> Path:
+    """variant: build an A/B copy with extra -D defines into
+    build/<variant>/ and bpperm/variants/libbpperm_<variant>.so (select it
+    with BPP_LIB=...)."""
+    bdir = BUILD / variant if variant else BUILD
+    out = ROOT / "bpperm" / "variants" / f"libbpperm_{variant}.so" if variant else OUT
+    bdir.mkdir(parents=True, exist_ok=True)
+    out.parent.mkdir(exist_ok=True)
     flags = ["-O1", "-g"] if debug else ["-O3"]
-    flags += ["-Wno-unused-result", "-Wno-pass-failed", "-pthread"]
+    flags += ["-Wno-unused-result", "-Wno-pass-failed", "-pthread"] + [f"-D{d}" for d in defines]
     srcs = sources()
     jobs = jobs or min(8, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, flags), srcs))
-    if OUT.exists() and OUT.stat().st_mtime >= max(o.stat().st_mtime for o in objs):
-        return OUT
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", str(OUT), *map(str, objs)]
+        objs = list(ex.map(lambda s: _compile(s, flags, bdir), srcs))
+    if out.exists() and out.stat().st_mtime >= max(o.stat().st_mtime for o in objs):
+        return out
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", str(out), *map(str, objs)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
-    return OUT
+    return out
 
 
 if __name__ == "__main__":
-    print(build(debug="--debug" in sys.argv))
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--debug", action="store_true")
+    ap.add_argument("--variant", default="")
+    ap.add_argument("-D", dest="defines", action="append", default=[])
+    a = ap.parse_args()
+    print(build(debug=a.debug, variant=a.variant, defines=a.defines))

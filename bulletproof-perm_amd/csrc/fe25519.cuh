@@ -29,6 +29,20 @@ struct fe {
 };
 
 #define MAD64(a, b, c) ((uint64_t)(uint32_t)(a) * (uint64_t)(uint32_t)(b) + (uint64_t)(c))
+#ifdef FE_MADC_ASM
+// Opaque v_mad_u64_u32 for the product-column chains (see tools/gen_fe10.py):
+// +5-7 % multiply throughput at 16 waves/SIMD, but the chain needs s_nop
+// wait states and a lone wave gets 25 % slower (tools/ubench/fe10bench).
+// Off by default: the compiler re-associates each column instead.
+FE_INLINE uint64_t fe_madc(uint32_t a, uint32_t b, uint64_t c) {
+  uint64_t d, unused;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(unused) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+#define MADC(a, b, c) fe_madc((a), (b), (c))
+#else
+#define MADC(a, b, c) MAD64(a, b, c)
+#endif
 #define FE_M26 0x3ffffffu
 #define FE_M25 0x1ffffffu
 
@@ -71,6 +85,22 @@ FE_INLINE fe fe_sub(const fe& a, const fe& b) {
 }
 
 FE_INLINE fe fe_neg(const fe& a) { return fe_sub(fe_zero(), a); }
+
+// Non-carrying forms for the point formulas, where a result only feeds
+// multiplier operands (limit 2^27.6): a, b tight ->
+//   fe_add_nc < 2^27 + 2^19,  fe_sub_nc < 2^27 + 2^26 + 2^18 (= 2^27.59).
+// Neither result may be the subtrahend of a later fe_sub / fe_sub_nc.
+FE_INLINE fe fe_add_nc(const fe& a, const fe& b) {
+  fe r;
+  _Pragma("unroll") for (int i = 0; i < FE_LIMBS; ++i) r.v[i] = a.v[i] + b.v[i];
+  return r;
+}
+FE_INLINE fe fe_sub_nc(const fe& a, const fe& b) {
+  fe r;
+  r.v[0] = a.v[0] + 0x7ffffdau - b.v[0];
+  _Pragma("unroll") for (int i = 1; i < FE_LIMBS; ++i) r.v[i] = a.v[i] + ((i & 1) ? 0x3fffffeu : 0x7fffffeu) - b.v[i];
+  return r;
+}
 
 #include "fe10_ops.inc"
 

@@ -41,16 +41,18 @@ FE_INLINE ge_niels ge_niels_identity() {
   return n;
 }
 
-// p + q, q affine Niels: 7M.
+// p + q, q affine Niels: 7M.  Sums feeding only multipliers stay
+// uncarried (fe_add_nc / fe_sub_nc bounds in fe25519.cuh); F = D - C has a
+// non-tight minuend and is carried.  Inputs and outputs are tight.
 FE_INLINE ge_p3 ge_madd(const ge_p3& p, const ge_niels& q) {
-  fe A = fe_mul(fe_sub(p.Y, p.X), q.ymx);
-  fe B = fe_mul(fe_add(p.Y, p.X), q.ypx);
+  fe A = fe_mul(fe_sub_nc(p.Y, p.X), q.ymx);
+  fe B = fe_mul(fe_add_nc(p.Y, p.X), q.ypx);
   fe C = fe_mul(p.T, q.xy2d);
-  fe D = fe_add(p.Z, p.Z);
-  fe E = fe_sub(B, A);
+  fe D = fe_add_nc(p.Z, p.Z);
+  fe E = fe_sub_nc(B, A);
   fe F = fe_sub(D, C);
-  fe G = fe_add(D, C);
-  fe H = fe_add(B, A);
+  fe G = fe_add_nc(D, C);
+  fe H = fe_add_nc(B, A);
   ge_p3 r;
   r.X = fe_mul(E, F);
   r.Y = fe_mul(G, H);
@@ -61,14 +63,14 @@ FE_INLINE ge_p3 ge_madd(const ge_p3& p, const ge_niels& q) {
 
 // p - q, q affine Niels (-q = (y-x, y+x, -2dxy)): 7M.
 FE_INLINE ge_p3 ge_msub(const ge_p3& p, const ge_niels& q) {
-  fe A = fe_mul(fe_sub(p.Y, p.X), q.ypx);
-  fe B = fe_mul(fe_add(p.Y, p.X), q.ymx);
+  fe A = fe_mul(fe_sub_nc(p.Y, p.X), q.ypx);
+  fe B = fe_mul(fe_add_nc(p.Y, p.X), q.ymx);
   fe C = fe_mul(p.T, q.xy2d);
-  fe D = fe_add(p.Z, p.Z);
-  fe E = fe_sub(B, A);
-  fe F = fe_add(D, C);
+  fe D = fe_add_nc(p.Z, p.Z);
+  fe E = fe_sub_nc(B, A);
+  fe F = fe_add_nc(D, C);
   fe G = fe_sub(D, C);
-  fe H = fe_add(B, A);
+  fe H = fe_add_nc(B, A);
   ge_p3 r;
   r.X = fe_mul(E, F);
   r.Y = fe_mul(G, H);
@@ -85,10 +87,11 @@ FE_INLINE ge_niels ge_niels_neg(const ge_niels& q) {
   return r;
 }
 
+// YpX / YmX only ever feed multipliers: left uncarried.
 FE_INLINE ge_cached ge_to_cached(const ge_p3& p) {
   ge_cached c;
-  c.YpX = fe_add(p.Y, p.X);
-  c.YmX = fe_sub(p.Y, p.X);
+  c.YpX = fe_add_nc(p.Y, p.X);
+  c.YmX = fe_sub_nc(p.Y, p.X);
   c.Z = p.Z;
   c.T2d = fe_mul(p.T, fe_const(FE_D2));
   return c;
@@ -96,15 +99,15 @@ FE_INLINE ge_cached ge_to_cached(const ge_p3& p) {
 
 // p + q (q projective Niels): 8M.
 FE_INLINE ge_p3 ge_add_cached(const ge_p3& p, const ge_cached& q) {
-  fe A = fe_mul(fe_sub(p.Y, p.X), q.YmX);
-  fe B = fe_mul(fe_add(p.Y, p.X), q.YpX);
+  fe A = fe_mul(fe_sub_nc(p.Y, p.X), q.YmX);
+  fe B = fe_mul(fe_add_nc(p.Y, p.X), q.YpX);
   fe C = fe_mul(p.T, q.T2d);
   fe ZZ = fe_mul(p.Z, q.Z);
-  fe D = fe_add(ZZ, ZZ);
-  fe E = fe_sub(B, A);
+  fe D = fe_add_nc(ZZ, ZZ);
+  fe E = fe_sub_nc(B, A);
   fe F = fe_sub(D, C);
-  fe G = fe_add(D, C);
-  fe H = fe_add(B, A);
+  fe G = fe_add_nc(D, C);
+  fe H = fe_add_nc(B, A);
   ge_p3 r;
   r.X = fe_mul(E, F);
   r.Y = fe_mul(G, H);
@@ -123,15 +126,17 @@ FE_INLINE ge_p3 ge_neg(const ge_p3& p) {
 }
 
 // 2p: 4M + 4S (dalek ProjectivePoint::double -> CompletedPoint -> extended).
+// YY+XX and YY-XX are subtrahends later, so carried; so is cT (its minuend
+// ZZ2 is not tight).
 FE_INLINE ge_p3 ge_dbl(const ge_p3& p) {
   fe XX = fe_sq(p.X);
   fe YY = fe_sq(p.Y);
   fe ZZ = fe_sq(p.Z);
-  fe ZZ2 = fe_add(ZZ, ZZ);
-  fe XpY2 = fe_sq(fe_add(p.X, p.Y));
+  fe ZZ2 = fe_add_nc(ZZ, ZZ);
+  fe XpY2 = fe_sq(fe_add_nc(p.X, p.Y));
   fe YYpXX = fe_add(YY, XX);
   fe YYmXX = fe_sub(YY, XX);
-  fe cX = fe_sub(XpY2, YYpXX);
+  fe cX = fe_sub_nc(XpY2, YYpXX);
   fe cT = fe_sub(ZZ2, YYmXX);
   ge_p3 r;
   r.X = fe_mul(cX, cT);

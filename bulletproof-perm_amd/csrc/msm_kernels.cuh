@@ -120,6 +120,12 @@ __global__ void k_msm_scatter(const uint32_t* __restrict__ scalars, const uint32
   });
 }
 
+#ifdef ACC_WAVES5
+#define ACC_ATTR __attribute__((amdgpu_waves_per_eu(5, 8)))
+#else
+#define ACC_ATTR
+#endif
+
 // Largest b with boff[b] <= i (boff non-decreasing, boff[0] = 0, i < boff[nb]).
 FE_INLINE uint32_t bucket_of(const uint32_t* __restrict__ boff, uint32_t nb, uint32_t i) {
   uint32_t lo = 0, hi = nb;  // boff[lo] <= i < boff[hi]
@@ -147,7 +153,7 @@ FE_INLINE ge_niels fetch_entry(const uint32_t* __restrict__ tbl, const uint32_t*
 // head[l] / tail[l] and k_msm_fixup adds the pieces.
 // Points with index < n0 come from tbl, the rest from tbl1[idx - n0] (so a
 // proof's own points can join the resident generators without a copy).
-__global__ void __launch_bounds__(256) k_msm_accumulate(const uint32_t* __restrict__ tbl,
+__global__ void __launch_bounds__(256) ACC_ATTR k_msm_accumulate(const uint32_t* __restrict__ tbl,
                                                        const uint32_t* __restrict__ tbl1, uint32_t n0,
                                                        const uint32_t* __restrict__ entries,
                                                        const uint32_t* __restrict__ boff, uint32_t nbuckets,

@@ -13,6 +13,16 @@ struct fe {
   uint32_t v[10];
 };
 #define MAD64(a, b, c) ((uint64_t)(uint32_t)(a) * (uint64_t)(uint32_t)(b) + (uint64_t)(c))
+#ifdef PLAIN
+#define MADC(a, b, c) MAD64(a, b, c)
+#else
+FE_INLINE uint64_t fe_madc(uint32_t a, uint32_t b, uint64_t c) {
+  uint64_t d, unused;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(unused) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+#define MADC(a, b, c) fe_madc((a), (b), (c))
+#endif
 #include "../../bulletproof-perm_amd/csrc/fe10_ops.inc"
 __device__ __constant__ const int OFF[10] = {0, 26, 51, 77, 102, 128, 153, 179, 204, 230};
 FE_INLINE fe from_words(const ::fe& a) {  // loose 8x32 (< 2^256) -> 10 limbs

@@ -64,10 +64,52 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
   BPP_TRY(ctx_ws(ctx, "msm_entries", (size_t)T * Wn * 4 + 16, &entries));  // +16: 16-B reads past the end
   BPP_TRY(ctx_ws(ctx, "msm_bsum", NB * P3_BYTES, &bsum));
   BPP_TRY(ctx_ws(ctx, "msm_wsum", nseg * P3_BYTES, &wsum));
-  BPP_HIP(hipMemsetAsync(cnt, 0, (NB + 1) * 4, ctx->stream));
-  BPP_HIP(hipMemsetAsync(cur, 0, NB * 4, ctx->stream));
-  const bool lds_sort = !fb && (M == 1) && (c <= 16) && (T >= 16384);
-  if (lds_sort && T) {
+  // (tmpA packs the point index in 24 bits)
+  const bool radix_sort = !fb && (M == 1) && (c >= 12) && (c <= 16) && (T >= 16384) && (T <= (1u << 24)) &&
+                          (!d_pidx) && !getenv("BPP_MSM_LDS_SORT");
+  const bool lds_sort = !fb && !radix_sort && (M == 1) && (c <= 16) && (T >= 16384);
+  if (!radix_sort) {
+    BPP_HIP(hipMemsetAsync(cnt, 0, (NB + 1) * 4, ctx->stream));
+    BPP_HIP(hipMemsetAsync(cur, 0, NB * 4, ctx->stream));
+  }
+  if (radix_sort) {
+    void *dig, *cntA, *offA, *tmpA;
+    BPP_TRY(ctx_ws(ctx, "msm_dig", (size_t)T * Wn * 4 + 16, &dig));
+    {
+      ProfScope ps(ctx, "msm_digits");
+      hipLaunchKernelGGL(k_msm_digits, dim3(grid_for(T, 256)), dim3(256), 0, ctx->stream, d_scal, g, (uint32_t*)dig);
+    }
+    BPP_TRY(ctx_check_launch(ctx, "k_msm_digits"));
+    const uint32_t chunk = RS_CHUNK;
+    const uint32_t nchunk = (T + chunk - 1) / chunk;
+    const uint32_t NC = g.B >> RS_FINE_BITS;  // <= 256 coarse bins per window
+    const size_t nA = (size_t)Wn * NC * nchunk;
+    BPP_TRY(ctx_ws(ctx, "msm_cntA", (nA + 1) * 4, &cntA));
+    BPP_TRY(ctx_ws(ctx, "msm_offA", (nA + 1) * 4, &offA));
+    BPP_TRY(ctx_ws(ctx, "msm_tmpA", (size_t)T * Wn * 4 + 16, &tmpA));
+    {
+      ProfScope ps(ctx, "msm_count");
+      BPP_HIP(hipMemsetAsync((uint32_t*)cntA + nA, 0, 4, ctx->stream));
+      hipLaunchKernelGGL(k_rsort_count, dim3(Wn * nchunk), dim3(RS_T), 0, ctx->stream, (const uint32_t*)dig, g, chunk,
+                         nchunk, NC, (uint32_t*)cntA);
+    }
+    BPP_TRY(ctx_check_launch(ctx, "k_rsort_count"));
+    {
+      ProfScope ps(ctx, "msm_scan");
+      BPP_TRY(scan_exclusive_u32(ctx, (const uint32_t*)cntA, (uint32_t*)offA, nA + 1));
+    }
+    {
+      ProfScope ps(ctx, "msm_scatter");
+      hipLaunchKernelGGL(k_rsort_scatter, dim3(Wn * nchunk), dim3(RS_T), 0, ctx->stream, (const uint32_t*)dig, d_pidx,
+                         g, nchunk, NC, (const uint32_t*)offA, (uint32_t*)tmpA);
+      hipLaunchKernelGGL(k_rsort_fine, dim3(Wn * NC), dim3(RS_T), 0, ctx->stream, (const uint32_t*)tmpA, nchunk,
+                         (const uint32_t*)offA, (uint32_t*)boff, (uint32_t*)entries);
+      // boff[NB] = number of entries
+      BPP_HIP(hipMemcpyAsync((uint32_t*)boff + NB, (const uint32_t*)offA + nA, 4, hipMemcpyDeviceToDevice,
+                             ctx->stream));
+    }
+    BPP_TRY(ctx_check_launch(ctx, "k_rsort_scatter/fine"));
+  } else if (lds_sort && T) {
     void* dig = nullptr;
     BPP_TRY(ctx_ws(ctx, "msm_dig", (size_t)T * Wn * 4 + 16, &dig));
     {
@@ -125,6 +167,7 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
     const uint32_t E_max = T * Wn;
     uint32_t K = 32;
     while (K > 4 && (E_max / K) < 256u * 1024u) K >>= 1;
+    if (const char* ek = getenv("BPP_MSM_K")) K = std::max<uint32_t>(4, (uint32_t)atoi(ek) & ~3u);
     const size_t lanes = (E_max + K - 1) / K + 1;
     void *head, *tail;
     BPP_TRY(ctx_ws(ctx, "msm_head", lanes * P3_BYTES, &head));

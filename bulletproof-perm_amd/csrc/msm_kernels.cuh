@@ -356,3 +356,167 @@ __global__ void __launch_bounds__(SORT_T) k_msm_scatter_lds(const uint32_t* __re
     entries[pos] = (pidx ? pidx[t] : t) | (code & DIG_SIGN);
   }
 }
+
+// ---------------------------------------------------------------------------
+// Two-pass (MSD) bucket sort for one large MSM, c >= 12.  The one-pass LDS
+// scatter above writes every entry as an isolated 4-B store (2^15 buckets
+// per window, ~1 entry per bucket per block: 9x write amplification
+// measured); here both passes stage in LDS and write runs.
+//   k_rsort_count   per (window, chunk of RS_CHUNK digits): histogram of the
+//                   coarse bin = bucket >> RS_FINE_BITS (<= 256 bins) ->
+//                   cntA[w][bin][chunk]
+//   (exclusive scan of cntA: offA = where each block's run of each bin goes;
+//    bins of a window and windows follow each other, the final order)
+//   k_rsort_scatter coarse scatter of (point idx | fine bits << 24 | sign)
+//   k_rsort_fine    one block per (window, coarse bin): LDS counting sort of
+//                   its segment by the fine bits; writes the final entries
+//                   and the bucket offsets boff of its 128 buckets
+#define RS_FINE_BITS 7
+#define RS_FINE_N (1u << RS_FINE_BITS)
+#define RS_T 256
+#define RS_CHUNK 4096  // digits per block in the coarse passes (LDS staging)
+#define RS_FMASK (0x7fu << 24)
+
+__global__ void __launch_bounds__(RS_T) k_rsort_count(const uint32_t* __restrict__ dig, MsmGeom g, uint32_t chunk,
+                                                     uint32_t nchunk, uint32_t NC, uint32_t* __restrict__ cntA) {
+  __shared__ uint32_t h[256];
+  const uint32_t w = blockIdx.x / nchunk, ch = blockIdx.x % nchunk;
+  for (uint32_t b = threadIdx.x; b < NC; b += RS_T) h[b] = 0;
+  __syncthreads();
+  const uint32_t t0 = ch * chunk, t1 = min(t0 + chunk, g.T);
+  const uint32_t* dw = dig + (size_t)w * g.T;
+  for (uint32_t t = t0 + threadIdx.x; t < t1; t += RS_T) {
+    const uint32_t code = dw[t];
+    if (code != DIG_ZERO) atomicAdd(&h[(code & ~DIG_SIGN) >> RS_FINE_BITS], 1u);
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < NC; b += RS_T) cntA[((size_t)w * NC + b) * nchunk + ch] = h[b];
+}
+
+// In-place exclusive scan of a[0..64 * per) (per <= 4) by wave 0; the
+// caller synchronises.  a[i] <- base + sum(a[0..i)).
+__device__ __forceinline__ void lds_excl_scan_w0(uint32_t* a, uint32_t per, uint32_t base) {
+  if (threadIdx.x >= 64) return;
+  uint32_t v[4], tot = 0;
+  for (uint32_t k = 0; k < per; ++k) {
+    v[k] = a[threadIdx.x * per + k];
+    tot += v[k];
+  }
+  uint32_t inc = tot;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t u = __shfl_up(inc, d, 64);
+    if ((int)threadIdx.x >= d) inc += u;
+  }
+  uint32_t run = base + inc - tot;
+  for (uint32_t k = 0; k < per; ++k) {
+    a[threadIdx.x * per + k] = run;
+    run += v[k];
+  }
+}
+
+// Coarse scatter with block-local staging: entries of the chunk are sorted
+// by coarse bin in LDS, then written out bin-run by bin-run (consecutive
+// lanes -> consecutive addresses).  (idx < 2^24 on this path.)
+__global__ void __launch_bounds__(RS_T) k_rsort_scatter(const uint32_t* __restrict__ dig,
+                                                       const uint32_t* __restrict__ pidx, MsmGeom g, uint32_t nchunk,
+                                                       uint32_t NC, const uint32_t* __restrict__ offA,
+                                                       uint32_t* __restrict__ tmpA) {
+  __shared__ uint32_t cnt[256], loc[256], gofs[256];
+  __shared__ uint32_t stage[RS_CHUNK];
+  __shared__ uint8_t sbin[RS_CHUNK];
+  const uint32_t w = blockIdx.x / nchunk, ch = blockIdx.x % nchunk;
+  for (uint32_t b = threadIdx.x; b < 256; b += RS_T) cnt[b] = 0;
+  __syncthreads();
+  const uint32_t t0 = ch * RS_CHUNK, t1 = min(t0 + RS_CHUNK, g.T);
+  const uint32_t* dw = dig + (size_t)w * g.T;
+  for (uint32_t t = t0 + threadIdx.x; t < t1; t += RS_T) {
+    const uint32_t code = dw[t];
+    if (code != DIG_ZERO) atomicAdd(&cnt[(code & ~DIG_SIGN) >> RS_FINE_BITS], 1u);
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < 256; b += RS_T) {
+    loc[b] = cnt[b];
+    gofs[b] = b < NC ? offA[((size_t)w * NC + b) * nchunk + ch] : 0u;
+  }
+  __syncthreads();
+  lds_excl_scan_w0(loc, 4, 0);
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < 256; b += RS_T) cnt[b] = loc[b];  // cursors
+  __syncthreads();
+  for (uint32_t t = t0 + threadIdx.x; t < t1; t += RS_T) {
+    const uint32_t code = dw[t];
+    if (code == DIG_ZERO) continue;
+    const uint32_t b = code & ~DIG_SIGN, bin = b >> RS_FINE_BITS;
+    const uint32_t p = atomicAdd(&cnt[bin], 1u);
+    stage[p] = (pidx ? pidx[t] : t) | ((b & (RS_FINE_N - 1)) << 24) | (code & DIG_SIGN);
+    sbin[p] = (uint8_t)bin;
+  }
+  __syncthreads();
+  const uint32_t n = cnt[255];  // end of the last bin = entries in this chunk
+  for (uint32_t j = threadIdx.x; j < n; j += RS_T) {
+    const uint32_t bin = sbin[j];
+    tmpA[gofs[bin] + j - loc[bin]] = stage[j];
+  }
+}
+
+// One block per (window, coarse bin): counting sort of its segment by the
+// fine bits, in LDS tiles of RS_FTILE entries with coalesced output runs.
+// A segment that fits one tile (all but the top window's, typically) is
+// read twice; longer ones get a counting pass first.
+#define RS_FTILE 8192
+__global__ void __launch_bounds__(RS_T) k_rsort_fine(const uint32_t* __restrict__ tmpA, uint32_t nchunk,
+                                                    const uint32_t* __restrict__ offA, uint32_t* __restrict__ boff,
+                                                    uint32_t* __restrict__ entries) {
+  __shared__ uint32_t base[RS_FINE_N], lcnt[RS_FINE_N], lloc[RS_FINE_N];
+  __shared__ uint32_t stage[RS_FTILE];
+  __shared__ uint8_t sf[RS_FTILE];
+  const uint32_t seg = blockIdx.x;  // w * NC + coarse bin
+  const uint32_t s = offA[(size_t)seg * nchunk], e = offA[(size_t)(seg + 1) * nchunk];
+  const bool one_tile = e - s <= RS_FTILE;
+  if (!one_tile) {
+    if (threadIdx.x < RS_FINE_N) base[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t i = s + threadIdx.x; i < e; i += RS_T) atomicAdd(&base[(tmpA[i] >> 24) & 0x7fu], 1u);
+    __syncthreads();
+    lds_excl_scan_w0(base, 2, s);
+    __syncthreads();
+    if (threadIdx.x < RS_FINE_N) boff[(size_t)seg * RS_FINE_N + threadIdx.x] = base[threadIdx.x];
+  }
+  for (uint32_t ts = s; ts < e || (one_tile && ts == s); ts += RS_FTILE) {
+    const uint32_t te = min(ts + RS_FTILE, e);
+    if (threadIdx.x < RS_FINE_N) lcnt[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t i = ts + threadIdx.x; i < te; i += RS_T) atomicAdd(&lcnt[(tmpA[i] >> 24) & 0x7fu], 1u);
+    __syncthreads();
+    if (threadIdx.x < RS_FINE_N) lloc[threadIdx.x] = lcnt[threadIdx.x];
+    __syncthreads();
+    lds_excl_scan_w0(lloc, 2, 0);
+    __syncthreads();
+    if (threadIdx.x < RS_FINE_N) {
+      lcnt[threadIdx.x] = lloc[threadIdx.x];  // cursors
+      if (one_tile) {
+        base[threadIdx.x] = s + lloc[threadIdx.x];
+        boff[(size_t)seg * RS_FINE_N + threadIdx.x] = s + lloc[threadIdx.x];
+      }
+    }
+    __syncthreads();
+    for (uint32_t i = ts + threadIdx.x; i < te; i += RS_T) {
+      const uint32_t v = tmpA[i];
+      const uint32_t f = (v >> 24) & 0x7fu;
+      const uint32_t p = atomicAdd(&lcnt[f], 1u);
+      stage[p] = v & ~RS_FMASK;
+      sf[p] = (uint8_t)f;
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < te - ts; j += RS_T) {
+      const uint32_t f = sf[j];
+      entries[base[f] + j - lloc[f]] = stage[j];
+    }
+    __syncthreads();
+    // advance the global cursors by this tile's counts (lcnt = lloc + count)
+    if (threadIdx.x < RS_FINE_N) base[threadIdx.x] += lcnt[threadIdx.x] - lloc[threadIdx.x];
+    __syncthreads();
+    if (one_tile) break;
+  }
+}

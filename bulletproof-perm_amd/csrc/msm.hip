@@ -165,8 +165,11 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
   {
     // entries per lane: enough lanes to fill the chip several times over
     const uint32_t E_max = T * Wn;
-    uint32_t K = 32;
-    while (K > 4 && (E_max / K) < 256u * 1024u) K >>= 1;
+    // K = entries per lane: about one round of lanes at the accumulate's
+    // 4 waves/SIMD occupancy (256 K lanes) -- fewer chunk borders, so fewer
+    // head/tail pieces for k_msm_fixup (2^20: K = 64 measured best of 32/64/128)
+    uint32_t K = 4;
+    while (K < 128 && E_max / (2 * K) >= 256u * 1024u) K <<= 1;
     if (const char* ek = getenv("BPP_MSM_K")) K = std::max<uint32_t>(4, (uint32_t)atoi(ek) & ~3u);
     const size_t lanes = (E_max + K - 1) / K + 1;
     void *head, *tail;

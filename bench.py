@@ -29,10 +29,12 @@ sys.path.insert(0, str(ROOT / "bulletproof-perm_amd"))
 
 L = 2**252 + 27742317777372353535851937790883648493
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
-# Integer-ALU roofline: dependent-free GF(2^255-19) multiplies per second on
-# the whole chip, measured by tools/ubench/felat (profiles/r01_felat.txt,
-# 16 waves/SIMD).  One mixed addition (ge_madd) = 7 field multiplies.
-FE_MUL_PEAK_GOPS = 230.0
+# Integer-ALU roofline: independent GF(2^255-19) multiplies per second on the
+# whole chip with the product's own field code (10-limb radix 2^25.5),
+# measured by tools/ubench/felat at 4096 x 64-lane blocks
+# (profiles/r01_felat_fe10.txt).  One mixed addition (ge_madd) = 7 field
+# multiplies.
+FE_MUL_PEAK_GOPS = 273.0
 
 
 def synth_scalars(n: int, seed: int) -> bytes:

@@ -1,4 +1,5 @@
-"""Large-size MSM parity (the single-MSM LDS sort path, n >= 2^14).
+"""Large-size MSM parity (the single-MSM sort paths, n >= 2^14: two-pass
+radix sort by default, the one-pass LDS sort under BPP_MSM_LDS_SORT=1).
 
 Exact: GPU vs the serial C restatement of dalek's MSM (oracle/c) at 2^14 and
 2^17 terms.  Full size (BASELINE config 3, 2^20 terms): size-independent
@@ -32,8 +33,10 @@ def big_table(ctx):
     t.close()
 
 
-@pytest.mark.parametrize("logn", [14, 17])
-def test_msm_exact_vs_cport(ctx, big_table, logn):
+@pytest.mark.parametrize("logn,lds", [(14, False), (17, False), (17, True)])
+def test_msm_exact_vs_cport(ctx, big_table, logn, lds, monkeypatch):
+    if lds:
+        monkeypatch.setenv("BPP_MSM_LDS_SORT", "1")
     raw, tbl = big_table
     n = 1 << logn
     sc = _sb(_scalars(n, logn))
@@ -60,11 +63,12 @@ def test_msm_2p20_linearity_and_partials(ctx, big_table):
     ctx.dev_free(d)
 
 
-def test_msm_all_equal_scalars(ctx, big_table):
+@pytest.mark.parametrize("n", [1 << 16, 1 << 20])
+def test_msm_all_equal_scalars(ctx, big_table, n):
     """Adversarial bucket skew: n equal scalars put every term of a window in
-    one bucket; sum_i k P_i == k * sum_i P_i."""
+    one bucket (one coarse bin of 2^20 entries: the multi-tile fine sort, and
+    2^14 accumulate chunks for fixup to join); sum_i k P_i == k * sum_i P_i."""
     _, tbl = big_table
-    n = 1 << 16
     k = _scalars(1, 9)[0]
     got = ctx.msm_table(_sb([k] * n), tbl, n)
     ones = ctx.msm_table(_sb([1] * n), tbl, n)

@@ -39,7 +39,7 @@ def _join(items: Iterable[bytes], width: int, what: str) -> bytes:
 
 
 class PointTable:
-    """A point table resident in HBM (affine-Niels, 96 B / point)."""
+    """A point table resident in HBM (affine Niels, 10-limb field, 128-B rows)."""
 
     def __init__(self, ctx: "Context", handle: int):
         self._ctx = ctx
@@ -185,7 +185,8 @@ class Context:
         idx = (C.c_uint32 * max(1, len(point_idx)))(*point_idx)
         out = C.create_string_buffer(32 * max(count, 1))
         check(self.lib.bpp_msm_batch(self.h, count, off, _buf(s), idx, table.handle, out), "bpp_msm_batch", self.h)
-        return [out.raw[32 * i: 32 * i + 32] for i in range(count)]
+        raw = out.raw  # .raw copies the whole buffer on every access
+        return [raw[32 * i: 32 * i + 32] for i in range(count)]
 
 
 def msm_windows(n: int) -> tuple[int, int]:
@@ -313,7 +314,8 @@ class Gens:
         out = C.create_string_buffer(32 * max(m, 1))
         check(self.ctx.lib.bpp_pedersen_commit_batch(self.ctx.h, self.h, _buf(vb), _buf(gb), m, out),
               "bpp_pedersen_commit_batch", self.ctx.h)
-        return [out.raw[32 * i: 32 * i + 32] for i in range(m)]
+        raw = out.raw
+        return [raw[32 * i: 32 * i + 32] for i in range(m)]
 
     def vec_commit(self, blind: bytes, a, b=None) -> bytes:
         ab = _join(a, 32, "a")
@@ -336,7 +338,8 @@ class Gens:
         check(self.ctx.lib.bpp_ipa_prove(self.ctx.h, self.h, tr.h, _buf(Q), _buf(gf) if gf else None,
                                          _buf(hf) if hf else None, _buf(ab), _buf(bb), n, Lo, Ro, ao, bo),
               "bpp_ipa_prove", self.ctx.h)
-        return ([Lo.raw[32 * i: 32 * i + 32] for i in range(lg)], [Ro.raw[32 * i: 32 * i + 32] for i in range(lg)],
+        lraw, rraw = Lo.raw, Ro.raw
+        return ([lraw[32 * i: 32 * i + 32] for i in range(lg)], [rraw[32 * i: 32 * i + 32] for i in range(lg)],
                 ao.raw, bo.raw)
 
     def ipa_verify(self, tr: Transcript, n: int, G_factors, H_factors, P: bytes, Q: bytes, L, R, a: bytes,
@@ -371,7 +374,8 @@ class PermProver:
         perm = (C.c_uint32 * self.k)()
         check(self.ctx.lib.bpp_perm_prove(self.ctx.h, self.gens.h, self.k, seed, _buf(self.label), len(self.label),
                                           pf, V, perm), "bpp_perm_prove", self.ctx.h)
-        return pf.raw, [V.raw[32 * j: 32 * j + 32] for j in range(self.m)], list(perm)
+        vraw = V.raw
+        return pf.raw, [vraw[32 * j: 32 * j + 32] for j in range(self.m)], list(perm)
 
     def prove_batch(self, seeds: Sequence[int]):
         cnt = len(seeds)
@@ -380,8 +384,9 @@ class PermProver:
         sd = (C.c_uint64 * cnt)(*seeds)
         check(self.ctx.lib.bpp_perm_prove_batch(self.ctx.h, self.gens.h, self.k, cnt, sd, _buf(self.label),
                                                 len(self.label), pf, V), "bpp_perm_prove_batch", self.ctx.h)
-        return ([pf.raw[i * self.proof_len:(i + 1) * self.proof_len] for i in range(cnt)],
-                [V.raw[i * 32 * self.m:(i + 1) * 32 * self.m] for i in range(cnt)])
+        praw, vraw = pf.raw, V.raw
+        return ([praw[i * self.proof_len:(i + 1) * self.proof_len] for i in range(cnt)],
+                [vraw[i * 32 * self.m:(i + 1) * 32 * self.m] for i in range(cnt)])
 
     def verify(self, proof: bytes, V) -> bool:
         vb = _join(V, 32, "V")

@@ -20,6 +20,7 @@ namespace perm {
 struct Entry {
   uint32_t q, col;
   hsc::Sc val;
+  hsc::Sc valR;  // Montgomery form of val (zW products in one step)
 };
 
 struct Circuit {

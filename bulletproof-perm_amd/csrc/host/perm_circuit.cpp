@@ -59,6 +59,8 @@ Circuit build(uint32_t k) {
   }
   C.WO.push_back({4 * k, 2 * k - 1, one});
   C.WV.push_back({4 * k + 1, X, one});
+  for (auto* W : {&C.WL, &C.WR, &C.WO, &C.WV})
+    for (Entry& e : *W) e.valR = hsc::to_mont(e.val);
   return C;
 }
 
@@ -96,7 +98,7 @@ void witness(const Circuit& C, const std::vector<uint32_t>& pi, const Sc& x, std
 
 std::vector<Sc> zW(const std::vector<Entry>& W, const std::vector<Sc>& zq, uint32_t ncols) {
   std::vector<Sc> out(ncols, hsc::zero());
-  for (const Entry& e : W) out[e.col] = hsc::add(out[e.col], hsc::mul(zq[e.q], e.val));
+  for (const Entry& e : W) out[e.col] = hsc::add(out[e.col], hsc::mulm(zq[e.q], e.valR));
   return out;
 }
 

@@ -105,6 +105,10 @@ static inline Sc mont(const Sc& a, const Sc& b) {
 
 static inline Sc mul(const Sc& a, const Sc& b) { return mont(mont(a, b), R2); }
 static inline Sc sq(const Sc& a) { return mul(a, a); }
+// Montgomery form b*R mod l of a canonical b; then mulm(a, to_mont(b)) = a*b
+// with one Montgomery step (for operands reused across many products).
+static inline Sc to_mont(const Sc& b) { return mont(b, R2); }
+static inline Sc mulm(const Sc& a, const Sc& bR) { return mont(a, bR); }
 
 // from 32 canonical little-endian bytes; false if >= l
 static inline bool from_canonical(Sc& out, const uint8_t b[32]) {
@@ -133,13 +137,15 @@ static inline Sc from_bytes_mod(const uint8_t b[32]) {
 
 static inline void to_bytes(uint8_t out[32], const Sc& a) { memcpy(out, a.v, 32); }
 
+// square-and-multiply in the Montgomery domain (one step per operation)
 static inline Sc pow(const Sc& a, const Sc& e) {
-  Sc r = one();
+  const Sc aR = to_mont(a);
+  Sc rR = to_mont(one());
   for (int i = 255; i >= 0; --i) {
-    r = sq(r);
-    if ((e.v[i >> 6] >> (i & 63)) & 1) r = mul(r, a);
+    rR = mont(rR, rR);
+    if ((e.v[i >> 6] >> (i & 63)) & 1) rR = mont(rR, aR);
   }
-  return r;
+  return mont(rR, one());
 }
 
 static inline Sc invert(const Sc& a) {
@@ -167,19 +173,33 @@ static inline Sc batch_invert(std::vector<Sc>& xs) {
   return allinv;
 }
 
+// sum a_i b_i: Montgomery products accumulated, one correction at the end
 static inline Sc inner_product(const std::vector<Sc>& a, const std::vector<Sc>& b) {
   Sc r = zero();
-  for (size_t i = 0; i < a.size(); ++i) r = add(r, mul(a[i], b[i]));
-  return r;
+  for (size_t i = 0; i < a.size(); ++i) r = add(r, mont(a[i], b[i]));
+  return mont(r, R2);
 }
 
 // (1, x, x^2, ..., x^{n-1})
 static inline std::vector<Sc> powers(const Sc& x, size_t n) {
   std::vector<Sc> r(n);
+  const Sc xR = to_mont(x);
   Sc c = one();
   for (size_t i = 0; i < n; ++i) {
     r[i] = c;
-    c = mul(c, x);
+    c = mont(c, xR);
+  }
+  return r;
+}
+
+// (R, xR, x^2 R, ...): Montgomery forms of the powers, for mulm
+static inline std::vector<Sc> powers_mont(const Sc& x, size_t n) {
+  std::vector<Sc> r(n);
+  const Sc xR = to_mont(x);
+  Sc c = to_mont(one());
+  for (size_t i = 0; i < n; ++i) {
+    r[i] = c;
+    c = mont(c, xR);
   }
   return r;
 }

@@ -103,8 +103,8 @@ std::vector<uint8_t> to_bytes(const std::vector<Sc>& v) {
 int upload_sc(bpp_ctx* ctx, const std::vector<Sc>& v, const char* name, uint32_t** d) {
   void* p = nullptr;
   BPP_TRY(ctx_ws(ctx, name, v.size() * 32 + 32, &p));
-  std::vector<uint8_t> b = to_bytes(v);
-  BPP_TRY(ctx_h2d(ctx, p, b.data(), b.size()));
+  static_assert(sizeof(Sc) == 32, "Sc is the 32-byte little-endian scalar");
+  BPP_TRY(ctx_h2d(ctx, p, v.data(), v.size() * 32));  // canonical Sc == its byte encoding
   *d = (uint32_t*)p;
   return BPP_OK;
 }
@@ -273,8 +273,11 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     st.tr.append_point("S", Pf.S.data());
     const Sc y = st.tr.challenge_scalar("y");
     const Sc z = st.tr.challenge_scalar("z");
-    std::vector<Sc> y_n = hsc::powers(y, n_p);
-    st.y_inv_n = hsc::powers(hsc::invert(y), n_p);
+    // Montgomery forms of the powers: one Montgomery step per product
+    const std::vector<Sc> y_nR = hsc::powers_mont(y, n_p);
+    const std::vector<Sc> y_inv_nR = hsc::powers_mont(hsc::invert(y), n_p);
+    st.y_inv_n.resize(n_p);
+    for (uint32_t i = 0; i < n_p; ++i) st.y_inv_n[i] = hsc::mont(y_inv_nR[i], hsc::one());
     std::vector<Sc> zq = hsc::powers(z, C.Q + 1);
     zq.erase(zq.begin());
     const std::vector<Sc> zWL = perm::zW(C.WL, zq, n_p), zWR = perm::zW(C.WR, zq, n_p),
@@ -287,10 +290,11 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     r1.resize(n_p);
     r3.resize(n_p);
     for (uint32_t i = 0; i < n_p; ++i) {
-      l1[i] = hsc::add(st.aL[i], hsc::mul(st.y_inv_n[i], zWR[i]));
-      r0[i] = hsc::sub(zWO[i], y_n[i]);
-      r1[i] = hsc::add(hsc::mul(y_n[i], st.aR[i]), zWL[i]);
-      r3[i] = hsc::mul(y_n[i], st.sR[i]);
+      const Sc y_i = hsc::mont(y_nR[i], hsc::one());
+      l1[i] = hsc::add(st.aL[i], hsc::mulm(zWR[i], y_inv_nR[i]));
+      r0[i] = hsc::sub(zWO[i], y_i);
+      r1[i] = hsc::add(hsc::mulm(st.aR[i], y_nR[i]), zWL[i]);
+      r3[i] = hsc::mulm(st.sR[i], y_nR[i]);
     }
     const std::vector<Sc>& l2 = st.aO;
     const std::vector<Sc>& l3 = st.sL;
@@ -339,9 +343,10 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
       const std::vector<Sc>& l3 = st.sL;
       st.l.resize(n_p);
       st.r.resize(n_p);
+      const Sc xR = hsc::to_mont(x), x2R = hsc::to_mont(xp[2]);
       for (uint32_t i = 0; i < n_p; ++i) {
-        st.l[i] = hsc::mul(x, add(l1[i], hsc::mul(x, add(l2[i], hsc::mul(x, l3[i])))));
-        st.r[i] = add(r0[i], hsc::mul(x, add(r1[i], hsc::mul(xp[2], r3[i]))));
+        st.l[i] = hsc::mulm(add(l1[i], hsc::mulm(add(l2[i], hsc::mulm(l3[i], xR)), xR)), xR);
+        st.r[i] = add(r0[i], hsc::mulm(add(r1[i], hsc::mulm(r3[i], x2R)), xR));
       }
       const Sc t_hat = hsc::inner_product(st.l, st.r);
       st.tr.append_scalar("TX", tau_x);
@@ -426,15 +431,18 @@ bool verify_scalars(const perm::Circuit& C, const Proof& P, merlin::Transcript& 
   using hsc::sub;
   Sc delta = hsc::zero();
   for (uint32_t i = 0; i < n_p; ++i) delta = add(delta, mul(mul(y_inv_n[i], zWR[i]), zWL[i]));
+  const Sc aR_ = hsc::to_mont(P.ipa.a), bR_ = hsc::to_mont(P.ipa.b), xR_ = hsc::to_mont(x), wtR = hsc::to_mont(wt);
   const Sc zc = hsc::inner_product(zq, c);
   const Sc a = P.ipa.a, b = P.ipa.b;
   // generators (merged t-check and IPA-check scalars)
   for (uint32_t i = 0; i < n_p; ++i) {
-    const Sc gi = sub(mul(a, s[i]), mul(mul(x, y_inv_n[i]), zWR[i]));
-    const Sc hi = add(sub(mul(mul(b, s[n_p - 1 - i]), y_inv_n[i]), mul(y_inv_n[i], add(mul(x, zWL[i]), zWO[i]))),
+    const Sc yiR = hsc::to_mont(y_inv_n[i]);
+    const Sc gi = sub(hsc::mulm(s[i], aR_), hsc::mulm(hsc::mulm(zWR[i], xR_), yiR));
+    const Sc hi = add(sub(hsc::mulm(hsc::mulm(s[n_p - 1 - i], bR_), yiR),
+                          hsc::mulm(add(hsc::mulm(zWL[i], xR_), zWO[i]), yiR)),
                       hsc::one());
-    gen_sc[i] = add(gen_sc[i], mul(wt, gi));
-    gen_sc[n_p + i] = add(gen_sc[n_p + i], mul(wt, hi));
+    gen_sc[i] = add(gen_sc[i], hsc::mulm(gi, wtR));
+    gen_sc[n_p + i] = add(gen_sc[n_p + i], hsc::mulm(hi, wtR));
   }
   const Sc tcheck_B = mul(r, sub(P.t_hat, mul(xp[2], add(delta, zc))));
   const Sc ipa_B = mul(w, sub(mul(a, b), P.t_hat));

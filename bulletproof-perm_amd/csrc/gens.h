@@ -8,6 +8,7 @@
 #include "msm_engine.h"
 
 #define FB_POS 64  // radix-16 positions per fixed base
+#define GENS_DT_MAX 4096  // generators for which direct tables are kept (2 GB at the limit)
 
 struct bpp_gens {
   bpp_ctx* ctx = nullptr;
@@ -16,6 +17,9 @@ struct bpp_gens {
   uint32_t* d_fb = nullptr;   // fixed-base tables for B and Bb: 2 x 64 x 8 Niels
   // window tables of every generator (FBW_W x 128 B each), built on first use
   mutable uint32_t* d_wt = nullptr;
+  // direct tables d * 2^(8w) * P (512 KB per generator), built on first use
+  // when 2n+2 <= GENS_DT_MAX
+  mutable uint32_t* d_dt = nullptr;
   uint32_t gidx(size_t i) const { return (uint32_t)i; }
   uint32_t hidx(size_t i) const { return (uint32_t)(n + i); }
   uint32_t bidx() const { return (uint32_t)(2 * n); }

@@ -11,6 +11,7 @@
 // fixed-base: per base a table of d*16^i*P (i < 64, d = 1..8) turns each
 // commitment into 2 x 64 mixed additions with signed radix-16 digits and no
 // doublings; one lane per commitment.
+#include <cstdlib>
 #include <cstring>
 
 #include "ctx.h"
@@ -166,9 +167,23 @@ int gens_points(bpp_ctx* ctx, const bpp_gens* g, MsmPoints* out) {
     }
     g->d_wt = d;
   }
+  if (!g->d_dt && np <= GENS_DT_MAX && !getenv("BPP_NO_DT")) {
+    uint32_t* d = nullptr;
+    if (hipMalloc(&d, (size_t)np * 32 * 128 * MSM_NIELS_WORDS * 4) != hipSuccess) {
+      ctx->err = "hipMalloc generator direct tables";
+      return BPP_ERR_NOMEM;
+    }
+    const int rc = dt_build(ctx, g->d_wt, np, d);
+    if (rc) {
+      hipFree(d);
+      return rc;
+    }
+    g->d_dt = d;
+  }
   *out = MsmPoints();
   out->tbl = g->d_tbl;
   out->wt = g->d_wt;
+  out->dt = g->d_dt;
   return BPP_OK;
 }
 
@@ -282,6 +297,7 @@ void bpp_gens_destroy(bpp_gens* g) {
   if (g->d_tbl) hipFree(g->d_tbl);
   if (g->d_fb) hipFree(g->d_fb);
   if (g->d_wt) hipFree(g->d_wt);
+  if (g->d_dt) hipFree(g->d_dt);
   delete g;
 }
 

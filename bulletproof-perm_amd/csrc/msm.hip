@@ -183,9 +183,19 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
     }
     BPP_TRY(ctx_check_launch(ctx, "k_msm_accumulate"));
     {
+      // a heavy bucket spans > FIX_MAX chunks, so holds > (FIX_MAX - 1) K
+      // entries: at most E / ((FIX_MAX - 1) K) + 1 of them
+      const size_t max_heavy = std::min<size_t>(NB, E_max / ((size_t)(FIX_MAX - 1) * K) + 1);
+      void* heavy = nullptr;
+      BPP_TRY(ctx_ws(ctx, "msm_heavy", (max_heavy + 1) * 4, &heavy));
+      BPP_HIP(hipMemsetAsync(heavy, 0, 4, ctx->stream));
       ProfScope ps(ctx, "msm_fixup");
       hipLaunchKernelGGL(k_msm_fixup, dim3(grid_for(NB, 256)), dim3(256), 0, ctx->stream, (const uint32_t*)boff,
-                         (uint32_t)NB, K, (const uint32_t*)head, (const uint32_t*)tail, (uint32_t*)bsum);
+                         (uint32_t)NB, K, (const uint32_t*)head, (const uint32_t*)tail, (uint32_t*)bsum,
+                         (uint32_t*)heavy);
+      hipLaunchKernelGGL(k_msm_fixup_heavy, dim3((unsigned)max_heavy), dim3(64), 0, ctx->stream,
+                         (const uint32_t*)boff, K, (const uint32_t*)head, (const uint32_t*)tail,
+                         (const uint32_t*)heavy, (uint32_t*)bsum);
     }
     BPP_TRY(ctx_check_launch(ctx, "k_msm_fixup"));
   }
@@ -420,6 +430,51 @@ static bool fb_wins(double terms_per_msm) {
   return pol == 1 || (pol == -1 && terms_per_msm <= 16384.0);
 }
 
+int dt_build(bpp_ctx* ctx, const uint32_t* d_wt, uint32_t npts, uint32_t* d_dt) {
+  if (!npts) return BPP_OK;
+  {
+    ProfScope ps(ctx, "dt_tables");
+    hipLaunchKernelGGL(k_dt_build, dim3(grid_for((size_t)npts * DT_ROWS_PER_GEN, 64)), dim3(64), 0, ctx->stream, d_wt,
+                       npts, d_dt);
+  }
+  return ctx_check_launch(ctx, "k_dt_build");
+}
+
+// Direct-table engine: one block per MSM (BPP_MSM_DT=0 disables, =1 forces).
+static bool use_dt(const MsmPoints& pts, uint32_t M, uint32_t T) {
+  if (!pts.dt || pts.tbl1 || M == 0) return false;
+  const char* e = getenv("BPP_MSM_DT");
+  const int pol = e ? atoi(e) : -1;
+  return pol == 1 || (pol == -1 && (double)T <= 16384.0 * (double)M);
+}
+
+static int msm_multi_dt_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx,
+                            const std::vector<uint32_t>& off, const MsmPoints& pts, uint32_t** d_res) {
+  const uint32_t M = (uint32_t)off.size() - 1;
+  const uint32_t T = off[M];
+  void *d_off, *res;
+  BPP_TRY(ctx_ws(ctx, "multi_off", (M + 1) * 4, &d_off));
+  BPP_TRY(ctx_h2d(ctx, d_off, off.data(), (M + 1) * 4));
+  BPP_TRY(ctx_ws(ctx, "dt_res", (size_t)M * P3_BYTES, &res));
+  const double e_avg = (double)T * DT_W / (double)M;  // table additions per MSM
+  {
+    ProfScope ps(ctx, "msm_direct");
+    // (no 1024-thread variant: capped at 128 VGPRs it spills in the main loop)
+    if (e_avg > 1024)
+      hipLaunchKernelGGL(k_dt_msm<512>, dim3(M), dim3(512), 0, ctx->stream, pts.dt, d_scal, d_pidx,
+                         (const uint32_t*)d_off, (uint32_t*)res);
+    else if (e_avg > 256)
+      hipLaunchKernelGGL(k_dt_msm<256>, dim3(M), dim3(256), 0, ctx->stream, pts.dt, d_scal, d_pidx,
+                         (const uint32_t*)d_off, (uint32_t*)res);
+    else
+      hipLaunchKernelGGL(k_dt_msm<64>, dim3(M), dim3(64), 0, ctx->stream, pts.dt, d_scal, d_pidx,
+                         (const uint32_t*)d_off, (uint32_t*)res);
+  }
+  BPP_TRY(ctx_check_launch(ctx, "k_dt_msm"));
+  *d_res = (uint32_t*)res;
+  return BPP_OK;
+}
+
 static bool use_fb(const MsmPoints& pts, uint32_t M, uint32_t T) {
   const bool have_fb = pts.wt && (!pts.tbl1 || pts.wt1);
   return have_fb && M > 0 && fb_wins((double)T / (double)M);
@@ -447,11 +502,13 @@ int msm_multi(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, cons
               const MsmPoints& pts, std::vector<h25519::ge>& out) {
   const uint32_t M = (uint32_t)off.size() - 1;
   const uint32_t T = off[M];
-  if (!use_fb(pts, M, T)) return msm_multi(ctx, d_scal, d_pidx, off, pts.tbl, pts.tbl1, pts.n0, out);
+  const bool dt = use_dt(pts, M, T);
+  if (!dt && !use_fb(pts, M, T)) return msm_multi(ctx, d_scal, d_pidx, off, pts.tbl, pts.tbl1, pts.n0, out);
   out.assign(M, h25519::ge_identity());
   if (M == 0 || T == 0) return BPP_OK;
   uint32_t* d_ws = nullptr;
-  BPP_TRY(msm_multi_fb_dev(ctx, d_scal, d_pidx, off, pts, &d_ws));
+  if (dt) BPP_TRY(msm_multi_dt_dev(ctx, d_scal, d_pidx, off, pts, &d_ws));
+  else BPP_TRY(msm_multi_fb_dev(ctx, d_scal, d_pidx, off, pts, &d_ws));
   void* h = nullptr;
   BPP_TRY(ctx_pinned(ctx, (size_t)M * P3_BYTES, &h));
   BPP_HIP(hipMemcpyAsync(h, d_ws, (size_t)M * P3_BYTES, hipMemcpyDeviceToHost, ctx->stream));
@@ -467,6 +524,11 @@ int msm_multi_enc(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, 
   if (M == 0) return BPP_OK;
   // Few results: host encoding (~10 us each) beats a latency-bound GPU
   // launch; many: one GPU lane per result.
+  if (M > 16 && T > 0 && use_dt(pts, M, T)) {
+    uint32_t* d_ws = nullptr;
+    BPP_TRY(msm_multi_dt_dev(ctx, d_scal, d_pidx, off, pts, &d_ws));
+    return points_compress_p3(ctx, d_ws, M, out_enc);
+  }
   if (M > 16 && T > 0 && use_fb(pts, M, T)) {
     uint32_t* d_ws = nullptr;
     BPP_TRY(msm_multi_fb_dev(ctx, d_scal, d_pidx, off, pts, &d_ws));

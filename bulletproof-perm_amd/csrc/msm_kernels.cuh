@@ -196,9 +196,13 @@ __global__ void __launch_bounds__(256) ACC_ATTR k_msm_accumulate(const uint32_t*
 
 // One lane per bucket: identity for empty buckets, and the sum of the
 // pieces for buckets that cross chunk borders.
+// A bucket spanning more than FIX_MAX chunks (bucket skew: the few buckets
+// of a narrow top window, equal scalars) is listed in heavy[1..] (count in
+// heavy[0]) and summed by a whole wave instead of one lane's serial chain.
+#define FIX_MAX 16
 __global__ void __launch_bounds__(256) k_msm_fixup(const uint32_t* __restrict__ boff, uint32_t nbuckets, uint32_t K,
                             const uint32_t* __restrict__ head, const uint32_t* __restrict__ tail,
-                            uint32_t* __restrict__ bsum) {
+                            uint32_t* __restrict__ bsum, uint32_t* __restrict__ heavy) {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= nbuckets) return;
   const uint32_t s = boff[b], e = boff[b + 1];
@@ -208,6 +212,10 @@ __global__ void __launch_bounds__(256) k_msm_fixup(const uint32_t* __restrict__ 
   }
   const uint32_t l0 = s / K, l1 = (e - 1) / K;
   if (l0 == l1) return;  // written by the accumulate lane
+  if (l1 - l0 >= FIX_MAX) {  // heavy (skewed) bucket: one wave in k_msm_fixup_heavy
+    heavy[1 + atomicAdd(&heavy[0], 1u)] = b;
+    return;
+  }
   ge_p3 acc = (s == l0 * K) ? load_p3(head, l0) : load_p3(tail, l0);
   for (uint32_t l = l0 + 1; l <= l1; ++l) acc = ge_add(acc, load_p3(head, l));
   store_p3(bsum, b, acc);
@@ -519,4 +527,110 @@ __global__ void __launch_bounds__(RS_T) k_rsort_fine(const uint32_t* __restrict_
     __syncthreads();
     if (one_tile) break;
   }
+}
+
+// ---------------------------------------------------------------------------
+// Direct fixed-base MSM over full radix-2^8 tables (small MSMs over
+// resident generators: A_I/A_O/S, IPA rounds, vector commitments).
+// Table row ((gen * 32 + w) << 7) + |d| - 1 holds d * 2^(8w) * G_gen
+// (d = 1..128), so a term is at most 32 table additions and an MSM is one
+// flat sum: no digit sort, no buckets, no bucket reduction.  One block per
+// MSM; lane j adds its slice of the MSM's (term, window) pairs, then a
+// wave-shuffle tree and an LDS step over the block's waves.
+#define DT_W 32
+#define DT_ROWS_PER_GEN (DT_W * 128)
+
+FE_INLINE uint32_t scalar_byte(const uint32_t s[8], uint32_t i) { return (s[i >> 2] >> (8 * (i & 3))) & 0xffu; }
+
+FE_INLINE ge_p3 ge_shfl_xor(const ge_p3& a, int m) {
+  ge_p3 o;
+  _Pragma("unroll") for (int k = 0; k < FE_LIMBS; ++k) {
+    o.X.v[k] = __shfl_xor(a.X.v[k], m, 64);
+    o.Y.v[k] = __shfl_xor(a.Y.v[k], m, 64);
+    o.Z.v[k] = __shfl_xor(a.Z.v[k], m, 64);
+    o.T.v[k] = __shfl_xor(a.T.v[k], m, 64);
+  }
+  return o;
+}
+
+template <int NT>
+__global__ void __launch_bounds__(NT) k_dt_msm(const uint32_t* __restrict__ dt, const uint32_t* __restrict__ scalars,
+                                               const uint32_t* __restrict__ pidx, const uint32_t* __restrict__ off,
+                                               uint32_t* __restrict__ out_p3) {
+  __shared__ uint32_t lds[(NT / 64) * P3_WORDS];
+  const uint32_t m = blockIdx.x;
+  const uint32_t t0 = off[m], t1 = off[m + 1];
+  const uint64_t E = (uint64_t)(t1 - t0) * DT_W;
+  const uint32_t e0 = (uint32_t)(E * threadIdx.x / NT), e1 = (uint32_t)(E * (threadIdx.x + 1) / NT);
+  ge_p3 acc = ge_identity();
+  uint32_t s[8], gen = 0, carry = 0, cur = 0xffffffffu;
+  for (uint32_t e = e0; e < e1; ++e) {
+    const uint32_t t = t0 + e / DT_W, w = e % DT_W;
+    if (t != cur) {  // (re)enter a term: scalar, generator, carry into window w
+      cur = t;
+      load_scalar(scalars, t, s);
+      gen = pidx ? pidx[t] : t;
+      carry = 0;
+      for (uint32_t ww = 0; ww < w; ++ww) carry = (scalar_byte(s, ww) + carry) >= 128u ? 1u : 0u;
+    }
+    const uint32_t v = scalar_byte(s, w) + carry;
+    int d;
+    if (v >= 128u && w + 1 < DT_W) {
+      d = (int)v - 256;
+      carry = 1;
+    } else {
+      d = (int)v;
+      carry = 0;
+    }
+    if (d == 0) continue;
+    const ge_niels q = load_niels(dt, gen * DT_ROWS_PER_GEN + w * 128u + (uint32_t)((d < 0 ? -d : d) - 1));
+    acc = d < 0 ? ge_msub(acc, q) : ge_madd(acc, q);
+  }
+  _Pragma("unroll") for (int k = 1; k < 64; k <<= 1) acc = ge_add(acc, ge_shfl_xor(acc, k));
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  if (NT > 64) {
+    if (lane == 0) store_p3(lds, wave, acc);
+    __syncthreads();
+    if (wave == 0) {
+      acc = lane < NT / 64 ? load_p3(lds, lane) : ge_identity();
+      _Pragma("unroll") for (int k = 1; k < NT / 64; k <<= 1) acc = ge_add(acc, ge_shfl_xor(acc, k));
+    }
+  }
+  if (threadIdx.x == 0) store_p3(out_p3, m, acc);
+}
+
+// Direct tables from the window tables: lane (k, w, d) -> d * wt[k*32 + w].
+__global__ void __launch_bounds__(64) k_dt_build(const uint32_t* __restrict__ wt, uint32_t ngen,
+                                                 uint32_t* __restrict__ dt) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)ngen * DT_ROWS_PER_GEN) return;
+  const uint32_t d = (uint32_t)(i & 127u) + 1u;
+  const size_t kw = i >> 7;  // k * 32 + w
+  const ge_p3 Q = ge_from_niels(load_niels(wt, (uint32_t)kw));
+  ge_p3 R = Q;
+  const int top = 31 - __clz(d);
+  for (int b = top - 1; b >= 0; --b) {
+    R = ge_dbl(R);
+    if ((d >> b) & 1u) R = ge_add(R, Q);
+  }
+  store_niels(dt, (uint32_t)i, ge_to_niels(R));
+}
+
+// One wave per heavy bucket: lane j sums pieces j, j+64, ... of the bucket's
+// chunk sequence, then a 6-level shuffle tree.  Blocks past heavy[0] exit.
+__global__ void __launch_bounds__(64) k_msm_fixup_heavy(const uint32_t* __restrict__ boff, uint32_t K,
+                                                        const uint32_t* __restrict__ head,
+                                                        const uint32_t* __restrict__ tail,
+                                                        const uint32_t* __restrict__ heavy, uint32_t* __restrict__ bsum) {
+  if (blockIdx.x >= heavy[0]) return;
+  const uint32_t b = heavy[1 + blockIdx.x];
+  const uint32_t s = boff[b], e = boff[b + 1];
+  const uint32_t l0 = s / K, l1 = (e - 1) / K;
+  ge_p3 acc = ge_identity();
+  for (uint32_t p = threadIdx.x; p <= l1 - l0; p += 64) {
+    const ge_p3 piece = p ? load_p3(head, l0 + p) : (s == l0 * K ? load_p3(head, l0) : load_p3(tail, l0));
+    acc = ge_add(acc, piece);
+  }
+  _Pragma("unroll") for (int k = 1; k < 64; k <<= 1) acc = ge_add(acc, ge_shfl_xor(acc, k));
+  if (threadIdx.x == 0) store_p3(bsum, b, acc);
 }

@@ -57,13 +57,15 @@ def test_perm_batch_verify(gens):
     assert not pr.verify_batch(bad, Vs)
 
 
-@pytest.mark.parametrize("mode", ["0", "1"])
+@pytest.mark.parametrize("mode", ["var", "fb", "dt"])
 def test_perm_proof_both_msm_engines(gens, monkeypatch, mode):
-    """BPP_MSM_FB=0 forces the variable-base (per-window Horner) engine,
-    =1 the fixed-base window-table engine; both must give the oracle's bytes
-    and verify (the verifier's proof points take the window-table path too)."""
+    """All three MSM engines (variable-base, fixed-base window tables, direct
+    tables) must give the oracle's proof bytes, and proofs must verify."""
     import bpperm
-    monkeypatch.setenv("BPP_MSM_FB", mode)
+    # var: per-window Pippenger; fb: window tables + shared buckets;
+    # dt: direct radix-2^8 tables (default for small MSMs over generators)
+    monkeypatch.setenv("BPP_MSM_DT", "1" if mode == "dt" else "0")
+    monkeypatch.setenv("BPP_MSM_FB", "1" if mode == "fb" else "0")
     want, perm = bp.ac_prove(6, 21)
     pr = bpperm.PermProver(gens, 6)
     proof, V, gperm = pr.prove(21)

@@ -95,10 +95,13 @@ def test_ipa_prove_matches_oracle_and_verifies(ctx, gens16, n):
     assert not gens16.ipa_verify(bpperm.Transcript(b"ipa-test"), *bad)
 
 
-@pytest.mark.parametrize("mode", ["0", "1"])
+@pytest.mark.parametrize("mode", ["var", "fb", "dt"])
 def test_ipa_and_vec_commit_both_msm_engines(ctx, gens16, monkeypatch, mode):
     import bpperm
-    monkeypatch.setenv("BPP_MSM_FB", mode)
+    # var: per-window Pippenger; fb: window tables + shared buckets;
+    # dt: direct radix-2^8 tables (default for small MSMs over generators)
+    monkeypatch.setenv("BPP_MSM_DT", "1" if mode == "dt" else "0")
+    monkeypatch.setenv("BPP_MSM_FB", "1" if mode == "fb" else "0")
     rng = Rng(300)
     oG, oH = merlin.bulletproof_gens(16)
     _, Bb = merlin.pedersen_gens_default()

@@ -65,16 +65,34 @@ def load_traffic(stage: str, log2n: int):
         return None
 
 
-def cpu_baseline(seconds: float = 15.0):
+def cpu_baseline(seconds: float = 12.0):
     """Serial C restatement of dalek-ng's Pippenger (oracle/c, 'port') timed
     on a bounded sample of the same workload: one 2^16-pair MSM, repeated
-    until ~`seconds` of CPU time, 1 thread."""
+    until ~`seconds` of CPU time, 1 thread (dalek-ng's serial backend is
+    single-threaded).  An all-host-cores figure (one MSM per thread) rides
+    along as `all_cores`."""
     try:
         sys.path.insert(0, str(ROOT))
         from oracle import cport
     except Exception as e:  # pragma: no cover
         return {"value": None, "unit": "pairs/s", "cores": 1, "kind": "port", "sample": f"unavailable: {e}"}
-    return cport.bench_msm(log2n=16, seconds=seconds)
+    out = cport.bench_msm(log2n=16, seconds=seconds)
+    out["all_cores"] = cport.bench_msm_threads(log2n=16, seconds=seconds / 2, threads=cport.host_cores())
+    return out
+
+
+def cpu_baseline_proofs(seconds: float = 8.0):
+    """52-card proofs/s of the serial C prover restatement (oracle/c/perm_cpu.c:
+    dalek-style MSMs, bulletproofs' folding IPA, merlin), 1 core and all
+    host cores (one proof per thread)."""
+    try:
+        sys.path.insert(0, str(ROOT))
+        from oracle import cport
+    except Exception as e:  # pragma: no cover
+        return {"value": None, "unit": "proofs/s", "cores": 1, "kind": "port", "sample": f"unavailable: {e}"}
+    out = cport.bench_prove(52, seconds=seconds, threads=1)
+    out["all_cores"] = cport.bench_prove(52, seconds=seconds / 2, threads=cport.host_cores())
+    return out
 
 
 def bench_proofs(ctx, args, world, rank, torch, dist):
@@ -135,7 +153,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--log2n", type=int, default=20, help="pairs per GPU = 2^log2n")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--verify", action="store_true", help="also recompute via a second window split")
     ap.add_argument("--proofs-per-gpu", type=int, default=128,
@@ -252,6 +270,8 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        if proofs is not None:
+            proofs["cpu_baseline"] = cpu_baseline_proofs()
     if rank == 0:
         print(json.dumps(line), flush=True)
     ctx.dev_free(d_sc)

@@ -15,6 +15,8 @@ from pathlib import Path
 HERE = Path(__file__).resolve().parent
 SRC = HERE / "c" / "dalek_port.c"
 LIB = HERE / "c" / "libdalekport.so"
+PERM_SRC = HERE / "c" / "perm_cpu.c"
+PERM_LIB = HERE / "c" / "libpermcpu.so"
 L = 2**252 + 27742317777372353535851937790883648493
 
 _lib = None
@@ -23,6 +25,11 @@ _lib = None
 def build(force: bool = False) -> Path:
     if force or not LIB.exists() or LIB.stat().st_mtime < SRC.stat().st_mtime:
         cmd = ["gcc", "-O3", "-march=x86-64-v3", "-mtune=native", "-shared", "-fPIC", "-o", str(LIB), str(SRC)]
+        subprocess.run(cmd, check=True)
+    newest = max(SRC.stat().st_mtime, PERM_SRC.stat().st_mtime)
+    if force or not PERM_LIB.exists() or PERM_LIB.stat().st_mtime < newest:
+        cmd = ["gcc", "-O3", "-march=x86-64-v3", "-mtune=native", "-shared", "-fPIC", "-I", str(SRC.parent), "-o",
+               str(PERM_LIB), str(PERM_SRC)]
         subprocess.run(cmd, check=True)
     return LIB
 
@@ -75,3 +82,94 @@ def bench_msm(log2n: int = 16, seconds: float = 15.0) -> dict:
     t = lib().port_time_msm(sc, pts, n, reps, out) if reps > 1 else t1
     return {"value": n * reps / t, "unit": "pairs/s", "cores": 1, "kind": "port",
             "sample": f"{reps} x 2^{log2n}-pair MSM (dalek-ng 4.1.1 Pippenger w=8 restated in C, 1 thread), {t:.1f} s"}
+
+
+# ------------------------------------------------------------ CPU prover port
+_plib = None
+
+
+def perm_lib():
+    global _plib
+    if _plib is None:
+        if not PERM_LIB.exists():
+            build()
+        _plib = C.CDLL(str(PERM_LIB))
+        _plib.cpu_perm_setup.argtypes = [C.c_uint32]
+        _plib.cpu_perm_proof_len.argtypes = [C.c_uint32]
+        _plib.cpu_perm_proof_len.restype = C.c_size_t
+        _plib.cpu_perm_prove.argtypes = [C.c_uint32, C.c_uint64, C.c_char_p, C.c_size_t, C.c_char_p, C.c_char_p]
+        _plib.cpu_perm_time.argtypes = [C.c_uint32, C.c_uint64, C.c_int, C.c_char_p, C.c_size_t]
+        _plib.cpu_perm_time.restype = C.c_double
+    return _plib
+
+
+def cpu_prove(k: int, seed: int, label: bytes = b"bp-perm"):
+    """-> (proof bytes, [V_j]) from the serial C prover (perm_cpu.c)."""
+    lib_ = perm_lib()
+    assert lib_.cpu_perm_setup(k) == 0
+    pl = lib_.cpu_perm_proof_len(k)
+    pf = C.create_string_buffer(pl)
+    V = C.create_string_buffer(32 * (2 * k + 1))
+    assert lib_.cpu_perm_prove(k, seed, label, len(label), pf, V) == 0
+    raw = V.raw
+    return pf.raw, [raw[32 * j: 32 * j + 32] for j in range(2 * k + 1)]
+
+
+def host_cores() -> int:
+    """CPUs this process may use: the cgroup quota when one is set (the GPU
+    box reports 256 CPUs but grants 16), else the affinity mask."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            return max(1, int(int(q) / int(p)))
+    except Exception:
+        pass
+    return len(os.sched_getaffinity(0))
+
+
+def bench_prove(k: int = 52, seconds: float = 10.0, threads: int = 1, label: bytes = b"bp-perm") -> dict:
+    """52-card proofs/s of the serial C prover: `threads` workers (one proof
+    at a time each, ctypes releases the GIL), ~`seconds` of wall time."""
+    import threading
+    lib_ = perm_lib()
+    assert lib_.cpu_perm_setup(k) == 0
+    t1 = lib_.cpu_perm_time(k, 10_000, 1, label, len(label))
+    per = max(1, int(seconds / max(t1, 1e-6)))
+    secs = [0.0] * threads
+
+    def work(i):
+        secs[i] = lib_.cpu_perm_time(k, 1_000_000 * (i + 1), per, label, len(label))
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    wall = max(secs)
+    return {"value": threads * per / wall, "unit": "proofs/s", "cores": threads, "kind": "port",
+            "sample": f"{threads} x {per} {k}-card proofs (serial C restatement: dalek-ng Straus/Pippenger MSMs, "
+                      f"bulletproofs folding IPA, merlin), {wall:.1f} s"}
+
+
+def bench_msm_threads(log2n: int = 16, seconds: float = 10.0, threads: int = 1) -> dict:
+    """All-cores MSM baseline: `threads` independent 2^log2n MSMs in parallel."""
+    import threading
+    n = 1 << log2n
+    sc, pts = synth(n, 7)
+    out = C.create_string_buffer(32)
+    t1 = lib().port_time_msm(sc, pts, n, 1, out)
+    reps = max(1, int(seconds / max(t1, 1e-6)))
+    secs = [0.0] * threads
+
+    def work(i):
+        o = C.create_string_buffer(32)
+        secs[i] = lib().port_time_msm(sc, pts, n, reps, o)
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    wall = max(secs)
+    return {"value": threads * n * reps / wall, "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": f"{threads} threads x {reps} x 2^{log2n}-pair MSM, {wall:.1f} s"}

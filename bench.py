@@ -159,6 +159,8 @@ def main():
     ap.add_argument("--proofs-per-gpu", type=int, default=128,
                     help="52-card proofs per GPU per batch (config 4: 1024 over 8 GPUs); 0 = skip")
     ap.add_argument("--proof-steps", type=int, default=3)
+    ap.add_argument("--msm-split", choices=["windows", "points"], default="windows",
+                    help="N>1: split the MSM's bucket windows (default) or its points over the ranks")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -172,26 +174,33 @@ def main():
         dist.init_process_group("nccl")
     import bpperm
 
-    n = (1 << args.log2n) * world
+    n_local = 1 << args.log2n
+    n = n_local * world
     ctx = bpperm.Context(local)
 
-    # ---- inputs resident in HBM before the timed region
+    # ---- inputs resident in HBM before the timed region.  The global MSM is
+    # the concatenation of `world` slices with per-slice seeds, so both
+    # partitions compute the same result (result_prefix agrees).
     t0 = time.time()
-    pts = ctx.from_uniform(synth_point_bytes(n, 3))
-    sc = synth_scalars(n, 2)
+    slices = range(world) if args.msm_split == "windows" else [rank]
+    pts = ctx.from_uniform(b"".join(synth_point_bytes(n_local, 3 + 1000 * s) for s in slices))
+    sc = b"".join(synth_scalars(n_local, 2 + 1000 * s) for s in slices)
+    n_here = len(sc) // 32
     d_sc = ctx.dev_alloc(len(sc))
     ctx.htod(d_sc, sc)
     setup_s = time.time() - t0
 
-    c, W = bpperm.msm_windows(n)
-    # contiguous window ranges per rank
-    cuts = [(W * r) // world for r in range(world + 1)]
-    wb, we = cuts[rank], cuts[rank + 1]
+    c, W = bpperm.msm_windows(n_here)
+    if args.msm_split == "windows":  # contiguous window ranges per rank (north_star's split)
+        cuts = [(W * r) // world for r in range(world + 1)]
+        wb, we = cuts[rank], cuts[rank + 1]
+    else:  # this rank's point slice, all windows
+        wb, we = 0, W
 
     def step():
         if world == 1:
             return ctx.msm_table_dev(d_sc, pts, n)
-        part = ctx.msm_table_dev_partial(d_sc, pts, n, wb, we)
+        part = ctx.msm_table_dev_partial(d_sc, pts, n_here, wb, we)
         t = torch.frombuffer(bytearray(part), dtype=torch.uint8).cuda()
         gathered = [torch.empty_like(t) for _ in range(world)]
         dist.all_gather(gathered, t)
@@ -222,7 +231,7 @@ def main():
         if world == 1:
             ctx.msm_table_dev(d_sc, pts, n)
         else:
-            ctx.msm_table_dev_partial(d_sc, pts, n, wb, we)
+            ctx.msm_table_dev_partial(d_sc, pts, n_here, wb, we)
     stages = {}
     for st in ("msm_digits", "msm_count", "msm_scan", "msm_scatter", "msm_accumulate", "msm_fixup", "msm_reduce"):
         ms, k = ctx.profile_get(st)
@@ -236,7 +245,8 @@ def main():
     ms_step = el / args.steps * 1e3
     value = n * args.steps / el
     acc_ms = stages["msm_accumulate"]
-    algo_bytes = 96 * n  # 32 B scalar + 64 B affine point per pair
+    algo_bytes = 96 * n_here  # 32 B scalar + 64 B affine point per pair this rank reads
+    madds = n_here * (we - wb)  # mixed additions in this rank's accumulate launch
     achieved = algo_bytes / (acc_ms * 1e-3) / 1e9 if acc_ms > 0 else None
 
     line = {
@@ -253,16 +263,17 @@ def main():
         "dtype": "u32 limbs (GF(2^255-19) integer)",
         "data": "synthetic: uniform scalars (SHAKE256 -> mod l), hash-to-group points (from_uniform_bytes on GPU)",
         "config": {"workload": f"ristretto255 Pippenger MSM, 2^{args.log2n} pairs per GPU (config 3; config 5 shape at N=4)",
-                   "pairs": n, "window_bits": c, "windows": W, "parallelism": f"window-partition x{world}"},
+                   "pairs": n, "window_bits": c, "windows": W,
+                   "parallelism": f"{'window' if args.msm_split == 'windows' else 'point'}-partition x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                      "traffic": load_traffic("msm_accumulate", args.log2n),
                      "kernel": "k_msm_accumulate", "kernel_ms": acc_ms,
                      "algo_bytes_per_launch": algo_bytes},
-        "alu_roofline": {"achieved": (7 * n * W / (acc_ms * 1e-3) / 1e9) if acc_ms > 0 else None,
+        "alu_roofline": {"achieved": (7 * madds / (acc_ms * 1e-3) / 1e9) if acc_ms > 0 else None,
                          "peak": FE_MUL_PEAK_GOPS, "unit": "G field-mul/s",
-                         "frac": (7 * n * W / (acc_ms * 1e-3) / 1e9 / FE_MUL_PEAK_GOPS) if acc_ms > 0 else None,
-                         "note": "k_msm_accumulate: n*W mixed additions x 7 field multiplies"},
+                         "frac": (7 * madds / (acc_ms * 1e-3) / 1e9 / FE_MUL_PEAK_GOPS) if acc_ms > 0 else None,
+                         "note": "k_msm_accumulate: (pairs x windows) mixed additions per launch x 7 field multiplies"},
         "stage_ms": stages,
         "proofs": proofs,
         "setup_s": setup_s,

@@ -8,6 +8,10 @@
    the 128-byte partials followed by an exact EC addition on every rank
    (bpp_partials_finish).  Payload: world x 128 B per MSM.
 
+   Alternative (SURVEY.md §8e asks to benchmark both): split the POINTS,
+   N/world per rank; every rank runs all W windows over its slice and the
+   same 128-byte partial exchange follows (bench.py --msm-split points).
+
 2. Independent proofs (config 4): proof i -> rank i mod world; no
    collective on the data path.
 
@@ -32,6 +36,22 @@ def distributed_msm(partial_fn: Callable[[int, int], bytes], W: int, rank: int, 
     compressed 32-byte result."""
     wb, we = window_ranges(W, world)[rank]
     part = partial_fn(wb, we)
+    assert len(part) == 128
+    return finish(all_gather(part))
+
+
+def point_ranges(n: int, world: int) -> list[tuple[int, int]]:
+    """Contiguous, near-equal point (term) ranges [b, e) for each rank."""
+    cuts = [(n * r) // world for r in range(world + 1)]
+    return [(cuts[r], cuts[r + 1]) for r in range(world)]
+
+
+def distributed_msm_points(partial_fn: Callable[[int, int], bytes], n: int, rank: int, world: int,
+                           all_gather: Callable[[bytes], Sequence[bytes]],
+                           finish: Callable[[Sequence[bytes]], bytes]) -> bytes:
+    """partial_fn(b, e) -> 128-byte raw MSM over terms [b, e) (all windows)."""
+    b, e = point_ranges(n, world)[rank]
+    part = partial_fn(b, e)
     assert len(part) == 128
     return finish(all_gather(part))
 

@@ -47,7 +47,13 @@ def _worker(rank, world, port, n, q):
 
         res = bdist.distributed_msm(partial, W, rank, world, bdist.torch_all_gather_bytes, bpperm.partials_finish)
         want = r255.encode(r255.msm(sc, pts))
-        q.put((rank, res == want, bdist.window_ranges(W, world)))
+
+        def partial_pts(b, e):  # alternative split: points, all windows
+            return r255.raw_point_bytes(r255.msm(sc[b:e], pts[b:e]))
+
+        res2 = bdist.distributed_msm_points(partial_pts, n, rank, world, bdist.torch_all_gather_bytes,
+                                            bpperm.partials_finish)
+        q.put((rank, res == want and res2 == want, bdist.window_ranges(W, world)))
     finally:
         dist.destroy_process_group()
 

@@ -95,7 +95,7 @@ def cpu_baseline_proofs(seconds: float = 8.0):
     return out
 
 
-def bench_proofs(ctx, args, world, rank, torch, dist):
+def bench_proofs(ctx, args, world, rank, torch, dist, cdev="cuda"):
     """Config 4: batches of 52-card permutation proofs, sharded one batch per
     GPU (independent proofs: no collective on the data path), proved in
     lockstep on each GPU; then the same proofs batch-verified (one MSM per
@@ -118,7 +118,7 @@ def bench_proofs(ctx, args, world, rank, torch, dist):
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         if world > 1:
-            tt = torch.tensor([el], dtype=torch.float64, device="cuda")
+            tt = torch.tensor([el], dtype=torch.float64, device=cdev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             el = tt.item()
         return out, el
@@ -169,9 +169,14 @@ def main():
     import torch
     import torch.distributed as dist
 
+    # BPP_DIST_BACKEND=gloo rehearses the N>1 path with several ranks on one
+    # GPU (RCCL needs one GPU per rank); the driver's runs use nccl = RCCL.
+    backend = os.environ.get("BPP_DIST_BACKEND", "nccl")
+    cdev = "cuda" if backend == "nccl" else "cpu"  # device of collective tensors
     if world > 1:
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(backend)
     import bpperm
 
     n_local = 1 << args.log2n
@@ -201,7 +206,7 @@ def main():
         if world == 1:
             return ctx.msm_table_dev(d_sc, pts, n)
         part = ctx.msm_table_dev_partial(d_sc, pts, n_here, wb, we)
-        t = torch.frombuffer(bytearray(part), dtype=torch.uint8).cuda()
+        t = torch.frombuffer(bytearray(part), dtype=torch.uint8).to(cdev)
         gathered = [torch.empty_like(t) for _ in range(world)]
         dist.all_gather(gathered, t)
         return bpperm.partials_finish([g.cpu().numpy().tobytes() for g in gathered])
@@ -219,7 +224,7 @@ def main():
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([el], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([el], dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = tt.item()
 
@@ -240,7 +245,7 @@ def main():
 
     proofs = None
     if args.proofs_per_gpu > 0:
-        proofs = bench_proofs(ctx, args, world, rank, torch, dist)
+        proofs = bench_proofs(ctx, args, world, rank, torch, dist, cdev)
 
     ms_step = el / args.steps * 1e3
     value = n * args.steps / el

@@ -97,3 +97,16 @@ def test_prove_batch_lockstep_bit_exact(gens):
         pf, V, _ = pr52.prove(seeds[i])
         assert proofs[i] == pf and Vs[i] == b"".join(V)
     assert pr52.verify_batch(proofs, Vs)
+
+
+def test_prove_batch_matches_c_prover_52_card(gens):
+    """GPU lockstep prover vs the serial C prover restatement (oracle/c/
+    perm_cpu.c, dalek-style MSMs + folding IPA): identical 52-card proofs."""
+    import bpperm
+    from oracle import cport
+    pr = bpperm.PermProver(gens, 52)
+    seeds = [5, 77, 1234]
+    proofs, Vs = pr.prove_batch(seeds)
+    for s, pf, V in zip(seeds, proofs, Vs):
+        cpf, cV = cport.cpu_prove(52, s)
+        assert pf == cpf and V == b"".join(cV)

@@ -1,14 +1,16 @@
 // Host-side parallel-for over independent proofs (transcripts, challenge
 // scalars, witness polynomials).  A persistent pool (spawning threads per
 // call costs ~20 us each, more than a batch of transcript operations):
-// threads = BPP_HOST_THREADS or min(hardware threads, 8); items are claimed
+// threads = BPP_HOST_THREADS or min(granted CPUs, 16); items are claimed
 // from an atomic counter; the calling thread works too.  Calls are
 // serialised; a call from inside a pool task runs inline.
 #pragma once
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -16,10 +18,26 @@
 
 namespace par {
 
+// CPUs granted to this process: the cgroup v2 quota when one is set (the
+// GPU box reports 256 CPUs but grants 16 per GPU), else the hardware count.
+inline unsigned granted_cpus() {
+  unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char q[32] = {0};
+    long period = 0;
+    if (fscanf(f, "%31s %ld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0)
+      hw = std::min<unsigned>(hw, std::max(1L, atol(q) / period));
+    fclose(f);
+  }
+  return hw;
+}
+
 inline unsigned threads() {
   static const unsigned n = [] {
     const char* e = getenv("BPP_HOST_THREADS");
-    const unsigned v = e ? (unsigned)atoi(e) : std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+    // measured on the box (16-CPU quota): 16 threads 6.8 ms vs 8 threads
+    // 7.4 ms per 128-proof batch, 19 vs 25 ms per 512
+    const unsigned v = e ? (unsigned)atoi(e) : std::min(16u, granted_cpus());
     return std::max(1u, v);
   }();
   return n;

@@ -457,13 +457,18 @@ static int msm_multi_dt_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t
   BPP_TRY(ctx_h2d(ctx, d_off, off.data(), (M + 1) * 4));
   BPP_TRY(ctx_ws(ctx, "dt_res", (size_t)M * P3_BYTES, &res));
   const double e_avg = (double)T * DT_W / (double)M;  // table additions per MSM
+  int nt = e_avg > 1024 ? 512 : e_avg > 256 ? 256 : 64;
+  if (const char* e = getenv("BPP_DT_NT")) nt = atoi(e);
   {
     ProfScope ps(ctx, "msm_direct");
     // (no 1024-thread variant: capped at 128 VGPRs it spills in the main loop)
-    if (e_avg > 1024)
+    if (nt == 128)
+      hipLaunchKernelGGL(k_dt_msm<128>, dim3(M), dim3(128), 0, ctx->stream, pts.dt, d_scal, d_pidx,
+                         (const uint32_t*)d_off, (uint32_t*)res);
+    else if (nt == 512)
       hipLaunchKernelGGL(k_dt_msm<512>, dim3(M), dim3(512), 0, ctx->stream, pts.dt, d_scal, d_pidx,
                          (const uint32_t*)d_off, (uint32_t*)res);
-    else if (e_avg > 256)
+    else if (nt == 256)
       hipLaunchKernelGGL(k_dt_msm<256>, dim3(M), dim3(256), 0, ctx->stream, pts.dt, d_scal, d_pidx,
                          (const uint32_t*)d_off, (uint32_t*)res);
     else

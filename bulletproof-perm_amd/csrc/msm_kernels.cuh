@@ -553,6 +553,42 @@ FE_INLINE ge_p3 ge_shfl_xor(const ge_p3& a, int m) {
   return o;
 }
 
+// Lane-local walk over the nonzero (term, window) digits of its slice.
+struct DtWalk {
+  const uint32_t* scalars;
+  const uint32_t* pidx;
+  uint32_t t0, e, e1, cur, gen, carry;
+  uint32_t s[8];
+  // next nonzero digit -> table row and sign; false when the slice is done
+  FE_INLINE bool next(uint32_t& row, bool& neg) {
+    for (; e < e1; ++e) {
+      const uint32_t t = t0 + e / DT_W, w = e % DT_W;
+      if (t != cur) {  // (re)enter a term: scalar, generator, carry into window w
+        cur = t;
+        load_scalar(scalars, t, s);
+        gen = pidx ? pidx[t] : t;
+        carry = 0;
+        for (uint32_t ww = 0; ww < w; ++ww) carry = (scalar_byte(s, ww) + carry) >= 128u ? 1u : 0u;
+      }
+      const uint32_t v = scalar_byte(s, w) + carry;
+      int d;
+      if (v >= 128u && w + 1 < DT_W) {
+        d = (int)v - 256;
+        carry = 1;
+      } else {
+        d = (int)v;
+        carry = 0;
+      }
+      if (d == 0) continue;
+      row = gen * DT_ROWS_PER_GEN + w * 128u + (uint32_t)((d < 0 ? -d : d) - 1);
+      neg = d < 0;
+      ++e;
+      return true;
+    }
+    return false;
+  }
+};
+
 template <int NT>
 __global__ void __launch_bounds__(NT) k_dt_msm(const uint32_t* __restrict__ dt, const uint32_t* __restrict__ scalars,
                                                const uint32_t* __restrict__ pidx, const uint32_t* __restrict__ off,
@@ -561,30 +597,20 @@ __global__ void __launch_bounds__(NT) k_dt_msm(const uint32_t* __restrict__ dt, 
   const uint32_t m = blockIdx.x;
   const uint32_t t0 = off[m], t1 = off[m + 1];
   const uint64_t E = (uint64_t)(t1 - t0) * DT_W;
-  const uint32_t e0 = (uint32_t)(E * threadIdx.x / NT), e1 = (uint32_t)(E * (threadIdx.x + 1) / NT);
+  DtWalk it;
+  it.scalars = scalars;
+  it.pidx = pidx;
+  it.t0 = t0;
+  it.e = (uint32_t)(E * threadIdx.x / NT);
+  it.e1 = (uint32_t)(E * (threadIdx.x + 1) / NT);
+  it.cur = 0xffffffffu;
   ge_p3 acc = ge_identity();
-  uint32_t s[8], gen = 0, carry = 0, cur = 0xffffffffu;
-  for (uint32_t e = e0; e < e1; ++e) {
-    const uint32_t t = t0 + e / DT_W, w = e % DT_W;
-    if (t != cur) {  // (re)enter a term: scalar, generator, carry into window w
-      cur = t;
-      load_scalar(scalars, t, s);
-      gen = pidx ? pidx[t] : t;
-      carry = 0;
-      for (uint32_t ww = 0; ww < w; ++ww) carry = (scalar_byte(s, ww) + carry) >= 128u ? 1u : 0u;
-    }
-    const uint32_t v = scalar_byte(s, w) + carry;
-    int d;
-    if (v >= 128u && w + 1 < DT_W) {
-      d = (int)v - 256;
-      carry = 1;
-    } else {
-      d = (int)v;
-      carry = 0;
-    }
-    if (d == 0) continue;
-    const ge_niels q = load_niels(dt, gen * DT_ROWS_PER_GEN + w * 128u + (uint32_t)((d < 0 ? -d : d) - 1));
-    acc = d < 0 ? ge_msub(acc, q) : ge_madd(acc, q);
+  // (a software-pipelined gather measured slower: 233 VGPRs, no latency won)
+  uint32_t row;
+  bool neg;
+  while (it.next(row, neg)) {
+    const ge_niels q = load_niels(dt, row);
+    acc = neg ? ge_msub(acc, q) : ge_madd(acc, q);
   }
   _Pragma("unroll") for (int k = 1; k < 64; k <<= 1) acc = ge_add(acc, ge_shfl_xor(acc, k));
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;

@@ -238,9 +238,11 @@ def main():
         else:
             ctx.msm_table_dev_partial(d_sc, pts, n_here, wb, we)
     stages = {}
+    launches = {}
     for st in ("msm_digits", "msm_count", "msm_scan", "msm_scatter", "msm_accumulate", "msm_fixup", "msm_reduce"):
         ms, k = ctx.profile_get(st)
-        stages[st] = ms / max(k, 1)
+        stages[st] = ms / max(k, 1)  # per launch
+        launches[st] = k / prof_steps  # launches per MSM (one per window group)
     ctx.profile(False)
 
     proofs = None
@@ -250,8 +252,13 @@ def main():
     ms_step = el / args.steps * 1e3
     value = n * args.steps / el
     acc_ms = stages["msm_accumulate"]
-    algo_bytes = 96 * n_here  # 32 B scalar + 64 B affine point per pair this rank reads
-    madds = n_here * (we - wb)  # mixed additions in this rank's accumulate launch
+    # The MSM runs as window groups (one accumulate launch per group, on two
+    # streams): one launch's share of the MSM's algorithmic bytes
+    # (32 B scalar + 64 B affine point per pair) and of its n*W
+    # mixed additions.
+    acc_launches = max(launches["msm_accumulate"], 1.0)
+    algo_bytes = 96 * n_here / acc_launches
+    madds = n_here * (we - wb) / acc_launches
     achieved = algo_bytes / (acc_ms * 1e-3) / 1e9 if acc_ms > 0 else None
 
     line = {
@@ -274,7 +281,7 @@ def main():
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                      "traffic": load_traffic("msm_accumulate", args.log2n),
                      "kernel": "k_msm_accumulate", "kernel_ms": acc_ms,
-                     "algo_bytes_per_launch": algo_bytes},
+                     "algo_bytes_per_launch": algo_bytes, "launches_per_msm": acc_launches},
         "alu_roofline": {"achieved": (7 * madds / (acc_ms * 1e-3) / 1e9) if acc_ms > 0 else None,
                          "peak": FE_MUL_PEAK_GOPS, "unit": "G field-mul/s",
                          "frac": (7 * madds / (acc_ms * 1e-3) / 1e9 / FE_MUL_PEAK_GOPS) if acc_ms > 0 else None,

@@ -121,6 +121,16 @@ ProfScope::~ProfScope() {
 }
 
 static void prof_resolve(bpp_ctx* ctx) {
+  // stages that ran on child streams count under the parent
+  for (bpp_ctx* c : ctx->children) {
+    prof_resolve(c);
+    for (auto& kv : c->prof_acc) {
+      auto& acc = ctx->prof_acc[kv.first];
+      acc.first += kv.second.first;
+      acc.second += kv.second.second;
+    }
+    c->prof_acc.clear();
+  }
   if (ctx->pending.empty()) return;
   hipStreamSynchronize(ctx->stream);
   for (auto& p : ctx->pending) {
@@ -178,6 +188,7 @@ void* bpp_ctx_stream(bpp_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; 
 int bpp_ctx_profile(bpp_ctx* ctx, int enable) {
   if (!ctx) return BPP_ERR_ARG;
   ctx->prof = enable != 0;
+  for (bpp_ctx* c : ctx->children) bpp_ctx_profile(c, enable);
   return BPP_OK;
 }
 

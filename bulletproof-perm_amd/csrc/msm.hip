@@ -38,6 +38,9 @@ uint32_t msm_choose_c(double n_per_msm) {
       best = c;
     }
   }
+  // BPP_MSM_C: window override for large single MSMs (A/B experiments)
+  if (const char* e = getenv("BPP_MSM_C"))
+    if (n_per_msm >= 65536.0) best = std::min(16u, std::max(12u, (uint32_t)atoi(e)));
   return best;
 }
 
@@ -228,6 +231,20 @@ static h25519::ge horner_host(const uint32_t* ws_words, uint32_t Wn, uint32_t c,
   return acc;
 }
 
+// Window groups for one large MSM (msm_single_dev).  Default 1: at 2^20
+// the two-stream pipeline measured slower (G=2 1.38 ms, G=4 1.70 ms vs
+// 1.26 ms), since the reduce and fixup are latency-bound (their time does
+// not shrink with fewer windows) and run G times, and kernels sharing CUs
+// with the VALU-saturating accumulation lose issue slots to it.
+// BPP_MSM_GROUPS=G selects the pipeline.
+uint32_t msm_window_groups(size_t n, uint32_t c, uint32_t Wn, bool indexed) {
+  (void)n;
+  (void)c;
+  uint32_t G = 1;
+  if (const char* e = getenv("BPP_MSM_GROUPS")) G = indexed ? 1u : (uint32_t)std::max(1, atoi(e));
+  return std::max<uint32_t>(1, std::min(G, Wn));
+}
+
 // Single MSM over device scalars + resident table, windows [wb, wb+Wn).
 int msm_single_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const uint32_t* d_tbl, size_t n,
                    uint32_t c, uint32_t wb, uint32_t Wn, h25519::ge* out) {
@@ -235,12 +252,53 @@ int msm_single_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx,
     *out = h25519::ge_identity();
     return BPP_OK;
   }
-  uint32_t* d_ws = nullptr;
-  BPP_TRY(msm_engine(ctx, d_scal, d_pidx, nullptr, 1, (uint32_t)n, c, wb, Wn, d_tbl, &d_ws));
   void* h = nullptr;
   BPP_TRY(ctx_pinned(ctx, (size_t)Wn * P3_BYTES, &h));
-  BPP_HIP(hipMemcpyAsync(h, d_ws, (size_t)Wn * P3_BYTES, hipMemcpyDeviceToHost, ctx->stream));
-  BPP_HIP(hipStreamSynchronize(ctx->stream));
+  const uint32_t G = msm_window_groups(n, c, Wn, d_pidx != nullptr);
+  if (G <= 1) {
+    uint32_t* d_ws = nullptr;
+    BPP_TRY(msm_engine(ctx, d_scal, d_pidx, nullptr, 1, (uint32_t)n, c, wb, Wn, d_tbl, &d_ws));
+    BPP_HIP(hipMemcpyAsync(h, d_ws, (size_t)Wn * P3_BYTES, hipMemcpyDeviceToHost, ctx->stream));
+    BPP_HIP(hipStreamSynchronize(ctx->stream));
+  } else {
+    // Window groups on two child streams: the sort of group g+1 (HBM-bound)
+    // and the bucket reduction of group g-1 (latency-bound, few waves) run
+    // under the accumulation of group g (VALU-bound).  Each child has its
+    // own workspaces, so groups on the same stream simply queue.
+    const uint32_t per = (Wn + G - 1) / G;
+    hipEvent_t ready = nullptr;
+    BPP_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+    BPP_HIP(hipEventRecord(ready, ctx->stream));
+    bpp_ctx* ch[2] = {nullptr, nullptr};
+    int rc = BPP_OK;
+    for (uint32_t g = 0, w0 = 0; g < G && w0 < Wn && rc == BPP_OK; ++g, w0 += per) {
+      const uint32_t wn = std::min(per, Wn - w0);
+      rc = ctx_child(ctx, g & 1, &ch[g & 1]);
+      if (rc) break;
+      bpp_ctx* cc = ch[g & 1];
+      cc->prof = ctx->prof;
+      if (hipStreamWaitEvent(cc->stream, ready, 0) != hipSuccess) {
+        rc = BPP_ERR_DEVICE;
+        break;
+      }
+      uint32_t* d_ws = nullptr;
+      rc = msm_engine(cc, d_scal, d_pidx, nullptr, 1, (uint32_t)n, c, wb + w0, wn, d_tbl, &d_ws);
+      if (rc) {
+        ctx->err = cc->err;
+        break;
+      }
+      if (hipMemcpyAsync((uint8_t*)h + (size_t)w0 * P3_BYTES, d_ws, (size_t)wn * P3_BYTES, hipMemcpyDeviceToHost,
+                         cc->stream) != hipSuccess)
+        rc = BPP_ERR_DEVICE;
+    }
+    for (bpp_ctx* cc : ch)
+      if (cc && hipStreamSynchronize(cc->stream) != hipSuccess && rc == BPP_OK) rc = BPP_ERR_DEVICE;
+    hipEventDestroy(ready);
+    if (rc) {
+      if (ctx->err.empty()) ctx->err = "window-group MSM launch failed";
+      return rc;
+    }
+  }
   *out = horner_host((const uint32_t*)h, Wn, c, wb);
   return BPP_OK;
 }

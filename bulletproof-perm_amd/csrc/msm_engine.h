@@ -12,6 +12,8 @@ uint32_t msm_choose_c(double n_per_msm);
 int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const uint32_t* d_off, uint32_t M,
                uint32_t T, uint32_t c, uint32_t wb, uint32_t Wn, const uint32_t* d_tbl, uint32_t** d_wsum_out,
                const uint32_t* d_tbl1 = nullptr, uint32_t n0 = 0xffffffffu, bool fb = false);
+// Window groups msm_single_dev pipelines over two child streams.
+uint32_t msm_window_groups(size_t n, uint32_t c, uint32_t Wn, bool indexed);
 int msm_single_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const uint32_t* d_tbl, size_t n,
                    uint32_t c, uint32_t wb, uint32_t Wn, h25519::ge* out);
 int upload_scalars(bpp_ctx* ctx, const uint8_t* scalars, size_t n, const char* name, uint32_t** d_out);

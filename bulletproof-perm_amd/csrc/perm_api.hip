@@ -628,18 +628,7 @@ int bpp_perm_prove_batch(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, size_t cou
           for (size_t i = b; i < e; ++i) Ps[i] = std::move(sub[i - b]);
       });
     for (auto& t : th) t.join();
-    if (ctx->prof)  // fold the children's stage times into this context's
-      for (bpp_ctx* kc : kids) {
-        double ms;
-        uint64_t n;
-        bpp_ctx_profile_get(kc, "", &ms, &n);  // resolves pending events
-        for (auto& kv : kc->prof_acc) {
-          auto& acc = ctx->prof_acc[kv.first];
-          acc.first += kv.second.first;
-          acc.second += kv.second.second;
-        }
-        bpp_ctx_profile_reset(kc);
-      }
+    // (the children's stage times fold into ctx's on its next profile query)
     for (size_t s = 0; s < S; ++s)
       if (rcs[s] != BPP_OK) {
         ctx->err = kids[s]->err;

@@ -79,6 +79,37 @@ FE_INLINE ge_p3 ge_msub(const ge_p3& p, const ge_niels& q) {
   return r;
 }
 
+// p + q (neg = false) or p - q (neg = true) without divergence: the sign
+// only swaps the (y+x, y-x) operands and the two D +- C sums, so a wave
+// whose lanes disagree on signs runs one 7M formula instead of both
+// ge_madd and ge_msub (or a carried fe_neg of 2dxy).  F, G are each either
+// the carried difference or the uncarried sum: both only feed multipliers.
+FE_INLINE ge_p3 ge_madd_signed(const ge_p3& p, const ge_niels& q, bool neg) {
+  fe qa, qb;
+  _Pragma("unroll") for (int i = 0; i < FE_LIMBS; ++i) {
+    qa.v[i] = neg ? q.ypx.v[i] : q.ymx.v[i];
+    qb.v[i] = neg ? q.ymx.v[i] : q.ypx.v[i];
+  }
+  fe A = fe_mul(fe_sub_nc(p.Y, p.X), qa);
+  fe B = fe_mul(fe_add_nc(p.Y, p.X), qb);
+  fe C = fe_mul(p.T, q.xy2d);
+  fe D = fe_add_nc(p.Z, p.Z);
+  fe E = fe_sub_nc(B, A);
+  fe H = fe_add_nc(B, A);
+  const fe Dm = fe_sub(D, C), Dp = fe_add_nc(D, C);
+  fe F, G;
+  _Pragma("unroll") for (int i = 0; i < FE_LIMBS; ++i) {
+    F.v[i] = neg ? Dp.v[i] : Dm.v[i];
+    G.v[i] = neg ? Dm.v[i] : Dp.v[i];
+  }
+  ge_p3 r;
+  r.X = fe_mul(E, F);
+  r.Y = fe_mul(G, H);
+  r.Z = fe_mul(F, G);
+  r.T = fe_mul(E, H);
+  return r;
+}
+
 FE_INLINE ge_niels ge_niels_neg(const ge_niels& q) {
   ge_niels r;
   r.ypx = q.ymx;

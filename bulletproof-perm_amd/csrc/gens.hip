@@ -73,7 +73,7 @@ __global__ void __launch_bounds__(256) k_pedersen(const uint32_t* __restrict__ f
       const int d = e[i];
       if (d == 0) continue;
       const ge_niels t = load_niels(fb, i * 8 + (uint32_t)((d < 0 ? -d : d) - 1));
-      acc = d < 0 ? ge_msub(acc, t) : ge_madd(acc, t);
+      acc = ge_madd_signed(acc, t, d < 0);
     }
     _Pragma("unroll") for (int i = 0; i < 8; ++i) s[i] = gam[8 * j + i];
     radix16(s, e);
@@ -81,7 +81,7 @@ __global__ void __launch_bounds__(256) k_pedersen(const uint32_t* __restrict__ f
       const int d = e[i];
       if (d == 0) continue;
       const ge_niels t = load_niels(fb, FB_POS * 8 + i * 8 + (uint32_t)((d < 0 ? -d : d) - 1));
-      acc = d < 0 ? ge_msub(acc, t) : ge_madd(acc, t);
+      acc = ge_madd_signed(acc, t, d < 0);
     }
   }
   _Pragma("unroll") for (int off = 1; off < PED_G; off <<= 1) {

@@ -173,14 +173,18 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
     // head/tail pieces for k_msm_fixup (2^20: K = 64 measured best of 32/64/128)
     uint32_t K = 4;
     while (K < 128 && E_max / (2 * K) >= 256u * 1024u) K <<= 1;
-    if (const char* ek = getenv("BPP_MSM_K")) K = std::max<uint32_t>(4, (uint32_t)atoi(ek) & ~3u);
+    if (const char* ek = getenv("BPP_MSM_K")) {  // rounded down to a power of two >= 4
+      const uint32_t want = std::max(4, atoi(ek));
+      for (K = 4; K * 2 <= want; K *= 2) {
+      }
+    }
     const size_t lanes = (E_max + K - 1) / K + 1;
     void *head, *tail;
     BPP_TRY(ctx_ws(ctx, "msm_head", lanes * P3_BYTES, &head));
     BPP_TRY(ctx_ws(ctx, "msm_tail", lanes * P3_BYTES, &tail));
     {
       ProfScope ps(ctx, "msm_accumulate");
-      hipLaunchKernelGGL(k_msm_accumulate, dim3(grid_for(lanes, 256)), dim3(256), 0, ctx->stream, d_tbl, d_tbl1, n0,
+      hipLaunchKernelGGL(k_msm_accumulate, dim3(grid_for(lanes, ACC_T)), dim3(ACC_T), 0, ctx->stream, d_tbl, d_tbl1, n0,
                          (const uint32_t*)entries, (const uint32_t*)boff, (uint32_t)NB, K, (uint32_t*)bsum,
                          (uint32_t*)head, (uint32_t*)tail);
     }

@@ -120,10 +120,12 @@ __global__ void k_msm_scatter(const uint32_t* __restrict__ scalars, const uint32
   });
 }
 
+// 4 waves per SIMD (<= 128 VGPRs; the LDS piece buffer also allows 4):
+// without the bound the post-barrier fold lifts the kernel to 187 VGPRs.
 #ifdef ACC_WAVES5
 #define ACC_ATTR __attribute__((amdgpu_waves_per_eu(5, 8)))
 #else
-#define ACC_ATTR
+#define ACC_ATTR __attribute__((amdgpu_waves_per_eu(4, 8)))
 #endif
 
 // Largest b with boff[b] <= i (boff non-decreasing, boff[0] = 0, i < boff[nb]).
@@ -146,62 +148,105 @@ FE_INLINE ge_niels fetch_entry(const uint32_t* __restrict__ tbl, const uint32_t*
   return q;
 }
 
+// A bucket spanning more than FIX_MAX chunks (bucket skew: the few buckets
+// of a narrow top window, equal scalars) is listed in heavy[1..] (count in
+// heavy[0]) by k_msm_fixup and summed by a whole wave instead of one lane's
+// serial chain.
+#define FIX_MAX 16
+#define ACC_T 256
+
 // Balanced bucket accumulation: lane l owns entries [l*K, (l+1)*K) of the
 // bucket-sorted entry array, so every lane does exactly K mixed additions
 // whatever the bucket-size distribution (the top window of a 253-bit scalar
 // is 8x denser than the others at c = 16).  A run (a bucket's entries inside
-// one chunk) that covers its whole bucket is written to bsum directly; the
-// first / last run of a chunk whose bucket crosses the chunk border goes to
-// head[l] / tail[l] and k_msm_fixup adds the pieces.
+// one chunk) that covers its whole bucket is written to bsum directly.  A
+// bucket crossing chunk borders is finished inside the workgroup when it can
+// be: the lanes holding its later pieces park them in LDS, and after a
+// barrier the lane where it starts adds them and writes bsum.  Only buckets
+// that leave the workgroup (or are heavy) keep global pieces -- the owner's
+// partial in tail[l], later pieces in head[l] -- for k_msm_fixup.
 // Points with index < n0 come from tbl, the rest from tbl1[idx - n0] (so a
 // proof's own points can join the resident generators without a copy).
-__global__ void __launch_bounds__(256) ACC_ATTR k_msm_accumulate(const uint32_t* __restrict__ tbl,
+__global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_t* __restrict__ tbl,
                                                        const uint32_t* __restrict__ tbl1, uint32_t n0,
                                                        const uint32_t* __restrict__ entries,
                                                        const uint32_t* __restrict__ boff, uint32_t nbuckets,
                                                        uint32_t K, uint32_t* __restrict__ bsum,
                                                        uint32_t* __restrict__ head, uint32_t* __restrict__ tail) {
-  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+  // K is a power of two (msm_engine)
+  __shared__ __attribute__((aligned(16))) uint32_t piece[ACC_T * P3_WORDS];
+  const uint32_t ks = 31 - __clz(K);
+  const uint32_t l = blockIdx.x * ACC_T + threadIdx.x;
+  const uint32_t lane_first = blockIdx.x * ACC_T, lane_last = lane_first + ACC_T - 1;
   const uint32_t E = boff[nbuckets];
   const uint32_t i0 = l * K;
-  if (i0 >= E) return;
   const uint32_t i1 = min(i0 + K, E);
-  uint32_t b = bucket_of(boff, nbuckets, i0);
-  uint32_t bstart = boff[b], bend = boff[b + 1];
-  bool first = true;
+  // a later piece of a bucket that started in an earlier chunk: to LDS when
+  // its owner is in this workgroup and will fold it, else to head[l]
+  auto park = [&](const ge_p3& v, uint32_t s, uint32_t e) {
+    const uint32_t l0 = s >> ks;
+    uint32_t* dst = ((((e - 1) >> ks) - l0) < FIX_MAX && l0 >= lane_first) ? piece + threadIdx.x * P3_WORDS
+                                                                           : head + (size_t)l * P3_WORDS;
+    store_p3(dst, 0, v);
+  };
+  bool owner = false;
+  uint32_t b = 0, bstart = 0, bend = 0;
   ge_p3 acc = ge_identity();
-  // entries are read 4 at a time (one 16-B load; K is a multiple of 4 and
-  // the array is padded): a lane's chunk is contiguous, so per-entry 4-B
-  // loads touch the same 128-B line K times across a long loop and
-  // re-fetch it once the table gathers have evicted it
-  uint4 e4 = make_uint4(0, 0, 0, 0);
-  for (uint32_t i = i0; i < i1; ++i) {
-    if (((i - i0) & 3u) == 0) e4 = *reinterpret_cast<const uint4*>(entries + i);
-    const uint32_t q = (i - i0) & 3u;
-    const uint32_t e = q == 0 ? e4.x : q == 1 ? e4.y : q == 2 ? e4.z : e4.w;
-    if (i == bend) {  // close the run of bucket b
-      if (bstart >= i0) store_p3(bsum, b, acc);  // whole bucket inside the chunk
-      else store_p3(head, l, acc);               // first run, bucket started earlier
-      first = false;
-      do { ++b; } while (boff[b + 1] <= i);
-      bstart = boff[b];
-      bend = boff[b + 1];
-      acc = ge_identity();
+  if (i0 < E) {
+    b = bucket_of(boff, nbuckets, i0);
+    bstart = boff[b];
+    bend = boff[b + 1];
+    // entries are read 4 at a time (one 16-B load; K is a multiple of 4 and
+    // the array is padded): a lane's chunk is contiguous, so per-entry 4-B
+    // loads touch the same 128-B line K times across a long loop and
+    // re-fetch it once the table gathers have evicted it
+    uint4 e4 = make_uint4(0, 0, 0, 0);
+    for (uint32_t i = i0; i < i1; ++i) {
+      if (((i - i0) & 3u) == 0) e4 = *reinterpret_cast<const uint4*>(entries + i);
+      const uint32_t q = (i - i0) & 3u;
+      const uint32_t e = q == 0 ? e4.x : q == 1 ? e4.y : q == 2 ? e4.z : e4.w;
+      if (i == bend) {  // close the run of bucket b
+        if (bstart >= i0) {
+          store_p3(bsum, b, acc);  // whole bucket inside the chunk
+        } else {
+          park(acc, bstart, bend);  // first run, bucket started earlier
+        }
+        do { ++b; } while (boff[b + 1] <= i);
+        bstart = boff[b];
+        bend = boff[b + 1];
+        acc = ge_identity();
+      }
+      acc = ge_madd(acc, fetch_entry(tbl, tbl1, n0, e));
     }
-    acc = ge_madd(acc, fetch_entry(tbl, tbl1, n0, e));
+    // last run [max(bstart, i0), i1)
+    if (bstart >= i0 && bend <= i1) {
+      store_p3(bsum, b, acc);
+    } else if (bstart < i0) {  // single run crossing both borders
+      park(acc, bstart, bend);
+    } else {  // bucket starts here and continues: its partial waits in
+      owner = true;  // tail[l] (holding it in registers across the barrier
+      store_p3(tail, l, acc);  // costs ~20 VGPRs in the main loop)
+    }
   }
-  // last run [max(bstart, i0), i1)
-  if (bstart >= i0 && bend <= i1) store_p3(bsum, b, acc);
-  else if (first) store_p3(head, l, acc);  // single run crossing a border
-  else store_p3(tail, l, acc);
+  __syncthreads();
+  if (owner) {
+    const uint32_t l1 = (bend - 1) >> ks;
+    if (l1 - l >= FIX_MAX) {  // heavy: k_msm_fixup_heavy's piece convention
+      if (bstart == i0) store_p3(head, l, load_p3(tail, l));
+      return;
+    }
+    const uint32_t last = min(l1, lane_last);
+    acc = load_p3(tail, l);
+    for (uint32_t m = l + 1; m <= last; ++m) acc = ge_add(acc, load_p3(piece, m - lane_first));
+    if (l1 <= lane_last) store_p3(bsum, b, acc);
+    else store_p3(tail, l, acc);  // continues past this workgroup
+  }
 }
 
 // One lane per bucket: identity for empty buckets, and the sum of the
-// pieces for buckets that cross chunk borders.
-// A bucket spanning more than FIX_MAX chunks (bucket skew: the few buckets
-// of a narrow top window, equal scalars) is listed in heavy[1..] (count in
-// heavy[0]) and summed by a whole wave instead of one lane's serial chain.
-#define FIX_MAX 16
+// global pieces of buckets that leave their owner's workgroup (tail[l0] =
+// the owner's partial including its workgroup's pieces, head[l] for lanes of
+// later workgroups); heavy buckets are listed for k_msm_fixup_heavy.
 __global__ void __launch_bounds__(256) k_msm_fixup(const uint32_t* __restrict__ boff, uint32_t nbuckets, uint32_t K,
                             const uint32_t* __restrict__ head, const uint32_t* __restrict__ tail,
                             uint32_t* __restrict__ bsum, uint32_t* __restrict__ heavy) {
@@ -218,8 +263,10 @@ __global__ void __launch_bounds__(256) k_msm_fixup(const uint32_t* __restrict__ 
     heavy[1 + atomicAdd(&heavy[0], 1u)] = b;
     return;
   }
-  ge_p3 acc = (s == l0 * K) ? load_p3(head, l0) : load_p3(tail, l0);
-  for (uint32_t l = l0 + 1; l <= l1; ++l) acc = ge_add(acc, load_p3(head, l));
+  const uint32_t next_wg = (l0 / ACC_T + 1) * ACC_T;
+  if (l1 < next_wg) return;  // finished inside the owner's workgroup
+  ge_p3 acc = load_p3(tail, l0);
+  for (uint32_t l = next_wg; l <= l1; ++l) acc = ge_add(acc, load_p3(head, l));
   store_p3(bsum, b, acc);
 }
 

@@ -170,7 +170,7 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
     const uint32_t E_max = T * Wn;
     // K = entries per lane: about one round of lanes at the accumulate's
     // 4 waves/SIMD occupancy (256 K lanes) -- fewer chunk borders, so fewer
-    // head/tail pieces for k_msm_fixup (2^20: K = 64 measured best of 32/64/128)
+    // head/tail pieces (2^20: K = 64 measured best of 32/64/128)
     uint32_t K = 4;
     while (K < 128 && E_max / (2 * K) >= 256u * 1024u) K <<= 1;
     if (const char* ek = getenv("BPP_MSM_K")) {  // rounded down to a power of two >= 4
@@ -179,41 +179,38 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
       }
     }
     const size_t lanes = (E_max + K - 1) / K + 1;
-    void *head, *tail;
+    uint32_t ks = 0;
+    while ((1u << ks) < K) ++ks;
+    // a heavy bucket spans > FIX_MAX chunks, so holds > (FIX_MAX - 1) K
+    // entries: at most E / ((FIX_MAX - 1) K) + 1 of them
+    const size_t max_heavy = std::min<size_t>(NB, E_max / ((size_t)(FIX_MAX - 1) * K) + 1);
+    void *head, *tail, *heavy;
     BPP_TRY(ctx_ws(ctx, "msm_head", lanes * P3_BYTES, &head));
     BPP_TRY(ctx_ws(ctx, "msm_tail", lanes * P3_BYTES, &tail));
+    BPP_TRY(ctx_ws(ctx, "msm_heavy", (max_heavy + 1) * 4, &heavy));
+    BPP_HIP(hipMemsetAsync(heavy, 0, 4, ctx->stream));
     {
       ProfScope ps(ctx, "msm_accumulate");
-      hipLaunchKernelGGL(k_msm_accumulate, dim3(grid_for(lanes, ACC_T)), dim3(ACC_T), 0, ctx->stream, d_tbl, d_tbl1, n0,
-                         (const uint32_t*)entries, (const uint32_t*)boff, (uint32_t)NB, K, (uint32_t*)bsum,
-                         (uint32_t*)head, (uint32_t*)tail);
+      hipLaunchKernelGGL(k_msm_accumulate, dim3(grid_for(lanes, ACC_T)), dim3(ACC_T), 0, ctx->stream, d_tbl, d_tbl1,
+                         n0, (const uint32_t*)entries, (const uint32_t*)boff, (uint32_t)NB, K, (uint32_t*)bsum,
+                         (uint32_t*)head, (uint32_t*)tail, (uint32_t*)heavy);
     }
     BPP_TRY(ctx_check_launch(ctx, "k_msm_accumulate"));
     {
-      // a heavy bucket spans > FIX_MAX chunks, so holds > (FIX_MAX - 1) K
-      // entries: at most E / ((FIX_MAX - 1) K) + 1 of them
-      const size_t max_heavy = std::min<size_t>(NB, E_max / ((size_t)(FIX_MAX - 1) * K) + 1);
-      void* heavy = nullptr;
-      BPP_TRY(ctx_ws(ctx, "msm_heavy", (max_heavy + 1) * 4, &heavy));
-      BPP_HIP(hipMemsetAsync(heavy, 0, 4, ctx->stream));
       ProfScope ps(ctx, "msm_fixup");
-      hipLaunchKernelGGL(k_msm_fixup, dim3(grid_for(NB, 256)), dim3(256), 0, ctx->stream, (const uint32_t*)boff,
-                         (uint32_t)NB, K, (const uint32_t*)head, (const uint32_t*)tail, (uint32_t*)bsum,
-                         (uint32_t*)heavy);
       hipLaunchKernelGGL(k_msm_fixup_heavy, dim3((unsigned)max_heavy), dim3(64), 0, ctx->stream,
                          (const uint32_t*)boff, K, (const uint32_t*)head, (const uint32_t*)tail,
                          (const uint32_t*)heavy, (uint32_t*)bsum);
     }
-    BPP_TRY(ctx_check_launch(ctx, "k_msm_fixup"));
-  }
-  {
-    const uint32_t L = g.B >= 512 ? 8 : (g.B >= 64 ? 4 : (g.B >= 8 ? 2 : 1));
+    BPP_TRY(ctx_check_launch(ctx, "k_msm_fixup_heavy"));
+    const uint32_t L = g.B >= 512 ? 8 : (g.B >= 64 ? 4 : (g.B >= 8 ? 2 : 1));  // <= RED_LMAX
     const uint32_t BPS = (g.B + RED_T * L - 1) / (RED_T * L);
     void* part = wsum;  // one block per segment: its partial is the sum
     if (BPS > 1) BPP_TRY(ctx_ws(ctx, "msm_rpart", nseg * BPS * P3_BYTES, &part));
     ProfScope ps(ctx, "msm_reduce");
     hipLaunchKernelGGL(k_msm_reduce_partial, dim3((unsigned)(nseg * BPS)), dim3(RED_T), 0, ctx->stream,
-                       (const uint32_t*)bsum, g, L, BPS, (uint32_t*)part);
+                       (const uint32_t*)boff, ks, (const uint32_t*)head, (const uint32_t*)tail, (const uint32_t*)bsum,
+                       g, L, BPS, (uint32_t*)part);
     if (BPS > 1)
       hipLaunchKernelGGL(k_msm_reduce_final, dim3((unsigned)nseg), dim3(RED_T), 0, ctx->stream,
                          (const uint32_t*)part, BPS, (uint32_t*)wsum);

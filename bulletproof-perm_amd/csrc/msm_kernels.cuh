@@ -150,8 +150,8 @@ FE_INLINE ge_niels fetch_entry(const uint32_t* __restrict__ tbl, const uint32_t*
 
 // A bucket spanning more than FIX_MAX chunks (bucket skew: the few buckets
 // of a narrow top window, equal scalars) is listed in heavy[1..] (count in
-// heavy[0]) by k_msm_fixup and summed by a whole wave instead of one lane's
-// serial chain.
+// heavy[0]) by the lane where it starts and summed by a whole wave
+// (k_msm_fixup_heavy) instead of one lane's serial chain.
 #define FIX_MAX 16
 #define ACC_T 256
 
@@ -164,7 +164,8 @@ FE_INLINE ge_niels fetch_entry(const uint32_t* __restrict__ tbl, const uint32_t*
 // be: the lanes holding its later pieces park them in LDS, and after a
 // barrier the lane where it starts adds them and writes bsum.  Only buckets
 // that leave the workgroup (or are heavy) keep global pieces -- the owner's
-// partial in tail[l], later pieces in head[l] -- for k_msm_fixup.
+// partial in tail[l], later pieces in head[l] -- and are assembled by the
+// bucket reduction (bucket_total); empty buckets are never written.
 // Points with index < n0 come from tbl, the rest from tbl1[idx - n0] (so a
 // proof's own points can join the resident generators without a copy).
 __global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_t* __restrict__ tbl,
@@ -172,7 +173,8 @@ __global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_
                                                        const uint32_t* __restrict__ entries,
                                                        const uint32_t* __restrict__ boff, uint32_t nbuckets,
                                                        uint32_t K, uint32_t* __restrict__ bsum,
-                                                       uint32_t* __restrict__ head, uint32_t* __restrict__ tail) {
+                                                       uint32_t* __restrict__ head, uint32_t* __restrict__ tail,
+                                                       uint32_t* __restrict__ heavy) {
   // K is a power of two (msm_engine)
   __shared__ __attribute__((aligned(16))) uint32_t piece[ACC_T * P3_WORDS];
   const uint32_t ks = 31 - __clz(K);
@@ -196,6 +198,8 @@ __global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_
     b = bucket_of(boff, nbuckets, i0);
     bstart = boff[b];
     bend = boff[b + 1];
+    // the lane where a bucket starts lists it if it is heavy
+    if (bstart == i0 && ((bend - 1) >> ks) - l >= FIX_MAX) heavy[1 + atomicAdd(&heavy[0], 1u)] = b;
     // entries are read 4 at a time (one 16-B load; K is a multiple of 4 and
     // the array is padded): a lane's chunk is contiguous, so per-entry 4-B
     // loads touch the same 128-B line K times across a long loop and
@@ -214,6 +218,7 @@ __global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_
         do { ++b; } while (boff[b + 1] <= i);
         bstart = boff[b];
         bend = boff[b + 1];
+        if (((bend - 1) >> ks) - l >= FIX_MAX) heavy[1 + atomicAdd(&heavy[0], 1u)] = b;
         acc = ge_identity();
       }
       acc = ge_madd(acc, fetch_entry(tbl, tbl1, n0, e));
@@ -243,41 +248,29 @@ __global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_
   }
 }
 
-// One lane per bucket: identity for empty buckets, and the sum of the
-// global pieces of buckets that leave their owner's workgroup (tail[l0] =
-// the owner's partial including its workgroup's pieces, head[l] for lanes of
-// later workgroups); heavy buckets are listed for k_msm_fixup_heavy.
-__global__ void __launch_bounds__(256) k_msm_fixup(const uint32_t* __restrict__ boff, uint32_t nbuckets, uint32_t K,
-                            const uint32_t* __restrict__ head, const uint32_t* __restrict__ tail,
-                            uint32_t* __restrict__ bsum, uint32_t* __restrict__ heavy) {
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nbuckets) return;
-  const uint32_t s = boff[b], e = boff[b + 1];
-  if (s == e) {
-    store_p3(bsum, b, ge_identity());
-    return;
-  }
-  const uint32_t l0 = s / K, l1 = (e - 1) / K;
-  if (l0 == l1) return;  // written by the accumulate lane
-  if (l1 - l0 >= FIX_MAX) {  // heavy (skewed) bucket: one wave in k_msm_fixup_heavy
-    heavy[1 + atomicAdd(&heavy[0], 1u)] = b;
-    return;
-  }
+// Total of non-empty bucket b (global index) spanning entries [bs, be):
+// bsum[b] unless the bucket left its owner's workgroup without being heavy
+// (then the owner's partial tail[l0] plus the head pieces of the lanes of
+// later workgroups).
+FE_INLINE ge_p3 bucket_total(size_t b, uint32_t bs, uint32_t be, uint32_t ks, const uint32_t* __restrict__ head,
+                             const uint32_t* __restrict__ tail, const uint32_t* __restrict__ bsum) {
+  const uint32_t l0 = bs >> ks, l1 = (be - 1) >> ks;
   const uint32_t next_wg = (l0 / ACC_T + 1) * ACC_T;
-  if (l1 < next_wg) return;  // finished inside the owner's workgroup
-  ge_p3 acc = load_p3(tail, l0);
-  for (uint32_t l = next_wg; l <= l1; ++l) acc = ge_add(acc, load_p3(head, l));
-  store_p3(bsum, b, acc);
+  if (l1 < next_wg || l1 - l0 >= FIX_MAX) return load_p3(bsum, b);
+  ge_p3 v = load_p3(tail, l0);
+  for (uint32_t l = next_wg; l <= l1; ++l) v = ge_add(v, load_p3(head, l));
+  return v;
 }
 
 // Bucket reduction sum_b (b+1) * bsum[b] per segment (msm, window), in two
 // launches so that enough lanes are in flight (the work is ~1/16 of the
 // accumulation but latency-bound if given few lanes):
 //   k_msm_reduce_partial: block (seg, j) of 64 lanes; lane t owns L buckets
-//     [lo, lo+L): running sum from the top gives sum (b-lo+1) B_b and
+//     [lo, lo+L) (bucket_total; empty ones are skipped): running sum from the top gives sum (b-lo+1) B_b and
 //     run = sum B_b, plus lo*run by double-and-add; LDS tree over the wave.
 //   k_msm_reduce_final: one 64-lane block per segment sums its BPS partials.
 #define RED_T 64
+#define RED_LMAX 8
 FE_INLINE ge_p3 lds_tree_sum(uint32_t* lds, ge_p3 v) {
   store_p3(lds, threadIdx.x, v);
   __syncthreads();
@@ -288,7 +281,10 @@ FE_INLINE ge_p3 lds_tree_sum(uint32_t* lds, ge_p3 v) {
   return load_p3(lds, 0);
 }
 
-__global__ void __launch_bounds__(RED_T) k_msm_reduce_partial(const uint32_t* __restrict__ bsum, MsmGeom g,
+__global__ void __launch_bounds__(RED_T) k_msm_reduce_partial(const uint32_t* __restrict__ boff, uint32_t ks,
+                                                             const uint32_t* __restrict__ head,
+                                                             const uint32_t* __restrict__ tail,
+                                                             const uint32_t* __restrict__ bsum, MsmGeom g,
                                                              uint32_t L, uint32_t BPS, uint32_t* __restrict__ part) {
   __shared__ uint32_t lds[RED_T * P3_WORDS];
   const uint32_t seg = blockIdx.x / BPS, j = blockIdx.x % BPS;
@@ -297,8 +293,14 @@ __global__ void __launch_bounds__(RED_T) k_msm_reduce_partial(const uint32_t* __
   const size_t base = (size_t)seg * g.B;
   ge_p3 run = ge_identity();
   ge_p3 acc = ge_identity();
+  // bucket offsets of the lane's range up front (L <= RED_LMAX): the
+  // bucket loads below then do not wait on them one by one
+  const uint32_t nb = lo < hi ? hi - lo : 0u;
+  uint32_t bo[RED_LMAX + 1];
+  _Pragma("unroll") for (uint32_t k = 0; k <= RED_LMAX; ++k) bo[k] = (nb && k <= nb) ? boff[base + lo + k] : 0u;
   for (uint32_t b = hi; b > lo; --b) {
-    run = ge_add(run, load_p3(bsum, base + b - 1));
+    const uint32_t bs = bo[b - 1 - lo], be = bo[b - lo];
+    if (bs != be) run = ge_add(run, bucket_total(base + b - 1, bs, be, ks, head, tail, bsum));
     acc = ge_add(acc, run);
   }
   if (lo < hi && lo > 0) {  // + lo * run

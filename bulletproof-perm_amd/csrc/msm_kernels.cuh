@@ -436,18 +436,28 @@ __global__ void __launch_bounds__(SORT_T) k_msm_scatter_lds(const uint32_t* __re
 #define RS_CHUNK 4096  // digits per block in the coarse passes (LDS staging)
 #define RS_FMASK (0x7fu << 24)
 
+// Digits of a chunk are loaded into registers in one batch of independent
+// coalesced loads (RS_PER per thread) before any LDS atomic: a load-then-
+// atomic loop leaves each load's latency exposed.
+#define RS_PER (RS_CHUNK / RS_T)
+FE_INLINE void rs_load_chunk(const uint32_t* __restrict__ dw, uint32_t t0, uint32_t t1, uint32_t v[RS_PER]) {
+  _Pragma("unroll") for (uint32_t k = 0; k < RS_PER; ++k) {
+    const uint32_t t = t0 + k * RS_T + threadIdx.x;
+    v[k] = t < t1 ? dw[t] : DIG_ZERO;
+  }
+}
+
 __global__ void __launch_bounds__(RS_T) k_rsort_count(const uint32_t* __restrict__ dig, MsmGeom g, uint32_t chunk,
                                                      uint32_t nchunk, uint32_t NC, uint32_t* __restrict__ cntA) {
   __shared__ uint32_t h[256];
   const uint32_t w = blockIdx.x / nchunk, ch = blockIdx.x % nchunk;
   for (uint32_t b = threadIdx.x; b < NC; b += RS_T) h[b] = 0;
+  const uint32_t t0 = ch * chunk, t1 = min(t0 + chunk, g.T);  // chunk == RS_CHUNK
+  uint32_t v[RS_PER];
+  rs_load_chunk(dig + (size_t)w * g.T, t0, t1, v);
   __syncthreads();
-  const uint32_t t0 = ch * chunk, t1 = min(t0 + chunk, g.T);
-  const uint32_t* dw = dig + (size_t)w * g.T;
-  for (uint32_t t = t0 + threadIdx.x; t < t1; t += RS_T) {
-    const uint32_t code = dw[t];
-    if (code != DIG_ZERO) atomicAdd(&h[(code & ~DIG_SIGN) >> RS_FINE_BITS], 1u);
-  }
+  _Pragma("unroll") for (uint32_t k = 0; k < RS_PER; ++k)
+    if (v[k] != DIG_ZERO) atomicAdd(&h[(v[k] & ~DIG_SIGN) >> RS_FINE_BITS], 1u);
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < NC; b += RS_T) cntA[((size_t)w * NC + b) * nchunk + ch] = h[b];
 }
@@ -488,11 +498,10 @@ __global__ void __launch_bounds__(RS_T) k_rsort_scatter(const uint32_t* __restri
   for (uint32_t b = threadIdx.x; b < 256; b += RS_T) cnt[b] = 0;
   __syncthreads();
   const uint32_t t0 = ch * RS_CHUNK, t1 = min(t0 + RS_CHUNK, g.T);
-  const uint32_t* dw = dig + (size_t)w * g.T;
-  for (uint32_t t = t0 + threadIdx.x; t < t1; t += RS_T) {
-    const uint32_t code = dw[t];
-    if (code != DIG_ZERO) atomicAdd(&cnt[(code & ~DIG_SIGN) >> RS_FINE_BITS], 1u);
-  }
+  uint32_t v[RS_PER];
+  rs_load_chunk(dig + (size_t)w * g.T, t0, t1, v);
+  _Pragma("unroll") for (uint32_t k = 0; k < RS_PER; ++k)
+    if (v[k] != DIG_ZERO) atomicAdd(&cnt[(v[k] & ~DIG_SIGN) >> RS_FINE_BITS], 1u);
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < 256; b += RS_T) {
     loc[b] = cnt[b];
@@ -503,9 +512,10 @@ __global__ void __launch_bounds__(RS_T) k_rsort_scatter(const uint32_t* __restri
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < 256; b += RS_T) cnt[b] = loc[b];  // cursors
   __syncthreads();
-  for (uint32_t t = t0 + threadIdx.x; t < t1; t += RS_T) {
-    const uint32_t code = dw[t];
+  _Pragma("unroll") for (uint32_t k = 0; k < RS_PER; ++k) {
+    const uint32_t code = v[k];
     if (code == DIG_ZERO) continue;
+    const uint32_t t = t0 + k * RS_T + threadIdx.x;
     const uint32_t b = code & ~DIG_SIGN, bin = b >> RS_FINE_BITS;
     const uint32_t p = atomicAdd(&cnt[bin], 1u);
     stage[p] = (pidx ? pidx[t] : t) | ((b & (RS_FINE_N - 1)) << 24) | (code & DIG_SIGN);
@@ -524,6 +534,7 @@ __global__ void __launch_bounds__(RS_T) k_rsort_scatter(const uint32_t* __restri
 // A segment that fits one tile (all but the top window's, typically) is
 // read twice; longer ones get a counting pass first.
 #define RS_FTILE 8192
+#define RS_FPER (RS_FTILE / RS_T)
 __global__ void __launch_bounds__(RS_T) k_rsort_fine(const uint32_t* __restrict__ tmpA, uint32_t nchunk,
                                                     const uint32_t* __restrict__ offA, uint32_t* __restrict__ boff,
                                                     uint32_t* __restrict__ entries) {
@@ -532,7 +543,38 @@ __global__ void __launch_bounds__(RS_T) k_rsort_fine(const uint32_t* __restrict_
   __shared__ uint8_t sf[RS_FTILE];
   const uint32_t seg = blockIdx.x;  // w * NC + coarse bin
   const uint32_t s = offA[(size_t)seg * nchunk], e = offA[(size_t)(seg + 1) * nchunk];
-  const bool one_tile = e - s <= RS_FTILE;
+  if (e - s <= RS_FTILE) {  // one tile, held in registers between the passes
+    uint32_t v[RS_FPER];
+    _Pragma("unroll") for (uint32_t k = 0; k < RS_FPER; ++k) {
+      const uint32_t i = s + k * RS_T + threadIdx.x;
+      v[k] = i < e ? tmpA[i] : 0u;
+    }
+    if (threadIdx.x < RS_FINE_N) lcnt[threadIdx.x] = 0;
+    __syncthreads();
+    _Pragma("unroll") for (uint32_t k = 0; k < RS_FPER; ++k)
+      if (k * RS_T + threadIdx.x < e - s) atomicAdd(&lcnt[(v[k] >> 24) & 0x7fu], 1u);
+    __syncthreads();
+    if (threadIdx.x < RS_FINE_N) lloc[threadIdx.x] = lcnt[threadIdx.x];
+    __syncthreads();
+    lds_excl_scan_w0(lloc, 2, 0);
+    __syncthreads();
+    if (threadIdx.x < RS_FINE_N) {
+      lcnt[threadIdx.x] = lloc[threadIdx.x];  // cursors
+      boff[(size_t)seg * RS_FINE_N + threadIdx.x] = s + lloc[threadIdx.x];
+    }
+    __syncthreads();
+    _Pragma("unroll") for (uint32_t k = 0; k < RS_FPER; ++k) {
+      if (k * RS_T + threadIdx.x >= e - s) continue;
+      const uint32_t f = (v[k] >> 24) & 0x7fu;
+      stage[atomicAdd(&lcnt[f], 1u)] = v[k] & ~RS_FMASK;
+    }
+    __syncthreads();
+    // stage is sorted by fine bin and the segment's entries are contiguous
+    // in the output: one coalesced copy
+    for (uint32_t j = threadIdx.x; j < e - s; j += RS_T) entries[s + j] = stage[j];
+    return;
+  }
+  const bool one_tile = false;
   if (!one_tile) {
     if (threadIdx.x < RS_FINE_N) base[threadIdx.x] = 0;
     __syncthreads();

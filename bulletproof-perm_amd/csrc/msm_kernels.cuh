@@ -533,7 +533,9 @@ __global__ void __launch_bounds__(RS_T) k_rsort_scatter(const uint32_t* __restri
 // fine bits, in LDS tiles of RS_FTILE entries with coalesced output runs.
 // A segment that fits one tile (all but the top window's, typically) is
 // read twice; longer ones get a counting pass first.
+#ifndef RS_FTILE
 #define RS_FTILE 8192
+#endif
 #define RS_FPER (RS_FTILE / RS_T)
 __global__ void __launch_bounds__(RS_T) k_rsort_fine(const uint32_t* __restrict__ tmpA, uint32_t nchunk,
                                                     const uint32_t* __restrict__ offA, uint32_t* __restrict__ boff,
@@ -541,7 +543,9 @@ __global__ void __launch_bounds__(RS_T) k_rsort_fine(const uint32_t* __restrict_
   __shared__ uint32_t base[RS_FINE_N], lcnt[RS_FINE_N], lloc[RS_FINE_N];
   __shared__ uint32_t stage[RS_FTILE];
   __shared__ uint8_t sf[RS_FTILE];
-  const uint32_t seg = blockIdx.x;  // w * NC + coarse bin
+  // w * NC + coarse bin, last first: the top window's few dense bins take
+  // the multi-tile path and should not be the grid's tail
+  const uint32_t seg = gridDim.x - 1 - blockIdx.x;
   const uint32_t s = offA[(size_t)seg * nchunk], e = offA[(size_t)(seg + 1) * nchunk];
   if (e - s <= RS_FTILE) {  // one tile, held in registers between the passes
     uint32_t v[RS_FPER];

@@ -7,6 +7,7 @@
 #pragma once
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -43,75 +44,89 @@ inline unsigned threads() {
   return n;
 }
 
+// Workers spin (with pause) for ~BPP_POOL_SPIN_US after each job before
+// sleeping on a condition variable, so the prover's stream of short host
+// phases (one every 0.1-0.3 ms) is not paid in futex wake-ups; the caller
+// waits only until every item is done and every worker that entered the
+// job has left it.
 class Pool {
  public:
   explicit Pool(unsigned workers) {
+    const char* e = getenv("BPP_POOL_SPIN_US");
+    spin_us_ = e ? atoi(e) : 300;
     for (unsigned i = 0; i < workers; ++i) th_.emplace_back([this] { loop(); });
   }
   ~Pool() {
     {
       std::lock_guard<std::mutex> g(mu_);
-      stop_ = true;
+      stop_.store(true);
     }
     cv_.notify_all();
     for (auto& t : th_) t.join();
   }
   void run(size_t n, const std::function<void(size_t)>& f) {
     std::lock_guard<std::mutex> call(call_mu_);
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      job_ = &f;
-      n_ = n;
-      next_.store(0);
-      active_ = (unsigned)th_.size();
-      ++gen_;
+    n_ = n;
+    next_.store(0);
+    done_.store(0);
+    job_.store(&f);
+    gen_.fetch_add(1);
+    if (sleepers_.load() > 0) {
+      { std::lock_guard<std::mutex> g(mu_); }
+      cv_.notify_all();
     }
-    cv_.notify_all();
     work(f, n);
-    std::unique_lock<std::mutex> g(mu_);
-    done_.wait(g, [this] { return active_ == 0; });
-    job_ = nullptr;
+    while (done_.load() < n) cpu_relax();
+    job_.store(nullptr);
+    while (inside_.load() != 0) cpu_relax();
   }
   static bool in_worker() { return tl_worker(); }
 
  private:
+  static void cpu_relax() { __builtin_ia32_pause(); }
   static bool& tl_worker() {
     static thread_local bool w = false;
     return w;
   }
   void work(const std::function<void(size_t)>& f, size_t n) {
-    for (size_t i; (i = next_.fetch_add(1)) < n;) f(i);
+    size_t k = 0;
+    for (size_t i; (i = next_.fetch_add(1)) < n; ++k) f(i);
+    if (k) done_.fetch_add(k);
   }
   void loop() {
     tl_worker() = true;
-    uint64_t seen = 0;
+    uint64_t seen = gen_.load();
     for (;;) {
-      const std::function<void(size_t)>* f;
-      size_t n;
-      {
-        std::unique_lock<std::mutex> g(mu_);
-        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
-        if (stop_) return;
-        seen = gen_;
-        f = job_;
-        n = n_;
+      // spin for a new generation, then sleep
+      auto t0 = std::chrono::steady_clock::now();
+      for (unsigned it = 0; gen_.load() == seen && !stop_.load(); ++it) {
+        cpu_relax();
+        if ((it & 255u) == 0 &&
+            std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us_)) {
+          std::unique_lock<std::mutex> g(mu_);
+          sleepers_.fetch_add(1);
+          cv_.wait(g, [&] { return stop_.load() || gen_.load() != seen; });
+          sleepers_.fetch_sub(1);
+          break;
+        }
       }
-      work(*f, n);
-      {
-        std::lock_guard<std::mutex> g(mu_);
-        if (--active_ == 0) done_.notify_one();
-      }
+      if (stop_.load()) return;
+      seen = gen_.load();
+      inside_.fetch_add(1);
+      if (const std::function<void(size_t)>* f = job_.load()) work(*f, n_);
+      inside_.fetch_sub(1);
     }
   }
   std::vector<std::thread> th_;
   std::mutex mu_, call_mu_;
-  std::condition_variable cv_, done_;
-  const std::function<void(size_t)>* job_ = nullptr;
+  std::condition_variable cv_;
+  std::atomic<const std::function<void(size_t)>*> job_{nullptr};
   size_t n_ = 0;
-  std::atomic<size_t> next_{0};
-  unsigned active_ = 0;
-  uint64_t gen_ = 0;
-  bool stop_ = false;
+  std::atomic<size_t> next_{0}, done_{0};
+  std::atomic<unsigned> inside_{0}, sleepers_{0};
+  std::atomic<uint64_t> gen_{0};
+  std::atomic<bool> stop_{false};
+  int spin_us_ = 300;
 };
 
 inline Pool& pool() {

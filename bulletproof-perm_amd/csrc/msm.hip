@@ -516,7 +516,10 @@ static int msm_multi_dt_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t
   BPP_TRY(ctx_h2d(ctx, d_off, off.data(), (M + 1) * 4));
   BPP_TRY(ctx_ws(ctx, "dt_res", (size_t)M * P3_BYTES, &res));
   const double e_avg = (double)T * DT_W / (double)M;  // table additions per MSM
-  int nt = e_avg > 1024 ? 512 : e_avg > 256 ? 256 : 64;
+  // 256 lanes per MSM measured best for the prover's batches (M = 256-384
+  // MSMs: 0.99 ms of direct-table time per 128 proofs vs 1.10-1.20 at 512
+  // and 1.42 at 128); 512 only when few large MSMs leave the chip empty
+  int nt = e_avg > 256 ? (M < 128 && e_avg > 2048 ? 512 : 256) : 64;
   if (const char* e = getenv("BPP_DT_NT")) nt = atoi(e);
   {
     ProfScope ps(ctx, "msm_direct");

@@ -703,40 +703,11 @@ __global__ void __launch_bounds__(NT) k_dt_msm(const uint32_t* __restrict__ dt, 
   it.cur = 0xffffffffu;
   ge_p3 acc = ge_identity();
   // (a software-pipelined gather measured slower: 233 VGPRs, no latency won)
-#ifdef DT_ILP2
-  // two independent chains: both gathers are in flight before either add
-  ge_p3 acc2 = ge_identity();
-  uint32_t r0, r1;
-  bool n0, n1;
-  while (it.next(r0, n0)) {
-    const bool h1 = it.next(r1, n1);
-    const ge_niels q0 = load_niels(dt, r0);
-    const ge_niels q1 = load_niels(dt, h1 ? r1 : r0);
-    acc = ge_madd_signed(acc, q0, n0);
-    if (!h1) break;
-    acc2 = ge_madd_signed(acc2, q1, n1);
-  }
-  acc = ge_add(acc, acc2);
-#else
+  // (measured: the gathers cost ~4 % of this kernel and two interleaved
+  // chains gain nothing; the add work and the block tree dominate)
   uint32_t row;
   bool neg;
-#ifdef DT_NOLOAD  // timing experiment only: wrong results
-  const ge_niels q0 = load_niels(dt, threadIdx.x);
-  while (it.next(row, neg)) {
-    ge_niels q = q0;
-    q.ypx.v[0] ^= row;
-    acc = ge_madd_signed(acc, q, neg);
-  }
-#else
-  while (it.next(row, neg)) {
-    acc = ge_madd_signed(acc, load_niels(dt, row), neg);
-  }
-#endif
-#endif
-#ifdef DT_NOTREE  // timing experiment only: wrong results
-  if (threadIdx.x == 0) store_p3(out_p3, m, acc);
-  return;
-#endif
+  while (it.next(row, neg)) acc = ge_madd_signed(acc, load_niels(dt, row), neg);
   _Pragma("unroll") for (int k = 1; k < 64; k <<= 1) acc = ge_add(acc, ge_shfl_xor(acc, k));
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   if (NT > 64) {

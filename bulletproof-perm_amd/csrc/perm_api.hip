@@ -27,6 +27,7 @@
 #include "host/perm.h"
 #include "ipa.h"
 #include "msm_engine.h"
+#include "poly.h"
 
 using hsc::Sc;
 
@@ -144,7 +145,7 @@ int msm_terms(bpp_ctx* ctx, const std::vector<Sc>& sc, const std::vector<uint32_
 struct ProverState {
   merlin::Transcript tr;
   std::vector<uint32_t> pi;
-  std::vector<Sc> gamma, sL, sR, taus, vals, aL, aR, aO, y_inv_n, l, r;
+  std::vector<Sc> gamma, sL, sR, taus, vals, aL, aR, aO;
   Sc alpha, beta, rho, x_perm, w;
   Sc t[7];
   explicit ProverState(const uint8_t* label, size_t llen) : tr(label, llen) {}
@@ -221,10 +222,11 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
   }
   MsmPoints pts;
   BPP_TRY(gens_points(ctx, G, &pts));
+  const uint32_t per = 3 + 5 * n_p;  // A_I/A_O/S terms per proof
+  uint32_t* d_s = nullptr;           // their scalars, reused by the polynomial stage
   // A_I, A_O, S of every proof: one batch of 3P MSMs
   hs.reset(new HostScope(ctx, "pb_msm_AI_AO_S"));
   {
-    const uint32_t per = 3 + 5 * n_p;  // terms per proof
     std::vector<Sc> sc((size_t)P * per);
     std::vector<uint32_t> idx((size_t)P * per), off(3 * P + 1);
     par::for_each(P, [&](size_t p) {
@@ -249,7 +251,6 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
       off[3 * p + 2] = (uint32_t)(p * per + 2 + 3 * n_p);
     }
     off[3 * P] = (uint32_t)(P * per);
-    uint32_t* d_s = nullptr;
     BPP_TRY(upload_sc(ctx, sc, "mt_s", &d_s));
     void* d_i = nullptr;
     BPP_TRY(ctx_ws(ctx, "mt_i", idx.size() * 4 + 4, &d_i));
@@ -262,53 +263,36 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
       memcpy(Ps[p].S.data(), &enc[96 * p + 64], 32);
     });
   }
-  // challenges y, z and the t(X) coefficients (host, per proof)
+  // challenges y, z (host transcripts), then the t(X) coefficients of every
+  // proof in one device launch (poly.hip); z^Q W_V stays on the host for tau_x
   hs.reset(new HostScope(ctx, "pb_host_poly"));
-  std::vector<std::vector<Sc>> l1s(P), r0s(P), r1s(P), r3s(P), zWVs(P);
-  par::for_each(P, [&](size_t p) {
-    ProverState& st = *S[p];
-    Proof& Pf = Ps[p];
-    st.tr.append_point("A_I", Pf.AI.data());
-    st.tr.append_point("A_O", Pf.AO.data());
-    st.tr.append_point("S", Pf.S.data());
-    const Sc y = st.tr.challenge_scalar("y");
-    const Sc z = st.tr.challenge_scalar("z");
-    // Montgomery forms of the powers: one Montgomery step per product
-    const std::vector<Sc> y_nR = hsc::powers_mont(y, n_p);
-    const std::vector<Sc> y_inv_nR = hsc::powers_mont(hsc::invert(y), n_p);
-    st.y_inv_n.resize(n_p);
-    for (uint32_t i = 0; i < n_p; ++i) st.y_inv_n[i] = hsc::mont(y_inv_nR[i], hsc::one());
-    std::vector<Sc> zq = hsc::powers(z, C.Q + 1);
-    zq.erase(zq.begin());
-    const std::vector<Sc> zWL = perm::zW(C.WL, zq, n_p), zWR = perm::zW(C.WR, zq, n_p),
-                          zWO = perm::zW(C.WO, zq, n_p);
-    zWVs[p] = perm::zW(C.WV, zq, m);
-    // l(X) = l1 X + l2 X^2 + l3 X^3 ; r(X) = r0 + r1 X + r3 X^3
-    std::vector<Sc>&l1 = l1s[p], &r0 = r0s[p], &r1 = r1s[p], &r3 = r3s[p];
-    l1.resize(n_p);
-    r0.resize(n_p);
-    r1.resize(n_p);
-    r3.resize(n_p);
-    for (uint32_t i = 0; i < n_p; ++i) {
-      const Sc y_i = hsc::mont(y_nR[i], hsc::one());
-      l1[i] = hsc::add(st.aL[i], hsc::mulm(zWR[i], y_inv_nR[i]));
-      r0[i] = hsc::sub(zWO[i], y_i);
-      r1[i] = hsc::add(hsc::mulm(st.aR[i], y_nR[i]), zWL[i]);
-      r3[i] = hsc::mulm(st.sR[i], y_nR[i]);
-    }
-    const std::vector<Sc>& l2 = st.aO;
-    const std::vector<Sc>& l3 = st.sL;
-    using hsc::add;
-    using hsc::inner_product;
-    st.t[1] = inner_product(l1, r0);
-    st.t[2] = add(inner_product(l1, r1), inner_product(l2, r0));
-    st.t[3] = add(inner_product(l2, r1), inner_product(l3, r0));
-    st.t[4] = add(inner_product(l1, r3), inner_product(l3, r1));
-    st.t[5] = inner_product(l2, r3);
-    st.t[6] = inner_product(l3, r3);
-  });
+  std::vector<std::vector<Sc>> zWVs(P);
+  {
+    std::vector<Sc> ys(P), ch((size_t)P * 3), tco;
+    par::for_each(P, [&](size_t p) {
+      ProverState& st = *S[p];
+      Proof& Pf = Ps[p];
+      st.tr.append_point("A_I", Pf.AI.data());
+      st.tr.append_point("A_O", Pf.AO.data());
+      st.tr.append_point("S", Pf.S.data());
+      ys[p] = st.tr.challenge_scalar("y");
+      const Sc z = st.tr.challenge_scalar("z");
+      ch[3 * p] = ys[p];
+      ch[3 * p + 2] = z;
+      std::vector<Sc> zq = hsc::powers(z, C.Q + 1);
+      zq.erase(zq.begin());
+      zWVs[p] = perm::zW(C.WV, zq, m);
+    });
+    std::vector<Sc> yinv = ys;
+    hsc::batch_invert(yinv);
+    for (size_t p = 0; p < P; ++p) ch[3 * p + 1] = yinv[p];
+    BPP_TRY(poly_coef_dev(ctx, C, (uint32_t)P, d_s, per, ch, tco));
+    for (size_t p = 0; p < P; ++p)
+      for (int j = 0; j < 6; ++j) S[p]->t[1 + j] = tco[6 * p + j];
+  }
   // T1, T3..T6 of every proof: one fixed-base launch
   hs.reset(new HostScope(ctx, "pb_pedersen_T_lr"));
+  uint32_t *d_l = nullptr, *d_r = nullptr, *d_hf = nullptr;  // IPA inputs, on the device
   {
     std::vector<Sc> v(5 * P), g(5 * P);
     static const int ti[5] = {1, 3, 4, 5, 6};
@@ -323,6 +307,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
       BPP_TRY(pedersen_host(ctx, G, v, g, T));
     }
     HostScope hs3(ctx, "pbT_host");
+    std::vector<Sc> xs(P), t_hat;
     par::for_each(P, [&](size_t p) {
       ProverState& st = *S[p];
       Proof& Pf = Ps[p];
@@ -331,50 +316,37 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
         Pf.T[i] = T[5 * p + i];
         st.tr.append_point(lab[i], Pf.T[i].data());
       }
-      const Sc x = st.tr.challenge_scalar("x");
+      xs[p] = st.tr.challenge_scalar("x");
+    });
+    BPP_TRY(poly_x_dev(ctx, C, (uint32_t)P, xs, &d_l, &d_r, &d_hf, t_hat));
+    par::for_each(P, [&](size_t p) {
+      ProverState& st = *S[p];
+      Proof& Pf = Ps[p];
+      const Sc x = xs[p];
       std::vector<Sc> xp = hsc::powers(x, 7);
       const int tidx[5] = {1, 3, 4, 5, 6};
       using hsc::add;
       Sc tau_x = hsc::mul(xp[2], hsc::inner_product(zWVs[p], st.gamma));
       for (int i = 0; i < 5; ++i) tau_x = add(tau_x, hsc::mul(st.taus[i], xp[tidx[i]]));
       const Sc mu = add(add(hsc::mul(st.alpha, x), hsc::mul(st.beta, xp[2])), hsc::mul(st.rho, xp[3]));
-      const std::vector<Sc>&l1 = l1s[p], &r0 = r0s[p], &r1 = r1s[p], &r3 = r3s[p];
-      const std::vector<Sc>& l2 = st.aO;
-      const std::vector<Sc>& l3 = st.sL;
-      st.l.resize(n_p);
-      st.r.resize(n_p);
-      const Sc xR = hsc::to_mont(x), x2R = hsc::to_mont(xp[2]);
-      for (uint32_t i = 0; i < n_p; ++i) {
-        st.l[i] = hsc::mulm(add(l1[i], hsc::mulm(add(l2[i], hsc::mulm(l3[i], xR)), xR)), xR);
-        st.r[i] = add(r0[i], hsc::mulm(add(r1[i], hsc::mulm(r3[i], x2R)), xR));
-      }
-      const Sc t_hat = hsc::inner_product(st.l, st.r);
       st.tr.append_scalar("TX", tau_x);
       st.tr.append_scalar("mu", mu);
-      st.tr.append_scalar("t", t_hat);
+      st.tr.append_scalar("t", t_hat[p]);
       Pf.tau_x = tau_x;
       Pf.mu = mu;
-      Pf.t_hat = t_hat;
+      Pf.t_hat = t_hat[p];
       st.w = st.tr.challenge_scalar("w");
     });
   }
   // IPA of every proof in lockstep
   hs.reset(new HostScope(ctx, "pb_ipa"));
   {
-    std::vector<Sc> L((size_t)P * n_p), R((size_t)P * n_p), HF((size_t)P * n_p);
     std::vector<Sc> qmul(P);
     std::vector<merlin::Transcript*> trs(P);
-    par::for_each(P, [&](size_t p) {
-      std::copy(S[p]->l.begin(), S[p]->l.end(), L.begin() + p * n_p);
-      std::copy(S[p]->r.begin(), S[p]->r.end(), R.begin() + p * n_p);
-      std::copy(S[p]->y_inv_n.begin(), S[p]->y_inv_n.end(), HF.begin() + p * n_p);
+    for (size_t p = 0; p < P; ++p) {
       qmul[p] = S[p]->w;
       trs[p] = &S[p]->tr;
-    });
-    uint32_t *d_l, *d_r, *d_hf;
-    BPP_TRY(upload_sc(ctx, L, "pf_l", &d_l));
-    BPP_TRY(upload_sc(ctx, R, "pf_r", &d_r));
-    BPP_TRY(upload_sc(ctx, HF, "pf_hf", &d_hf));
+    }
     IpaGens ig;
     ig.pts = pts;
     ig.gbase = 0;
@@ -550,6 +522,8 @@ int verify_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const 
   std::vector<h25519::ge> res;
   MsmPoints pts;
   BPP_TRY(gens_points(ctx, G, &pts));
+  const uint32_t per = 3 + 5 * n_p;  // A_I/A_O/S terms per proof
+  uint32_t* d_s = nullptr;           // their scalars, reused by the polynomial stage
   BPP_TRY(msm_points_extra(ctx, &pts, d_x, (uint32_t)(enc.size() / 32), n0, "pv_x_wt", (double)sc.size()));
   BPP_TRY(msm_terms(ctx, sc, idx, {0, (uint32_t)sc.size()}, pts, res));
   uint8_t e[32];

@@ -1,0 +1,19 @@
+// Device vector-polynomial stage of the batched prover (poly.hip).
+#pragma once
+#include <vector>
+
+#include "ctx.h"
+#include "host/perm.h"
+
+// t_1, t_3..t_6 inputs: for P proofs, with d_sc the A_I/A_O/S scalar array
+// ([P][per], per = 3 + 5 n_p: alpha, a_L, a_R, beta, a_O, rho, s_L, s_R,
+// canonical) and ch = [P][y, y^-1, z] (canonical): t = [P][t_1..t_6].
+// Keeps the l(X), r(X) coefficient vectors and the H factors y^-i on the
+// device for poly_x_dev.
+int poly_coef_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint32_t* d_sc, uint32_t per,
+                  const std::vector<hsc::Sc>& ch, std::vector<hsc::Sc>& t);
+
+// l = l(x), r = r(x) ([P][n_p], canonical, on the device for the IPA), the
+// H factors, and t_hat = <l, r> per proof.
+int poly_x_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const std::vector<hsc::Sc>& x, uint32_t** d_l,
+               uint32_t** d_r, uint32_t** d_hf, std::vector<hsc::Sc>& t_hat);

@@ -197,6 +197,15 @@ def msm_windows(n: int) -> tuple[int, int]:
     return c.value, w.value
 
 
+def double_compress(raw_points: Sequence[bytes]) -> list[bytes]:
+    """compress(2 P) for raw 128-byte extended points (host batch encoding)."""
+    lib = _lib.load()
+    data = b"".join(raw_points)
+    out = C.create_string_buffer(32 * len(raw_points))
+    check(lib.bpp_points_double_compress(_buf(data), len(raw_points), out), "bpp_points_double_compress")
+    return [out.raw[32 * i:32 * i + 32] for i in range(len(raw_points))]
+
+
 def partials_finish(partials: Sequence[bytes]) -> bytes:
     lib = _lib.load()
     data = b"".join(partials)

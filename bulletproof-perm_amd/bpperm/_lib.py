@@ -56,6 +56,7 @@ SIGNATURES = {
     "bpp_msm_windows": (i32, [sz, C.POINTER(u32), C.POINTER(u32)]),
     "bpp_msm_table_dev_partial": (i32, [vp, vp, vp, sz, u32, u32, vp]),
     "bpp_partials_finish": (i32, [vp, sz, vp]),
+    "bpp_points_double_compress": (i32, [vp, sz, vp]),
     "bpp_msm_batch": (i32, [vp, sz, vp, vp, vp, vp, vp]),
     "bpp_gens_create": (i32, [vp, sz, C.POINTER(vp)]),
     "bpp_gens_from_points": (i32, [vp, vp, vp, sz, vp, vp, C.POINTER(vp)]),

@@ -1,115 +1,151 @@
-// Host-side GF(2^255-19) / Edwards / ristretto255 (radix 2^64, 4 limbs).
+// Host-side GF(2^255-19) / Edwards / ristretto255 (radix 2^51, 5 limbs).
 //
 // Product code, not the oracle: finishes what the GPU hands back (the
 // Horner combine of a large MSM's W window sums, compression of a single
 // result point, proof-level point equality) where a lone GPU lane would be
-// latency-bound.  Independent of the device's 8 x 32-bit representation and
-// of the oracle's radix-2^51 port.
+// latency-bound.  Independent of the device's 10 x 32-bit representation
+// and of the oracle's C port.
 #pragma once
 #include <stdint.h>
 #include <string.h>
+
+#include <vector>
 
 namespace h25519 {
 
 typedef unsigned __int128 u128;
 
+// radix 2^51, five limbs; every function returns "carried" limbs
+// (< 2^51 + 2^18), which is what fe_mul / fe_sub accept.
 struct fe {
-  uint64_t v[4];
+  uint64_t v[5];
 };
 
-static inline fe fe_zero() { return fe{{0, 0, 0, 0}}; }
-static inline fe fe_one() { return fe{{1, 0, 0, 0}}; }
+static const uint64_t FE_M51 = (1ULL << 51) - 1;
 
-// value = a (256 bits) + top * 2^256 -> loose (< 2^256)
-static inline fe fe_fold(fe a, uint64_t top) {
-  uint64_t hi = (top << 1) | (a.v[3] >> 63);
-  a.v[3] &= 0x7fffffffffffffffULL;
-  u128 c = (u128)a.v[0] + (u128)hi * 19u;
-  a.v[0] = (uint64_t)c;
-  for (int i = 1; i < 4; ++i) {
-    c = (u128)a.v[i] + (uint64_t)(c >> 64);
-    a.v[i] = (uint64_t)c;
-  }
+static inline fe fe_zero() { return fe{{0, 0, 0, 0, 0}}; }
+static inline fe fe_one() { return fe{{1, 0, 0, 0, 0}}; }
+
+static inline fe fe_carry(fe a) {
+  uint64_t c;
+  c = a.v[0] >> 51; a.v[0] &= FE_M51; a.v[1] += c;
+  c = a.v[1] >> 51; a.v[1] &= FE_M51; a.v[2] += c;
+  c = a.v[2] >> 51; a.v[2] &= FE_M51; a.v[3] += c;
+  c = a.v[3] >> 51; a.v[3] &= FE_M51; a.v[4] += c;
+  c = a.v[4] >> 51; a.v[4] &= FE_M51; a.v[0] += 19 * c;
   return a;
 }
 
 static inline fe fe_add(const fe& a, const fe& b) {
   fe r;
-  u128 c = 0;
-  for (int i = 0; i < 4; ++i) {
-    c = (u128)a.v[i] + b.v[i] + (uint64_t)(c >> 64);
-    r.v[i] = (uint64_t)c;
-  }
-  return fe_fold(r, (uint64_t)(c >> 64));
+  for (int i = 0; i < 5; ++i) r.v[i] = a.v[i] + b.v[i];
+  return fe_carry(r);
 }
 
+// a + 4p - b (4p limbs exceed any carried limb)
 static inline fe fe_sub(const fe& a, const fe& b) {
-  // a + (4p - b), 4p = 2^257 - 76
-  const uint64_t fp[4] = {0xffffffffffffffb4ULL, ~0ULL, ~0ULL, ~0ULL};
-  uint64_t t[4];
-  uint64_t borrow = 0;
-  for (int i = 0; i < 4; ++i) {
-    u128 d = (u128)fp[i] - b.v[i] - borrow;
-    t[i] = (uint64_t)d;
-    borrow = (uint64_t)(d >> 64) & 1;
-  }
-  uint64_t top = 1 - borrow;
   fe r;
-  u128 c = 0;
-  for (int i = 0; i < 4; ++i) {
-    c = (u128)a.v[i] + t[i] + (uint64_t)(c >> 64);
-    r.v[i] = (uint64_t)c;
-  }
-  return fe_fold(r, (uint64_t)(c >> 64) + top);
+  r.v[0] = a.v[0] + 0x1fffffffffffb4ULL - b.v[0];
+  for (int i = 1; i < 5; ++i) r.v[i] = a.v[i] + 0x1ffffffffffffcULL - b.v[i];
+  return fe_carry(r);
 }
 
 static inline fe fe_neg(const fe& a) { return fe_sub(fe_zero(), a); }
 
-static inline fe fe_mul(const fe& a, const fe& b) {
-  uint64_t t[8] = {0};
-  for (int i = 0; i < 4; ++i) {
-    u128 c = 0;
-    for (int j = 0; j < 4; ++j) {
-      c = (u128)a.v[i] * b.v[j] + t[i + j] + (uint64_t)(c >> 64);
-      t[i + j] = (uint64_t)c;
-    }
-    t[i + 4] = (uint64_t)(c >> 64);
-  }
+static inline fe fe_reduce128(u128 t0, u128 t1, u128 t2, u128 t3, u128 t4) {
   fe r;
-  u128 c = 0;
-  for (int i = 0; i < 4; ++i) {
-    c = (u128)t[4 + i] * 38u + t[i] + (uint64_t)(c >> 64);
-    r.v[i] = (uint64_t)c;
-  }
-  return fe_fold(r, (uint64_t)(c >> 64));
+  t1 += (uint64_t)(t0 >> 51); r.v[0] = (uint64_t)t0 & FE_M51;
+  t2 += (uint64_t)(t1 >> 51); r.v[1] = (uint64_t)t1 & FE_M51;
+  t3 += (uint64_t)(t2 >> 51); r.v[2] = (uint64_t)t2 & FE_M51;
+  t4 += (uint64_t)(t3 >> 51); r.v[3] = (uint64_t)t3 & FE_M51;
+  const uint64_t c = (uint64_t)(t4 >> 51);
+  r.v[4] = (uint64_t)t4 & FE_M51;
+  r.v[0] += 19 * c;
+  r.v[1] += r.v[0] >> 51;
+  r.v[0] &= FE_M51;
+  return r;
 }
 
-static inline fe fe_sq(const fe& a) { return fe_mul(a, a); }
+static inline fe fe_mul(const fe& a, const fe& b) {
+  const uint64_t b1 = 19 * b.v[1], b2 = 19 * b.v[2], b3 = 19 * b.v[3], b4 = 19 * b.v[4];
+  const u128 t0 = (u128)a.v[0] * b.v[0] + (u128)a.v[1] * b4 + (u128)a.v[2] * b3 + (u128)a.v[3] * b2 +
+                  (u128)a.v[4] * b1;
+  const u128 t1 = (u128)a.v[0] * b.v[1] + (u128)a.v[1] * b.v[0] + (u128)a.v[2] * b4 + (u128)a.v[3] * b3 +
+                  (u128)a.v[4] * b2;
+  const u128 t2 = (u128)a.v[0] * b.v[2] + (u128)a.v[1] * b.v[1] + (u128)a.v[2] * b.v[0] + (u128)a.v[3] * b4 +
+                  (u128)a.v[4] * b3;
+  const u128 t3 = (u128)a.v[0] * b.v[3] + (u128)a.v[1] * b.v[2] + (u128)a.v[2] * b.v[1] + (u128)a.v[3] * b.v[0] +
+                  (u128)a.v[4] * b4;
+  const u128 t4 = (u128)a.v[0] * b.v[4] + (u128)a.v[1] * b.v[3] + (u128)a.v[2] * b.v[2] + (u128)a.v[3] * b.v[1] +
+                  (u128)a.v[4] * b.v[0];
+  return fe_reduce128(t0, t1, t2, t3, t4);
+}
+
+static inline fe fe_sq(const fe& a) {
+  const uint64_t d0 = 2 * a.v[0], d1 = 2 * a.v[1], d3_19 = 38 * a.v[3], a3_19 = 19 * a.v[3], a4_19 = 19 * a.v[4];
+  const u128 t0 = (u128)a.v[0] * a.v[0] + (u128)d1 * a4_19 + (u128)(2 * a.v[2]) * a3_19;
+  const u128 t1 = (u128)d0 * a.v[1] + (u128)(2 * a.v[2]) * a4_19 + (u128)a.v[3] * a3_19;
+  const u128 t2 = (u128)d0 * a.v[2] + (u128)a.v[1] * a.v[1] + (u128)d3_19 * a.v[4];
+  const u128 t3 = (u128)d0 * a.v[3] + (u128)d1 * a.v[2] + (u128)a.v[4] * a4_19;
+  const u128 t4 = (u128)d0 * a.v[4] + (u128)d1 * a.v[3] + (u128)a.v[2] * a.v[2];
+  return fe_reduce128(t0, t1, t2, t3, t4);
+}
 
 static inline fe fe_sqn(fe a, int n) {
   for (int i = 0; i < n; ++i) a = fe_sq(a);
   return a;
 }
 
-static inline fe fe_canon(fe a) {
-  a = fe_fold(a, 0);
+// canonical little-endian 256-bit value (< p) of a (limbs < 2^53)
+static inline void fe_to_u256(uint64_t w[4], const fe& a) {
+  u128 acc = (u128)a.v[0] + ((u128)a.v[1] << 51);
+  w[0] = (uint64_t)acc;
+  acc >>= 64;
+  acc += (u128)a.v[2] << 38;
+  w[1] = (uint64_t)acc;
+  acc >>= 64;
+  acc += (u128)a.v[3] << 25;
+  w[2] = (uint64_t)acc;
+  acc >>= 64;
+  acc += (u128)a.v[4] << 12;
+  w[3] = (uint64_t)acc;
+  uint64_t top = (uint64_t)(acc >> 64);
+  for (int pass = 0; pass < 2; ++pass) {  // fold bits >= 255 (2^255 = 19)
+    const uint64_t hi = (top << 1) | (w[3] >> 63);
+    w[3] &= 0x7fffffffffffffffULL;
+    u128 c = (u128)w[0] + (u128)hi * 19u;
+    w[0] = (uint64_t)c;
+    for (int i = 1; i < 4; ++i) {
+      c = (u128)w[i] + (uint64_t)(c >> 64);
+      w[i] = (uint64_t)c;
+    }
+    top = 0;
+  }
+  // now < 2^255; subtract p when value + 19 >= 2^255
   uint64_t t[4];
-  u128 c = (u128)a.v[0] + 19u;
+  u128 c = (u128)w[0] + 19u;
   t[0] = (uint64_t)c;
   for (int i = 1; i < 4; ++i) {
-    c = (u128)a.v[i] + (uint64_t)(c >> 64);
+    c = (u128)w[i] + (uint64_t)(c >> 64);
     t[i] = (uint64_t)c;
   }
   if (t[3] >> 63) {
     t[3] &= 0x7fffffffffffffffULL;
-    for (int i = 0; i < 4; ++i) a.v[i] = t[i];
+    for (int i = 0; i < 4; ++i) w[i] = t[i];
   }
-  return a;
+}
+
+static inline fe fe_from_u256(const uint64_t w[4], uint64_t top);
+// fully reduced: limbs < 2^51 and value < p
+static inline fe fe_canon(const fe& a) {
+  uint64_t w[4];
+  fe_to_u256(w, a);
+  return fe_from_u256(w, 0);
 }
 
 static inline bool fe_iszero(const fe& a) {
   fe c = fe_canon(a);
-  return (c.v[0] | c.v[1] | c.v[2] | c.v[3]) == 0;
+  return (c.v[0] | c.v[1] | c.v[2] | c.v[3] | c.v[4]) == 0;
 }
 static inline bool fe_eq(const fe& a, const fe& b) { return fe_iszero(fe_sub(a, b)); }
 static inline bool fe_isneg(const fe& a) { return fe_canon(a).v[0] & 1; }
@@ -139,31 +175,52 @@ static inline fe fe_pow22523(const fe& z) {
   return fe_mul(fe_sqn(a, 2), z);
 }
 
-static inline fe fe_from_bytes(const uint8_t b[32]) {
+// 256-bit little-endian value (+ top * 2^256), reduced mod p on the way in
+static inline fe fe_from_u256(const uint64_t w[4], uint64_t top) {
   fe r;
-  memcpy(r.v, b, 32);  // little-endian host
-  return r;
+  r.v[0] = w[0] & FE_M51;
+  r.v[1] = ((w[0] >> 51) | (w[1] << 13)) & FE_M51;
+  r.v[2] = ((w[1] >> 38) | (w[2] << 26)) & FE_M51;
+  r.v[3] = ((w[2] >> 25) | (w[3] << 39)) & FE_M51;
+  r.v[4] = (w[3] >> 12) & FE_M51;
+  // bit 255 and top * 2^256 (2^255 = 19, 2^256 = 38 mod p)
+  r.v[0] += 19 * (w[3] >> 63) + 38 * top;
+  return fe_carry(r);
+}
+static inline fe fe_from_bytes(const uint8_t b[32]) {
+  uint64_t w[4];
+  memcpy(w, b, 32);  // little-endian host
+  return fe_from_u256(w, 0);
 }
 static inline void fe_to_bytes(uint8_t b[32], const fe& a) {
-  fe c = fe_canon(a);
-  memcpy(b, c.v, 32);
+  uint64_t w[4];
+  fe_to_u256(w, a);
+  memcpy(b, w, 32);
 }
 static inline fe fe_from_words(const uint32_t w[8]) {
-  fe r;
-  for (int i = 0; i < 4; ++i) r.v[i] = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
-  return r;
+  uint64_t q[4];
+  for (int i = 0; i < 4; ++i) q[i] = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
+  return fe_from_u256(q, 0);
 }
 static inline void fe_to_words(uint32_t w[8], const fe& a) {
+  uint64_t q[4];
+  fe_to_u256(q, a);
   for (int i = 0; i < 4; ++i) {
-    w[2 * i] = (uint32_t)a.v[i];
-    w[2 * i + 1] = (uint32_t)(a.v[i] >> 32);
+    w[2 * i] = (uint32_t)q[i];
+    w[2 * i + 1] = (uint32_t)(q[i] >> 32);
   }
 }
 
-static const fe FE_D = {{0x75eb4dca135978a3ULL, 0x00700a4d4141d8abULL, 0x8cc740797779e898ULL, 0x52036cee2b6ffe73ULL}};
-static const fe FE_D2 = {{0xebd69b9426b2f159ULL, 0x00e0149a8283b156ULL, 0x198e80f2eef3d130ULL, 0x2406d9dc56dffce7ULL}};
-static const fe FE_SQRT_M1 = {{0xc4ee1b274a0ea0b0ULL, 0x2f431806ad2fe478ULL, 0x2b4d00993dfbd7a7ULL, 0x2b8324804fc1df0bULL}};
-static const fe FE_INVSQRT_A_MINUS_D = {{0x99c8fdaa805d40eaULL, 0x9d2f16175a4172beULL, 0x16c27b91fe01d840ULL, 0x786c8905cfaffca2ULL}};
+static inline fe fe_c(uint64_t a, uint64_t b, uint64_t c, uint64_t d) {
+  const uint64_t w[4] = {a, b, c, d};
+  return fe_from_u256(w, 0);
+}
+static const fe FE_D = fe_c(0x75eb4dca135978a3ULL, 0x00700a4d4141d8abULL, 0x8cc740797779e898ULL, 0x52036cee2b6ffe73ULL);
+static const fe FE_D2 = fe_c(0xebd69b9426b2f159ULL, 0x00e0149a8283b156ULL, 0x198e80f2eef3d130ULL, 0x2406d9dc56dffce7ULL);
+static const fe FE_SQRT_M1 =
+    fe_c(0xc4ee1b274a0ea0b0ULL, 0x2f431806ad2fe478ULL, 0x2b4d00993dfbd7a7ULL, 0x2b8324804fc1df0bULL);
+static const fe FE_INVSQRT_A_MINUS_D =
+    fe_c(0x99c8fdaa805d40eaULL, 0x9d2f16175a4172beULL, 0x16c27b91fe01d840ULL, 0x786c8905cfaffca2ULL);
 
 struct ge {
   fe X, Y, Z, T;
@@ -228,6 +285,66 @@ static inline void encode(uint8_t out[32], const ge& p) {
   fe_to_bytes(out, fe_abs(fe_mul(den_inv, fe_sub(p.Z, y))));
 }
 
+// Encodings of 2*P_i for a batch with ONE field inversion per call
+// (RFC 9496's encode needs an inverse square root per point; for a doubled
+// point it is rational).  With e = 2XY, f = Z^2 + dT^2, g = Y^2 + X^2,
+// h = Z^2 - dT^2, 2P = (eh : gf : fh : eg), and for that representative
+// u1 * u2^2 = W^2 (a - d) with W = 2 e f^2 g h T Z (curve equation:
+// h^2 - g^2 = -4 (1 + d) T^2 Z^2), so SQRT_RATIO_M1(1, u1 u2^2) =
+// |INVSQRT_A_MINUS_D / W|.  W = 0 exactly for the torsion representatives
+// of the identity, whose double encodes to zero.  The rest is encode().
+// (The prover computes P = C/2 with halved scalars and encodes C = 2P.)
+static inline void encode_double_batch(const ge* pts, size_t n, uint8_t* out) {
+  struct St {
+    fe X, Y, Z, T, W;
+  };
+  std::vector<St> st(n);
+  std::vector<fe> acc(n);
+  fe run = fe_one();
+  for (size_t i = 0; i < n; ++i) {
+    const ge& p = pts[i];
+    const fe XX = fe_sq(p.X), YY = fe_sq(p.Y), ZZ = fe_sq(p.Z), dTT = fe_mul(fe_sq(p.T), FE_D);
+    const fe e = fe_mul(fe_add(p.X, p.X), p.Y);
+    const fe f = fe_add(ZZ, dTT), g = fe_add(YY, XX), h = fe_sub(ZZ, dTT);
+    St& q = st[i];
+    q.X = fe_mul(e, h);
+    q.Y = fe_mul(g, f);
+    q.Z = fe_mul(f, h);
+    q.T = fe_mul(e, g);
+    // W = 2 e f^2 g h T Z = 2 * X' * Z'... : (eh)(fg)(f)(T Z) * 2
+    fe W = fe_mul(fe_mul(q.X, q.Y), fe_mul(f, fe_mul(p.T, p.Z)));
+    W = fe_add(W, W);
+    q.W = fe_iszero(W) ? fe_zero() : W;
+    acc[i] = run;
+    if (!fe_iszero(q.W)) run = fe_mul(run, q.W);
+  }
+  fe inv = fe_invert(run);
+  for (size_t i = n; i-- > 0;) {
+    St& q = st[i];
+    uint8_t* o = out + 32 * i;
+    if (fe_iszero(q.W)) {
+      memset(o, 0, 32);
+      continue;
+    }
+    const fe Winv = fe_mul(inv, acc[i]);
+    inv = fe_mul(inv, q.W);
+    const fe isq = fe_abs(fe_mul(FE_INVSQRT_A_MINUS_D, Winv));
+    const fe u1 = fe_mul(fe_add(q.Z, q.Y), fe_sub(q.Z, q.Y));
+    const fe u2 = fe_mul(q.X, q.Y);
+    const fe den1 = fe_mul(isq, u1), den2 = fe_mul(isq, u2);
+    const fe z_inv = fe_mul(fe_mul(den1, den2), q.T);
+    const bool rotate = fe_isneg(fe_mul(q.T, z_inv));
+    fe x = q.X, y = q.Y, den_inv = den2;
+    if (rotate) {
+      x = fe_mul(q.Y, FE_SQRT_M1);
+      y = fe_mul(q.X, FE_SQRT_M1);
+      den_inv = fe_mul(den1, FE_INVSQRT_A_MINUS_D);
+    }
+    if (fe_isneg(fe_mul(x, z_inv))) y = fe_neg(y);
+    fe_to_bytes(o, fe_abs(fe_mul(den_inv, fe_sub(q.Z, y))));
+  }
+}
+
 static inline bool decode(ge& out, const uint8_t in[32]) {
   fe s = fe_from_bytes(in);
   uint8_t chk[32];
@@ -266,7 +383,7 @@ static inline fe fe_from_dev(const uint32_t w[10]) {
       t[k] = (uint64_t)c;
     }
   }
-  return fe_fold(fe{{t[0], t[1], t[2], t[3]}}, t[4]);
+  return fe_from_u256(t, t[4]);
 }
 // device extended point (40 words, csrc/layout.h P3_WORDS) -> host point
 static inline ge ge_from_dev(const uint32_t* w) {

@@ -61,6 +61,22 @@ static inline Sc add(const Sc& a, const Sc& b) {
   return r;
 }
 
+// a / 2 mod l for canonical a: a even -> a >> 1, odd -> (a + l) >> 1
+static inline Sc half(const Sc& a) {
+  Sc t = a;
+  if (a.v[0] & 1) {
+    unsigned __int128 c = 0;
+    for (int i = 0; i < 4; ++i) {
+      c += (unsigned __int128)a.v[i] + L.v[i];
+      t.v[i] = (uint64_t)c;
+      c >>= 64;
+    }
+  }
+  for (int i = 0; i < 3; ++i) t.v[i] = (t.v[i] >> 1) | (t.v[i + 1] << 63);
+  t.v[3] >>= 1;
+  return t;
+}
+
 static inline Sc sub(const Sc& a, const Sc& b) {
   uint64_t br;
   Sc r = sub_raw(a, b, &br);

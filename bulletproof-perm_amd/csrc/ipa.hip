@@ -236,7 +236,9 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
     BPP_TRY(ctx_check_launch(ctx, "ipa round kernels"));
     {
       HostScope hs(ctx, "ipa_msm");
-      BPP_TRY(msm_multi_enc(ctx, (const uint32_t*)scal, (const uint32_t*)pidx, off, g.pts, enc.data()));
+      // L/2, R/2 from halved term scalars, encoded as L, R (msm_multi_enc)
+      BPP_TRY(sc_halve_dev(ctx, (const uint32_t*)scal, (uint32_t*)scal, PT));
+      BPP_TRY(msm_multi_enc(ctx, (const uint32_t*)scal, (const uint32_t*)pidx, off, g.pts, enc.data(), true));
     }
     HostScope hs(ctx, "ipa_host");
     par::for_each(P, [&](size_t p) {

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "ctx.h"
 #include "host/fe64.h"
@@ -364,6 +365,18 @@ int bpp_partials_finish(const uint8_t* partials, size_t count, uint8_t out[32]) 
   return BPP_OK;
 }
 
+int bpp_points_double_compress(const uint8_t* raw, size_t count, uint8_t* out) {
+  if ((!raw || !out) && count) return BPP_ERR_ARG;
+  std::vector<h25519::ge> pts(count);
+  for (size_t i = 0; i < count; ++i) {
+    uint32_t w[32];
+    memcpy(w, raw + 128 * i, 128);
+    pts[i] = h25519::ge_from_words(w);
+  }
+  h25519::encode_double_batch(pts.data(), count, out);
+  return BPP_OK;
+}
+
 int bpp_msm_table(bpp_ctx* ctx, const uint8_t* scalars, const bpp_points* tbl, size_t n, uint8_t out[32]) {
   if (!ctx || !tbl || !out || (!scalars && n)) return BPP_ERR_ARG;
   if (n > tbl->n) return BPP_ERR_LEN;
@@ -585,25 +598,26 @@ int msm_multi(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, cons
 }
 
 int msm_multi_enc(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const std::vector<uint32_t>& off,
-                  const MsmPoints& pts, uint8_t* out_enc) {
+                  const MsmPoints& pts, uint8_t* out_enc, bool doubled) {
   const uint32_t M = (uint32_t)off.size() - 1;
   const uint32_t T = off[M];
   if (M == 0) return BPP_OK;
-  // Few results: host encoding (~10 us each) beats a latency-bound GPU
-  // launch; many: one GPU lane per result.
-  if (M > 16 && T > 0 && use_dt(pts, M, T)) {
+  // Few results: host encoding beats a latency-bound GPU launch; many: one
+  // GPU lane per result, or (doubled) the host batch encoding of 2 R_m.
+  if (M > 16 && T > 0 && (use_dt(pts, M, T) || use_fb(pts, M, T))) {
     uint32_t* d_ws = nullptr;
-    BPP_TRY(msm_multi_dt_dev(ctx, d_scal, d_pidx, off, pts, &d_ws));
-    return points_compress_p3(ctx, d_ws, M, out_enc);
-  }
-  if (M > 16 && T > 0 && use_fb(pts, M, T)) {
-    uint32_t* d_ws = nullptr;
-    BPP_TRY(msm_multi_fb_dev(ctx, d_scal, d_pidx, off, pts, &d_ws));
-    return points_compress_p3(ctx, d_ws, M, out_enc);
+    if (use_dt(pts, M, T))
+      BPP_TRY(msm_multi_dt_dev(ctx, d_scal, d_pidx, off, pts, &d_ws));
+    else
+      BPP_TRY(msm_multi_fb_dev(ctx, d_scal, d_pidx, off, pts, &d_ws));
+    return doubled ? points_double_encode_p3(ctx, d_ws, M, out_enc) : points_compress_p3(ctx, d_ws, M, out_enc);
   }
   std::vector<h25519::ge> res;
   BPP_TRY(msm_multi(ctx, d_scal, d_pidx, off, pts, res));
-  for (uint32_t m = 0; m < M; ++m) h25519::encode(out_enc + 32 * (size_t)m, res[m]);
+  if (doubled)
+    h25519::encode_double_batch(res.data(), M, out_enc);
+  else
+    for (uint32_t m = 0; m < M; ++m) h25519::encode(out_enc + 32 * (size_t)m, res[m]);
   return BPP_OK;
 }
 

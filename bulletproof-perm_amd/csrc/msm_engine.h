@@ -18,6 +18,10 @@ int msm_single_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx,
                    uint32_t c, uint32_t wb, uint32_t Wn, h25519::ge* out);
 int upload_scalars(bpp_ctx* ctx, const uint8_t* scalars, size_t n, const char* name, uint32_t** d_out);
 int points_compress_p3(bpp_ctx* ctx, const uint32_t* d_p3, size_t n, uint8_t* out_host);
+// out = encodings of 2 * P_i (host batch encoding; see points.hip)
+int points_double_encode_p3(bpp_ctx* ctx, const uint32_t* d_p3, size_t n, uint8_t* out_host);
+// d_out[i] = d_in[i] / 2 mod l (canonical scalars; in place allowed)
+int sc_halve_dev(bpp_ctx* ctx, const uint32_t* d_in, uint32_t* d_out, size_t n);
 #include <vector>
 // Fixed-base window tables: entry k*FBW_W + w = 2^(FBW_C*w) * P_k (affine
 // Niels).  An MSM over such points needs no per-window Horner combine: all
@@ -47,7 +51,11 @@ int msm_points_extra(bpp_ctx* ctx, MsmPoints* pts, const uint32_t* d_x, uint32_t
 int msm_multi(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const std::vector<uint32_t>& off,
               const MsmPoints& pts, std::vector<h25519::ge>& out);
 // Same, results compressed (M x 32 B).
+// doubled: d_scal holds halved scalars s/2 and out_enc gets the encodings of
+// 2 * result (host batch encoding, one inversion instead of a per-point
+// inverse square root)
 int msm_multi_enc(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const std::vector<uint32_t>& off,
-                  const MsmPoints& pts, uint8_t* out_enc);
+                  const MsmPoints& pts, uint8_t* out_enc,
+                  bool doubled = false);
 int msm_multi(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const std::vector<uint32_t>& off,
               const uint32_t* d_tbl, const uint32_t* d_tbl1, uint32_t n0, std::vector<h25519::ge>& out);

@@ -28,6 +28,7 @@
 #include "ipa.h"
 #include "msm_engine.h"
 #include "poly.h"
+#include "layout.h"
 
 using hsc::Sc;
 
@@ -111,23 +112,49 @@ int upload_sc(bpp_ctx* ctx, const std::vector<Sc>& v, const char* name, uint32_t
 }
 
 // Fixed-base commitments v_i*B + g_i*Bb, returned compressed.
+// Small batches (<= PED_DOUBLE_MAX) commit with halved scalars and encode
+// C = 2 (C / 2) on the host (points_double_encode_p3): one inversion per
+// chunk instead of a ~70 us per-point inverse-square-root chain on the GPU.
+#define PED_DOUBLE_MAX 2048
 int pedersen_host(bpp_ctx* ctx, const bpp_gens* g, const std::vector<Sc>& v, const std::vector<Sc>& gam,
                   std::vector<Enc32>& out) {
+  const size_t m = v.size();
+  const bool doubled = m <= PED_DOUBLE_MAX;
   uint32_t *d_v, *d_g;
   {
     HostScope hs(ctx, "ped_upload");
-    BPP_TRY(upload_sc(ctx, v, "pp_v", &d_v));
-    BPP_TRY(upload_sc(ctx, gam, "pp_g", &d_g));
+    if (doubled) {
+      std::vector<Sc> hv(m), hg(m);
+      for (size_t i = 0; i < m; ++i) {
+        hv[i] = hsc::half(v[i]);
+        hg[i] = hsc::half(gam[i]);
+      }
+      BPP_TRY(upload_sc(ctx, hv, "pp_v", &d_v));
+      BPP_TRY(upload_sc(ctx, hg, "pp_g", &d_g));
+    } else {
+      BPP_TRY(upload_sc(ctx, v, "pp_v", &d_v));
+      BPP_TRY(upload_sc(ctx, gam, "pp_g", &d_g));
+    }
+  }
+  out.resize(m);
+  if (doubled) {
+    void* d_p3 = nullptr;
+    BPP_TRY(ctx_ws(ctx, "pp_p3", m * P3_BYTES, &d_p3));
+    {
+      HostScope hs(ctx, "ped_kernels");
+      BPP_TRY(pedersen_dev(ctx, g, d_v, d_g, m, nullptr, (uint32_t*)d_p3));
+    }
+    HostScope hs(ctx, "ped_d2h");
+    return points_double_encode_p3(ctx, (const uint32_t*)d_p3, m, out[0].data());
   }
   void* d_out = nullptr;
-  BPP_TRY(ctx_ws(ctx, "pp_out", v.size() * 32, &d_out));
+  BPP_TRY(ctx_ws(ctx, "pp_out", m * 32, &d_out));
   {
     HostScope hs(ctx, "ped_kernels");
-    BPP_TRY(pedersen_dev(ctx, g, d_v, d_g, v.size(), (uint32_t*)d_out, nullptr));
+    BPP_TRY(pedersen_dev(ctx, g, d_v, d_g, m, (uint32_t*)d_out, nullptr));
   }
   HostScope hs(ctx, "ped_d2h");
-  out.resize(v.size());
-  BPP_TRY(ctx_d2h(ctx, out.data(), d_out, v.size() * 32));
+  BPP_TRY(ctx_d2h(ctx, out.data(), d_out, m * 32));
   return BPP_OK;
 }
 
@@ -255,8 +282,12 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     void* d_i = nullptr;
     BPP_TRY(ctx_ws(ctx, "mt_i", idx.size() * 4 + 4, &d_i));
     BPP_TRY(ctx_h2d(ctx, d_i, idx.data(), idx.size() * 4));
+    // MSMs of the halved scalars, encoded as 2 * result (msm_multi_enc)
+    void* d_sh = nullptr;
+    BPP_TRY(ctx_ws(ctx, "mt_s_half", sc.size() * 32 + 32, &d_sh));
+    BPP_TRY(sc_halve_dev(ctx, d_s, (uint32_t*)d_sh, sc.size()));
     std::vector<uint8_t> enc(3 * P * 32);
-    BPP_TRY(msm_multi_enc(ctx, d_s, (const uint32_t*)d_i, off, pts, enc.data()));
+    BPP_TRY(msm_multi_enc(ctx, (const uint32_t*)d_sh, (const uint32_t*)d_i, off, pts, enc.data(), true));
     par::for_each(P, [&](size_t p) {
       memcpy(Ps[p].AI.data(), &enc[96 * p], 32);
       memcpy(Ps[p].AO.data(), &enc[96 * p + 32], 32);

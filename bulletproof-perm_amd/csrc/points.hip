@@ -5,9 +5,13 @@
 // Reference sites: compress circuit_lib.rs:231-233,368-412; decompress
 // circuit_lib.rs:532 (`unwrap()` -> BPP_ERR_DECOMPRESS here);
 // RistrettoPoint::random lib.rs:165-180 (from_uniform_bytes of rng bytes).
+#include <algorithm>
 #include <cstring>
+#include <vector>
 
 #include "ctx.h"
+#include "host/fe64.h"
+#include "host/par.h"
 #include "ge_io.cuh"
 
 __global__ void __launch_bounds__(64) k_decompress(const uint32_t* __restrict__ enc, size_t n, uint32_t* __restrict__ tbl,
@@ -76,6 +80,52 @@ int points_compress_p3(bpp_ctx* ctx, const uint32_t* d_p3, size_t n, uint8_t* ou
   BPP_TRY(ctx_check_launch(ctx, "k_compress_p3"));
   BPP_TRY(ctx_d2h(ctx, out_host, d_out, n * 32));
   return BPP_OK;
+}
+
+// Encodings of 2*P_i for n device points (P3 layout): the raw points come
+// back to the host and are encoded in chunks with one field inversion each
+// (h25519::encode_double_batch).  For small batches this beats the
+// per-point inverse-square-root chain of k_compress_p3 (~70 us of serial
+// field ops on one lane); callers compute P_i = C_i / 2 from halved scalars.
+int points_double_encode_p3(bpp_ctx* ctx, const uint32_t* d_p3, size_t n, uint8_t* out_host) {
+  if (!n) return BPP_OK;
+  std::vector<uint32_t> raw(n * P3_WORDS);
+  BPP_TRY(ctx_d2h(ctx, raw.data(), d_p3, n * P3_BYTES));
+  HostScope hs(ctx, "double_encode");
+  const size_t chunks = std::min<size_t>(par::threads(), (n + 7) / 8);
+  par::for_each(chunks, [&](size_t c) {
+    const size_t b = n * c / chunks, e = n * (c + 1) / chunks;
+    std::vector<h25519::ge> pts(e - b);
+    for (size_t i = b; i < e; ++i) pts[i - b] = h25519::ge_from_dev(raw.data() + i * P3_WORDS);
+    h25519::encode_double_batch(pts.data(), e - b, out_host + 32 * b);
+  });
+  return BPP_OK;
+}
+
+// s / 2 mod l for canonical scalars: s even -> s >> 1, odd -> (s + l) >> 1
+__global__ void __launch_bounds__(256) k_sc_halve(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                 size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  static constexpr uint32_t Lw[8] = {0x5cf5d3edu, 0x5812631au, 0xa2f79cd6u, 0x14def9deu, 0, 0, 0, 0x10000000u};
+  uint32_t s[8];
+  _Pragma("unroll") for (int k = 0; k < 8; ++k) s[k] = in[8 * i + k];
+  const uint32_t odd = s[0] & 1u;
+  uint64_t c = 0;
+  _Pragma("unroll") for (int k = 0; k < 8; ++k) {
+    c += (uint64_t)s[k] + (odd ? Lw[k] : 0u);
+    s[k] = (uint32_t)c;
+    c >>= 32;
+  }
+  _Pragma("unroll") for (int k = 0; k < 7; ++k) s[k] = (s[k] >> 1) | (s[k + 1] << 31);
+  s[7] >>= 1;  // s + l < 2^254: no carry out
+  _Pragma("unroll") for (int k = 0; k < 8; ++k) out[8 * i + k] = s[k];
+}
+
+int sc_halve_dev(bpp_ctx* ctx, const uint32_t* d_in, uint32_t* d_out, size_t n) {
+  if (!n) return BPP_OK;
+  hipLaunchKernelGGL(k_sc_halve, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, d_in, d_out, n);
+  return ctx_check_launch(ctx, "k_sc_halve");
 }
 
 extern "C" {

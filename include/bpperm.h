@@ -110,6 +110,13 @@ int bpp_msm_table_dev_partial(bpp_ctx* ctx, const void* d_scalars, const bpp_poi
                               uint32_t w_begin, uint32_t w_end, uint8_t partial[128]);
 /* Sum raw extended partial points (count x 128 bytes) and compress. */
 int bpp_partials_finish(const uint8_t* partials, size_t count, uint8_t out[32]);
+/* Host batch encoding of doubled points: out[i] = compress(2 * P_i) for raw
+ * extended points P_i (count x 128 bytes), one field inversion per call
+ * instead of one inverse square root per point (the prover computes C / 2
+ * from halved scalars and encodes C this way).  Replaces the per-point
+ * RistrettoPoint::compress of the reference's commitments and IPA L/R
+ * (circuit_lib.rs:231-233) where batches are small; host-only. */
+int bpp_points_double_compress(const uint8_t* raw, size_t count, uint8_t* out);
 /* count independent MSMs; MSM j covers terms [offsets[j], offsets[j+1]) of
  * `scalars` (32 bytes each) and `point_idx` (indices into tbl). */
 int bpp_msm_batch(bpp_ctx* ctx, size_t count, const uint64_t* offsets, const uint8_t* scalars,

@@ -28,6 +28,6 @@ print(f"B={B} threads={os.environ.get('BPP_HOST_THREADS')} streams={os.environ.g
       f"reps={ts} profiled wall={w:.2f} ms")
 for st in ("pb_rng", "pb_pedersen_V", "pb_pedersen_Vx_witness", "pb_msm_AI_AO_S", "pb_host_poly", "pbT_pedersen",
            "pbT_host", "pb_ipa", "ipa_msm", "ipa_host", "ped_upload", "ped_kernels", "ped_d2h", "pedersen",
-           "compress", "msm_direct"):
+           "compress", "msm_direct", "double_encode", "poly_coef", "poly_x"):
     ms, k = ctx.profile_get(st)
     print(f"  {st:22s} {ms:8.3f} ms over {k}")

@@ -2,7 +2,8 @@
 
     python bulletproof-perm_amd/build.py [--debug]
 
-Every .hip / .cpp under csrc/ is compiled with hipcc --offload-arch=gfx950
+Every .hip under csrc/ is compiled with hipcc --offload-arch=gfx950 (host/*.cpp
+with the host C++ compiler, g++ by default)
 into build/ and linked into bpperm/libbpperm.so next to the ctypes wrapper,
 so the shared object travels with a gpurun snapshot.
 """
@@ -19,6 +20,7 @@ CSRC = ROOT / "csrc"
 BUILD = ROOT / "build"
 OUT = ROOT / "bpperm" / "libbpperm.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+HOSTCXX = os.environ.get("BPP_HOSTCXX", "g++")
 ARCH = os.environ.get("BPP_ARCH", "gfx950")
 
 
@@ -32,8 +34,12 @@ def _compile(src: Path, flags, bdir: Path = BUILD) -> Path:
         [ROOT.parent / "include" / "bpperm.h"]
     if obj.exists() and obj.stat().st_mtime >= max(d.stat().st_mtime for d in deps):
         return obj
-    lang = ["-x", "hip"] if src.suffix == ".hip" else []
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", *flags, *lang, "-c", str(src), "-o", str(obj)]
+    if src.suffix == ".hip":
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", *flags, "-x", "hip", "-c", str(src), "-o",
+               str(obj)]
+    else:  # host-only C++ (Keccak, circuit): the host compiler, no device pass
+        hflags = [f for f in flags if f not in ("-Xarch_host", "-Wno-pass-failed")]
+        cmd = [HOSTCXX, "-fPIC", "-std=c++17", *hflags, "-c", str(src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

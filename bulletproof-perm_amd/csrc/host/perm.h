@@ -64,6 +64,13 @@ struct Rng {
 
 std::vector<uint32_t> fisher_yates(uint32_t k, Rng& rng);
 
+// The prover's random draws from SHAKE256("bpperm-prove" || seed), in the
+// fixed order pi (Fisher-Yates), gamma[m], alpha, beta, rho, s_L[n_p],
+// s_R[n_p], tau[5] (the stand-in for thread_rng, circuit_lib.rs:175).
+void draw_prover_randomness(const Circuit& C, uint64_t seed, std::vector<uint32_t>& pi, std::vector<hsc::Sc>& gamma,
+                            hsc::Sc& alpha, hsc::Sc& beta, hsc::Sc& rho, std::vector<hsc::Sc>& sL,
+                            std::vector<hsc::Sc>& sR, std::vector<hsc::Sc>& taus);
+
 size_t proof_len(uint32_t k);
 
 }  // namespace perm

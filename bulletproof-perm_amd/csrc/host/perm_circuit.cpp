@@ -112,6 +112,24 @@ std::vector<uint32_t> fisher_yates(uint32_t k, Rng& rng) {
   return p;
 }
 
+void draw_prover_randomness(const Circuit& C, uint64_t seed, std::vector<uint32_t>& pi, std::vector<Sc>& gamma,
+                            Sc& alpha, Sc& beta, Sc& rho, std::vector<Sc>& sL, std::vector<Sc>& sR,
+                            std::vector<Sc>& taus) {
+  Rng rng("bpperm-prove", seed);
+  pi = fisher_yates(C.k, rng);
+  gamma.resize(C.m);
+  for (auto& g : gamma) g = rng.scalar();
+  alpha = rng.scalar();
+  beta = rng.scalar();
+  rho = rng.scalar();
+  sL.resize(C.n_p);
+  sR.resize(C.n_p);
+  taus.resize(5);
+  for (auto& x : sL) x = rng.scalar();
+  for (auto& x : sR) x = rng.scalar();
+  for (auto& x : taus) x = rng.scalar();
+}
+
 size_t proof_len(uint32_t k) {
   Circuit C;
   uint32_t n_p = 1, lg = 0;

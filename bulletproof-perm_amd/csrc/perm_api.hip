@@ -196,19 +196,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
   std::unique_ptr<HostScope> hs(new HostScope(ctx, "pb_rng"));
   par::for_each(P, [&](size_t p) {
     ProverState& st = *S[p];
-    perm::Rng rng("bpperm-prove", seeds[p]);
-    st.pi = perm::fisher_yates(k, rng);
-    st.gamma.resize(m);
-    for (auto& g : st.gamma) g = rng.scalar();
-    st.alpha = rng.scalar();
-    st.beta = rng.scalar();
-    st.rho = rng.scalar();
-    st.sL.resize(n_p);
-    st.sR.resize(n_p);
-    st.taus.resize(5);
-    for (auto& x : st.sL) x = rng.scalar();
-    for (auto& x : st.sR) x = rng.scalar();
-    for (auto& x : st.taus) x = rng.scalar();
+    perm::draw_prover_randomness(C, seeds[p], st.pi, st.gamma, st.alpha, st.beta, st.rho, st.sL, st.sR, st.taus);
     st.tr.arithmetic_domain_sep(n_p);
   });
 

@@ -9,6 +9,7 @@
 
 #define FB_POS 64  // radix-16 positions per fixed base
 #define GENS_DT_MAX 4096  // generators for which direct tables are kept (2 GB at the limit)
+#define GENS_DT16_MAX 320  // ... with 16-bit windows (20 GB at the limit)
 
 struct bpp_gens {
   bpp_ctx* ctx = nullptr;
@@ -17,9 +18,12 @@ struct bpp_gens {
   uint32_t* d_fb = nullptr;   // fixed-base tables for B and Bb: 2 x 64 x 8 Niels
   // window tables of every generator (FBW_W x 128 B each), built on first use
   mutable uint32_t* d_wt = nullptr;
-  // direct tables d * 2^(8w) * P (512 KB per generator), built on first use
-  // when 2n+2 <= GENS_DT_MAX
+  // direct tables d * 2^(c w) * P, built on first use when 2n+2 <=
+  // GENS_DT_MAX: c = 8 (512 KB per generator, 32 table additions per
+  // scalar), or c = 16 with BPP_DT_C=16 up to GENS_DT16_MAX generators
+  // (64 MB per generator, 16 additions)
   mutable uint32_t* d_dt = nullptr;
+  mutable uint32_t dt_c = 8;
   uint32_t gidx(size_t i) const { return (uint32_t)i; }
   uint32_t hidx(size_t i) const { return (uint32_t)(n + i); }
   uint32_t bidx() const { return (uint32_t)(2 * n); }

@@ -502,12 +502,28 @@ static bool fb_wins(double terms_per_msm) {
   return pol == 1 || (pol == -1 && terms_per_msm <= 16384.0);
 }
 
-int dt_build(bpp_ctx* ctx, const uint32_t* d_wt, uint32_t npts, uint32_t* d_dt) {
+static DtGeom dt_geom(uint32_t c) {
+  DtGeom g;
+  g.c = c;
+  g.W = 256 / c;
+  return g;
+}
+
+size_t dt_bytes(uint32_t npts, uint32_t c) {
+  return (size_t)npts * (256 / c) * ((size_t)1 << (c - 1)) * MSM_NIELS_WORDS * 4;
+}
+
+int dt_build(bpp_ctx* ctx, const uint32_t* d_wt, uint32_t npts, uint32_t c, uint32_t* d_dt) {
   if (!npts) return BPP_OK;
+  if (c != 8 && c != 16) {
+    ctx->err = "dt_build: window width must be 8 or 16";
+    return BPP_ERR_ARG;
+  }
+  const DtGeom g = dt_geom(c);
   {
     ProfScope ps(ctx, "dt_tables");
-    hipLaunchKernelGGL(k_dt_build, dim3(grid_for((size_t)npts * DT_ROWS_PER_GEN, 64)), dim3(64), 0, ctx->stream, d_wt,
-                       npts, d_dt);
+    const size_t rows = (size_t)npts * g.W * ((size_t)1 << (c - 1));
+    hipLaunchKernelGGL(k_dt_build, dim3(grid_for(rows, 64)), dim3(64), 0, ctx->stream, d_wt, npts, g, d_dt);
   }
   return ctx_check_launch(ctx, "k_dt_build");
 }
@@ -528,7 +544,8 @@ static int msm_multi_dt_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t
   BPP_TRY(ctx_ws(ctx, "multi_off", (M + 1) * 4, &d_off));
   BPP_TRY(ctx_h2d(ctx, d_off, off.data(), (M + 1) * 4));
   BPP_TRY(ctx_ws(ctx, "dt_res", (size_t)M * P3_BYTES, &res));
-  const double e_avg = (double)T * DT_W / (double)M;  // table additions per MSM
+  const DtGeom dg = dt_geom(pts.dt_c);
+  const double e_avg = (double)T * dg.W / (double)M;  // table additions per MSM
   // 256 lanes per MSM measured best for the prover's batches (M = 256-384
   // MSMs: 0.99 ms of direct-table time per 128 proofs vs 1.10-1.20 at 512
   // and 1.42 at 128); 512 only when few large MSMs leave the chip empty
@@ -538,16 +555,16 @@ static int msm_multi_dt_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t
     ProfScope ps(ctx, "msm_direct");
     // (no 1024-thread variant: capped at 128 VGPRs it spills in the main loop)
     if (nt == 128)
-      hipLaunchKernelGGL(k_dt_msm<128>, dim3(M), dim3(128), 0, ctx->stream, pts.dt, d_scal, d_pidx,
+      hipLaunchKernelGGL(k_dt_msm<128>, dim3(M), dim3(128), 0, ctx->stream, pts.dt, dg, d_scal, d_pidx,
                          (const uint32_t*)d_off, (uint32_t*)res);
     else if (nt == 512)
-      hipLaunchKernelGGL(k_dt_msm<512>, dim3(M), dim3(512), 0, ctx->stream, pts.dt, d_scal, d_pidx,
+      hipLaunchKernelGGL(k_dt_msm<512>, dim3(M), dim3(512), 0, ctx->stream, pts.dt, dg, d_scal, d_pidx,
                          (const uint32_t*)d_off, (uint32_t*)res);
     else if (nt == 256)
-      hipLaunchKernelGGL(k_dt_msm<256>, dim3(M), dim3(256), 0, ctx->stream, pts.dt, d_scal, d_pidx,
+      hipLaunchKernelGGL(k_dt_msm<256>, dim3(M), dim3(256), 0, ctx->stream, pts.dt, dg, d_scal, d_pidx,
                          (const uint32_t*)d_off, (uint32_t*)res);
     else
-      hipLaunchKernelGGL(k_dt_msm<64>, dim3(M), dim3(64), 0, ctx->stream, pts.dt, d_scal, d_pidx,
+      hipLaunchKernelGGL(k_dt_msm<64>, dim3(M), dim3(64), 0, ctx->stream, pts.dt, dg, d_scal, d_pidx,
                          (const uint32_t*)d_off, (uint32_t*)res);
   }
   BPP_TRY(ctx_check_launch(ctx, "k_dt_msm"));

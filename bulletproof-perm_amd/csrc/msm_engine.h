@@ -37,10 +37,14 @@ struct MsmPoints {
   uint32_t n0 = 0xffffffffu;
   const uint32_t* wt = nullptr;
   const uint32_t* wt1 = nullptr;
-  const uint32_t* dt = nullptr;  // direct radix-2^8 tables of tbl (msm_kernels.cuh k_dt_msm), or null
+  const uint32_t* dt = nullptr;  // direct radix-2^dt_c tables of tbl (msm_kernels.cuh k_dt_msm), or null
+  uint32_t dt_c = 8;
 };
-// d * 2^(8w) * P for every table point, w < 32, d = 1..128 (128-B rows)
-int dt_build(bpp_ctx* ctx, const uint32_t* d_wt, uint32_t npts, uint32_t* d_dt);
+// d * 2^(c w) * P for every table point, w < 256 / c, d = 1..2^(c-1)
+// (128-B rows; c = 8 or 16)
+int dt_build(bpp_ctx* ctx, const uint32_t* d_wt, uint32_t npts, uint32_t c, uint32_t* d_dt);
+// bytes of the direct tables of npts points at window width c
+size_t dt_bytes(uint32_t npts, uint32_t c);
 // Adds nx extra points (device Niels table d_x) at indices n0.. to *pts,
 // building their window tables in workspace `ws_name` when pts has tables
 // and MSMs of `terms_per_msm` terms would take the fixed-base engine.

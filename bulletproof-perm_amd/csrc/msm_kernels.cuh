@@ -627,17 +627,18 @@ __global__ void __launch_bounds__(RS_T) k_rsort_fine(const uint32_t* __restrict_
 }
 
 // ---------------------------------------------------------------------------
-// Direct fixed-base MSM over full radix-2^8 tables (small MSMs over
-// resident generators: A_I/A_O/S, IPA rounds, vector commitments).
-// Table row ((gen * 32 + w) << 7) + |d| - 1 holds d * 2^(8w) * G_gen
-// (d = 1..128), so a term is at most 32 table additions and an MSM is one
-// flat sum: no digit sort, no buckets, no bucket reduction.  One block per
-// MSM; lane j adds its slice of the MSM's (term, window) pairs, then a
+// Direct fixed-base MSM over full radix-2^c tables (c = 8 or 16; small MSMs
+// over resident generators: A_I/A_O/S, IPA rounds, vector commitments).
+// With W = 256 / c windows and h = 2^(c-1) rows per window, table row
+// (gen * W + w) * h + |d| - 1 holds d * 2^(c w) * G_gen (d = 1..h, signed
+// digits), so a term is at most W table additions and an MSM is one flat
+// sum: no digit sort, no buckets, no bucket reduction.  One block per MSM;
+// lane j adds its slice of the MSM's (term, window) pairs, then a
 // wave-shuffle tree and an LDS step over the block's waves.
-#define DT_W 32
-#define DT_ROWS_PER_GEN (DT_W * 128)
-
-FE_INLINE uint32_t scalar_byte(const uint32_t s[8], uint32_t i) { return (s[i >> 2] >> (8 * (i & 3))) & 0xffu; }
+struct DtGeom {
+  uint32_t c, W;  // window bits (8 or 16), windows (32 or 16)
+};
+FE_INLINE uint32_t dt_half(const DtGeom& g) { return 1u << (g.c - 1); }
 
 FE_INLINE ge_p3 ge_shfl_xor(const ge_p3& a, int m) {
   ge_p3 o;
@@ -650,34 +651,49 @@ FE_INLINE ge_p3 ge_shfl_xor(const ge_p3& a, int m) {
   return o;
 }
 
+// Bits [pos, pos + c) of a 256-bit scalar held in registers, with the word
+// picked by selects (a runtime index into s[] would put it in scratch).
+FE_INLINE uint32_t word_sel(const uint32_t s[8], uint32_t i) {
+  uint32_t r = 0;
+  _Pragma("unroll") for (uint32_t k = 0; k < 8; ++k) r = (i == k) ? s[k] : r;
+  return r;
+}
+FE_INLINE uint32_t scalar_bits_sel(const uint32_t s[8], uint32_t pos, uint32_t c) {
+  const uint32_t wi = pos >> 5, sh = pos & 31;
+  const uint64_t v = ((uint64_t)word_sel(s, wi) | ((uint64_t)word_sel(s, wi + 1) << 32)) >> sh;
+  return (uint32_t)v & ((1u << c) - 1u);
+}
+
 // Lane-local walk over the nonzero (term, window) digits of its slice.
 struct DtWalk {
   const uint32_t* scalars;
   const uint32_t* pidx;
+  DtGeom g;
   uint32_t t0, e, e1, cur, gen, carry;
   uint32_t s[8];
   // next nonzero digit -> table row and sign; false when the slice is done
   FE_INLINE bool next(uint32_t& row, bool& neg) {
+    const uint32_t half = dt_half(g);
     for (; e < e1; ++e) {
-      const uint32_t t = t0 + e / DT_W, w = e % DT_W;
+      const uint32_t t = t0 + e / g.W, w = e % g.W;
       if (t != cur) {  // (re)enter a term: scalar, generator, carry into window w
         cur = t;
         load_scalar(scalars, t, s);
         gen = pidx ? pidx[t] : t;
         carry = 0;
-        for (uint32_t ww = 0; ww < w; ++ww) carry = (scalar_byte(s, ww) + carry) >= 128u ? 1u : 0u;
+        for (uint32_t ww = 0; ww < w; ++ww) carry = (scalar_bits_sel(s, ww * g.c, g.c) + carry) >= half ? 1u : 0u;
       }
-      const uint32_t v = scalar_byte(s, w) + carry;
+      const uint32_t v = scalar_bits_sel(s, w * g.c, g.c) + carry;
       int d;
-      if (v >= 128u && w + 1 < DT_W) {
-        d = (int)v - 256;
+      if (v >= half && w + 1 < g.W) {
+        d = (int)v - (int)(2 * half);
         carry = 1;
       } else {
         d = (int)v;
         carry = 0;
       }
       if (d == 0) continue;
-      row = gen * DT_ROWS_PER_GEN + w * 128u + (uint32_t)((d < 0 ? -d : d) - 1);
+      row = (gen * g.W + w) * half + (uint32_t)((d < 0 ? -d : d) - 1);
       neg = d < 0;
       ++e;
       return true;
@@ -687,16 +703,18 @@ struct DtWalk {
 };
 
 template <int NT>
-__global__ void __launch_bounds__(NT) k_dt_msm(const uint32_t* __restrict__ dt, const uint32_t* __restrict__ scalars,
+__global__ void __launch_bounds__(NT) k_dt_msm(const uint32_t* __restrict__ dt, DtGeom dg,
+                                               const uint32_t* __restrict__ scalars,
                                                const uint32_t* __restrict__ pidx, const uint32_t* __restrict__ off,
                                                uint32_t* __restrict__ out_p3) {
   __shared__ uint32_t lds[(NT / 64) * P3_WORDS];
   const uint32_t m = blockIdx.x;
   const uint32_t t0 = off[m], t1 = off[m + 1];
-  const uint64_t E = (uint64_t)(t1 - t0) * DT_W;
+  const uint64_t E = (uint64_t)(t1 - t0) * dg.W;
   DtWalk it;
   it.scalars = scalars;
   it.pidx = pidx;
+  it.g = dg;
   it.t0 = t0;
   it.e = (uint32_t)(E * threadIdx.x / NT);
   it.e1 = (uint32_t)(E * (threadIdx.x + 1) / NT);
@@ -721,14 +739,17 @@ __global__ void __launch_bounds__(NT) k_dt_msm(const uint32_t* __restrict__ dt, 
   if (threadIdx.x == 0) store_p3(out_p3, m, acc);
 }
 
-// Direct tables from the window tables: lane (k, w, d) -> d * wt[k*32 + w].
-__global__ void __launch_bounds__(64) k_dt_build(const uint32_t* __restrict__ wt, uint32_t ngen,
+// Direct tables from the window tables (wt[k * 32 + u] = 2^(8u) P_k):
+// lane (k, w, d) -> d * 2^(c w) P_k = d * wt[k * 32 + w c / 8].
+__global__ void __launch_bounds__(64) k_dt_build(const uint32_t* __restrict__ wt, uint32_t ngen, DtGeom dg,
                                                  uint32_t* __restrict__ dt) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (size_t)ngen * DT_ROWS_PER_GEN) return;
-  const uint32_t d = (uint32_t)(i & 127u) + 1u;
-  const size_t kw = i >> 7;  // k * 32 + w
-  const ge_p3 Q = ge_from_niels(load_niels(wt, (uint32_t)kw));
+  const uint32_t half = dt_half(dg);
+  if (i >= (size_t)ngen * dg.W * half) return;
+  const uint32_t d = (uint32_t)(i & (half - 1)) + 1u;
+  const size_t kw = i >> (dg.c - 1);  // k * W + w
+  const uint32_t k = (uint32_t)(kw / dg.W), w = (uint32_t)(kw % dg.W);
+  const ge_p3 Q = ge_from_niels(load_niels(wt, k * 32u + w * (dg.c / 8u)));
   ge_p3 R = Q;
   const int top = 31 - __clz(d);
   for (int b = top - 1; b >= 0; --b) {

@@ -133,15 +133,32 @@ static inline bool from_canonical(Sc& out, const uint8_t b[32]) {
 }
 
 // dalek Scalar::from_bytes_mod_order_wide (64 bytes)
+// x = lo + hi * 2^256: hi * 2^256 mod l = mont(hi, R2) (one Montgomery
+// product), lo mod l by folding its top 4 bits (2^252 = -delta mod l with
+// delta = l - 2^252 < 2^125).
+static inline Sc reduce256(Sc a) {
+  const uint64_t q = a.v[3] >> 60;  // a = q * 2^252 + (a mod 2^252)
+  a.v[3] &= 0x0fffffffffffffffULL;
+  // a - q * delta, delta = L.v[0..1] (L = 2^252 + delta)
+  const u128 p0 = (u128)q * L.v[0], p1 = (u128)q * L.v[1] + (uint64_t)(p0 >> 64);
+  const Sc qd = {{(uint64_t)p0, (uint64_t)p1, (uint64_t)(p1 >> 64), 0}};
+  uint64_t br;
+  Sc r = sub_raw(a, qd, &br);
+  if (br) {  // negative (> -2^129): add l once
+    u128 c = 0;
+    for (int i = 0; i < 4; ++i) {
+      c = (u128)r.v[i] + L.v[i] + (uint64_t)(c >> 64);
+      r.v[i] = (uint64_t)c;
+    }
+  }
+  return r;
+}
+
 static inline Sc from_wide(const uint8_t b[64]) {
   Sc lo, hi;
   memcpy(lo.v, b, 32);
   memcpy(hi.v, b + 32, 32);
-  // lo*R*R^-1... : mont(lo, R2) = lo*R mod l (Montgomery form of lo)
-  Sc a = mont(lo, R2);
-  Sc c = mont(hi, R3);  // hi*R^2 mod l = Montgomery form of hi*2^256
-  Sc s = add(a, c);
-  return mont(s, one());  // leave Montgomery form
+  return add(reduce256(lo), mont(hi, R2));
 }
 
 // dalek Scalar::from_bytes_mod_order (32 bytes, any value)

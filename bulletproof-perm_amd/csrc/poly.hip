@@ -4,7 +4,7 @@
 // the proofs of a lockstep batch).  Host side: the transcript challenges
 // (y, z, x) and scalar bookkeeping only.
 //
-// Per proof (one workgroup, lane i = gate i, n_p gates; Montgomery domain,
+// Per proof (one workgroup; lane i handles gates i, i + 256, ...; Montgomery domain,
 // R = 2^256 as in sc25519.cuh and host/scalar.h):
 //   k_poly_coef  y^i, y^-i, z^(q+1) (LDS), the sparse column sums
 //                zW_L, zW_R, zW_O (column-CSR of the circuit matrices), the
@@ -22,6 +22,7 @@
 #include "sc25519.cuh"
 
 #define POLY_SLOTS 7  // l1 r0 r1 r3 l2 l3 (Montgomery) per gate
+#define POLY_T 256    // lanes per proof; lane i handles gates i, i + POLY_T, ...
 
 FE_INLINE sc sc_one_mont() {
   sc one = sc_zero();
@@ -63,8 +64,8 @@ FE_INLINE sc col_sum(const uint32_t* __restrict__ cp, const uint32_t* __restrict
   return acc;
 }
 
-// grid = P proofs, block = max(64, n_p); dynamic LDS = Q * 32 + 16 * 6 * 32
-__global__ void __launch_bounds__(1024) k_poly_coef(uint32_t n_p, uint32_t Q, uint32_t per,
+// grid = P proofs, block = poly_block(n_p); dynamic LDS = Q * 32 + (POLY_T / 64) * 6 * 32
+__global__ void __launch_bounds__(POLY_T) k_poly_coef(uint32_t n_p, uint32_t Q, uint32_t per,
                                                    const uint32_t* __restrict__ sc_in,
                                                    const uint32_t* __restrict__ ch,
                                                    const uint32_t* __restrict__ cp, const uint32_t* __restrict__ ce,
@@ -73,15 +74,15 @@ __global__ void __launch_bounds__(1024) k_poly_coef(uint32_t n_p, uint32_t Q, ui
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* zp = lds;           // [Q] z^(q+1)
   uint32_t* red = lds + 8 * Q;  // reduction scratch
-  const uint32_t p = blockIdx.x, i = threadIdx.x;
+  const uint32_t p = blockIdx.x;
   const sc oneR = sc_one_mont();
   const sc yR = sc_to_mont(sc_load(ch + 24 * p)), yiR = sc_to_mont(sc_load(ch + 24 * p + 8)),
            zR = sc_to_mont(sc_load(ch + 24 * p + 16));
-  for (uint32_t q = i; q < Q; q += blockDim.x) sc_store(zp + 8 * q, sc_pow_small(zR, q + 1, oneR));
+  for (uint32_t q = threadIdx.x; q < Q; q += blockDim.x) sc_store(zp + 8 * q, sc_pow_small(zR, q + 1, oneR));
   __syncthreads();
   sc t[6];
   _Pragma("unroll") for (int j = 0; j < 6; ++j) t[j] = sc_zero();
-  if (i < n_p) {
+  for (uint32_t i = threadIdx.x; i < n_p; i += blockDim.x) {
     const uint32_t* s = sc_in + (size_t)p * per * 8;
     const sc aL = sc_to_mont(sc_load(s + 8 * (1 + i)));
     const sc aR = sc_to_mont(sc_load(s + 8 * (1 + n_p + i)));
@@ -95,12 +96,12 @@ __global__ void __launch_bounds__(1024) k_poly_coef(uint32_t n_p, uint32_t Q, ui
     const sc r0 = sc_sub(zWO, yp);
     const sc r1 = sc_add(sc_mont(aR, yp), zWL);
     const sc r3 = sc_mont(sR, yp);
-    t[0] = sc_mont(l1, r0);
-    t[1] = sc_add(sc_mont(l1, r1), sc_mont(l2, r0));
-    t[2] = sc_add(sc_mont(l2, r1), sc_mont(l3, r0));
-    t[3] = sc_add(sc_mont(l1, r3), sc_mont(l3, r1));
-    t[4] = sc_mont(l2, r3);
-    t[5] = sc_mont(l3, r3);
+    t[0] = sc_add(t[0], sc_mont(l1, r0));
+    t[1] = sc_add(t[1], sc_add(sc_mont(l1, r1), sc_mont(l2, r0)));
+    t[2] = sc_add(t[2], sc_add(sc_mont(l2, r1), sc_mont(l3, r0)));
+    t[3] = sc_add(t[3], sc_add(sc_mont(l1, r3), sc_mont(l3, r1)));
+    t[4] = sc_add(t[4], sc_mont(l2, r3));
+    t[5] = sc_add(t[5], sc_mont(l3, r3));
     uint32_t* v = vec + ((size_t)p * n_p + i) * POLY_SLOTS * 8;
     sc_store(v + 0, l1);
     sc_store(v + 8, r0);
@@ -111,31 +112,31 @@ __global__ void __launch_bounds__(1024) k_poly_coef(uint32_t n_p, uint32_t Q, ui
     sc_store(hf + ((size_t)p * n_p + i) * 8, sc_from_mont(yip));  // H factors y^-i
   }
   sc_block_sum<6>(t, red);
-  if (i == 0)
+  if (threadIdx.x == 0)
     _Pragma("unroll") for (int j = 0; j < 6; ++j) sc_store(t_out + (6 * p + j) * 8, sc_from_mont(t[j]));
 }
 
-// grid = P, block = max(64, n_p)
-__global__ void __launch_bounds__(1024) k_poly_x(uint32_t n_p, const uint32_t* __restrict__ xs,
+// grid = P, block = poly_block(n_p)
+__global__ void __launch_bounds__(POLY_T) k_poly_x(uint32_t n_p, const uint32_t* __restrict__ xs,
                                                 const uint32_t* __restrict__ vec, uint32_t* __restrict__ l_out,
                                                 uint32_t* __restrict__ r_out, uint32_t* __restrict__ that_out) {
-  __shared__ __attribute__((aligned(16))) uint32_t red[16 * 8];
-  const uint32_t p = blockIdx.x, i = threadIdx.x;
+  __shared__ __attribute__((aligned(16))) uint32_t red[(POLY_T / 64) * 8];
+  const uint32_t p = blockIdx.x;
   const sc xR = sc_to_mont(sc_load(xs + 8 * p));
   const sc x2R = sc_mont(xR, xR);
   sc th[1] = {sc_zero()};
-  if (i < n_p) {
+  for (uint32_t i = threadIdx.x; i < n_p; i += blockDim.x) {
     const uint32_t* v = vec + ((size_t)p * n_p + i) * POLY_SLOTS * 8;
     const sc l1 = sc_load(v), r0 = sc_load(v + 8), r1 = sc_load(v + 16), r3 = sc_load(v + 24), l2 = sc_load(v + 32),
              l3 = sc_load(v + 40);
     const sc l = sc_mont(sc_add(l1, sc_mont(sc_add(l2, sc_mont(l3, xR)), xR)), xR);
     const sc r = sc_add(r0, sc_mont(sc_add(r1, sc_mont(r3, x2R)), xR));
-    th[0] = sc_mont(l, r);
+    th[0] = sc_add(th[0], sc_mont(l, r));
     sc_store(l_out + ((size_t)p * n_p + i) * 8, sc_from_mont(l));
     sc_store(r_out + ((size_t)p * n_p + i) * 8, sc_from_mont(r));
   }
   sc_block_sum<1>(th, red);
-  if (i == 0) sc_store(that_out + 8 * p, sc_from_mont(th[0]));
+  if (threadIdx.x == 0) sc_store(that_out + 8 * p, sc_from_mont(th[0]));
 }
 
 namespace {
@@ -165,16 +166,12 @@ void build_csr(const perm::Circuit& C, std::vector<uint32_t>& cp, std::vector<ui
   }
 }
 
-unsigned poly_block(uint32_t n_p) { return n_p < 64 ? 64u : n_p; }
+unsigned poly_block(uint32_t n_p) { return n_p < 64 ? 64u : (n_p > POLY_T ? POLY_T : n_p); }
 
 }  // namespace
 
 int poly_coef_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint32_t* d_sc, uint32_t per,
                   const std::vector<hsc::Sc>& ch, std::vector<hsc::Sc>& t) {
-  if (C.n_p > 1024) {
-    ctx->err = "poly_coef_dev: n_p > 1024";
-    return BPP_ERR_ARG;
-  }
   std::vector<uint32_t> cp, ce;
   build_csr(C, cp, ce);
   void *d_cp, *d_ce, *d_ch, *d_vec, *d_hf, *d_t;
@@ -188,7 +185,7 @@ int poly_coef_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint32
   BPP_TRY(ctx_h2d(ctx, d_ce, ce.data(), ce.size() * 4));
   BPP_TRY(ctx_h2d(ctx, d_ch, ch.data(), ch.size() * 32));
   const unsigned nt = poly_block(C.n_p);
-  const size_t lds = (size_t)C.Q * 32 + 16 * 6 * 32;
+  const size_t lds = (size_t)C.Q * 32 + (POLY_T / 64) * 6 * 32;
   {
     ProfScope ps(ctx, "poly_coef");
     hipLaunchKernelGGL(k_poly_coef, dim3(P), dim3(nt), lds, ctx->stream, C.n_p, C.Q, per, d_sc,

@@ -49,7 +49,8 @@ static unsigned grid_for(size_t n, unsigned t) { return (unsigned)((n + t - 1) /
 
 int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const uint32_t* d_off, uint32_t M,
                uint32_t T, uint32_t c, uint32_t wb, uint32_t Wn, const uint32_t* d_tbl, uint32_t** d_wsum_out,
-               const uint32_t* d_tbl1, uint32_t n0, bool fb) {
+               const uint32_t* d_tbl1, uint32_t n0, bool fb, uint32_t* terms_out) {
+  if (terms_out) *terms_out = 1;
   MsmGeom g;
   g.M = M;
   g.T = T;
@@ -204,6 +205,26 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
                          (const uint32_t*)heavy, (uint32_t*)bsum);
     }
     BPP_TRY(ctx_check_launch(ctx, "k_msm_fixup_heavy"));
+    if (terms_out && M == 1 && !fb && g.B >= (1u << RWAVE_SHIFT) && g.B <= (64u << RWAVE_SHIFT) &&
+        !getenv("BPP_MSM_OLD_REDUCE")) {
+      // power-of-two weights left to the host Horner (k_msm_reduce_wave)
+      const uint32_t nw = g.B >> RWAVE_SHIFT;
+      uint32_t J = 0;
+      while ((1u << J) < nw) ++J;
+      void* part = nullptr;
+      BPP_TRY(ctx_ws(ctx, "msm_rpart", nseg * nw * 2 * P3_BYTES, &part));
+      BPP_TRY(ctx_ws(ctx, "msm_wsum_terms", nseg * (1 + J) * P3_BYTES, &wsum));
+      ProfScope ps(ctx, "msm_reduce");
+      hipLaunchKernelGGL(k_msm_reduce_wave, dim3((unsigned)(nseg * nw)), dim3(64), 0, ctx->stream,
+                         (const uint32_t*)boff, ks, (const uint32_t*)head, (const uint32_t*)tail, (const uint32_t*)bsum,
+                         g, (uint32_t*)part);
+      hipLaunchKernelGGL(k_msm_reduce_bits, dim3((unsigned)(nseg * (1 + J))), dim3(64), 0, ctx->stream,
+                         (const uint32_t*)part, g, 1 + J, (uint32_t*)wsum);
+      BPP_TRY(ctx_check_launch(ctx, "k_msm_reduce_wave/bits"));
+      *terms_out = 1 + J;
+      *d_wsum_out = (uint32_t*)wsum;
+      return BPP_OK;
+    }
     const uint32_t L = g.B >= 512 ? 8 : (g.B >= 64 ? 4 : (g.B >= 8 ? 2 : 1));  // <= RED_LMAX
     const uint32_t BPS = (g.B + RED_T * L - 1) / (RED_T * L);
     void* part = wsum;  // one block per segment: its partial is the sum
@@ -223,13 +244,29 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
 
 // Host Horner: sum_j 2^(c*(wb+j)) * ws[j], j < Wn.
 static h25519::ge horner_host(const uint32_t* ws_words, uint32_t Wn, uint32_t c, uint32_t wb) {
+  return horner_host_terms(ws_words, Wn, 1, c, wb);
+}
+
+// Window j = term 0 + sum_k 2^(RWAVE_SHIFT + k) term 1+k: one Horner pass
+// over all terms in descending bit position (the term offsets < c fall
+// between the doublings the window combine does anyway).
+h25519::ge horner_host_terms(const uint32_t* ws_words, uint32_t Wn, uint32_t nterms, uint32_t c, uint32_t wb) {
   using namespace h25519;
-  ge acc = ge_from_dev(ws_words + (size_t)(Wn - 1) * P3_WORDS);
-  for (int j = (int)Wn - 2; j >= 0; --j) {
-    for (uint32_t k = 0; k < c; ++k) acc = ge_dbl(acc);
-    acc = ge_add(acc, ge_from_dev(ws_words + (size_t)j * P3_WORDS));
+  ge acc = ge_identity();
+  bool started = false;
+  uint32_t pos = 0;  // bit position acc is currently scaled to
+  for (int j = (int)Wn - 1; j >= 0; --j) {
+    for (int k = (int)nterms - 1; k >= 0; --k) {
+      const uint32_t off = c * (uint32_t)j + (k ? RWAVE_SHIFT + (uint32_t)(k - 1) : 0u);
+      const ge v = ge_from_dev(ws_words + ((size_t)j * nterms + (size_t)k) * P3_WORDS);
+      if (started)
+        for (; pos > off; --pos) acc = ge_dbl(acc);
+      acc = started ? ge_add(acc, v) : v;
+      started = true;
+      pos = off;
+    }
   }
-  for (uint32_t k = 0; k < c * wb; ++k) acc = ge_dbl(acc);
+  for (uint32_t k = 0; k < pos + c * wb; ++k) acc = ge_dbl(acc);
   return acc;
 }
 
@@ -259,9 +296,14 @@ int msm_single_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx,
   const uint32_t G = msm_window_groups(n, c, Wn, d_pidx != nullptr);
   if (G <= 1) {
     uint32_t* d_ws = nullptr;
-    BPP_TRY(msm_engine(ctx, d_scal, d_pidx, nullptr, 1, (uint32_t)n, c, wb, Wn, d_tbl, &d_ws));
-    BPP_HIP(hipMemcpyAsync(h, d_ws, (size_t)Wn * P3_BYTES, hipMemcpyDeviceToHost, ctx->stream));
+    uint32_t nterms = 1;
+    BPP_TRY(msm_engine(ctx, d_scal, d_pidx, nullptr, 1, (uint32_t)n, c, wb, Wn, d_tbl, &d_ws, nullptr, 0xffffffffu,
+                       false, &nterms));
+    if (nterms > 1) BPP_TRY(ctx_pinned(ctx, (size_t)Wn * nterms * P3_BYTES, &h));
+    BPP_HIP(hipMemcpyAsync(h, d_ws, (size_t)Wn * nterms * P3_BYTES, hipMemcpyDeviceToHost, ctx->stream));
     BPP_HIP(hipStreamSynchronize(ctx->stream));
+    *out = horner_host_terms((const uint32_t*)h, Wn, nterms, c, wb);
+    return BPP_OK;
   } else {
     // Window groups on two child streams: the sort of group g+1 (HBM-bound)
     // and the bucket reduction of group g-1 (latency-bound, few waves) run
@@ -653,13 +695,16 @@ int msm_multi(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, cons
   const uint32_t c = msm_choose_c((double)T / (double)M);
   const uint32_t W = (254 + c - 1) / c;
   uint32_t* d_ws = nullptr;
-  BPP_TRY(msm_engine(ctx, d_scal, d_pidx, (const uint32_t*)d_off, M, T, c, 0, W, d_tbl, &d_ws, d_tbl1, n0));
+  uint32_t nterms = 1;
+  BPP_TRY(msm_engine(ctx, d_scal, d_pidx, (const uint32_t*)d_off, M, T, c, 0, W, d_tbl, &d_ws, d_tbl1, n0, false,
+                     M == 1 ? &nterms : nullptr));
   if (M <= 8) {
     void* h = nullptr;
-    BPP_TRY(ctx_pinned(ctx, (size_t)M * W * P3_BYTES, &h));
-    BPP_HIP(hipMemcpyAsync(h, d_ws, (size_t)M * W * P3_BYTES, hipMemcpyDeviceToHost, ctx->stream));
+    BPP_TRY(ctx_pinned(ctx, (size_t)M * W * nterms * P3_BYTES, &h));
+    BPP_HIP(hipMemcpyAsync(h, d_ws, (size_t)M * W * nterms * P3_BYTES, hipMemcpyDeviceToHost, ctx->stream));
     BPP_HIP(hipStreamSynchronize(ctx->stream));
-    for (uint32_t m = 0; m < M; ++m) out[m] = horner_host((const uint32_t*)h + (size_t)m * W * P3_WORDS, W, c, 0);
+    for (uint32_t m = 0; m < M; ++m)
+      out[m] = horner_host_terms((const uint32_t*)h + (size_t)m * W * nterms * P3_WORDS, W, nterms, c, 0);
     return BPP_OK;
   }
   MsmGeom g;

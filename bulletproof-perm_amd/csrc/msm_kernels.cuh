@@ -270,6 +270,27 @@ FE_INLINE ge_p3 bucket_total(size_t b, uint32_t bs, uint32_t be, uint32_t ks, co
 //     run = sum B_b, plus lo*run by double-and-add; LDS tree over the wave.
 //   k_msm_reduce_final: one 64-lane block per segment sums its BPS partials.
 #define RED_T 64
+FE_INLINE ge_p3 ge_shfl_xor(const ge_p3& a, int m) {
+  ge_p3 o;
+  _Pragma("unroll") for (int k = 0; k < FE_LIMBS; ++k) {
+    o.X.v[k] = __shfl_xor(a.X.v[k], m, 64);
+    o.Y.v[k] = __shfl_xor(a.Y.v[k], m, 64);
+    o.Z.v[k] = __shfl_xor(a.Z.v[k], m, 64);
+    o.T.v[k] = __shfl_xor(a.T.v[k], m, 64);
+  }
+  return o;
+}
+// value of lane (self + d) of the wave (d < 64; lanes past the end read their own)
+FE_INLINE ge_p3 ge_shfl_down(const ge_p3& a, int d) {
+  ge_p3 o;
+  _Pragma("unroll") for (int k = 0; k < FE_LIMBS; ++k) {
+    o.X.v[k] = __shfl_down(a.X.v[k], d, 64);
+    o.Y.v[k] = __shfl_down(a.Y.v[k], d, 64);
+    o.Z.v[k] = __shfl_down(a.Z.v[k], d, 64);
+    o.T.v[k] = __shfl_down(a.T.v[k], d, 64);
+  }
+  return o;
+}
 #define RED_LMAX 8
 FE_INLINE ge_p3 lds_tree_sum(uint32_t* lds, ge_p3 v) {
   store_p3(lds, threadIdx.x, v);
@@ -324,6 +345,66 @@ __global__ void __launch_bounds__(RED_T) k_msm_reduce_final(const uint32_t* __re
   for (uint32_t j = threadIdx.x; j < BPS; j += RED_T) acc = ge_add(acc, load_p3(part, (size_t)seg * BPS + j));
   const ge_p3 tot = lds_tree_sum(lds, acc);
   if (threadIdx.x == 0) store_p3(wsum, seg, tot);
+}
+
+// Bucket reduction for one large MSM (B >= 512 buckets per window) whose
+// power-of-two weights are left to the host Horner, which doubles between
+// windows anyway.  With b = 512 w + 8 t + i (wave w, lane t, i < 8):
+//   sum_b (b+1) S_b = sum_{w,t} acc_{w,t}            acc = sum_i (i+1) S_b
+//                   + 8 sum_w sum_{t>=1} suf_{w,t}    suf = suffix sum of the lanes' run = sum_i S_b
+//                   + 512 sum_w w R_w                 R_w = suf_{w,0}
+// k_msm_reduce_wave: one 64-lane wave per (segment, w): 16 running-sum
+//   additions per lane, a 6-step suffix scan, v = acc + 8 suf (t >= 1), a
+//   6-step butterfly; writes V_w = sum_t v and R_w.  Every lane does the
+//   same 30 point operations (the old per-lane lo * run double-and-add took
+//   ~21 of its 48).
+// k_msm_reduce_bits: one wave per (segment, term): term 0 is X = sum_w V_w,
+//   term 1 + j is Y_j = sum_{w : bit j of w} R_w, so that
+//   sum_b (b+1) S_b = X + sum_j 2^(9+j) Y_j (horner_host_terms).
+#define RWAVE_L 8
+#define RWAVE_SHIFT 9  // log2(RWAVE_L * 64)
+__global__ void __launch_bounds__(64) k_msm_reduce_wave(const uint32_t* __restrict__ boff, uint32_t ks,
+                                                       const uint32_t* __restrict__ head,
+                                                       const uint32_t* __restrict__ tail,
+                                                       const uint32_t* __restrict__ bsum, MsmGeom g,
+                                                       uint32_t* __restrict__ part) {
+  const uint32_t nw = g.B >> RWAVE_SHIFT;
+  const uint32_t seg = blockIdx.x / nw, w = blockIdx.x % nw;
+  const uint32_t t = threadIdx.x;
+  const uint32_t lo = (w * 64 + t) * RWAVE_L;
+  const size_t base = (size_t)seg * g.B + lo;
+  uint32_t bo[RWAVE_L + 1];
+  _Pragma("unroll") for (uint32_t k = 0; k <= RWAVE_L; ++k) bo[k] = boff[base + k];
+  ge_p3 run = ge_identity();
+  ge_p3 acc = ge_identity();
+  for (int i = RWAVE_L - 1; i >= 0; --i) {
+    if (bo[i] != bo[i + 1]) run = ge_add(run, bucket_total(base + i, bo[i], bo[i + 1], ks, head, tail, bsum));
+    acc = ge_add(acc, run);
+  }
+  ge_p3 suf = run;  // inclusive suffix sum over lanes t..63
+  _Pragma("unroll") for (int d = 1; d < 64; d <<= 1) {
+    const ge_p3 s2 = ge_add(suf, ge_shfl_down(suf, d));
+    if (t + d < 64) suf = s2;
+  }
+  ge_p3 v = ge_add(acc, ge_dbl(ge_dbl(ge_dbl(suf))));
+  if (t == 0) v = acc;
+  _Pragma("unroll") for (int k = 1; k < 64; k <<= 1) v = ge_add(v, ge_shfl_xor(v, k));
+  if (t == 0) {
+    store_p3(part, 2 * (size_t)blockIdx.x, v);
+    store_p3(part, 2 * (size_t)blockIdx.x + 1, suf);  // lane 0: R_w
+  }
+}
+
+// terms per segment = 1 + log2(nw)
+__global__ void __launch_bounds__(64) k_msm_reduce_bits(const uint32_t* __restrict__ part, MsmGeom g,
+                                                       uint32_t nterms, uint32_t* __restrict__ out) {
+  const uint32_t nw = g.B >> RWAVE_SHIFT;
+  const uint32_t seg = blockIdx.x / nterms, term = blockIdx.x % nterms;
+  const uint32_t w = threadIdx.x;
+  const bool take = w < nw && (term == 0 || ((w >> (term - 1)) & 1u));
+  ge_p3 v = take ? load_p3(part, 2 * ((size_t)seg * nw + w) + (term ? 1 : 0)) : ge_identity();
+  _Pragma("unroll") for (int k = 1; k < 64; k <<= 1) v = ge_add(v, ge_shfl_xor(v, k));
+  if (w == 0) store_p3(out, blockIdx.x, v);
 }
 
 // One lane per MSM: Horner over its W window sums.
@@ -640,16 +721,6 @@ struct DtGeom {
 };
 FE_INLINE uint32_t dt_half(const DtGeom& g) { return 1u << (g.c - 1); }
 
-FE_INLINE ge_p3 ge_shfl_xor(const ge_p3& a, int m) {
-  ge_p3 o;
-  _Pragma("unroll") for (int k = 0; k < FE_LIMBS; ++k) {
-    o.X.v[k] = __shfl_xor(a.X.v[k], m, 64);
-    o.Y.v[k] = __shfl_xor(a.Y.v[k], m, 64);
-    o.Z.v[k] = __shfl_xor(a.Z.v[k], m, 64);
-    o.T.v[k] = __shfl_xor(a.T.v[k], m, 64);
-  }
-  return o;
-}
 
 // Bits [pos, pos + c) of a 256-bit scalar held in registers, with the word
 // picked by selects (a runtime index into s[] would put it in scratch).

@@ -21,6 +21,8 @@ from typing import Iterable, Sequence
 from . import _lib
 from ._lib import BppError, check
 
+MSM_INFLIGHT = 4  # BPP_MSM_INFLIGHT (include/bpperm.h)
+
 __all__ = ["Context", "PointTable", "BppError", "vartime_multiscalar_mul", "default_context"]
 
 
@@ -176,6 +178,21 @@ class Context:
         out = C.create_string_buffer(128)
         check(self.lib.bpp_msm_table_dev_partial(self.h, C.c_void_p(d_scalars), table.handle, n, w_begin, w_end, out),
               "bpp_msm_table_dev_partial", self.h)
+        return out.raw
+
+    # Asynchronous single MSMs (at most two in flight): submit returns a
+    # ticket at once; collect waits for it and returns the compressed result
+    # (or the raw 128-byte partial of windows [w_begin, w_end)).
+    def msm_submit(self, d_scalars: int, table: PointTable, n: int, w_begin: int = 0, w_end: int = 0) -> int:
+        t = C.c_uint64()
+        check(self.lib.bpp_msm_submit(self.h, C.c_void_p(d_scalars), table.handle, n, w_begin, w_end, C.byref(t)),
+              "bpp_msm_submit", self.h)
+        return t.value
+
+    def msm_collect(self, ticket: int, partial: bool = False) -> bytes:
+        out = C.create_string_buffer(128 if partial else 32)
+        args = (None, out) if partial else (out, None)
+        check(self.lib.bpp_msm_collect(self.h, ticket, *args), "bpp_msm_collect", self.h)
         return out.raw
 
     def msm_batch(self, offsets: Sequence[int], scalars, point_idx: Sequence[int], table: PointTable) -> list[bytes]:

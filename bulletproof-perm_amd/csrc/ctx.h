@@ -36,6 +36,22 @@ struct bpp_ctx {
   // child contexts (own stream + workspaces) for sub-batches in flight
   // concurrently with this one
   std::vector<bpp_ctx*> children;
+  // bpp_msm_submit / bpp_msm_collect: up to BPP_MSM_INFLIGHT single MSMs in
+  // flight, slot s running on child context s
+  struct MsmSlot {
+    bool busy = false;
+    uint64_t ticket = 0;
+    hipEvent_t done = nullptr;
+    uint32_t c = 0, wb = 0, Wn = 0, nterms = 1;
+    void* h = nullptr;  // window terms (child's pinned buffer)
+  };
+  MsmSlot msm_slot[BPP_MSM_INFLIGHT];
+  uint64_t msm_next_ticket = 1;
+  hipEvent_t msm_acc_ev[BPP_MSM_INFLIGHT] = {};  // slot s's accumulation done
+  hipEvent_t msm_last_acc = nullptr;              // that of the last submitted MSM
+  // msm_engine hooks (set by bpp_msm_submit on a child): wait for acc_wait
+  // before the bucket accumulation, record acc_done after it
+  hipEvent_t acc_wait = nullptr, acc_done = nullptr;
 };
 
 struct bpp_points {

@@ -177,6 +177,10 @@ void bpp_ctx_destroy(bpp_ctx* ctx) {
     hipEventDestroy(p.b);
   }
   for (auto e : ctx->ev_pool) hipEventDestroy(e);
+  for (auto& sl : ctx->msm_slot)
+    if (sl.done) hipEventDestroy(sl.done);
+  for (auto e : ctx->msm_acc_ev)
+    if (e) hipEventDestroy(e);
   hipStreamDestroy(ctx->stream);
   delete ctx;
 }

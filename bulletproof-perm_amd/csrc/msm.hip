@@ -191,6 +191,7 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
     BPP_TRY(ctx_ws(ctx, "msm_tail", lanes * P3_BYTES, &tail));
     BPP_TRY(ctx_ws(ctx, "msm_heavy", (max_heavy + 1) * 4, &heavy));
     BPP_HIP(hipMemsetAsync(heavy, 0, 4, ctx->stream));
+    if (ctx->acc_wait) BPP_HIP(hipStreamWaitEvent(ctx->stream, ctx->acc_wait, 0));
     {
       ProfScope ps(ctx, "msm_accumulate");
       hipLaunchKernelGGL(k_msm_accumulate, dim3(grid_for(lanes, ACC_T)), dim3(ACC_T), 0, ctx->stream, d_tbl, d_tbl1,
@@ -205,6 +206,7 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
                          (const uint32_t*)heavy, (uint32_t*)bsum);
     }
     BPP_TRY(ctx_check_launch(ctx, "k_msm_fixup_heavy"));
+    if (ctx->acc_done) BPP_HIP(hipEventRecord(ctx->acc_done, ctx->stream));
     if (terms_out && M == 1 && !fb && g.B >= (1u << RWAVE_SHIFT) && g.B <= (64u << RWAVE_SHIFT) &&
         !getenv("BPP_MSM_OLD_REDUCE")) {
       // power-of-two weights left to the host Horner (k_msm_reduce_wave)
@@ -392,6 +394,95 @@ int bpp_msm_table_dev_partial(bpp_ctx* ctx, const void* d_scalars, const bpp_poi
   h25519::ge r;
   BPP_TRY(msm_single_dev(ctx, (const uint32_t*)d_scalars, nullptr, tbl->d, n, c, w_begin, w_end - w_begin, &r));
   h25519::ge_to_words((uint32_t*)partial, r);
+  return BPP_OK;
+}
+
+int bpp_msm_submit(bpp_ctx* ctx, const void* d_scalars, const bpp_points* tbl, size_t n, uint32_t w_begin,
+                   uint32_t w_end, uint64_t* ticket) {
+  if (!ctx || !tbl || !ticket || (!d_scalars && n)) return BPP_ERR_ARG;
+  if (n > tbl->n || n >= 0x80000000ull) return BPP_ERR_LEN;
+  const uint32_t c = msm_choose_c((double)(n ? n : 1));
+  const uint32_t W = (254 + c - 1) / c;
+  if (w_end == 0) w_end = W;
+  if (w_begin > w_end || w_end > W) return BPP_ERR_ARG;
+  const uint64_t t = ctx->msm_next_ticket;
+  // lowest free slot: k MSMs kept in flight reuse the same k child contexts
+  // (and their warm workspaces)
+  size_t s = BPP_MSM_INFLIGHT;
+  for (size_t i = BPP_MSM_INFLIGHT; i-- > 0;)
+    if (!ctx->msm_slot[i].busy) s = i;
+  if (s == BPP_MSM_INFLIGHT) {
+    ctx->err = "bpp_msm_submit: " + std::to_string(BPP_MSM_INFLIGHT) + " MSMs already in flight (collect one first)";
+    return BPP_ERR_ARG;
+  }
+  bpp_ctx::MsmSlot& sl = ctx->msm_slot[s];
+  BPP_HIP(hipSetDevice(ctx->device));
+  bpp_ctx* ch = nullptr;
+  BPP_TRY(ctx_child(ctx, s, &ch));
+  ch->prof = ctx->prof;
+  if (!sl.done) BPP_HIP(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+  // inputs written on ctx's stream before this call are visible to the child
+  BPP_HIP(hipEventRecord(sl.done, ctx->stream));
+  BPP_HIP(hipStreamWaitEvent(ch->stream, sl.done, 0));
+  sl.c = c;
+  sl.wb = w_begin;
+  sl.Wn = w_end - w_begin;
+  sl.nterms = 1;
+  if (n && sl.Wn) {
+    // accumulations run one after another (each fills every SIMD's VGPRs):
+    // this MSM's sort overlaps the previous one's accumulation, and its
+    // accumulation the previous one's bucket reduction and host combine
+    // (opt-in BPP_MSM_STAGGER=1; measured slower than letting in-flight MSMs
+    // share the device freely: 1.17 vs 1.04 ms per 2^20 MSM)
+    const bool stagger = getenv("BPP_MSM_STAGGER") != nullptr;
+    if (stagger) {
+      if (!ctx->msm_acc_ev[s]) BPP_HIP(hipEventCreateWithFlags(&ctx->msm_acc_ev[s], hipEventDisableTiming));
+      ch->acc_wait = ctx->msm_last_acc;
+      ch->acc_done = ctx->msm_acc_ev[s];
+    }
+    uint32_t* d_ws = nullptr;
+    const int rc = msm_engine(ch, (const uint32_t*)d_scalars, nullptr, nullptr, 1, (uint32_t)n, c, w_begin, sl.Wn,
+                              tbl->d, &d_ws, nullptr, 0xffffffffu, false, &sl.nterms);
+    ch->acc_wait = ch->acc_done = nullptr;
+    if (stagger) ctx->msm_last_acc = rc == BPP_OK ? ctx->msm_acc_ev[s] : nullptr;
+    if (rc) {
+      ctx->err = ch->err;
+      return rc;
+    }
+    const size_t bytes = (size_t)sl.Wn * sl.nterms * P3_BYTES;
+    int prc = ctx_pinned(ch, bytes, &sl.h);
+    if (prc) {
+      ctx->err = ch->err;
+      return prc;
+    }
+    BPP_HIP(hipMemcpyAsync(sl.h, d_ws, bytes, hipMemcpyDeviceToHost, ch->stream));
+  }
+  BPP_HIP(hipEventRecord(sl.done, ch->stream));
+  sl.busy = true;
+  sl.ticket = t;
+  *ticket = t;
+  ++ctx->msm_next_ticket;
+  return BPP_OK;
+}
+
+int bpp_msm_collect(bpp_ctx* ctx, uint64_t ticket, uint8_t out[32], uint8_t partial[128]) {
+  if (!ctx) return BPP_ERR_ARG;
+  size_t s = BPP_MSM_INFLIGHT;
+  for (size_t i = 0; i < BPP_MSM_INFLIGHT; ++i)
+    if (ctx->msm_slot[i].busy && ctx->msm_slot[i].ticket == ticket) s = i;
+  if (s == BPP_MSM_INFLIGHT) {
+    ctx->err = "bpp_msm_collect: unknown or already collected ticket";
+    return BPP_ERR_ARG;
+  }
+  bpp_ctx::MsmSlot& sl = ctx->msm_slot[s];
+  sl.busy = false;
+  BPP_HIP(hipSetDevice(ctx->device));
+  BPP_HIP(hipEventSynchronize(sl.done));
+  h25519::ge r = h25519::ge_identity();
+  if (sl.h && sl.Wn) r = horner_host_terms((const uint32_t*)sl.h, sl.Wn, sl.nterms, sl.c, sl.wb);
+  sl.h = nullptr;
+  if (out) h25519::encode(out, r);
+  if (partial) h25519::ge_to_words((uint32_t*)partial, r);
   return BPP_OK;
 }
 

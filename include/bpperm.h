@@ -108,6 +108,22 @@ int bpp_msm_table_dev(bpp_ctx* ctx, const void* d_scalars, const bpp_points* tbl
 int bpp_msm_windows(size_t n, uint32_t* c, uint32_t* windows);
 int bpp_msm_table_dev_partial(bpp_ctx* ctx, const void* d_scalars, const bpp_points* tbl, size_t n,
                               uint32_t w_begin, uint32_t w_end, uint8_t partial[128]);
+/* Asynchronous single MSMs over a resident table, for a stream of
+ * independent MSMs (e.g. successive batch verifications): submit enqueues
+ * the whole device pipeline of one MSM (windows [w_begin, w_end); w_end = 0
+ * means all windows) on its own stream and returns at once; collect waits
+ * for that MSM, runs its host window combine and returns the compressed
+ * result (`out`, full MSMs) and/or the raw 128-byte partial (`partial`, as
+ * bpp_msm_table_dev_partial).  At most BPP_MSM_INFLIGHT MSMs may be
+ * outstanding (submit fails with BPP_ERR_ARG otherwise), so the device runs
+ * MSM i+1's digit sort beside MSM i's latency-bound bucket reduction while
+ * the host combines MSM i-1's windows (two in flight measured best).  d_scalars must stay valid until
+ * collect; each outstanding MSM needs its own scalar buffer contents.
+ * Same-result guarantee: collect(submit(s)) == bpp_msm_table_dev(s). */
+#define BPP_MSM_INFLIGHT 4
+int bpp_msm_submit(bpp_ctx* ctx, const void* d_scalars, const bpp_points* tbl, size_t n, uint32_t w_begin,
+                   uint32_t w_end, uint64_t* ticket);
+int bpp_msm_collect(bpp_ctx* ctx, uint64_t ticket, uint8_t out[32], uint8_t partial[128]);
 /* Sum raw extended partial points (count x 128 bytes) and compress. */
 int bpp_partials_finish(const uint8_t* partials, size_t count, uint8_t out[32]);
 /* Host batch encoding of doubled points: out[i] = compress(2 * P_i) for raw

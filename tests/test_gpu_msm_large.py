@@ -10,6 +10,7 @@ import hashlib
 
 import pytest
 
+from bpperm._lib import BppError
 from oracle import cport, ristretto as r255
 
 pytestmark = pytest.mark.gpu
@@ -73,3 +74,44 @@ def test_msm_all_equal_scalars(ctx, big_table, n):
     got = ctx.msm_table(_sb([k] * n), tbl, n)
     ones = ctx.msm_table(_sb([1] * n), tbl, n)
     assert got == r255.encode(r255.ed_mul(k, r255.decode(ones)))
+
+
+def test_msm_async_submit_collect(ctx, big_table):
+    """bpp_msm_submit / bpp_msm_collect: two MSMs in flight give the same
+    results as one at a time (collected out of order), window partials
+    through the async path sum to the full MSM, one more than BPP_MSM_INFLIGHT outstanding submits
+    is refused, and an unknown ticket is refused."""
+    import bpperm
+    from bpperm import dist as bdist
+    raw, tbl = big_table
+    n = 1 << 17
+    sa, sb_ = _sb(_scalars(n, 31)), _sb(_scalars(n, 32))
+    da, db = ctx.dev_alloc(32 * n), ctx.dev_alloc(32 * n)
+    ctx.htod(da, sa)
+    ctx.htod(db, sb_)
+    want_a, want_b = ctx.msm_table_dev(da, tbl, n), ctx.msm_table_dev(db, tbl, n)
+    assert want_a == cport.msm(sa, cport.from_uniform(raw[: 64 * n]))
+    ta = ctx.msm_submit(da, tbl, n)
+    tb = ctx.msm_submit(db, tbl, n)
+    extra = [ctx.msm_submit(da, tbl, n) for _ in range(bpperm.MSM_INFLIGHT - 2)]
+    with pytest.raises(BppError):
+        ctx.msm_submit(da, tbl, n)
+    assert ctx.msm_collect(tb) == want_b
+    assert ctx.msm_collect(ta) == want_a
+    assert all(ctx.msm_collect(t) == want_a for t in extra)
+    with pytest.raises(BppError):
+        ctx.msm_collect(ta)
+    c, W = bpperm.msm_windows(n)
+    parts = []
+    for a, b in bdist.window_ranges(W, 3):
+        parts.append(ctx.msm_collect(ctx.msm_submit(da, tbl, n, a, b), partial=True))
+    assert bpperm.partials_finish(parts) == want_a
+    # a long stream, two in flight, alternating inputs
+    got, tick = [], ctx.msm_submit(da, tbl, n)
+    for i in range(6):
+        nxt = ctx.msm_submit(db if i % 2 == 0 else da, tbl, n) if i < 5 else None
+        got.append(ctx.msm_collect(tick))
+        tick = nxt
+    assert got == [want_a, want_b] * 3
+    ctx.dev_free(da)
+    ctx.dev_free(db)

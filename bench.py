@@ -99,13 +99,26 @@ def bench_proofs(ctx, args, world, rank, torch, dist, cdev="cuda"):
     """Config 4: batches of 52-card permutation proofs, sharded one batch per
     GPU (independent proofs: no collective on the data path), proved in
     lockstep on each GPU; then the same proofs batch-verified (one MSM per
-    GPU's batch).  Returns whole-job proofs/s (max time over ranks)."""
+    batch).  Throughput: `--proof-streams` batches in flight per GPU, each
+    driven by its own host thread and context (own HIP stream; ctypes drops
+    the GIL), so one batch's host phases (transcripts, challenges) run while
+    another's kernels occupy the GPU.  Returns whole-job proofs/s (max time
+    over ranks) and the one-batch-at-a-time latency."""
+    import threading
+
     import bpperm
     B = args.proofs_per_gpu
-    gens = bpperm.Gens(ctx, 128)
-    pr = bpperm.PermProver(gens, 52)
-    seeds = lambda step: [((step * world + rank) * B + i) for i in range(B)]  # noqa: E731
-    pr.prove_batch(seeds(10_000))  # warmup (window tables, workspaces)
+    S = max(1, args.proof_streams)
+    ctxs = [ctx] + [bpperm.Context(ctx.device) for _ in range(S - 1)]
+    gens = [bpperm.Gens(c, 128) for c in ctxs]
+    provers = [bpperm.PermProver(g, 52) for g in gens]
+
+    def seeds(step, s):
+        return [(((step * S + s) * world + rank) * B + i) for i in range(B)]
+
+    for s, pr in enumerate(provers):  # warmup (window tables, workspaces)
+        pr.prove_batch(seeds(10_000, s))
+        pr.prove_batch(seeds(10_001, s))
 
     def timed(fn):
         if world > 1:
@@ -123,28 +136,51 @@ def bench_proofs(ctx, args, world, rank, torch, dist, cdev="cuda"):
             el = tt.item()
         return out, el
 
-    batches = []
+    def in_flight(fn):
+        res = [None] * S
+        errs = []
 
-    def prove_all():
-        for st in range(args.proof_steps):
-            batches.append(pr.prove_batch(seeds(st)))
+        def run(s):
+            try:
+                res[s] = fn(s)
+            except Exception as e:  # surfaced after the join
+                errs.append(e)
 
-    _, el_p = timed(prove_all)
+        th = [threading.Thread(target=run, args=(s,)) for s in range(S)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if errs:
+            raise errs[0]
+        return res
 
-    def verify_all():
+    # one batch at a time on one stream (latency)
+    _, el_one = timed(lambda: [provers[0].prove_batch(seeds(20_000 + st, 0)) for st in range(args.proof_steps)])
+    # S batches in flight (throughput)
+    batches, el_p = timed(lambda: in_flight(
+        lambda s: [provers[s].prove_batch(seeds(st, s)) for st in range(args.proof_steps)]))
+
+    def verify_stream(s):
         ok = True
-        for proofs, Vs in batches:
-            ok &= pr.verify_batch(proofs, Vs)
+        for proofs, Vs in batches[s]:
+            ok &= provers[s].verify_batch(proofs, Vs)
         return ok
 
-    ok, el_v = timed(verify_all)
-    total = B * world * args.proof_steps
-    gens.close()
+    oks, el_v = timed(lambda: in_flight(verify_stream))
+    total = B * S * world * args.proof_steps
+    for g in gens:
+        g.close()
+    for c in ctxs[1:]:
+        c.close()
     return {"metric": "52-card permutation proofs/sec (prove)", "value": total / el_p, "unit": "proofs/s",
-            "ms_per_batch": el_p / args.proof_steps * 1e3, "proofs_per_gpu_per_batch": B, "batches": args.proof_steps,
-            "verify_batch_proofs_per_sec": total / el_v, "verify_ms_per_batch": el_v / args.proof_steps * 1e3,
-            "all_verified": bool(ok), "n_gpus": world, "scaling": "weak",
-            "config": "config 4: 52-card sound-mode permutation proofs, one lockstep batch per GPU per step"}
+            "ms_per_batch": el_p / (args.proof_steps * S) * 1e3, "proofs_per_gpu_per_batch": B,
+            "batches_in_flight_per_gpu": S, "batches": args.proof_steps * S,
+            "latency_ms_per_batch": el_one / args.proof_steps * 1e3,
+            "verify_batch_proofs_per_sec": total / el_v, "verify_ms_per_batch": el_v / (args.proof_steps * S) * 1e3,
+            "all_verified": bool(all(oks)), "n_gpus": world, "scaling": "weak",
+            "config": f"config 4: 52-card sound-mode permutation proofs, lockstep batches of {B} per GPU, "
+                      f"{S} batches in flight per GPU (one host thread + context each)"}
 
 
 def main():
@@ -158,7 +194,8 @@ def main():
     ap.add_argument("--verify", action="store_true", help="also recompute via a second window split")
     ap.add_argument("--proofs-per-gpu", type=int, default=128,
                     help="52-card proofs per GPU per batch (config 4: 1024 over 8 GPUs); 0 = skip")
-    ap.add_argument("--proof-steps", type=int, default=3)
+    ap.add_argument("--proof-steps", type=int, default=6, help="batches per stream")
+    ap.add_argument("--proof-streams", type=int, default=3, help="proof batches in flight per GPU")
     ap.add_argument("--inflight", type=int, default=2, help="independent MSMs in flight (1..4)")
     ap.add_argument("--msm-split", choices=["windows", "points"], default="windows",
                     help="N>1: split the MSM's bucket windows (default) or its points over the ranks")

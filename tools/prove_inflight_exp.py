@@ -1,0 +1,44 @@
+"""Aggregate 52-card proofs/s with T host threads, each driving its own
+context (own stream) over batches of B proofs: do batches in flight overlap
+one batch's host phases with another's GPU phases?"""
+import sys
+import threading
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "bulletproof-perm_amd"))
+import os  # noqa: E402
+
+if os.environ.get("WITH_TORCH"):
+    import torch
+import bpperm  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 128
+T = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+reps = int(sys.argv[3]) if len(sys.argv) > 3 else 6
+provers = []
+for t in range(T):
+    ctx = bpperm.Context(0)
+    g = bpperm.Gens(ctx, 128)
+    pr = bpperm.PermProver(g, 52)
+    pr.prove_batch(list(range(B)))
+    pr.prove_batch(list(range(B)))
+    provers.append(pr)
+
+
+def work(t):
+    for r in range(reps):
+        provers[t].prove_batch(list(range(B * (r + 10 * t), B * (r + 10 * t + 1))))
+
+
+if os.environ.get("WITH_TORCH"):
+    torch.cuda.synchronize()
+th = [threading.Thread(target=work, args=(t,)) for t in range(T)]
+t0 = time.perf_counter()
+for x in th:
+    x.start()
+for x in th:
+    x.join()
+el = time.perf_counter() - t0
+print(f"B={B} T={T}: {T * reps * B / el:.0f} proofs/s ({el / (T * reps) * 1e3:.3f} ms per batch)")

@@ -37,6 +37,7 @@ def main():
     stage_of = {"k_msm_accumulate": "msm_accumulate", "k_rsort_scatter": "msm_scatter_coarse",
                 "k_rsort_fine": "msm_scatter_fine", "k_rsort_count": "msm_count", "k_msm_digits": "msm_digits",
                 "k_msm_reduce_partial": "msm_reduce", "k_msm_reduce_final": "msm_reduce_final",
+                "k_msm_reduce_wave": "msm_reduce_wave", "k_msm_reduce_bits": "msm_reduce_bits",
                 "k_msm_fixup_heavy": "msm_fixup", "k_msm_fixup": "msm_fixup", "k_msm_scatter_lds": "msm_scatter_lds", "k_msm_count_lds": "msm_count_lds"}
     for k, st in stage_of.items():
         if k not in fetch or k not in write:

@@ -1,0 +1,167 @@
+// Eight Keccak-f[1600] states at once in AVX-512 registers (lane i of
+// instance j = 64-bit element j of zmm i), and the prover's eight SHAKE256
+// random streams built on it.  The EPYC hosts of the GPU boxes (Zen 5) run
+// 512-bit vprolq / vpternlogq at full width: eight permutations cost about
+// two scalar ones.  Callers check keccak_x8_available() (runtime CPUID) and
+// fall back to the scalar keccak_f1600 otherwise; both give identical bytes.
+#include <immintrin.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "perm.h"
+
+namespace merlin {
+
+static const uint64_t RCX[24] = {
+    0x0000000000000001ULL, 0x0000000000008082ULL, 0x800000000000808AULL, 0x8000000080008000ULL,
+    0x000000000000808BULL, 0x0000000080000001ULL, 0x8000000080008081ULL, 0x8000000000008009ULL,
+    0x000000000000008AULL, 0x0000000000000088ULL, 0x0000000080008009ULL, 0x000000008000000AULL,
+    0x000000008000808BULL, 0x800000000000008BULL, 0x8000000000008089ULL, 0x8000000000008003ULL,
+    0x8000000000008002ULL, 0x8000000000000080ULL, 0x000000000000800AULL, 0x800000008000000AULL,
+    0x8000000080008081ULL, 0x8000000000008080ULL, 0x0000000080000001ULL, 0x8000000080008008ULL,
+};
+
+bool keccak_x8_available() {
+  static const bool ok = __builtin_cpu_supports("avx512f");
+  return ok;
+}
+
+#define X8_TARGET __attribute__((target("avx512f")))
+
+// rho offsets and pi destinations: B[pi(i)] = rol(A[i] ^ D[i % 5], RHO[i])
+X8_TARGET static inline void keccak_x8_rounds(__m512i a[25]) {
+  for (int round = 0; round < 24; ++round) {
+    __m512i c[5], d[5];
+#pragma GCC unroll 5
+    for (int x = 0; x < 5; ++x)
+      c[x] = _mm512_ternarylogic_epi64(_mm512_ternarylogic_epi64(a[x], a[x + 5], a[x + 10], 0x96), a[x + 15],
+                                       a[x + 20], 0x96);
+#pragma GCC unroll 5
+    for (int x = 0; x < 5; ++x) d[x] = _mm512_xor_si512(c[(x + 4) % 5], _mm512_rol_epi64(c[(x + 1) % 5], 1));
+    __m512i b[25];
+    b[0] = _mm512_xor_si512(a[0], d[0]);
+    b[1] = _mm512_rol_epi64(_mm512_xor_si512(a[6], d[1]), 44);
+    b[2] = _mm512_rol_epi64(_mm512_xor_si512(a[12], d[2]), 43);
+    b[3] = _mm512_rol_epi64(_mm512_xor_si512(a[18], d[3]), 21);
+    b[4] = _mm512_rol_epi64(_mm512_xor_si512(a[24], d[4]), 14);
+    b[5] = _mm512_rol_epi64(_mm512_xor_si512(a[3], d[3]), 28);
+    b[6] = _mm512_rol_epi64(_mm512_xor_si512(a[9], d[4]), 20);
+    b[7] = _mm512_rol_epi64(_mm512_xor_si512(a[10], d[0]), 3);
+    b[8] = _mm512_rol_epi64(_mm512_xor_si512(a[16], d[1]), 45);
+    b[9] = _mm512_rol_epi64(_mm512_xor_si512(a[22], d[2]), 61);
+    b[10] = _mm512_rol_epi64(_mm512_xor_si512(a[1], d[1]), 1);
+    b[11] = _mm512_rol_epi64(_mm512_xor_si512(a[7], d[2]), 6);
+    b[12] = _mm512_rol_epi64(_mm512_xor_si512(a[13], d[3]), 25);
+    b[13] = _mm512_rol_epi64(_mm512_xor_si512(a[19], d[4]), 8);
+    b[14] = _mm512_rol_epi64(_mm512_xor_si512(a[20], d[0]), 18);
+    b[15] = _mm512_rol_epi64(_mm512_xor_si512(a[4], d[4]), 27);
+    b[16] = _mm512_rol_epi64(_mm512_xor_si512(a[5], d[0]), 36);
+    b[17] = _mm512_rol_epi64(_mm512_xor_si512(a[11], d[1]), 10);
+    b[18] = _mm512_rol_epi64(_mm512_xor_si512(a[17], d[2]), 15);
+    b[19] = _mm512_rol_epi64(_mm512_xor_si512(a[23], d[3]), 56);
+    b[20] = _mm512_rol_epi64(_mm512_xor_si512(a[2], d[2]), 62);
+    b[21] = _mm512_rol_epi64(_mm512_xor_si512(a[8], d[3]), 55);
+    b[22] = _mm512_rol_epi64(_mm512_xor_si512(a[14], d[4]), 39);
+    b[23] = _mm512_rol_epi64(_mm512_xor_si512(a[15], d[0]), 41);
+    b[24] = _mm512_rol_epi64(_mm512_xor_si512(a[21], d[1]), 2);
+    // chi: a = b0 ^ (~b1 & b2)  (ternary-logic table 0xD2)
+#pragma GCC unroll 5
+    for (int y = 0; y < 25; y += 5) {
+#pragma GCC unroll 5
+      for (int x = 0; x < 5; ++x)
+        a[y + x] = _mm512_ternarylogic_epi64(b[y + x], b[y + (x + 1) % 5], b[y + (x + 2) % 5], 0xD2);
+    }
+    a[0] = _mm512_xor_si512(a[0], _mm512_set1_epi64((long long)RCX[round]));
+  }
+}
+
+// 8 SHAKE256 streams of `len` bytes each (len a multiple of 136 not needed),
+// inputs of one common length < 136 bytes.
+X8_TARGET void shake256_x8(const uint8_t* const in[8], size_t inlen, uint8_t* const out[8], size_t len) {
+  alignas(64) uint64_t lanes[25][8];
+  memset(lanes, 0, sizeof lanes);
+  for (int j = 0; j < 8; ++j) {
+    uint8_t blk[136];
+    memset(blk, 0, sizeof blk);
+    memcpy(blk, in[j], inlen);
+    blk[inlen] ^= 0x1F;
+    blk[135] ^= 0x80;
+    for (int i = 0; i < 17; ++i) memcpy(&lanes[i][j], blk + 8 * i, 8);
+  }
+  __m512i a[25];
+  for (int i = 0; i < 25; ++i) a[i] = _mm512_load_si512((const void*)lanes[i]);
+  for (size_t pos = 0; pos < len; pos += 136) {
+    keccak_x8_rounds(a);
+    for (int i = 0; i < 17; ++i) _mm512_store_si512((void*)lanes[i], a[i]);
+    const size_t k = len - pos < 136 ? len - pos : 136;
+    for (int j = 0; j < 8; ++j) {
+      uint8_t blk[136];
+      for (int i = 0; i < 17; ++i) memcpy(blk + 8 * i, &lanes[i][j], 8);
+      memcpy(out[j] + pos, blk, k);
+    }
+  }
+}
+
+}  // namespace merlin
+
+namespace perm {
+
+// Same draws as draw_prover_randomness, from a byte buffer holding the
+// stream (the fixed draw order consumes a fixed number of bytes).
+static void parse_randomness(const Circuit& C, const uint8_t* s, std::vector<uint32_t>& pi,
+                             std::vector<hsc::Sc>& gamma, hsc::Sc& alpha, hsc::Sc& beta, hsc::Sc& rho,
+                             std::vector<hsc::Sc>& sL, std::vector<hsc::Sc>& sR, std::vector<hsc::Sc>& taus) {
+  pi.resize(C.k);
+  for (uint32_t i = 0; i < C.k; ++i) pi[i] = i;
+  for (uint32_t i = C.k - 1; i > 0; --i) {
+    uint64_t x;
+    memcpy(&x, s, 8);
+    s += 8;
+    const uint32_t j = (uint32_t)(x % (uint64_t)(i + 1));
+    std::swap(pi[i], pi[j]);
+  }
+  auto scalar = [&]() {
+    const hsc::Sc v = hsc::from_wide(s);
+    s += 64;
+    return v;
+  };
+  gamma.resize(C.m);
+  for (auto& g : gamma) g = scalar();
+  alpha = scalar();
+  beta = scalar();
+  rho = scalar();
+  sL.resize(C.n_p);
+  sR.resize(C.n_p);
+  taus.resize(5);
+  for (auto& x : sL) x = scalar();
+  for (auto& x : sR) x = scalar();
+  for (auto& x : taus) x = scalar();
+}
+
+size_t randomness_bytes(const Circuit& C) { return 8 * (size_t)(C.k - 1) + 64 * ((size_t)C.m + 3 + 2 * C.n_p + 5); }
+
+void draw_prover_randomness_x8(const Circuit& C, const uint64_t seeds[8], RandomDraws out[8]) {
+  const size_t len = randomness_bytes(C);
+  if (!merlin::keccak_x8_available()) {
+    for (int j = 0; j < 8; ++j)
+      draw_prover_randomness(C, seeds[j], out[j].pi, out[j].gamma, out[j].alpha, out[j].beta, out[j].rho, out[j].sL,
+                             out[j].sR, out[j].taus);
+    return;
+  }
+  std::vector<uint8_t> buf(8 * len);
+  uint8_t in[8][20];
+  const uint8_t* inp[8];
+  uint8_t* outp[8];
+  for (int j = 0; j < 8; ++j) {
+    memcpy(in[j], "bpperm-prove", 12);
+    memcpy(in[j] + 12, &seeds[j], 8);
+    inp[j] = in[j];
+    outp[j] = buf.data() + (size_t)j * len;
+  }
+  merlin::shake256_x8(inp, 20, outp, len);
+  for (int j = 0; j < 8; ++j)
+    parse_randomness(C, outp[j], out[j].pi, out[j].gamma, out[j].alpha, out[j].beta, out[j].rho, out[j].sL,
+                     out[j].sR, out[j].taus);
+}
+
+}  // namespace perm

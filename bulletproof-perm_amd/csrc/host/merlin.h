@@ -20,6 +20,9 @@ static inline uint64_t rol(uint64_t x, int n) { return n ? (x << n) | (x >> (64 
 
 // Keccak-f[1600] (host/keccak.cpp, compiled by the host C++ compiler)
 void keccak_f1600(uint64_t st[25]);
+// host/keccak_x8.cpp: eight states per AVX-512 permutation
+bool keccak_x8_available();
+void shake256_x8(const uint8_t* const in[8], size_t inlen, uint8_t* const out[8], size_t len);
 
 // SHAKE256 XOF (rate 136, domain 0x1F): bulletproofs' GeneratorsChain and
 // PedersenGens::default's SHA3-512 hash-to-point need it.

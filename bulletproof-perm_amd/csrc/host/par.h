@@ -2,8 +2,8 @@
 // scalars, witness polynomials).  A persistent pool (spawning threads per
 // call costs ~20 us each, more than a batch of transcript operations):
 // threads = BPP_HOST_THREADS or min(granted CPUs, 16); items are claimed
-// from an atomic counter; the calling thread works too.  Calls are
-// serialised; a call from inside a pool task runs inline.
+// from an atomic counter; the calling thread works too.  Concurrent calls
+// share the workers; a call from inside a pool task runs inline.
 #pragma once
 #include <algorithm>
 #include <atomic>
@@ -44,11 +44,14 @@ inline unsigned threads() {
   return n;
 }
 
-// Workers spin (with pause) for ~BPP_POOL_SPIN_US after each job before
-// sleeping on a condition variable, so the prover's stream of short host
-// phases (one every 0.1-0.3 ms) is not paid in futex wake-ups; the caller
-// waits only until every item is done and every worker that entered the
-// job has left it.
+// Workers spin (with pause) for ~BPP_POOL_SPIN_US after their last item
+// before sleeping on a condition variable, so the prover's stream of short
+// host phases (one every 0.1-0.3 ms) is not paid in futex wake-ups.  Several
+// callers (independent proof batches in flight, one driver thread each) may
+// run jobs at once: active jobs sit in a list and workers claim items from
+// any of them, so one batch's host phase does not queue behind another's.
+// A caller works on its own job, waits until every item is done, unlists
+// the job and waits for the workers still inside it to leave.
 class Pool {
  public:
   explicit Pool(unsigned workers) {
@@ -65,66 +68,80 @@ class Pool {
     for (auto& t : th_) t.join();
   }
   void run(size_t n, const std::function<void(size_t)>& f) {
-    std::lock_guard<std::mutex> call(call_mu_);
-    n_ = n;
-    next_.store(0);
-    done_.store(0);
-    job_.store(&f);
-    gen_.fetch_add(1);
-    if (sleepers_.load() > 0) {
-      { std::lock_guard<std::mutex> g(mu_); }
-      cv_.notify_all();
+    Job j;
+    j.f = &f;
+    j.n = n;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      jobs_.push_back(&j);
+      njobs_.fetch_add(1);
     }
-    work(f, n);
-    while (done_.load() < n) cpu_relax();
-    job_.store(nullptr);
-    while (inside_.load() != 0) cpu_relax();
+    if (sleepers_.load() > 0) cv_.notify_all();
+    work(j);
+    while (j.done.load() < n) cpu_relax();
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      jobs_.erase(std::find(jobs_.begin(), jobs_.end(), &j));
+      njobs_.fetch_sub(1);
+    }
+    while (j.inside.load() != 0) cpu_relax();
   }
   static bool in_worker() { return tl_worker(); }
 
  private:
+  struct Job {
+    const std::function<void(size_t)>* f = nullptr;
+    size_t n = 0;
+    std::atomic<size_t> next{0}, done{0};
+    std::atomic<unsigned> inside{0};
+  };
   static void cpu_relax() { __builtin_ia32_pause(); }
   static bool& tl_worker() {
     static thread_local bool w = false;
     return w;
   }
-  void work(const std::function<void(size_t)>& f, size_t n) {
+  static void work(Job& j) {
     size_t k = 0;
-    for (size_t i; (i = next_.fetch_add(1)) < n; ++k) f(i);
-    if (k) done_.fetch_add(k);
+    for (size_t i; (i = j.next.fetch_add(1)) < j.n; ++k) (*j.f)(i);
+    if (k) j.done.fetch_add(k);
+  }
+  // a listed job with unclaimed items, entered (inside + 1), or null
+  Job* claim() {
+    std::lock_guard<std::mutex> g(mu_);
+    for (Job* j : jobs_)
+      if (j->next.load() < j->n) {
+        j->inside.fetch_add(1);
+        return j;
+      }
+    return nullptr;
   }
   void loop() {
     tl_worker() = true;
-    uint64_t seen = gen_.load();
-    for (;;) {
-      // spin for a new generation, then sleep
-      auto t0 = std::chrono::steady_clock::now();
-      for (unsigned it = 0; gen_.load() == seen && !stop_.load(); ++it) {
-        cpu_relax();
-        if ((it & 255u) == 0 &&
-            std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us_)) {
-          std::unique_lock<std::mutex> g(mu_);
-          sleepers_.fetch_add(1);
-          cv_.wait(g, [&] { return stop_.load() || gen_.load() != seen; });
-          sleepers_.fetch_sub(1);
-          break;
+    auto t0 = std::chrono::steady_clock::now();
+    for (unsigned it = 0; !stop_.load(); ++it) {
+      if (njobs_.load() > 0) {
+        if (Job* j = claim()) {
+          work(*j);
+          j->inside.fetch_sub(1);
+          t0 = std::chrono::steady_clock::now();
+          continue;
         }
       }
-      if (stop_.load()) return;
-      seen = gen_.load();
-      inside_.fetch_add(1);
-      if (const std::function<void(size_t)>* f = job_.load()) work(*f, n_);
-      inside_.fetch_sub(1);
+      cpu_relax();
+      if ((it & 255u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us_)) {
+        std::unique_lock<std::mutex> g(mu_);
+        sleepers_.fetch_add(1);
+        cv_.wait(g, [&] { return stop_.load() || njobs_.load() > 0; });
+        sleepers_.fetch_sub(1);
+        t0 = std::chrono::steady_clock::now();
+      }
     }
   }
   std::vector<std::thread> th_;
-  std::mutex mu_, call_mu_;
+  std::mutex mu_;
   std::condition_variable cv_;
-  std::atomic<const std::function<void(size_t)>*> job_{nullptr};
-  size_t n_ = 0;
-  std::atomic<size_t> next_{0}, done_{0};
-  std::atomic<unsigned> inside_{0}, sleepers_{0};
-  std::atomic<uint64_t> gen_{0};
+  std::vector<Job*> jobs_;
+  std::atomic<unsigned> njobs_{0}, sleepers_{0};
   std::atomic<bool> stop_{false};
   int spin_us_ = 300;
 };

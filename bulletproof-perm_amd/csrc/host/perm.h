@@ -71,6 +71,19 @@ void draw_prover_randomness(const Circuit& C, uint64_t seed, std::vector<uint32_
                             hsc::Sc& alpha, hsc::Sc& beta, hsc::Sc& rho, std::vector<hsc::Sc>& sL,
                             std::vector<hsc::Sc>& sR, std::vector<hsc::Sc>& taus);
 
+struct RandomDraws {
+  std::vector<uint32_t> pi;
+  std::vector<hsc::Sc> gamma, sL, sR, taus;
+  hsc::Sc alpha, beta, rho;
+};
+// Bytes of the SHAKE256 stream one proof's draws consume (fixed: the
+// Fisher-Yates steps take one u64 each, every scalar 64 bytes).
+size_t randomness_bytes(const Circuit& C);
+// The draws of eight proofs at once: the eight SHAKE256 streams run through
+// an AVX-512 8-way Keccak (host/keccak_x8.cpp; scalar fallback without
+// AVX-512), byte-identical to draw_prover_randomness.
+void draw_prover_randomness_x8(const Circuit& C, const uint64_t seeds[8], RandomDraws out[8]);
+
 size_t proof_len(uint32_t k);
 
 }  // namespace perm

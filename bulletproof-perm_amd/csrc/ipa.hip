@@ -252,10 +252,10 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
       u[p] = trs[p]->challenge_scalar("u");
     });
     ui = u;
-    hsc::batch_invert(ui);
-    for (uint32_t p = 0; p < P; ++p) {
-      const sc um = to_dev_sc(hsc::mul(u[p], SC_R_MOD_L));
-      const sc uim = to_dev_sc(hsc::mul(ui[p], SC_R_MOD_L));
+    hsc::batch_invert(ui, false);
+    for (uint32_t p = 0; p < P; ++p) {  // device Montgomery forms u R, u^-1 R
+      const sc um = to_dev_sc(hsc::to_mont(u[p]));
+      const sc uim = to_dev_sc(hsc::to_mont(ui[p]));
       memcpy(&uw[16 * (size_t)p], um.v, 32);
       memcpy(&uw[16 * (size_t)p + 8], uim.v, 32);
     }

@@ -193,11 +193,25 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
   for (size_t p = 0; p < P; ++p) S[p].reset(new ProverState(label, llen));
 
   // RNG draws (order fixed: pi, gamma, alpha beta rho, s_L, s_R, tau x5)
+  // (eight proofs' SHAKE256 streams per AVX-512 Keccak, perm::draw_prover_randomness_x8)
   std::unique_ptr<HostScope> hs(new HostScope(ctx, "pb_rng"));
-  par::for_each(P, [&](size_t p) {
-    ProverState& st = *S[p];
-    perm::draw_prover_randomness(C, seeds[p], st.pi, st.gamma, st.alpha, st.beta, st.rho, st.sL, st.sR, st.taus);
-    st.tr.arithmetic_domain_sep(n_p);
+  par::for_each((P + 7) / 8, [&](size_t gi) {
+    uint64_t sd[8];
+    perm::RandomDraws d[8];
+    for (size_t j = 0; j < 8; ++j) sd[j] = seeds[std::min(8 * gi + j, P - 1)];
+    perm::draw_prover_randomness_x8(C, sd, d);
+    for (size_t j = 0; j < 8 && 8 * gi + j < P; ++j) {
+      ProverState& st = *S[8 * gi + j];
+      st.pi = std::move(d[j].pi);
+      st.gamma = std::move(d[j].gamma);
+      st.sL = std::move(d[j].sL);
+      st.sR = std::move(d[j].sR);
+      st.taus = std::move(d[j].taus);
+      st.alpha = d[j].alpha;
+      st.beta = d[j].beta;
+      st.rho = d[j].rho;
+      st.tr.arithmetic_domain_sep(n_p);
+    }
   });
 
   // V_0..V_2k-1 of every proof: one fixed-base launch
@@ -303,7 +317,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
       zWVs[p] = perm::zW(C.WV, zq, m);
     });
     std::vector<Sc> yinv = ys;
-    hsc::batch_invert(yinv);
+    hsc::batch_invert(yinv, false);
     for (size_t p = 0; p < P; ++p) ch[3 * p + 1] = yinv[p];
     BPP_TRY(poly_coef_dev(ctx, C, (uint32_t)P, d_s, per, ch, tco));
     for (size_t p = 0; p < P; ++p)

@@ -115,3 +115,39 @@ def test_msm_async_submit_collect(ctx, big_table):
     assert got == [want_a, want_b] * 3
     ctx.dev_free(da)
     ctx.dev_free(db)
+
+
+def test_msm_2p22_config5_window_partition(ctx):
+    """Config 5 shape (one 2^22-term batch-verify MSM, bucket windows
+    partitioned over 8 GPUs), rehearsed on one GPU: the 8 ranks' window
+    partials (bpp_msm_submit/collect, windows split as bpperm.dist does)
+    sum to the full MSM, and the full MSM is linear in the scalars."""
+    import bpperm
+    from bpperm import dist as bdist
+    n = 1 << 22
+    raw = hashlib.shake_256(b"config5-points").digest(64 * n)
+    tbl = ctx.from_uniform(raw)
+    del raw
+    # scalars < 2^252 < l (canonical): top nibble cleared
+    sraw = bytearray(hashlib.shake_256(b"config5-scalars").digest(32 * n))
+    sraw[31::32] = bytes(b & 0x0F for b in sraw[31::32])
+    d = ctx.dev_alloc(32 * n)
+    ctx.htod(d, bytes(sraw))
+    full = ctx.msm_table_dev(d, tbl, n)
+    c, W = bpperm.msm_windows(n)
+    ranges = bdist.window_ranges(W, 8)
+    parts = []
+    for a, b in ranges:
+        parts.append(ctx.msm_collect(ctx.msm_submit(d, tbl, n, a, b), partial=True))
+    assert bpperm.partials_finish(parts) == full
+    # linearity on the doubled scalars (2s < 2^253 < l stays canonical)
+    import numpy as np
+    a = np.frombuffer(bytes(sraw), dtype="<u8").reshape(n, 4)
+    carry = np.concatenate([np.zeros((n, 1), dtype=np.uint64), a[:, :3] >> np.uint64(63)], axis=1)
+    dbl = ((a << np.uint64(1)) | carry).astype("<u8").tobytes()
+    ctx.htod(d, dbl)
+    got2 = ctx.msm_table_dev(d, tbl, n)
+    P = r255.decode(full)
+    assert got2 == r255.encode(r255.ed_add(P, P))
+    ctx.dev_free(d)
+    tbl.close()

@@ -79,10 +79,10 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
   }
   if (radix_sort) {
     void *dig, *cntA, *offA, *tmpA;
-    BPP_TRY(ctx_ws(ctx, "msm_dig", (size_t)T * Wn * 4 + 16, &dig));
+    BPP_TRY(ctx_ws(ctx, "msm_dig", (size_t)T * Wn * sizeof(dig_t) + 16, &dig));
     {
       ProfScope ps(ctx, "msm_digits");
-      hipLaunchKernelGGL(k_msm_digits, dim3(grid_for(T, 256)), dim3(256), 0, ctx->stream, d_scal, g, (uint32_t*)dig);
+      hipLaunchKernelGGL(k_msm_digits, dim3(grid_for(T, 256)), dim3(256), 0, ctx->stream, d_scal, g, (dig_t*)dig);
     }
     BPP_TRY(ctx_check_launch(ctx, "k_msm_digits"));
     const uint32_t chunk = RS_CHUNK;
@@ -95,7 +95,7 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
     {
       ProfScope ps(ctx, "msm_count");
       BPP_HIP(hipMemsetAsync((uint32_t*)cntA + nA, 0, 4, ctx->stream));
-      hipLaunchKernelGGL(k_rsort_count, dim3(Wn * nchunk), dim3(RS_T), 0, ctx->stream, (const uint32_t*)dig, g, chunk,
+      hipLaunchKernelGGL(k_rsort_count, dim3(Wn * nchunk), dim3(RS_T), 0, ctx->stream, (const dig_t*)dig, g, chunk,
                          nchunk, NC, (uint32_t*)cntA);
     }
     BPP_TRY(ctx_check_launch(ctx, "k_rsort_count"));
@@ -105,7 +105,7 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
     }
     {
       ProfScope ps(ctx, "msm_scatter");
-      hipLaunchKernelGGL(k_rsort_scatter, dim3(Wn * nchunk), dim3(RS_T), 0, ctx->stream, (const uint32_t*)dig, d_pidx,
+      hipLaunchKernelGGL(k_rsort_scatter, dim3(Wn * nchunk), dim3(RS_T), 0, ctx->stream, (const dig_t*)dig, d_pidx,
                          g, nchunk, NC, (const uint32_t*)offA, (uint32_t*)tmpA);
       hipLaunchKernelGGL(k_rsort_fine, dim3(Wn * NC), dim3(RS_T), 0, ctx->stream, (const uint32_t*)tmpA, nchunk,
                          (const uint32_t*)offA, (uint32_t*)boff, (uint32_t*)entries);
@@ -116,10 +116,10 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
     BPP_TRY(ctx_check_launch(ctx, "k_rsort_scatter/fine"));
   } else if (lds_sort && T) {
     void* dig = nullptr;
-    BPP_TRY(ctx_ws(ctx, "msm_dig", (size_t)T * Wn * 4 + 16, &dig));
+    BPP_TRY(ctx_ws(ctx, "msm_dig", (size_t)T * Wn * sizeof(dig_t) + 16, &dig));
     {
       ProfScope ps(ctx, "msm_digits");
-      hipLaunchKernelGGL(k_msm_digits, dim3(grid_for(T, 256)), dim3(256), 0, ctx->stream, d_scal, g, (uint32_t*)dig);
+      hipLaunchKernelGGL(k_msm_digits, dim3(grid_for(T, 256)), dim3(256), 0, ctx->stream, d_scal, g, (dig_t*)dig);
     }
     BPP_TRY(ctx_check_launch(ctx, "k_msm_digits"));
     // ~2 blocks per CU in total
@@ -135,7 +135,7 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
     }
     {
       ProfScope ps(ctx, "msm_count");
-      hipLaunchKernelGGL(k_msm_count_lds, dim3(Wn * nchunk), dim3(SORT_T), lds, ctx->stream, (const uint32_t*)dig, g,
+      hipLaunchKernelGGL(k_msm_count_lds, dim3(Wn * nchunk), dim3(SORT_T), lds, ctx->stream, (const dig_t*)dig, g,
                          chunk, nchunk, (uint32_t*)cnt);
     }
     BPP_TRY(ctx_check_launch(ctx, "k_msm_count_lds"));
@@ -145,7 +145,7 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
     }
     {
       ProfScope ps(ctx, "msm_scatter");
-      hipLaunchKernelGGL(k_msm_scatter_lds, dim3(Wn * nchunk), dim3(SORT_T), lds, ctx->stream, (const uint32_t*)dig,
+      hipLaunchKernelGGL(k_msm_scatter_lds, dim3(Wn * nchunk), dim3(SORT_T), lds, ctx->stream, (const dig_t*)dig,
                          d_pidx, g, chunk, nchunk, (const uint32_t*)boff, (uint32_t*)cur, (uint32_t*)entries);
     }
     BPP_TRY(ctx_check_launch(ctx, "k_msm_scatter_lds"));

@@ -422,39 +422,60 @@ __global__ void __launch_bounds__(64) k_msm_horner(const uint32_t* __restrict__ 
 
 // ---------------------------------------------------------------------------
 // Single large MSM sort path (M == 1, c <= 16): digits are recoded once into
-// a window-major uint32 array (code = sign << 31 | (|d| - 1), ~0 = zero
-// digit), then one workgroup per (window, chunk of terms) builds the bucket
+// a window-major array of 16-bit codes (below), widened in registers to
+// sign << 31 | (|d| - 1) (~0 = zero digit), then one workgroup per (window,
+// chunk of terms) builds the bucket
 // histogram in LDS.  Global memory then sees one coalesced atomic per
 // (block, bucket) instead of one scattered memory-side atomic per
 // (term, window) — the global-atomic kernels above ran at ~26 G atomics/s.
 #define DIG_ZERO 0xFFFFFFFFu
 #define DIG_SIGN 0x80000000u
+// In HBM the codes are 16-bit (sign << 15 | (|d| - 1); |d| - 1 < 2^15 for
+// c <= 16, and 0x7FFF -- the code of d = +2^15, which signed recoding never
+// produces -- marks a zero digit): half the digit traffic of the sort passes.
+typedef uint16_t dig_t;
+#define DIG16_ZERO 0x7FFFu
+FE_INLINE uint32_t dig_expand(uint32_t c16) {
+  return c16 == DIG16_ZERO ? DIG_ZERO : ((c16 & 0x7FFFu) | ((c16 & 0x8000u) << 16));
+}
 #define SORT_T 1024
 
 __global__ void __launch_bounds__(256) k_msm_digits(const uint32_t* __restrict__ scalars, MsmGeom g,
-                                                   uint32_t* __restrict__ dig) {
+                                                   dig_t* __restrict__ dig) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= g.T) return;
   uint32_t s[8];
   load_scalar(scalars, t, s);
-  for (uint32_t w = 0; w < g.Wn; ++w) dig[(size_t)w * g.T + t] = DIG_ZERO;
-  for_each_digit(s, g, [&](uint32_t w, int d) {
-    const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u;
-    dig[(size_t)w * g.T + t] = b | (d < 0 ? DIG_SIGN : 0u);
-  });
+  // for_each_digit's recoding, every window of [wb, wb + Wn) written once
+  uint32_t carry = 0;
+  const uint32_t half = 1u << (g.c - 1);
+  for (uint32_t w = 0; w < g.wb + g.Wn; ++w) {
+    const uint32_t v = scalar_bits(s, (int)(w * g.c), (int)g.c) + carry;
+    int d;
+    if (v >= half && w + 1 < g.W) {
+      d = (int)v - (int)(1u << g.c);
+      carry = 1;
+    } else {
+      d = (int)v;
+      carry = 0;
+    }
+    if (w < g.wb) continue;
+    const uint32_t code = d == 0 ? DIG16_ZERO : (((uint32_t)(d < 0 ? -d : d) - 1u) | (d < 0 ? 0x8000u : 0u));
+    dig[(size_t)(w - g.wb) * g.T + t] = (dig_t)code;
+  }
 }
 
 // grid = Wn * nchunk blocks; dynamic LDS = B * 4 bytes
-__global__ void __launch_bounds__(SORT_T) k_msm_count_lds(const uint32_t* __restrict__ dig, MsmGeom g, uint32_t chunk,
+__global__ void __launch_bounds__(SORT_T) k_msm_count_lds(const dig_t* __restrict__ dig, MsmGeom g, uint32_t chunk,
                                                          uint32_t nchunk, uint32_t* __restrict__ cnt) {
   extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
   const uint32_t w = blockIdx.x / nchunk, ch = blockIdx.x % nchunk;
   for (uint32_t b = threadIdx.x; b < g.B; b += SORT_T) hist[b] = 0;
   __syncthreads();
   const uint32_t t0 = ch * chunk, t1 = min(t0 + chunk, g.T);
-  const uint32_t* dw = dig + (size_t)w * g.T;
+  const dig_t* dw = dig + (size_t)w * g.T;
   for (uint32_t t = t0 + threadIdx.x; t < t1; t += SORT_T) {
-    const uint32_t code = dw[t];
+    const uint32_t code = dig_expand(dw[t]);
     if (code != DIG_ZERO) atomicAdd(&hist[code & ~DIG_SIGN], 1u);
   }
   __syncthreads();
@@ -465,7 +486,7 @@ __global__ void __launch_bounds__(SORT_T) k_msm_count_lds(const uint32_t* __rest
   }
 }
 
-__global__ void __launch_bounds__(SORT_T) k_msm_scatter_lds(const uint32_t* __restrict__ dig,
+__global__ void __launch_bounds__(SORT_T) k_msm_scatter_lds(const dig_t* __restrict__ dig,
                                                            const uint32_t* __restrict__ pidx, MsmGeom g,
                                                            uint32_t chunk, uint32_t nchunk,
                                                            const uint32_t* __restrict__ boff,
@@ -476,9 +497,9 @@ __global__ void __launch_bounds__(SORT_T) k_msm_scatter_lds(const uint32_t* __re
   for (uint32_t b = threadIdx.x; b < g.B; b += SORT_T) hist[b] = 0;
   __syncthreads();
   const uint32_t t0 = ch * chunk, t1 = min(t0 + chunk, g.T);
-  const uint32_t* dw = dig + (size_t)w * g.T;
+  const dig_t* dw = dig + (size_t)w * g.T;
   for (uint32_t t = t0 + threadIdx.x; t < t1; t += SORT_T) {
-    const uint32_t code = dw[t];
+    const uint32_t code = dig_expand(dw[t]);
     if (code != DIG_ZERO) atomicAdd(&hist[code & ~DIG_SIGN], 1u);
   }
   __syncthreads();
@@ -490,7 +511,7 @@ __global__ void __launch_bounds__(SORT_T) k_msm_scatter_lds(const uint32_t* __re
   }
   __syncthreads();
   for (uint32_t t = t0 + threadIdx.x; t < t1; t += SORT_T) {
-    const uint32_t code = dw[t];
+    const uint32_t code = dig_expand(dw[t]);
     if (code == DIG_ZERO) continue;
     const uint32_t pos = atomicAdd(&hist[code & ~DIG_SIGN], 1u);
     entries[pos] = (pidx ? pidx[t] : t) | (code & DIG_SIGN);
@@ -521,14 +542,14 @@ __global__ void __launch_bounds__(SORT_T) k_msm_scatter_lds(const uint32_t* __re
 // coalesced loads (RS_PER per thread) before any LDS atomic: a load-then-
 // atomic loop leaves each load's latency exposed.
 #define RS_PER (RS_CHUNK / RS_T)
-FE_INLINE void rs_load_chunk(const uint32_t* __restrict__ dw, uint32_t t0, uint32_t t1, uint32_t v[RS_PER]) {
+FE_INLINE void rs_load_chunk(const dig_t* __restrict__ dw, uint32_t t0, uint32_t t1, uint32_t v[RS_PER]) {
   _Pragma("unroll") for (uint32_t k = 0; k < RS_PER; ++k) {
     const uint32_t t = t0 + k * RS_T + threadIdx.x;
-    v[k] = t < t1 ? dw[t] : DIG_ZERO;
+    v[k] = t < t1 ? dig_expand(dw[t]) : DIG_ZERO;
   }
 }
 
-__global__ void __launch_bounds__(RS_T) k_rsort_count(const uint32_t* __restrict__ dig, MsmGeom g, uint32_t chunk,
+__global__ void __launch_bounds__(RS_T) k_rsort_count(const dig_t* __restrict__ dig, MsmGeom g, uint32_t chunk,
                                                      uint32_t nchunk, uint32_t NC, uint32_t* __restrict__ cntA) {
   __shared__ uint32_t h[256];
   const uint32_t w = blockIdx.x / nchunk, ch = blockIdx.x % nchunk;
@@ -568,7 +589,7 @@ __device__ __forceinline__ void lds_excl_scan_w0(uint32_t* a, uint32_t per, uint
 // Coarse scatter with block-local staging: entries of the chunk are sorted
 // by coarse bin in LDS, then written out bin-run by bin-run (consecutive
 // lanes -> consecutive addresses).  (idx < 2^24 on this path.)
-__global__ void __launch_bounds__(RS_T) k_rsort_scatter(const uint32_t* __restrict__ dig,
+__global__ void __launch_bounds__(RS_T) k_rsort_scatter(const dig_t* __restrict__ dig,
                                                        const uint32_t* __restrict__ pidx, MsmGeom g, uint32_t nchunk,
                                                        uint32_t NC, const uint32_t* __restrict__ offA,
                                                        uint32_t* __restrict__ tmpA) {

@@ -71,8 +71,31 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
   BPP_TRY(ctx_ws(ctx, "msm_wsum", nseg * P3_BYTES, &wsum));
   // (tmpA packs the point index in 24 bits)
   const bool radix_sort = !fb && (M == 1) && (c >= 12) && (c <= 16) && (T >= 16384) && (T <= (1u << 24)) &&
-                          (!d_pidx) && !getenv("BPP_MSM_LDS_SORT");
+                          (!d_pidx) && (size_t)Wn * (g.B >> RS_FINE_BITS) <= RS_DC_HMAX &&
+                          !getenv("BPP_MSM_LDS_SORT");
   const bool lds_sort = !fb && !radix_sort && (M == 1) && (c <= 16) && (T >= 16384);
+  // entries per lane: enough lanes to fill the chip several times over
+  const uint32_t E_max = T * Wn;
+  // K = entries per lane: about one round of lanes at the accumulate's
+  // 4 waves/SIMD occupancy (256 K lanes) -- fewer chunk borders, so fewer
+  // head/tail pieces (2^20: K = 64 measured best of 32/64/128)
+  uint32_t K = 4;
+  while (K < 128 && E_max / (2 * K) >= 256u * 1024u) K <<= 1;
+  if (const char* ek = getenv("BPP_MSM_K")) {  // rounded down to a power of two >= 4
+    const uint32_t want = std::max(4, atoi(ek));
+    for (K = 4; K * 2 <= want; K *= 2) {
+    }
+  }
+  const size_t lanes = (E_max + K - 1) / K + 1;
+  uint32_t ks = 0;
+  while ((1u << ks) < K) ++ks;
+  // a heavy bucket spans > FIX_MAX chunks, so holds > (FIX_MAX - 1) K
+  // entries: at most E / ((FIX_MAX - 1) K) + 1 of them
+  const size_t max_heavy = std::min<size_t>(NB, E_max / ((size_t)(FIX_MAX - 1) * K) + 1);
+  void *head, *tail, *heavy;
+  BPP_TRY(ctx_ws(ctx, "msm_head", lanes * P3_BYTES, &head));
+  BPP_TRY(ctx_ws(ctx, "msm_tail", lanes * P3_BYTES, &tail));
+  BPP_TRY(ctx_ws(ctx, "msm_heavy", (max_heavy + 1) * 4, &heavy));
   if (!radix_sort) {
     BPP_HIP(hipMemsetAsync(cnt, 0, (NB + 1) * 4, ctx->stream));
     BPP_HIP(hipMemsetAsync(cur, 0, NB * 4, ctx->stream));
@@ -80,25 +103,18 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
   if (radix_sort) {
     void *dig, *cntA, *offA, *tmpA;
     BPP_TRY(ctx_ws(ctx, "msm_dig", (size_t)T * Wn * sizeof(dig_t) + 16, &dig));
-    {
-      ProfScope ps(ctx, "msm_digits");
-      hipLaunchKernelGGL(k_msm_digits, dim3(grid_for(T, 256)), dim3(256), 0, ctx->stream, d_scal, g, (dig_t*)dig);
-    }
-    BPP_TRY(ctx_check_launch(ctx, "k_msm_digits"));
-    const uint32_t chunk = RS_CHUNK;
-    const uint32_t nchunk = (T + chunk - 1) / chunk;
+    const uint32_t nchunk = (T + RS_CHUNK - 1) / RS_CHUNK;
     const uint32_t NC = g.B >> RS_FINE_BITS;  // <= 256 coarse bins per window
     const size_t nA = (size_t)Wn * NC * nchunk;
     BPP_TRY(ctx_ws(ctx, "msm_cntA", (nA + 1) * 4, &cntA));
     BPP_TRY(ctx_ws(ctx, "msm_offA", (nA + 1) * 4, &offA));
     BPP_TRY(ctx_ws(ctx, "msm_tmpA", (size_t)T * Wn * 4 + 16, &tmpA));
     {
-      ProfScope ps(ctx, "msm_count");
-      BPP_HIP(hipMemsetAsync((uint32_t*)cntA + nA, 0, 4, ctx->stream));
-      hipLaunchKernelGGL(k_rsort_count, dim3(Wn * nchunk), dim3(RS_T), 0, ctx->stream, (const dig_t*)dig, g, chunk,
-                         nchunk, NC, (uint32_t*)cntA);
+      ProfScope ps(ctx, "msm_digits");  // digits + coarse counts
+      hipLaunchKernelGGL(k_rsort_digits_count, dim3(nchunk), dim3(RS_DC_T), 0, ctx->stream, d_scal, g, nchunk, NC,
+                         (dig_t*)dig, (uint32_t*)cntA, (uint32_t*)cntA + nA, (uint32_t*)heavy);
     }
-    BPP_TRY(ctx_check_launch(ctx, "k_rsort_count"));
+    BPP_TRY(ctx_check_launch(ctx, "k_rsort_digits_count"));
     {
       ProfScope ps(ctx, "msm_scan");
       BPP_TRY(scan_exclusive_u32(ctx, (const uint32_t*)cntA, (uint32_t*)offA, nA + 1));
@@ -107,11 +123,9 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
       ProfScope ps(ctx, "msm_scatter");
       hipLaunchKernelGGL(k_rsort_scatter, dim3(Wn * nchunk), dim3(RS_T), 0, ctx->stream, (const dig_t*)dig, d_pidx,
                          g, nchunk, NC, (const uint32_t*)offA, (uint32_t*)tmpA);
-      hipLaunchKernelGGL(k_rsort_fine, dim3(Wn * NC), dim3(RS_T), 0, ctx->stream, (const uint32_t*)tmpA, nchunk,
-                         (const uint32_t*)offA, (uint32_t*)boff, (uint32_t*)entries);
-      // boff[NB] = number of entries
-      BPP_HIP(hipMemcpyAsync((uint32_t*)boff + NB, (const uint32_t*)offA + nA, 4, hipMemcpyDeviceToDevice,
-                             ctx->stream));
+      hipLaunchKernelGGL(k_rsort_fine, dim3(Wn * NC), dim3(RS_FT), 0, ctx->stream, (const uint32_t*)tmpA, nchunk,
+                         (const uint32_t*)offA, (uint32_t*)boff, (uint32_t*)entries, (uint32_t*)boff + NB,
+                         (const uint32_t*)offA + nA);
     }
     BPP_TRY(ctx_check_launch(ctx, "k_rsort_scatter/fine"));
   } else if (lds_sort && T) {
@@ -168,29 +182,7 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
     BPP_TRY(ctx_check_launch(ctx, "k_msm_scatter"));
   }
   {
-    // entries per lane: enough lanes to fill the chip several times over
-    const uint32_t E_max = T * Wn;
-    // K = entries per lane: about one round of lanes at the accumulate's
-    // 4 waves/SIMD occupancy (256 K lanes) -- fewer chunk borders, so fewer
-    // head/tail pieces (2^20: K = 64 measured best of 32/64/128)
-    uint32_t K = 4;
-    while (K < 128 && E_max / (2 * K) >= 256u * 1024u) K <<= 1;
-    if (const char* ek = getenv("BPP_MSM_K")) {  // rounded down to a power of two >= 4
-      const uint32_t want = std::max(4, atoi(ek));
-      for (K = 4; K * 2 <= want; K *= 2) {
-      }
-    }
-    const size_t lanes = (E_max + K - 1) / K + 1;
-    uint32_t ks = 0;
-    while ((1u << ks) < K) ++ks;
-    // a heavy bucket spans > FIX_MAX chunks, so holds > (FIX_MAX - 1) K
-    // entries: at most E / ((FIX_MAX - 1) K) + 1 of them
-    const size_t max_heavy = std::min<size_t>(NB, E_max / ((size_t)(FIX_MAX - 1) * K) + 1);
-    void *head, *tail, *heavy;
-    BPP_TRY(ctx_ws(ctx, "msm_head", lanes * P3_BYTES, &head));
-    BPP_TRY(ctx_ws(ctx, "msm_tail", lanes * P3_BYTES, &tail));
-    BPP_TRY(ctx_ws(ctx, "msm_heavy", (max_heavy + 1) * 4, &heavy));
-    BPP_HIP(hipMemsetAsync(heavy, 0, 4, ctx->stream));
+    if (!radix_sort) BPP_HIP(hipMemsetAsync(heavy, 0, 4, ctx->stream));  // (radix: cleared by its first kernel)
     if (ctx->acc_wait) BPP_HIP(hipStreamWaitEvent(ctx->stream, ctx->acc_wait, 0));
     {
       ProfScope ps(ctx, "msm_accumulate");

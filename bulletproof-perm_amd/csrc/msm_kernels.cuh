@@ -33,6 +33,19 @@ FE_INLINE uint32_t scalar_bits(const uint32_t s[8], int pos, int c) {
   return (uint32_t)v & ((1u << c) - 1u);
 }
 
+// Bits [pos, pos + c) of a 256-bit scalar held in registers, with the word
+// picked by selects (a runtime index into s[] would put it in scratch).
+FE_INLINE uint32_t word_sel(const uint32_t s[8], uint32_t i) {
+  uint32_t r = 0;
+  _Pragma("unroll") for (uint32_t k = 0; k < 8; ++k) r = (i == k) ? s[k] : r;
+  return r;
+}
+FE_INLINE uint32_t scalar_bits_sel(const uint32_t s[8], uint32_t pos, uint32_t c) {
+  const uint32_t wi = pos >> 5, sh = pos & 31;
+  const uint64_t v = ((uint64_t)word_sel(s, wi) | ((uint64_t)word_sel(s, wi + 1) << 32)) >> sh;
+  return (uint32_t)v & ((1u << c) - 1u);
+}
+
 FE_INLINE void load_scalar(const uint32_t* __restrict__ sc, size_t t, uint32_t s[8]) {
   const uint4* p = reinterpret_cast<const uint4*>(sc + t * 8);
   uint4 a = p[0], b = p[1];
@@ -564,6 +577,59 @@ __global__ void __launch_bounds__(RS_T) k_rsort_count(const dig_t* __restrict__ 
   for (uint32_t b = threadIdx.x; b < NC; b += RS_T) cntA[((size_t)w * NC + b) * nchunk + ch] = h[b];
 }
 
+// Digits and the coarse histogram in one pass over the scalars (the radix
+// path's first kernel; replaces k_msm_digits + k_rsort_count, so the digit
+// codes are written once and first read back by the scatter): block = one
+// chunk of RS_CHUNK terms, every window of [wb, wb + Wn); LDS histogram of
+// the Wn x NC coarse bins -> cntA[(w * NC + bin) * nchunk + ch].  Block 0
+// also clears the two words later passes need zeroed (the scan's trailing
+// count, the accumulation's heavy-bucket counter): no memset launches.
+#define RS_DC_T 1024
+#define RS_DC_HMAX 4096  // Wn * NC <= 16 * 256 for c <= 16
+__global__ void __launch_bounds__(RS_DC_T) k_rsort_digits_count(const uint32_t* __restrict__ scalars, MsmGeom g,
+                                                              uint32_t nchunk, uint32_t NC, dig_t* __restrict__ dig,
+                                                              uint32_t* __restrict__ cntA, uint32_t* __restrict__ z0,
+                                                              uint32_t* __restrict__ z1) {
+  __shared__ uint32_t h[RS_DC_HMAX];
+  const uint32_t ch = blockIdx.x, nh = g.Wn * NC;
+  for (uint32_t i = threadIdx.x; i < nh; i += RS_DC_T) h[i] = 0;
+  if (ch == 0 && threadIdx.x == 0) {
+    *z0 = 0;
+    *z1 = 0;
+  }
+  __syncthreads();
+  const uint32_t half = 1u << (g.c - 1);
+  for (uint32_t k = 0; k < RS_CHUNK / RS_DC_T; ++k) {
+    const uint32_t t = ch * RS_CHUNK + k * RS_DC_T + threadIdx.x;
+    if (t >= g.T) continue;
+    uint32_t s[8];
+    load_scalar(scalars, t, s);
+    uint32_t carry = 0;
+    for (uint32_t w = 0; w < g.wb + g.Wn; ++w) {
+      const uint32_t v = scalar_bits_sel(s, w * g.c, g.c) + carry;
+      int d;
+      if (v >= half && w + 1 < g.W) {
+        d = (int)v - (int)(2 * half);
+        carry = 1;
+      } else {
+        d = (int)v;
+        carry = 0;
+      }
+      if (w < g.wb) continue;
+      const uint32_t ww = w - g.wb;
+      uint32_t code = DIG16_ZERO;
+      if (d != 0) {
+        const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u;
+        code = b | (d < 0 ? 0x8000u : 0u);
+        atomicAdd(&h[ww * NC + (b >> RS_FINE_BITS)], 1u);
+      }
+      dig[(size_t)ww * g.T + t] = (dig_t)code;
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nh; i += RS_DC_T) cntA[(size_t)i * nchunk + ch] = h[i];
+}
+
 // In-place exclusive scan of a[0..64 * per) (per <= 4) by wave 0; the
 // caller synchronises.  a[i] <- base + sum(a[0..i)).
 __device__ __forceinline__ void lds_excl_scan_w0(uint32_t* a, uint32_t per, uint32_t base) {
@@ -638,27 +704,30 @@ __global__ void __launch_bounds__(RS_T) k_rsort_scatter(const dig_t* __restrict_
 #ifndef RS_FTILE
 #define RS_FTILE 8192
 #endif
-#define RS_FPER (RS_FTILE / RS_T)
-__global__ void __launch_bounds__(RS_T) k_rsort_fine(const uint32_t* __restrict__ tmpA, uint32_t nchunk,
+#define RS_FT 512  // 8 waves per block: 4 blocks (40 KB LDS each) = 32 waves per CU
+#define RS_FPER (RS_FTILE / RS_FT)
+__global__ void __launch_bounds__(RS_FT) k_rsort_fine(const uint32_t* __restrict__ tmpA, uint32_t nchunk,
                                                     const uint32_t* __restrict__ offA, uint32_t* __restrict__ boff,
-                                                    uint32_t* __restrict__ entries) {
+                                                    uint32_t* __restrict__ entries, uint32_t* __restrict__ end_dst,
+                                                    const uint32_t* __restrict__ end_src) {
   __shared__ uint32_t base[RS_FINE_N], lcnt[RS_FINE_N], lloc[RS_FINE_N];
   __shared__ uint32_t stage[RS_FTILE];
   __shared__ uint8_t sf[RS_FTILE];
   // w * NC + coarse bin, last first: the top window's few dense bins take
   // the multi-tile path and should not be the grid's tail
   const uint32_t seg = gridDim.x - 1 - blockIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *end_dst = *end_src;  // boff[NB] = number of entries
   const uint32_t s = offA[(size_t)seg * nchunk], e = offA[(size_t)(seg + 1) * nchunk];
   if (e - s <= RS_FTILE) {  // one tile, held in registers between the passes
     uint32_t v[RS_FPER];
     _Pragma("unroll") for (uint32_t k = 0; k < RS_FPER; ++k) {
-      const uint32_t i = s + k * RS_T + threadIdx.x;
+      const uint32_t i = s + k * RS_FT + threadIdx.x;
       v[k] = i < e ? tmpA[i] : 0u;
     }
     if (threadIdx.x < RS_FINE_N) lcnt[threadIdx.x] = 0;
     __syncthreads();
     _Pragma("unroll") for (uint32_t k = 0; k < RS_FPER; ++k)
-      if (k * RS_T + threadIdx.x < e - s) atomicAdd(&lcnt[(v[k] >> 24) & 0x7fu], 1u);
+      if (k * RS_FT + threadIdx.x < e - s) atomicAdd(&lcnt[(v[k] >> 24) & 0x7fu], 1u);
     __syncthreads();
     if (threadIdx.x < RS_FINE_N) lloc[threadIdx.x] = lcnt[threadIdx.x];
     __syncthreads();
@@ -670,21 +739,21 @@ __global__ void __launch_bounds__(RS_T) k_rsort_fine(const uint32_t* __restrict_
     }
     __syncthreads();
     _Pragma("unroll") for (uint32_t k = 0; k < RS_FPER; ++k) {
-      if (k * RS_T + threadIdx.x >= e - s) continue;
+      if (k * RS_FT + threadIdx.x >= e - s) continue;
       const uint32_t f = (v[k] >> 24) & 0x7fu;
       stage[atomicAdd(&lcnt[f], 1u)] = v[k] & ~RS_FMASK;
     }
     __syncthreads();
     // stage is sorted by fine bin and the segment's entries are contiguous
     // in the output: one coalesced copy
-    for (uint32_t j = threadIdx.x; j < e - s; j += RS_T) entries[s + j] = stage[j];
+    for (uint32_t j = threadIdx.x; j < e - s; j += RS_FT) entries[s + j] = stage[j];
     return;
   }
   const bool one_tile = false;
   if (!one_tile) {
     if (threadIdx.x < RS_FINE_N) base[threadIdx.x] = 0;
     __syncthreads();
-    for (uint32_t i = s + threadIdx.x; i < e; i += RS_T) atomicAdd(&base[(tmpA[i] >> 24) & 0x7fu], 1u);
+    for (uint32_t i = s + threadIdx.x; i < e; i += RS_FT) atomicAdd(&base[(tmpA[i] >> 24) & 0x7fu], 1u);
     __syncthreads();
     lds_excl_scan_w0(base, 2, s);
     __syncthreads();
@@ -694,7 +763,7 @@ __global__ void __launch_bounds__(RS_T) k_rsort_fine(const uint32_t* __restrict_
     const uint32_t te = min(ts + RS_FTILE, e);
     if (threadIdx.x < RS_FINE_N) lcnt[threadIdx.x] = 0;
     __syncthreads();
-    for (uint32_t i = ts + threadIdx.x; i < te; i += RS_T) atomicAdd(&lcnt[(tmpA[i] >> 24) & 0x7fu], 1u);
+    for (uint32_t i = ts + threadIdx.x; i < te; i += RS_FT) atomicAdd(&lcnt[(tmpA[i] >> 24) & 0x7fu], 1u);
     __syncthreads();
     if (threadIdx.x < RS_FINE_N) lloc[threadIdx.x] = lcnt[threadIdx.x];
     __syncthreads();
@@ -708,7 +777,7 @@ __global__ void __launch_bounds__(RS_T) k_rsort_fine(const uint32_t* __restrict_
       }
     }
     __syncthreads();
-    for (uint32_t i = ts + threadIdx.x; i < te; i += RS_T) {
+    for (uint32_t i = ts + threadIdx.x; i < te; i += RS_FT) {
       const uint32_t v = tmpA[i];
       const uint32_t f = (v >> 24) & 0x7fu;
       const uint32_t p = atomicAdd(&lcnt[f], 1u);
@@ -716,7 +785,7 @@ __global__ void __launch_bounds__(RS_T) k_rsort_fine(const uint32_t* __restrict_
       sf[p] = (uint8_t)f;
     }
     __syncthreads();
-    for (uint32_t j = threadIdx.x; j < te - ts; j += RS_T) {
+    for (uint32_t j = threadIdx.x; j < te - ts; j += RS_FT) {
       const uint32_t f = sf[j];
       entries[base[f] + j - lloc[f]] = stage[j];
     }
@@ -743,18 +812,6 @@ struct DtGeom {
 FE_INLINE uint32_t dt_half(const DtGeom& g) { return 1u << (g.c - 1); }
 
 
-// Bits [pos, pos + c) of a 256-bit scalar held in registers, with the word
-// picked by selects (a runtime index into s[] would put it in scratch).
-FE_INLINE uint32_t word_sel(const uint32_t s[8], uint32_t i) {
-  uint32_t r = 0;
-  _Pragma("unroll") for (uint32_t k = 0; k < 8; ++k) r = (i == k) ? s[k] : r;
-  return r;
-}
-FE_INLINE uint32_t scalar_bits_sel(const uint32_t s[8], uint32_t pos, uint32_t c) {
-  const uint32_t wi = pos >> 5, sh = pos & 31;
-  const uint64_t v = ((uint64_t)word_sel(s, wi) | ((uint64_t)word_sel(s, wi + 1) << 32)) >> sh;
-  return (uint32_t)v & ((1u << c) - 1u);
-}
 
 // Lane-local walk over the nonzero (term, window) digits of its slice.
 struct DtWalk {

@@ -52,6 +52,10 @@ struct bpp_ctx {
   // msm_engine hooks (set by bpp_msm_submit on a child): wait for acc_wait
   // before the bucket accumulation, record acc_done after it
   hipEvent_t acc_wait = nullptr, acc_done = nullptr;
+  // extra dynamic LDS per accumulation workgroup (bpp_msm_submit sets it when
+  // another MSM is in flight: 3 instead of 4 workgroups per CU, so the other
+  // MSM's sort kernels run beside the accumulation)
+  size_t acc_lds_pad = 0;
 };
 
 struct bpp_points {

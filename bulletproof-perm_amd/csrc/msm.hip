@@ -186,7 +186,8 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
     if (ctx->acc_wait) BPP_HIP(hipStreamWaitEvent(ctx->stream, ctx->acc_wait, 0));
     {
       ProfScope ps(ctx, "msm_accumulate");
-      hipLaunchKernelGGL(k_msm_accumulate, dim3(grid_for(lanes, ACC_T)), dim3(ACC_T), 0, ctx->stream, d_tbl, d_tbl1,
+      hipLaunchKernelGGL(k_msm_accumulate, dim3(grid_for(lanes, ACC_T)), dim3(ACC_T), ctx->acc_lds_pad, ctx->stream,
+                         d_tbl, d_tbl1,
                          n0, (const uint32_t*)entries, (const uint32_t*)boff, (uint32_t)NB, K, (uint32_t*)bsum,
                          (uint32_t*)head, (uint32_t*)tail, (uint32_t*)heavy);
     }
@@ -412,6 +413,14 @@ int bpp_msm_submit(bpp_ctx* ctx, const void* d_scalars, const bpp_points* tbl, s
   bpp_ctx* ch = nullptr;
   BPP_TRY(ctx_child(ctx, s, &ch));
   ch->prof = ctx->prof;
+  // Another MSM in flight: hold this accumulation to 3 workgroups per CU
+  // (LDS 40 + 13 KB each) so the other MSM's sort runs beside it rather than
+  // after it -- 2^20, two in flight: 0.97 -> 0.945 ms per MSM; alone it
+  // would cost the accumulation ~8 % (BPP_ACC_LDS_PAD overrides the pad).
+  bool others = false;
+  for (size_t i = 0; i < BPP_MSM_INFLIGHT; ++i) others |= ctx->msm_slot[i].busy;
+  static const long pad_env = getenv("BPP_ACC_LDS_PAD") ? atol(getenv("BPP_ACC_LDS_PAD")) : -1;
+  ch->acc_lds_pad = others ? (pad_env >= 0 ? (size_t)pad_env : (size_t)13000) : 0;
   if (!sl.done) BPP_HIP(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
   // inputs written on ctx's stream before this call are visible to the child
   BPP_HIP(hipEventRecord(sl.done, ctx->stream));

@@ -110,6 +110,41 @@ FE_INLINE ge_p3 ge_madd_signed(const ge_p3& p, const ge_niels& q, bool neg) {
   return r;
 }
 
+// ge_madd_signed in two halves, so that a caller can issue the loads of its
+// next operand between them (the operand is dead after the first half):
+// half 1 = the three multiplies that read q, half 2 = the four that do not.
+struct ge_madd_mid {
+  fe E, F, G, H;
+};
+FE_INLINE ge_madd_mid ge_madd_signed_h1(const ge_p3& p, const ge_niels& q, bool neg) {
+  fe qa, qb;
+  _Pragma("unroll") for (int i = 0; i < FE_LIMBS; ++i) {
+    qa.v[i] = neg ? q.ypx.v[i] : q.ymx.v[i];
+    qb.v[i] = neg ? q.ymx.v[i] : q.ypx.v[i];
+  }
+  fe A = fe_mul(fe_sub_nc(p.Y, p.X), qa);
+  fe B = fe_mul(fe_add_nc(p.Y, p.X), qb);
+  fe C = fe_mul(p.T, q.xy2d);
+  fe D = fe_add_nc(p.Z, p.Z);
+  ge_madd_mid m;
+  m.E = fe_sub_nc(B, A);
+  m.H = fe_add_nc(B, A);
+  const fe Dm = fe_sub(D, C), Dp = fe_add_nc(D, C);
+  _Pragma("unroll") for (int i = 0; i < FE_LIMBS; ++i) {
+    m.F.v[i] = neg ? Dp.v[i] : Dm.v[i];
+    m.G.v[i] = neg ? Dm.v[i] : Dp.v[i];
+  }
+  return m;
+}
+FE_INLINE ge_p3 ge_madd_h2(const ge_madd_mid& m) {
+  ge_p3 r;
+  r.X = fe_mul(m.E, m.F);
+  r.Y = fe_mul(m.G, m.H);
+  r.Z = fe_mul(m.F, m.G);
+  r.T = fe_mul(m.E, m.H);
+  return r;
+}
+
 FE_INLINE ge_niels ge_niels_neg(const ge_niels& q) {
   ge_niels r;
   r.ypx = q.ymx;

@@ -1,7 +1,7 @@
 // Host-side parallel-for over independent proofs (transcripts, challenge
 // scalars, witness polynomials).  A persistent pool (spawning threads per
 // call costs ~20 us each, more than a batch of transcript operations):
-// threads = BPP_HOST_THREADS or min(granted CPUs, 16); items are claimed
+// threads = BPP_HOST_THREADS or min(granted CPUs, 16) / 2; items are claimed
 // from an atomic counter; the calling thread works too.  Concurrent calls
 // share the workers; a call from inside a pool task runs inline.
 #pragma once
@@ -36,9 +36,13 @@ inline unsigned granted_cpus() {
 inline unsigned threads() {
   static const unsigned n = [] {
     const char* e = getenv("BPP_HOST_THREADS");
-    // measured on the box (16-CPU quota): 16 threads 6.8 ms vs 8 threads
-    // 7.4 ms per 128-proof batch, 19 vs 25 ms per 512
-    const unsigned v = e ? (unsigned)atoi(e) : std::min(16u, granted_cpus());
+    // Half the granted CPUs (8 of the box's 16): every batch in flight has
+    // its own driver thread that works on its jobs too, so 8 batches + 7
+    // workers fill the quota without oversubscribing it.  Measured on the
+    // box, 128-proof batches: 16 threads x 4 in flight 52-64 K proofs/s,
+    // 8 x 8 75-80 K, 8 x 12 80-83 K, 4 x 12 80-81 K; one batch alone
+    // 5.57 ms with 16 threads vs 5.60 ms with 8 (tools/gpu_exp4.sh).
+    const unsigned v = e ? (unsigned)atoi(e) : std::max(1u, std::min(16u, granted_cpus()) / 2);
     return std::max(1u, v);
   }();
   return n;

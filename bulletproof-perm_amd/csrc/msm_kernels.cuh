@@ -135,7 +135,9 @@ __global__ void k_msm_scatter(const uint32_t* __restrict__ scalars, const uint32
 
 // 4 waves per SIMD (<= 128 VGPRs; the LDS piece buffer also allows 4):
 // without the bound the post-barrier fold lifts the kernel to 187 VGPRs.
-#ifdef ACC_WAVES5
+#if defined(ACC_WAVES3)
+#define ACC_ATTR __attribute__((amdgpu_waves_per_eu(3, 8)))
+#elif defined(ACC_WAVES5)
 #define ACC_ATTR __attribute__((amdgpu_waves_per_eu(5, 8)))
 #else
 #define ACC_ATTR __attribute__((amdgpu_waves_per_eu(4, 8)))
@@ -159,6 +161,14 @@ FE_INLINE ge_niels fetch_entry(const uint32_t* __restrict__ tbl, const uint32_t*
   ge_niels q = pi < n0 ? load_niels(tbl, pi) : load_niels(tbl1, pi - n0);
   if (e & 0x80000000u) q = ge_niels_neg(q);
   return q;
+}
+
+// Table point of entry e without its sign (bit 31 is applied by the caller).
+FE_INLINE ge_niels fetch_entry_raw(const uint32_t* __restrict__ tbl, const uint32_t* __restrict__ tbl1, uint32_t n0,
+                                   uint32_t e) {
+  const uint32_t pi = e & 0x7fffffffu;
+  const bool lo = pi < n0;  // one load sequence from a selected base
+  return load_niels(lo ? tbl : tbl1, lo ? pi : pi - n0);
 }
 
 // A bucket spanning more than FIX_MAX chunks (bucket skew: the few buckets
@@ -218,10 +228,19 @@ __global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_
     // loads touch the same 128-B line K times across a long loop and
     // re-fetch it once the table gathers have evicted it
     uint4 e4 = make_uint4(0, 0, 0, 0);
+#ifdef ACC_PREFETCH
+    // software pipeline: the next entry's 128-B row is gathered while the
+    // four multiplies of this addition that do not read the operand run
+    e4 = *reinterpret_cast<const uint4*>(entries + i0);
+    uint32_t e = e4.x;
+    ge_niels qn = fetch_entry_raw(tbl, tbl1, n0, e);
+    for (uint32_t i = i0; i < i1; ++i) {
+#else
     for (uint32_t i = i0; i < i1; ++i) {
       if (((i - i0) & 3u) == 0) e4 = *reinterpret_cast<const uint4*>(entries + i);
       const uint32_t q = (i - i0) & 3u;
       const uint32_t e = q == 0 ? e4.x : q == 1 ? e4.y : q == 2 ? e4.z : e4.w;
+#endif
       if (i == bend) {  // close the run of bucket b
         if (bstart >= i0) {
           store_p3(bsum, b, acc);  // whole bucket inside the chunk
@@ -234,7 +253,18 @@ __global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_
         if (((bend - 1) >> ks) - l >= FIX_MAX) heavy[1 + atomicAdd(&heavy[0], 1u)] = b;
         acc = ge_identity();
       }
+#ifdef ACC_PREFETCH
+      const ge_madd_mid mid = ge_madd_signed_h1(acc, qn, e >> 31);
+      if (i + 1 < i1) {
+        const uint32_t q = (i + 1 - i0) & 3u;
+        if (q == 0) e4 = *reinterpret_cast<const uint4*>(entries + i + 1);
+        e = q == 0 ? e4.x : q == 1 ? e4.y : q == 2 ? e4.z : e4.w;
+        qn = fetch_entry_raw(tbl, tbl1, n0, e);
+      }
+      acc = ge_madd_h2(mid);
+#else
       acc = ge_madd(acc, fetch_entry(tbl, tbl1, n0, e));
+#endif
     }
     // last run [max(bstart, i0), i1)
     if (bstart >= i0 && bend <= i1) {

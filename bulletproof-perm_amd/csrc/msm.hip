@@ -60,6 +60,18 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
   g.Wn = Wn;
   g.B = 1u << (c - 1);
   g.fb = fb ? 1u : 0u;
+  {
+    // radix sort: the top window holds 253 - c (W - 1) bits (canonical
+    // scalars < l < 2^253), i.e. buckets < 2^top; spread them over all
+    // NC = B / 2^RS_FINE_BITS coarse bins (rs_fbits)
+    const int top = 253 - (int)(c * (g.W - 1)), lognc = (int)c - 1 - RS_FINE_BITS;
+    g.tfb = (top >= (int)c - 1 || lognc < 0) ? RS_FINE_BITS : (uint32_t)std::max(0, top - lognc);
+    for (int i = 0; i < 8; ++i) g.K[i] = 0;
+    for (uint32_t w = 0; w + 1 < g.W; ++w) {  // bit c w + c - 1 (< 256)
+      const uint32_t pos = c * w + c - 1;
+      g.K[pos >> 5] |= 1u << (pos & 31);
+    }
+  }
   const size_t nseg = fb ? (size_t)M : (size_t)M * Wn;
   const size_t NB = nseg * g.B;
   void *cnt, *cur, *boff, *entries, *bsum, *wsum;
@@ -125,7 +137,7 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
                          g, nchunk, NC, (const uint32_t*)offA, (uint32_t*)tmpA);
       hipLaunchKernelGGL(k_rsort_fine, dim3(Wn * NC), dim3(RS_FT), 0, ctx->stream, (const uint32_t*)tmpA, nchunk,
                          (const uint32_t*)offA, (uint32_t*)boff, (uint32_t*)entries, (uint32_t*)boff + NB,
-                         (const uint32_t*)offA + nA);
+                         (const uint32_t*)offA + nA, g, NC);
     }
     BPP_TRY(ctx_check_launch(ctx, "k_rsort_scatter/fine"));
   } else if (lds_sort && T) {

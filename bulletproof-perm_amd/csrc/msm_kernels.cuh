@@ -74,6 +74,9 @@ struct MsmGeom {
   uint32_t fb;      // fixed-base mode: point idx -> idx*W + w in a table of
                     // precomputed 2^(c*w) multiples; all windows of an MSM
                     // share one bucket set (no Horner combine)
+  uint32_t K[8];     // sum_{w < W-1} 2^(c-1) 2^(cw), little-endian words (rs_signed_digit)
+  uint32_t tfb = 7;  // radix sort: fine bits of the top window (RS_FINE_BITS
+                    // unless it is narrow: see rs_fbits)
 };
 
 // Signed digit loop: calls f(w - wb, digit) for every window in
@@ -581,6 +584,22 @@ __global__ void __launch_bounds__(SORT_T) k_msm_scatter_lds(const dig_t* __restr
 #define RS_CHUNK 4096  // digits per block in the coarse passes (LDS staging)
 #define RS_FMASK (0x7fu << 24)
 
+// Fine bits of window ww of a launch.  Bucket b of a window sorts into
+// coarse bin b >> fbits and fine slot b & (2^fbits - 1).  The top window of
+// a 253-bit scalar holds fewer bits than the others (13 at c = 16: buckets
+// < 2^13, not 2^15), so with 7 fine bits it would fill only 64 of the 256
+// coarse bins, each 4x as dense: at 2^23 terms (one rank's share of the
+// N = 8 window split) its bins exceed the fine sort's one-tile capacity 16x
+// and serialise in the multi-tile path.  Its fine bits are therefore
+// g.tfb = top bits - log2(NC) (5 at c = 16), spreading it over all coarse
+// bins; its buckets at and above NC << tfb are empty (canonical scalars).
+FE_INLINE uint32_t rs_fbits(const MsmGeom& g, uint32_t ww) {
+  return g.wb + ww + 1 == g.W ? g.tfb : RS_FINE_BITS;
+}
+// coarse bin of bucket b (clamped: a non-canonical device scalar gives a
+// wrong result, never an out-of-range bin)
+FE_INLINE uint32_t rs_bin(uint32_t b, uint32_t fbits, uint32_t NC) { return min(b >> fbits, NC - 1); }
+
 // Digits of a chunk are loaded into registers in one batch of independent
 // coalesced loads (RS_PER per thread) before any LDS atomic: a load-then-
 // atomic loop leaves each load's latency exposed.
@@ -602,7 +621,7 @@ __global__ void __launch_bounds__(RS_T) k_rsort_count(const dig_t* __restrict__ 
   rs_load_chunk(dig + (size_t)w * g.T, t0, t1, v);
   __syncthreads();
   _Pragma("unroll") for (uint32_t k = 0; k < RS_PER; ++k)
-    if (v[k] != DIG_ZERO) atomicAdd(&h[(v[k] & ~DIG_SIGN) >> RS_FINE_BITS], 1u);
+    if (v[k] != DIG_ZERO) atomicAdd(&h[rs_bin(v[k] & ~DIG_SIGN, rs_fbits(g, w), NC)], 1u);
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < NC; b += RS_T) cntA[((size_t)w * NC + b) * nchunk + ch] = h[b];
 }
@@ -634,24 +653,27 @@ __global__ void __launch_bounds__(RS_DC_T) k_rsort_digits_count(const uint32_t* 
     if (t >= g.T) continue;
     uint32_t s[8];
     load_scalar(scalars, t, s);
-    uint32_t carry = 0;
-    for (uint32_t w = 0; w < g.wb + g.Wn; ++w) {
-      const uint32_t v = scalar_bits_sel(s, w * g.c, g.c) + carry;
-      int d;
-      if (v >= half && w + 1 < g.W) {
-        d = (int)v - (int)(2 * half);
-        carry = 1;
-      } else {
-        d = (int)v;
-        carry = 0;
-      }
-      if (w < g.wb) continue;
-      const uint32_t ww = w - g.wb;
+    // Signed digits in closed form: with K = sum_{w < W-1} 2^(c-1) 2^(cw),
+    // digit w = ((s + K) >> cw mod 2^c) - 2^(c-1) below the top window and
+    // (s + K) >> c(W-1) at it -- the digits of the sequential recoding
+    // (v >= 2^(c-1) -> v - 2^c, carry 1), but a window costs O(1) instead of
+    // a carry walk from window 0 (the rank holding the top windows of a
+    // window-split MSM walked all W)
+    uint64_t acc = 0;
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) {
+      acc += (uint64_t)s[i] + g.K[i];
+      s[i] = (uint32_t)acc;
+      acc >>= 32;
+    }
+    for (uint32_t ww = 0; ww < g.Wn; ++ww) {
+      const uint32_t w = g.wb + ww;
+      const uint32_t v = scalar_bits_sel(s, w * g.c, g.c);
+      const int d = w + 1 < g.W ? (int)v - (int)half : (int)v;
       uint32_t code = DIG16_ZERO;
       if (d != 0) {
         const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u;
         code = b | (d < 0 ? 0x8000u : 0u);
-        atomicAdd(&h[ww * NC + (b >> RS_FINE_BITS)], 1u);
+        atomicAdd(&h[ww * NC + rs_bin(b, rs_fbits(g, ww), NC)], 1u);
       }
       dig[(size_t)ww * g.T + t] = (dig_t)code;
     }
@@ -693,13 +715,14 @@ __global__ void __launch_bounds__(RS_T) k_rsort_scatter(const dig_t* __restrict_
   __shared__ uint32_t stage[RS_CHUNK];
   __shared__ uint8_t sbin[RS_CHUNK];
   const uint32_t w = blockIdx.x / nchunk, ch = blockIdx.x % nchunk;
+  const uint32_t fbits = rs_fbits(g, w);
   for (uint32_t b = threadIdx.x; b < 256; b += RS_T) cnt[b] = 0;
   __syncthreads();
   const uint32_t t0 = ch * RS_CHUNK, t1 = min(t0 + RS_CHUNK, g.T);
   uint32_t v[RS_PER];
   rs_load_chunk(dig + (size_t)w * g.T, t0, t1, v);
   _Pragma("unroll") for (uint32_t k = 0; k < RS_PER; ++k)
-    if (v[k] != DIG_ZERO) atomicAdd(&cnt[(v[k] & ~DIG_SIGN) >> RS_FINE_BITS], 1u);
+    if (v[k] != DIG_ZERO) atomicAdd(&cnt[rs_bin(v[k] & ~DIG_SIGN, fbits, NC)], 1u);
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < 256; b += RS_T) {
     loc[b] = cnt[b];
@@ -714,9 +737,9 @@ __global__ void __launch_bounds__(RS_T) k_rsort_scatter(const dig_t* __restrict_
     const uint32_t code = v[k];
     if (code == DIG_ZERO) continue;
     const uint32_t t = t0 + k * RS_T + threadIdx.x;
-    const uint32_t b = code & ~DIG_SIGN, bin = b >> RS_FINE_BITS;
+    const uint32_t b = code & ~DIG_SIGN, bin = rs_bin(b, fbits, NC);
     const uint32_t p = atomicAdd(&cnt[bin], 1u);
-    stage[p] = (pidx ? pidx[t] : t) | ((b & (RS_FINE_N - 1)) << 24) | (code & DIG_SIGN);
+    stage[p] = (pidx ? pidx[t] : t) | (((b - (bin << fbits)) & (RS_FINE_N - 1)) << 24) | (code & DIG_SIGN);
     sbin[p] = (uint8_t)bin;
   }
   __syncthreads();
@@ -739,15 +762,24 @@ __global__ void __launch_bounds__(RS_T) k_rsort_scatter(const dig_t* __restrict_
 __global__ void __launch_bounds__(RS_FT) k_rsort_fine(const uint32_t* __restrict__ tmpA, uint32_t nchunk,
                                                     const uint32_t* __restrict__ offA, uint32_t* __restrict__ boff,
                                                     uint32_t* __restrict__ entries, uint32_t* __restrict__ end_dst,
-                                                    const uint32_t* __restrict__ end_src) {
+                                                    const uint32_t* __restrict__ end_src, MsmGeom g, uint32_t NC) {
   __shared__ uint32_t base[RS_FINE_N], lcnt[RS_FINE_N], lloc[RS_FINE_N];
   __shared__ uint32_t stage[RS_FTILE];
   __shared__ uint8_t sf[RS_FTILE];
-  // w * NC + coarse bin, last first: the top window's few dense bins take
-  // the multi-tile path and should not be the grid's tail
+  // w * NC + coarse bin, last first: the top window's dense bins (if any
+  // take the multi-tile path) should not be the grid's tail
   const uint32_t seg = gridDim.x - 1 - blockIdx.x;
   if (blockIdx.x == 0 && threadIdx.x == 0) *end_dst = *end_src;  // boff[NB] = number of entries
   const uint32_t s = offA[(size_t)seg * nchunk], e = offA[(size_t)(seg + 1) * nchunk];
+  // this segment's buckets: w * B + (coarse << fbits) + f, f < 2^fbits
+  const uint32_t w = seg / NC, coarse = seg % NC, fbits = rs_fbits(g, w);
+  const uint32_t nf = 1u << fbits;
+  uint32_t* const sboff = boff + (size_t)w * g.B + (coarse << fbits);
+  if (fbits < RS_FINE_BITS) {  // narrow top window: its buckets from NC << fbits up are empty
+    const uint32_t wend = offA[(size_t)(w + 1) * NC * nchunk];
+    const uint32_t lo = NC << fbits, per = (g.B - lo) / NC;
+    for (uint32_t j = threadIdx.x; j < per; j += RS_FT) boff[(size_t)w * g.B + lo + coarse * per + j] = wend;
+  }
   if (e - s <= RS_FTILE) {  // one tile, held in registers between the passes
     uint32_t v[RS_FPER];
     _Pragma("unroll") for (uint32_t k = 0; k < RS_FPER; ++k) {
@@ -765,7 +797,7 @@ __global__ void __launch_bounds__(RS_FT) k_rsort_fine(const uint32_t* __restrict
     __syncthreads();
     if (threadIdx.x < RS_FINE_N) {
       lcnt[threadIdx.x] = lloc[threadIdx.x];  // cursors
-      boff[(size_t)seg * RS_FINE_N + threadIdx.x] = s + lloc[threadIdx.x];
+      if (threadIdx.x < nf) sboff[threadIdx.x] = s + lloc[threadIdx.x];
     }
     __syncthreads();
     _Pragma("unroll") for (uint32_t k = 0; k < RS_FPER; ++k) {
@@ -787,7 +819,7 @@ __global__ void __launch_bounds__(RS_FT) k_rsort_fine(const uint32_t* __restrict
     __syncthreads();
     lds_excl_scan_w0(base, 2, s);
     __syncthreads();
-    if (threadIdx.x < RS_FINE_N) boff[(size_t)seg * RS_FINE_N + threadIdx.x] = base[threadIdx.x];
+    if (threadIdx.x < nf) sboff[threadIdx.x] = base[threadIdx.x];
   }
   for (uint32_t ts = s; ts < e || (one_tile && ts == s); ts += RS_FTILE) {
     const uint32_t te = min(ts + RS_FTILE, e);
@@ -803,7 +835,7 @@ __global__ void __launch_bounds__(RS_FT) k_rsort_fine(const uint32_t* __restrict
       lcnt[threadIdx.x] = lloc[threadIdx.x];  // cursors
       if (one_tile) {
         base[threadIdx.x] = s + lloc[threadIdx.x];
-        boff[(size_t)seg * RS_FINE_N + threadIdx.x] = s + lloc[threadIdx.x];
+        if (threadIdx.x < nf) sboff[threadIdx.x] = s + lloc[threadIdx.x];
       }
     }
     __syncthreads();

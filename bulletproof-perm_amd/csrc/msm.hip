@@ -206,7 +206,7 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
     BPP_TRY(ctx_check_launch(ctx, "k_msm_accumulate"));
     {
       ProfScope ps(ctx, "msm_fixup");
-      hipLaunchKernelGGL(k_msm_fixup_heavy, dim3((unsigned)max_heavy), dim3(64), 0, ctx->stream,
+      hipLaunchKernelGGL(k_msm_fixup_heavy, dim3((unsigned)std::min<size_t>(max_heavy, 4096)), dim3(64), 0, ctx->stream,
                          (const uint32_t*)boff, K, (const uint32_t*)head, (const uint32_t*)tail,
                          (const uint32_t*)heavy, (uint32_t*)bsum);
     }

@@ -178,7 +178,9 @@ FE_INLINE ge_niels fetch_entry_raw(const uint32_t* __restrict__ tbl, const uint3
 // of a narrow top window, equal scalars) is listed in heavy[1..] (count in
 // heavy[0]) by the lane where it starts and summed by a whole wave
 // (k_msm_fixup_heavy) instead of one lane's serial chain.
-#define FIX_MAX 16
+#ifndef FIX_MAX
+#define FIX_MAX 8
+#endif
 #define ACC_T 256
 
 // Balanced bucket accumulation: lane l owns entries [l*K, (l+1)*K) of the
@@ -976,15 +978,20 @@ __global__ void __launch_bounds__(64) k_msm_fixup_heavy(const uint32_t* __restri
                                                         const uint32_t* __restrict__ head,
                                                         const uint32_t* __restrict__ tail,
                                                         const uint32_t* __restrict__ heavy, uint32_t* __restrict__ bsum) {
-  if (blockIdx.x >= heavy[0]) return;
-  const uint32_t b = heavy[1 + blockIdx.x];
-  const uint32_t s = boff[b], e = boff[b + 1];
-  const uint32_t l0 = s / K, l1 = (e - 1) / K;
-  ge_p3 acc = ge_identity();
-  for (uint32_t p = threadIdx.x; p <= l1 - l0; p += 64) {
-    const ge_p3 piece = p ? load_p3(head, l0 + p) : (s == l0 * K ? load_p3(head, l0) : load_p3(tail, l0));
-    acc = ge_add(acc, piece);
+  // grid-stride over the listed buckets (the grid is sized for the worst
+  // case; most of it would otherwise be empty blocks)
+  for (uint32_t hb = blockIdx.x; hb < heavy[0]; hb += gridDim.x) {
+    const uint32_t b = heavy[1 + hb];
+    const uint32_t s = boff[b], e = boff[b + 1];
+    const uint32_t l0 = s / K, np = (e - 1) / K - l0 + 1;  // pieces
+    auto piece = [&](uint32_t p) {
+      return p ? load_p3(head, l0 + p) : (s == l0 * K ? load_p3(head, l0) : load_p3(tail, l0));
+    };
+    ge_p3 acc = threadIdx.x < np ? piece(threadIdx.x) : ge_identity();
+    for (uint32_t p = threadIdx.x + 64; p < np; p += 64) acc = ge_add(acc, piece(p));
+    // butterfly over the lanes that hold pieces only (np is wave-uniform):
+    // 4 levels for the 9-16 pieces of a top-window bucket at 2^22 terms
+    for (uint32_t k = 1; k < 64 && k < np; k <<= 1) acc = ge_add(acc, ge_shfl_xor(acc, k));
+    if (threadIdx.x == 0) store_p3(bsum, b, acc);
   }
-  _Pragma("unroll") for (int k = 1; k < 64; k <<= 1) acc = ge_add(acc, ge_shfl_xor(acc, k));
-  if (threadIdx.x == 0) store_p3(bsum, b, acc);
 }

@@ -920,7 +920,7 @@ __global__ void __launch_bounds__(NT) k_dt_msm(const uint32_t* __restrict__ dt, 
                                                const uint32_t* __restrict__ scalars,
                                                const uint32_t* __restrict__ pidx, const uint32_t* __restrict__ off,
                                                uint32_t* __restrict__ out_p3) {
-  __shared__ uint32_t lds[(NT / 64) * P3_WORDS];
+  __shared__ uint32_t tl[NT * P3_WORDS];  // 40 KB at NT = 256
   const uint32_t m = blockIdx.x;
   const uint32_t t0 = off[m], t1 = off[m + 1];
   const uint64_t E = (uint64_t)(t1 - t0) * dg.W;
@@ -939,17 +939,17 @@ __global__ void __launch_bounds__(NT) k_dt_msm(const uint32_t* __restrict__ dt, 
   uint32_t row;
   bool neg;
   while (it.next(row, neg)) acc = ge_madd_signed(acc, load_niels(dt, row), neg);
-  _Pragma("unroll") for (int k = 1; k < 64; k <<= 1) acc = ge_add(acc, ge_shfl_xor(acc, k));
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-  if (NT > 64) {
-    if (lane == 0) store_p3(lds, wave, acc);
+  // block tree in LDS whose waves retire as it narrows: 9 wave-additions
+  // per 256-lane block against 4 x 6 levels of a wave butterfly + 2, at the
+  // same depth (8 additions); measured +4 % proofs/s at 8 batches in flight,
+  // one batch 5.80 -> 5.60 ms
+  store_p3(tl, threadIdx.x, acc);
+  __syncthreads();
+  for (uint32_t s = NT / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) store_p3(tl, threadIdx.x, ge_add(load_p3(tl, threadIdx.x), load_p3(tl, threadIdx.x + s)));
     __syncthreads();
-    if (wave == 0) {
-      acc = lane < NT / 64 ? load_p3(lds, lane) : ge_identity();
-      _Pragma("unroll") for (int k = 1; k < NT / 64; k <<= 1) acc = ge_add(acc, ge_shfl_xor(acc, k));
-    }
   }
-  if (threadIdx.x == 0) store_p3(out_p3, m, acc);
+  if (threadIdx.x == 0) store_p3(out_p3, m, load_p3(tl, 0));
 }
 
 // Direct tables from the window tables (wt[k * 32 + u] = 2^(8u) P_k):

@@ -933,12 +933,28 @@ __global__ void __launch_bounds__(NT) k_dt_msm(const uint32_t* __restrict__ dt, 
   it.e1 = (uint32_t)(E * (threadIdx.x + 1) / NT);
   it.cur = 0xffffffffu;
   ge_p3 acc = ge_identity();
-  // (a software-pipelined gather measured slower: 233 VGPRs, no latency won)
+  // (an earlier software-pipelined gather that held a whole second row
+  // across the addition measured slower: 233 VGPRs)
   // (measured: the gathers cost ~4 % of this kernel and two interleaved
   // chains gain nothing; the add work and the block tree dominate)
   uint32_t row;
   bool neg;
-  while (it.next(row, neg)) acc = ge_madd_signed(acc, load_niels(dt, row), neg);
+  // software pipeline: the walk to the next digit and its row gather are
+  // issued between the halves of the current addition (145 VGPRs; measured
+  // +2-4 % proofs/s at 8 batches in flight, one batch 5.88 -> 5.55 ms)
+  if (it.next(row, neg)) {
+    ge_niels q = load_niels(dt, row);
+    for (;;) {
+      const ge_madd_mid mid = ge_madd_signed_h1(acc, q, neg);
+      uint32_t row2;
+      bool neg2;
+      const bool more = it.next(row2, neg2);
+      if (more) q = load_niels(dt, row2);
+      acc = ge_madd_h2(mid);
+      if (!more) break;
+      neg = neg2;
+    }
+  }
   // block tree in LDS whose waves retire as it narrows: 9 wave-additions
   // per 256-lane block against 4 x 6 levels of a wave butterfly + 2, at the
   // same depth (8 additions); measured +4 % proofs/s at 8 batches in flight,

@@ -197,7 +197,7 @@ def main():
     ap.add_argument("--proof-steps", type=int, default=16,
                     help="batches per stream (8 streams x 16 = 128 batches, ~0.25 s timed)")
     ap.add_argument("--proof-streams", type=int, default=8, help="proof batches in flight per GPU")
-    ap.add_argument("--inflight", type=int, default=2, help="independent MSMs in flight (1..4)")
+    ap.add_argument("--inflight", type=int, default=3, help="independent MSMs in flight (1..4)")
     ap.add_argument("--msm-split", choices=["windows", "points"], default="windows",
                     help="N>1: split the MSM's bucket windows (default) or its points over the ranks")
     args = ap.parse_args()
@@ -264,10 +264,11 @@ def main():
         return bpperm.partials_finish([g.cpu().numpy().tobytes() for g in gathered])
 
     def run_pipelined(k):
-        """k MSMs (alternating scalar vectors), two in flight: MSM i+1 is
-        submitted before MSM i is collected, so the device sorts i+1 beside
-        i's bucket reduction and the host combines i's windows (and, N > 1,
-        all-gathers its partial) while the device accumulates i+1."""
+        """k MSMs (alternating scalar vectors), --inflight of them in flight
+        (3 by default): MSM i+1 is submitted before MSM i is collected, so
+        the device sorts i+1 beside i's bucket reduction and the host
+        combines i's windows (and, N > 1, all-gathers its partial) while
+        the device accumulates i+1."""
         bufs = (d_sc, d_sc2)
         we_ = we if world > 1 else 0
         out, ticks = [], []

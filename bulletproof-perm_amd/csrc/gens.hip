@@ -56,7 +56,10 @@ FE_INLINE void radix16(const uint32_t s[8], int8_t e[64]) {
 // additions), then the 16 partial sums are combined with 4 xor-shuffle
 // levels.  A one-lane-per-commitment kernel would chain 128 additions (the
 // GPU's per-lane field-multiply latency is ~0.3 us, profiles/r01_felat.txt).
+#ifndef PED_G
 #define PED_G 16
+#endif
+#define PED_PER (FB_POS / PED_G)  // radix-16 digits per lane and scalar
 __global__ void __launch_bounds__(256) k_pedersen(const uint32_t* __restrict__ fb, const uint32_t* __restrict__ v,
                                                   const uint32_t* __restrict__ gam, size_t m,
                                                   uint32_t* __restrict__ out_p3) {
@@ -69,7 +72,7 @@ __global__ void __launch_bounds__(256) k_pedersen(const uint32_t* __restrict__ f
     int8_t e[64];
     _Pragma("unroll") for (int i = 0; i < 8; ++i) s[i] = v[8 * j + i];
     radix16(s, e);
-    for (uint32_t i = 4 * q; i < 4 * q + 4; ++i) {
+    for (uint32_t i = PED_PER * q; i < PED_PER * (q + 1); ++i) {
       const int d = e[i];
       if (d == 0) continue;
       const ge_niels t = load_niels(fb, i * 8 + (uint32_t)((d < 0 ? -d : d) - 1));
@@ -77,7 +80,7 @@ __global__ void __launch_bounds__(256) k_pedersen(const uint32_t* __restrict__ f
     }
     _Pragma("unroll") for (int i = 0; i < 8; ++i) s[i] = gam[8 * j + i];
     radix16(s, e);
-    for (uint32_t i = 4 * q; i < 4 * q + 4; ++i) {
+    for (uint32_t i = PED_PER * q; i < PED_PER * (q + 1); ++i) {
       const int d = e[i];
       if (d == 0) continue;
       const ge_niels t = load_niels(fb, FB_POS * 8 + i * 8 + (uint32_t)((d < 0 ? -d : d) - 1));

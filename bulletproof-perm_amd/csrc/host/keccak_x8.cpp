@@ -75,6 +75,13 @@ X8_TARGET static inline void keccak_x8_rounds(__m512i a[25]) {
   }
 }
 
+X8_TARGET static void keccak_x8_lanes(uint64_t lanes[25][8]) {
+  __m512i a[25];
+  for (int i = 0; i < 25; ++i) a[i] = _mm512_loadu_si512((const void*)lanes[i]);
+  keccak_x8_rounds(a);
+  for (int i = 0; i < 25; ++i) _mm512_storeu_si512((void*)lanes[i], a[i]);
+}
+
 // 8 SHAKE256 streams of `len` bytes each (len a multiple of 136 not needed),
 // inputs of one common length < 136 bytes.
 X8_TARGET void shake256_x8(const uint8_t* const in[8], size_t inlen, uint8_t* const out[8], size_t len) {
@@ -100,6 +107,21 @@ X8_TARGET void shake256_x8(const uint8_t* const in[8], size_t inlen, uint8_t* co
       memcpy(out[j] + pos, blk, k);
     }
   }
+}
+
+// Eight lane-interleaved states (lanes[i][j] = word i of state j) permuted
+// together (StrobeX8, merlin.h).
+void keccak_f1600_x8(uint64_t lanes[25][8]) {
+  if (!keccak_x8_available()) {
+    for (int j = 0; j < 8; ++j) {
+      uint64_t st[25];
+      for (int i = 0; i < 25; ++i) st[i] = lanes[i][j];
+      keccak_f1600(st);
+      for (int i = 0; i < 25; ++i) lanes[i][j] = st[i];
+    }
+    return;
+  }
+  keccak_x8_lanes(lanes);
 }
 
 }  // namespace merlin

@@ -22,6 +22,7 @@ static inline uint64_t rol(uint64_t x, int n) { return n ? (x << n) | (x >> (64 
 void keccak_f1600(uint64_t st[25]);
 // host/keccak_x8.cpp: eight states per AVX-512 permutation
 bool keccak_x8_available();
+void keccak_f1600_x8(uint64_t lanes[25][8]);  // lanes[i][j] = word i of state j
 void shake256_x8(const uint8_t* const in[8], size_t inlen, uint8_t* const out[8], size_t len);
 
 // SHAKE256 XOF (rate 136, domain 0x1F): bulletproofs' GeneratorsChain and
@@ -226,6 +227,101 @@ struct Transcript {
     uint8_t buf[64];
     challenge_bytes(label, buf, 64);
     return hsc::from_wide(buf);
+  }
+};
+
+// Eight transcripts in lockstep.  Proofs of one batch run the same
+// transcript operations with the same lengths, so their STROBE positions
+// agree and their permutations can run together on the 8-way Keccak:
+// load() takes 8 transcripts (equal positions), the ops below take one
+// message per instance, store() writes the states back.  Byte-identical to
+// running each Transcript alone.
+struct TranscriptX8 {
+  alignas(64) uint64_t L[25][8];
+  uint8_t pos = 0, pos_begin = 0, cur_flags = 0;
+
+  uint8_t& byte(int j, int k) { return reinterpret_cast<uint8_t*>(&L[k >> 3][j])[k & 7]; }
+  bool load(Transcript* const t[8]) {
+    for (int j = 0; j < 8; ++j) {
+      const Strobe128& s = t[j]->s;
+      if (s.pos != t[0]->s.pos || s.pos_begin != t[0]->s.pos_begin || s.cur_flags != t[0]->s.cur_flags) return false;
+      for (int i = 0; i < 25; ++i) memcpy(&L[i][j], s.st + 8 * i, 8);
+    }
+    pos = t[0]->s.pos;
+    pos_begin = t[0]->s.pos_begin;
+    cur_flags = t[0]->s.cur_flags;
+    return true;
+  }
+  void store(Transcript* const t[8]) {
+    for (int j = 0; j < 8; ++j) {
+      Strobe128& s = t[j]->s;
+      for (int i = 0; i < 25; ++i) memcpy(s.st + 8 * i, &L[i][j], 8);
+      s.pos = pos;
+      s.pos_begin = pos_begin;
+      s.cur_flags = cur_flags;
+    }
+  }
+  void run_f() {
+    for (int j = 0; j < 8; ++j) {
+      byte(j, pos) ^= pos_begin;
+      byte(j, pos + 1) ^= 0x04;
+      byte(j, STROBE_R + 1) ^= 0x80;
+    }
+    keccak_f1600_x8(L);
+    pos = 0;
+    pos_begin = 0;
+  }
+  // d[j] = instance j's bytes (stride 0 when `same`: one buffer for all)
+  void absorb(const uint8_t* const d[8], size_t n) {
+    for (size_t i = 0; i < n; ++i) {
+      for (int j = 0; j < 8; ++j) byte(j, pos) ^= d[j][i];
+      if (++pos == STROBE_R) run_f();
+    }
+  }
+  void absorb_same(const uint8_t* d, size_t n) {
+    const uint8_t* const dd[8] = {d, d, d, d, d, d, d, d};
+    absorb(dd, n);
+  }
+  void squeeze(uint8_t* const d[8], size_t n) {
+    for (size_t i = 0; i < n; ++i) {
+      for (int j = 0; j < 8; ++j) {
+        d[j][i] = byte(j, pos);
+        byte(j, pos) = 0;
+      }
+      if (++pos == STROBE_R) run_f();
+    }
+  }
+  void begin_op(uint8_t flags, bool more) {
+    if (more) return;
+    const uint8_t old_begin = pos_begin;
+    pos_begin = pos + 1;
+    cur_flags = flags;
+    const uint8_t hdr[2] = {old_begin, flags};
+    absorb_same(hdr, 2);
+    if ((flags & (FLAG_C | FLAG_K)) && pos != 0) run_f();
+  }
+  void meta_label_len(const char* label, uint32_t len) {
+    begin_op(FLAG_M | FLAG_A, false);
+    absorb_same((const uint8_t*)label, strlen(label));
+    uint8_t le[4];
+    memcpy(le, &len, 4);
+    absorb_same(le, 4);  // meta_ad(more = true)
+  }
+  void append(const char* label, const uint8_t* const msg[8], size_t n) {
+    meta_label_len(label, (uint32_t)n);
+    begin_op(FLAG_A, false);
+    absorb(msg, n);
+  }
+  void challenge_bytes(const char* label, uint8_t* const out[8], size_t n) {
+    meta_label_len(label, (uint32_t)n);
+    begin_op(FLAG_I | FLAG_A | FLAG_C, false);
+    squeeze(out, n);
+  }
+  void challenge_scalar(const char* label, hsc::Sc out[8]) {
+    uint8_t buf[8][64];
+    uint8_t* const o[8] = {buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], buf[6], buf[7]};
+    challenge_bytes(label, o, 64);
+    for (int j = 0; j < 8; ++j) out[j] = hsc::from_wide(buf[j]);
   }
 };
 

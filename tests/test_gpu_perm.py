@@ -91,9 +91,9 @@ def test_prove_batch_lockstep_bit_exact(gens):
         assert pf == want.to_bytes()
         assert V == b"".join(want.V)
     pr52 = bpperm.PermProver(gens, 52)
-    seeds = list(range(100, 140))
+    seeds = list(range(100, 141))  # 5 lockstep transcript groups of 8 + a tail of 1
     proofs, Vs = pr52.prove_batch(seeds)
-    for i in (0, 17, 39):
+    for i in (0, 17, 39, 40):
         pf, V, _ = pr52.prove(seeds[i])
         assert proofs[i] == pf and Vs[i] == b"".join(V)
     assert pr52.verify_batch(proofs, Vs)

@@ -186,7 +186,7 @@ def bench_proofs(ctx, args, world, rank, torch, dist, cdev="cuda"):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--log2n", type=int, default=20, help="pairs per GPU = 2^log2n")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)

@@ -21,6 +21,57 @@
 
 static unsigned grid_for(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
+// Pedersen commitments over the generators' radix-256 direct tables
+// (gens_points; row (gen * 32 + w) * 128 + |d| - 1 = d 2^(8w) gen): a
+// commitment v B + gamma B~ is a 2-term MSM over gens 2n and 2n + 1.  Eight
+// lanes per commitment, lane q owns windows [4q, 4q + 4) of both scalars =
+// byte lanes of word q of s + K (closed-form signed digits, K = 128 in bytes
+// 0..30): at most 8 table additions (a V commitment's v < 64 has one), then
+// a 3-level butterfly -- against 16 lanes x (4 radix-16 additions + 4
+// butterfly levels) in k_pedersen.
+#define PEDDT_G 8
+__global__ void __launch_bounds__(256) k_pedersen_dt(const uint32_t* __restrict__ dt, uint32_t gb,
+                                                     const uint32_t* __restrict__ v, const uint32_t* __restrict__ gam,
+                                                     size_t m, uint32_t* __restrict__ out_p3) {
+  const size_t gt = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t j = gt / PEDDT_G;
+  const uint32_t q = (uint32_t)(gt % PEDDT_G);
+  ge_p3 acc = ge_identity();
+  if (j < m) {
+    for (uint32_t which = 0; which < 2; ++which) {
+      const uint32_t* sp = (which ? gam : v) + 8 * j;
+      uint32_t s[8];
+      uint64_t c = 0;
+      _Pragma("unroll") for (int i = 0; i < 8; ++i) {
+        c += (uint64_t)sp[i] + (i < 7 ? 0x80808080u : 0x00808080u);
+        s[i] = (uint32_t)c;
+        c >>= 32;
+      }
+      uint32_t word = 0;  // s[q] by selects (a runtime index would go to scratch)
+      _Pragma("unroll") for (uint32_t i = 0; i < 8; ++i) word = q == i ? s[i] : word;
+      const uint32_t gen = gb + which;
+      _Pragma("unroll") for (uint32_t b = 0; b < 4; ++b) {
+        const uint32_t w = 4 * q + b, byte = (word >> (8 * b)) & 0xffu;
+        const int d = w < 31 ? (int)byte - 128 : (int)byte;
+        if (d == 0) continue;
+        const uint32_t row = (gen * 32u + w) * 128u + (uint32_t)((d < 0 ? -d : d) - 1);
+        acc = ge_madd_signed(acc, load_niels(dt, row), d < 0);
+      }
+    }
+  }
+  _Pragma("unroll") for (int off = 1; off < PEDDT_G; off <<= 1) {
+    ge_p3 o;
+    _Pragma("unroll") for (int i = 0; i < FE_LIMBS; ++i) {
+      o.X.v[i] = __shfl_xor(acc.X.v[i], off, 64);
+      o.Y.v[i] = __shfl_xor(acc.Y.v[i], off, 64);
+      o.Z.v[i] = __shfl_xor(acc.Z.v[i], off, 64);
+      o.T.v[i] = __shfl_xor(acc.T.v[i], off, 64);
+    }
+    acc = ge_add(acc, o);
+  }
+  if (j < m && q == 0) store_p3(out_p3, j, acc);
+}
+
 // declared in points.hip
 __global__ void k_decompress(const uint32_t* __restrict__ enc, size_t n, uint32_t* __restrict__ tbl,
                              unsigned long long* __restrict__ bad);
@@ -138,10 +189,21 @@ int pedersen_dev(bpp_ctx* ctx, const bpp_gens* g, const uint32_t* d_v, const uin
     BPP_TRY(ctx_ws(ctx, "ped_p3", m * P3_BYTES, &w));
     p3 = (uint32_t*)w;
   }
+  // BPP_PED_DT=1: commit over the radix-256 direct tables (k_pedersen_dt).
+  // Half the table additions, but measured slower with 8 proof batches in
+  // flight (68-79 K vs 80-82 K proofs/s; equal one batch at a time): its
+  // 1 MB of B / B~ rows compete in L2 with the concurrent direct-table MSMs,
+  // while k_pedersen's 128 KB radix-16 table stays resident.
+  MsmPoints pts;
+  const bool use_dt = getenv("BPP_PED_DT") && gens_points(ctx, g, &pts) == BPP_OK && pts.dt && pts.dt_c == 8;
   {
     ProfScope ps(ctx, "pedersen");
-    hipLaunchKernelGGL(k_pedersen, dim3(grid_for(m * PED_G, 256)), dim3(256), 0, ctx->stream, g->d_fb, d_v, d_gam, m,
-                       p3);
+    if (use_dt)
+      hipLaunchKernelGGL(k_pedersen_dt, dim3(grid_for(m * PEDDT_G, 256)), dim3(256), 0, ctx->stream, pts.dt,
+                         g->bidx(), d_v, d_gam, m, p3);
+    else
+      hipLaunchKernelGGL(k_pedersen, dim3(grid_for(m * PED_G, 256)), dim3(256), 0, ctx->stream, g->d_fb, d_v, d_gam,
+                         m, p3);
   }
   BPP_TRY(ctx_check_launch(ctx, "k_pedersen"));
   if (d_out_enc) {

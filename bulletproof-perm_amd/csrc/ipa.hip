@@ -44,7 +44,9 @@ __global__ void __launch_bounds__(256) k_ipa_init(uint32_t n, uint32_t P, const 
 }
 
 // terms of L at [0, n+1), of R at [n+1, 2n+2) of each instance; slots n and
-// 2n+1 (Q) are written by k_ipa_cross_final.
+// 2n+1 (Q) are written by k_ipa_cross_final.  Both write HALF the term
+// scalars: the round's MSMs give L/2, R/2, encoded as L = 2 (L/2) on the host
+// (msm_multi_enc), so no separate halving pass over the term array.
 __global__ void __launch_bounds__(256) k_ipa_terms(uint32_t n, uint32_t lg_n, uint32_t P, uint32_t m, uint32_t lg_h,
                                                   const uint32_t* __restrict__ am, const uint32_t* __restrict__ bm,
                                                   const uint32_t* __restrict__ fG, const uint32_t* __restrict__ fH,
@@ -65,8 +67,8 @@ __global__ void __launch_bounds__(256) k_ipa_terms(uint32_t n, uint32_t lg_n, ui
   const size_t tb = inst * (2 * (size_t)n + 2);
   const size_t posG = tb + (hi ? cidx : (n + 1) + cidx);
   const size_t posH = tb + (hi ? (n + 1) + (n >> 1) + cidx : (n >> 1) + cidx);
-  sc_store(scal + 8 * posG, sG);
-  sc_store(scal + 8 * posH, sH);
+  sc_store(scal + 8 * posG, sc_half(sG));
+  sc_store(scal + 8 * posH, sc_half(sH));
   pidx[posG] = gbase + k;
   pidx[posH] = hbase + k;
 }
@@ -124,8 +126,8 @@ __global__ void __launch_bounds__(64) k_ipa_cross_final(uint32_t nblk, uint32_t 
   // Montgomery c * canonical qmul -> canonical c*qmul
   const sc q = sc_load(qmul + 8 * inst);
   const size_t tb = (size_t)inst * (2 * (size_t)n + 2);
-  sc_store(scal + 8 * (tb + n), sc_mont(sl, q));
-  sc_store(scal + 8 * (tb + 2 * n + 1), sc_mont(sr, q));
+  sc_store(scal + 8 * (tb + n), sc_half(sc_mont(sl, q)));
+  sc_store(scal + 8 * (tb + 2 * n + 1), sc_half(sc_mont(sr, q)));
   pidx[tb + n] = qidx;
   pidx[tb + 2 * n + 1] = qidx;
 }
@@ -236,8 +238,8 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
     BPP_TRY(ctx_check_launch(ctx, "ipa round kernels"));
     {
       HostScope hs(ctx, "ipa_msm");
-      // L/2, R/2 from halved term scalars, encoded as L, R (msm_multi_enc)
-      BPP_TRY(sc_halve_dev(ctx, (const uint32_t*)scal, (uint32_t*)scal, PT));
+      // L/2, R/2 from the halved term scalars (k_ipa_terms, k_ipa_cross_final),
+      // encoded as L, R (msm_multi_enc)
       BPP_TRY(msm_multi_enc(ctx, (const uint32_t*)scal, (const uint32_t*)pidx, off, g.pts, enc.data(), true));
     }
     HostScope hs(ctx, "ipa_host");

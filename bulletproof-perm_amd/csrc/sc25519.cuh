@@ -96,6 +96,21 @@ FE_INLINE sc sc_mont(const sc& a, const sc& b) {
   return r;
 }
 
+// a / 2 mod l for canonical a: (a + (a odd ? l : 0)) >> 1 (a + l < 2^254)
+FE_INLINE sc sc_half(const sc& a) {
+  const uint32_t odd = a.v[0] & 1u;
+  sc r;
+  uint64_t c = 0;
+  _Pragma("unroll") for (int k = 0; k < 8; ++k) {
+    c += (uint64_t)a.v[k] + (odd ? SC_L[k] : 0u);
+    r.v[k] = (uint32_t)c;
+    c >>= 32;
+  }
+  _Pragma("unroll") for (int k = 0; k < 7; ++k) r.v[k] = (r.v[k] >> 1) | (r.v[k + 1] << 31);
+  r.v[7] >>= 1;
+  return r;
+}
+
 FE_INLINE sc sc_load(const uint32_t* p) {
   const uint4* q = reinterpret_cast<const uint4*>(p);
   uint4 a = q[0], b = q[1];

@@ -56,7 +56,7 @@ FE_INLINE ge_p3 ge_madd(const ge_p3& p, const ge_niels& q) {
   ge_p3 r;
   r.X = fe_mul(E, F);
   r.Y = fe_mul(G, H);
-  r.Z = fe_mul(F, G);
+  r.Z = fe_mul(G, F);  // F as the second operand in X and Z: its 19x limbs are shared
   r.T = fe_mul(E, H);
   return r;
 }
@@ -74,7 +74,7 @@ FE_INLINE ge_p3 ge_msub(const ge_p3& p, const ge_niels& q) {
   ge_p3 r;
   r.X = fe_mul(E, F);
   r.Y = fe_mul(G, H);
-  r.Z = fe_mul(F, G);
+  r.Z = fe_mul(G, F);  // F as the second operand in X and Z: its 19x limbs are shared
   r.T = fe_mul(E, H);
   return r;
 }
@@ -105,7 +105,7 @@ FE_INLINE ge_p3 ge_madd_signed(const ge_p3& p, const ge_niels& q, bool neg) {
   ge_p3 r;
   r.X = fe_mul(E, F);
   r.Y = fe_mul(G, H);
-  r.Z = fe_mul(F, G);
+  r.Z = fe_mul(G, F);  // F as the second operand in X and Z: its 19x limbs are shared
   r.T = fe_mul(E, H);
   return r;
 }
@@ -140,7 +140,7 @@ FE_INLINE ge_p3 ge_madd_h2(const ge_madd_mid& m) {
   ge_p3 r;
   r.X = fe_mul(m.E, m.F);
   r.Y = fe_mul(m.G, m.H);
-  r.Z = fe_mul(m.F, m.G);
+  r.Z = fe_mul(m.G, m.F);  // F second in X and Z: its 19x limbs are shared
   r.T = fe_mul(m.E, m.H);
   return r;
 }
@@ -177,7 +177,7 @@ FE_INLINE ge_p3 ge_add_cached(const ge_p3& p, const ge_cached& q) {
   ge_p3 r;
   r.X = fe_mul(E, F);
   r.Y = fe_mul(G, H);
-  r.Z = fe_mul(F, G);
+  r.Z = fe_mul(G, F);  // F as the second operand in X and Z: its 19x limbs are shared
   r.T = fe_mul(E, H);
   return r;
 }

@@ -119,7 +119,8 @@ int upload_sc(bpp_ctx* ctx, const std::vector<Sc>& v, const char* name, uint32_t
 int pedersen_host(bpp_ctx* ctx, const bpp_gens* g, const std::vector<Sc>& v, const std::vector<Sc>& gam,
                   std::vector<Enc32>& out) {
   const size_t m = v.size();
-  const bool doubled = m <= PED_DOUBLE_MAX;
+  static const size_t dmax = getenv("BPP_PED_DOUBLE_MAX") ? (size_t)atol(getenv("BPP_PED_DOUBLE_MAX")) : PED_DOUBLE_MAX;
+  const bool doubled = m <= dmax;
   uint32_t *d_v, *d_g;
   {
     HostScope hs(ctx, "ped_upload");

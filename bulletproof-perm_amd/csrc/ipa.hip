@@ -51,9 +51,9 @@ __global__ void __launch_bounds__(256) k_ipa_terms(uint32_t n, uint32_t lg_n, ui
                                                   const uint32_t* __restrict__ am, const uint32_t* __restrict__ bm,
                                                   const uint32_t* __restrict__ fG, const uint32_t* __restrict__ fH,
                                                   uint32_t gbase, uint32_t hbase, uint32_t* __restrict__ scal,
-                                                  uint32_t* __restrict__ pidx) {
+                                                  uint32_t* __restrict__ pidx, uint32_t* __restrict__ part) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (size_t)n * P) return;
+  if (t >= (size_t)n * P) return;  // (n >= 64 when part is set: whole waves leave)
   const size_t inst = t >> lg_n;
   const uint32_t k = (uint32_t)(t & (n - 1));
   const uint32_t h = m >> 1;
@@ -71,6 +71,25 @@ __global__ void __launch_bounds__(256) k_ipa_terms(uint32_t n, uint32_t lg_n, ui
   sc_store(scal + 8 * posH, sc_half(sH));
   pidx[posG] = gbase + k;
   pidx[posH] = hbase + k;
+  if (part) {
+    // fused cross products (n >= 64, so a wave lies in one instance): lane k
+    // < h adds a_k b_{k+h} to c_L and a_{k+h} b_k to c_R; one partial per
+    // wave -> part[inst][k / 64], summed by k_ipa_cross_final
+    sc cl = sc_zero(), cr = sc_zero();
+    if (k < h) {
+      const sc a0 = sc_load(am + 8 * (ib + k)), a1 = sc_load(am + 8 * (ib + k + h));
+      const sc b0 = sc_load(bm + 8 * (ib + k)), b1 = sc_load(bm + 8 * (ib + k + h));
+      cl = sc_mont(a0, b1);
+      cr = sc_mont(a1, b0);
+    }
+    cl = sc_wave_sum(cl);
+    cr = sc_wave_sum(cr);
+    if ((threadIdx.x & 63u) == 0) {
+      const size_t o = 16 * (inst * (size_t)(n >> 6) + (k >> 6));
+      sc_store(part + o, cl);
+      sc_store(part + o + 8, cr);
+    }
+  }
 }
 
 // grid (nb, P): block x of instance y sums its stride of
@@ -199,7 +218,10 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
   const uint32_t cross_blocks =
       std::max<uint32_t>(1, std::min<uint32_t>({64u, grid_for(std::max<uint32_t>(n / 2, 1), CROSS_T),
                                                  std::max<uint32_t>(1, 512 / P)}));
-  BPP_TRY(ctx_ws(ctx, "ipa_part", (size_t)P * cross_blocks * 64, &part));
+  // cross products fused into k_ipa_terms (one partial per wave) when every
+  // wave lies in one instance; k_ipa_cross otherwise
+  const bool fuse_cross = n >= 64 && !getenv("BPP_IPA_CROSS");
+  BPP_TRY(ctx_ws(ctx, "ipa_part", (size_t)P * std::max<uint32_t>(cross_blocks, n / 64) * 64, &part));
   {
     std::vector<uint32_t> qw((size_t)P * 8);
     for (uint32_t p = 0; p < P; ++p) {
@@ -228,10 +250,13 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
       ProfScope ps(ctx, "ipa_terms");
       hipLaunchKernelGGL(k_ipa_terms, dim3(grid_for(PN, 256)), dim3(256), 0, ctx->stream, n, lg_n, P, m, lg_h,
                          (const uint32_t*)am, (const uint32_t*)bm, (const uint32_t*)fG, (const uint32_t*)fH, g.gbase,
-                         g.hbase, (uint32_t*)scal, (uint32_t*)pidx);
-      const uint32_t nb = std::min<uint32_t>(cross_blocks, grid_for(h, CROSS_T));
-      hipLaunchKernelGGL(k_ipa_cross, dim3(nb, P), dim3(CROSS_T), 0, ctx->stream, n, h, (const uint32_t*)am,
-                         (const uint32_t*)bm, (uint32_t*)part);
+                         g.hbase, (uint32_t*)scal, (uint32_t*)pidx, fuse_cross ? (uint32_t*)part : nullptr);
+      uint32_t nb = n / 64;  // partials per instance (fused: one per wave)
+      if (!fuse_cross) {
+        nb = std::min<uint32_t>(cross_blocks, grid_for(h, CROSS_T));
+        hipLaunchKernelGGL(k_ipa_cross, dim3(nb, P), dim3(CROSS_T), 0, ctx->stream, n, h, (const uint32_t*)am,
+                           (const uint32_t*)bm, (uint32_t*)part);
+      }
       hipLaunchKernelGGL(k_ipa_cross_final, dim3(grid_for(P, 64)), dim3(64), 0, ctx->stream, nb, P,
                          (const uint32_t*)part, (const uint32_t*)d_q, g.qidx, n, (uint32_t*)scal, (uint32_t*)pidx);
     }

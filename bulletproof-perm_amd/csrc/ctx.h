@@ -56,6 +56,12 @@ struct bpp_ctx {
   // another MSM is in flight: 3 instead of 4 workgroups per CU, so the other
   // MSM's sort kernels run beside the accumulation)
   size_t acc_lds_pad = 0;
+  // contents of the "multi_off" workspace as last uploaded (msm.hip
+  // upload_offsets): the prover's IPA rounds pass the same MSM offsets every
+  // round, so an unchanged array skips its copy.  Cleared by any workspace
+  // reallocation (ctx_ws).
+  void* off_cache_ptr = nullptr;
+  std::vector<uint32_t> off_cache;
 };
 
 struct bpp_points {

@@ -22,6 +22,7 @@ static void stage_copy(void* dst, const void* src, size_t bytes) {
 int ctx_ws(bpp_ctx* ctx, const char* name, size_t bytes, void** out) {
   auto& b = ctx->ws[name];
   if (b.bytes < bytes) {
+    ctx->off_cache_ptr = nullptr;  // an address may be reused: forget cached contents
     if (b.p) BPP_HIP(hipFree(b.p));
     b.p = nullptr;
     b.bytes = 0;

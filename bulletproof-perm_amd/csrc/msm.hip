@@ -47,6 +47,19 @@ uint32_t msm_choose_c(double n_per_msm) {
 
 static unsigned grid_for(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
+// MSM offsets to the "multi_off" workspace, skipped when it already holds
+// exactly these (same stream, nothing else writes it; ctx.h off_cache)
+static int upload_offsets(bpp_ctx* ctx, const std::vector<uint32_t>& off, void** d_off) {
+  BPP_TRY(ctx_ws(ctx, "multi_off", off.size() * 4, d_off));
+  static const bool nocache = getenv("BPP_NO_OFF_CACHE") != nullptr;
+  if (nocache || *d_off != ctx->off_cache_ptr || off != ctx->off_cache) {
+    BPP_TRY(ctx_h2d(ctx, *d_off, off.data(), off.size() * 4));
+    ctx->off_cache_ptr = *d_off;
+    ctx->off_cache = off;
+  }
+  return BPP_OK;
+}
+
 int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const uint32_t* d_off, uint32_t M,
                uint32_t T, uint32_t c, uint32_t wb, uint32_t Wn, const uint32_t* d_tbl, uint32_t** d_wsum_out,
                const uint32_t* d_tbl1, uint32_t n0, bool fb, uint32_t* terms_out) {
@@ -687,8 +700,7 @@ static int msm_multi_dt_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t
   const uint32_t M = (uint32_t)off.size() - 1;
   const uint32_t T = off[M];
   void *d_off, *res;
-  BPP_TRY(ctx_ws(ctx, "multi_off", (M + 1) * 4, &d_off));
-  BPP_TRY(ctx_h2d(ctx, d_off, off.data(), (M + 1) * 4));
+  BPP_TRY(upload_offsets(ctx, off, &d_off));
   BPP_TRY(ctx_ws(ctx, "dt_res", (size_t)M * P3_BYTES, &res));
   const DtGeom dg = dt_geom(pts.dt_c);
   const double e_avg = (double)T * dg.W / (double)M;  // table additions per MSM
@@ -734,8 +746,7 @@ static int msm_multi_fb_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t
     return BPP_ERR_LEN;
   }
   void* d_off = nullptr;
-  BPP_TRY(ctx_ws(ctx, "multi_off", (M + 1) * 4, &d_off));
-  BPP_TRY(ctx_h2d(ctx, d_off, off.data(), (M + 1) * 4));
+  BPP_TRY(upload_offsets(ctx, off, &d_off));
   const uint32_t n0w = pts.n0 == 0xffffffffu ? 0xffffffffu : pts.n0 * FBW_W;
   return msm_engine(ctx, d_scal, d_pidx, (const uint32_t*)d_off, M, T, FBW_C, 0, FBW_W, pts.wt, d_res, pts.wt1, n0w,
                     true);
@@ -794,8 +805,7 @@ int msm_multi(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, cons
   out.assign(M, h25519::ge_identity());
   if (M == 0 || T == 0) return BPP_OK;
   void* d_off = nullptr;
-  BPP_TRY(ctx_ws(ctx, "multi_off", (M + 1) * 4, &d_off));
-  BPP_TRY(ctx_h2d(ctx, d_off, off.data(), (M + 1) * 4));
+  BPP_TRY(upload_offsets(ctx, off, &d_off));
   const uint32_t c = msm_choose_c((double)T / (double)M);
   const uint32_t W = (254 + c - 1) / c;
   uint32_t* d_ws = nullptr;

@@ -62,6 +62,9 @@ struct bpp_ctx {
   // reallocation (ctx_ws).
   void* off_cache_ptr = nullptr;
   std::vector<uint32_t> off_cache;
+  // ctx_h2d_const: per workspace name, the address and bytes last uploaded
+  // (cleared with off_cache on any workspace reallocation)
+  std::map<std::string, std::pair<void*, std::vector<uint8_t>>> h2d_cache;
 };
 
 struct bpp_points {
@@ -92,6 +95,10 @@ int ctx_pinned(bpp_ctx* ctx, size_t bytes, void** out);
 // hipMemcpyAsync measured up to ~25 ms on a 20 KB copy on the box); the host
 // buffer may be freed as soon as this returns.
 int ctx_h2d(bpp_ctx* ctx, void* d, const void* h, size_t bytes);
+// ctx_h2d that skips the copy when workspace `name` (at d) already holds
+// exactly these bytes: for arrays that repeat batch after batch (circuit
+// CSR, generator indices).  Only for workspaces no kernel writes.
+int ctx_h2d_const(bpp_ctx* ctx, const char* name, void* d, const void* h, size_t bytes);
 // Device->host copy through the arena; synchronous (stream synchronised).
 int ctx_d2h(bpp_ctx* ctx, void* h, const void* d, size_t bytes);
 // hipStreamSynchronize + recycle the upload arena.

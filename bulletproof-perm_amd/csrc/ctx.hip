@@ -23,6 +23,7 @@ int ctx_ws(bpp_ctx* ctx, const char* name, size_t bytes, void** out) {
   auto& b = ctx->ws[name];
   if (b.bytes < bytes) {
     ctx->off_cache_ptr = nullptr;  // an address may be reused: forget cached contents
+    ctx->h2d_cache.clear();
     if (b.p) BPP_HIP(hipFree(b.p));
     b.p = nullptr;
     b.bytes = 0;
@@ -76,6 +77,16 @@ int ctx_h2d(bpp_ctx* ctx, void* d, const void* h, size_t bytes) {
   BPP_TRY(stage_take(ctx, bytes, &p));
   stage_copy(p, h, bytes);
   BPP_HIP(hipMemcpyAsync(d, p, bytes, hipMemcpyHostToDevice, ctx->stream));
+  return BPP_OK;
+}
+
+int ctx_h2d_const(bpp_ctx* ctx, const char* name, void* d, const void* h, size_t bytes) {
+  static const bool nocache = getenv("BPP_NO_OFF_CACHE") != nullptr;
+  auto& e = ctx->h2d_cache[name];
+  if (!nocache && e.first == d && e.second.size() == bytes && !memcmp(e.second.data(), h, bytes)) return BPP_OK;
+  BPP_TRY(ctx_h2d(ctx, d, h, bytes));
+  e.first = d;
+  e.second.assign((const uint8_t*)h, (const uint8_t*)h + bytes);
   return BPP_OK;
 }
 

@@ -165,7 +165,7 @@ int msm_terms(bpp_ctx* ctx, const std::vector<Sc>& sc, const std::vector<uint32_
   BPP_TRY(upload_sc(ctx, sc, "mt_s", &d_s));
   void* d_i = nullptr;
   BPP_TRY(ctx_ws(ctx, "mt_i", idx.size() * 4 + 4, &d_i));
-  BPP_TRY(ctx_h2d(ctx, d_i, idx.data(), idx.size() * 4));
+  BPP_TRY(ctx_h2d_const(ctx, "mt_i", d_i, idx.data(), idx.size() * 4));
   return msm_multi(ctx, d_s, (const uint32_t*)d_i, off, pts, res);
 }
 
@@ -317,7 +317,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     BPP_TRY(upload_sc(ctx, sc, "mt_s", &d_s));
     void* d_i = nullptr;
     BPP_TRY(ctx_ws(ctx, "mt_i", idx.size() * 4 + 4, &d_i));
-    BPP_TRY(ctx_h2d(ctx, d_i, idx.data(), idx.size() * 4));
+    BPP_TRY(ctx_h2d_const(ctx, "mt_i", d_i, idx.data(), idx.size() * 4));  // generator indices: same every batch
     // MSMs of the halved scalars, encoded as 2 * result (msm_multi_enc)
     void* d_sh = nullptr;
     BPP_TRY(ctx_ws(ctx, "mt_s_half", sc.size() * 32 + 32, &d_sh));

@@ -181,8 +181,8 @@ int poly_coef_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint32
   BPP_TRY(ctx_ws(ctx, "poly_vec", (size_t)P * C.n_p * POLY_SLOTS * 32, &d_vec));
   BPP_TRY(ctx_ws(ctx, "poly_hf", (size_t)P * C.n_p * 32, &d_hf));
   BPP_TRY(ctx_ws(ctx, "poly_t", (size_t)P * 6 * 32, &d_t));
-  BPP_TRY(ctx_h2d(ctx, d_cp, cp.data(), cp.size() * 4));
-  BPP_TRY(ctx_h2d(ctx, d_ce, ce.data(), ce.size() * 4));
+  BPP_TRY(ctx_h2d_const(ctx, "poly_cp", d_cp, cp.data(), cp.size() * 4));  // the circuit: same every batch
+  BPP_TRY(ctx_h2d_const(ctx, "poly_ce", d_ce, ce.data(), ce.size() * 4));
   BPP_TRY(ctx_h2d(ctx, d_ch, ch.data(), ch.size() * 32));
   const unsigned nt = poly_block(C.n_p);
   const size_t lds = (size_t)C.Q * 32 + (POLY_T / 64) * 6 * 32;

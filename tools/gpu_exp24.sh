@@ -1,4 +1,4 @@
-# fused cross + cross-final in k_ipa_terms (default) vs separate kernels (BPP_IPA_CROSS=1)
+# (rejected) cross + cross-final both fused in k_ipa_terms ("cache") vs separate kernels ("upl", BPP_IPA_CROSS=1)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp

@@ -47,11 +47,6 @@ struct bpp_ctx {
   };
   MsmSlot msm_slot[BPP_MSM_INFLIGHT];
   uint64_t msm_next_ticket = 1;
-  hipEvent_t msm_acc_ev[BPP_MSM_INFLIGHT] = {};  // slot s's accumulation done
-  hipEvent_t msm_last_acc = nullptr;              // that of the last submitted MSM
-  // msm_engine hooks (set by bpp_msm_submit on a child): wait for acc_wait
-  // before the bucket accumulation, record acc_done after it
-  hipEvent_t acc_wait = nullptr, acc_done = nullptr;
   // extra dynamic LDS per accumulation workgroup (bpp_msm_submit sets it when
   // another MSM is in flight: 3 instead of 4 workgroups per CU, so the other
   // MSM's sort kernels run beside the accumulation)

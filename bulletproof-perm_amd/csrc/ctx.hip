@@ -81,9 +81,8 @@ int ctx_h2d(bpp_ctx* ctx, void* d, const void* h, size_t bytes) {
 }
 
 int ctx_h2d_const(bpp_ctx* ctx, const char* name, void* d, const void* h, size_t bytes) {
-  static const bool nocache = getenv("BPP_NO_OFF_CACHE") != nullptr;
   auto& e = ctx->h2d_cache[name];
-  if (!nocache && e.first == d && e.second.size() == bytes && !memcmp(e.second.data(), h, bytes)) return BPP_OK;
+  if (e.first == d && e.second.size() == bytes && !memcmp(e.second.data(), h, bytes)) return BPP_OK;
   BPP_TRY(ctx_h2d(ctx, d, h, bytes));
   e.first = d;
   e.second.assign((const uint8_t*)h, (const uint8_t*)h + bytes);
@@ -206,8 +205,6 @@ void bpp_ctx_destroy(bpp_ctx* ctx) {
   for (auto e : ctx->ev_pool) hipEventDestroy(e);
   for (auto& sl : ctx->msm_slot)
     if (sl.done) hipEventDestroy(sl.done);
-  for (auto e : ctx->msm_acc_ev)
-    if (e) hipEventDestroy(e);
   hipStreamDestroy(ctx->stream);
   delete ctx;
 }

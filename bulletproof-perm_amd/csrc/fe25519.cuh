@@ -29,20 +29,11 @@ struct fe {
 };
 
 #define MAD64(a, b, c) ((uint64_t)(uint32_t)(a) * (uint64_t)(uint32_t)(b) + (uint64_t)(c))
-#ifdef FE_MADC_ASM
-// Opaque v_mad_u64_u32 for the product-column chains (see tools/gen_fe10.py):
-// +5-7 % multiply throughput at 16 waves/SIMD, but the chain needs s_nop
-// wait states and a lone wave gets 25 % slower (tools/ubench/fe10bench).
-// Off by default: the compiler re-associates each column instead.
-FE_INLINE uint64_t fe_madc(uint32_t a, uint32_t b, uint64_t c) {
-  uint64_t d, unused;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(unused) : "v"(a), "v"(b), "v"(c));
-  return d;
-}
-#define MADC(a, b, c) fe_madc((a), (b), (c))
-#else
+// (an opaque inline-asm v_mad_u64_u32 for the column chains measured +5-7 %
+// multiply throughput at 16 waves/SIMD but 25 % slower on a lone wave, and
+// no gain in the MSM: not kept; the compiler re-associates
+// each column instead)
 #define MADC(a, b, c) MAD64(a, b, c)
-#endif
 #define FE_M26 0x3ffffffu
 #define FE_M25 0x1ffffffu
 

@@ -2,6 +2,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <mutex>
 #include <vector>
 
 #include "ctx.h"
@@ -9,7 +10,6 @@
 
 #define FB_POS 64  // radix-16 positions per fixed base
 #define GENS_DT_MAX 4096  // generators for which direct tables are kept (2 GB at the limit)
-#define GENS_DT16_MAX 320  // ... with 16-bit windows (20 GB at the limit)
 
 struct bpp_gens {
   bpp_ctx* ctx = nullptr;
@@ -18,12 +18,14 @@ struct bpp_gens {
   uint32_t* d_fb = nullptr;   // fixed-base tables for B and Bb: 2 x 64 x 8 Niels
   // window tables of every generator (FBW_W x 128 B each), built on first use
   mutable uint32_t* d_wt = nullptr;
-  // direct tables d * 2^(c w) * P, built on first use when 2n+2 <=
-  // GENS_DT_MAX: c = 8 (512 KB per generator, 32 table additions per
-  // scalar), or c = 16 with BPP_DT_C=16 up to GENS_DT16_MAX generators
-  // (64 MB per generator, 16 additions)
+  // direct tables d * 2^(8 w) * P, built on first use when 2n+2 <=
+  // GENS_DT_MAX (512 KB per generator, 32 table additions per scalar)
   mutable uint32_t* d_dt = nullptr;
   mutable uint32_t dt_c = 8;
+  // guards the first-use builds of d_wt / d_dt: contexts on other streams
+  // (bpp_perm_prove_batch sub-batches, callers sharing one gens across
+  // threads) may ask for the tables at the same time
+  mutable std::mutex build_mu;
   uint32_t gidx(size_t i) const { return (uint32_t)i; }
   uint32_t hidx(size_t i) const { return (uint32_t)(n + i); }
   uint32_t bidx() const { return (uint32_t)(2 * n); }

@@ -21,57 +21,6 @@
 
 static unsigned grid_for(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
-// Pedersen commitments over the generators' radix-256 direct tables
-// (gens_points; row (gen * 32 + w) * 128 + |d| - 1 = d 2^(8w) gen): a
-// commitment v B + gamma B~ is a 2-term MSM over gens 2n and 2n + 1.  Eight
-// lanes per commitment, lane q owns windows [4q, 4q + 4) of both scalars =
-// byte lanes of word q of s + K (closed-form signed digits, K = 128 in bytes
-// 0..30): at most 8 table additions (a V commitment's v < 64 has one), then
-// a 3-level butterfly -- against 16 lanes x (4 radix-16 additions + 4
-// butterfly levels) in k_pedersen.
-#define PEDDT_G 8
-__global__ void __launch_bounds__(256) k_pedersen_dt(const uint32_t* __restrict__ dt, uint32_t gb,
-                                                     const uint32_t* __restrict__ v, const uint32_t* __restrict__ gam,
-                                                     size_t m, uint32_t* __restrict__ out_p3) {
-  const size_t gt = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t j = gt / PEDDT_G;
-  const uint32_t q = (uint32_t)(gt % PEDDT_G);
-  ge_p3 acc = ge_identity();
-  if (j < m) {
-    for (uint32_t which = 0; which < 2; ++which) {
-      const uint32_t* sp = (which ? gam : v) + 8 * j;
-      uint32_t s[8];
-      uint64_t c = 0;
-      _Pragma("unroll") for (int i = 0; i < 8; ++i) {
-        c += (uint64_t)sp[i] + (i < 7 ? 0x80808080u : 0x00808080u);
-        s[i] = (uint32_t)c;
-        c >>= 32;
-      }
-      uint32_t word = 0;  // s[q] by selects (a runtime index would go to scratch)
-      _Pragma("unroll") for (uint32_t i = 0; i < 8; ++i) word = q == i ? s[i] : word;
-      const uint32_t gen = gb + which;
-      _Pragma("unroll") for (uint32_t b = 0; b < 4; ++b) {
-        const uint32_t w = 4 * q + b, byte = (word >> (8 * b)) & 0xffu;
-        const int d = w < 31 ? (int)byte - 128 : (int)byte;
-        if (d == 0) continue;
-        const uint32_t row = (gen * 32u + w) * 128u + (uint32_t)((d < 0 ? -d : d) - 1);
-        acc = ge_madd_signed(acc, load_niels(dt, row), d < 0);
-      }
-    }
-  }
-  _Pragma("unroll") for (int off = 1; off < PEDDT_G; off <<= 1) {
-    ge_p3 o;
-    _Pragma("unroll") for (int i = 0; i < FE_LIMBS; ++i) {
-      o.X.v[i] = __shfl_xor(acc.X.v[i], off, 64);
-      o.Y.v[i] = __shfl_xor(acc.Y.v[i], off, 64);
-      o.Z.v[i] = __shfl_xor(acc.Z.v[i], off, 64);
-      o.T.v[i] = __shfl_xor(acc.T.v[i], off, 64);
-    }
-    acc = ge_add(acc, o);
-  }
-  if (j < m && q == 0) store_p3(out_p3, j, acc);
-}
-
 // declared in points.hip
 __global__ void k_decompress(const uint32_t* __restrict__ enc, size_t n, uint32_t* __restrict__ tbl,
                              unsigned long long* __restrict__ bad);
@@ -89,27 +38,51 @@ __global__ void __launch_bounds__(64) k_fb_tables(const uint32_t* __restrict__ t
   store_niels(fb, t, ge_to_niels(acc));
 }
 
-FE_INLINE void radix16(const uint32_t s[8], int8_t e[64]) {
-  _Pragma("unroll") for (int i = 0; i < 8; ++i) {
-    _Pragma("unroll") for (int j = 0; j < 8; ++j) e[8 * i + j] = (int8_t)((s[i] >> (4 * j)) & 15u);
+// Bits [16q, 16q + 16) of s + K, K = 8 * sum_{i<63} 16^i: nibble i of s + K
+// minus 8 is signed radix-16 digit i of s (i < 63, digits in [-8, 8)) and
+// nibble 63 the top digit (s < 2^253: at most 2), the same digits as a
+// carry-propagating recoding, in closed form and without a data-dependent
+// index (the word is picked by selects).
+FE_INLINE uint32_t ped_digit_bits(const uint32_t* __restrict__ sp, uint32_t q) {
+  uint64_t c = 0;
+  uint32_t word = 0;
+  _Pragma("unroll") for (uint32_t i = 0; i < 8; ++i) {
+    c += (uint64_t)sp[i] + (i < 7 ? 0x88888888u : 0x08888888u);
+    word = (q >> 1) == i ? (uint32_t)c : word;
+    c >>= 32;
   }
-  int carry = 0;
-  _Pragma("unroll") for (int i = 0; i < 63; ++i) {
-    int v = e[i] + carry;
-    carry = (v + 8) >> 4;
-    e[i] = (int8_t)(v - (carry << 4));
-  }
-  e[63] = (int8_t)(e[63] + carry);
+  return (word >> (16 * (q & 1))) & 0xffffu;
 }
 
-// P_j = v_j * B + g_j * Bb, PED_G lanes per commitment: lane q adds the
-// table entries of radix-16 positions [4q, 4q+4) of both scalars (8 mixed
-// additions), then the 16 partial sums are combined with 4 xor-shuffle
-// levels.  A one-lane-per-commitment kernel would chain 128 additions (the
-// GPU's per-lane field-multiply latency is ~0.3 us, profiles/r01_felat.txt).
-#ifndef PED_G
+// Constant-time table lookup (dalek's LookupTable::select, which
+// PedersenGens::commit's constant-time multiscalar_mul uses): all eight
+// rows d * 16^pos * P (d = 1..8) are loaded and the one for |d| is kept by
+// masks; d = 0 keeps the Niels identity.  The loads and the instruction
+// stream do not depend on the digit.
+FE_INLINE ge_niels ped_select_ct(const uint32_t* __restrict__ fb, uint32_t row0, uint32_t ad) {
+  ge_niels r = ge_niels_identity();
+  _Pragma("unroll 2") for (uint32_t j = 1; j <= 8; ++j) {
+    const ge_niels t = load_niels(fb, row0 + j - 1);
+    const uint32_t mask = 0u - (uint32_t)(ad == j);
+    _Pragma("unroll") for (int i = 0; i < FE_LIMBS; ++i) {
+      r.ypx.v[i] ^= (r.ypx.v[i] ^ t.ypx.v[i]) & mask;
+      r.ymx.v[i] ^= (r.ymx.v[i] ^ t.ymx.v[i]) & mask;
+      r.xy2d.v[i] ^= (r.xy2d.v[i] ^ t.xy2d.v[i]) & mask;
+    }
+  }
+  return r;
+}
+
+// P_j = v_j * B + g_j * Bb (PedersenGens::commit, weights.rs:58-61), PED_G
+// lanes per commitment: lane q adds the table entries of radix-16 positions
+// [4q, 4q+4) of both scalars (always 8 mixed additions: no zero skip), then
+// the 16 partial sums are combined with 4 xor-shuffle levels.  Constant time
+// in v and gamma like the reference's commit: digits in closed form,
+// ped_select_ct over all eight rows, signs by operand selects
+// (ge_madd_signed).  A one-lane-per-commitment kernel would chain 128
+// additions (the GPU's per-lane field-multiply latency is ~0.3 us,
+// profiles/r01_felat.txt).
 #define PED_G 16
-#endif
 #define PED_PER (FB_POS / PED_G)  // radix-16 digits per lane and scalar
 __global__ void __launch_bounds__(256) k_pedersen(const uint32_t* __restrict__ fb, const uint32_t* __restrict__ v,
                                                   const uint32_t* __restrict__ gam, size_t m,
@@ -119,23 +92,17 @@ __global__ void __launch_bounds__(256) k_pedersen(const uint32_t* __restrict__ f
   const uint32_t q = (uint32_t)(gt % PED_G);
   ge_p3 acc = ge_identity();
   if (j < m) {
-    uint32_t s[8];
-    int8_t e[64];
-    _Pragma("unroll") for (int i = 0; i < 8; ++i) s[i] = v[8 * j + i];
-    radix16(s, e);
-    for (uint32_t i = PED_PER * q; i < PED_PER * (q + 1); ++i) {
-      const int d = e[i];
-      if (d == 0) continue;
-      const ge_niels t = load_niels(fb, i * 8 + (uint32_t)((d < 0 ? -d : d) - 1));
-      acc = ge_madd_signed(acc, t, d < 0);
-    }
-    _Pragma("unroll") for (int i = 0; i < 8; ++i) s[i] = gam[8 * j + i];
-    radix16(s, e);
-    for (uint32_t i = PED_PER * q; i < PED_PER * (q + 1); ++i) {
-      const int d = e[i];
-      if (d == 0) continue;
-      const ge_niels t = load_niels(fb, FB_POS * 8 + i * 8 + (uint32_t)((d < 0 ? -d : d) - 1));
-      acc = ge_madd_signed(acc, t, d < 0);
+    _Pragma("unroll 1") for (uint32_t which = 0; which < 2; ++which) {
+      const uint32_t bits = ped_digit_bits((which ? gam : v) + 8 * j, q);
+      _Pragma("unroll 1") for (uint32_t b = 0; b < PED_PER; ++b) {
+        const uint32_t pos = PED_PER * q + b;
+        const int nib = (int)((bits >> (4 * b)) & 15u);
+        const int d = pos < FB_POS - 1 ? nib - 8 : nib;
+        const int sg = d >> 31;  // 0 or -1
+        const uint32_t ad = (uint32_t)((d ^ sg) - sg);
+        const ge_niels t = ped_select_ct(fb, (which * FB_POS + pos) * 8, ad);
+        acc = ge_madd_signed(acc, t, sg != 0);
+      }
     }
   }
   _Pragma("unroll") for (int off = 1; off < PED_G; off <<= 1) {
@@ -189,21 +156,15 @@ int pedersen_dev(bpp_ctx* ctx, const bpp_gens* g, const uint32_t* d_v, const uin
     BPP_TRY(ctx_ws(ctx, "ped_p3", m * P3_BYTES, &w));
     p3 = (uint32_t*)w;
   }
-  // BPP_PED_DT=1: commit over the radix-256 direct tables (k_pedersen_dt).
-  // Half the table additions, but measured slower with 8 proof batches in
-  // flight (68-79 K vs 80-82 K proofs/s; equal one batch at a time): its
-  // 1 MB of B / B~ rows compete in L2 with the concurrent direct-table MSMs,
-  // while k_pedersen's 128 KB radix-16 table stays resident.
-  MsmPoints pts;
-  const bool use_dt = getenv("BPP_PED_DT") && gens_points(ctx, g, &pts) == BPP_OK && pts.dt && pts.dt_c == 8;
+  // (commitments as 2-term MSMs over B / B~'s radix-256 direct tables, 8
+  // lanes each, halve the table additions but measured slower with 8 proof
+  // batches in flight, 68-79 K vs 80-82 K proofs/s: their 1 MB of rows
+  // compete in L2 with the concurrent direct-table MSMs, while this kernel's
+  // 128 KB radix-16 table stays resident)
   {
     ProfScope ps(ctx, "pedersen");
-    if (use_dt)
-      hipLaunchKernelGGL(k_pedersen_dt, dim3(grid_for(m * PEDDT_G, 256)), dim3(256), 0, ctx->stream, pts.dt,
-                         g->bidx(), d_v, d_gam, m, p3);
-    else
-      hipLaunchKernelGGL(k_pedersen, dim3(grid_for(m * PED_G, 256)), dim3(256), 0, ctx->stream, g->d_fb, d_v, d_gam,
-                         m, p3);
+    hipLaunchKernelGGL(k_pedersen, dim3(grid_for(m * PED_G, 256)), dim3(256), 0, ctx->stream, g->d_fb, d_v, d_gam, m,
+                       p3);
   }
   BPP_TRY(ctx_check_launch(ctx, "k_pedersen"));
   if (d_out_enc) {
@@ -219,32 +180,43 @@ int pedersen_dev(bpp_ctx* ctx, const bpp_gens* g, const uint32_t* d_v, const uin
 
 int gens_points(bpp_ctx* ctx, const bpp_gens* g, MsmPoints* out) {
   const uint32_t np = (uint32_t)(2 * g->n + 2);
+  // First use builds the tables on this context's stream.  They are
+  // published only after that stream has finished them (hipStreamSynchronize),
+  // under the gens' lock, so a context on another stream never reads a
+  // half-built table and two first users cannot both build one.
+  std::lock_guard<std::mutex> lock(g->build_mu);
   if (!g->d_wt) {
     uint32_t* d = nullptr;
     if (hipMalloc(&d, (size_t)np * FBW_W * MSM_NIELS_WORDS * 4) != hipSuccess) {
       ctx->err = "hipMalloc generator window tables";
       return BPP_ERR_NOMEM;
     }
-    const int rc = fbw_build(ctx, g->d_tbl, np, d);
+    int rc = fbw_build(ctx, g->d_tbl, np, d);
+    if (!rc && hipStreamSynchronize(ctx->stream) != hipSuccess) {
+      ctx->err = "window-table build failed";
+      rc = BPP_ERR_DEVICE;
+    }
     if (rc) {
       hipFree(d);
       return rc;
     }
     g->d_wt = d;
   }
-  if (!g->d_dt && np <= GENS_DT_MAX && !getenv("BPP_NO_DT")) {
-    // c = 8 by default: 16-bit windows halve the table additions but
-    // measured no faster (0.94 vs 0.91 ms of direct-table time per
-    // 128-proof batch; 16.5 GB of tables gathered at random); BPP_DT_C=16
-    uint32_t c = 8;
-    if (const char* e = getenv("BPP_DT_C")) c = atoi(e) == 16 ? 16u : 8u;
-    if (c == 16 && np > GENS_DT16_MAX) c = 8;
+  if (!g->d_dt && np <= GENS_DT_MAX) {
+    // c = 8: 16-bit windows halve the table additions but measured no
+    // faster (0.94 vs 0.91 ms of direct-table time per 128-proof batch;
+    // 16.5 GB of tables gathered at random)
+    const uint32_t c = 8;
     uint32_t* d = nullptr;
     if (hipMalloc(&d, dt_bytes(np, c)) != hipSuccess) {
       ctx->err = "hipMalloc generator direct tables";
       return BPP_ERR_NOMEM;
     }
-    const int rc = dt_build(ctx, g->d_wt, np, c, d);
+    int rc = dt_build(ctx, g->d_wt, np, c, d);
+    if (!rc && hipStreamSynchronize(ctx->stream) != hipSuccess) {
+      ctx->err = "direct-table build failed";
+      rc = BPP_ERR_DEVICE;
+    }
     if (rc) {
       hipFree(d);
       return rc;

@@ -220,7 +220,7 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
                                                  std::max<uint32_t>(1, 512 / P)}));
   // cross products fused into k_ipa_terms (one partial per wave) when every
   // wave lies in one instance; k_ipa_cross otherwise
-  const bool fuse_cross = n >= 64 && !getenv("BPP_IPA_CROSS");
+  const bool fuse_cross = n >= 64;
   BPP_TRY(ctx_ws(ctx, "ipa_part", (size_t)P * std::max<uint32_t>(cross_blocks, n / 64) * 64, &part));
   {
     std::vector<uint32_t> qw((size_t)P * 8);

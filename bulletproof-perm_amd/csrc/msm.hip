@@ -39,9 +39,6 @@ uint32_t msm_choose_c(double n_per_msm) {
       best = c;
     }
   }
-  // BPP_MSM_C: window override for large single MSMs (A/B experiments)
-  if (const char* e = getenv("BPP_MSM_C"))
-    if (n_per_msm >= 65536.0) best = std::min(16u, std::max(12u, (uint32_t)atoi(e)));
   return best;
 }
 
@@ -51,8 +48,7 @@ static unsigned grid_for(size_t n, unsigned t) { return (unsigned)((n + t - 1) /
 // exactly these (same stream, nothing else writes it; ctx.h off_cache)
 static int upload_offsets(bpp_ctx* ctx, const std::vector<uint32_t>& off, void** d_off) {
   BPP_TRY(ctx_ws(ctx, "multi_off", off.size() * 4, d_off));
-  static const bool nocache = getenv("BPP_NO_OFF_CACHE") != nullptr;
-  if (nocache || *d_off != ctx->off_cache_ptr || off != ctx->off_cache) {
+  if (*d_off != ctx->off_cache_ptr || off != ctx->off_cache) {
     BPP_TRY(ctx_h2d(ctx, *d_off, off.data(), off.size() * 4));
     ctx->off_cache_ptr = *d_off;
     ctx->off_cache = off;
@@ -106,11 +102,6 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
   // head/tail pieces (2^20: K = 64 measured best of 32/64/128)
   uint32_t K = 4;
   while (K < 128 && E_max / (2 * K) >= 256u * 1024u) K <<= 1;
-  if (const char* ek = getenv("BPP_MSM_K")) {  // rounded down to a power of two >= 4
-    const uint32_t want = std::max(4, atoi(ek));
-    for (K = 4; K * 2 <= want; K *= 2) {
-    }
-  }
   const size_t lanes = (E_max + K - 1) / K + 1;
   uint32_t ks = 0;
   while ((1u << ks) < K) ++ks;
@@ -208,7 +199,6 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
   }
   {
     if (!radix_sort) BPP_HIP(hipMemsetAsync(heavy, 0, 4, ctx->stream));  // (radix: cleared by its first kernel)
-    if (ctx->acc_wait) BPP_HIP(hipStreamWaitEvent(ctx->stream, ctx->acc_wait, 0));
     {
       ProfScope ps(ctx, "msm_accumulate");
       hipLaunchKernelGGL(k_msm_accumulate, dim3(grid_for(lanes, ACC_T)), dim3(ACC_T), ctx->acc_lds_pad, ctx->stream,
@@ -224,9 +214,7 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
                          (const uint32_t*)heavy, (uint32_t*)bsum);
     }
     BPP_TRY(ctx_check_launch(ctx, "k_msm_fixup_heavy"));
-    if (ctx->acc_done) BPP_HIP(hipEventRecord(ctx->acc_done, ctx->stream));
-    if (terms_out && M == 1 && !fb && g.B >= (1u << RWAVE_SHIFT) && g.B <= (64u << RWAVE_SHIFT) &&
-        !getenv("BPP_MSM_OLD_REDUCE")) {
+    if (terms_out && M == 1 && !fb && g.B >= (1u << RWAVE_SHIFT) && g.B <= (64u << RWAVE_SHIFT)) {
       // power-of-two weights left to the host Horner (k_msm_reduce_wave)
       const uint32_t nw = g.B >> RWAVE_SHIFT;
       uint32_t J = 0;
@@ -262,11 +250,6 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
   return BPP_OK;
 }
 
-// Host Horner: sum_j 2^(c*(wb+j)) * ws[j], j < Wn.
-static h25519::ge horner_host(const uint32_t* ws_words, uint32_t Wn, uint32_t c, uint32_t wb) {
-  return horner_host_terms(ws_words, Wn, 1, c, wb);
-}
-
 // Window j = term 0 + sum_k 2^(RWAVE_SHIFT + k) term 1+k: one Horner pass
 // over all terms in descending bit position (the term offsets < c fall
 // between the doublings the window combine does anyway).
@@ -290,20 +273,6 @@ h25519::ge horner_host_terms(const uint32_t* ws_words, uint32_t Wn, uint32_t nte
   return acc;
 }
 
-// Window groups for one large MSM (msm_single_dev).  Default 1: at 2^20
-// the two-stream pipeline measured slower (G=2 1.38 ms, G=4 1.70 ms vs
-// 1.26 ms), since the reduce and fixup are latency-bound (their time does
-// not shrink with fewer windows) and run G times, and kernels sharing CUs
-// with the VALU-saturating accumulation lose issue slots to it.
-// BPP_MSM_GROUPS=G selects the pipeline.
-uint32_t msm_window_groups(size_t n, uint32_t c, uint32_t Wn, bool indexed) {
-  (void)n;
-  (void)c;
-  uint32_t G = 1;
-  if (const char* e = getenv("BPP_MSM_GROUPS")) G = indexed ? 1u : (uint32_t)std::max(1, atoi(e));
-  return std::max<uint32_t>(1, std::min(G, Wn));
-}
-
 // Single MSM over device scalars + resident table, windows [wb, wb+Wn).
 int msm_single_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const uint32_t* d_tbl, size_t n,
                    uint32_t c, uint32_t wb, uint32_t Wn, h25519::ge* out) {
@@ -311,59 +280,18 @@ int msm_single_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx,
     *out = h25519::ge_identity();
     return BPP_OK;
   }
+  // (window groups pipelined over two child streams measured slower: G = 2
+  // 1.38 ms, G = 4 1.70 ms vs 1.26 ms at 2^20 -- the reduce and fixup are
+  // latency-bound and would run G times)
+  uint32_t* d_ws = nullptr;
+  uint32_t nterms = 1;
+  BPP_TRY(msm_engine(ctx, d_scal, d_pidx, nullptr, 1, (uint32_t)n, c, wb, Wn, d_tbl, &d_ws, nullptr, 0xffffffffu,
+                     false, &nterms));
   void* h = nullptr;
-  BPP_TRY(ctx_pinned(ctx, (size_t)Wn * P3_BYTES, &h));
-  const uint32_t G = msm_window_groups(n, c, Wn, d_pidx != nullptr);
-  if (G <= 1) {
-    uint32_t* d_ws = nullptr;
-    uint32_t nterms = 1;
-    BPP_TRY(msm_engine(ctx, d_scal, d_pidx, nullptr, 1, (uint32_t)n, c, wb, Wn, d_tbl, &d_ws, nullptr, 0xffffffffu,
-                       false, &nterms));
-    if (nterms > 1) BPP_TRY(ctx_pinned(ctx, (size_t)Wn * nterms * P3_BYTES, &h));
-    BPP_HIP(hipMemcpyAsync(h, d_ws, (size_t)Wn * nterms * P3_BYTES, hipMemcpyDeviceToHost, ctx->stream));
-    BPP_HIP(hipStreamSynchronize(ctx->stream));
-    *out = horner_host_terms((const uint32_t*)h, Wn, nterms, c, wb);
-    return BPP_OK;
-  } else {
-    // Window groups on two child streams: the sort of group g+1 (HBM-bound)
-    // and the bucket reduction of group g-1 (latency-bound, few waves) run
-    // under the accumulation of group g (VALU-bound).  Each child has its
-    // own workspaces, so groups on the same stream simply queue.
-    const uint32_t per = (Wn + G - 1) / G;
-    hipEvent_t ready = nullptr;
-    BPP_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
-    BPP_HIP(hipEventRecord(ready, ctx->stream));
-    bpp_ctx* ch[2] = {nullptr, nullptr};
-    int rc = BPP_OK;
-    for (uint32_t g = 0, w0 = 0; g < G && w0 < Wn && rc == BPP_OK; ++g, w0 += per) {
-      const uint32_t wn = std::min(per, Wn - w0);
-      rc = ctx_child(ctx, g & 1, &ch[g & 1]);
-      if (rc) break;
-      bpp_ctx* cc = ch[g & 1];
-      cc->prof = ctx->prof;
-      if (hipStreamWaitEvent(cc->stream, ready, 0) != hipSuccess) {
-        rc = BPP_ERR_DEVICE;
-        break;
-      }
-      uint32_t* d_ws = nullptr;
-      rc = msm_engine(cc, d_scal, d_pidx, nullptr, 1, (uint32_t)n, c, wb + w0, wn, d_tbl, &d_ws);
-      if (rc) {
-        ctx->err = cc->err;
-        break;
-      }
-      if (hipMemcpyAsync((uint8_t*)h + (size_t)w0 * P3_BYTES, d_ws, (size_t)wn * P3_BYTES, hipMemcpyDeviceToHost,
-                         cc->stream) != hipSuccess)
-        rc = BPP_ERR_DEVICE;
-    }
-    for (bpp_ctx* cc : ch)
-      if (cc && hipStreamSynchronize(cc->stream) != hipSuccess && rc == BPP_OK) rc = BPP_ERR_DEVICE;
-    hipEventDestroy(ready);
-    if (rc) {
-      if (ctx->err.empty()) ctx->err = "window-group MSM launch failed";
-      return rc;
-    }
-  }
-  *out = horner_host((const uint32_t*)h, Wn, c, wb);
+  BPP_TRY(ctx_pinned(ctx, (size_t)Wn * nterms * P3_BYTES, &h));
+  BPP_HIP(hipMemcpyAsync(h, d_ws, (size_t)Wn * nterms * P3_BYTES, hipMemcpyDeviceToHost, ctx->stream));
+  BPP_HIP(hipStreamSynchronize(ctx->stream));
+  *out = horner_host_terms((const uint32_t*)h, Wn, nterms, c, wb);
   return BPP_OK;
 }
 
@@ -444,8 +372,7 @@ int bpp_msm_submit(bpp_ctx* ctx, const void* d_scalars, const bpp_points* tbl, s
   // would cost the accumulation ~8 % (BPP_ACC_LDS_PAD overrides the pad).
   bool others = false;
   for (size_t i = 0; i < BPP_MSM_INFLIGHT; ++i) others |= ctx->msm_slot[i].busy;
-  static const long pad_env = getenv("BPP_ACC_LDS_PAD") ? atol(getenv("BPP_ACC_LDS_PAD")) : -1;
-  ch->acc_lds_pad = others ? (pad_env >= 0 ? (size_t)pad_env : (size_t)13000) : 0;
+  ch->acc_lds_pad = others ? (size_t)13000 : 0;
   if (!sl.done) BPP_HIP(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
   // inputs written on ctx's stream before this call are visible to the child
   BPP_HIP(hipEventRecord(sl.done, ctx->stream));
@@ -455,22 +382,11 @@ int bpp_msm_submit(bpp_ctx* ctx, const void* d_scalars, const bpp_points* tbl, s
   sl.Wn = w_end - w_begin;
   sl.nterms = 1;
   if (n && sl.Wn) {
-    // accumulations run one after another (each fills every SIMD's VGPRs):
-    // this MSM's sort overlaps the previous one's accumulation, and its
-    // accumulation the previous one's bucket reduction and host combine
-    // (opt-in BPP_MSM_STAGGER=1; measured slower than letting in-flight MSMs
-    // share the device freely: 1.17 vs 1.04 ms per 2^20 MSM)
-    const bool stagger = getenv("BPP_MSM_STAGGER") != nullptr;
-    if (stagger) {
-      if (!ctx->msm_acc_ev[s]) BPP_HIP(hipEventCreateWithFlags(&ctx->msm_acc_ev[s], hipEventDisableTiming));
-      ch->acc_wait = ctx->msm_last_acc;
-      ch->acc_done = ctx->msm_acc_ev[s];
-    }
+    // (in-flight MSMs share the device freely: serialising their
+    // accumulations measured slower, 1.17 vs 1.04 ms per 2^20 MSM)
     uint32_t* d_ws = nullptr;
     const int rc = msm_engine(ch, (const uint32_t*)d_scalars, nullptr, nullptr, 1, (uint32_t)n, c, w_begin, sl.Wn,
                               tbl->d, &d_ws, nullptr, 0xffffffffu, false, &sl.nterms);
-    ch->acc_wait = ch->acc_done = nullptr;
-    if (stagger) ctx->msm_last_acc = rc == BPP_OK ? ctx->msm_acc_ev[s] : nullptr;
     if (rc) {
       ctx->err = ch->err;
       return rc;
@@ -501,9 +417,19 @@ int bpp_msm_collect(bpp_ctx* ctx, uint64_t ticket, uint8_t out[32], uint8_t part
     return BPP_ERR_ARG;
   }
   bpp_ctx::MsmSlot& sl = ctx->msm_slot[s];
-  sl.busy = false;
   BPP_HIP(hipSetDevice(ctx->device));
-  BPP_HIP(hipEventSynchronize(sl.done));
+  // the slot (its child stream and pinned buffer) is released only once the
+  // child's copies are known to be done; on a failed wait the child stream
+  // is drained before the slot can be reused
+  if (hipEventSynchronize(sl.done) != hipSuccess) {
+    bpp_ctx* ch = s < ctx->children.size() ? ctx->children[s] : nullptr;
+    if (ch) hipStreamSynchronize(ch->stream);
+    sl.busy = false;
+    sl.h = nullptr;
+    ctx->err = "bpp_msm_collect: device error while waiting for the MSM";
+    return BPP_ERR_DEVICE;
+  }
+  sl.busy = false;
   h25519::ge r = h25519::ge_identity();
   if (sl.h && sl.Wn) r = horner_host_terms((const uint32_t*)sl.h, sl.Wn, sl.nterms, sl.c, sl.wb);
   sl.h = nullptr;
@@ -707,8 +633,7 @@ static int msm_multi_dt_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t
   // 256 lanes per MSM measured best for the prover's batches (M = 256-384
   // MSMs: 0.99 ms of direct-table time per 128 proofs vs 1.10-1.20 at 512
   // and 1.42 at 128); 512 only when few large MSMs leave the chip empty
-  int nt = e_avg > 256 ? (M < 128 && e_avg > 2048 ? 512 : 256) : 64;
-  if (const char* e = getenv("BPP_DT_NT")) nt = atoi(e);
+  const int nt = e_avg > 256 ? (M < 128 && e_avg > 2048 ? 512 : 256) : 64;
   {
     ProfScope ps(ctx, "msm_direct");
     // (no 1024-thread variant: capped at 128 VGPRs it spills in the main loop)

@@ -18,8 +18,6 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
 // (k_msm_reduce_wave); *terms_out = terms per window (1 = plain sums).
 // Host Horner over such terms: sum_j 2^(c (wb + j)) * window_j.
 h25519::ge horner_host_terms(const uint32_t* ws_words, uint32_t Wn, uint32_t nterms, uint32_t c, uint32_t wb);
-// Window groups msm_single_dev pipelines over two child streams.
-uint32_t msm_window_groups(size_t n, uint32_t c, uint32_t Wn, bool indexed);
 int msm_single_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const uint32_t* d_tbl, size_t n,
                    uint32_t c, uint32_t wb, uint32_t Wn, h25519::ge* out);
 int upload_scalars(bpp_ctx* ctx, const uint8_t* scalars, size_t n, const char* name, uint32_t** d_out);

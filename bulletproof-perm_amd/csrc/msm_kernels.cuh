@@ -138,13 +138,9 @@ __global__ void k_msm_scatter(const uint32_t* __restrict__ scalars, const uint32
 
 // 4 waves per SIMD (<= 128 VGPRs; the LDS piece buffer also allows 4):
 // without the bound the post-barrier fold lifts the kernel to 187 VGPRs.
-#if defined(ACC_WAVES3)
-#define ACC_ATTR __attribute__((amdgpu_waves_per_eu(3, 8)))
-#elif defined(ACC_WAVES5)
-#define ACC_ATTR __attribute__((amdgpu_waves_per_eu(5, 8)))
-#else
+// (3 waves, with or without a software-pipelined row gather, measured equal
+// alone and slower in the pipelined stream: DESIGN.md §4)
 #define ACC_ATTR __attribute__((amdgpu_waves_per_eu(4, 8)))
-#endif
 
 // Largest b with boff[b] <= i (boff non-decreasing, boff[0] = 0, i < boff[nb]).
 FE_INLINE uint32_t bucket_of(const uint32_t* __restrict__ boff, uint32_t nb, uint32_t i) {
@@ -166,21 +162,11 @@ FE_INLINE ge_niels fetch_entry(const uint32_t* __restrict__ tbl, const uint32_t*
   return q;
 }
 
-// Table point of entry e without its sign (bit 31 is applied by the caller).
-FE_INLINE ge_niels fetch_entry_raw(const uint32_t* __restrict__ tbl, const uint32_t* __restrict__ tbl1, uint32_t n0,
-                                   uint32_t e) {
-  const uint32_t pi = e & 0x7fffffffu;
-  const bool lo = pi < n0;  // one load sequence from a selected base
-  return load_niels(lo ? tbl : tbl1, lo ? pi : pi - n0);
-}
-
 // A bucket spanning more than FIX_MAX chunks (bucket skew: the few buckets
 // of a narrow top window, equal scalars) is listed in heavy[1..] (count in
 // heavy[0]) by the lane where it starts and summed by a whole wave
 // (k_msm_fixup_heavy) instead of one lane's serial chain.
-#ifndef FIX_MAX
 #define FIX_MAX 8
-#endif
 #define ACC_T 256
 
 // Balanced bucket accumulation: lane l owns entries [l*K, (l+1)*K) of the
@@ -233,19 +219,10 @@ __global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_
     // loads touch the same 128-B line K times across a long loop and
     // re-fetch it once the table gathers have evicted it
     uint4 e4 = make_uint4(0, 0, 0, 0);
-#ifdef ACC_PREFETCH
-    // software pipeline: the next entry's 128-B row is gathered while the
-    // four multiplies of this addition that do not read the operand run
-    e4 = *reinterpret_cast<const uint4*>(entries + i0);
-    uint32_t e = e4.x;
-    ge_niels qn = fetch_entry_raw(tbl, tbl1, n0, e);
-    for (uint32_t i = i0; i < i1; ++i) {
-#else
     for (uint32_t i = i0; i < i1; ++i) {
       if (((i - i0) & 3u) == 0) e4 = *reinterpret_cast<const uint4*>(entries + i);
       const uint32_t q = (i - i0) & 3u;
       const uint32_t e = q == 0 ? e4.x : q == 1 ? e4.y : q == 2 ? e4.z : e4.w;
-#endif
       if (i == bend) {  // close the run of bucket b
         if (bstart >= i0) {
           store_p3(bsum, b, acc);  // whole bucket inside the chunk
@@ -258,18 +235,7 @@ __global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_
         if (((bend - 1) >> ks) - l >= FIX_MAX) heavy[1 + atomicAdd(&heavy[0], 1u)] = b;
         acc = ge_identity();
       }
-#ifdef ACC_PREFETCH
-      const ge_madd_mid mid = ge_madd_signed_h1(acc, qn, e >> 31);
-      if (i + 1 < i1) {
-        const uint32_t q = (i + 1 - i0) & 3u;
-        if (q == 0) e4 = *reinterpret_cast<const uint4*>(entries + i + 1);
-        e = q == 0 ? e4.x : q == 1 ? e4.y : q == 2 ? e4.z : e4.w;
-        qn = fetch_entry_raw(tbl, tbl1, n0, e);
-      }
-      acc = ge_madd_h2(mid);
-#else
       acc = ge_madd(acc, fetch_entry(tbl, tbl1, n0, e));
-#endif
     }
     // last run [max(bstart, i0), i1)
     if (bstart >= i0 && bend <= i1) {
@@ -756,9 +722,7 @@ __global__ void __launch_bounds__(RS_T) k_rsort_scatter(const dig_t* __restrict_
 // fine bits, in LDS tiles of RS_FTILE entries with coalesced output runs.
 // A segment that fits one tile (all but the top window's, typically) is
 // read twice; longer ones get a counting pass first.
-#ifndef RS_FTILE
 #define RS_FTILE 8192
-#endif
 #define RS_FT 512  // 8 waves per block: 4 blocks (40 KB LDS each) = 32 waves per CU
 #define RS_FPER (RS_FTILE / RS_FT)
 __global__ void __launch_bounds__(RS_FT) k_rsort_fine(const uint32_t* __restrict__ tmpA, uint32_t nchunk,

@@ -65,6 +65,38 @@ def from_uniform(bytes64: bytes) -> bytes:
     return out.raw
 
 
+def _chunks(n: int, parts: int):
+    return [(n * i // parts, n * (i + 1) // parts) for i in range(parts)]
+
+
+def from_uniform_threads(bytes64: bytes, threads: int | None = None) -> bytes:
+    """from_uniform over `threads` workers (ctypes drops the GIL)."""
+    import concurrent.futures as cf
+    n = len(bytes64) // 64
+    threads = max(1, min(threads or host_cores(), n or 1))
+    with cf.ThreadPoolExecutor(threads) as ex:
+        outs = list(ex.map(lambda ab: from_uniform(bytes64[64 * ab[0]: 64 * ab[1]]), _chunks(n, threads)))
+    return b"".join(outs)
+
+
+def msm_threads(scalars: bytes, points: bytes, threads: int | None = None) -> bytes:
+    """Exact MSM on all host cores: the terms split into `threads` chunks,
+    each a serial dalek-style MSM (port_msm), the chunk results decoded and
+    summed with the Python spec oracle.  Test / golden-generation only."""
+    import concurrent.futures as cf
+
+    from oracle import ristretto as r255
+    n = len(scalars) // 32
+    threads = max(1, min(threads or host_cores(), n or 1))
+    with cf.ThreadPoolExecutor(threads) as ex:
+        parts = list(ex.map(lambda ab: msm(scalars[32 * ab[0]: 32 * ab[1]], points[32 * ab[0]: 32 * ab[1]]),
+                            _chunks(n, threads)))
+    acc = r255.IDENTITY
+    for p in parts:
+        acc = r255.ed_add(acc, r255.decode(p))
+    return r255.encode(acc)
+
+
 def synth(n: int, seed: int):
     raw = hashlib.shake_256(b"cpu-scalars" + seed.to_bytes(8, "little")).digest(64 * n)
     sc = b"".join((int.from_bytes(raw[64 * i: 64 * i + 64], "little") % L).to_bytes(32, "little") for i in range(n))

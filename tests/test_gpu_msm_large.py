@@ -151,3 +151,68 @@ def test_msm_2p22_config5_window_partition(ctx):
     assert got2 == r255.encode(r255.ed_add(P, P))
     ctx.dev_free(d)
     tbl.close()
+
+
+def _bench_inputs(ctx, world, seed_base=2):
+    import bench
+    n = 1 << 20
+    tbl = ctx.from_uniform(b"".join(bench.synth_point_bytes(n, 3 + 1000 * s) for s in range(world)))
+    sc = b"".join(bench.synth_scalars(n, seed_base + 1000 * s) for s in range(world))
+    d = ctx.dev_alloc(len(sc))
+    ctx.htod(d, sc)
+    return tbl, d, world * n
+
+
+def test_msm_2p20_exact_vs_cport_golden(ctx):
+    """Config 3 at its full size, exact: the bench's own 2^20 inputs (both
+    scalar vectors of its pipelined stream) against the C port's result
+    (tests/golden/bench_msm.json, make_bench_golden.py), one MSM at a time
+    and through the submit/collect stream bench.py times."""
+    import json
+    from pathlib import Path
+    gold = json.loads((Path(__file__).parent / "golden" / "bench_msm.json").read_text())["world"]["1"]
+    tbl, d, n = _bench_inputs(ctx, 1)
+    assert ctx.msm_table_dev(d, tbl, n).hex() == gold["result"]
+    import bench
+    d2 = ctx.dev_alloc(32 * n)
+    ctx.htod(d2, bench.synth_scalars(n, 7))
+    t1 = ctx.msm_submit(d, tbl, n)
+    t2 = ctx.msm_submit(d2, tbl, n)
+    t3 = ctx.msm_submit(d, tbl, n)
+    assert ctx.msm_collect(t1).hex() == gold["result"]
+    assert ctx.msm_collect(t2).hex() == gold["result2"]
+    assert ctx.msm_collect(t3).hex() == gold["result"]
+    ctx.dev_free(d)
+    ctx.dev_free(d2)
+    tbl.close()
+
+
+def test_msm_2p21_both_partitions_exact(ctx):
+    """bench.py at N = 2, rehearsed on one GPU: the window split (each rank
+    all 2^21 points, half the windows) and the point split (each rank its
+    2^20-point slice, all windows) both reproduce the C port's 2^21 result
+    after the exact partial addition (bpp_partials_finish)."""
+    import json
+    from pathlib import Path
+
+    import bpperm
+    from bpperm import dist as bdist
+    gold = json.loads((Path(__file__).parent / "golden" / "bench_msm.json").read_text())["world"]["2"]
+    tbl, d, n = _bench_inputs(ctx, 2)
+    c, W = bpperm.msm_windows(n)
+    parts = [ctx.msm_table_dev_partial(d, tbl, n, a, b) for a, b in bdist.window_ranges(W, 2)]
+    assert bpperm.partials_finish(parts).hex() == gold["result"]
+    tbl.close()
+    ctx.dev_free(d)
+    import bench
+    half = 1 << 20
+    parts = []
+    for s in range(2):
+        t = ctx.from_uniform(bench.synth_point_bytes(half, 3 + 1000 * s))
+        ds = ctx.dev_alloc(32 * half)
+        ctx.htod(ds, bench.synth_scalars(half, 2 + 1000 * s))
+        _, Wh = bpperm.msm_windows(half)
+        parts.append(ctx.msm_table_dev_partial(ds, t, half, 0, Wh))
+        ctx.dev_free(ds)
+        t.close()
+    assert bpperm.partials_finish(parts).hex() == gold["result"]

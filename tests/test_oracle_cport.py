@@ -61,3 +61,32 @@ def test_cpu_prover_matches_python_oracle(k, seed):
     want, _ = bp.ac_prove(k, seed)
     pf, V = cport.cpu_prove(k, seed)
     assert pf == want.to_bytes() and V == want.V
+
+
+def test_cport_threaded_helpers_match_serial():
+    """msm_threads / from_uniform_threads (the golden generator's all-cores
+    path) equal the serial port."""
+    raw = b"".join(Rng(5, b"thr").bytes(64) for _ in range(1))  # seed material
+    import hashlib
+    raw = hashlib.shake_256(raw).digest(64 * 3000)
+    pts = cport.from_uniform(raw)
+    assert cport.from_uniform_threads(raw, threads=7) == pts
+    sc = b"".join((int.from_bytes(hashlib.sha512(i.to_bytes(4, "little")).digest(), "little") % r255.L)
+                  .to_bytes(32, "little") for i in range(3000))
+    assert cport.msm_threads(sc, pts, threads=5) == cport.msm(sc, pts)
+
+
+def test_bench_golden_is_prefix_consistent():
+    """tests/golden/bench_msm.json (make_bench_golden.py): the world-1 entry
+    of the bench's inputs at a reduced size reproduces from the serial port,
+    and the file covers N = 1, 2, 4, 8 with distinct results."""
+    import bench
+    gold = json.loads((Path(__file__).parent / "golden" / "bench_msm.json").read_text())
+    assert gold["log2n"] == 20 and sorted(gold["world"]) == ["1", "2", "4", "8"]
+    res = {v["result"] for v in gold["world"].values()} | {v["result2"] for v in gold["world"].values()}
+    assert len(res) == 8
+    # the generator's own path on a 2^10 slice: threaded == serial
+    n = 1 << 10
+    pts = cport.from_uniform(bench.synth_point_bytes(n, 3))
+    sc = bench.synth_scalars(n, 2)
+    assert cport.msm_threads(sc, pts, threads=3) == cport.msm(sc, pts)

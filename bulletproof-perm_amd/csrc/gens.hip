@@ -38,74 +38,90 @@ __global__ void __launch_bounds__(64) k_fb_tables(const uint32_t* __restrict__ t
   store_niels(fb, t, ge_to_niels(acc));
 }
 
-// Bits [16q, 16q + 16) of s + K, K = 8 * sum_{i<63} 16^i: nibble i of s + K
-// minus 8 is signed radix-16 digit i of s (i < 63, digits in [-8, 8)) and
-// nibble 63 the top digit (s < 2^253: at most 2), the same digits as a
-// carry-propagating recoding, in closed form and without a data-dependent
-// index (the word is picked by selects).
-FE_INLINE uint32_t ped_digit_bits(const uint32_t* __restrict__ sp, uint32_t q) {
-  uint64_t c = 0;
-  uint32_t word = 0;
-  _Pragma("unroll") for (uint32_t i = 0; i < 8; ++i) {
-    c += (uint64_t)sp[i] + (i < 7 ? 0x88888888u : 0x08888888u);
-    word = (q >> 1) == i ? (uint32_t)c : word;
-    c >>= 32;
+// Pedersen commitments P_j = v_j * B + g_j * Bb (PedersenGens::commit,
+// weights.rs:58-61), constant time in v and gamma like the reference's
+// commit (a constant-time 2-term multiscalar_mul).
+//
+// Signed radix-16 digits in closed form: nibble i of s + K, K = 8 * sum_{i<63}
+// 16^i, minus 8 is digit i (i < 63, in [-8, 8)) and nibble 63 the top digit
+// (s < 2^253: at most 2) -- the digits of a carry-propagating recoding,
+// without a data-dependent branch or index.  Table row (which * 64 + pos) * 8
+// + |d| - 1 of fb holds |d| * 16^pos * (B, Bb)[which].
+//
+// The work is split by POSITION GROUP, not by commitment: block (x, g) handles
+// positions [Pg, Pg + P) of both scalars (P = 64 / G) for 256 commitments, one
+// commitment per lane (2P mixed additions each).  Every lane of the block
+// reads the same 16P table rows, staged once in LDS (16 KB at G = 8), so each
+// lookup is a broadcast LDS read; the lookup is dalek's LookupTable::select -- all eight rows of a
+// position read, the one for |d| kept by masks, d = 0 keeping the Niels
+// identity -- and signs are operand selects (ge_madd_signed).  Loads and
+// instruction stream are independent of the digits.  The G partial sums of
+// a commitment are added by k_pedersen_sum (G lanes, log2 G butterfly levels).
+// G = 8 for large batches (13 312 V commitments per 128 proofs: fewest
+// partials), G = 32 for small ones (latency: 4 additions per lane).
+#define PED_T 256
+template <int G>
+__global__ void __launch_bounds__(PED_T) k_pedersen(const uint32_t* __restrict__ fb, const uint32_t* __restrict__ v,
+                                                    const uint32_t* __restrict__ gam, size_t m,
+                                                    uint32_t* __restrict__ part) {
+  constexpr uint32_t PED_GPOS = FB_POS / G;    // positions per group
+  constexpr uint32_t PED_ROWS = 2 * PED_GPOS * 8;  // table rows one block needs
+  __shared__ __attribute__((aligned(16))) uint32_t rows[PED_ROWS * MSM_NIELS_WORDS];
+  const uint32_t g = blockIdx.y;
+  // stage rows (which, b, d) = fb row (which * 64 + 8g + b) * 8 + d - 1
+  for (uint32_t i = threadIdx.x; i < PED_ROWS * (MSM_NIELS_WORDS / 4); i += PED_T) {
+    const uint32_t r = i / (MSM_NIELS_WORDS / 4), c = i % (MSM_NIELS_WORDS / 4);
+    const uint32_t which = r / (PED_GPOS * 8), rem = r % (PED_GPOS * 8);
+    const uint32_t src = (which * FB_POS + PED_GPOS * g) * 8 + rem;
+    reinterpret_cast<uint4*>(rows)[i] = reinterpret_cast<const uint4*>(fb + (size_t)src * MSM_NIELS_WORDS)[c];
   }
-  return (word >> (16 * (q & 1))) & 0xffffu;
-}
-
-// Constant-time table lookup (dalek's LookupTable::select, which
-// PedersenGens::commit's constant-time multiscalar_mul uses): all eight
-// rows d * 16^pos * P (d = 1..8) are loaded and the one for |d| is kept by
-// masks; d = 0 keeps the Niels identity.  The loads and the instruction
-// stream do not depend on the digit.
-FE_INLINE ge_niels ped_select_ct(const uint32_t* __restrict__ fb, uint32_t row0, uint32_t ad) {
-  ge_niels r = ge_niels_identity();
-  _Pragma("unroll 2") for (uint32_t j = 1; j <= 8; ++j) {
-    const ge_niels t = load_niels(fb, row0 + j - 1);
-    const uint32_t mask = 0u - (uint32_t)(ad == j);
-    _Pragma("unroll") for (int i = 0; i < FE_LIMBS; ++i) {
-      r.ypx.v[i] ^= (r.ypx.v[i] ^ t.ypx.v[i]) & mask;
-      r.ymx.v[i] ^= (r.ymx.v[i] ^ t.ymx.v[i]) & mask;
-      r.xy2d.v[i] ^= (r.xy2d.v[i] ^ t.xy2d.v[i]) & mask;
-    }
-  }
-  return r;
-}
-
-// P_j = v_j * B + g_j * Bb (PedersenGens::commit, weights.rs:58-61), PED_G
-// lanes per commitment: lane q adds the table entries of radix-16 positions
-// [4q, 4q+4) of both scalars (always 8 mixed additions: no zero skip), then
-// the 16 partial sums are combined with 4 xor-shuffle levels.  Constant time
-// in v and gamma like the reference's commit: digits in closed form,
-// ped_select_ct over all eight rows, signs by operand selects
-// (ge_madd_signed).  A one-lane-per-commitment kernel would chain 128
-// additions (the GPU's per-lane field-multiply latency is ~0.3 us,
-// profiles/r01_felat.txt).
-#define PED_G 16
-#define PED_PER (FB_POS / PED_G)  // radix-16 digits per lane and scalar
-__global__ void __launch_bounds__(256) k_pedersen(const uint32_t* __restrict__ fb, const uint32_t* __restrict__ v,
-                                                  const uint32_t* __restrict__ gam, size_t m,
-                                                  uint32_t* __restrict__ out_p3) {
-  const size_t gt = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t j = gt / PED_G;
-  const uint32_t q = (uint32_t)(gt % PED_G);
+  __syncthreads();
+  const size_t j = (size_t)blockIdx.x * PED_T + threadIdx.x;
+  if (j >= m) return;
   ge_p3 acc = ge_identity();
-  if (j < m) {
-    _Pragma("unroll 1") for (uint32_t which = 0; which < 2; ++which) {
-      const uint32_t bits = ped_digit_bits((which ? gam : v) + 8 * j, q);
-      _Pragma("unroll 1") for (uint32_t b = 0; b < PED_PER; ++b) {
-        const uint32_t pos = PED_PER * q + b;
-        const int nib = (int)((bits >> (4 * b)) & 15u);
-        const int d = pos < FB_POS - 1 ? nib - 8 : nib;
-        const int sg = d >> 31;  // 0 or -1
-        const uint32_t ad = (uint32_t)((d ^ sg) - sg);
-        const ge_niels t = ped_select_ct(fb, (which * FB_POS + pos) * 8, ad);
-        acc = ge_madd_signed(acc, t, sg != 0);
+  _Pragma("unroll 1") for (uint32_t which = 0; which < 2; ++which) {
+    // word Pg / 8 of s + K holds the nibbles of positions [Pg, Pg + P)
+    const uint32_t* sp = (which ? gam : v) + 8 * j;
+    const uint32_t wsel = PED_GPOS * g / 8, sh = 4 * (PED_GPOS * g % 8);
+    uint64_t c = 0;
+    uint32_t word = 0;
+    _Pragma("unroll") for (uint32_t i = 0; i < 8; ++i) {
+      c += (uint64_t)sp[i] + (i < 7 ? 0x88888888u : 0x08888888u);
+      word = wsel == i ? (uint32_t)c : word;
+      c >>= 32;
+    }
+    word >>= sh;
+    _Pragma("unroll 1") for (uint32_t b = 0; b < PED_GPOS; ++b) {
+      const int nib = (int)((word >> (4 * b)) & 15u);
+      const int d = PED_GPOS * g + b < FB_POS - 1 ? nib - 8 : nib;
+      const int sg = d >> 31;  // 0 or -1
+      const uint32_t ad = (uint32_t)((d ^ sg) - sg);
+      const uint32_t r0 = (which * PED_GPOS + b) * 8;
+      ge_niels t = ge_niels_identity();
+      _Pragma("unroll 2") for (uint32_t k = 1; k <= 8; ++k) {
+        const ge_niels e = load_niels(rows, r0 + k - 1);
+        const bool hit = ad == k;
+        _Pragma("unroll") for (int i = 0; i < FE_LIMBS; ++i) {
+          t.ypx.v[i] = hit ? e.ypx.v[i] : t.ypx.v[i];
+          t.ymx.v[i] = hit ? e.ymx.v[i] : t.ymx.v[i];
+          t.xy2d.v[i] = hit ? e.xy2d.v[i] : t.xy2d.v[i];
+        }
       }
+      acc = ge_madd_signed(acc, t, sg != 0);
     }
   }
-  _Pragma("unroll") for (int off = 1; off < PED_G; off <<= 1) {
+  store_p3(part, (size_t)g * m + j, acc);
+}
+
+// P_j = sum of its G partials: G lanes per commitment, log2 G levels.
+template <int G>
+__global__ void __launch_bounds__(256) k_pedersen_sum(const uint32_t* __restrict__ part, size_t m,
+                                                      uint32_t* __restrict__ out_p3) {
+  const size_t gt = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t j = gt / G;
+  const uint32_t q = (uint32_t)(gt % G);
+  ge_p3 acc = j < m ? load_p3(part, (size_t)q * m + j) : ge_identity();
+  _Pragma("unroll") for (int off = 1; off < G; off <<= 1) {
     ge_p3 o;
     _Pragma("unroll") for (int i = 0; i < FE_LIMBS; ++i) {
       o.X.v[i] = __shfl_xor(acc.X.v[i], off, 64);
@@ -161,10 +177,22 @@ int pedersen_dev(bpp_ctx* ctx, const bpp_gens* g, const uint32_t* d_v, const uin
   // batches in flight, 68-79 K vs 80-82 K proofs/s: their 1 MB of rows
   // compete in L2 with the concurrent direct-table MSMs, while this kernel's
   // 128 KB radix-16 table stays resident)
+  const uint32_t G = m <= 2048 ? 32 : 8;
+  void* part = nullptr;
+  BPP_TRY(ctx_ws(ctx, "ped_part", m * G * P3_BYTES, &part));
   {
     ProfScope ps(ctx, "pedersen");
-    hipLaunchKernelGGL(k_pedersen, dim3(grid_for(m * PED_G, 256)), dim3(256), 0, ctx->stream, g->d_fb, d_v, d_gam, m,
-                       p3);
+    if (G == 32) {
+      hipLaunchKernelGGL(k_pedersen<32>, dim3(grid_for(m, PED_T), 32), dim3(PED_T), 0, ctx->stream, g->d_fb, d_v,
+                         d_gam, m, (uint32_t*)part);
+      hipLaunchKernelGGL(k_pedersen_sum<32>, dim3(grid_for(m * 32, 256)), dim3(256), 0, ctx->stream,
+                         (const uint32_t*)part, m, p3);
+    } else {
+      hipLaunchKernelGGL(k_pedersen<8>, dim3(grid_for(m, PED_T), 8), dim3(PED_T), 0, ctx->stream, g->d_fb, d_v,
+                         d_gam, m, (uint32_t*)part);
+      hipLaunchKernelGGL(k_pedersen_sum<8>, dim3(grid_for(m * 8, 256)), dim3(256), 0, ctx->stream,
+                         (const uint32_t*)part, m, p3);
+    }
   }
   BPP_TRY(ctx_check_launch(ctx, "k_pedersen"));
   if (d_out_enc) {

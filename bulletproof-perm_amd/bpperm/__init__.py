@@ -114,6 +114,21 @@ class Context:
     def profile_reset(self):
         self.lib.bpp_ctx_profile_reset(self.h)
 
+    WORK_COUNTERS = ("msm_terms", "madds", "padds", "msm_launches")
+
+    def work(self) -> dict:
+        """Algorithmic work issued on this context since the last work_reset
+        (bpp_ctx_work_get): MSM terms, mixed additions, point additions."""
+        out = {}
+        for name in self.WORK_COUNTERS:
+            v = C.c_uint64()
+            check(self.lib.bpp_ctx_work_get(self.h, name.encode(), C.byref(v)), "bpp_ctx_work_get", self.h)
+            out[name] = v.value
+        return out
+
+    def work_reset(self):
+        self.lib.bpp_ctx_work_reset(self.h)
+
     # ---------------------------------------------------------- device memory
     def dev_alloc(self, nbytes: int) -> int:
         p = C.c_void_p()
@@ -385,9 +400,12 @@ class PermProver:
     """Permutation proof over resident generators — the sound-mode restatement
     of ACProof::ArithmeticCircuitProof (circuit_lib.rs:139-585)."""
 
-    def __init__(self, gens: Gens, k: int, label: bytes = b"bp-perm"):
+    def __init__(self, gens: Gens, k: int, label: bytes = b"bp-perm", ctx: "Context | None" = None):
+        """ctx: the context (stream, workspaces) proofs run on; default the
+        generators' own.  One generator set may serve several contexts, e.g.
+        one per host thread with batches in flight."""
         self.gens = gens
-        self.ctx = gens.ctx
+        self.ctx = ctx or gens.ctx
         self.k = k
         self.label = label
         self.proof_len = int(self.ctx.lib.bpp_perm_proof_len(k))

@@ -40,6 +40,8 @@ SIGNATURES = {
     "bpp_ctx_profile": (i32, [vp, i32]),
     "bpp_ctx_profile_get": (i32, [vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(u64)]),
     "bpp_ctx_profile_reset": (None, [vp]),
+    "bpp_ctx_work_get": (i32, [vp, C.c_char_p, C.POINTER(u64)]),
+    "bpp_ctx_work_reset": (None, [vp]),
     "bpp_dev_alloc": (i32, [vp, sz, C.POINTER(vp)]),
     "bpp_dev_free": (i32, [vp, vp]),
     "bpp_memcpy_htod": (i32, [vp, vp, vp, sz]),

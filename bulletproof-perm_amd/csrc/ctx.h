@@ -60,6 +60,11 @@ struct bpp_ctx {
   // ctx_h2d_const: per workspace name, the address and bytes last uploaded
   // (cleared with off_cache on any workspace reallocation)
   std::map<std::string, std::pair<void*, std::vector<uint8_t>>> h2d_cache;
+  // algorithmic work issued on this context (bpp_ctx_work_get): "msm_terms"
+  // (scalar-point terms of every MSM and Pedersen commitment launched),
+  // "madds" (mixed additions of a table point), "padds" (additions of two
+  // extended points: trees, bucket reductions), "msm_launches"
+  std::map<std::string, uint64_t> work;
 };
 
 struct bpp_points {
@@ -129,6 +134,8 @@ struct HostScope {
 };
 
 int ctx_check_launch(bpp_ctx* ctx, const char* what);
+// Adds to a work counter (see bpp_ctx::work).
+inline void ctx_work(bpp_ctx* ctx, const char* name, uint64_t n) { ctx->work[name] += n; }
 
 // scan.hip
 int scan_exclusive_u32(bpp_ctx* ctx, const uint32_t* d_in, uint32_t* d_out, size_t n);

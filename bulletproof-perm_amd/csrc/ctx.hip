@@ -229,6 +229,28 @@ int bpp_ctx_profile_get(bpp_ctx* ctx, const char* stage, double* ms, uint64_t* l
   return BPP_OK;
 }
 
+static void work_resolve(bpp_ctx* ctx) {
+  for (bpp_ctx* c : ctx->children) {
+    work_resolve(c);
+    for (auto& kv : c->work) ctx->work[kv.first] += kv.second;
+    c->work.clear();
+  }
+}
+
+int bpp_ctx_work_get(bpp_ctx* ctx, const char* name, uint64_t* value) {
+  if (!ctx || !name || !value) return BPP_ERR_ARG;
+  work_resolve(ctx);
+  auto it = ctx->work.find(name);
+  *value = it == ctx->work.end() ? 0 : it->second;
+  return BPP_OK;
+}
+
+void bpp_ctx_work_reset(bpp_ctx* ctx) {
+  if (!ctx) return;
+  work_resolve(ctx);
+  ctx->work.clear();
+}
+
 void bpp_ctx_profile_reset(bpp_ctx* ctx) {
   if (!ctx) return;
   prof_resolve(ctx);

@@ -9,7 +9,9 @@
 #include "msm_engine.h"
 
 #define FB_POS 64  // radix-16 positions per fixed base
-#define GENS_DT_MAX 4096  // generators for which direct tables are kept (2 GB at the limit)
+#define GENS_DT_MAX 4096  // generators for which direct tables are kept (c >= 8: 2 GB at the limit)
+#define GENS_DT_BUDGET (4ull << 30)  // HBM for one generator set's direct tables (288 GB per GPU)
+#define GENS_DT_CMAX 13  // widest direct-table window (2^12 rows per window)
 
 struct bpp_gens {
   bpp_ctx* ctx = nullptr;
@@ -18,8 +20,9 @@ struct bpp_gens {
   uint32_t* d_fb = nullptr;   // fixed-base tables for B and Bb: 2 x 64 x 8 Niels
   // window tables of every generator (FBW_W x 128 B each), built on first use
   mutable uint32_t* d_wt = nullptr;
-  // direct tables d * 2^(8 w) * P, built on first use when 2n+2 <=
-  // GENS_DT_MAX (512 KB per generator, 32 table additions per scalar)
+  // direct tables d * 2^(c w) * P (d <= 2^(c-1), w < ceil(254 / c)), built
+  // on first use when 2n+2 <= GENS_DT_MAX, c the widest window within
+  // GENS_DT_BUDGET (gens_points)
   mutable uint32_t* d_dt = nullptr;
   mutable uint32_t dt_c = 8;
   // guards the first-use builds of d_wt / d_dt: contexts on other streams

@@ -178,6 +178,10 @@ int pedersen_dev(bpp_ctx* ctx, const bpp_gens* g, const uint32_t* d_v, const uin
   // compete in L2 with the concurrent direct-table MSMs, while this kernel's
   // 128 KB radix-16 table stays resident)
   const uint32_t G = m <= 2048 ? 32 : 8;
+  ctx_work(ctx, "msm_terms", 2 * (uint64_t)m);
+  ctx_work(ctx, "madds", 2 * (uint64_t)FB_POS * m);  // constant time: every position of both scalars
+  ctx_work(ctx, "padds", (uint64_t)(G - 1) * m);
+  ctx_work(ctx, "msm_launches", 1);
   void* part = nullptr;
   BPP_TRY(ctx_ws(ctx, "ped_part", m * G * P3_BYTES, &part));
   {
@@ -231,10 +235,13 @@ int gens_points(bpp_ctx* ctx, const bpp_gens* g, MsmPoints* out) {
     g->d_wt = d;
   }
   if (!g->d_dt && np <= GENS_DT_MAX) {
-    // c = 8: 16-bit windows halve the table additions but measured no
-    // faster (0.94 vs 0.91 ms of direct-table time per 128-proof batch;
-    // 16.5 GB of tables gathered at random)
-    const uint32_t c = 8;
+    // The widest window (fewest table additions per term: W = ceil(254 / c))
+    // whose tables fit GENS_DT_BUDGET: c = 13 (W = 20, 2.7 GB) for the
+    // 258 generators of a 52-card proof, against W = 32 at c = 8.  Measured
+    // in isolation (tools/ubench/dtbench, 8 batches' IPA rounds in one
+    // launch): 446 / 376 / 337 / 312 / 294 us at c = 8 / 11 / 12 / 13 / 16.
+    uint32_t c = 8;
+    while (c < GENS_DT_CMAX && dt_bytes(np, c + 1) <= GENS_DT_BUDGET) ++c;
     uint32_t* d = nullptr;
     if (hipMalloc(&d, dt_bytes(np, c)) != hipSuccess) {
       ctx->err = "hipMalloc generator direct tables";

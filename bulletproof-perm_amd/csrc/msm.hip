@@ -83,6 +83,10 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
   }
   const size_t nseg = fb ? (size_t)M : (size_t)M * Wn;
   const size_t NB = nseg * g.B;
+  ctx_work(ctx, "msm_terms", T);
+  ctx_work(ctx, "madds", (uint64_t)T * Wn);
+  ctx_work(ctx, "padds", (uint64_t)2 * NB);  // running sums of the bucket reduction
+  ctx_work(ctx, "msm_launches", 1);
   void *cnt, *cur, *boff, *entries, *bsum, *wsum;
   BPP_TRY(ctx_ws(ctx, "msm_cnt", (NB + 1) * 4, &cnt));
   BPP_TRY(ctx_ws(ctx, "msm_cur", NB * 4, &cur));
@@ -590,24 +594,35 @@ static bool fb_wins(double terms_per_msm) {
 static DtGeom dt_geom(uint32_t c) {
   DtGeom g;
   g.c = c;
-  g.W = 256 / c;
+  g.W = (254 + c - 1) / c;
+  g.H = 1u << (c - 1);
+  for (int i = 0; i < 8; ++i) g.K[i] = 0;
+  for (uint32_t w = 0; w + 1 < g.W; ++w) {  // bit c w + c - 1 (< 253)
+    const uint32_t pos = c * w + c - 1;
+    g.K[pos >> 5] |= 1u << (pos & 31);
+  }
   return g;
 }
 
 size_t dt_bytes(uint32_t npts, uint32_t c) {
-  return (size_t)npts * (256 / c) * ((size_t)1 << (c - 1)) * MSM_NIELS_WORDS * 4;
+  const DtGeom g = dt_geom(c);
+  return (size_t)npts * g.W * g.H * MSM_NIELS_WORDS * 4;
 }
 
 int dt_build(bpp_ctx* ctx, const uint32_t* d_wt, uint32_t npts, uint32_t c, uint32_t* d_dt) {
   if (!npts) return BPP_OK;
-  if (c != 8 && c != 16) {
-    ctx->err = "dt_build: window width must be 8 or 16";
+  if (c < 8 || c > 13) {
+    ctx->err = "dt_build: window width must be 8..13";
     return BPP_ERR_ARG;
   }
   const DtGeom g = dt_geom(c);
+  const size_t rows = (size_t)npts * g.W * g.H;
+  if (rows >= 0x100000000ull) {
+    ctx->err = "dt_build: table too large";
+    return BPP_ERR_LEN;
+  }
   {
     ProfScope ps(ctx, "dt_tables");
-    const size_t rows = (size_t)npts * g.W * ((size_t)1 << (c - 1));
     hipLaunchKernelGGL(k_dt_build, dim3(grid_for(rows, 64)), dim3(64), 0, ctx->stream, d_wt, npts, g, d_dt);
   }
   return ctx_check_launch(ctx, "k_dt_build");
@@ -629,26 +644,22 @@ static int msm_multi_dt_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t
   BPP_TRY(upload_offsets(ctx, off, &d_off));
   BPP_TRY(ctx_ws(ctx, "dt_res", (size_t)M * P3_BYTES, &res));
   const DtGeom dg = dt_geom(pts.dt_c);
-  const double e_avg = (double)T * dg.W / (double)M;  // table additions per MSM
-  // 256 lanes per MSM measured best for the prover's batches (M = 256-384
-  // MSMs: 0.99 ms of direct-table time per 128 proofs vs 1.10-1.20 at 512
-  // and 1.42 at 128); 512 only when few large MSMs leave the chip empty
-  const int nt = e_avg > 256 ? (M < 128 && e_avg > 2048 ? 512 : 256) : 64;
+  // W lanes per term group: the largest multiple of W within DT_NT_MAX lanes
+  // whose groups each still get about two terms (small MSMs: fewer lanes,
+  // a shallower tree); ~512 lanes measured slower at 8 proof batches in
+  // flight
+  const double t_avg = (double)T / (double)M;
+  uint32_t TG = DT_NT_MAX / dg.W;
+  while (TG > 1 && t_avg < 2.0 * TG) TG >>= 1;
+  const uint32_t nt = TG * dg.W;
+  ctx_work(ctx, "msm_terms", T);
+  ctx_work(ctx, "madds", (uint64_t)T * dg.W);
+  ctx_work(ctx, "padds", (uint64_t)M * (nt - 1));
+  ctx_work(ctx, "msm_launches", 1);
   {
     ProfScope ps(ctx, "msm_direct");
-    // (no 1024-thread variant: capped at 128 VGPRs it spills in the main loop)
-    if (nt == 128)
-      hipLaunchKernelGGL(k_dt_msm<128>, dim3(M), dim3(128), 0, ctx->stream, pts.dt, dg, d_scal, d_pidx,
-                         (const uint32_t*)d_off, (uint32_t*)res);
-    else if (nt == 512)
-      hipLaunchKernelGGL(k_dt_msm<512>, dim3(M), dim3(512), 0, ctx->stream, pts.dt, dg, d_scal, d_pidx,
-                         (const uint32_t*)d_off, (uint32_t*)res);
-    else if (nt == 256)
-      hipLaunchKernelGGL(k_dt_msm<256>, dim3(M), dim3(256), 0, ctx->stream, pts.dt, dg, d_scal, d_pidx,
-                         (const uint32_t*)d_off, (uint32_t*)res);
-    else
-      hipLaunchKernelGGL(k_dt_msm<64>, dim3(M), dim3(64), 0, ctx->stream, pts.dt, dg, d_scal, d_pidx,
-                         (const uint32_t*)d_off, (uint32_t*)res);
+    hipLaunchKernelGGL(k_dt_msm, dim3(M), dim3(nt), (size_t)nt * P3_BYTES, ctx->stream, pts.dt, dg, d_scal, d_pidx,
+                       (const uint32_t*)d_off, (uint32_t*)res);
   }
   BPP_TRY(ctx_check_launch(ctx, "k_dt_msm"));
   *d_res = (uint32_t*)res;

@@ -826,123 +826,144 @@ __global__ void __launch_bounds__(RS_FT) k_rsort_fine(const uint32_t* __restrict
 }
 
 // ---------------------------------------------------------------------------
-// Direct fixed-base MSM over full radix-2^c tables (c = 8 or 16; small MSMs
-// over resident generators: A_I/A_O/S, IPA rounds, vector commitments).
-// With W = 256 / c windows and h = 2^(c-1) rows per window, table row
-// (gen * W + w) * h + |d| - 1 holds d * 2^(c w) * G_gen (d = 1..h, signed
-// digits), so a term is at most W table additions and an MSM is one flat
-// sum: no digit sort, no buckets, no bucket reduction.  One block per MSM;
-// lane j adds its slice of the MSM's (term, window) pairs, then a
-// wave-shuffle tree and an LDS step over the block's waves.
+// Direct fixed-base MSM over full radix-2^c tables (small MSMs over resident
+// generators: A_I/A_O/S, IPA rounds, vector commitments).  With
+// W = ceil(254 / c) windows and H = 2^(c-1) rows per window, table row
+// (gen * W + w) * H + |d| - 1 holds d * 2^(c w) * G_gen (d = 1..H), so a term
+// is at most W table additions and an MSM is one flat sum: no digit sort, no
+// buckets, no bucket reduction.
+//
+// Digits in closed form: with K = sum_{w < W-1} 2^(c w + c - 1) (host,
+// DtGeom::K), field w of s + K minus H is signed digit w in [-H, H) for
+// w < W - 1 and field W - 1 the top digit (>= 0; s < 2^253 so s + K < 2^254),
+// the digits of a carry-propagating signed recoding without the carry chain.
+//
+// One block per MSM, blockDim = W * TG lanes: lane (tg, w) owns WINDOW w of
+// terms tg, tg + TG, tg + 2 TG, ... -- the window is fixed per lane, so the
+// digit is a fixed bit field of s + K (no per-entry division or scan), and
+// the W lanes sharing a term read the same 32 scalar bytes.  Then an LDS
+// tree over the block's lanes.
 struct DtGeom {
-  uint32_t c, W;  // window bits (8 or 16), windows (32 or 16)
+  uint32_t c, W, H;  // window bits, windows, rows per window (2^(c-1))
+  uint32_t K[8];     // sum_{w < W-1} 2^(c w + c - 1), little-endian words
 };
-FE_INLINE uint32_t dt_half(const DtGeom& g) { return 1u << (g.c - 1); }
+#define DT_NT_MAX 256
 
+FE_INLINE uint32_t sel8(const uint32_t v[8], uint32_t i) {  // v[i], 0 for i >= 8 (no scratch)
+  uint32_t r = 0;
+  _Pragma("unroll") for (uint32_t k = 0; k < 8; ++k) r = i == k ? v[k] : r;
+  return r;
+}
 
-
-// Lane-local walk over the nonzero (term, window) digits of its slice.
-struct DtWalk {
-  const uint32_t* scalars;
-  const uint32_t* pidx;
-  DtGeom g;
-  uint32_t t0, e, e1, cur, gen, carry;
-  uint32_t s[8];
-  // next nonzero digit -> table row and sign; false when the slice is done
-  FE_INLINE bool next(uint32_t& row, bool& neg) {
-    const uint32_t half = dt_half(g);
-    for (; e < e1; ++e) {
-      const uint32_t t = t0 + e / g.W, w = e % g.W;
-      if (t != cur) {  // (re)enter a term: scalar, generator, carry into window w
-        cur = t;
-        load_scalar(scalars, t, s);
-        gen = pidx ? pidx[t] : t;
-        carry = 0;
-        for (uint32_t ww = 0; ww < w; ++ww) carry = (scalar_bits_sel(s, ww * g.c, g.c) + carry) >= half ? 1u : 0u;
-      }
-      const uint32_t v = scalar_bits_sel(s, w * g.c, g.c) + carry;
-      int d;
-      if (v >= half && w + 1 < g.W) {
-        d = (int)v - (int)(2 * half);
-        carry = 1;
-      } else {
-        d = (int)v;
-        carry = 0;
-      }
-      if (d == 0) continue;
-      row = (gen * g.W + w) * half + (uint32_t)((d < 0 ? -d : d) - 1);
-      neg = d < 0;
-      ++e;
-      return true;
+// Table row of window w of a term (scalar s, generator gen); d = 0 gives
+// row of |d| = 1 and zero = true (the caller adds the identity instead).
+struct DtLane {
+  uint32_t w, wi, sh, fmask, W, H;
+  bool top;
+  FE_INLINE void row_of(const DtGeom& g, const uint32_t sc[8], uint32_t gen, uint32_t& row, bool& neg,
+                        bool& zero) const {
+    uint32_t s[8];
+    uint64_t c = 0;
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) {
+      c += (uint64_t)sc[i] + g.K[i];
+      s[i] = (uint32_t)c;
+      c >>= 32;
     }
-    return false;
+    const uint32_t lo = sel8(s, wi), hi = sel8(s, wi + 1);
+    const uint32_t f = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & fmask;
+    const int d = top ? (int)f : (int)f - (int)H;
+    const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
+    zero = ad == 0;
+    neg = d < 0;
+    row = (gen * W + w) * H + (zero ? 0u : ad - 1u);
   }
 };
 
-template <int NT>
-__global__ void __launch_bounds__(NT) k_dt_msm(const uint32_t* __restrict__ dt, DtGeom dg,
-                                               const uint32_t* __restrict__ scalars,
-                                               const uint32_t* __restrict__ pidx, const uint32_t* __restrict__ off,
-                                               uint32_t* __restrict__ out_p3) {
-  __shared__ uint32_t tl[NT * P3_WORDS];  // 40 KB at NT = 256
+__global__ void __launch_bounds__(DT_NT_MAX) k_dt_msm(const uint32_t* __restrict__ dt, DtGeom dg,
+                                                    const uint32_t* __restrict__ scalars,
+                                                    const uint32_t* __restrict__ pidx, const uint32_t* __restrict__ off,
+                                                    uint32_t* __restrict__ out_p3) {
+  extern __shared__ uint32_t tl[];  // blockDim.x extended points (40 KB at 256 lanes)
+  const uint32_t nt = blockDim.x, TG = nt / dg.W;
   const uint32_t m = blockIdx.x;
-  const uint32_t t0 = off[m], t1 = off[m + 1];
-  const uint64_t E = (uint64_t)(t1 - t0) * dg.W;
-  DtWalk it;
-  it.scalars = scalars;
-  it.pidx = pidx;
-  it.g = dg;
-  it.t0 = t0;
-  it.e = (uint32_t)(E * threadIdx.x / NT);
-  it.e1 = (uint32_t)(E * (threadIdx.x + 1) / NT);
-  it.cur = 0xffffffffu;
+  const uint32_t tg = threadIdx.x / dg.W;
+  DtLane ln;
+  ln.w = threadIdx.x % dg.W;
+  ln.wi = (dg.c * ln.w) >> 5;
+  ln.sh = (dg.c * ln.w) & 31;
+  ln.fmask = (1u << dg.c) - 1u;
+  ln.W = dg.W;
+  ln.H = dg.H;
+  ln.top = ln.w + 1 == dg.W;
+  const uint32_t t1 = off[m + 1];
+  uint32_t t = off[m] + tg;
   ge_p3 acc = ge_identity();
-  // (an earlier software-pipelined gather that held a whole second row
-  // across the addition measured slower: 233 VGPRs)
-  // (measured: the gathers cost ~4 % of this kernel and two interleaved
-  // chains gain nothing; the add work and the block tree dominate)
-  uint32_t row;
-  bool neg;
-  // software pipeline: the walk to the next digit and its row gather are
-  // issued between the halves of the current addition (145 VGPRs; measured
-  // +2-4 % proofs/s at 8 batches in flight, one batch 5.88 -> 5.55 ms)
-  if (it.next(row, neg)) {
+  // Software pipeline over this lane's terms t, t + TG, ...: the scalar and
+  // generator index of the term after next are loaded one whole addition
+  // ahead, and the next term's 128-B table row is gathered between the two
+  // halves of the current addition (the operand is dead after its first
+  // three multiplies).  A zero digit adds the identity (no divergent skip).
+  if (tg < TG && t < t1) {
+    uint32_t sc[8];
+    load_scalar(scalars, t, sc);
+    uint32_t gen = pidx ? pidx[t] : t;
+    uint32_t tn = t + TG;
+    uint32_t scn[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t genn = 0;
+    if (tn < t1) {
+      load_scalar(scalars, tn, scn);
+      genn = pidx ? pidx[tn] : tn;
+    }
+    uint32_t row;
+    bool neg, zero;
+    ln.row_of(dg, sc, gen, row, neg, zero);
     ge_niels q = load_niels(dt, row);
     for (;;) {
+      if (zero) q = ge_niels_identity();
       const ge_madd_mid mid = ge_madd_signed_h1(acc, q, neg);
-      uint32_t row2;
-      bool neg2;
-      const bool more = it.next(row2, neg2);
-      if (more) q = load_niels(dt, row2);
+      const bool more = tn < t1;
+      bool neg2 = false, zero2 = false;
+      if (more) {
+        uint32_t row2;
+        ln.row_of(dg, scn, genn, row2, neg2, zero2);
+        q = load_niels(dt, row2);
+        tn += TG;
+        if (tn < t1) {
+          load_scalar(scalars, tn, scn);
+          genn = pidx ? pidx[tn] : tn;
+        }
+      }
       acc = ge_madd_h2(mid);
       if (!more) break;
       neg = neg2;
+      zero = zero2;
     }
   }
-  // block tree in LDS whose waves retire as it narrows: 9 wave-additions
-  // per 256-lane block against 4 x 6 levels of a wave butterfly + 2, at the
-  // same depth (8 additions); measured +4 % proofs/s at 8 batches in flight,
-  // one batch 5.80 -> 5.60 ms
+  // block tree in LDS whose waves retire as it narrows
   store_p3(tl, threadIdx.x, acc);
   __syncthreads();
-  for (uint32_t s = NT / 2; s > 0; s >>= 1) {
-    if (threadIdx.x < s) store_p3(tl, threadIdx.x, ge_add(load_p3(tl, threadIdx.x), load_p3(tl, threadIdx.x + s)));
+  uint32_t p2 = 1;
+  while (p2 < nt) p2 <<= 1;
+  for (uint32_t s = p2 >> 1; s > 0; s >>= 1) {
+    if (threadIdx.x < s && threadIdx.x + s < nt)
+      store_p3(tl, threadIdx.x, ge_add(load_p3(tl, threadIdx.x), load_p3(tl, threadIdx.x + s)));
     __syncthreads();
   }
   if (threadIdx.x == 0) store_p3(out_p3, m, load_p3(tl, 0));
 }
 
-// Direct tables from the window tables (wt[k * 32 + u] = 2^(8u) P_k):
-// lane (k, w, d) -> d * 2^(c w) P_k = d * wt[k * 32 + w c / 8].
+// Direct tables from the window tables (wt[k * 32 + u] = 2^(8u) P_k): lane
+// (k, w, d) -> d * 2^(c w) P_k = d * 2^r * wt[k * 32 + u], c w = 8u + r.
 __global__ void __launch_bounds__(64) k_dt_build(const uint32_t* __restrict__ wt, uint32_t ngen, DtGeom dg,
                                                  uint32_t* __restrict__ dt) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t half = dt_half(dg);
-  if (i >= (size_t)ngen * dg.W * half) return;
-  const uint32_t d = (uint32_t)(i & (half - 1)) + 1u;
+  if (i >= (size_t)ngen * dg.W * dg.H) return;
+  const uint32_t d = (uint32_t)(i & (dg.H - 1)) + 1u;
   const size_t kw = i >> (dg.c - 1);  // k * W + w
   const uint32_t k = (uint32_t)(kw / dg.W), w = (uint32_t)(kw % dg.W);
-  const ge_p3 Q = ge_from_niels(load_niels(wt, k * 32u + w * (dg.c / 8u)));
+  const uint32_t bit = dg.c * w;
+  ge_p3 Q = ge_from_niels(load_niels(wt, k * 32u + (bit >> 3)));
+  for (uint32_t r = 0; r < (bit & 7u); ++r) Q = ge_dbl(Q);
   ge_p3 R = Q;
   const int top = 31 - __clz(d);
   for (int b = top - 1; b >= 0; --b) {

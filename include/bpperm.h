@@ -71,6 +71,14 @@ int bpp_ctx_profile(bpp_ctx* ctx, int enable);
  * ("msm_accumulate", "msm_reduce", "msm_count", "msm_scatter", ...). */
 int bpp_ctx_profile_get(bpp_ctx* ctx, const char* stage, double* ms, uint64_t* launches);
 void bpp_ctx_profile_reset(bpp_ctx* ctx);
+/* Algorithmic work issued on this context (and its child streams) since the
+ * last reset, counted at launch time: "msm_terms" (scalar-point terms of every
+ * MSM and Pedersen commitment), "madds" (mixed additions of a table point:
+ * direct-table MSMs count every window of every term), "padds" (additions of
+ * two extended points in trees and bucket reductions), "msm_launches".  The
+ * roofline of the proof path (96 B x terms) reads these. */
+int bpp_ctx_work_get(bpp_ctx* ctx, const char* name, uint64_t* value);
+void bpp_ctx_work_reset(bpp_ctx* ctx);
 
 /* Device memory helpers, so callers can stage inputs resident in HBM. */
 int bpp_dev_alloc(bpp_ctx* ctx, size_t bytes, void** dptr);

@@ -36,8 +36,8 @@ def _check_sample(seeds, proofs, Vs, picks):
 def test_config4_eight_batches_in_flight_bit_exact():
     import bpperm
     ctxs = [bpperm.Context(0) for _ in range(S)]
-    gens = [bpperm.Gens(c, 128) for c in ctxs]
-    provers = [bpperm.PermProver(g, K) for g in gens]
+    gens = bpperm.Gens(ctxs[0], 128)  # one resident generator set, as bench.py
+    provers = [bpperm.PermProver(gens, K, ctx=c) for c in ctxs]
     out = [None] * S
     errs = []
 
@@ -70,8 +70,7 @@ def test_config4_eight_batches_in_flight_bit_exact():
     Vbad = list(Vs)
     Vbad[10], Vbad[11] = Vbad[11], Vbad[10]
     assert not provers[3].verify_batch(proofs, Vbad)
-    for g in gens:
-        g.close()
+    gens.close()
     for c in ctxs:
         c.close()
 
@@ -126,9 +125,7 @@ def test_shared_fresh_gens_across_threads():
 
     def run(s):
         try:
-            # PermProver binds gens.ctx; prove through the other context's stream
-            pr = bpperm.PermProver(g, K)
-            pr.ctx = others[s]
+            pr = bpperm.PermProver(g, K, ctx=others[s])
             out[s] = pr.prove_batch([55_000 + 100 * s + i for i in range(16)])
         except Exception as e:
             errs.append(e)

@@ -18,10 +18,15 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 128
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 6
 provers = []
+shared = None
 for t in range(T):
     ctx = bpperm.Context(0)
-    g = bpperm.Gens(ctx, 128)
-    pr = bpperm.PermProver(g, 52)
+    if os.environ.get("SHARED_GENS"):  # one resident generator set for every context
+        shared = shared or bpperm.Gens(ctx, 128)
+        g = shared
+    else:
+        g = bpperm.Gens(ctx, 128)
+    pr = bpperm.PermProver(g, 52, ctx=ctx)
     pr.prove_batch(list(range(B)))
     pr.prove_batch(list(range(B)))
     provers.append(pr)

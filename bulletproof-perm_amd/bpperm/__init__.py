@@ -114,7 +114,7 @@ class Context:
     def profile_reset(self):
         self.lib.bpp_ctx_profile_reset(self.h)
 
-    WORK_COUNTERS = ("msm_terms", "madds", "padds", "msm_launches")
+    WORK_COUNTERS = ("msm_terms", "madds", "padds", "msm_launches", "dt_terms", "dt_madds", "dt_launches")
 
     def work(self) -> dict:
         """Algorithmic work issued on this context since the last work_reset

@@ -656,6 +656,9 @@ static int msm_multi_dt_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t
   ctx_work(ctx, "madds", (uint64_t)T * dg.W);
   ctx_work(ctx, "padds", (uint64_t)M * (nt - 1));
   ctx_work(ctx, "msm_launches", 1);
+  ctx_work(ctx, "dt_terms", T);  // the direct-table kernel's own share
+  ctx_work(ctx, "dt_madds", (uint64_t)T * dg.W);
+  ctx_work(ctx, "dt_launches", 1);
   {
     ProfScope ps(ctx, "msm_direct");
     hipLaunchKernelGGL(k_dt_msm, dim3(M), dim3(nt), (size_t)nt * P3_BYTES, ctx->stream, pts.dt, dg, d_scal, d_pidx,

@@ -75,7 +75,8 @@ void bpp_ctx_profile_reset(bpp_ctx* ctx);
  * last reset, counted at launch time: "msm_terms" (scalar-point terms of every
  * MSM and Pedersen commitment), "madds" (mixed additions of a table point:
  * direct-table MSMs count every window of every term), "padds" (additions of
- * two extended points in trees and bucket reductions), "msm_launches".  The
+ * two extended points in trees and bucket reductions), "msm_launches", and
+ * the direct-table kernel's own "dt_terms" / "dt_madds" / "dt_launches".  The
  * roofline of the proof path (96 B x terms) reads these. */
 int bpp_ctx_work_get(bpp_ctx* ctx, const char* name, uint64_t* value);
 void bpp_ctx_work_reset(bpp_ctx* ctx);

@@ -23,7 +23,8 @@ from ._lib import BppError, check
 
 MSM_INFLIGHT = 4  # BPP_MSM_INFLIGHT (include/bpperm.h)
 
-__all__ = ["Context", "PointTable", "BppError", "vartime_multiscalar_mul", "default_context"]
+__all__ = ["Context", "PointTable", "BppError", "vartime_multiscalar_mul", "default_context", "VerifyJob",
+           "partials_is_identity"]
 
 
 def _buf(b: bytes):
@@ -450,3 +451,88 @@ class PermProver:
             return False
         check(rc, "bpp_perm_verify_batch", self.ctx.h)
         return True
+
+    def verify_job(self, proofs: Sequence[bytes], Vs: Sequence[bytes]) -> "VerifyJob":
+        """Host phase of a batch verification that may be split over GPUs."""
+        return VerifyJob(self.k, proofs, Vs, self.label)
+
+    def verify_partial(self, job: "VerifyJob", r_all: bytes, first: int, w_begin: int, w_end: int) -> bytes:
+        """128-B raw partial of job's MSM over windows [w_begin, w_end) (see
+        bpp_perm_verify_partial); r_all = every rank's r challenges."""
+        part = C.create_string_buffer(128)
+        check(self.ctx.lib.bpp_perm_verify_partial(self.ctx.h, self.gens.h, job.h, _buf(r_all), len(r_all) // 32,
+                                                   first, w_begin, w_end, part),
+              "bpp_perm_verify_partial", self.ctx.h)
+        return part.raw
+
+
+class VerifyJob:
+    """Parsed proofs with their transcripts replayed (host only, no GPU):
+    bpp_perm_verify_begin.  `r` holds each proof's weight challenge; the
+    batch weights are derived from every rank's r (r_all)."""
+
+    def __init__(self, k: int, proofs: Sequence[bytes], Vs: Sequence[bytes], label: bytes = b"bp-perm"):
+        self.lib = _lib.load()
+        self.k = k
+        self.count = len(proofs)
+        h = C.c_void_p()
+        r = C.create_string_buffer(32 * self.count + 1)
+        rc = self.lib.bpp_perm_verify_begin(k, self.count, _buf(label), len(label), _buf(b"".join(proofs)),
+                                            _buf(b"".join(Vs)), r, C.byref(h))
+        if rc == 6:
+            self.h = None
+            self.r = None
+            return
+        check(rc, "bpp_perm_verify_begin")
+        self.h = h
+        self.r = r.raw[:32 * self.count]
+
+    @property
+    def ok(self) -> bool:
+        """False if a proof was malformed (the batch cannot verify)."""
+        return self.h is not None
+
+    def terms(self) -> int:
+        n = C.c_size_t()
+        check(self.lib.bpp_perm_verify_terms(self.h, C.byref(n)), "bpp_perm_verify_terms")
+        return n.value
+
+    def windows(self) -> tuple[int, int]:
+        return msm_windows(self.terms())
+
+    def scalars(self, r_all: bytes, first: int):
+        """(scalars, proof-point encodings) of the job's MSM (host): the
+        first 2 n_p + 2 scalars go to G[0..n_p), H[0..n_p), B, B_blinding."""
+        T = self.terms()
+        n_p = 1
+        while n_p < 2 * self.k:
+            n_p <<= 1
+        npts = T - (2 * n_p + 2)
+        sc = C.create_string_buffer(32 * T)
+        pts = C.create_string_buffer(32 * max(npts, 1))
+        check(self.lib.bpp_perm_verify_scalars(self.h, _buf(r_all), len(r_all) // 32, first, sc, pts),
+              "bpp_perm_verify_scalars")
+        sraw, praw = sc.raw, pts.raw
+        return ([sraw[32 * i: 32 * i + 32] for i in range(T)], [praw[32 * i: 32 * i + 32] for i in range(npts)])
+
+    def close(self):
+        if self.h is not None:
+            self.lib.bpp_perm_verify_end(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def partials_is_identity(partials: Sequence[bytes]) -> bool:
+    """True iff the raw partial points add up to the identity."""
+    raw = _join(partials, 128, "partial")
+    rc = _lib.load().bpp_partials_is_identity(_buf(raw), len(partials))
+    if rc == 6:
+        return False
+    check(rc, "bpp_partials_is_identity")
+    return True
+

@@ -83,6 +83,12 @@ SIGNATURES = {
     "bpp_perm_prove_batch": (i32, [vp, vp, u32, sz, vp, vp, sz, vp, vp]),
     "bpp_perm_verify": (i32, [vp, vp, u32, vp, sz, vp, sz, vp]),
     "bpp_perm_verify_batch": (i32, [vp, vp, u32, sz, vp, sz, vp, vp]),
+    "bpp_perm_verify_begin": (i32, [u32, sz, vp, sz, vp, vp, vp, C.POINTER(vp)]),
+    "bpp_perm_verify_terms": (i32, [vp, C.POINTER(sz)]),
+    "bpp_perm_verify_scalars": (i32, [vp, vp, sz, sz, vp, vp]),
+    "bpp_perm_verify_partial": (i32, [vp, vp, vp, vp, sz, sz, u32, u32, vp]),
+    "bpp_perm_verify_end": (None, [vp]),
+    "bpp_partials_is_identity": (i32, [vp, sz]),
 }
 
 _lib = None

@@ -15,6 +15,14 @@
 2. Independent proofs (config 4): proof i -> rank i mod world; no
    collective on the data path.
 
+3. Batch verification (config 5): the weighted checks of all proofs form
+   ONE MSM (bpp_perm_verify_*).  Window split (north_star): every rank
+   replays every proof and runs its window range; the 128-byte partials are
+   all-gathered and must add up to the identity.  Proof split: each rank
+   replays only its slice, the 32-byte weight challenges r are all-gathered
+   (the batch weights depend on every proof), each rank runs all windows of
+   its slice's MSM, then the same 128-byte exchange.
+
 The functions take the collective as a callable so the same code runs over
 RCCL on GPUs (bench.py) and over gloo on CPU (tests/test_dist_gloo.py).
 """
@@ -73,3 +81,53 @@ def torch_all_gather_bytes(payload: bytes, device=None) -> list[bytes]:
     out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
     dist.all_gather(out, t)
     return [o.cpu().numpy().tobytes() for o in out]
+
+
+def torch_all_gather_bytes_var(payload: bytes, device=None) -> list[bytes]:
+    """all_gather of per-rank payloads of different lengths (sizes first,
+    then the payloads padded to the longest)."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size()
+    n = torch.tensor([len(payload)], dtype=torch.int64, device=device)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n)
+    sizes = [int(x.item()) for x in sizes]
+    mx = max(max(sizes), 1)
+    t = torch.zeros(mx, dtype=torch.uint8)
+    if payload:
+        t[:len(payload)] = torch.frombuffer(bytearray(payload), dtype=torch.uint8)
+    if device is not None:
+        t = t.to(device)
+    out = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [o.cpu().numpy().tobytes()[:sz] for o, sz in zip(out, sizes)]
+
+
+def distributed_verify(prover, proofs, Vs, rank: int, world: int, split: str = "windows", device=None) -> bool:
+    """Batch-verify `proofs` (all of them, identical on every rank) with the
+    MSM partitioned over the ranks (split = "windows" or "proofs")."""
+    import bpperm
+
+    if split == "windows":
+        job = bpperm.VerifyJob(prover.k, proofs, Vs, prover.label)
+        ok = job.ok
+        if ok:
+            wb, we = window_ranges(job.windows()[1], world)[rank]
+            part = prover.verify_partial(job, job.r, 0, wb, we)
+        else:
+            part = bytes(128)
+        job.close()
+    else:
+        b, e = point_ranges(len(proofs), world)[rank]
+        job = bpperm.VerifyJob(prover.k, proofs[b:e], Vs[b:e], prover.label)
+        ok = job.ok
+        r_all = b"".join(torch_all_gather_bytes_var(job.r if ok else bytes(32 * (e - b)), device))
+        part = prover.verify_partial(job, r_all, b, 0, job.windows()[1]) if ok else bytes(128)
+        job.close()
+    parts = torch_all_gather_bytes(part, device)
+    # a rank that rejected a proof in its replay vetoes the batch
+    flags = torch_all_gather_bytes(bytes([1 if ok else 0]), device)
+    return all(f == b"\x01" for f in flags) and bpperm.partials_is_identity(parts)
+

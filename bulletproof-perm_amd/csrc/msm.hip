@@ -277,9 +277,10 @@ h25519::ge horner_host_terms(const uint32_t* ws_words, uint32_t Wn, uint32_t nte
   return acc;
 }
 
-// Single MSM over device scalars + resident table, windows [wb, wb+Wn).
+// Single MSM over device scalars + resident table(s), windows [wb, wb+Wn).
+// Point index i < n0 reads d_tbl[i], otherwise d_tbl1[i - n0].
 int msm_single_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const uint32_t* d_tbl, size_t n,
-                   uint32_t c, uint32_t wb, uint32_t Wn, h25519::ge* out) {
+                   uint32_t c, uint32_t wb, uint32_t Wn, h25519::ge* out, const uint32_t* d_tbl1, uint32_t n0) {
   if (n == 0 || Wn == 0) {
     *out = h25519::ge_identity();
     return BPP_OK;
@@ -289,8 +290,8 @@ int msm_single_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx,
   // latency-bound and would run G times)
   uint32_t* d_ws = nullptr;
   uint32_t nterms = 1;
-  BPP_TRY(msm_engine(ctx, d_scal, d_pidx, nullptr, 1, (uint32_t)n, c, wb, Wn, d_tbl, &d_ws, nullptr, 0xffffffffu,
-                     false, &nterms));
+  BPP_TRY(msm_engine(ctx, d_scal, d_pidx, nullptr, 1, (uint32_t)n, c, wb, Wn, d_tbl, &d_ws, d_tbl1, n0, false,
+                     &nterms));
   void* h = nullptr;
   BPP_TRY(ctx_pinned(ctx, (size_t)Wn * nterms * P3_BYTES, &h));
   BPP_HIP(hipMemcpyAsync(h, d_ws, (size_t)Wn * nterms * P3_BYTES, hipMemcpyDeviceToHost, ctx->stream));

@@ -19,7 +19,8 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
 // Host Horner over such terms: sum_j 2^(c (wb + j)) * window_j.
 h25519::ge horner_host_terms(const uint32_t* ws_words, uint32_t Wn, uint32_t nterms, uint32_t c, uint32_t wb);
 int msm_single_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const uint32_t* d_tbl, size_t n,
-                   uint32_t c, uint32_t wb, uint32_t Wn, h25519::ge* out);
+                   uint32_t c, uint32_t wb, uint32_t Wn, h25519::ge* out, const uint32_t* d_tbl1 = nullptr,
+                   uint32_t n0 = 0xffffffffu);
 int upload_scalars(bpp_ctx* ctx, const uint8_t* scalars, size_t n, const char* name, uint32_t** d_out);
 int points_compress_p3(bpp_ctx* ctx, const uint32_t* d_p3, size_t n, uint8_t* out_host);
 // out = encodings of 2 * P_i (host batch encoding; see points.hip)

@@ -429,11 +429,12 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
   return BPP_OK;
 }
 
-// Verifier: host scalars for one proof.  gen_sc (2n_p + 2: G, H, B, Bb) is
-// ACCUMULATED with weight `wt`; proof-point scalars (m + 8 + 2lg, order
-// V, A_I, A_O, S, T1..T6, L.., R..) are appended to pt_sc.
-bool verify_scalars(const perm::Circuit& C, const Proof& P, merlin::Transcript& tr, const Sc& wt,
-                    std::vector<Sc>& gen_sc, std::vector<Sc>& pt_sc, Sc* weight_challenge) {
+// Verifier: host scalars for one proof, unweighted (the batch weight is
+// applied when the batch is merged, verify_terms_weighted).  gen_sc (2n_p +
+// 2: G, H, B, Bb) is set; proof-point scalars (m + 8 + 2lg, order V, A_I,
+// A_O, S, T1..T6, L.., R..) are appended to pt_sc.
+bool verify_scalars(const perm::Circuit& C, const Proof& P, merlin::Transcript& tr, std::vector<Sc>& gen_sc,
+                    std::vector<Sc>& pt_sc, Sc* weight_challenge) {
   const uint32_t k = C.k, n_p = C.n_p, m = C.m;
   if (P.V.size() != m) return false;
   tr.arithmetic_domain_sep(n_p);
@@ -472,7 +473,7 @@ bool verify_scalars(const perm::Circuit& C, const Proof& P, merlin::Transcript& 
   using hsc::sub;
   Sc delta = hsc::zero();
   for (uint32_t i = 0; i < n_p; ++i) delta = add(delta, mul(mul(y_inv_n[i], zWR[i]), zWL[i]));
-  const Sc aR_ = hsc::to_mont(P.ipa.a), bR_ = hsc::to_mont(P.ipa.b), xR_ = hsc::to_mont(x), wtR = hsc::to_mont(wt);
+  const Sc aR_ = hsc::to_mont(P.ipa.a), bR_ = hsc::to_mont(P.ipa.b), xR_ = hsc::to_mont(x);
   const Sc zc = hsc::inner_product(zq, c);
   const Sc a = P.ipa.a, b = P.ipa.b;
   // generators (merged t-check and IPA-check scalars)
@@ -482,22 +483,23 @@ bool verify_scalars(const perm::Circuit& C, const Proof& P, merlin::Transcript& 
     const Sc hi = add(sub(hsc::mulm(hsc::mulm(s[n_p - 1 - i], bR_), yiR),
                           hsc::mulm(add(hsc::mulm(zWL[i], xR_), zWO[i]), yiR)),
                       hsc::one());
-    gen_sc[i] = add(gen_sc[i], hsc::mulm(gi, wtR));
-    gen_sc[n_p + i] = add(gen_sc[n_p + i], hsc::mulm(hi, wtR));
+    gen_sc[i] = gi;
+    gen_sc[n_p + i] = hi;
   }
   const Sc tcheck_B = mul(r, sub(P.t_hat, mul(xp[2], add(delta, zc))));
   const Sc ipa_B = mul(w, sub(mul(a, b), P.t_hat));
-  gen_sc[2 * n_p] = add(gen_sc[2 * n_p], mul(wt, add(tcheck_B, ipa_B)));
-  gen_sc[2 * n_p + 1] = add(gen_sc[2 * n_p + 1], mul(wt, add(mul(r, P.tau_x), P.mu)));
+  gen_sc[2 * n_p] = add(tcheck_B, ipa_B);
+  gen_sc[2 * n_p + 1] = add(mul(r, P.tau_x), P.mu);
   // proof points
-  for (uint32_t j = 0; j < m; ++j) pt_sc.push_back(mul(wt, neg(mul(mul(r, xp[2]), zWV[j]))));
-  pt_sc.push_back(mul(wt, neg(x)));
-  pt_sc.push_back(mul(wt, neg(xp[2])));
-  pt_sc.push_back(mul(wt, neg(xp[3])));
+  const Sc rx2R = hsc::to_mont(mul(r, xp[2]));
+  for (uint32_t j = 0; j < m; ++j) pt_sc.push_back(neg(hsc::mulm(zWV[j], rx2R)));
+  pt_sc.push_back(neg(x));
+  pt_sc.push_back(neg(xp[2]));
+  pt_sc.push_back(neg(xp[3]));
   const int tidx[5] = {1, 3, 4, 5, 6};
-  for (int i = 0; i < 5; ++i) pt_sc.push_back(mul(wt, neg(mul(r, xp[tidx[i]]))));
-  for (uint32_t j = 0; j < C.lg; ++j) pt_sc.push_back(mul(wt, neg(u_sq[j])));
-  for (uint32_t j = 0; j < C.lg; ++j) pt_sc.push_back(mul(wt, neg(uinv_sq[j])));
+  for (int i = 0; i < 5; ++i) pt_sc.push_back(neg(mul(r, xp[tidx[i]])));
+  for (uint32_t j = 0; j < C.lg; ++j) pt_sc.push_back(neg(u_sq[j]));
+  for (uint32_t j = 0; j < C.lg; ++j) pt_sc.push_back(neg(uinv_sq[j]));
   return true;
 }
 
@@ -512,91 +514,159 @@ void proof_points(const Proof& P, std::vector<uint8_t>& enc) {
   for (auto& r : P.ipa.R) add(r);
 }
 
-// Verify `count` proofs with ONE MSM: generator scalars summed across proofs
-// with per-proof weights from a batch transcript.
-int verify_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const uint8_t* label, size_t llen,
-                 size_t count, const uint8_t* proofs, size_t proof_stride, const uint8_t* V) {
+}  // namespace
+
+// A batch verification split into its host replay (begin) and its weighted
+// MSM (partial), so that the MSM can be partitioned over GPUs: by bucket
+// windows (every rank holds every proof) or by proofs (each rank holds a
+// slice; only the r challenges are exchanged before the MSM).
+struct bpp_verify_job {
+  perm::Circuit C;
+  size_t count = 0, npt = 0;
+  std::vector<Proof> Ps;
+  std::vector<Sc> rs;                         // per-proof weight challenges
+  std::vector<std::vector<Sc>> gen_p, pt_p;  // unweighted generator / proof-point scalars
+};
+
+namespace {
+
+// pass 1 (parallel over proofs): parse, replay each transcript, and collect
+// the unweighted generator / proof-point scalars and the proof's weight
+// challenge r (circuit_lib.rs:478-585 restated in sound mode)
+int verify_begin(const perm::Circuit& C, const uint8_t* label, size_t llen, size_t count, const uint8_t* proofs,
+                 size_t proof_stride, const uint8_t* V, std::unique_ptr<bpp_verify_job>& job) {
   const uint32_t n_p = C.n_p;
+  job.reset(new bpp_verify_job);
+  bpp_verify_job& J = *job;
+  J.C = C;
+  J.count = count;
+  J.Ps.resize(count);
+  J.rs.resize(count);
+  J.gen_p.resize(count);
+  J.pt_p.resize(count);
+  std::vector<uint8_t> ok(count, 0);
+  par::for_each(count, [&](size_t p) {
+    if (!deserialize(C, proofs + p * proof_stride, perm::proof_len(C.k), V + p * 32 * C.m, J.Ps[p])) return;
+    merlin::Transcript tr(label, llen);
+    J.gen_p[p].assign(2 * n_p + 2, hsc::zero());
+    ok[p] = verify_scalars(C, J.Ps[p], tr, J.gen_p[p], J.pt_p[p], &J.rs[p]) ? 1 : 0;
+  });
+  for (size_t p = 0; p < count; ++p)
+    if (!ok[p]) return BPP_ERR_VERIFY;
+  J.npt = count ? J.pt_p[0].size() : 0;
+  return BPP_OK;
+}
+
+// Terms of the job's MSM: merged generators (G, H, B, Bb) + every proof point.
+size_t verify_terms(const bpp_verify_job& J) { return 2 * (size_t)J.C.n_p + 2 + J.count * J.npt; }
+
+// Per-proof weights from a batch transcript over all `total` r challenges
+// (a single proof keeps weight one).
+std::vector<Sc> batch_weights(const Sc* r_all, size_t total) {
+  std::vector<Sc> wts(total, hsc::one());
+  if (total > 1) {
+    merlin::Transcript batch((const uint8_t*)"bp-perm-batch-verify", 20);
+    for (size_t p = 0; p < total; ++p) batch.append_scalar("r", r_all[p]);
+    for (size_t p = 0; p < total; ++p) wts[p] = batch.challenge_scalar("proof-weight");
+  }
+  return wts;
+}
+
+// pass 2 (host): the job's MSM terms with its proofs weighted by
+// wts[first + p] -- generator scalars merged across its proofs (G[0..n_p),
+// H[0..n_p), B, Bb), then each proof's points (V, A_I, A_O, S, T1..T6, L..,
+// R..) weighted by their proof's weight; enc = those points' encodings.
+int verify_terms_weighted(const bpp_verify_job& J, const Sc* r_all, size_t total, size_t first, std::vector<Sc>& sc,
+                          std::vector<uint8_t>& enc) {
+  const uint32_t n_p = J.C.n_p;
+  const size_t count = J.count, npt = J.npt;
+  if (first > total || count > total - first) return BPP_ERR_ARG;
+  std::vector<Sc> wR = batch_weights(r_all, total);  // -> Montgomery form (one step per product)
+  for (auto& w : wR) w = hsc::to_mont(w);
+  const Sc* wts = wR.data() + first;
+  const size_t NG = 2 * (size_t)n_p + 2;
+  sc.assign(NG + count * npt, hsc::zero());
+  enc.assign(count * npt * 32, 0);
+  // proof chunks with private generator accumulators (each reads its proofs'
+  // rows contiguously), summed at the end
+  const size_t chunks = std::max<size_t>(1, std::min<size_t>(count, 64));
+  std::vector<std::vector<Sc>> acc(chunks, std::vector<Sc>(NG, hsc::zero()));
+  par::for_each(chunks, [&](size_t ch) {
+    std::vector<Sc>& a = acc[ch];
+    std::vector<uint8_t> e;
+    for (size_t p = ch * count / chunks; p < (ch + 1) * count / chunks; ++p) {
+      const Sc& w = wts[p];
+      for (size_t i = 0; i < NG; ++i) a[i] = hsc::add(a[i], hsc::mulm(J.gen_p[p][i], w));
+      for (size_t j = 0; j < npt; ++j) sc[NG + p * npt + j] = hsc::mulm(J.pt_p[p][j], w);
+      e.clear();
+      proof_points(J.Ps[p], e);
+      memcpy(&enc[p * npt * 32], e.data(), npt * 32);
+    }
+  });
+  for (size_t ch = 0; ch < chunks; ++ch)
+    for (size_t i = 0; i < NG; ++i) sc[i] = hsc::add(sc[i], acc[ch][i]);
+  return BPP_OK;
+}
+
+// pass 2 (device): ONE MSM over the job's terms, windows [wb, we) of its
+// c-bit signed digits (c = msm_choose_c(terms)) -> raw partial point.
+int verify_partial(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J, const Sc* r_all, size_t total,
+                   size_t first, uint32_t wb, uint32_t we, h25519::ge* out) {
+  const uint32_t n_p = J.C.n_p;
   if (G->n < n_p) {
     ctx->err = "generators shorter than the padded circuit";
     return BPP_ERR_LEN;
   }
-  // pass 1 (parallel over proofs): parse, replay each transcript, and
-  // collect the unweighted generator / proof-point scalars and the proof's
-  // weight challenge r
-  std::vector<Proof> Ps(count);
-  std::vector<Sc> rs(count);
-  std::vector<std::vector<Sc>> gen_p(count), pt_p(count);
-  std::vector<uint8_t> ok(count, 0);
-  par::for_each(count, [&](size_t p) {
-    if (!deserialize(C, proofs + p * proof_stride, perm::proof_len(C.k), V + p * 32 * C.m, Ps[p])) return;
-    merlin::Transcript tr(label, llen);
-    gen_p[p].assign(2 * n_p + 2, hsc::zero());
-    ok[p] = verify_scalars(C, Ps[p], tr, hsc::one(), gen_p[p], pt_p[p], &rs[p]) ? 1 : 0;
-  });
-  for (size_t p = 0; p < count; ++p)
-    if (!ok[p]) return BPP_ERR_VERIFY;
-  // per-proof weights from a batch transcript over all r (serial, cheap)
-  std::vector<Sc> wts(count, hsc::one());
-  if (count > 1) {
-    merlin::Transcript batch((const uint8_t*)"bp-perm-batch-verify", 20);
-    for (size_t p = 0; p < count; ++p) batch.append_scalar("r", rs[p]);
-    for (size_t p = 0; p < count; ++p) wts[p] = batch.challenge_scalar("proof-weight");
-  }
-  // pass 2: weighted sums (generators merged across proofs; proof points
-  // each weighted by their proof's weight)
-  const size_t npt = pt_p[0].size();
-  std::vector<Sc> gen_sc(2 * n_p + 2, hsc::zero());
-  std::vector<Sc> pt_sc(count * npt);
   const size_t NG = 2 * (size_t)n_p + 2;
-  const size_t gchunks = std::min<size_t>(NG, 64);
-  par::for_each(gchunks, [&](size_t c) {
-    for (size_t i = c * NG / gchunks; i < (c + 1) * NG / gchunks; ++i) {
-      Sc acc = hsc::zero();
-      for (size_t p = 0; p < count; ++p) acc = hsc::add(acc, hsc::mul(wts[p], gen_p[p][i]));
-      gen_sc[i] = acc;
-    }
-  });
-  std::vector<uint8_t> enc(count * (npt * 32));
-  par::for_each(count, [&](size_t p) {
-    for (size_t j = 0; j < npt; ++j) pt_sc[p * npt + j] = hsc::mul(wts[p], pt_p[p][j]);
-    std::vector<uint8_t> e;
-    e.reserve(npt * 32);
-    proof_points(Ps[p], e);
-    memcpy(&enc[p * npt * 32], e.data(), npt * 32);
-  });
+  std::vector<Sc> sc;
+  std::vector<uint8_t> enc;
+  {
+    HostScope hs(ctx, "verify_terms");
+    BPP_TRY(verify_terms_weighted(J, r_all, total, first, sc, enc));
+  }
   uint32_t* d_x = nullptr;
   int rc = decompress_ws(ctx, enc.data(), enc.size() / 32, "pv_x", &d_x);
   if (rc == BPP_ERR_DECOMPRESS) return BPP_ERR_VERIFY;
   BPP_TRY(rc);
+  // term t reads generator t of the resident table (G[0..n_p), H[0..n_p),
+  // B, Bb) or proof point t - NG; the index list is needed only when the
+  // generator set is longer than the padded circuit
   const uint32_t n0 = (uint32_t)(2 * G->n + 2);
-  std::vector<Sc> sc;
-  std::vector<uint32_t> idx;
-  for (uint32_t i = 0; i < n_p; ++i) {
-    sc.push_back(gen_sc[i]);
-    idx.push_back(G->gidx(i));
+  uint32_t* d_idx = nullptr;
+  if (G->n != n_p) {
+    std::vector<uint32_t> idx(sc.size());
+    for (uint32_t i = 0; i < n_p; ++i) {
+      idx[i] = G->gidx(i);
+      idx[n_p + i] = G->hidx(i);
+    }
+    idx[2 * n_p] = G->bidx();
+    idx[2 * n_p + 1] = G->bbidx();
+    for (size_t j = NG; j < sc.size(); ++j) idx[j] = n0 + (uint32_t)(j - NG);
+    void* d = nullptr;
+    BPP_TRY(ctx_ws(ctx, "pv_idx", idx.size() * 4 + 4, &d));
+    BPP_TRY(ctx_h2d(ctx, d, idx.data(), idx.size() * 4));
+    d_idx = (uint32_t*)d;
   }
-  for (uint32_t i = 0; i < n_p; ++i) {
-    sc.push_back(gen_sc[n_p + i]);
-    idx.push_back(G->hidx(i));
+  uint32_t* d_s = nullptr;
+  BPP_TRY(upload_sc(ctx, sc, "pv_s", &d_s));
+  const uint32_t c = msm_choose_c((double)sc.size());
+  return msm_single_dev(ctx, d_s, d_idx, G->d_tbl, sc.size(), c, wb, we - wb, out, d_x, n0);
+}
+
+// Verify `count` proofs with ONE MSM: generator scalars summed across proofs
+// with per-proof weights from a batch transcript.
+int verify_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const uint8_t* label, size_t llen,
+                 size_t count, const uint8_t* proofs, size_t proof_stride, const uint8_t* V) {
+  std::unique_ptr<bpp_verify_job> job;
+  {
+    HostScope hs(ctx, "verify_replay");
+    BPP_TRY(verify_begin(C, label, llen, count, proofs, proof_stride, V, job));
   }
-  sc.push_back(gen_sc[2 * n_p]);
-  idx.push_back(G->bidx());
-  sc.push_back(gen_sc[2 * n_p + 1]);
-  idx.push_back(G->bbidx());
-  for (size_t j = 0; j < pt_sc.size(); ++j) {
-    sc.push_back(pt_sc[j]);
-    idx.push_back(n0 + (uint32_t)j);
-  }
-  std::vector<h25519::ge> res;
-  MsmPoints pts;
-  BPP_TRY(gens_points(ctx, G, &pts));
-  const uint32_t per = 3 + 5 * n_p;  // A_I/A_O/S terms per proof
-  uint32_t* d_s = nullptr;           // their scalars, reused by the polynomial stage
-  BPP_TRY(msm_points_extra(ctx, &pts, d_x, (uint32_t)(enc.size() / 32), n0, "pv_x_wt", (double)sc.size()));
-  BPP_TRY(msm_terms(ctx, sc, idx, {0, (uint32_t)sc.size()}, pts, res));
+  const uint32_t c = msm_choose_c((double)verify_terms(*job));
+  h25519::ge res;
+  BPP_TRY(verify_partial(ctx, G, *job, job->rs.data(), count, 0, 0, (254 + c - 1) / c, &res));
   uint8_t e[32];
-  h25519::encode(e, res[0]);
+  h25519::encode(e, res);
   static const uint8_t zero[32] = {0};
   return memcmp(e, zero, 32) == 0 ? BPP_OK : BPP_ERR_VERIFY;
 }
@@ -701,6 +771,68 @@ int bpp_perm_verify_batch(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, size_t co
   BPP_HIP(hipSetDevice(ctx->device));
   const perm::Circuit C = perm::build(k);
   return verify_batch(ctx, G, C, label, llen, count, proofs, perm::proof_len(k), V);
+}
+
+int bpp_perm_verify_begin(uint32_t k, size_t count, const uint8_t* label, size_t llen, const uint8_t* proofs,
+                          const uint8_t* V, uint8_t* r_out, bpp_verify_job** out) {
+  if (!out || ((!proofs || !V) && count) || (!label && llen) || k < 2 || k > (1u << 20)) return BPP_ERR_ARG;
+  *out = nullptr;
+  const perm::Circuit C = perm::build(k);
+  std::unique_ptr<bpp_verify_job> job;
+  BPP_TRY(verify_begin(C, label, llen, count, proofs, perm::proof_len(k), V, job));
+  if (r_out)
+    for (size_t p = 0; p < count; ++p) hsc::to_bytes(r_out + 32 * p, job->rs[p]);
+  *out = job.release();
+  return BPP_OK;
+}
+
+int bpp_perm_verify_terms(const bpp_verify_job* job, size_t* terms) {
+  if (!job || !terms) return BPP_ERR_ARG;
+  *terms = verify_terms(*job);
+  return BPP_OK;
+}
+
+static int parse_rs(const uint8_t* r_all, size_t total, std::vector<Sc>& rs) {
+  rs.resize(total);
+  for (size_t p = 0; p < total; ++p)
+    if (!hsc::from_canonical(rs[p], r_all + 32 * p)) return BPP_ERR_NONCANONICAL;
+  return BPP_OK;
+}
+
+int bpp_perm_verify_scalars(const bpp_verify_job* job, const uint8_t* r_all, size_t total, size_t first,
+                            uint8_t* scalars_out, uint8_t* points_out) {
+  if (!job || (!r_all && total) || !scalars_out || (!points_out && job->count)) return BPP_ERR_ARG;
+  std::vector<Sc> rs, sc;
+  std::vector<uint8_t> enc;
+  BPP_TRY(parse_rs(r_all, total, rs));
+  BPP_TRY(verify_terms_weighted(*job, rs.data(), total, first, sc, enc));
+  for (size_t i = 0; i < sc.size(); ++i) hsc::to_bytes(scalars_out + 32 * i, sc[i]);
+  if (!enc.empty()) memcpy(points_out, enc.data(), enc.size());
+  return BPP_OK;
+}
+
+int bpp_perm_verify_partial(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job* job, const uint8_t* r_all,
+                            size_t total, size_t first, uint32_t w_begin, uint32_t w_end, uint8_t partial[128]) {
+  if (!ctx || !G || !job || !partial || (!r_all && total)) return BPP_ERR_ARG;
+  const uint32_t c = msm_choose_c((double)verify_terms(*job));
+  if (w_begin > w_end || w_end > (254 + c - 1) / c) return BPP_ERR_ARG;
+  std::vector<Sc> rs;
+  BPP_TRY(parse_rs(r_all, total, rs));
+  if (first > total || job->count > total - first) return BPP_ERR_ARG;
+  BPP_HIP(hipSetDevice(ctx->device));
+  h25519::ge r = h25519::ge_identity();
+  if (job->count) BPP_TRY(verify_partial(ctx, G, *job, rs.data(), total, first, w_begin, w_end, &r));
+  h25519::ge_to_words((uint32_t*)partial, r);
+  return BPP_OK;
+}
+
+void bpp_perm_verify_end(bpp_verify_job* job) { delete job; }
+
+int bpp_partials_is_identity(const uint8_t* partials, size_t count) {
+  uint8_t e[32];
+  BPP_TRY(bpp_partials_finish(partials, count, e));
+  static const uint8_t zero[32] = {0};
+  return memcmp(e, zero, 32) == 0 ? BPP_OK : BPP_ERR_VERIFY;
 }
 
 }  // extern "C"

@@ -225,6 +225,36 @@ int bpp_perm_verify(bpp_ctx* ctx, const bpp_gens* g, uint32_t k, const uint8_t* 
 int bpp_perm_verify_batch(bpp_ctx* ctx, const bpp_gens* g, uint32_t k, size_t count, const uint8_t* label,
                           size_t llen, const uint8_t* proofs, const uint8_t* V);
 
+/* Batch verification split for several GPUs (north_star: "the single large
+ * verifier MSM partitions its bucket windows across GPUs"; reference verify
+ * circuit_lib.rs:478-585).  Host phase, no GPU: parse `count` proofs, replay
+ * their transcripts and return each proof's weight challenge r (count x 32
+ * B, may be NULL).  BPP_ERR_VERIFY if a proof is malformed or its transcript
+ * rejects a point encoding. */
+typedef struct bpp_verify_job bpp_verify_job;
+int bpp_perm_verify_begin(uint32_t k, size_t count, const uint8_t* label, size_t llen, const uint8_t* proofs,
+                          const uint8_t* V, uint8_t* r_out, bpp_verify_job** out);
+/* Terms of the job's MSM: 2 n_p + 2 merged generators + count x (m + 8 +
+ * 2 log2 n_p) proof points.  bpp_msm_windows(terms) gives c and W. */
+int bpp_perm_verify_terms(const bpp_verify_job* job, size_t* terms);
+/* The job's MSM terms (host): proof weights come from a batch transcript
+ * over all `total` r challenges (r_all, every rank's in proof order), this
+ * job's proofs being [first, first + count).  scalars_out: terms x 32 B
+ * (G[0..n_p), H[0..n_p), B, B_blinding, then the proof points'); points_out:
+ * the proof points' encodings ((terms - 2 n_p - 2) x 32 B). */
+int bpp_perm_verify_scalars(const bpp_verify_job* job, const uint8_t* r_all, size_t total, size_t first,
+                            uint8_t* scalars_out, uint8_t* points_out);
+/* The job's MSM over bucket windows [w_begin, w_end) on this GPU -> 128-B
+ * raw partial point.  The batch verifies iff the partials of every window
+ * range (window split: every rank's job holds all proofs) or of every proof
+ * slice (proof split: all windows each) sum to the identity
+ * (bpp_partials_is_identity). */
+int bpp_perm_verify_partial(bpp_ctx* ctx, const bpp_gens* g, const bpp_verify_job* job, const uint8_t* r_all,
+                            size_t total, size_t first, uint32_t w_begin, uint32_t w_end, uint8_t partial[128]);
+void bpp_perm_verify_end(bpp_verify_job* job);
+/* BPP_OK if the partials add up to the identity, else BPP_ERR_VERIFY. */
+int bpp_partials_is_identity(const uint8_t* partials, size_t count);
+
 #ifdef __cplusplus
 }
 #endif

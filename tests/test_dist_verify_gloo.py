@@ -1,0 +1,142 @@
+"""World-size-2 gloo test of the multi-GPU batch verifier (CPU only).
+
+The product's host phase runs on every rank: bpp_perm_verify_begin parses
+and replays the transcripts of the rank's proofs and returns their weight
+challenges r; the r's are all-gathered; bpp_perm_verify_scalars builds the
+rank's weighted MSM terms.  Only the MSM itself (bpp_perm_verify_partial on
+a GPU) is replaced here by the oracle, so partition + exchange + combine
+(bpp_partials_is_identity) are checked end to end without a GPU, for both
+splits of SURVEY.md §8(e):
+
+* proof split: rank r holds proofs [first, first + count), all windows;
+* window split (north_star): every rank holds every proof, windows
+  window_ranges(W, world)[rank].
+
+Proofs come from the serial C prover (oracle/c/perm_cpu.c, byte-equal to the
+GPU prover in tests/test_gpu_perm.py).  Reference: verify,
+circuit_lib.rs:478-585."""
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+K = 2
+COUNT = 5
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, tamper, q):
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    sys.path.insert(0, str(root / "bulletproof-perm_amd"))
+    sys.path.insert(0, str(root))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+
+    import bpperm
+    from bpperm import dist as bdist
+    from oracle import cport
+    from oracle import ristretto as r255
+    from oracle.merlin import bulletproof_gens, pedersen_gens_default
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        proofs, Vs = [], []
+        for s in range(COUNT):
+            pf, V = cport.cpu_prove(K, 100 + s)
+            if tamper and s == 3:  # t_hat + 1 (still canonical): must be rejected
+                t = int.from_bytes(pf[8 * 32 + 64: 8 * 32 + 96], "little")
+                pf = pf[:8 * 32 + 64] + ((t + 1) % r255.L).to_bytes(32, "little") + pf[8 * 32 + 96:]
+            proofs.append(pf)
+            Vs.append(b"".join(V))
+        n_p = 4
+        G, H = bulletproof_gens(n_p)
+        B, Bb = pedersen_gens_default()
+        gens = list(G) + list(H) + [B, Bb]
+
+        def partial(job, r_all, first, wb=None, we=None):
+            sc, pts = job.scalars(r_all, first)
+            s_int = [int.from_bytes(x, "little") for x in sc]
+            P = gens + [r255.decode(p) for p in pts]
+            if wb is None:
+                return r255.raw_point_bytes(r255.msm(s_int, P))
+            c, W = job.windows()
+            return r255.raw_point_bytes(r255.msm_window_partial(s_int, P, c, W, wb, we))
+
+        # proof split: this rank's slice, r's exchanged, all windows
+        b, e = bdist.point_ranges(COUNT, world)[rank]
+        job = bpperm.VerifyJob(K, proofs[b:e], Vs[b:e])
+        assert job.ok
+        r_all = b"".join(bdist.torch_all_gather_bytes_var(job.r))
+        ok_split = bpperm.partials_is_identity(bdist.torch_all_gather_bytes(partial(job, r_all, b)))
+        job.close()
+
+        # window split: every proof on every rank, a window range each
+        job = bpperm.VerifyJob(K, proofs, Vs)
+        c, W = job.windows()
+        wb, we = bdist.window_ranges(W, world)[rank]
+        ok_win = bpperm.partials_is_identity(bdist.torch_all_gather_bytes(partial(job, job.r, 0, wb, we)))
+        job.close()
+        q.put((rank, ok_split, ok_win))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("tamper", [False, True])
+def test_verify_split_over_gloo(tamper):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, tamper, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+        assert p.exitcode == 0
+    results = sorted(q.get() for _ in range(world))
+    for _, ok_split, ok_win in results:
+        assert ok_split == (not tamper)
+        assert ok_win == (not tamper)
+
+
+def test_verify_job_host_phase_matches_oracle():
+    """The product's host replay + weighting, fed to the oracle's MSM, gives
+    the identity for honest proofs; a malformed proof fails in begin."""
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    sys.path.insert(0, str(root / "bulletproof-perm_amd"))
+    sys.path.insert(0, str(root))
+    import bpperm
+    from oracle import cport
+    from oracle import ristretto as r255
+    from oracle.merlin import bulletproof_gens, pedersen_gens_default
+
+    proofs, Vs = zip(*[cport.cpu_prove(K, 7 + s) for s in range(3)])
+    Vs = [b"".join(v) for v in Vs]
+    job = bpperm.VerifyJob(K, proofs, Vs)
+    assert job.ok and len(job.r) == 96
+    T = job.terms()
+    assert T == 2 * 4 + 2 + 3 * (2 * K + 1 + 8 + 2 * 2)
+    sc, pts = job.scalars(job.r, 0)
+    G, H = bulletproof_gens(4)
+    B, Bb = pedersen_gens_default()
+    P = list(G) + list(H) + [B, Bb] + [r255.decode(p) for p in pts]
+    assert r255.equal(r255.msm([int.from_bytes(x, "little") for x in sc], P), r255.IDENTITY)
+    job.close()
+    # A_I = the identity encoding: validate_and_append_point rejects it
+    # (transcript_protocol.rs:48-60); undecodable points fail later, in the
+    # GPU decompression of bpp_perm_verify_partial
+    bad = bytes(32) + proofs[1][32:]
+    job = bpperm.VerifyJob(K, [proofs[0], bad], Vs[:2])
+    assert not job.ok

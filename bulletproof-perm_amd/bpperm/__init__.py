@@ -433,6 +433,20 @@ class PermProver:
         return ([praw[i * self.proof_len:(i + 1) * self.proof_len] for i in range(cnt)],
                 [vraw[i * 32 * self.m:(i + 1) * 32 * self.m] for i in range(cnt)])
 
+    def prove_batch_entropy(self, count: int, seeds32: bytes | None = None):
+        """Production proving: 32 bytes of entropy per proof (seeds32) or,
+        when None, from the OS CSPRNG (bpp_perm_prove_batch_entropy)."""
+        if seeds32 is not None and len(seeds32) != 32 * count:
+            raise ValueError("seeds32 must hold 32 bytes per proof")
+        pf = C.create_string_buffer(self.proof_len * count)
+        V = C.create_string_buffer(32 * self.m * count)
+        check(self.ctx.lib.bpp_perm_prove_batch_entropy(self.ctx.h, self.gens.h, self.k, count, _buf(seeds32 or b""),
+                                                        _buf(self.label), len(self.label), pf, V),
+              "bpp_perm_prove_batch_entropy", self.ctx.h)
+        praw, vraw = pf.raw, V.raw
+        return ([praw[i * self.proof_len:(i + 1) * self.proof_len] for i in range(count)],
+                [vraw[i * 32 * self.m:(i + 1) * 32 * self.m] for i in range(count)])
+
     def verify(self, proof: bytes, V) -> bool:
         vb = _join(V, 32, "V")
         rc = self.ctx.lib.bpp_perm_verify(self.ctx.h, self.gens.h, self.k, _buf(self.label), len(self.label),

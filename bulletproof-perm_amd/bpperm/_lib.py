@@ -81,6 +81,7 @@ SIGNATURES = {
     "bpp_perm_proof_len": (sz, [u32]),
     "bpp_perm_prove": (i32, [vp, vp, u32, u64, vp, sz, vp, vp, vp]),
     "bpp_perm_prove_batch": (i32, [vp, vp, u32, sz, vp, vp, sz, vp, vp]),
+    "bpp_perm_prove_batch_entropy": (i32, [vp, vp, u32, sz, vp, vp, sz, vp, vp]),
     "bpp_perm_verify": (i32, [vp, vp, u32, vp, sz, vp, sz, vp]),
     "bpp_perm_verify_batch": (i32, [vp, vp, u32, sz, vp, sz, vp, vp]),
     "bpp_perm_verify_begin": (i32, [u32, sz, vp, sz, vp, vp, vp, C.POINTER(vp)]),

@@ -81,7 +81,12 @@ class Pool {
       njobs_.fetch_add(1);
     }
     if (sleepers_.load() > 0) cv_.notify_all();
+    // the caller works on its own job too; a for_each from one of its tasks
+    // runs inline, as it does from a worker's (found by TSan: the nested
+    // call went to the pool and ran the inner body on several threads)
+    tl_task() = true;
     work(j);
+    tl_task() = false;
     while (j.done.load() < n) cpu_relax();
     {
       std::lock_guard<std::mutex> g(mu_);
@@ -90,7 +95,7 @@ class Pool {
     }
     while (j.inside.load() != 0) cpu_relax();
   }
-  static bool in_worker() { return tl_worker(); }
+  static bool in_worker() { return tl_worker() || tl_task(); }
 
  private:
   struct Job {
@@ -103,6 +108,10 @@ class Pool {
   static bool& tl_worker() {
     static thread_local bool w = false;
     return w;
+  }
+  static bool& tl_task() {
+    static thread_local bool t = false;
+    return t;
   }
   static void work(Job& j) {
     size_t k = 0;

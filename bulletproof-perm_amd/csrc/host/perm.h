@@ -38,15 +38,34 @@ void witness(const Circuit& C, const std::vector<uint32_t>& pi, const hsc::Sc& x
 // (z^Q)^T W as a dense vector of length ncols
 std::vector<hsc::Sc> zW(const std::vector<Entry>& W, const std::vector<hsc::Sc>& zq, uint32_t ncols);
 
-// SHAKE256(domain || seed_le64) byte stream (oracle/merlin.py Rng)
+// Prover seed: the 8-byte little-endian u64 of the deterministic test
+// entry points (bpp_perm_prove / _batch) or 32 bytes of caller / OS entropy
+// (bpp_perm_prove_batch_entropy), absorbed after the domain string.
+struct Seed {
+  uint8_t b[32] = {0};
+  uint32_t len = 8;
+  static Seed u64(uint64_t x) {
+    Seed s;
+    memcpy(s.b, &x, 8);
+    s.len = 8;
+    return s;
+  }
+  static Seed bytes32(const uint8_t* p) {
+    Seed s;
+    memcpy(s.b, p, 32);
+    s.len = 32;
+    return s;
+  }
+};
+
+// SHAKE256(domain || seed bytes) byte stream (oracle/merlin.py Rng)
 struct Rng {
   merlin::Shake256 sh;
-  Rng(const char* domain, uint64_t seed) {
+  Rng(const char* domain, const Seed& seed) {
     sh.update((const uint8_t*)domain, strlen(domain));
-    uint8_t b[8];
-    memcpy(b, &seed, 8);
-    sh.update(b, 8);
+    sh.update(seed.b, seed.len);
   }
+  Rng(const char* domain, uint64_t seed) : Rng(domain, Seed::u64(seed)) {}
   void bytes(uint8_t* out, size_t n) { sh.read(out, n); }
   uint64_t u64() {
     uint8_t b[8];
@@ -67,7 +86,7 @@ std::vector<uint32_t> fisher_yates(uint32_t k, Rng& rng);
 // The prover's random draws from SHAKE256("bpperm-prove" || seed), in the
 // fixed order pi (Fisher-Yates), gamma[m], alpha, beta, rho, s_L[n_p],
 // s_R[n_p], tau[5] (the stand-in for thread_rng, circuit_lib.rs:175).
-void draw_prover_randomness(const Circuit& C, uint64_t seed, std::vector<uint32_t>& pi, std::vector<hsc::Sc>& gamma,
+void draw_prover_randomness(const Circuit& C, const Seed& seed, std::vector<uint32_t>& pi, std::vector<hsc::Sc>& gamma,
                             hsc::Sc& alpha, hsc::Sc& beta, hsc::Sc& rho, std::vector<hsc::Sc>& sL,
                             std::vector<hsc::Sc>& sR, std::vector<hsc::Sc>& taus);
 
@@ -82,7 +101,8 @@ size_t randomness_bytes(const Circuit& C);
 // The draws of eight proofs at once: the eight SHAKE256 streams run through
 // an AVX-512 8-way Keccak (host/keccak_x8.cpp; scalar fallback without
 // AVX-512), byte-identical to draw_prover_randomness.
-void draw_prover_randomness_x8(const Circuit& C, const uint64_t seeds[8], RandomDraws out[8]);
+// (the eight seeds must have the same length)
+void draw_prover_randomness_x8(const Circuit& C, const Seed seeds[8], RandomDraws out[8]);
 
 size_t proof_len(uint32_t k);
 

@@ -112,7 +112,7 @@ std::vector<uint32_t> fisher_yates(uint32_t k, Rng& rng) {
   return p;
 }
 
-void draw_prover_randomness(const Circuit& C, uint64_t seed, std::vector<uint32_t>& pi, std::vector<Sc>& gamma,
+void draw_prover_randomness(const Circuit& C, const Seed& seed, std::vector<uint32_t>& pi, std::vector<Sc>& gamma,
                             Sc& alpha, Sc& beta, Sc& rho, std::vector<Sc>& sL, std::vector<Sc>& sR,
                             std::vector<Sc>& taus) {
   Rng rng("bpperm-prove", seed);

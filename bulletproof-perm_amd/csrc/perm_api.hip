@@ -16,8 +16,10 @@
 //                                       generator scalars merged)
 // Transcript order and RNG draw order match oracle/bulletproofs.py
 // ac_prove / ac_verify exactly (tests compare proof bytes).
+#include <cerrno>
 #include <cstring>
 #include <cstdlib>
+#include <sys/random.h>
 #include <memory>
 #include <thread>
 
@@ -186,7 +188,7 @@ struct ProverState {
 // round) is ONE launch sequence for the whole batch, and the per-proof host
 // work between them (transcripts, challenges, polynomial coefficients) runs
 // on a thread pool.  Outputs are identical to proving one at a time.
-int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const std::vector<uint64_t>& seeds,
+int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const std::vector<perm::Seed>& seeds,
                 const uint8_t* label, size_t llen, std::vector<Proof>& Ps) {
   const uint32_t k = C.k, n_p = C.n_p, m = C.m;
   const size_t P = seeds.size();
@@ -199,7 +201,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
   // (eight proofs' SHAKE256 streams per AVX-512 Keccak, perm::draw_prover_randomness_x8)
   std::unique_ptr<HostScope> hs(new HostScope(ctx, "pb_rng"));
   par::for_each((P + 7) / 8, [&](size_t gi) {
-    uint64_t sd[8];
+    perm::Seed sd[8];
     perm::RandomDraws d[8];
     for (size_t j = 0; j < 8; ++j) sd[j] = seeds[std::min(8 * gi + j, P - 1)];
     perm::draw_prover_randomness_x8(C, sd, d);
@@ -687,18 +689,16 @@ int bpp_perm_prove(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, uint64_t seed, c
   }
   BPP_HIP(hipSetDevice(ctx->device));
   std::vector<Proof> Ps;
-  BPP_TRY(prove_batch(ctx, G, C, {seed}, label, llen, Ps));
+  BPP_TRY(prove_batch(ctx, G, C, {perm::Seed::u64(seed)}, label, llen, Ps));
   serialize(C, Ps[0], proof_out);
   for (uint32_t j = 0; j < C.m; ++j) memcpy(V_out + 32 * j, Ps[0].V[j].data(), 32);
   if (perm_out) memcpy(perm_out, Ps[0].pi.data(), 4 * k);
   return BPP_OK;
 }
 
-int bpp_perm_prove_batch(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, size_t count, const uint64_t* seeds,
-                         const uint8_t* label, size_t llen, uint8_t* proofs_out, uint8_t* V_out) {
-  if (!ctx || !G || (!seeds && count) || ((!proofs_out || !V_out) && count) || (!label && llen) || k < 2 ||
-      k > (1u << 20))
-    return BPP_ERR_ARG;
+static int prove_batch_api(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, const std::vector<perm::Seed>& seeds,
+                           const uint8_t* label, size_t llen, uint8_t* proofs_out, uint8_t* V_out) {
+  const size_t count = seeds.size();
   if (!count) return BPP_OK;
   const perm::Circuit C = perm::build(k);
   if (G->n < C.n_p) {
@@ -720,7 +720,7 @@ int bpp_perm_prove_batch(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, size_t cou
     BPP_TRY(gens_points(ctx, G, &warm));
   }
   if (S <= 1) {
-    BPP_TRY(prove_batch(ctx, G, C, std::vector<uint64_t>(seeds, seeds + count), label, llen, Ps));
+    BPP_TRY(prove_batch(ctx, G, C, seeds, label, llen, Ps));
   } else {
     std::vector<bpp_ctx*> kids(S);
     for (size_t s = 0; s < S; ++s) BPP_TRY(ctx_child(ctx, s, &kids[s]));
@@ -736,7 +736,8 @@ int bpp_perm_prove_batch(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, size_t cou
           return;
         }
         std::vector<Proof> sub;
-        rcs[s] = prove_batch(kc, G, C, std::vector<uint64_t>(seeds + b, seeds + e), label, llen, sub);
+        rcs[s] = prove_batch(kc, G, C, std::vector<perm::Seed>(seeds.begin() + b, seeds.begin() + e), label,
+                             llen, sub);
         if (rcs[s] == BPP_OK)
           for (size_t i = b; i < e; ++i) Ps[i] = std::move(sub[i - b]);
       });
@@ -753,6 +754,42 @@ int bpp_perm_prove_batch(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, size_t cou
     for (uint32_t j = 0; j < C.m; ++j) memcpy(V_out + (p * C.m + j) * 32, Ps[p].V[j].data(), 32);
   });
   return BPP_OK;
+}
+
+int bpp_perm_prove_batch(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, size_t count, const uint64_t* seeds,
+                         const uint8_t* label, size_t llen, uint8_t* proofs_out, uint8_t* V_out) {
+  if (!ctx || !G || (!seeds && count) || ((!proofs_out || !V_out) && count) || (!label && llen) || k < 2 ||
+      k > (1u << 20))
+    return BPP_ERR_ARG;
+  std::vector<perm::Seed> sd(count);
+  for (size_t i = 0; i < count; ++i) sd[i] = perm::Seed::u64(seeds[i]);
+  return prove_batch_api(ctx, G, k, sd, label, llen, proofs_out, V_out);
+}
+
+int bpp_perm_prove_batch_entropy(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, size_t count, const uint8_t* seeds32,
+                                 const uint8_t* label, size_t llen, uint8_t* proofs_out, uint8_t* V_out) {
+  if (!ctx || !G || ((!proofs_out || !V_out) && count) || (!label && llen) || k < 2 || k > (1u << 20))
+    return BPP_ERR_ARG;
+  std::vector<uint8_t> ent;
+  if (!seeds32 && count) {  // the OS CSPRNG, the reference's thread_rng() (circuit_lib.rs:175)
+    ent.resize(32 * count);
+    size_t got = 0;
+    while (got < ent.size()) {
+      const ssize_t r = getrandom(ent.data() + got, ent.size() - got, 0);
+      if (r < 0) {
+        if (errno == EINTR) continue;
+        ctx->err = "getrandom failed";
+        return BPP_ERR_DEVICE;
+      }
+      got += (size_t)r;
+    }
+    seeds32 = ent.data();
+  }
+  std::vector<perm::Seed> sd(count);
+  for (size_t i = 0; i < count; ++i) sd[i] = perm::Seed::bytes32(seeds32 + 32 * i);
+  const int rc = prove_batch_api(ctx, G, k, sd, label, llen, proofs_out, V_out);
+  if (!ent.empty()) memset(ent.data(), 0, ent.size());
+  return rc;
 }
 
 int bpp_perm_verify(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, const uint8_t* label, size_t llen,

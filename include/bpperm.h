@@ -217,6 +217,14 @@ int bpp_perm_prove(bpp_ctx* ctx, const bpp_gens* g, uint32_t k, uint64_t seed, c
                    uint8_t* proof_out, uint8_t* V_out, uint32_t* perm_out);
 int bpp_perm_prove_batch(bpp_ctx* ctx, const bpp_gens* g, uint32_t k, size_t count, const uint64_t* seeds,
                          const uint8_t* label, size_t llen, uint8_t* proofs_out, uint8_t* V_out);
+/* The u64 seeds above are deterministic TEST hooks (64 bits of entropy, so
+ * a guessable seed reveals the witness).  Production proofs: 32 bytes of
+ * entropy per proof from the caller (seeds32, count x 32 B), or seeds32 =
+ * NULL to draw them from the OS CSPRNG (getrandom), as the reference draws
+ * from thread_rng (circuit_lib.rs:175, weights.rs:39,59).  The blindings
+ * are SHAKE256("bpperm-prove" || seed32) in the same draw order. */
+int bpp_perm_prove_batch_entropy(bpp_ctx* ctx, const bpp_gens* g, uint32_t k, size_t count, const uint8_t* seeds32,
+                                 const uint8_t* label, size_t llen, uint8_t* proofs_out, uint8_t* V_out);
 /* BPP_OK or BPP_ERR_VERIFY (ProofError::VerificationError). One GPU MSM. */
 int bpp_perm_verify(bpp_ctx* ctx, const bpp_gens* g, uint32_t k, const uint8_t* label, size_t llen,
                     const uint8_t* proof, size_t proof_len, const uint8_t* V);

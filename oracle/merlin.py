@@ -232,8 +232,11 @@ class Rng:
     'random' blindings are reproducible: SHAKE256("bpperm-rng" || seed_le64).
     Stands in for the reference's `rand::thread_rng()` (circuit_lib.rs:175)."""
 
-    def __init__(self, seed: int, domain: bytes = b"bpperm-rng"):
-        self._xof = hashlib.shake_256(domain + struct.pack("<Q", seed))
+    def __init__(self, seed, domain: bytes = b"bpperm-rng"):
+        # an int is the u64 test seed (8 bytes LE); bytes are taken as is
+        # (the 32-byte entropy seeds of bpp_perm_prove_batch_entropy)
+        sb = bytes(seed) if isinstance(seed, (bytes, bytearray)) else struct.pack("<Q", seed)
+        self._xof = hashlib.shake_256(domain + sb)
         self._pos = 0
         self._buf = b""
 

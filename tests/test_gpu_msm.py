@@ -119,3 +119,57 @@ def test_msm_golden_vectors(ctx):
         assert b"".join(tbl.compress()) == pts
         assert ctx.msm(bytes.fromhex(case["scalars"]), pts).hex() == case["result"], case["n"]
         assert ctx.msm_table(bytes.fromhex(case["scalars"]), tbl).hex() == case["result"], case["n"]
+
+
+def _gpu_decodes(ctx, enc: bytes):
+    import bpperm
+    try:
+        t = ctx.decompress([enc])
+    except bpperm.BppError as e:
+        assert e.name == "BPP_ERR_DECOMPRESS"
+        return None
+    out = t.compress()[0]
+    t.close()
+    return out
+
+
+def test_rfc9496_bad_encodings_rejected_by_gpu_decoder(ctx):
+    """RFC 9496 §A.2 bad encodings (tests/test_oracle_kat.py) through the GPU
+    decoder: every one is BPP_ERR_DECOMPRESS, alone and inside a batch of
+    valid encodings (bad_index reported)."""
+    from test_oracle_kat import BAD_ENCODINGS
+    good = [r255.encode(p) for p in _points(5, 9)[1]]
+    import bpperm
+    for h in BAD_ENCODINGS:
+        enc = bytes.fromhex(h)
+        with pytest.raises(r255.DecodeError):
+            r255.decode(enc)
+        assert _gpu_decodes(ctx, enc) is None, h
+        with pytest.raises(bpperm.BppError) as ei:
+            ctx.decompress(good[:4] + [enc] + good[4:])
+        assert ei.value.name == "BPP_ERR_DECOMPRESS"
+
+
+def test_random_encodings_accept_reject_matches_oracle(ctx):
+    """Random 32-byte strings (most invalid: non-canonical, negative or
+    non-square) and their low-bit-cleared variants: the GPU decoder accepts
+    exactly what the oracle accepts, and re-encodes accepted ones canonically."""
+    rng = Rng(77, b"codec-sweep")
+    cases = []
+    for _ in range(48):
+        b = bytearray(rng.bytes(32))
+        b[31] &= 0x7F
+        cases.append(bytes(b))
+        b[0] &= 0xFE  # even s: about half of these are valid encodings
+        cases.append(bytes(b))
+    agree = accepted = 0
+    for enc in cases:
+        try:
+            want = r255.encode(r255.decode(enc))
+        except r255.DecodeError:
+            want = None
+        got = _gpu_decodes(ctx, enc)
+        assert got == want, enc.hex()
+        agree += 1
+        accepted += want is not None
+    assert agree == len(cases) and 0 < accepted < len(cases)

@@ -1,0 +1,37 @@
+"""Host C++ of libbpperm under ASan + UBSan and under TSan:
+tests/c/host_sanitize.cpp is compiled with the library's host sources
+(Keccak, 8-way Keccak, circuit) and run on the CPU.  The GPU kernels are not
+sanitized (GPU ASan / xnack are unavailable on the pool)."""
+import os
+import shutil
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+CSRC = ROOT / "bulletproof-perm_amd" / "csrc"
+SRCS = [ROOT / "tests" / "c" / "host_sanitize.cpp", *sorted((CSRC / "host").glob("*.cpp"))]
+
+
+def _build_run(tmp_path, name, flags, env_extra):
+    exe = tmp_path / name
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-pthread", "-march=x86-64-v3",
+           "-I", str(CSRC), *flags, *map(str, SRCS), "-o", str(exe)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    env = dict(os.environ, BPP_HOST_THREADS="4", **env_extra)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    assert r.stdout.strip() == "ok"
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not installed")
+def test_host_asan_ubsan(tmp_path):
+    _build_run(tmp_path, "host_asan", ["-fsanitize=address,undefined", "-fno-sanitize-recover=all"],
+               {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0", "UBSAN_OPTIONS": "print_stacktrace=1"})
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not installed")
+def test_host_tsan(tmp_path):
+    _build_run(tmp_path, "host_tsan", ["-fsanitize=thread"], {"TSAN_OPTIONS": "halt_on_error=1"})

@@ -1,0 +1,119 @@
+// Direct-table MSM lane walk and block tree (shared by k_dt_msm,
+// msm_kernels.cuh, and the fused IPA round, ipa.hip).
+//
+// Digits in closed form: with K = sum_{w < W-1} 2^(c w + c - 1) (host,
+// DtGeom::K), field w of s + K minus H is signed digit w in [-H, H) for
+// w < W - 1 and field W - 1 the top digit (>= 0; s < 2^253 so s + K < 2^254),
+// the digits of a carry-propagating signed recoding without the carry chain.
+//
+// One block per MSM, blockDim = W * TG lanes: lane (tg, w) owns WINDOW w of
+// terms tg, tg + TG, tg + 2 TG, ... -- the window is fixed per lane, so the
+// digit is a fixed bit field of s + K (no per-entry division or scan), and
+// the W lanes sharing a term read the same 32 scalar bytes.  Then an LDS
+// tree over the block's lanes.
+#pragma once
+#include "ge_io.cuh"
+
+struct DtGeom {
+  uint32_t c, W, H;  // window bits, windows, rows per window (2^(c-1))
+  uint32_t K[8];     // sum_{w < W-1} 2^(c w + c - 1), little-endian words
+};
+#define DT_NT_MAX 256
+
+FE_INLINE uint32_t sel8(const uint32_t v[8], uint32_t i) {  // v[i], 0 for i >= 8 (no scratch)
+  uint32_t r = 0;
+  _Pragma("unroll") for (uint32_t k = 0; k < 8; ++k) r = i == k ? v[k] : r;
+  return r;
+}
+
+// Table row of window w of a term (scalar s, generator gen); d = 0 gives
+// row of |d| = 1 and zero = true (the caller adds the identity instead).
+struct DtLane {
+  uint32_t w, wi, sh, fmask, W, H;
+  bool top;
+  FE_INLINE static DtLane make(const DtGeom& g, uint32_t w) {
+    DtLane ln;
+    ln.w = w;
+    ln.wi = (g.c * w) >> 5;
+    ln.sh = (g.c * w) & 31;
+    ln.fmask = (1u << g.c) - 1u;
+    ln.W = g.W;
+    ln.H = g.H;
+    ln.top = w + 1 == g.W;
+    return ln;
+  }
+  FE_INLINE void row_of(const DtGeom& g, const uint32_t sc[8], uint32_t gen, uint32_t& row, bool& neg,
+                        bool& zero) const {
+    uint32_t s[8];
+    uint64_t c = 0;
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) {
+      c += (uint64_t)sc[i] + g.K[i];
+      s[i] = (uint32_t)c;
+      c >>= 32;
+    }
+    const uint32_t lo = sel8(s, wi), hi = sel8(s, wi + 1);
+    const uint32_t f = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & fmask;
+    const int d = top ? (int)f : (int)f - (int)H;
+    const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
+    zero = ad == 0;
+    neg = d < 0;
+    row = (gen * W + w) * H + (zero ? 0u : ad - 1u);
+  }
+};
+
+// One lane's walk over terms t, t + TG, ... < t1 (src(t, s, gen) supplies
+// a term's scalar words and generator index).  Software pipeline: the scalar
+// and generator index of the term after next are loaded one whole addition
+// ahead, and the next term's 128-B table row is gathered between the two
+// halves of the current addition (the operand is dead after its first three
+// multiplies).  A zero digit adds the identity (no divergent skip).
+template <class Src>
+FE_INLINE ge_p3 dt_walk(const uint32_t* __restrict__ dt, const DtGeom& dg, const DtLane& ln, uint32_t t, uint32_t t1,
+                        uint32_t TG, const Src& src) {
+  ge_p3 acc = ge_identity();
+  if (t >= t1) return acc;
+  uint32_t sc[8];
+  uint32_t gen;
+  src(t, sc, gen);
+  uint32_t tn = t + TG;
+  uint32_t scn[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t genn = 0;
+  if (tn < t1) src(tn, scn, genn);
+  uint32_t row;
+  bool neg, zero;
+  ln.row_of(dg, sc, gen, row, neg, zero);
+  ge_niels q = load_niels(dt, row);
+  for (;;) {
+    if (zero) q = ge_niels_identity();
+    const ge_madd_mid mid = ge_madd_signed_h1(acc, q, neg);
+    const bool more = tn < t1;
+    bool neg2 = false, zero2 = false;
+    if (more) {
+      uint32_t row2;
+      ln.row_of(dg, scn, genn, row2, neg2, zero2);
+      q = load_niels(dt, row2);
+      tn += TG;
+      if (tn < t1) src(tn, scn, genn);
+    }
+    acc = ge_madd_h2(mid);
+    if (!more) break;
+    neg = neg2;
+    zero = zero2;
+  }
+  return acc;
+}
+
+// Block tree in LDS (tl: blockDim.x extended points) whose waves retire as it
+// narrows; lane 0 writes the block's sum to out_p3[m].
+FE_INLINE void dt_block_tree(uint32_t* tl, const ge_p3& acc, uint32_t nt, uint32_t* __restrict__ out_p3, uint32_t m) {
+  store_p3(tl, threadIdx.x, acc);
+  __syncthreads();
+  uint32_t p2 = 1;
+  while (p2 < nt) p2 <<= 1;
+  for (uint32_t s = p2 >> 1; s > 0; s >>= 1) {
+    if (threadIdx.x < s && threadIdx.x + s < nt)
+      store_p3(tl, threadIdx.x, ge_add(load_p3(tl, threadIdx.x), load_p3(tl, threadIdx.x + s)));
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) store_p3(out_p3, m, load_p3(tl, 0));
+}

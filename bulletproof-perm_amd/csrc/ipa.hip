@@ -18,12 +18,23 @@
 #include <cstring>
 
 #include "ctx.h"
+#include "dt_walk.cuh"
 #include "ipa.h"
 #include "msm_engine.h"
 #include "host/par.h"
 #include "sc25519.cuh"
 
+DtGeom dt_geom(uint32_t c);                                     // msm.hip
+bool msm_use_dt(const MsmPoints& pts, uint32_t M, uint32_t T);  // msm.hip
+
 static unsigned grid_for(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
+
+// widest IPA run as one launch per round (k_ipa_round_dt; its LDS holds the
+// n + 1 terms and the round's a, b within 64 KB; 0 builds the four-kernel
+// rounds everywhere, for A/B runs)
+#ifndef IPA_FUSED_NMAX
+#define IPA_FUSED_NMAX 512
+#endif
 
 // All kernels run P independent instances of the same length n in lockstep
 // (a batch of proofs); per-instance arrays are [P][n] scalars, the MSM term
@@ -175,6 +186,122 @@ __global__ void __launch_bounds__(256) k_ipa_fold(uint32_t n, uint32_t lg_n, uin
   }
 }
 
+// One whole IPA round per launch over the direct tables (the fused form of
+// k_ipa_fold + k_ipa_terms + k_ipa_cross_final + k_dt_msm): block 2i + s is
+// instance i's L (s = 0) or R (s = 1).  The block
+//   1. folds the previous round's challenge into a, b (length 2m -> m) and
+//      the generator factors fG, fH (all n) when `fold`, reading set *_in and
+//      (side 0 only) writing set *_out -- the two sides compute the same
+//      values, so the other side's reads of *_in never race with a write;
+//   2. builds its n + 1 halved term scalars in LDS (as k_ipa_terms: L gets
+//      a_lo fG_hi and b_hi fH_lo, R the mirror) and c_L or c_R (block
+//      reduction of a_lo b_hi / a_hi b_lo) times qmul for the Q term;
+//   3. runs the direct-table walk over those terms and the block tree
+//      (dt_walk.cuh) -> out_p3[blockIdx.x] = L/2 or R/2.
+// One launch per round instead of four: the latency of three small kernels
+// and their passes over the [P][n] arrays leave every round of a batch.
+__global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
+    const uint32_t* __restrict__ dt, DtGeom dg, uint32_t n, uint32_t m, uint32_t lg_h, uint32_t fold,
+    const uint32_t* __restrict__ am_in, const uint32_t* __restrict__ bm_in, const uint32_t* __restrict__ fG_in,
+    const uint32_t* __restrict__ fH_in, uint32_t* __restrict__ am_out, uint32_t* __restrict__ bm_out,
+    uint32_t* __restrict__ fG_out, uint32_t* __restrict__ fH_out, const uint32_t* __restrict__ u,
+    const uint32_t* __restrict__ qmul, uint32_t gbase, uint32_t hbase, uint32_t qidx, uint32_t TG,
+    uint32_t* __restrict__ out_p3) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  uint32_t* tsc = lds;                           // (n + 1) x 8 words: halved term scalars
+  uint32_t* tgen = lds + 8 * (n + 1);            // n + 1 generator indices
+  uint32_t* sa = tgen + ((n + 1 + 3) & ~3u);     // m x 8: a (Montgomery), this round
+  uint32_t* sb = sa + 8 * m;                     // m x 8: b
+  uint32_t* red = sb + 8 * m;                    // 4 waves x 8 words
+  const uint32_t nt = blockDim.x, tid = threadIdx.x;
+  const uint32_t inst = blockIdx.x >> 1, side = blockIdx.x & 1u;
+  const size_t ib = (size_t)inst * n;
+  const bool writer = fold && side == 0;
+  sc um = sc_zero(), uim = sc_zero();
+  if (fold) {
+    um = sc_load(u + 16 * inst);
+    uim = sc_load(u + 16 * inst + 8);
+  }
+  // 1. a, b of this round (length m) into LDS
+  for (uint32_t p = tid; p < m; p += nt) {
+    sc a, b;
+    if (fold) {  // G' = u^-1 G_lo + u G_hi: a' = a_lo u + a_hi u^-1, b' = b_lo u^-1 + b_hi u
+      a = sc_add(sc_mont(sc_load(am_in + 8 * (ib + p)), um), sc_mont(sc_load(am_in + 8 * (ib + p + m)), uim));
+      b = sc_add(sc_mont(sc_load(bm_in + 8 * (ib + p)), uim), sc_mont(sc_load(bm_in + 8 * (ib + p + m)), um));
+      if (writer) {
+        sc_store(am_out + 8 * (ib + p), a);
+        sc_store(bm_out + 8 * (ib + p), b);
+      }
+    } else {
+      a = sc_load(am_in + 8 * (ib + p));
+      b = sc_load(bm_in + 8 * (ib + p));
+    }
+    sc_store(sa + 8 * p, a);
+    sc_store(sb + 8 * p, b);
+  }
+  __syncthreads();
+  // 2. term scalars: every k gives one G term and one H term, to this side
+  // or the other
+  const uint32_t h = m >> 1;
+  for (uint32_t k = tid; k < n; k += nt) {
+    sc fg = sc_load(fG_in + 8 * (ib + k)), fh = sc_load(fH_in + 8 * (ib + k));
+    if (fold) {
+      const bool hi_prev = (k & (2 * m - 1)) & m;
+      fg = sc_mont(fg, hi_prev ? um : uim);
+      fh = sc_mont(fh, hi_prev ? uim : um);
+      if (writer) {
+        sc_store(fG_out + 8 * (ib + k), fg);
+        sc_store(fH_out + 8 * (ib + k), fh);
+      }
+    }
+    const uint32_t r = k & (m - 1);
+    const bool hi = (r & h) != 0;
+    const uint32_t p = r ^ h;
+    const uint32_t cidx = ((k >> (lg_h + 1)) << lg_h) | (k & (h - 1));
+    if (hi == (side == 0)) {
+      sc_store(tsc + 8 * cidx, sc_half(sc_mont(sc_load(sa + 8 * p), fg)));
+      tgen[cidx] = gbase + k;
+    } else {
+      sc_store(tsc + 8 * ((n >> 1) + cidx), sc_half(sc_mont(sc_load(sb + 8 * p), fh)));
+      tgen[(n >> 1) + cidx] = hbase + k;
+    }
+  }
+  // c_L = <a_lo, b_hi> (L) or c_R = <a_hi, b_lo> (R), Montgomery form
+  sc c = sc_zero();
+  for (uint32_t j = tid; j < h; j += nt)
+    c = sc_add(c, side == 0 ? sc_mont(sc_load(sa + 8 * j), sc_load(sb + 8 * (j + h)))
+                            : sc_mont(sc_load(sa + 8 * (j + h)), sc_load(sb + 8 * j)));
+  c = sc_wave_sum(c);
+  if ((tid & 63u) == 0) sc_store(red + 8 * (tid >> 6), c);
+  __syncthreads();
+  if (tid == 0) {
+    sc t = sc_zero();
+    for (uint32_t wv = 0; wv < (nt + 63) / 64; ++wv) t = sc_add(t, sc_load(red + 8 * wv));
+    sc_store(tsc + 8 * n, sc_half(sc_mont(t, sc_load(qmul + 8 * inst))));  // Montgomery c * canonical q
+    tgen[n] = qidx;
+  }
+  __syncthreads();
+  // 3. direct-table walk over the LDS terms, then the block tree (reusing LDS)
+  const uint32_t tg = tid / dg.W;
+  const DtLane ln = DtLane::make(dg, tid % dg.W);
+  const ge_p3 acc = tg < TG ? dt_walk(dt, dg, ln, tg, n + 1, TG,
+                                      [&](uint32_t t, uint32_t s[8], uint32_t& gen) {
+                                        const sc v = sc_load(tsc + 8 * t);
+                                        _Pragma("unroll") for (int i = 0; i < 8; ++i) s[i] = v.v[i];
+                                        gen = tgen[t];
+                                      })
+                            : ge_identity();
+  __syncthreads();
+  dt_block_tree(lds, acc, nt, out_p3, blockIdx.x);
+}
+
+// LDS words of k_ipa_round_dt: terms + indices + a, b + wave partials, or
+// the block tree, whichever is larger
+static size_t ipa_round_lds_words(uint32_t n, uint32_t nt) {
+  const size_t prologue = 8 * (size_t)(n + 1) + ((n + 1 + 3) & ~3u) + 16 * (size_t)n + 32;
+  return std::max(prologue, (size_t)nt * P3_WORDS);
+}
+
 static sc to_dev_sc(const hsc::Sc& x) {
   sc r;
   for (int i = 0; i < 4; ++i) {
@@ -242,26 +369,69 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
   std::vector<uint8_t> enc((size_t)2 * P * 32);
   std::vector<hsc::Sc> u(P), ui(P);
   std::vector<uint32_t> uw((size_t)P * 16);
-  uint32_t m = n;
-  uint32_t lg_h = lg_n ? lg_n - 1 : 0;  // log2(n/2)
+  // One launch per round (k_ipa_round_dt) when the generators have direct
+  // tables: the state (a, b, fG, fH) alternates between two sets so that a
+  // round's blocks read the previous state while side 0 writes the next.
+  const bool fused = n >= 2 && n <= IPA_FUSED_NMAX && !g.pts.tbl1 && msm_use_dt(g.pts, 2 * P, (uint32_t)PT);
+  uint32_t* S[2][4] = {{(uint32_t*)am, (uint32_t*)bm, (uint32_t*)fG, (uint32_t*)fH}, {nullptr, nullptr, nullptr, nullptr}};
+  void* d_res = nullptr;
+  DtGeom dg;
+  uint32_t TG = 1, nt = 1;
+  if (fused) {
+    static const char* names[4] = {"ipa_am1", "ipa_bm1", "ipa_fG1", "ipa_fH1"};
+    for (int i = 0; i < 4; ++i) {
+      void* d = nullptr;
+      BPP_TRY(ctx_ws(ctx, names[i], PN * 32, &d));
+      S[1][i] = (uint32_t*)d;
+    }
+    BPP_TRY(ctx_ws(ctx, "ipa_res", (size_t)2 * P * P3_BYTES, &d_res));
+    dg = dt_geom(g.pts.dt_c);
+    TG = DT_NT_MAX / dg.W;  // as msm_multi_dt_dev for (n + 1)-term MSMs
+    while (TG > 1 && (double)(n + 1) < 2.0 * TG) TG >>= 1;
+    nt = TG * dg.W;
+  }
+  int cur = 0;  // set holding the state at the start of a round (before its fold)
+  uint32_t m = n, round = 0;
+  uint32_t lg_h = lg_n ? lg_n - 1 : 0;  // log2(m/2)
   while (m > 1) {
     const uint32_t h = m >> 1;
-    {
-      ProfScope ps(ctx, "ipa_terms");
-      hipLaunchKernelGGL(k_ipa_terms, dim3(grid_for(PN, 256)), dim3(256), 0, ctx->stream, n, lg_n, P, m, lg_h,
-                         (const uint32_t*)am, (const uint32_t*)bm, (const uint32_t*)fG, (const uint32_t*)fH, g.gbase,
-                         g.hbase, (uint32_t*)scal, (uint32_t*)pidx, fuse_cross ? (uint32_t*)part : nullptr);
-      uint32_t nb = n / 64;  // partials per instance (fused: one per wave)
-      if (!fuse_cross) {
-        nb = std::min<uint32_t>(cross_blocks, grid_for(h, CROSS_T));
-        hipLaunchKernelGGL(k_ipa_cross, dim3(nb, P), dim3(CROSS_T), 0, ctx->stream, n, h, (const uint32_t*)am,
-                           (const uint32_t*)bm, (uint32_t*)part);
+    if (fused) {
+      const int in = cur, outs = cur ^ 1;
+      {
+        ProfScope ps(ctx, "msm_direct");
+        hipLaunchKernelGGL(k_ipa_round_dt, dim3(2 * P), dim3(nt), ipa_round_lds_words(n, nt) * 4, ctx->stream,
+                           g.pts.dt, dg, n, m, lg_h, round ? 1u : 0u, S[in][0], S[in][1], S[in][2], S[in][3],
+                           S[outs][0], S[outs][1], S[outs][2], S[outs][3], (const uint32_t*)d_u, (const uint32_t*)d_q,
+                           g.gbase, g.hbase, g.qidx, TG, (uint32_t*)d_res);
       }
-      hipLaunchKernelGGL(k_ipa_cross_final, dim3(grid_for(P, 64)), dim3(64), 0, ctx->stream, nb, P,
-                         (const uint32_t*)part, (const uint32_t*)d_q, g.qidx, n, (uint32_t*)scal, (uint32_t*)pidx);
-    }
-    BPP_TRY(ctx_check_launch(ctx, "ipa round kernels"));
-    {
+      BPP_TRY(ctx_check_launch(ctx, "k_ipa_round_dt"));
+      if (round) cur = outs;
+      const uint64_t terms = (uint64_t)2 * P * (n + 1);
+      ctx_work(ctx, "msm_terms", terms);
+      ctx_work(ctx, "madds", terms * dg.W);
+      ctx_work(ctx, "padds", (uint64_t)2 * P * (nt - 1));
+      ctx_work(ctx, "msm_launches", 1);
+      ctx_work(ctx, "dt_terms", terms);
+      ctx_work(ctx, "dt_madds", terms * dg.W);
+      ctx_work(ctx, "dt_launches", 1);
+      HostScope hs(ctx, "ipa_msm");
+      BPP_TRY(points_double_encode_p3(ctx, (const uint32_t*)d_res, 2 * (size_t)P, enc.data()));
+    } else {
+      {
+        ProfScope ps(ctx, "ipa_terms");
+        hipLaunchKernelGGL(k_ipa_terms, dim3(grid_for(PN, 256)), dim3(256), 0, ctx->stream, n, lg_n, P, m, lg_h,
+                           (const uint32_t*)am, (const uint32_t*)bm, (const uint32_t*)fG, (const uint32_t*)fH,
+                           g.gbase, g.hbase, (uint32_t*)scal, (uint32_t*)pidx, fuse_cross ? (uint32_t*)part : nullptr);
+        uint32_t nb = n / 64;  // partials per instance (fused: one per wave)
+        if (!fuse_cross) {
+          nb = std::min<uint32_t>(cross_blocks, grid_for(h, CROSS_T));
+          hipLaunchKernelGGL(k_ipa_cross, dim3(nb, P), dim3(CROSS_T), 0, ctx->stream, n, h, (const uint32_t*)am,
+                             (const uint32_t*)bm, (uint32_t*)part);
+        }
+        hipLaunchKernelGGL(k_ipa_cross_final, dim3(grid_for(P, 64)), dim3(64), 0, ctx->stream, nb, P,
+                           (const uint32_t*)part, (const uint32_t*)d_q, g.qidx, n, (uint32_t*)scal, (uint32_t*)pidx);
+      }
+      BPP_TRY(ctx_check_launch(ctx, "ipa round kernels"));
       HostScope hs(ctx, "ipa_msm");
       // L/2, R/2 from the halved term scalars (k_ipa_terms, k_ipa_cross_final),
       // encoded as L, R (msm_multi_enc)
@@ -287,15 +457,21 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
       memcpy(&uw[16 * (size_t)p + 8], uim.v, 32);
     }
     BPP_TRY(ctx_h2d(ctx, d_u, uw.data(), uw.size() * 4));
-    {
+    // the fused rounds fold inside the next round's launch; the last
+    // challenge (and every challenge of the unfused path) is folded here
+    if (!fused || h == 1) {
+      uint32_t** st = S[cur];
       ProfScope ps(ctx, "ipa_fold");
-      hipLaunchKernelGGL(k_ipa_fold, dim3(grid_for(PN, 256)), dim3(256), 0, ctx->stream, n, lg_n, P, m, (uint32_t*)am,
-                         (uint32_t*)bm, (uint32_t*)fG, (uint32_t*)fH, (const uint32_t*)d_u);
+      hipLaunchKernelGGL(k_ipa_fold, dim3(grid_for(PN, 256)), dim3(256), 0, ctx->stream, n, lg_n, P, m, st[0], st[1],
+                         st[2], st[3], (const uint32_t*)d_u);
     }
     BPP_TRY(ctx_check_launch(ctx, "k_ipa_fold"));
     m = h;
+    ++round;
     if (lg_h) --lg_h;
   }
+  am = S[cur][0];
+  bm = S[cur][1];
   // a, b = element 0 of each instance
   std::vector<uint32_t> ab((size_t)P * 16);
   {

@@ -227,11 +227,13 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
       BPP_TRY(ctx_ws(ctx, "msm_rpart", nseg * nw * 2 * P3_BYTES, &part));
       BPP_TRY(ctx_ws(ctx, "msm_wsum_terms", nseg * (1 + J) * P3_BYTES, &wsum));
       ProfScope ps(ctx, "msm_reduce");
+#ifndef EXP_NO_REDUCE  // (timing experiment only: results are wrong without it)
       hipLaunchKernelGGL(k_msm_reduce_wave, dim3((unsigned)(nseg * nw)), dim3(64), 0, ctx->stream,
                          (const uint32_t*)boff, ks, (const uint32_t*)head, (const uint32_t*)tail, (const uint32_t*)bsum,
                          g, (uint32_t*)part);
       hipLaunchKernelGGL(k_msm_reduce_bits, dim3((unsigned)(nseg * (1 + J))), dim3(64), 0, ctx->stream,
                          (const uint32_t*)part, g, 1 + J, (uint32_t*)wsum);
+#endif
       BPP_TRY(ctx_check_launch(ctx, "k_msm_reduce_wave/bits"));
       *terms_out = 1 + J;
       *d_wsum_out = (uint32_t*)wsum;
@@ -592,7 +594,7 @@ static bool fb_wins(double terms_per_msm) {
   return pol == 1 || (pol == -1 && terms_per_msm <= 16384.0);
 }
 
-static DtGeom dt_geom(uint32_t c) {
+DtGeom dt_geom(uint32_t c) {
   DtGeom g;
   g.c = c;
   g.W = (254 + c - 1) / c;
@@ -630,7 +632,7 @@ int dt_build(bpp_ctx* ctx, const uint32_t* d_wt, uint32_t npts, uint32_t c, uint
 }
 
 // Direct-table engine: one block per MSM (BPP_MSM_DT=0 disables, =1 forces).
-static bool use_dt(const MsmPoints& pts, uint32_t M, uint32_t T) {
+bool msm_use_dt(const MsmPoints& pts, uint32_t M, uint32_t T) {
   if (!pts.dt || pts.tbl1 || M == 0) return false;
   const char* e = getenv("BPP_MSM_DT");
   const int pol = e ? atoi(e) : -1;
@@ -696,7 +698,7 @@ int msm_multi(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, cons
               const MsmPoints& pts, std::vector<h25519::ge>& out) {
   const uint32_t M = (uint32_t)off.size() - 1;
   const uint32_t T = off[M];
-  const bool dt = use_dt(pts, M, T);
+  const bool dt = msm_use_dt(pts, M, T);
   if (!dt && !use_fb(pts, M, T)) return msm_multi(ctx, d_scal, d_pidx, off, pts.tbl, pts.tbl1, pts.n0, out);
   out.assign(M, h25519::ge_identity());
   if (M == 0 || T == 0) return BPP_OK;
@@ -718,9 +720,9 @@ int msm_multi_enc(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, 
   if (M == 0) return BPP_OK;
   // Few results: host encoding beats a latency-bound GPU launch; many: one
   // GPU lane per result, or (doubled) the host batch encoding of 2 R_m.
-  if (M > 16 && T > 0 && (use_dt(pts, M, T) || use_fb(pts, M, T))) {
+  if (M > 16 && T > 0 && (msm_use_dt(pts, M, T) || use_fb(pts, M, T))) {
     uint32_t* d_ws = nullptr;
-    if (use_dt(pts, M, T))
+    if (msm_use_dt(pts, M, T))
       BPP_TRY(msm_multi_dt_dev(ctx, d_scal, d_pidx, off, pts, &d_ws));
     else
       BPP_TRY(msm_multi_fb_dev(ctx, d_scal, d_pidx, off, pts, &d_ws));

@@ -843,41 +843,7 @@ __global__ void __launch_bounds__(RS_FT) k_rsort_fine(const uint32_t* __restrict
 // digit is a fixed bit field of s + K (no per-entry division or scan), and
 // the W lanes sharing a term read the same 32 scalar bytes.  Then an LDS
 // tree over the block's lanes.
-struct DtGeom {
-  uint32_t c, W, H;  // window bits, windows, rows per window (2^(c-1))
-  uint32_t K[8];     // sum_{w < W-1} 2^(c w + c - 1), little-endian words
-};
-#define DT_NT_MAX 256
-
-FE_INLINE uint32_t sel8(const uint32_t v[8], uint32_t i) {  // v[i], 0 for i >= 8 (no scratch)
-  uint32_t r = 0;
-  _Pragma("unroll") for (uint32_t k = 0; k < 8; ++k) r = i == k ? v[k] : r;
-  return r;
-}
-
-// Table row of window w of a term (scalar s, generator gen); d = 0 gives
-// row of |d| = 1 and zero = true (the caller adds the identity instead).
-struct DtLane {
-  uint32_t w, wi, sh, fmask, W, H;
-  bool top;
-  FE_INLINE void row_of(const DtGeom& g, const uint32_t sc[8], uint32_t gen, uint32_t& row, bool& neg,
-                        bool& zero) const {
-    uint32_t s[8];
-    uint64_t c = 0;
-    _Pragma("unroll") for (int i = 0; i < 8; ++i) {
-      c += (uint64_t)sc[i] + g.K[i];
-      s[i] = (uint32_t)c;
-      c >>= 32;
-    }
-    const uint32_t lo = sel8(s, wi), hi = sel8(s, wi + 1);
-    const uint32_t f = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & fmask;
-    const int d = top ? (int)f : (int)f - (int)H;
-    const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
-    zero = ad == 0;
-    neg = d < 0;
-    row = (gen * W + w) * H + (zero ? 0u : ad - 1u);
-  }
-};
+#include "dt_walk.cuh"
 
 __global__ void __launch_bounds__(DT_NT_MAX) k_dt_msm(const uint32_t* __restrict__ dt, DtGeom dg,
                                                     const uint32_t* __restrict__ scalars,
@@ -886,70 +852,15 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_dt_msm(const uint32_t* __restrict
   extern __shared__ uint32_t tl[];  // blockDim.x extended points (40 KB at 256 lanes)
   const uint32_t nt = blockDim.x, TG = nt / dg.W;
   const uint32_t m = blockIdx.x;
+  const DtLane ln = DtLane::make(dg, threadIdx.x % dg.W);
   const uint32_t tg = threadIdx.x / dg.W;
-  DtLane ln;
-  ln.w = threadIdx.x % dg.W;
-  ln.wi = (dg.c * ln.w) >> 5;
-  ln.sh = (dg.c * ln.w) & 31;
-  ln.fmask = (1u << dg.c) - 1u;
-  ln.W = dg.W;
-  ln.H = dg.H;
-  ln.top = ln.w + 1 == dg.W;
-  const uint32_t t1 = off[m + 1];
-  uint32_t t = off[m] + tg;
-  ge_p3 acc = ge_identity();
-  // Software pipeline over this lane's terms t, t + TG, ...: the scalar and
-  // generator index of the term after next are loaded one whole addition
-  // ahead, and the next term's 128-B table row is gathered between the two
-  // halves of the current addition (the operand is dead after its first
-  // three multiplies).  A zero digit adds the identity (no divergent skip).
-  if (tg < TG && t < t1) {
-    uint32_t sc[8];
-    load_scalar(scalars, t, sc);
-    uint32_t gen = pidx ? pidx[t] : t;
-    uint32_t tn = t + TG;
-    uint32_t scn[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint32_t genn = 0;
-    if (tn < t1) {
-      load_scalar(scalars, tn, scn);
-      genn = pidx ? pidx[tn] : tn;
-    }
-    uint32_t row;
-    bool neg, zero;
-    ln.row_of(dg, sc, gen, row, neg, zero);
-    ge_niels q = load_niels(dt, row);
-    for (;;) {
-      if (zero) q = ge_niels_identity();
-      const ge_madd_mid mid = ge_madd_signed_h1(acc, q, neg);
-      const bool more = tn < t1;
-      bool neg2 = false, zero2 = false;
-      if (more) {
-        uint32_t row2;
-        ln.row_of(dg, scn, genn, row2, neg2, zero2);
-        q = load_niels(dt, row2);
-        tn += TG;
-        if (tn < t1) {
-          load_scalar(scalars, tn, scn);
-          genn = pidx ? pidx[tn] : tn;
-        }
-      }
-      acc = ge_madd_h2(mid);
-      if (!more) break;
-      neg = neg2;
-      zero = zero2;
-    }
-  }
-  // block tree in LDS whose waves retire as it narrows
-  store_p3(tl, threadIdx.x, acc);
-  __syncthreads();
-  uint32_t p2 = 1;
-  while (p2 < nt) p2 <<= 1;
-  for (uint32_t s = p2 >> 1; s > 0; s >>= 1) {
-    if (threadIdx.x < s && threadIdx.x + s < nt)
-      store_p3(tl, threadIdx.x, ge_add(load_p3(tl, threadIdx.x), load_p3(tl, threadIdx.x + s)));
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) store_p3(out_p3, m, load_p3(tl, 0));
+  const ge_p3 acc = tg < TG ? dt_walk(dt, dg, ln, off[m] + tg, off[m + 1], TG,
+                                      [&](uint32_t t, uint32_t s[8], uint32_t& gen) {
+                                        load_scalar(scalars, t, s);
+                                        gen = pidx ? pidx[t] : t;
+                                      })
+                            : ge_identity();
+  dt_block_tree(tl, acc, nt, out_p3, m);
 }
 
 // Direct tables from the window tables (wt[k * 32 + u] = 2^(8u) P_k): lane

@@ -39,11 +39,16 @@ def work(t):
 
 if os.environ.get("WITH_TORCH"):
     torch.cuda.synchronize()
+import resource  # noqa: E402
 th = [threading.Thread(target=work, args=(t,)) for t in range(T)]
+ru0 = resource.getrusage(resource.RUSAGE_SELF)
 t0 = time.perf_counter()
 for x in th:
     x.start()
 for x in th:
     x.join()
 el = time.perf_counter() - t0
-print(f"B={B} T={T}: {T * reps * B / el:.0f} proofs/s ({el / (T * reps) * 1e3:.3f} ms per batch)")
+ru1 = resource.getrusage(resource.RUSAGE_SELF)
+cpu = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
+print(f"B={B} T={T}: {T * reps * B / el:.0f} proofs/s ({el / (T * reps) * 1e3:.3f} ms per batch), "
+      f"host CPU {cpu / el:.1f} cores busy, {cpu / (T * reps * B) * 1e6:.1f} us CPU per proof")

@@ -15,11 +15,13 @@
 // k_ipa_cross), a 2-MSM batch through the Pippenger engine, the Fiat-Shamir
 // challenge on the host, and the scalar fold (k_ipa_fold).  L, R, a, b are
 // identical group elements / scalars to the folding form (same transcript).
+#include <cstdlib>
 #include <cstring>
 
 #include "ctx.h"
 #include "dt_walk.cuh"
 #include "ipa.h"
+#include "merlin_dev.h"
 #include "msm_engine.h"
 #include "host/par.h"
 #include "sc25519.cuh"
@@ -197,7 +199,9 @@ __global__ void __launch_bounds__(256) k_ipa_fold(uint32_t n, uint32_t lg_n, uin
 //      a_lo fG_hi and b_hi fH_lo, R the mirror) and c_L or c_R (block
 //      reduction of a_lo b_hi / a_hi b_lo) times qmul for the Q term;
 //   3. runs the direct-table walk over those terms and the block tree
-//      (dt_walk.cuh) -> out_p3[blockIdx.x] = L/2 or R/2.
+//      (dt_walk.cuh) -> out_p3[blockIdx.x] = L/2 or R/2 (halve: the host
+//      encodes 2 (L/2)), or L / R (the device transcript path encodes them
+//      on the GPU).
 // One launch per round instead of four: the latency of three small kernels
 // and their passes over the [P][n] arrays leave every round of a batch.
 __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
@@ -205,7 +209,7 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
     const uint32_t* __restrict__ am_in, const uint32_t* __restrict__ bm_in, const uint32_t* __restrict__ fG_in,
     const uint32_t* __restrict__ fH_in, uint32_t* __restrict__ am_out, uint32_t* __restrict__ bm_out,
     uint32_t* __restrict__ fG_out, uint32_t* __restrict__ fH_out, const uint32_t* __restrict__ u,
-    const uint32_t* __restrict__ qmul, uint32_t gbase, uint32_t hbase, uint32_t qidx, uint32_t TG,
+    const uint32_t* __restrict__ qmul, uint32_t gbase, uint32_t hbase, uint32_t qidx, uint32_t TG, uint32_t halve,
     uint32_t* __restrict__ out_p3) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* tsc = lds;                           // (n + 1) x 8 words: halved term scalars
@@ -259,10 +263,12 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
     const uint32_t p = r ^ h;
     const uint32_t cidx = ((k >> (lg_h + 1)) << lg_h) | (k & (h - 1));
     if (hi == (side == 0)) {
-      sc_store(tsc + 8 * cidx, sc_half(sc_mont(sc_load(sa + 8 * p), fg)));
+      const sc x = sc_mont(sc_load(sa + 8 * p), fg);
+      sc_store(tsc + 8 * cidx, halve ? sc_half(x) : x);
       tgen[cidx] = gbase + k;
     } else {
-      sc_store(tsc + 8 * ((n >> 1) + cidx), sc_half(sc_mont(sc_load(sb + 8 * p), fh)));
+      const sc x = sc_mont(sc_load(sb + 8 * p), fh);
+      sc_store(tsc + 8 * ((n >> 1) + cidx), halve ? sc_half(x) : x);
       tgen[(n >> 1) + cidx] = hbase + k;
     }
   }
@@ -277,7 +283,8 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
   if (tid == 0) {
     sc t = sc_zero();
     for (uint32_t wv = 0; wv < (nt + 63) / 64; ++wv) t = sc_add(t, sc_load(red + 8 * wv));
-    sc_store(tsc + 8 * n, sc_half(sc_mont(t, sc_load(qmul + 8 * inst))));  // Montgomery c * canonical q
+    const sc cq = sc_mont(t, sc_load(qmul + 8 * inst));  // Montgomery c * canonical q
+    sc_store(tsc + 8 * n, halve ? sc_half(cq) : cq);
     tgen[n] = qidx;
   }
   __syncthreads();
@@ -390,6 +397,20 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
     while (TG > 1 && (double)(n + 1) < 2.0 * TG) TG >>= 1;
     nt = TG * dg.W;
   }
+  // Device transcript path (an A/B experiment: see
+  // DESIGN.md): the rounds run back to back on the stream -- fused MSM,
+  // k_compress_p3 of L and R, k_ipa_transcript_step (Merlin + u^-1) --
+  // with no host round trip; L, R and the transcripts come back at the end.
+  const char* dm_env = getenv("BPP_IPA_DEVICE_MERLIN");
+  const bool dev_merlin = fused && dm_env && atoi(dm_env) != 0;
+  void *d_states = nullptr, *d_lr = nullptr;
+  if (dev_merlin) {
+    std::vector<uint8_t> stt((size_t)P * MERLIN_DEV_STATE_BYTES);
+    for (uint32_t p = 0; p < P; ++p) merlin_state_export(*trs[p], &stt[(size_t)p * MERLIN_DEV_STATE_BYTES]);
+    BPP_TRY(ctx_ws(ctx, "ipa_mstate", stt.size(), &d_states));
+    BPP_TRY(ctx_h2d(ctx, d_states, stt.data(), stt.size()));
+    BPP_TRY(ctx_ws(ctx, "ipa_lr", (size_t)lg_n * P * 64, &d_lr));
+  }
   int cur = 0;  // set holding the state at the start of a round (before its fold)
   uint32_t m = n, round = 0;
   uint32_t lg_h = lg_n ? lg_n - 1 : 0;  // log2(m/2)
@@ -402,7 +423,7 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
         hipLaunchKernelGGL(k_ipa_round_dt, dim3(2 * P), dim3(nt), ipa_round_lds_words(n, nt) * 4, ctx->stream,
                            g.pts.dt, dg, n, m, lg_h, round ? 1u : 0u, S[in][0], S[in][1], S[in][2], S[in][3],
                            S[outs][0], S[outs][1], S[outs][2], S[outs][3], (const uint32_t*)d_u, (const uint32_t*)d_q,
-                           g.gbase, g.hbase, g.qidx, TG, (uint32_t*)d_res);
+                           g.gbase, g.hbase, g.qidx, TG, dev_merlin ? 0u : 1u, (uint32_t*)d_res);
       }
       BPP_TRY(ctx_check_launch(ctx, "k_ipa_round_dt"));
       if (round) cur = outs;
@@ -414,8 +435,14 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
       ctx_work(ctx, "dt_terms", terms);
       ctx_work(ctx, "dt_madds", terms * dg.W);
       ctx_work(ctx, "dt_launches", 1);
-      HostScope hs(ctx, "ipa_msm");
-      BPP_TRY(points_double_encode_p3(ctx, (const uint32_t*)d_res, 2 * (size_t)P, enc.data()));
+      if (dev_merlin) {
+        uint8_t* lr = (uint8_t*)d_lr + (size_t)round * P * 64;
+        BPP_TRY(points_compress_p3_dev(ctx, (const uint32_t*)d_res, 2 * (size_t)P, lr));
+        BPP_TRY(ipa_transcript_step_dev(ctx, P, (uint8_t*)d_states, lr, (uint32_t*)d_u));
+      } else {
+        HostScope hs(ctx, "ipa_msm");
+        BPP_TRY(points_double_encode_p3(ctx, (const uint32_t*)d_res, 2 * (size_t)P, enc.data()));
+      }
     } else {
       {
         ProfScope ps(ctx, "ipa_terms");
@@ -437,6 +464,7 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
       // encoded as L, R (msm_multi_enc)
       BPP_TRY(msm_multi_enc(ctx, (const uint32_t*)scal, (const uint32_t*)pidx, off, g.pts, enc.data(), true));
     }
+    if (!dev_merlin) {
     HostScope hs(ctx, "ipa_host");
     par::for_each(P, [&](size_t p) {
       Enc32 Le, Re;
@@ -457,6 +485,7 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
       memcpy(&uw[16 * (size_t)p + 8], uim.v, 32);
     }
     BPP_TRY(ctx_h2d(ctx, d_u, uw.data(), uw.size() * 4));
+    }
     // the fused rounds fold inside the next round's launch; the last
     // challenge (and every challenge of the unfused path) is folded here
     if (!fused || h == 1) {
@@ -472,6 +501,21 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
   }
   am = S[cur][0];
   bm = S[cur][1];
+  if (dev_merlin) {  // L, R of every round and the transcripts back to the host
+    std::vector<uint8_t> lr((size_t)lg_n * P * 64), stt((size_t)P * MERLIN_DEV_STATE_BYTES);
+    BPP_TRY(ctx_d2h(ctx, lr.data(), d_lr, lr.size()));
+    BPP_TRY(ctx_d2h(ctx, stt.data(), d_states, stt.size()));
+    for (uint32_t p = 0; p < P; ++p) {
+      merlin_state_import(*trs[p], &stt[(size_t)p * MERLIN_DEV_STATE_BYTES]);
+      for (uint32_t j = 0; j < lg_n; ++j) {
+        Enc32 Le, Re;
+        memcpy(Le.data(), &lr[((size_t)j * P + p) * 64], 32);
+        memcpy(Re.data(), &lr[((size_t)j * P + p) * 64 + 32], 32);
+        out[p].L.push_back(Le);
+        out[p].R.push_back(Re);
+      }
+    }
+  }
   // a, b = element 0 of each instance
   std::vector<uint32_t> ab((size_t)P * 16);
   {

@@ -23,6 +23,8 @@ int msm_single_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx,
                    uint32_t n0 = 0xffffffffu);
 int upload_scalars(bpp_ctx* ctx, const uint8_t* scalars, size_t n, const char* name, uint32_t** d_out);
 int points_compress_p3(bpp_ctx* ctx, const uint32_t* d_p3, size_t n, uint8_t* out_host);
+// same, encodings left on the device (d_out: n x 32 B)
+int points_compress_p3_dev(bpp_ctx* ctx, const uint32_t* d_p3, size_t n, uint8_t* d_out);
 // out = encodings of 2 * P_i (host batch encoding; see points.hip)
 int points_double_encode_p3(bpp_ctx* ctx, const uint32_t* d_p3, size_t n, uint8_t* out_host);
 // d_out[i] = d_in[i] / 2 mod l (canonical scalars; in place allowed)

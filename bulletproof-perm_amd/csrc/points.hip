@@ -70,14 +70,19 @@ __global__ void __launch_bounds__(64) k_compress_p3(const uint32_t* __restrict__
 
 static unsigned grid_for(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
-int points_compress_p3(bpp_ctx* ctx, const uint32_t* d_p3, size_t n, uint8_t* out_host) {
-  void* d_out = nullptr;
-  BPP_TRY(ctx_ws(ctx, "compress_out", n * 32, &d_out));
+int points_compress_p3_dev(bpp_ctx* ctx, const uint32_t* d_p3, size_t n, uint8_t* d_out) {
+  if (!n) return BPP_OK;
   {
     ProfScope ps(ctx, "compress");
     hipLaunchKernelGGL(k_compress_p3, dim3(grid_for(n, 64)), dim3(64), 0, ctx->stream, d_p3, n, (uint32_t*)d_out);
   }
-  BPP_TRY(ctx_check_launch(ctx, "k_compress_p3"));
+  return ctx_check_launch(ctx, "k_compress_p3");
+}
+
+int points_compress_p3(bpp_ctx* ctx, const uint32_t* d_p3, size_t n, uint8_t* out_host) {
+  void* d_out = nullptr;
+  BPP_TRY(ctx_ws(ctx, "compress_out", n * 32, &d_out));
+  BPP_TRY(points_compress_p3_dev(ctx, d_p3, n, (uint8_t*)d_out));
   BPP_TRY(ctx_d2h(ctx, out_host, d_out, n * 32));
   return BPP_OK;
 }

@@ -181,6 +181,8 @@ static inline Sc pow(const Sc& a, const Sc& e) {
   return mont(rR, one());
 }
 
+static inline bool is_zero(const Sc& a) { return (a.v[0] | a.v[1] | a.v[2] | a.v[3]) == 0; }
+
 static inline Sc invert(const Sc& a) {
   Sc e = sub_raw(L, from_u64(2), nullptr);
   return pow(a, e);

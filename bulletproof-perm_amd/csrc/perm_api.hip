@@ -431,48 +431,78 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
   return BPP_OK;
 }
 
-// Verifier: host scalars for one proof, unweighted (the batch weight is
-// applied when the batch is merged, verify_terms_weighted).  gen_sc (2n_p +
-// 2: G, H, B, Bb) is set; proof-point scalars (m + 8 + 2lg, order V, A_I,
-// A_O, S, T1..T6, L.., R..) are appended to pt_sc.
-bool verify_scalars(const perm::Circuit& C, const Proof& P, merlin::Transcript& tr, std::vector<Sc>& gen_sc,
-                    std::vector<Sc>& pt_sc, Sc* weight_challenge) {
+// Verifier, phase 1: replay one proof's transcript (all Fiat-Shamir
+// challenges; point validation as validate_and_append_point).
+struct VerifyChallenges {
+  Sc x_perm, y, z, x, w, r;
+  std::vector<Sc> u;  // IPA round challenges
+};
+
+bool verify_replay(const perm::Circuit& C, const Proof& P, merlin::Transcript& tr, VerifyChallenges& ch) {
   const uint32_t k = C.k, n_p = C.n_p, m = C.m;
-  if (P.V.size() != m) return false;
+  if (P.V.size() != m || P.ipa.L.size() != C.lg || P.ipa.R.size() != C.lg) return false;
   tr.arithmetic_domain_sep(n_p);
   for (uint32_t j = 0; j < 2 * k; ++j) tr.append_point("V", P.V[j].data());
-  const Sc x_perm = tr.challenge_scalar("x_perm");
+  ch.x_perm = tr.challenge_scalar("x_perm");
   tr.append_point("V", P.V[2 * k].data());
   if (!tr.validate_and_append_point("A_I", P.AI.data())) return false;
   if (!tr.validate_and_append_point("A_O", P.AO.data())) return false;
   if (!tr.validate_and_append_point("S", P.S.data())) return false;
-  const Sc y = tr.challenge_scalar("y");
-  const Sc z = tr.challenge_scalar("z");
+  ch.y = tr.challenge_scalar("y");
+  ch.z = tr.challenge_scalar("z");
   static const char* lab[5] = {"T1", "T3", "T4", "T5", "T6"};
   for (int i = 0; i < 5; ++i)
     if (!tr.validate_and_append_point(lab[i], P.T[i].data())) return false;
-  const Sc x = tr.challenge_scalar("x");
+  ch.x = tr.challenge_scalar("x");
   tr.append_scalar("TX", P.tau_x);
   tr.append_scalar("mu", P.mu);
   tr.append_scalar("t", P.t_hat);
-  const Sc w = tr.challenge_scalar("w");
-  std::vector<Sc> u_sq, uinv_sq, s;
-  if (!ipa_verification_scalars(tr, n_p, P.ipa.L, P.ipa.R, u_sq, uinv_sq, s)) return false;
-  const Sc r = tr.challenge_scalar("t-check-weight");
-  if (weight_challenge) *weight_challenge = r;
+  ch.w = tr.challenge_scalar("w");
+  // bulletproofs InnerProductProof::verification_scalars, transcript part
+  tr.innerproduct_domain_sep(n_p);
+  ch.u.resize(C.lg);
+  for (uint32_t j = 0; j < C.lg; ++j) {
+    if (!tr.validate_and_append_point("L", P.ipa.L[j].data())) return false;
+    if (!tr.validate_and_append_point("R", P.ipa.R[j].data())) return false;
+    ch.u[j] = tr.challenge_scalar("u");
+  }
+  ch.r = tr.challenge_scalar("t-check-weight");
+  return true;
+}
 
-  std::vector<Sc> xp = hsc::powers(x, 7);
-  std::vector<Sc> y_inv_n = hsc::powers(hsc::invert(y), n_p);
-  std::vector<Sc> zq = hsc::powers(z, C.Q + 1);
-  zq.erase(zq.begin());
-  const std::vector<Sc> zWL = perm::zW(C.WL, zq, n_p), zWR = perm::zW(C.WR, zq, n_p), zWO = perm::zW(C.WO, zq, n_p),
-                        zWV = perm::zW(C.WV, zq, m);
-  std::vector<Sc> c = C.c;
-  c[C.Q - 1] = hsc::neg(x_perm);
+// Verifier, phase 2: the proof's unweighted MSM scalars from its challenges
+// and the inverses y^-1, u_j^-1 (batch-inverted across proofs by the
+// caller).  gen_sc (2n_p + 2: G, H, B, Bb) is set; proof-point scalars
+// (m + 8 + 2lg, order V, A_I, A_O, S, T1..T6, L.., R..) are appended.
+void verify_expand(const perm::Circuit& C, const Proof& P, const VerifyChallenges& ch, const Sc& y_inv,
+                   const Sc* u_inv, std::vector<Sc>& gen_sc, std::vector<Sc>& pt_sc) {
+  const uint32_t n_p = C.n_p, m = C.m, lg = C.lg;
   using hsc::add;
   using hsc::mul;
   using hsc::neg;
   using hsc::sub;
+  // s_i = prod_j u_j^(+-1) (bulletproofs verification_scalars)
+  std::vector<Sc> u_sq(lg), uinv_sq(lg), s(n_p);
+  Sc allinv = hsc::one();
+  for (uint32_t j = 0; j < lg; ++j) {
+    u_sq[j] = hsc::sq(ch.u[j]);
+    uinv_sq[j] = hsc::sq(u_inv[j]);
+    allinv = mul(allinv, u_inv[j]);
+  }
+  s[0] = allinv;
+  for (uint32_t i = 1; i < n_p; ++i) {
+    const uint32_t lg_i = 31 - __builtin_clz(i), kk = 1u << lg_i;
+    s[i] = mul(s[i - kk], u_sq[lg - 1 - lg_i]);
+  }
+  const Sc x = ch.x, r = ch.r, w = ch.w;
+  std::vector<Sc> xp = hsc::powers(x, 7);
+  std::vector<Sc> y_inv_n = hsc::powers(y_inv, n_p);
+  std::vector<Sc> zq = hsc::powers(ch.z, C.Q + 1);
+  zq.erase(zq.begin());
+  const std::vector<Sc> zWL = perm::zW(C.WL, zq, n_p), zWR = perm::zW(C.WR, zq, n_p), zWO = perm::zW(C.WO, zq, n_p),
+                        zWV = perm::zW(C.WV, zq, m);
+  std::vector<Sc> c = C.c;
+  c[C.Q - 1] = hsc::neg(ch.x_perm);
   Sc delta = hsc::zero();
   for (uint32_t i = 0; i < n_p; ++i) delta = add(delta, mul(mul(y_inv_n[i], zWR[i]), zWL[i]));
   const Sc aR_ = hsc::to_mont(P.ipa.a), bR_ = hsc::to_mont(P.ipa.b), xR_ = hsc::to_mont(x);
@@ -500,9 +530,8 @@ bool verify_scalars(const perm::Circuit& C, const Proof& P, merlin::Transcript& 
   pt_sc.push_back(neg(xp[3]));
   const int tidx[5] = {1, 3, 4, 5, 6};
   for (int i = 0; i < 5; ++i) pt_sc.push_back(neg(mul(r, xp[tidx[i]])));
-  for (uint32_t j = 0; j < C.lg; ++j) pt_sc.push_back(neg(u_sq[j]));
-  for (uint32_t j = 0; j < C.lg; ++j) pt_sc.push_back(neg(uinv_sq[j]));
-  return true;
+  for (uint32_t j = 0; j < lg; ++j) pt_sc.push_back(neg(u_sq[j]));
+  for (uint32_t j = 0; j < lg; ++j) pt_sc.push_back(neg(uinv_sq[j]));
 }
 
 void proof_points(const Proof& P, std::vector<uint8_t>& enc) {
@@ -547,11 +576,35 @@ int verify_begin(const perm::Circuit& C, const uint8_t* label, size_t llen, size
   J.gen_p.resize(count);
   J.pt_p.resize(count);
   std::vector<uint8_t> ok(count, 0);
-  par::for_each(count, [&](size_t p) {
-    if (!deserialize(C, proofs + p * proof_stride, perm::proof_len(C.k), V + p * 32 * C.m, J.Ps[p])) return;
-    merlin::Transcript tr(label, llen);
-    J.gen_p[p].assign(2 * n_p + 2, hsc::zero());
-    ok[p] = verify_scalars(C, J.Ps[p], tr, J.gen_p[p], J.pt_p[p], &J.rs[p]) ? 1 : 0;
+  // chunks of proofs: replay their transcripts, invert every y and u of the
+  // chunk with ONE inversion (Montgomery's trick), then expand the scalars
+  const size_t chunks = std::max<size_t>(1, std::min<size_t>(count, 64));
+  par::for_each(chunks, [&](size_t chk) {
+    const size_t p0 = chk * count / chunks, p1 = (chk + 1) * count / chunks;
+    std::vector<VerifyChallenges> ch(p1 - p0);
+    std::vector<Sc> inv;
+    inv.reserve((p1 - p0) * (1 + C.lg));
+    for (size_t p = p0; p < p1; ++p) {
+      if (!deserialize(C, proofs + p * proof_stride, perm::proof_len(C.k), V + p * 32 * C.m, J.Ps[p])) return;
+      merlin::Transcript tr(label, llen);
+      if (!verify_replay(C, J.Ps[p], tr, ch[p - p0])) return;
+      // a zero challenge has negligible probability; it would make the
+      // batch inversion fail, so such a proof is rejected
+      if (hsc::is_zero(ch[p - p0].y)) return;
+      inv.push_back(ch[p - p0].y);
+      for (const Sc& u : ch[p - p0].u) {
+        if (hsc::is_zero(u)) return;
+        inv.push_back(u);
+      }
+    }
+    hsc::batch_invert(inv, false);
+    for (size_t p = p0; p < p1; ++p) {
+      const Sc* iv = &inv[(p - p0) * (1 + C.lg)];
+      J.gen_p[p].assign(2 * n_p + 2, hsc::zero());
+      verify_expand(C, J.Ps[p], ch[p - p0], iv[0], iv + 1, J.gen_p[p], J.pt_p[p]);
+      J.rs[p] = ch[p - p0].r;
+      ok[p] = 1;
+    }
   });
   for (size_t p = 0; p < count; ++p)
     if (!ok[p]) return BPP_ERR_VERIFY;

@@ -21,6 +21,7 @@
 #include <cstdlib>
 #include <sys/random.h>
 #include <memory>
+#include <mutex>
 #include <thread>
 
 #include "ctx.h"
@@ -555,61 +556,79 @@ struct bpp_verify_job {
   perm::Circuit C;
   size_t count = 0, npt = 0;
   std::vector<Proof> Ps;
-  std::vector<Sc> rs;                         // per-proof weight challenges
-  std::vector<std::vector<Sc>> gen_p, pt_p;  // unweighted generator / proof-point scalars
+  std::vector<Sc> rs;                 // per-proof weight challenges
+  std::vector<VerifyChallenges> ch;   // every proof's transcript challenges
+  std::vector<Sc> inv;                // per proof: y^-1, u_0^-1 .. u_{lg-1}^-1
+  // unweighted generator / proof-point scalars, expanded on the host only
+  // when asked for (bpp_perm_verify_scalars); the GPU path expands them on
+  // the device (k_verify_scalars)
+  mutable std::mutex mu;
+  mutable bool expanded = false;
+  mutable std::vector<std::vector<Sc>> gen_p, pt_p;
 };
 
 namespace {
 
-// pass 1 (parallel over proofs): parse, replay each transcript, and collect
-// the unweighted generator / proof-point scalars and the proof's weight
-// challenge r (circuit_lib.rs:478-585 restated in sound mode)
+// pass 1 (parallel over chunks of proofs): parse, replay each transcript
+// (all challenges and the proof's weight challenge r), and invert every y
+// and u of a chunk with ONE inversion (Montgomery's trick)
+// (circuit_lib.rs:478-585 restated in sound mode)
 int verify_begin(const perm::Circuit& C, const uint8_t* label, size_t llen, size_t count, const uint8_t* proofs,
                  size_t proof_stride, const uint8_t* V, std::unique_ptr<bpp_verify_job>& job) {
-  const uint32_t n_p = C.n_p;
   job.reset(new bpp_verify_job);
   bpp_verify_job& J = *job;
   J.C = C;
   J.count = count;
+  J.npt = (size_t)C.m + 8 + 2 * C.lg;
   J.Ps.resize(count);
   J.rs.resize(count);
-  J.gen_p.resize(count);
-  J.pt_p.resize(count);
+  J.ch.resize(count);
+  J.inv.resize(count * (1 + C.lg));
   std::vector<uint8_t> ok(count, 0);
-  // chunks of proofs: replay their transcripts, invert every y and u of the
-  // chunk with ONE inversion (Montgomery's trick), then expand the scalars
   const size_t chunks = std::max<size_t>(1, std::min<size_t>(count, 64));
   par::for_each(chunks, [&](size_t chk) {
     const size_t p0 = chk * count / chunks, p1 = (chk + 1) * count / chunks;
-    std::vector<VerifyChallenges> ch(p1 - p0);
     std::vector<Sc> inv;
     inv.reserve((p1 - p0) * (1 + C.lg));
     for (size_t p = p0; p < p1; ++p) {
       if (!deserialize(C, proofs + p * proof_stride, perm::proof_len(C.k), V + p * 32 * C.m, J.Ps[p])) return;
       merlin::Transcript tr(label, llen);
-      if (!verify_replay(C, J.Ps[p], tr, ch[p - p0])) return;
+      VerifyChallenges& ch = J.ch[p];
+      if (!verify_replay(C, J.Ps[p], tr, ch)) return;
       // a zero challenge has negligible probability; it would make the
       // batch inversion fail, so such a proof is rejected
-      if (hsc::is_zero(ch[p - p0].y)) return;
-      inv.push_back(ch[p - p0].y);
-      for (const Sc& u : ch[p - p0].u) {
+      if (hsc::is_zero(ch.y)) return;
+      inv.push_back(ch.y);
+      for (const Sc& u : ch.u) {
         if (hsc::is_zero(u)) return;
         inv.push_back(u);
       }
     }
     hsc::batch_invert(inv, false);
+    std::copy(inv.begin(), inv.end(), J.inv.begin() + p0 * (1 + C.lg));
     for (size_t p = p0; p < p1; ++p) {
-      const Sc* iv = &inv[(p - p0) * (1 + C.lg)];
-      J.gen_p[p].assign(2 * n_p + 2, hsc::zero());
-      verify_expand(C, J.Ps[p], ch[p - p0], iv[0], iv + 1, J.gen_p[p], J.pt_p[p]);
-      J.rs[p] = ch[p - p0].r;
+      J.rs[p] = J.ch[p].r;
       ok[p] = 1;
     }
   });
   for (size_t p = 0; p < count; ++p)
     if (!ok[p]) return BPP_ERR_VERIFY;
-  J.npt = count ? J.pt_p[0].size() : 0;
   return BPP_OK;
+}
+
+// Host expansion of every proof's unweighted scalars (verify_expand), once.
+void job_expand_host(const bpp_verify_job& J) {
+  std::lock_guard<std::mutex> g(J.mu);
+  if (J.expanded) return;
+  const perm::Circuit& C = J.C;
+  J.gen_p.assign(J.count, std::vector<Sc>());
+  J.pt_p.assign(J.count, std::vector<Sc>());
+  par::for_each(J.count, [&](size_t p) {
+    J.gen_p[p].assign(2 * C.n_p + 2, hsc::zero());
+    const Sc* iv = &J.inv[p * (1 + C.lg)];
+    verify_expand(C, J.Ps[p], J.ch[p], iv[0], iv + 1, J.gen_p[p], J.pt_p[p]);
+  });
+  J.expanded = true;
 }
 
 // Terms of the job's MSM: merged generators (G, H, B, Bb) + every proof point.
@@ -636,6 +655,7 @@ int verify_terms_weighted(const bpp_verify_job& J, const Sc* r_all, size_t total
   const uint32_t n_p = J.C.n_p;
   const size_t count = J.count, npt = J.npt;
   if (first > total || count > total - first) return BPP_ERR_ARG;
+  job_expand_host(J);
   std::vector<Sc> wR = batch_weights(r_all, total);  // -> Montgomery form (one step per product)
   for (auto& w : wR) w = hsc::to_mont(w);
   const Sc* wts = wR.data() + first;
@@ -672,13 +692,46 @@ int verify_partial(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J, con
     ctx->err = "generators shorter than the padded circuit";
     return BPP_ERR_LEN;
   }
-  const size_t NG = 2 * (size_t)n_p + 2;
-  std::vector<Sc> sc;
-  std::vector<uint8_t> enc;
+  const size_t NG = 2 * (size_t)n_p + 2, count = J.count, npt = J.npt, T = NG + count * npt;
+  if (first > total || count > total - first) return BPP_ERR_ARG;
+  const uint32_t lg = J.C.lg, nrec = 12 + 2 * lg;
+  // per-proof records for k_verify_scalars and the proof points' encodings
+  std::vector<uint32_t> rec(count * nrec * 8);
+  std::vector<uint8_t> enc(count * npt * 32);
   {
     HostScope hs(ctx, "verify_terms");
-    BPP_TRY(verify_terms_weighted(J, r_all, total, first, sc, enc));
+    const std::vector<Sc> wts = batch_weights(r_all, total);
+    par::for_each(count, [&](size_t p) {
+      const VerifyChallenges& ch = J.ch[p];
+      const Proof& P = J.Ps[p];
+      const Sc* iv = &J.inv[p * (1 + lg)];
+      uint32_t* r = &rec[p * nrec * 8];
+      auto put = [&](uint32_t k, const Sc& v) { hsc::to_bytes((uint8_t*)(r + 8 * k), v); };
+      put(0, ch.x_perm);
+      put(1, iv[0]);
+      put(2, ch.z);
+      put(3, ch.x);
+      put(4, ch.w);
+      put(5, ch.r);
+      put(6, P.ipa.a);
+      put(7, P.ipa.b);
+      put(8, P.t_hat);
+      put(9, P.tau_x);
+      put(10, P.mu);
+      put(11, wts[first + p]);
+      for (uint32_t j = 0; j < lg; ++j) {
+        put(12 + j, ch.u[j]);
+        put(12 + lg + j, iv[1 + j]);
+      }
+      std::vector<uint8_t> e;
+      e.reserve(npt * 32);
+      proof_points(P, e);
+      memcpy(&enc[p * npt * 32], e.data(), npt * 32);
+    });
   }
+  void* d_sv = nullptr;
+  BPP_TRY(ctx_ws(ctx, "pv_s", T * 32 + 32, &d_sv));
+  BPP_TRY(verify_scalars_dev(ctx, J.C, (uint32_t)count, rec, (uint32_t*)d_sv));
   uint32_t* d_x = nullptr;
   int rc = decompress_ws(ctx, enc.data(), enc.size() / 32, "pv_x", &d_x);
   if (rc == BPP_ERR_DECOMPRESS) return BPP_ERR_VERIFY;
@@ -689,23 +742,21 @@ int verify_partial(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J, con
   const uint32_t n0 = (uint32_t)(2 * G->n + 2);
   uint32_t* d_idx = nullptr;
   if (G->n != n_p) {
-    std::vector<uint32_t> idx(sc.size());
+    std::vector<uint32_t> idx(T);
     for (uint32_t i = 0; i < n_p; ++i) {
       idx[i] = G->gidx(i);
       idx[n_p + i] = G->hidx(i);
     }
     idx[2 * n_p] = G->bidx();
     idx[2 * n_p + 1] = G->bbidx();
-    for (size_t j = NG; j < sc.size(); ++j) idx[j] = n0 + (uint32_t)(j - NG);
+    for (size_t j = NG; j < T; ++j) idx[j] = n0 + (uint32_t)(j - NG);
     void* d = nullptr;
     BPP_TRY(ctx_ws(ctx, "pv_idx", idx.size() * 4 + 4, &d));
     BPP_TRY(ctx_h2d(ctx, d, idx.data(), idx.size() * 4));
     d_idx = (uint32_t*)d;
   }
-  uint32_t* d_s = nullptr;
-  BPP_TRY(upload_sc(ctx, sc, "pv_s", &d_s));
-  const uint32_t c = msm_choose_c((double)sc.size());
-  return msm_single_dev(ctx, d_s, d_idx, G->d_tbl, sc.size(), c, wb, we - wb, out, d_x, n0);
+  const uint32_t c = msm_choose_c((double)T);
+  return msm_single_dev(ctx, (const uint32_t*)d_sv, d_idx, G->d_tbl, T, c, wb, we - wb, out, d_x, n0);
 }
 
 // Verify `count` proofs with ONE MSM: generator scalars summed across proofs

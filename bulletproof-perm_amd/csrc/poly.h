@@ -17,3 +17,11 @@ int poly_coef_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint32
 // H factors, and t_hat = <l, r> per proof.
 int poly_x_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const std::vector<hsc::Sc>& x, uint32_t** d_l,
                uint32_t** d_r, uint32_t** d_hf, std::vector<hsc::Sc>& t_hat);
+
+// The batch verifier's MSM scalars for `count` proofs (k_verify_scalars +
+// k_verify_merge): rec = [count][12 + 2 lg] canonical scalars (x_perm,
+// y^-1, z, x, w, r, a, b, t_hat, tau_x, mu, weight, u_j.., u_j^-1..);
+// d_sc (device) receives the 2 n_p + 2 merged generator scalars then
+// count x (m + 8 + 2 lg) weighted proof-point scalars.
+int verify_scalars_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const std::vector<uint32_t>& rec,
+                       uint32_t* d_sc);

@@ -139,20 +139,132 @@ __global__ void __launch_bounds__(POLY_T) k_poly_x(uint32_t n_p, const uint32_t*
   if (threadIdx.x == 0) sc_store(that_out + 8 * p, sc_from_mont(th[0]));
 }
 
+// ---------------------------------------------------------------------------
+// Batch verifier's MSM scalars on the GPU (the verifier side of the same
+// circuit algebra, circuit_lib.rs:478-585 in sound form; host restatement
+// perm_api.hip verify_expand, which bpp_perm_verify_scalars still uses).
+// One workgroup per proof; rec[p] = VREC_N canonical scalars:
+#define VREC_XPERM 0
+#define VREC_YINV 1
+#define VREC_Z 2
+#define VREC_X 3
+#define VREC_W 4
+#define VREC_R 5
+#define VREC_A 6
+#define VREC_B 7
+#define VREC_THAT 8
+#define VREC_TAUX 9
+#define VREC_MU 10
+#define VREC_WT 11  // the proof's batch weight
+#define VREC_U 12   // u_j (lg), then u_j^-1 (lg)
+// Writes wt * (generator scalars) to gen[p][2 n_p + 2] (summed over proofs by
+// k_verify_merge) and wt * (proof-point scalars) to sc_out[NG + p npt + j]
+// (V_0..V_{m-1}, A_I, A_O, S, T1 T3 T4 T5 T6, L_0.., R_0..), canonical.
+__global__ void __launch_bounds__(POLY_T) k_verify_scalars(
+    uint32_t n_p, uint32_t m, uint32_t Q, uint32_t lg, const uint32_t* __restrict__ rec,
+    const uint32_t* __restrict__ cp, const uint32_t* __restrict__ ce, const uint32_t* __restrict__ cR,
+    uint32_t* __restrict__ gen, uint32_t* __restrict__ sc_out, uint32_t NG, uint32_t npt) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  uint32_t* zp = lds;           // [Q] z^(q+1), Montgomery
+  uint32_t* red = lds + 8 * Q;  // reduction scratch
+  const uint32_t p = blockIdx.x, nrec = VREC_U + 2 * lg;
+  const uint32_t* R = rec + (size_t)p * nrec * 8;
+  const sc oneR = sc_one_mont();
+  auto ldm = [&](uint32_t k) { return sc_to_mont(sc_load(R + 8 * k)); };
+  const sc zR = ldm(VREC_Z), xR = ldm(VREC_X), yiR = ldm(VREC_YINV), aR = ldm(VREC_A), bR = ldm(VREC_B),
+           wtR = ldm(VREC_WT), rR = ldm(VREC_R);
+  for (uint32_t q = threadIdx.x; q < Q; q += blockDim.x) sc_store(zp + 8 * q, sc_pow_small(zR, q + 1, oneR));
+  // s_0 = prod u_j^-1; s_i = s_0 prod_{bit k of i} u_{lg-1-k}^2 (bulletproofs
+  // verification_scalars)
+  sc s0R = oneR;
+  for (uint32_t j = 0; j < lg; ++j) s0R = sc_mont(s0R, ldm(VREC_U + lg + j));
+  __syncthreads();
+  auto s_of = [&](uint32_t i) {
+    sc v = s0R;
+    for (uint32_t k = 0; k < lg; ++k)
+      if ((i >> k) & 1u) {
+        const sc u = ldm(VREC_U + lg - 1 - k);
+        v = sc_mont(v, sc_mont(u, u));
+      }
+    return v;
+  };
+  const size_t gb = (size_t)p * NG;
+  sc acc[2] = {sc_zero(), sc_zero()};  // delta = sum y^-i zWR_i zWL_i, zc = <z^Q, c>
+  for (uint32_t i = threadIdx.x; i < n_p; i += blockDim.x) {
+    const sc yi = sc_pow_small(yiR, i, oneR);
+    const sc zWL = col_sum(cp, ce, i, zp), zWR = col_sum(cp + (n_p + 1), ce, i, zp),
+             zWO = col_sum(cp + 2 * (n_p + 1), ce, i, zp);
+    acc[0] = sc_add(acc[0], sc_mont(sc_mont(yi, zWR), zWL));
+    const sc gi = sc_sub(sc_mont(s_of(i), aR), sc_mont(sc_mont(zWR, xR), yi));
+    const sc hi = sc_add(sc_sub(sc_mont(sc_mont(s_of(n_p - 1 - i), bR), yi), sc_mont(sc_add(sc_mont(zWL, xR), zWO), yi)),
+                         oneR);
+    sc_store(gen + 8 * (gb + i), sc_from_mont(sc_mont(gi, wtR)));
+    sc_store(gen + 8 * (gb + n_p + i), sc_from_mont(sc_mont(hi, wtR)));
+  }
+  for (uint32_t q = threadIdx.x; q < Q; q += blockDim.x) {
+    const sc c = q + 1 == Q ? sc_neg(ldm(VREC_XPERM)) : sc_to_mont(sc_load(cR + 8 * q));
+    acc[1] = sc_add(acc[1], sc_mont(sc_load(zp + 8 * q), c));
+  }
+  const sc x2R = sc_mont(xR, xR);
+  const sc wrx2R = sc_mont(sc_mont(wtR, rR), x2R);
+  const size_t pb = NG + (size_t)p * npt;
+  // V_j: -wt r x^2 zWV_j (zWV from the fourth column-CSR, m columns)
+  for (uint32_t j = threadIdx.x; j < m; j += blockDim.x)
+    sc_store(sc_out + 8 * (pb + j), sc_from_mont(sc_neg(sc_mont(col_sum(cp + 3 * (n_p + 1), ce, j, zp), wrx2R))));
+  // A_I, A_O, S: -wt x^(1,2,3); T_k: -wt r x^k (k = 1, 3..6); L_j: -wt u_j^2; R_j: -wt u_j^-2
+  for (uint32_t j = threadIdx.x; j < 8 + 2 * lg; j += blockDim.x) {
+    sc v;
+    if (j < 3) {
+      v = xR;
+      for (uint32_t e = 0; e < j; ++e) v = sc_mont(v, xR);
+    } else if (j < 8) {
+      const uint32_t e = j == 3 ? 1u : j - 1;  // T1, T3, T4, T5, T6
+      v = sc_mont(rR, sc_pow_small(xR, e, oneR));
+    } else {
+      const sc u = ldm(j < 8 + lg ? VREC_U + (j - 8) : VREC_U + lg + (j - 8 - lg));
+      v = sc_mont(u, u);
+    }
+    sc_store(sc_out + 8 * (pb + m + j), sc_from_mont(sc_neg(sc_mont(v, wtR))));
+  }
+  sc_block_sum<2>(acc, red);
+  if (threadIdx.x == 0) {
+    // B: wt (r (t_hat - x^2 (delta + zc)) + w (a b - t_hat)); B_blinding: wt (r tau_x + mu)
+    const sc thR = ldm(VREC_THAT);
+    const sc tB = sc_mont(rR, sc_sub(thR, sc_mont(x2R, sc_add(acc[0], acc[1]))));
+    const sc iB = sc_mont(ldm(VREC_W), sc_sub(sc_mont(aR, bR), thR));
+    sc_store(gen + 8 * (gb + 2 * n_p), sc_from_mont(sc_mont(sc_add(tB, iB), wtR)));
+    const sc bb = sc_add(sc_mont(rR, ldm(VREC_TAUX)), ldm(VREC_MU));
+    sc_store(gen + 8 * (gb + 2 * n_p + 1), sc_from_mont(sc_mont(bb, wtR)));
+  }
+}
+
+// sc_out[i] = sum_p gen[p][i] (one workgroup per generator column)
+__global__ void __launch_bounds__(POLY_T) k_verify_merge(uint32_t count, uint32_t NG, const uint32_t* __restrict__ gen,
+                                                      uint32_t* __restrict__ sc_out) {
+  __shared__ __attribute__((aligned(16))) uint32_t red[(POLY_T / 64) * 8];
+  const uint32_t i = blockIdx.x;
+  sc acc[1] = {sc_zero()};
+  for (uint32_t p = threadIdx.x; p < count; p += blockDim.x) acc[0] = sc_add(acc[0], sc_load(gen + 8 * ((size_t)p * NG + i)));
+  sc_block_sum<1>(acc, red);
+  if (threadIdx.x == 0) sc_store(sc_out + 8 * i, acc[0]);
+}
+
 namespace {
 
 // Column-CSR of WL, WR, WO over the n_p gate columns: cp[3][n_p + 1],
-// entries (q, valR[8]) as 9 words.
-void build_csr(const perm::Circuit& C, std::vector<uint32_t>& cp, std::vector<uint32_t>& ce) {
+// entries (q, valR[8]) as 9 words; with_v appends WV over its m columns at
+// cp[3 (n_p + 1)] (m + 1 offsets, the verifier's V scalars).
+void build_csr(const perm::Circuit& C, std::vector<uint32_t>& cp, std::vector<uint32_t>& ce, bool with_v = false) {
   const uint32_t n_p = C.n_p;
-  cp.assign(3 * (n_p + 1), 0);
+  cp.assign(3 * (n_p + 1) + (with_v ? C.m + 1 : 0), 0);
   ce.clear();
-  const std::vector<perm::Entry>* Ws[3] = {&C.WL, &C.WR, &C.WO};
+  const std::vector<perm::Entry>* Ws[4] = {&C.WL, &C.WR, &C.WO, &C.WV};
   uint32_t total = 0;
-  for (int w = 0; w < 3; ++w) {
-    std::vector<std::vector<const perm::Entry*>> cols(n_p);
+  for (int w = 0; w < (with_v ? 4 : 3); ++w) {
+    const uint32_t ncol = w == 3 ? C.m : n_p;
+    std::vector<std::vector<const perm::Entry*>> cols(ncol);
     for (const perm::Entry& e : *Ws[w]) cols[e.col].push_back(&e);
-    for (uint32_t c = 0; c < n_p; ++c) {
+    for (uint32_t c = 0; c < ncol; ++c) {
       cp[w * (n_p + 1) + c] = total;
       for (const perm::Entry* e : cols[c]) {
         ce.push_back(e->q);
@@ -162,7 +274,7 @@ void build_csr(const perm::Circuit& C, std::vector<uint32_t>& cp, std::vector<ui
         ++total;
       }
     }
-    cp[w * (n_p + 1) + n_p] = total;
+    cp[w * (n_p + 1) + ncol] = total;
   }
 }
 
@@ -219,4 +331,34 @@ int poly_x_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const std::vect
   *d_r = (uint32_t*)d_ro;
   *d_hf = (uint32_t*)hf;
   return BPP_OK;
+}
+
+int verify_scalars_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const std::vector<uint32_t>& rec,
+                       uint32_t* d_sc) {
+  std::vector<uint32_t> cp, ce;
+  build_csr(C, cp, ce, true);
+  std::vector<uint32_t> cw((size_t)C.Q * 8);
+  for (uint32_t q = 0; q < C.Q; ++q) memcpy(&cw[8 * (size_t)q], C.c[q].v, 32);
+  const uint32_t NG = 2 * C.n_p + 2, npt = C.m + 8 + 2 * C.lg;
+  void *d_cp, *d_ce, *d_c, *d_rec, *d_gen;
+  BPP_TRY(ctx_ws(ctx, "vs_cp", cp.size() * 4, &d_cp));
+  BPP_TRY(ctx_ws(ctx, "vs_ce", ce.size() * 4 + 4, &d_ce));
+  BPP_TRY(ctx_ws(ctx, "vs_c", cw.size() * 4, &d_c));
+  BPP_TRY(ctx_ws(ctx, "vs_rec", rec.size() * 4, &d_rec));
+  BPP_TRY(ctx_ws(ctx, "vs_gen", (size_t)count * NG * 32, &d_gen));
+  BPP_TRY(ctx_h2d_const(ctx, "vs_cp", d_cp, cp.data(), cp.size() * 4));  // the circuit: same every batch
+  BPP_TRY(ctx_h2d_const(ctx, "vs_ce", d_ce, ce.data(), ce.size() * 4));
+  BPP_TRY(ctx_h2d_const(ctx, "vs_c", d_c, cw.data(), cw.size() * 4));
+  BPP_TRY(ctx_h2d(ctx, d_rec, rec.data(), rec.size() * 4));
+  const unsigned nt = poly_block(std::max(C.n_p, C.m));
+  const size_t lds = (size_t)C.Q * 32 + (POLY_T / 64) * 2 * 32;
+  {
+    ProfScope ps(ctx, "verify_scalars");
+    hipLaunchKernelGGL(k_verify_scalars, dim3(count), dim3(nt), lds, ctx->stream, C.n_p, C.m, C.Q, C.lg,
+                       (const uint32_t*)d_rec, (const uint32_t*)d_cp, (const uint32_t*)d_ce, (const uint32_t*)d_c,
+                       (uint32_t*)d_gen, d_sc, NG, npt);
+    hipLaunchKernelGGL(k_verify_merge, dim3(NG), dim3(POLY_T), 0, ctx->stream, count, NG, (const uint32_t*)d_gen,
+                       d_sc);
+  }
+  return ctx_check_launch(ctx, "k_verify_scalars/merge");
 }

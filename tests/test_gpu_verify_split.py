@@ -126,3 +126,29 @@ def test_large_batch_radix_path(ctx):
     assert pr.verify_batch(proofs, Vs)
     assert bpperm.partials_is_identity(_window_partials(pr, proofs, Vs, 8))
     g.close()
+
+
+def test_device_scalars_match_host_expansion(setup, ctx):
+    """k_verify_scalars (the GPU path of bpp_perm_verify_partial) computes
+    the same MSM as the host expansion (bpp_perm_verify_scalars, also used by
+    the gloo test): the job's whole-window partial equals the C port's MSM
+    over the host scalars and the generator / proof-point encodings."""
+    import bpperm
+    from oracle import cport
+    gens, pr, proofs, Vs = setup
+    bad = list(proofs)
+    b = bytearray(bad[9])
+    b[8 * 32 + 40] ^= 4  # mu: a non-identity sum, so the comparison is not trivially 0 == 0
+    bad[9] = bytes(b)
+    job = bpperm.VerifyJob(K, bad[:24], Vs[:24])
+    first = 5
+    # the job as a slice [first, first + 24) of a larger batch: the weights
+    # come from every r (the others' stand-ins are small canonical scalars)
+    r_all = b"".join(bytes([(i * 7 + 1) % 251]) + bytes(31) for i in range(first)) + job.r
+    c, W = job.windows()
+    got = bpperm.partials_finish([pr.verify_partial(job, r_all, first, 0, W)])
+    sc, pts = job.scalars(r_all, first)
+    G, H, B, Bb = gens.export()  # n = n_p = 128: G[0..n_p), H[0..n_p), B, B_blinding
+    want = cport.msm(b"".join(sc), b"".join(list(G) + list(H) + [B, Bb] + pts))
+    assert got == want and got != bytes(32)
+    job.close()

@@ -41,7 +41,7 @@ inline unsigned threads() {
     // workers fill the quota without oversubscribing it.  Measured on the
     // box, 128-proof batches: 16 threads x 4 in flight 52-64 K proofs/s,
     // 8 x 8 75-80 K, 8 x 12 80-83 K, 4 x 12 80-81 K; one batch alone
-    // 5.57 ms with 16 threads vs 5.60 ms with 8 (tools/gpu_exp4.sh).
+    // 5.57 ms with 16 threads vs 5.60 ms with 8 (tools/EXPERIMENTS.md exp2-4).
     const unsigned v = e ? (unsigned)atoi(e) : std::max(1u, std::min(16u, granted_cpus()) / 2);
     return std::max(1u, v);
   }();

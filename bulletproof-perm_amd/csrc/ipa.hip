@@ -291,6 +291,10 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
   // 3. direct-table walk over the LDS terms, then the block tree (reusing LDS)
   const uint32_t tg = tid / dg.W;
   const DtLane ln = DtLane::make(dg, tid % dg.W);
+#ifdef EXP_IPA_NOWALK  // timing experiment only (wrong results): no walk, no tree
+  if (tid == 0) store_p3(out_p3, blockIdx.x, ge_identity());
+  return;
+#endif
   const ge_p3 acc = tg < TG ? dt_walk(dt, dg, ln, tg, n + 1, TG,
                                       [&](uint32_t t, uint32_t s[8], uint32_t& gen) {
                                         const sc v = sc_load(tsc + 8 * t);

@@ -297,7 +297,7 @@ int msm_single_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx,
   void* h = nullptr;
   BPP_TRY(ctx_pinned(ctx, (size_t)Wn * nterms * P3_BYTES, &h));
   BPP_HIP(hipMemcpyAsync(h, d_ws, (size_t)Wn * nterms * P3_BYTES, hipMemcpyDeviceToHost, ctx->stream));
-  BPP_HIP(hipStreamSynchronize(ctx->stream));
+  BPP_TRY(ctx_sync(ctx));
   *out = horner_host_terms((const uint32_t*)h, Wn, nterms, c, wb);
   return BPP_OK;
 }
@@ -708,7 +708,7 @@ int msm_multi(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, cons
   void* h = nullptr;
   BPP_TRY(ctx_pinned(ctx, (size_t)M * P3_BYTES, &h));
   BPP_HIP(hipMemcpyAsync(h, d_ws, (size_t)M * P3_BYTES, hipMemcpyDeviceToHost, ctx->stream));
-  BPP_HIP(hipStreamSynchronize(ctx->stream));
+  BPP_TRY(ctx_sync(ctx));
   for (uint32_t m = 0; m < M; ++m) out[m] = h25519::ge_from_dev((const uint32_t*)h + (size_t)m * P3_WORDS);
   return BPP_OK;
 }
@@ -758,7 +758,7 @@ int msm_multi(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, cons
     void* h = nullptr;
     BPP_TRY(ctx_pinned(ctx, (size_t)M * W * nterms * P3_BYTES, &h));
     BPP_HIP(hipMemcpyAsync(h, d_ws, (size_t)M * W * nterms * P3_BYTES, hipMemcpyDeviceToHost, ctx->stream));
-    BPP_HIP(hipStreamSynchronize(ctx->stream));
+    BPP_TRY(ctx_sync(ctx));
     for (uint32_t m = 0; m < M; ++m)
       out[m] = horner_host_terms((const uint32_t*)h + (size_t)m * W * nterms * P3_WORDS, W, nterms, c, 0);
     return BPP_OK;

@@ -854,6 +854,10 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_dt_msm(const uint32_t* __restrict
   const uint32_t m = blockIdx.x;
   const DtLane ln = DtLane::make(dg, threadIdx.x % dg.W);
   const uint32_t tg = threadIdx.x / dg.W;
+#ifdef EXP_DT_NOWALK  // timing experiment only (wrong results): no walk, no tree
+  if (threadIdx.x == 0) store_p3(out_p3, m, ge_identity());
+  return;
+#endif
   const ge_p3 acc = tg < TG ? dt_walk(dt, dg, ln, off[m] + tg, off[m + 1], TG,
                                       [&](uint32_t t, uint32_t s[8], uint32_t& gen) {
                                         load_scalar(scalars, t, s);

@@ -218,6 +218,11 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
       st.rho = d[j].rho;
       st.tr.arithmetic_domain_sep(n_p);
     }
+#ifdef EXP_HOST_BURN_US  // timing experiment only: extra host CPU per proof
+    const auto t0 = std::chrono::steady_clock::now();
+    while (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(8 * EXP_HOST_BURN_US)) {
+    }
+#endif
   });
 
   // V_0..V_2k-1 of every proof: one fixed-base launch

@@ -209,7 +209,7 @@ int bpp_points_from_uniform(bpp_ctx* ctx, const uint8_t* bytes64, size_t n, bpp_
                          P->d);
     }
     BPP_TRY(ctx_check_launch(ctx, "k_from_uniform"));
-    BPP_HIP(hipStreamSynchronize(ctx->stream));
+    BPP_TRY(ctx_sync(ctx));
   }
   *out = P;
   return BPP_OK;
@@ -227,7 +227,7 @@ int bpp_points_compress(bpp_ctx* ctx, const bpp_points* pts, uint8_t* out) {
   }
   BPP_TRY(ctx_check_launch(ctx, "k_compress_niels"));
   BPP_HIP(hipMemcpyAsync(out, d_out, pts->n * 32, hipMemcpyDeviceToHost, ctx->stream));
-  BPP_HIP(hipStreamSynchronize(ctx->stream));
+  BPP_TRY(ctx_sync(ctx));
   return BPP_OK;
 }
 

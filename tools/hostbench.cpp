@@ -29,7 +29,7 @@ int main() {
   hsc::Sc al, be, rh;
   uint64_t seed = 1;
   printf("draw_prover_randomness  %8.3f us/proof\n",
-         time_us([&] { perm::draw_prover_randomness(C, seed++, pi, gamma, al, be, rh, sL, sR, taus); }, 2000));
+         time_us([&] { perm::draw_prover_randomness(C, perm::Seed::u64(seed++), pi, gamma, al, be, rh, sL, sR, taus); }, 2000));
   uint8_t pt[32] = {0};
   printf("transcript 105 V + ch   %8.3f us/proof\n", time_us(
                                                            [&] {

@@ -40,6 +40,12 @@ def work(t):
 if os.environ.get("WITH_TORCH"):
     torch.cuda.synchronize()
 import resource  # noqa: E402
+PHASES = ["pb_rng", "pb_pedersen_V", "pb_pedersen_Vx_witness", "pb_msm_AI_AO_S", "pb_host_poly",
+          "pb_pedersen_T_lr", "pb_ipa", "ipa_host", "ipa_msm", "ped_d2h", "msm_direct", "double_encode"]
+if os.environ.get("PHASES"):  # per-phase wall time of a batch under the in-flight load
+    for pr in provers:
+        pr.ctx.profile(True)
+        pr.ctx.profile_reset()
 th = [threading.Thread(target=work, args=(t,)) for t in range(T)]
 ru0 = resource.getrusage(resource.RUSAGE_SELF)
 t0 = time.perf_counter()
@@ -52,3 +58,12 @@ ru1 = resource.getrusage(resource.RUSAGE_SELF)
 cpu = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
 print(f"B={B} T={T}: {T * reps * B / el:.0f} proofs/s ({el / (T * reps) * 1e3:.3f} ms per batch), "
       f"host CPU {cpu / el:.1f} cores busy, {cpu / (T * reps * B) * 1e6:.1f} us CPU per proof")
+if os.environ.get("PHASES"):
+    for ph in PHASES:
+        tot = 0.0
+        for pr in provers:
+            try:
+                tot += pr.ctx.profile_get(ph)[0]
+            except Exception:
+                pass
+        print(f"  {ph:24s} {tot / (T * reps):8.3f} ms per batch under load")

@@ -10,7 +10,7 @@ d, nb = sys.argv[1], int(sys.argv[2])
 ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].split("(")[0].replace("void ", "")[:26])
             for r in csv.DictReader(open(f"{d}/run_kernel_trace.csv")))
 # steady window: the middle 80 % of the prove kernels' span (skip setup/warmup tails)
-ped = [e for e in ev if e[2].startswith("k_ipa_fold")]
+ped = [e for e in ev if e[2].startswith("k_ipa_round_dt")]
 lo = ped[len(ped) // 10][0]
 hi = ped[len(ped) * 9 // 10][1]
 win = [e for e in ev if e[0] >= lo and e[1] <= hi]
@@ -25,7 +25,7 @@ for s, e, _ in win:
 busy += cur_e - cur_s
 span = hi - lo
 tot = sum(e - s for s, e, _ in win)
-folds = sum(1 for e in win if e[2].startswith("k_ipa_fold"))
+folds = sum(1 for e in win if e[2].startswith("k_ipa_round_dt"))
 batches = folds / 7.0
 per = defaultdict(float)
 for s, e, n in win:

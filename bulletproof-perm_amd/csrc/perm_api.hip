@@ -225,6 +225,17 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
 #endif
   });
 
+  // every proof's blindings gamma[0..m) on the device for tau_x's
+  // <z^Q W_V, gamma> (k_poly_coef); the stream is idle here
+  uint32_t* d_gamma = nullptr;
+  {
+    void* d = nullptr;
+    BPP_TRY(ctx_ws(ctx, "pb_gamma", (size_t)P * m * 32, &d));
+    d_gamma = (uint32_t*)d;
+    std::vector<Sc> gam((size_t)P * m);
+    for (size_t p = 0; p < P; ++p) std::copy(S[p]->gamma.begin(), S[p]->gamma.end(), gam.begin() + p * m);
+    BPP_TRY(ctx_h2d(ctx, d_gamma, gam.data(), gam.size() * 32));
+  }
   // V_0..V_2k-1 of every proof: one fixed-base launch
   hs.reset(new HostScope(ctx, "pb_pedersen_V"));
   {
@@ -343,7 +354,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
   // challenges y, z (host transcripts), then the t(X) coefficients of every
   // proof in one device launch (poly.hip); z^Q W_V stays on the host for tau_x
   hs.reset(new HostScope(ctx, "pb_host_poly"));
-  std::vector<std::vector<Sc>> zWVs(P);
+  std::vector<Sc> zwvg(P);  // <z^Q W_V, gamma> per proof (k_poly_coef)
   {
     std::vector<Sc> ys(P), ch((size_t)P * 3), tco;
     par::for_each(P, [&](size_t p) {
@@ -356,16 +367,15 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
       const Sc z = st.tr.challenge_scalar("z");
       ch[3 * p] = ys[p];
       ch[3 * p + 2] = z;
-      std::vector<Sc> zq = hsc::powers(z, C.Q + 1);
-      zq.erase(zq.begin());
-      zWVs[p] = perm::zW(C.WV, zq, m);
     });
     std::vector<Sc> yinv = ys;
     hsc::batch_invert(yinv, false);
     for (size_t p = 0; p < P; ++p) ch[3 * p + 1] = yinv[p];
-    BPP_TRY(poly_coef_dev(ctx, C, (uint32_t)P, d_s, per, ch, tco));
-    for (size_t p = 0; p < P; ++p)
-      for (int j = 0; j < 6; ++j) S[p]->t[1 + j] = tco[6 * p + j];
+    BPP_TRY(poly_coef_dev(ctx, C, (uint32_t)P, d_s, per, d_gamma, ch, tco));
+    for (size_t p = 0; p < P; ++p) {
+      for (int j = 0; j < 6; ++j) S[p]->t[1 + j] = tco[7 * p + j];
+      zwvg[p] = tco[7 * p + 6];
+    }
   }
   // T1, T3..T6 of every proof: one fixed-base launch
   hs.reset(new HostScope(ctx, "pb_pedersen_T_lr"));
@@ -403,7 +413,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
       std::vector<Sc> xp = hsc::powers(x, 7);
       const int tidx[5] = {1, 3, 4, 5, 6};
       using hsc::add;
-      Sc tau_x = hsc::mul(xp[2], hsc::inner_product(zWVs[p], st.gamma));
+      Sc tau_x = hsc::mul(xp[2], zwvg[p]);
       for (int i = 0; i < 5; ++i) tau_x = add(tau_x, hsc::mul(st.taus[i], xp[tidx[i]]));
       const Sc mu = add(add(hsc::mul(st.alpha, x), hsc::mul(st.beta, xp[2])), hsc::mul(st.rho, xp[3]));
       st.tr.append_scalar("TX", tau_x);

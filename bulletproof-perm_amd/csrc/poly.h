@@ -7,11 +7,12 @@
 
 // t_1, t_3..t_6 inputs: for P proofs, with d_sc the A_I/A_O/S scalar array
 // ([P][per], per = 3 + 5 n_p: alpha, a_L, a_R, beta, a_O, rho, s_L, s_R,
-// canonical) and ch = [P][y, y^-1, z] (canonical): t = [P][t_1..t_6].
+// canonical), d_gamma the V blindings ([P][m], canonical) and ch =
+// [P][y, y^-1, z] (canonical): t = [P][t_1..t_6, <z^Q W_V, gamma>].
 // Keeps the l(X), r(X) coefficient vectors and the H factors y^-i on the
 // device for poly_x_dev.
 int poly_coef_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint32_t* d_sc, uint32_t per,
-                  const std::vector<hsc::Sc>& ch, std::vector<hsc::Sc>& t);
+                  const uint32_t* d_gamma, const std::vector<hsc::Sc>& ch, std::vector<hsc::Sc>& t);
 
 // l = l(x), r = r(x) ([P][n_p], canonical, on the device for the IPA), the
 // H factors, and t_hat = <l, r> per proof.

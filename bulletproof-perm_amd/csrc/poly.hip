@@ -10,11 +10,14 @@
 //                zW_L, zW_R, zW_O (column-CSR of the circuit matrices), the
 //                coefficient vectors of l(X) = l1 X + l2 X^2 + l3 X^3 and
 //                r(X) = r0 + r1 X + r3 X^3, and the six t_i = inner products
-//                (workgroup reduction) -> host for the T commitments
+//                (workgroup reduction) -> host for the T commitments; also
+//                <z^Q W_V, gamma> (the V columns of the same CSR against the
+//                proof's blindings) -> host for tau_x
 //   k_poly_x     l = l(x), r = r(x) straight into the IPA's input arrays,
 //                t_hat = <l, r> -> host
 // Identical values to the host formulas they replace (perm_api.hip history;
 // oracle/bulletproofs.py prove()), hence identical proof bytes (tests).
+#include <algorithm>
 #include <cstring>
 
 #include "ctx.h"
@@ -64,13 +67,15 @@ FE_INLINE sc col_sum(const uint32_t* __restrict__ cp, const uint32_t* __restrict
   return acc;
 }
 
-// grid = P proofs, block = poly_block(n_p); dynamic LDS = Q * 32 + (POLY_T / 64) * 6 * 32
-__global__ void __launch_bounds__(POLY_T) k_poly_coef(uint32_t n_p, uint32_t Q, uint32_t per,
+// grid = P proofs, block = poly_block(max(n_p, m)); dynamic LDS = Q * 32 + (POLY_T / 64) * 7 * 32
+// t_out[p] = t_1..t_6, <z^Q W_V, gamma_p> (gamma: [P][m] canonical)
+#define POLY_NT 7
+__global__ void __launch_bounds__(POLY_T) k_poly_coef(uint32_t n_p, uint32_t m, uint32_t Q, uint32_t per,
                                                    const uint32_t* __restrict__ sc_in,
                                                    const uint32_t* __restrict__ ch,
                                                    const uint32_t* __restrict__ cp, const uint32_t* __restrict__ ce,
-                                                   uint32_t* __restrict__ vec, uint32_t* __restrict__ hf,
-                                                   uint32_t* __restrict__ t_out) {
+                                                   const uint32_t* __restrict__ gamma, uint32_t* __restrict__ vec,
+                                                   uint32_t* __restrict__ hf, uint32_t* __restrict__ t_out) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* zp = lds;           // [Q] z^(q+1)
   uint32_t* red = lds + 8 * Q;  // reduction scratch
@@ -80,8 +85,8 @@ __global__ void __launch_bounds__(POLY_T) k_poly_coef(uint32_t n_p, uint32_t Q, 
            zR = sc_to_mont(sc_load(ch + 24 * p + 16));
   for (uint32_t q = threadIdx.x; q < Q; q += blockDim.x) sc_store(zp + 8 * q, sc_pow_small(zR, q + 1, oneR));
   __syncthreads();
-  sc t[6];
-  _Pragma("unroll") for (int j = 0; j < 6; ++j) t[j] = sc_zero();
+  sc t[POLY_NT];
+  _Pragma("unroll") for (int j = 0; j < POLY_NT; ++j) t[j] = sc_zero();
   for (uint32_t i = threadIdx.x; i < n_p; i += blockDim.x) {
     const uint32_t* s = sc_in + (size_t)p * per * 8;
     const sc aL = sc_to_mont(sc_load(s + 8 * (1 + i)));
@@ -111,9 +116,14 @@ __global__ void __launch_bounds__(POLY_T) k_poly_coef(uint32_t n_p, uint32_t Q, 
     sc_store(v + 40, l3);
     sc_store(hf + ((size_t)p * n_p + i) * 8, sc_from_mont(yip));  // H factors y^-i
   }
-  sc_block_sum<6>(t, red);
+  // tau_x's <z^Q W_V, gamma>: V column j of the fourth CSR block (Montgomery)
+  // times gamma_j (canonical) is canonical z^Q W_V[j] gamma_j; to_mont keeps
+  // the sum in the Montgomery domain of the other six
+  for (uint32_t j = threadIdx.x; j < m; j += blockDim.x)
+    t[6] = sc_add(t[6], sc_mont(col_sum(cp + 3 * (n_p + 1), ce, j, zp), sc_to_mont(sc_load(gamma + 8 * ((size_t)p * m + j)))));
+  sc_block_sum<POLY_NT>(t, red);
   if (threadIdx.x == 0)
-    _Pragma("unroll") for (int j = 0; j < 6; ++j) sc_store(t_out + (6 * p + j) * 8, sc_from_mont(t[j]));
+    _Pragma("unroll") for (int j = 0; j < POLY_NT; ++j) sc_store(t_out + (POLY_NT * p + j) * 8, sc_from_mont(t[j]));
 }
 
 // grid = P, block = poly_block(n_p)
@@ -283,30 +293,30 @@ unsigned poly_block(uint32_t n_p) { return n_p < 64 ? 64u : (n_p > POLY_T ? POLY
 }  // namespace
 
 int poly_coef_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint32_t* d_sc, uint32_t per,
-                  const std::vector<hsc::Sc>& ch, std::vector<hsc::Sc>& t) {
+                  const uint32_t* d_gamma, const std::vector<hsc::Sc>& ch, std::vector<hsc::Sc>& t) {
   std::vector<uint32_t> cp, ce;
-  build_csr(C, cp, ce);
+  build_csr(C, cp, ce, true);
   void *d_cp, *d_ce, *d_ch, *d_vec, *d_hf, *d_t;
   BPP_TRY(ctx_ws(ctx, "poly_cp", cp.size() * 4, &d_cp));
   BPP_TRY(ctx_ws(ctx, "poly_ce", ce.size() * 4 + 4, &d_ce));
   BPP_TRY(ctx_ws(ctx, "poly_ch", ch.size() * 32, &d_ch));
   BPP_TRY(ctx_ws(ctx, "poly_vec", (size_t)P * C.n_p * POLY_SLOTS * 32, &d_vec));
   BPP_TRY(ctx_ws(ctx, "poly_hf", (size_t)P * C.n_p * 32, &d_hf));
-  BPP_TRY(ctx_ws(ctx, "poly_t", (size_t)P * 6 * 32, &d_t));
+  BPP_TRY(ctx_ws(ctx, "poly_t", (size_t)P * POLY_NT * 32, &d_t));
   BPP_TRY(ctx_h2d_const(ctx, "poly_cp", d_cp, cp.data(), cp.size() * 4));  // the circuit: same every batch
   BPP_TRY(ctx_h2d_const(ctx, "poly_ce", d_ce, ce.data(), ce.size() * 4));
   BPP_TRY(ctx_h2d(ctx, d_ch, ch.data(), ch.size() * 32));
-  const unsigned nt = poly_block(C.n_p);
-  const size_t lds = (size_t)C.Q * 32 + (POLY_T / 64) * 6 * 32;
+  const unsigned nt = poly_block(std::max(C.n_p, C.m));
+  const size_t lds = (size_t)C.Q * 32 + (POLY_T / 64) * POLY_NT * 32;
   {
     ProfScope ps(ctx, "poly_coef");
-    hipLaunchKernelGGL(k_poly_coef, dim3(P), dim3(nt), lds, ctx->stream, C.n_p, C.Q, per, d_sc,
-                       (const uint32_t*)d_ch, (const uint32_t*)d_cp, (const uint32_t*)d_ce, (uint32_t*)d_vec,
-                       (uint32_t*)d_hf, (uint32_t*)d_t);
+    hipLaunchKernelGGL(k_poly_coef, dim3(P), dim3(nt), lds, ctx->stream, C.n_p, C.m, C.Q, per, d_sc,
+                       (const uint32_t*)d_ch, (const uint32_t*)d_cp, (const uint32_t*)d_ce, d_gamma,
+                       (uint32_t*)d_vec, (uint32_t*)d_hf, (uint32_t*)d_t);
   }
   BPP_TRY(ctx_check_launch(ctx, "k_poly_coef"));
-  t.resize((size_t)P * 6);
-  return ctx_d2h(ctx, t.data(), d_t, (size_t)P * 6 * 32);
+  t.resize((size_t)P * POLY_NT);
+  return ctx_d2h(ctx, t.data(), d_t, (size_t)P * POLY_NT * 32);
 }
 
 int poly_x_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const std::vector<hsc::Sc>& x, uint32_t** d_l,

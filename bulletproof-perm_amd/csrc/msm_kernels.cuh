@@ -361,22 +361,29 @@ __global__ void __launch_bounds__(RED_T) k_msm_reduce_final(const uint32_t* __re
   if (threadIdx.x == 0) store_p3(wsum, seg, tot);
 }
 
-// Bucket reduction for one large MSM (B >= 512 buckets per window) whose
+// Bucket reduction for one large MSM (B >= 1024 buckets per window) whose
 // power-of-two weights are left to the host Horner, which doubles between
-// windows anyway.  With b = 512 w + 8 t + i (wave w, lane t, i < 8):
+// windows anyway.  With L = RWAVE_L buckets per lane and
+// b = 64 L w + L t + i (wave w, lane t, i < L):
 //   sum_b (b+1) S_b = sum_{w,t} acc_{w,t}            acc = sum_i (i+1) S_b
-//                   + 8 sum_w sum_{t>=1} suf_{w,t}    suf = suffix sum of the lanes' run = sum_i S_b
-//                   + 512 sum_w w R_w                 R_w = suf_{w,0}
-// k_msm_reduce_wave: one 64-lane wave per (segment, w): 16 running-sum
-//   additions per lane, a 6-step suffix scan, v = acc + 8 suf (t >= 1), a
-//   6-step butterfly; writes V_w = sum_t v and R_w.  Every lane does the
-//   same 30 point operations (the old per-lane lo * run double-and-add took
-//   ~21 of its 48).
+//                   + L sum_w sum_{t>=1} suf_{w,t}    suf = suffix sum of the lanes' run = sum_i S_b
+//                   + 64 L sum_w w R_w                R_w = suf_{w,0}
+// k_msm_reduce_wave: one 64-lane wave per (segment, w): 2L running-sum
+//   additions per lane, a 6-step suffix scan, v = acc + L suf (t >= 1), a
+//   6-step butterfly; writes V_w = sum_t v and R_w.
 // k_msm_reduce_bits: one wave per (segment, term): term 0 is X = sum_w V_w,
 //   term 1 + j is Y_j = sum_{w : bit j of w} R_w, so that
-//   sum_b (b+1) S_b = X + sum_j 2^(9+j) Y_j (horner_host_terms).
-#define RWAVE_L 8
-#define RWAVE_SHIFT 9  // log2(RWAVE_L * 64)
+//   sum_b (b+1) S_b = X + sum_j 2^(RWAVE_SHIFT+j) Y_j (horner_host_terms).
+// L = 16 (32 waves per 2^15-bucket window): 2^20 three in flight 0.888 /
+// 0.892 ms per MSM against 0.913 / 0.899 at L = 8 (whose reduce costs more
+// issue slots: 12 scan / butterfly additions per 8 buckets instead of per
+// 16); alone the reduce takes 0.233 vs 0.170 ms and L = 32 0.339 ms
+// (0.899 / 0.904 pipelined).
+#ifndef RWAVE_LOG
+#define RWAVE_LOG 4  // log2 buckets per lane
+#endif
+#define RWAVE_L (1 << RWAVE_LOG)
+#define RWAVE_SHIFT (RWAVE_LOG + 6)  // log2(RWAVE_L * 64)
 __global__ void __launch_bounds__(64) k_msm_reduce_wave(const uint32_t* __restrict__ boff, uint32_t ks,
                                                        const uint32_t* __restrict__ head,
                                                        const uint32_t* __restrict__ tail,
@@ -391,16 +398,21 @@ __global__ void __launch_bounds__(64) k_msm_reduce_wave(const uint32_t* __restri
   _Pragma("unroll") for (uint32_t k = 0; k <= RWAVE_L; ++k) bo[k] = boff[base + k];
   ge_p3 run = ge_identity();
   ge_p3 acc = ge_identity();
-  for (int i = RWAVE_L - 1; i >= 0; --i) {
-    if (bo[i] != bo[i + 1]) run = ge_add(run, bucket_total(base + i, bo[i], bo[i + 1], ks, head, tail, bsum));
-    acc = ge_add(acc, run);
-  }
+  // a lane whose buckets are all empty (most of the narrow top window's)
+  // keeps run = acc = identity without the additions
+  if (bo[0] != bo[RWAVE_L])
+    for (int i = RWAVE_L - 1; i >= 0; --i) {
+      if (bo[i] != bo[i + 1]) run = ge_add(run, bucket_total(base + i, bo[i], bo[i + 1], ks, head, tail, bsum));
+      acc = ge_add(acc, run);
+    }
   ge_p3 suf = run;  // inclusive suffix sum over lanes t..63
   _Pragma("unroll") for (int d = 1; d < 64; d <<= 1) {
     const ge_p3 s2 = ge_add(suf, ge_shfl_down(suf, d));
     if (t + d < 64) suf = s2;
   }
-  ge_p3 v = ge_add(acc, ge_dbl(ge_dbl(ge_dbl(suf))));
+  ge_p3 suf8 = suf;  // RWAVE_L * suf
+  _Pragma("unroll") for (int k = 0; k < RWAVE_LOG; ++k) suf8 = ge_dbl(suf8);
+  ge_p3 v = ge_add(acc, suf8);
   if (t == 0) v = acc;
   _Pragma("unroll") for (int k = 1; k < 64; k <<= 1) v = ge_add(v, ge_shfl_xor(v, k));
   if (t == 0) {

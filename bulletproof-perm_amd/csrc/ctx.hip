@@ -1,6 +1,19 @@
 // Context, workspace, profiling and device-memory entry points of the C ABI.
+#include <malloc.h>
+
 #include <algorithm>
 #include <cstring>
+
+// glibc's dynamic mmap threshold makes every batch's few-hundred-KB to
+// few-MB host vectors (scalar arrays, encodings, staging) alternate between
+// mmap and trimmed arena tops: mprotect, munmap and fresh-page faults showed
+// up in a host profile of 8 batches in flight.  A fixed threshold and no
+// trimming keep that memory in the arenas (the process's steady footprint
+// is a few hundred MB).
+__attribute__((constructor)) static void bpp_tune_malloc() {
+  mallopt(M_MMAP_THRESHOLD, 64 << 20);
+  mallopt(M_TRIM_THRESHOLD, 1 << 30);
+}
 
 #include "ctx.h"
 #include "host/par.h"

@@ -162,15 +162,16 @@ static void parse_randomness(const Circuit& C, const uint8_t* s, std::vector<uin
 
 size_t randomness_bytes(const Circuit& C) { return 8 * (size_t)(C.k - 1) + 64 * ((size_t)C.m + 3 + 2 * C.n_p + 5); }
 
-void draw_prover_randomness_x8(const Circuit& C, const Seed seeds[8], RandomDraws out[8]) {
+void draw_prover_randomness_x8(const Circuit& C, const Seed seeds[8], RandomDraws* const out[8]) {
   const size_t len = randomness_bytes(C);
   if (!merlin::keccak_x8_available()) {
     for (int j = 0; j < 8; ++j)
-      draw_prover_randomness(C, seeds[j], out[j].pi, out[j].gamma, out[j].alpha, out[j].beta, out[j].rho, out[j].sL,
-                             out[j].sR, out[j].taus);
+      draw_prover_randomness(C, seeds[j], out[j]->pi, out[j]->gamma, out[j]->alpha, out[j]->beta, out[j]->rho,
+                             out[j]->sL, out[j]->sR, out[j]->taus);
     return;
   }
-  std::vector<uint8_t> buf(8 * len);
+  static thread_local std::vector<uint8_t> buf;  // ~195 KB per call: reused, not re-mapped
+  buf.resize(8 * len);
   uint8_t in[8][12 + 32];
   const uint8_t* inp[8];
   uint8_t* outp[8];
@@ -182,8 +183,8 @@ void draw_prover_randomness_x8(const Circuit& C, const Seed seeds[8], RandomDraw
   }
   merlin::shake256_x8(inp, 12 + seeds[0].len, outp, len);
   for (int j = 0; j < 8; ++j)
-    parse_randomness(C, outp[j], out[j].pi, out[j].gamma, out[j].alpha, out[j].beta, out[j].rho, out[j].sL,
-                     out[j].sR, out[j].taus);
+    parse_randomness(C, outp[j], out[j]->pi, out[j]->gamma, out[j]->alpha, out[j]->beta, out[j]->rho, out[j]->sL,
+                     out[j]->sR, out[j]->taus);
 }
 
 }  // namespace perm

@@ -102,7 +102,7 @@ size_t randomness_bytes(const Circuit& C);
 // an AVX-512 8-way Keccak (host/keccak_x8.cpp; scalar fallback without
 // AVX-512), byte-identical to draw_prover_randomness.
 // (the eight seeds must have the same length)
-void draw_prover_randomness_x8(const Circuit& C, const Seed seeds[8], RandomDraws out[8]);
+void draw_prover_randomness_x8(const Circuit& C, const Seed seeds[8], RandomDraws* const out[8]);
 
 size_t proof_len(uint32_t k);
 

@@ -337,7 +337,11 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
     return BPP_ERR_LEN;
   }
   if (qmul.size() != P) return BPP_ERR_ARG;
-  out.assign(P, IpaProofHost());
+  out.resize(P);  // (callers may pass vectors back for reuse: keep their capacity)
+  for (auto& o : out) {
+    o.L.clear();
+    o.R.clear();
+  }
   if (!P) return BPP_OK;
   uint32_t lg_n = 0;
   while ((1u << lg_n) < n) ++lg_n;

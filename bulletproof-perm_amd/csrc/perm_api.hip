@@ -174,14 +174,17 @@ int msm_terms(bpp_ctx* ctx, const std::vector<Sc>& sc, const std::vector<uint32_
   return msm_multi(ctx, d_s, (const uint32_t*)d_i, off, pts, res);
 }
 
-// Per-proof prover state carried between the lockstep phases.
+// Per-proof prover state carried between the lockstep phases.  The states
+// (and their vectors) persist per driver thread across batches: a host
+// profile of 8 batches in flight spent ~20 % of the host CPU in malloc /
+// free and arena locks, largely vectors allocated by pool workers and freed
+// by the driver thread at the end of every batch.
 struct ProverState {
   merlin::Transcript tr;
-  std::vector<uint32_t> pi;
-  std::vector<Sc> gamma, sL, sR, taus, vals, aL, aR, aO;
-  Sc alpha, beta, rho, x_perm, w;
+  perm::RandomDraws d;  // pi, gamma, alpha, beta, rho, s_L, s_R, tau
+  std::vector<Sc> vals, aL, aR, aO;
+  Sc x_perm, w;
   Sc t[7];
-  explicit ProverState(const uint8_t* label, size_t llen) : tr(label, llen) {}
 };
 
 // Proves `seeds.size()` permutation proofs in lockstep: every GPU step
@@ -193,31 +196,28 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
                 const uint8_t* label, size_t llen, std::vector<Proof>& Ps) {
   const uint32_t k = C.k, n_p = C.n_p, m = C.m;
   const size_t P = seeds.size();
-  Ps.assign(P, Proof());
+  Ps.resize(P);
   if (!P) return BPP_OK;
-  std::vector<std::unique_ptr<ProverState>> S(P);
-  for (size_t p = 0; p < P; ++p) S[p].reset(new ProverState(label, llen));
+  // (a plain reference: pool workers must reach THIS thread's states, a
+  // thread_local named inside their lambdas would be their own)
+  static thread_local std::vector<std::unique_ptr<ProverState>> S_tl;
+  std::vector<std::unique_ptr<ProverState>>& S = S_tl;
+  while (S.size() < P) S.emplace_back(new ProverState());
+  par::for_each(P, [&](size_t p) { S[p]->tr = merlin::Transcript(label, llen); });
 
   // RNG draws (order fixed: pi, gamma, alpha beta rho, s_L, s_R, tau x5)
   // (eight proofs' SHAKE256 streams per AVX-512 Keccak, perm::draw_prover_randomness_x8)
   std::unique_ptr<HostScope> hs(new HostScope(ctx, "pb_rng"));
   par::for_each((P + 7) / 8, [&](size_t gi) {
     perm::Seed sd[8];
-    perm::RandomDraws d[8];
-    for (size_t j = 0; j < 8; ++j) sd[j] = seeds[std::min(8 * gi + j, P - 1)];
-    perm::draw_prover_randomness_x8(C, sd, d);
-    for (size_t j = 0; j < 8 && 8 * gi + j < P; ++j) {
-      ProverState& st = *S[8 * gi + j];
-      st.pi = std::move(d[j].pi);
-      st.gamma = std::move(d[j].gamma);
-      st.sL = std::move(d[j].sL);
-      st.sR = std::move(d[j].sR);
-      st.taus = std::move(d[j].taus);
-      st.alpha = d[j].alpha;
-      st.beta = d[j].beta;
-      st.rho = d[j].rho;
-      st.tr.arithmetic_domain_sep(n_p);
+    perm::RandomDraws* d[8];
+    perm::RandomDraws spare;  // a short last group's padding lanes
+    for (size_t j = 0; j < 8; ++j) {
+      sd[j] = seeds[std::min(8 * gi + j, P - 1)];
+      d[j] = 8 * gi + j < P ? &S[8 * gi + j]->d : &spare;
     }
+    perm::draw_prover_randomness_x8(C, sd, d);
+    for (size_t j = 0; j < 8 && 8 * gi + j < P; ++j) S[8 * gi + j]->tr.arithmetic_domain_sep(n_p);
 #ifdef EXP_HOST_BURN_US  // timing experiment only: extra host CPU per proof
     const auto t0 = std::chrono::steady_clock::now();
     while (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(8 * EXP_HOST_BURN_US)) {
@@ -233,7 +233,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     BPP_TRY(ctx_ws(ctx, "pb_gamma", (size_t)P * m * 32, &d));
     d_gamma = (uint32_t*)d;
     std::vector<Sc> gam((size_t)P * m);
-    for (size_t p = 0; p < P; ++p) std::copy(S[p]->gamma.begin(), S[p]->gamma.end(), gam.begin() + p * m);
+    for (size_t p = 0; p < P; ++p) std::copy(S[p]->d.gamma.begin(), S[p]->d.gamma.end(), gam.begin() + p * m);
     BPP_TRY(ctx_h2d(ctx, d_gamma, gam.data(), gam.size() * 32));
   }
   // V_0..V_2k-1 of every proof: one fixed-base launch
@@ -243,9 +243,9 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     par::for_each(P, [&](size_t p) {
       for (uint32_t i = 0; i < k; ++i) {
         v[p * 2 * k + i] = hsc::from_u64(i + 1);
-        v[p * 2 * k + k + i] = hsc::from_u64(S[p]->pi[i] + 1);
+        v[p * 2 * k + k + i] = hsc::from_u64(S[p]->d.pi[i] + 1);
       }
-      for (uint32_t i = 0; i < 2 * k; ++i) g[p * 2 * k + i] = S[p]->gamma[i];
+      for (uint32_t i = 0; i < 2 * k; ++i) g[p * 2 * k + i] = S[p]->d.gamma[i];
     });
     std::vector<Enc32> V;
     BPP_TRY(pedersen_host(ctx, G, v, g, V));
@@ -294,14 +294,14 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     std::vector<Sc> v(P), g(P);
     for (size_t p = 0; p < P; ++p) {
       v[p] = S[p]->x_perm;
-      g[p] = S[p]->gamma[2 * k];
+      g[p] = S[p]->d.gamma[2 * k];
     }
     std::vector<Enc32> Vx;
     BPP_TRY(pedersen_host(ctx, G, v, g, Vx));
     par::for_each(P, [&](size_t p) {
       Ps[p].V.push_back(Vx[p]);
       S[p]->tr.append_point("V", Vx[p].data());
-      perm::witness(C, S[p]->pi, S[p]->x_perm, S[p]->vals, S[p]->aL, S[p]->aR, S[p]->aO);
+      perm::witness(C, S[p]->d.pi, S[p]->x_perm, S[p]->vals, S[p]->aL, S[p]->aR, S[p]->aO);
     });
   }
   MsmPoints pts;
@@ -320,14 +320,14 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
         sc[t] = s;
         idx[t++] = i;
       };
-      add(st.alpha, G->bbidx());
+      add(st.d.alpha, G->bbidx());
       for (uint32_t i = 0; i < n_p; ++i) add(st.aL[i], G->gidx(i));
       for (uint32_t i = 0; i < n_p; ++i) add(st.aR[i], G->hidx(i));
-      add(st.beta, G->bbidx());
+      add(st.d.beta, G->bbidx());
       for (uint32_t i = 0; i < n_p; ++i) add(st.aO[i], G->gidx(i));
-      add(st.rho, G->bbidx());
-      for (uint32_t i = 0; i < n_p; ++i) add(st.sL[i], G->gidx(i));
-      for (uint32_t i = 0; i < n_p; ++i) add(st.sR[i], G->hidx(i));
+      add(st.d.rho, G->bbidx());
+      for (uint32_t i = 0; i < n_p; ++i) add(st.d.sL[i], G->gidx(i));
+      for (uint32_t i = 0; i < n_p; ++i) add(st.d.sR[i], G->hidx(i));
     });
     for (size_t p = 0; p < P; ++p) {
       off[3 * p] = (uint32_t)(p * per);
@@ -386,7 +386,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     for (size_t p = 0; p < P; ++p)
       for (int i = 0; i < 5; ++i) {
         v[5 * p + i] = S[p]->t[ti[i]];
-        g[5 * p + i] = S[p]->taus[i];
+        g[5 * p + i] = S[p]->d.taus[i];
       }
     std::vector<Enc32> T;
     {
@@ -410,12 +410,14 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
       ProverState& st = *S[p];
       Proof& Pf = Ps[p];
       const Sc x = xs[p];
-      std::vector<Sc> xp = hsc::powers(x, 7);
+      Sc xp[7];
+      xp[0] = hsc::one();
+      for (int i = 1; i < 7; ++i) xp[i] = hsc::mul(xp[i - 1], x);
       const int tidx[5] = {1, 3, 4, 5, 6};
       using hsc::add;
       Sc tau_x = hsc::mul(xp[2], zwvg[p]);
-      for (int i = 0; i < 5; ++i) tau_x = add(tau_x, hsc::mul(st.taus[i], xp[tidx[i]]));
-      const Sc mu = add(add(hsc::mul(st.alpha, x), hsc::mul(st.beta, xp[2])), hsc::mul(st.rho, xp[3]));
+      for (int i = 0; i < 5; ++i) tau_x = add(tau_x, hsc::mul(st.d.taus[i], xp[tidx[i]]));
+      const Sc mu = add(add(hsc::mul(st.d.alpha, x), hsc::mul(st.d.beta, xp[2])), hsc::mul(st.d.rho, xp[3]));
       st.tr.append_scalar("TX", tau_x);
       st.tr.append_scalar("mu", mu);
       st.tr.append_scalar("t", t_hat[p]);
@@ -439,11 +441,12 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     ig.gbase = 0;
     ig.hbase = (uint32_t)G->n;
     ig.qidx = G->bidx();
-    std::vector<IpaProofHost> ipas;
+    static thread_local std::vector<IpaProofHost> ipas_tl;
+    std::vector<IpaProofHost>& ipas = ipas_tl;
     BPP_TRY(ipa_prove_batch_dev(ctx, trs, ig, n_p, nullptr, d_hf, d_l, d_r, qmul, ipas));
-    for (size_t p = 0; p < P; ++p) Ps[p].ipa = std::move(ipas[p]);
+    for (size_t p = 0; p < P; ++p) std::swap(Ps[p].ipa, ipas[p]);  // (both keep their capacity)
   }
-  for (size_t p = 0; p < P; ++p) Ps[p].pi = S[p]->pi;
+  for (size_t p = 0; p < P; ++p) Ps[p].pi.assign(S[p]->d.pi.begin(), S[p]->d.pi.end());
   return BPP_OK;
 }
 
@@ -826,7 +829,9 @@ static int prove_batch_api(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, const st
   }
   BPP_HIP(hipSetDevice(ctx->device));
   const size_t pl = perm::proof_len(k);
-  std::vector<Proof> Ps(count);
+  static thread_local std::vector<Proof> Ps_tl;  // reused batch after batch (ProverState note)
+  std::vector<Proof>& Ps = Ps_tl;                // (the workers below must see this thread's)
+  Ps.resize(count);
   // Sub-batches in flight on S streams (child contexts), one host thread
   // each: while one sub-batch waits on transcripts / challenges on the host,
   // the others' MSM and Pedersen kernels fill the GPU (a lockstep batch of

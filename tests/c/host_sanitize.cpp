@@ -100,7 +100,9 @@ static int test_draws() {
       sd[j] = kind ? perm::Seed::bytes32(b) : perm::Seed::u64(1000 + j);
     }
     perm::RandomDraws d[8];
-    perm::draw_prover_randomness_x8(C, sd, d);
+    perm::RandomDraws* dp[8];
+    for (int j = 0; j < 8; ++j) dp[j] = &d[j];
+    perm::draw_prover_randomness_x8(C, sd, dp);
     for (int j = 0; j < 8; ++j) {
       std::vector<uint32_t> pi;
       std::vector<hsc::Sc> gamma, sL, sR, taus;

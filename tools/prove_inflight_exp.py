@@ -46,6 +46,13 @@ if os.environ.get("PHASES"):  # per-phase wall time of a batch under the in-flig
     for pr in provers:
         pr.ctx.profile(True)
         pr.ctx.profile_reset()
+hp = None
+if os.environ.get("HOSTPROF"):  # CPU sampling of the timed region (tools/hostprof)
+    import ctypes
+    hp = ctypes.CDLL(str(ROOT / "tools" / "hostprof" / "libhostprof.so"))
+    hp.hp_stop.argtypes = [ctypes.c_char_p]
+    hp.hp_stop.restype = ctypes.c_long
+    hp.hp_start(2000)
 th = [threading.Thread(target=work, args=(t,)) for t in range(T)]
 ru0 = resource.getrusage(resource.RUSAGE_SELF)
 t0 = time.perf_counter()
@@ -54,6 +61,8 @@ for x in th:
 for x in th:
     x.join()
 el = time.perf_counter() - t0
+if hp is not None:
+    print("hostprof samples:", hp.hp_stop(os.environ["HOSTPROF"].encode()))
 ru1 = resource.getrusage(resource.RUSAGE_SELF)
 cpu = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
 print(f"B={B} T={T}: {T * reps * B / el:.0f} proofs/s ({el / (T * reps) * 1e3:.3f} ms per batch), "

@@ -24,6 +24,7 @@ struct bpp_ctx {
   // pinned upload arena: bump-allocated, recycled after a stream sync
   uint8_t* stage = nullptr;
   size_t stage_cap = 0, stage_used = 0;
+  hipEvent_t sync_ev = nullptr;  // ctx_sync's completion event
   // profiling
   bool prof = false;
   struct Pend {
@@ -101,10 +102,8 @@ int ctx_h2d(bpp_ctx* ctx, void* d, const void* h, size_t bytes);
 int ctx_h2d_const(bpp_ctx* ctx, const char* name, void* d, const void* h, size_t bytes);
 // Device->host copy through the arena; synchronous (stream synchronised).
 int ctx_d2h(bpp_ctx* ctx, void* h, const void* d, size_t bytes);
-// hipStreamSynchronize + recycle the upload arena.  (Polling an event with
-// short sleeps, or a blocking-sync event, to free the waiting core for the
-// host pool measured within the box's +-15 % noise at 8 batches in flight:
-// tools/gpu_syncwait.sh)
+// Wait for ctx's stream (event poll with short sleeps, see ctx.hip) +
+// recycle the upload arena.
 int ctx_sync(bpp_ctx* ctx);
 // i-th child context of ctx (created on first use, destroyed with ctx).
 int ctx_child(bpp_ctx* ctx, size_t i, bpp_ctx** out);

@@ -1,5 +1,6 @@
 // Context, workspace, profiling and device-memory entry points of the C ABI.
 #include <malloc.h>
+#include <time.h>
 
 #include <algorithm>
 #include <cstring>
@@ -60,8 +61,21 @@ int ctx_pinned(bpp_ctx* ctx, size_t bytes, void** out) {
   return BPP_OK;
 }
 
+// The waiting thread polls an event with 5 us sleeps instead of
+// hipStreamSynchronize's spin: with 8-12 proof batches in flight, their
+// driver threads spinning in the HSA signal wait were ~25 % of the host CPU
+// samples (tools/hostprof).  12 batches in flight: 104-108.5 K vs 99.5-100.6
+// K proofs/s with 8 and the spin, 11.9 vs 14.3 host cores busy
+// (tools/ab_sync.sh; 2 / 10 us sleeps measured the same; a
+// hipEventBlockingSync event kept the spin's CPU and throughput).
 int ctx_sync(bpp_ctx* ctx) {
-  BPP_HIP(hipStreamSynchronize(ctx->stream));
+  if (!ctx->sync_ev) BPP_HIP(hipEventCreateWithFlags(&ctx->sync_ev, hipEventDisableTiming));
+  BPP_HIP(hipEventRecord(ctx->sync_ev, ctx->stream));
+  for (hipError_t r; (r = hipEventQuery(ctx->sync_ev)) != hipSuccess;) {
+    if (r != hipErrorNotReady) BPP_HIP(r);
+    struct timespec ts = {0, 5000L};
+    nanosleep(&ts, nullptr);
+  }
   ctx->stage_used = 0;
   return BPP_OK;
 }
@@ -216,6 +230,7 @@ void bpp_ctx_destroy(bpp_ctx* ctx) {
     hipEventDestroy(p.b);
   }
   for (auto e : ctx->ev_pool) hipEventDestroy(e);
+  if (ctx->sync_ev) hipEventDestroy(ctx->sync_ev);
   for (auto& sl : ctx->msm_slot)
     if (sl.done) hipEventDestroy(sl.done);
   hipStreamDestroy(ctx->stream);

@@ -67,6 +67,22 @@ FE_INLINE sc col_sum(const uint32_t* __restrict__ cp, const uint32_t* __restrict
   return acc;
 }
 
+// Column sum split over the whole workgroup (every lane must call it): for
+// the few columns with many entries -- W_V's x column holds one entry per
+// a_L / a_R row using x (2k + 1 of them), which as one lane's serial chain
+// doubled k_poly_coef (126 -> 292 us) and dominated k_verify_scalars.
+// Valid in lane 0; `red` is the workgroup-sum scratch.
+#define HEAVY_COL 8
+FE_INLINE sc col_sum_block(const uint32_t* __restrict__ cp, const uint32_t* __restrict__ ce, uint32_t col,
+                           const uint32_t* zp, uint32_t* red) {
+  sc v[1] = {sc_zero()};
+  for (uint32_t e = cp[col] + threadIdx.x; e < cp[col + 1]; e += blockDim.x)
+    v[0] = sc_add(v[0], sc_mont(sc_load(zp + 8 * ce[9 * e]), sc_load(ce + 9 * e + 1)));
+  sc_block_sum<1>(v, red);
+  __syncthreads();  // red is reused by the next call
+  return v[0];
+}
+
 // grid = P proofs, block = poly_block(max(n_p, m)); dynamic LDS = Q * 32 + (POLY_T / 64) * 7 * 32
 // t_out[p] = t_1..t_6, <z^Q W_V, gamma_p> (gamma: [P][m] canonical)
 #define POLY_NT 7
@@ -119,8 +135,15 @@ __global__ void __launch_bounds__(POLY_T) k_poly_coef(uint32_t n_p, uint32_t m, 
   // tau_x's <z^Q W_V, gamma>: V column j of the fourth CSR block (Montgomery)
   // times gamma_j (canonical) is canonical z^Q W_V[j] gamma_j; to_mont keeps
   // the sum in the Montgomery domain of the other six
+  const uint32_t* cpv = cp + 3 * (n_p + 1);
+  const uint32_t* gam = gamma + 8 * (size_t)p * m;
   for (uint32_t j = threadIdx.x; j < m; j += blockDim.x)
-    t[6] = sc_add(t[6], sc_mont(col_sum(cp + 3 * (n_p + 1), ce, j, zp), sc_to_mont(sc_load(gamma + 8 * ((size_t)p * m + j)))));
+    if (cpv[j + 1] - cpv[j] <= HEAVY_COL) t[6] = sc_add(t[6], sc_mont(col_sum(cpv, ce, j, zp), sc_to_mont(sc_load(gam + 8 * j))));
+  for (uint32_t j = 0; j < m; ++j)  // (uniform: every lane reads the same offsets)
+    if (cpv[j + 1] - cpv[j] > HEAVY_COL) {
+      const sc cs = col_sum_block(cpv, ce, j, zp, red);
+      if (threadIdx.x == 0) t[6] = sc_add(t[6], sc_mont(cs, sc_to_mont(sc_load(gam + 8 * j))));
+    }
   sc_block_sum<POLY_NT>(t, red);
   if (threadIdx.x == 0)
     _Pragma("unroll") for (int j = 0; j < POLY_NT; ++j) sc_store(t_out + (POLY_NT * p + j) * 8, sc_from_mont(t[j]));
@@ -218,9 +241,17 @@ __global__ void __launch_bounds__(POLY_T) k_verify_scalars(
   const sc x2R = sc_mont(xR, xR);
   const sc wrx2R = sc_mont(sc_mont(wtR, rR), x2R);
   const size_t pb = NG + (size_t)p * npt;
-  // V_j: -wt r x^2 zWV_j (zWV from the fourth column-CSR, m columns)
+  // V_j: -wt r x^2 zWV_j (zWV from the fourth column-CSR, m columns; the
+  // heavy x column summed by the whole workgroup)
+  const uint32_t* cpv = cp + 3 * (n_p + 1);
   for (uint32_t j = threadIdx.x; j < m; j += blockDim.x)
-    sc_store(sc_out + 8 * (pb + j), sc_from_mont(sc_neg(sc_mont(col_sum(cp + 3 * (n_p + 1), ce, j, zp), wrx2R))));
+    if (cpv[j + 1] - cpv[j] <= HEAVY_COL)
+      sc_store(sc_out + 8 * (pb + j), sc_from_mont(sc_neg(sc_mont(col_sum(cpv, ce, j, zp), wrx2R))));
+  for (uint32_t j = 0; j < m; ++j)
+    if (cpv[j + 1] - cpv[j] > HEAVY_COL) {
+      const sc cs = col_sum_block(cpv, ce, j, zp, red);
+      if (threadIdx.x == 0) sc_store(sc_out + 8 * (pb + j), sc_from_mont(sc_neg(sc_mont(cs, wrx2R))));
+    }
   // A_I, A_O, S: -wt x^(1,2,3); T_k: -wt r x^k (k = 1, 3..6); L_j: -wt u_j^2; R_j: -wt u_j^-2
   for (uint32_t j = threadIdx.x; j < 8 + 2 * lg; j += blockDim.x) {
     sc v;

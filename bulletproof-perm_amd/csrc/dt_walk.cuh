@@ -103,17 +103,48 @@ FE_INLINE ge_p3 dt_walk(const uint32_t* __restrict__ dt, const DtGeom& dg, const
   return acc;
 }
 
+// Extended points in LDS as 10 planes of 16-byte chunks (chunk i of slot j
+// at plane i, position j): consecutive lanes touch consecutive 16 B, where
+// the 160-B-per-point layout of store_p3 put 4 lanes on the same banks (PMC:
+// ~2.7 LDS bank conflicts per LDS instruction in the trees).
+FE_INLINE void lds_store_p3(uint32_t* tl, uint32_t nslots, uint32_t j, const ge_p3& r) {
+  uint32_t w[40];
+  _Pragma("unroll") for (int i = 0; i < FE_LIMBS; ++i) {
+    w[i] = r.X.v[i];
+    w[10 + i] = r.Y.v[i];
+    w[20 + i] = r.Z.v[i];
+    w[30 + i] = r.T.v[i];
+  }
+  uint4* p = reinterpret_cast<uint4*>(tl);
+  const uint4* q = reinterpret_cast<const uint4*>(w);
+  _Pragma("unroll") for (int i = 0; i < 10; ++i) p[(size_t)i * nslots + j] = q[i];
+}
+FE_INLINE ge_p3 lds_load_p3(const uint32_t* tl, uint32_t nslots, uint32_t j) {
+  const uint4* p = reinterpret_cast<const uint4*>(tl);
+  uint4 q[10];
+  _Pragma("unroll") for (int i = 0; i < 10; ++i) q[i] = p[(size_t)i * nslots + j];
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(q);
+  ge_p3 r;
+  _Pragma("unroll") for (int i = 0; i < FE_LIMBS; ++i) {
+    r.X.v[i] = w[i];
+    r.Y.v[i] = w[10 + i];
+    r.Z.v[i] = w[20 + i];
+    r.T.v[i] = w[30 + i];
+  }
+  return r;
+}
+
 // Block tree in LDS (tl: blockDim.x extended points) whose waves retire as it
 // narrows; lane 0 writes the block's sum to out_p3[m].
 FE_INLINE void dt_block_tree(uint32_t* tl, const ge_p3& acc, uint32_t nt, uint32_t* __restrict__ out_p3, uint32_t m) {
-  store_p3(tl, threadIdx.x, acc);
+  lds_store_p3(tl, nt, threadIdx.x, acc);
   __syncthreads();
   uint32_t p2 = 1;
   while (p2 < nt) p2 <<= 1;
   for (uint32_t s = p2 >> 1; s > 0; s >>= 1) {
     if (threadIdx.x < s && threadIdx.x + s < nt)
-      store_p3(tl, threadIdx.x, ge_add(load_p3(tl, threadIdx.x), load_p3(tl, threadIdx.x + s)));
+      lds_store_p3(tl, nt, threadIdx.x, ge_add(lds_load_p3(tl, nt, threadIdx.x), lds_load_p3(tl, nt, threadIdx.x + s)));
     __syncthreads();
   }
-  if (threadIdx.x == 0) store_p3(out_p3, m, load_p3(tl, 0));
+  if (threadIdx.x == 0) store_p3(out_p3, m, lds_load_p3(tl, nt, 0));
 }

@@ -35,3 +35,17 @@ def test_host_asan_ubsan(tmp_path):
 @pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not installed")
 def test_host_tsan(tmp_path):
     _build_run(tmp_path, "host_tsan", ["-fsanitize=thread"], {"TSAN_OPTIONS": "halt_on_error=1"})
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not installed")
+def test_from_wide_fast_path_matches_montgomery_form(tmp_path):
+    """hsc::from_wide (the 2^252 = -delta folding used for every wide draw and
+    challenge) equals the Montgomery-form reduction on 2 M inputs, under
+    UBSan (signed shifts / carries)."""
+    exe = tmp_path / "from_wide"
+    cmd = ["g++", "-std=c++17", "-O2", "-g", "-march=x86-64-v3", "-fsanitize=undefined", "-fno-sanitize-recover=all",
+           "-I", str(CSRC), str(ROOT / "tests" / "c" / "from_wide_check.cpp"), "-o", str(exe)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "mismatches: 0" in r.stdout, (r.stdout + r.stderr)[-2000:]

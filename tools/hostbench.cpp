@@ -30,6 +30,22 @@ int main() {
   uint64_t seed = 1;
   printf("draw_prover_randomness  %8.3f us/proof\n",
          time_us([&] { perm::draw_prover_randomness(C, perm::Seed::u64(seed++), pi, gamma, al, be, rh, sL, sR, taus); }, 2000));
+  {
+    perm::Seed sd[8];
+    perm::RandomDraws d[8];
+    perm::RandomDraws* dp[8];
+    for (int j = 0; j < 8; ++j) dp[j] = &d[j];
+    printf("draw_prover_randomness_x8 %6.3f us/proof\n", time_us([&] {
+             for (int j = 0; j < 8; ++j) sd[j] = perm::Seed::u64(seed++);
+             perm::draw_prover_randomness_x8(C, sd, dp);
+           }, 500) / 8);
+    uint8_t wide[64];
+    for (int i = 0; i < 64; ++i) wide[i] = (uint8_t)(i * 37 + 1);
+    volatile uint64_t sink = 0;
+    printf("from_wide               %8.3f ns\n", time_us([&] {
+             for (int r = 0; r < 1000; ++r) { wide[0] = (uint8_t)r; sink += hsc::from_wide(wide).v[0]; }
+           }, 200));
+  }
   uint8_t pt[32] = {0};
   printf("transcript 105 V + ch   %8.3f us/proof\n", time_us(
                                                            [&] {

@@ -67,7 +67,11 @@ int ctx_pinned(bpp_ctx* ctx, size_t bytes, void** out) {
 // samples (tools/hostprof).  12 batches in flight: 104-108.5 K vs 99.5-100.6
 // K proofs/s with 8 and the spin, 11.9 vs 14.3 host cores busy
 // (tools/ab_sync.sh; 2 / 10 us sleeps measured the same; a
-// hipEventBlockingSync event kept the spin's CPU and throughput).
+// hipEventBlockingSync event kept the spin's CPU and throughput).  A 5 us
+// nanosleep sleeps ~55 us under the default 50 us timer slack (65 vs 16 us
+// per launch + copy + wait round trip, tools/ubench/hipapi), but a 1 us slack,
+// with or without a 15 us spin first, measured within noise (105-117 K vs
+// 101-120 K proofs/s at 12 in flight).
 int ctx_sync(bpp_ctx* ctx) {
   if (!ctx->sync_ev) BPP_HIP(hipEventCreateWithFlags(&ctx->sync_ev, hipEventDisableTiming));
   BPP_HIP(hipEventRecord(ctx->sync_ev, ctx->stream));

@@ -12,6 +12,9 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
+#include <vector>
+
 #include "scalar.h"
 
 namespace merlin {
@@ -324,5 +327,35 @@ struct TranscriptX8 {
     for (int j = 0; j < 8; ++j) out[j] = hsc::from_wide(buf[j]);
   }
 };
+
+// Runs transcript operations on P transcripts that are in lockstep, eight at
+// a time on the 8-way Keccak: fx8(X, idx, real) performs the group's ops on X
+// (instance j is transcript idx[j]; lanes j >= real pad a short last group
+// with copies of its last transcript, whose results the caller drops);
+// f1(p) performs the same ops on transcript p alone when a group is not in
+// lockstep.  `for_groups` runs the groups (the host pool's for_each).
+template <class ForGroups, class FX8, class F1>
+void lockstep_x8(const std::vector<Transcript*>& trs, ForGroups&& for_groups, FX8&& fx8, F1&& f1) {
+  const size_t P = trs.size();
+  for_groups((P + 7) / 8, [&](size_t gi) {
+    Transcript pad;  // (a short last group's padding lanes share one copy)
+    Transcript* t[8];
+    size_t idx[8];
+    const size_t real = std::min<size_t>(8, P - 8 * gi);
+    for (size_t j = 0; j < 8; ++j) idx[j] = 8 * gi + std::min(j, real - 1);
+    if (real < 8) pad = *trs[idx[real - 1]];
+    for (size_t j = 0; j < 8; ++j) t[j] = j < real ? trs[idx[j]] : &pad;
+    TranscriptX8 X;
+    if (!X.load(t)) {
+      for (size_t j = 0; j < real; ++j) f1(idx[j]);
+      return;
+    }
+    fx8(X, idx, real);
+    // padding lanes share `pad`: store only the real ones (pad's state is dropped)
+    Transcript* tr[8];
+    for (size_t j = 0; j < 8; ++j) tr[j] = j < real ? t[j] : &pad;
+    X.store(tr);
+  });
+}
 
 }  // namespace merlin

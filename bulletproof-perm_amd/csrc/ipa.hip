@@ -16,6 +16,7 @@
 // challenge on the host, and the scalar fold (k_ipa_fold).  L, R, a, b are
 // identical group elements / scalars to the folding form (same transcript).
 #include <cstdlib>
+#include <functional>
 #include <cstring>
 
 #include "ctx.h"
@@ -474,16 +475,34 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
     }
     if (!dev_merlin) {
     HostScope hs(ctx, "ipa_host");
-    par::for_each(P, [&](size_t p) {
+    // L, R appends and the u challenge of eight proofs at a time on the
+    // 8-way Keccak (their transcripts are in lockstep)
+    merlin::lockstep_x8(
+        trs, [](size_t n, const std::function<void(size_t)>& f) { par::for_each(n, f); },
+        [&](merlin::TranscriptX8& X, const size_t* idx, size_t real) {
+          const uint8_t *lm[8], *rm[8];
+          for (int j = 0; j < 8; ++j) {
+            lm[j] = enc.data() + 64 * idx[j];
+            rm[j] = lm[j] + 32;
+          }
+          X.append("L", lm, 32);
+          X.append("R", rm, 32);
+          hsc::Sc u8[8];
+          X.challenge_scalar("u", u8);
+          for (size_t j = 0; j < real; ++j) u[idx[j]] = u8[j];
+        },
+        [&](size_t p) {
+          trs[p]->append_point("L", enc.data() + 64 * p);
+          trs[p]->append_point("R", enc.data() + 64 * p + 32);
+          u[p] = trs[p]->challenge_scalar("u");
+        });
+    for (uint32_t p = 0; p < P; ++p) {
       Enc32 Le, Re;
       memcpy(Le.data(), enc.data() + 64 * p, 32);
       memcpy(Re.data(), enc.data() + 64 * p + 32, 32);
       out[p].L.push_back(Le);
       out[p].R.push_back(Re);
-      trs[p]->append_point("L", Le.data());
-      trs[p]->append_point("R", Re.data());
-      u[p] = trs[p]->challenge_scalar("u");
-    });
+    }
     ui = u;
     hsc::batch_invert(ui, false);
     for (uint32_t p = 0; p < P; ++p) {  // device Montgomery forms u R, u^-1 R

@@ -20,6 +20,7 @@
 #include <cstring>
 #include <cstdlib>
 #include <sys/random.h>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -204,6 +205,9 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
   std::vector<std::unique_ptr<ProverState>>& S = S_tl;
   while (S.size() < P) S.emplace_back(new ProverState());
   par::for_each(P, [&](size_t p) { S[p]->tr = merlin::Transcript(label, llen); });
+  std::vector<merlin::Transcript*> trs(P);  // this batch's transcripts (lockstep_x8)
+  for (size_t p = 0; p < P; ++p) trs[p] = &S[p]->tr;
+  const auto for_groups = [](size_t n, const std::function<void(size_t)>& f) { par::for_each(n, f); };
 
   // RNG draws (order fixed: pi, gamma, alpha beta rho, s_L, s_R, tau x5)
   // (eight proofs' SHAKE256 streams per AVX-512 Keccak, perm::draw_prover_randomness_x8)
@@ -357,17 +361,35 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
   std::vector<Sc> zwvg(P);  // <z^Q W_V, gamma> per proof (k_poly_coef)
   {
     std::vector<Sc> ys(P), ch((size_t)P * 3), tco;
-    par::for_each(P, [&](size_t p) {
-      ProverState& st = *S[p];
-      Proof& Pf = Ps[p];
-      st.tr.append_point("A_I", Pf.AI.data());
-      st.tr.append_point("A_O", Pf.AO.data());
-      st.tr.append_point("S", Pf.S.data());
-      ys[p] = st.tr.challenge_scalar("y");
-      const Sc z = st.tr.challenge_scalar("z");
-      ch[3 * p] = ys[p];
-      ch[3 * p + 2] = z;
-    });
+    merlin::lockstep_x8(
+        trs, for_groups,
+        [&](merlin::TranscriptX8& X, const size_t* idx, size_t real) {
+          const uint8_t* m[8];
+          for (int j = 0; j < 8; ++j) m[j] = Ps[idx[j]].AI.data();
+          X.append("A_I", m, 32);
+          for (int j = 0; j < 8; ++j) m[j] = Ps[idx[j]].AO.data();
+          X.append("A_O", m, 32);
+          for (int j = 0; j < 8; ++j) m[j] = Ps[idx[j]].S.data();
+          X.append("S", m, 32);
+          Sc y8[8], z8[8];
+          X.challenge_scalar("y", y8);
+          X.challenge_scalar("z", z8);
+          for (size_t j = 0; j < real; ++j) {
+            ys[idx[j]] = y8[j];
+            ch[3 * idx[j]] = y8[j];
+            ch[3 * idx[j] + 2] = z8[j];
+          }
+        },
+        [&](size_t p) {
+          ProverState& st = *S[p];
+          Proof& Pf = Ps[p];
+          st.tr.append_point("A_I", Pf.AI.data());
+          st.tr.append_point("A_O", Pf.AO.data());
+          st.tr.append_point("S", Pf.S.data());
+          ys[p] = st.tr.challenge_scalar("y");
+          ch[3 * p] = ys[p];
+          ch[3 * p + 2] = st.tr.challenge_scalar("z");
+        });
     std::vector<Sc> yinv = ys;
     hsc::batch_invert(yinv, false);
     for (size_t p = 0; p < P; ++p) ch[3 * p + 1] = yinv[p];
@@ -395,16 +417,25 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     }
     HostScope hs3(ctx, "pbT_host");
     std::vector<Sc> xs(P), t_hat;
-    par::for_each(P, [&](size_t p) {
-      ProverState& st = *S[p];
-      Proof& Pf = Ps[p];
-      const char* lab[5] = {"T1", "T3", "T4", "T5", "T6"};
-      for (int i = 0; i < 5; ++i) {
-        Pf.T[i] = T[5 * p + i];
-        st.tr.append_point(lab[i], Pf.T[i].data());
-      }
-      xs[p] = st.tr.challenge_scalar("x");
-    });
+    static const char* Tlab[5] = {"T1", "T3", "T4", "T5", "T6"};
+    for (size_t p = 0; p < P; ++p)
+      for (int i = 0; i < 5; ++i) Ps[p].T[i] = T[5 * p + i];
+    merlin::lockstep_x8(
+        trs, for_groups,
+        [&](merlin::TranscriptX8& X, const size_t* idx, size_t real) {
+          const uint8_t* msg[8];
+          for (int i = 0; i < 5; ++i) {
+            for (int j = 0; j < 8; ++j) msg[j] = Ps[idx[j]].T[i].data();
+            X.append(Tlab[i], msg, 32);
+          }
+          Sc x8[8];
+          X.challenge_scalar("x", x8);
+          for (size_t j = 0; j < real; ++j) xs[idx[j]] = x8[j];
+        },
+        [&](size_t p) {
+          for (int i = 0; i < 5; ++i) S[p]->tr.append_point(Tlab[i], Ps[p].T[i].data());
+          xs[p] = S[p]->tr.challenge_scalar("x");
+        });
     BPP_TRY(poly_x_dev(ctx, C, (uint32_t)P, xs, &d_l, &d_r, &d_hf, t_hat));
     par::for_each(P, [&](size_t p) {
       ProverState& st = *S[p];
@@ -417,25 +448,42 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
       using hsc::add;
       Sc tau_x = hsc::mul(xp[2], zwvg[p]);
       for (int i = 0; i < 5; ++i) tau_x = add(tau_x, hsc::mul(st.d.taus[i], xp[tidx[i]]));
-      const Sc mu = add(add(hsc::mul(st.d.alpha, x), hsc::mul(st.d.beta, xp[2])), hsc::mul(st.d.rho, xp[3]));
-      st.tr.append_scalar("TX", tau_x);
-      st.tr.append_scalar("mu", mu);
-      st.tr.append_scalar("t", t_hat[p]);
       Pf.tau_x = tau_x;
-      Pf.mu = mu;
+      Pf.mu = add(add(hsc::mul(st.d.alpha, x), hsc::mul(st.d.beta, xp[2])), hsc::mul(st.d.rho, xp[3]));
       Pf.t_hat = t_hat[p];
-      st.w = st.tr.challenge_scalar("w");
     });
+    merlin::lockstep_x8(
+        trs, for_groups,
+        [&](merlin::TranscriptX8& X, const size_t* idx, size_t real) {
+          uint8_t b[3][8][32];
+          const uint8_t* msg[8];
+          for (int j = 0; j < 8; ++j) {
+            hsc::to_bytes(b[0][j], Ps[idx[j]].tau_x);
+            hsc::to_bytes(b[1][j], Ps[idx[j]].mu);
+            hsc::to_bytes(b[2][j], Ps[idx[j]].t_hat);
+          }
+          static const char* lab[3] = {"TX", "mu", "t"};
+          for (int i = 0; i < 3; ++i) {
+            for (int j = 0; j < 8; ++j) msg[j] = b[i][j];
+            X.append(lab[i], msg, 32);
+          }
+          Sc w8[8];
+          X.challenge_scalar("w", w8);
+          for (size_t j = 0; j < real; ++j) S[idx[j]]->w = w8[j];
+        },
+        [&](size_t p) {
+          ProverState& st = *S[p];
+          st.tr.append_scalar("TX", Ps[p].tau_x);
+          st.tr.append_scalar("mu", Ps[p].mu);
+          st.tr.append_scalar("t", Ps[p].t_hat);
+          st.w = st.tr.challenge_scalar("w");
+        });
   }
   // IPA of every proof in lockstep
   hs.reset(new HostScope(ctx, "pb_ipa"));
   {
     std::vector<Sc> qmul(P);
-    std::vector<merlin::Transcript*> trs(P);
-    for (size_t p = 0; p < P; ++p) {
-      qmul[p] = S[p]->w;
-      trs[p] = &S[p]->tr;
-    }
+    for (size_t p = 0; p < P; ++p) qmul[p] = S[p]->w;
     IpaGens ig;
     ig.pts = pts;
     ig.gbase = 0;

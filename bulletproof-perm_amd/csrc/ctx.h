@@ -96,6 +96,11 @@ int ctx_pinned(bpp_ctx* ctx, size_t bytes, void** out);
 // hipMemcpyAsync measured up to ~25 ms on a 20 KB copy on the box); the host
 // buffer may be freed as soon as this returns.
 int ctx_h2d(bpp_ctx* ctx, void* d, const void* h, size_t bytes);
+// Two-step form for data produced straight into the pinned arena:
+// ctx_h2d_stage hands out `bytes` of staging (valid until the next
+// ctx_sync), ctx_h2d_staged enqueues its copy to d.
+int ctx_h2d_stage(bpp_ctx* ctx, size_t bytes, uint8_t** p);
+int ctx_h2d_staged(bpp_ctx* ctx, void* d, const uint8_t* p, size_t bytes);
 // ctx_h2d that skips the copy when workspace `name` (at d) already holds
 // exactly these bytes: for arrays that repeat batch after batch (circuit
 // CSR, generator indices).  Only for workspaces no kernel writes.

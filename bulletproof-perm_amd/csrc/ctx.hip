@@ -102,6 +102,13 @@ static int stage_take(bpp_ctx* ctx, size_t bytes, uint8_t** out) {
   return BPP_OK;
 }
 
+int ctx_h2d_stage(bpp_ctx* ctx, size_t bytes, uint8_t** p) { return stage_take(ctx, bytes, p); }
+
+int ctx_h2d_staged(bpp_ctx* ctx, void* d, const uint8_t* p, size_t bytes) {
+  if (bytes) BPP_HIP(hipMemcpyAsync(d, p, bytes, hipMemcpyHostToDevice, ctx->stream));
+  return BPP_OK;
+}
+
 int ctx_h2d(bpp_ctx* ctx, void* d, const void* h, size_t bytes) {
   if (!bytes) return BPP_OK;
   uint8_t* p = nullptr;

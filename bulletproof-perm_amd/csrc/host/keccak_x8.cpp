@@ -160,6 +160,27 @@ static void parse_randomness(const Circuit& C, const uint8_t* s, std::vector<uin
   for (auto& x : taus) x = scalar();
 }
 
+// pi, alpha, beta, rho, tau only (gamma, s_L, s_R skipped: device-reduced)
+static void parse_randomness_host_part(const Circuit& C, const uint8_t* s, std::vector<uint32_t>& pi,
+                                       hsc::Sc& alpha, hsc::Sc& beta, hsc::Sc& rho, std::vector<hsc::Sc>& taus) {
+  pi.resize(C.k);
+  for (uint32_t i = 0; i < C.k; ++i) pi[i] = i;
+  for (uint32_t i = C.k - 1; i > 0; --i) {
+    uint64_t x;
+    memcpy(&x, s, 8);
+    s += 8;
+    const uint32_t j = (uint32_t)(x % (uint64_t)(i + 1));
+    std::swap(pi[i], pi[j]);
+  }
+  s += 64 * (size_t)C.m;
+  alpha = hsc::from_wide(s);
+  beta = hsc::from_wide(s + 64);
+  rho = hsc::from_wide(s + 128);
+  s += 192 + 128 * (size_t)C.n_p;
+  taus.resize(5);
+  for (int i = 0; i < 5; ++i) taus[i] = hsc::from_wide(s + 64 * i);
+}
+
 size_t randomness_bytes(const Circuit& C) { return 8 * (size_t)(C.k - 1) + 64 * ((size_t)C.m + 3 + 2 * C.n_p + 5); }
 
 void draw_prover_randomness_x8(const Circuit& C, const Seed seeds[8], RandomDraws* const out[8]) {
@@ -185,6 +206,36 @@ void draw_prover_randomness_x8(const Circuit& C, const Seed seeds[8], RandomDraw
   for (int j = 0; j < 8; ++j)
     parse_randomness(C, outp[j], out[j]->pi, out[j]->gamma, out[j]->alpha, out[j]->beta, out[j]->rho, out[j]->sL,
                      out[j]->sR, out[j]->taus);
+}
+
+}  // namespace perm
+
+namespace perm {
+
+void draw_prover_randomness_x8_stream(const Circuit& C, const Seed seeds[8], uint8_t* const stream[8],
+                                      RandomDraws* const out[8]) {
+  const size_t len = randomness_bytes(C);
+  if (!merlin::keccak_x8_available()) {
+    for (int j = 0; j < 8; ++j) {
+      Rng rng("bpperm-prove", seeds[j]);
+      rng.bytes(stream[j], len);
+    }
+  } else {
+    uint8_t in[8][12 + 32];
+    const uint8_t* inp[8];
+    for (int j = 0; j < 8; ++j) {
+      memcpy(in[j], "bpperm-prove", 12);
+      memcpy(in[j] + 12, seeds[j].b, seeds[j].len);
+      inp[j] = in[j];
+    }
+    merlin::shake256_x8(inp, 12 + seeds[0].len, stream, len);
+  }
+  for (int j = 0; j < 8; ++j) {
+    out[j]->gamma.clear();
+    out[j]->sL.clear();
+    out[j]->sR.clear();
+    parse_randomness_host_part(C, stream[j], out[j]->pi, out[j]->alpha, out[j]->beta, out[j]->rho, out[j]->taus);
+  }
 }
 
 }  // namespace perm

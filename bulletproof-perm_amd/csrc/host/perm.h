@@ -103,6 +103,12 @@ size_t randomness_bytes(const Circuit& C);
 // AVX-512), byte-identical to draw_prover_randomness.
 // (the eight seeds must have the same length)
 void draw_prover_randomness_x8(const Circuit& C, const Seed seeds[8], RandomDraws* const out[8]);
+// As above, but the eight streams are written to stream[j] (randomness_bytes
+// each) and only pi, alpha, beta, rho and tau are parsed on the host: gamma,
+// s_L and s_R stay in the streams (reduced on the GPU, poly.h
+// draws_reduce_dev) and out[j]'s vectors for them are left empty.
+void draw_prover_randomness_x8_stream(const Circuit& C, const Seed seeds[8], uint8_t* const stream[8],
+                                      RandomDraws* const out[8]);
 
 size_t proof_len(uint32_t k);
 

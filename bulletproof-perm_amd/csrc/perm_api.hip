@@ -180,6 +180,13 @@ int msm_terms(bpp_ctx* ctx, const std::vector<Sc>& sc, const std::vector<uint32_
 // profile of 8 batches in flight spent ~20 % of the host CPU in malloc /
 // free and arena locks, largely vectors allocated by pool workers and freed
 // by the driver thread at the end of every batch.
+// Batch-sized host arrays, also reused batch after batch (resize to the same
+// size neither allocates nor zero-fills; every element is written before use).
+struct ProverScratch {
+  std::vector<Enc32> V;
+  std::vector<uint32_t> idx;
+};
+
 struct ProverState {
   merlin::Transcript tr;
   perm::RandomDraws d;  // pi, gamma, alpha, beta, rho, s_L, s_R, tau
@@ -205,103 +212,119 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
   std::vector<std::unique_ptr<ProverState>>& S = S_tl;
   while (S.size() < P) S.emplace_back(new ProverState());
   par::for_each(P, [&](size_t p) { S[p]->tr = merlin::Transcript(label, llen); });
+  static thread_local ProverScratch scr_tl;
+  ProverScratch& scr = scr_tl;
   std::vector<merlin::Transcript*> trs(P);  // this batch's transcripts (lockstep_x8)
   for (size_t p = 0; p < P; ++p) trs[p] = &S[p]->tr;
   const auto for_groups = [](size_t n, const std::function<void(size_t)>& f) { par::for_each(n, f); };
 
-  // RNG draws (order fixed: pi, gamma, alpha beta rho, s_L, s_R, tau x5)
-  // (eight proofs' SHAKE256 streams per AVX-512 Keccak, perm::draw_prover_randomness_x8)
+  const uint32_t per = 3 + 5 * n_p;  // A_I/A_O/S terms per proof
+  // RNG draws (order fixed: pi, gamma, alpha beta rho, s_L, s_R, tau x5):
+  // eight proofs' SHAKE256 streams per AVX-512 Keccak, written straight into
+  // the pinned upload arena; the host parses pi, alpha, beta, rho, tau and
+  // the GPU reduces the 2 n_p + m wide draws it alone uses (gamma -> [P][m],
+  // s_L / s_R -> their slots of the A_I/A_O/S scalar array)
   std::unique_ptr<HostScope> hs(new HostScope(ctx, "pb_rng"));
-  par::for_each((P + 7) / 8, [&](size_t gi) {
-    perm::Seed sd[8];
-    perm::RandomDraws* d[8];
-    perm::RandomDraws spare;  // a short last group's padding lanes
-    for (size_t j = 0; j < 8; ++j) {
-      sd[j] = seeds[std::min(8 * gi + j, P - 1)];
-      d[j] = 8 * gi + j < P ? &S[8 * gi + j]->d : &spare;
-    }
-    perm::draw_prover_randomness_x8(C, sd, d);
-    for (size_t j = 0; j < 8 && 8 * gi + j < P; ++j) S[8 * gi + j]->tr.arithmetic_domain_sep(n_p);
-#ifdef EXP_HOST_BURN_US  // timing experiment only: extra host CPU per proof
-    const auto t0 = std::chrono::steady_clock::now();
-    while (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(8 * EXP_HOST_BURN_US)) {
-    }
-#endif
-  });
-
-  // every proof's blindings gamma[0..m) on the device for tau_x's
-  // <z^Q W_V, gamma> (k_poly_coef); the stream is idle here
-  uint32_t* d_gamma = nullptr;
+  const size_t rlen = perm::randomness_bytes(C);
+  uint32_t *d_gamma = nullptr, *d_s = nullptr, *d_pi = nullptr;
   {
-    void* d = nullptr;
-    BPP_TRY(ctx_ws(ctx, "pb_gamma", (size_t)P * m * 32, &d));
-    d_gamma = (uint32_t*)d;
-    std::vector<Sc> gam((size_t)P * m);
-    for (size_t p = 0; p < P; ++p) std::copy(S[p]->d.gamma.begin(), S[p]->d.gamma.end(), gam.begin() + p * m);
-    BPP_TRY(ctx_h2d(ctx, d_gamma, gam.data(), gam.size() * 32));
-  }
-  // V_0..V_2k-1 of every proof: one fixed-base launch
-  hs.reset(new HostScope(ctx, "pb_pedersen_V"));
-  {
-    std::vector<Sc> v((size_t)P * 2 * k), g((size_t)P * 2 * k);
-    par::for_each(P, [&](size_t p) {
-      for (uint32_t i = 0; i < k; ++i) {
-        v[p * 2 * k + i] = hsc::from_u64(i + 1);
-        v[p * 2 * k + k + i] = hsc::from_u64(S[p]->d.pi[i] + 1);
-      }
-      for (uint32_t i = 0; i < 2 * k; ++i) g[p * 2 * k + i] = S[p]->d.gamma[i];
-    });
-    std::vector<Enc32> V;
-    BPP_TRY(pedersen_host(ctx, G, v, g, V));
-    // the 2k "V" appends and x_perm of eight proofs at a time in lockstep
-    // on the 8-way Keccak (merlin::TranscriptX8, byte-identical; 2.5x on
-    // this phase's ~26 us of permutations per proof); a short last group
-    // pads with copies of its last transcript whose results are dropped
+    void *dg = nullptr, *dsc = nullptr, *dst = nullptr, *dpi = nullptr;
+    BPP_TRY(ctx_ws(ctx, "pb_gamma", (size_t)P * m * 32, &dg));
+    BPP_TRY(ctx_ws(ctx, "mt_s", (size_t)P * per * 32 + 32, &dsc));
+    BPP_TRY(ctx_ws(ctx, "pb_stream", P * rlen, &dst));
+    BPP_TRY(ctx_ws(ctx, "pb_pi", (size_t)P * k * 4, &dpi));
+    d_gamma = (uint32_t*)dg;
+    d_s = (uint32_t*)dsc;
+    d_pi = (uint32_t*)dpi;
+    // (one staging region: a second take could recycle the arena under the first)
+    uint8_t* stream = nullptr;
+    BPP_TRY(ctx_h2d_stage(ctx, P * rlen + (size_t)P * k * 4, &stream));
+    uint8_t* pis = stream + P * rlen;
     par::for_each((P + 7) / 8, [&](size_t gi) {
-      std::vector<merlin::Transcript> pad;  // copies for a short last group only
-      pad.reserve(8);
-      merlin::Transcript* t[8];
-      const uint8_t* msg[8];
-      size_t pj[8];
+      perm::Seed sd[8];
+      perm::RandomDraws* d[8];
+      uint8_t* out[8];
+      perm::RandomDraws spare;                 // a short last group's padding lanes
+      static thread_local std::vector<uint8_t> pad_stream;
+      pad_stream.resize(rlen);
       for (size_t j = 0; j < 8; ++j) {
-        pj[j] = std::min(8 * gi + j, P - 1);
-        if (8 * gi + j < P) {
-          t[j] = &S[pj[j]]->tr;
-        } else {
-          pad.push_back(S[pj[j]]->tr);
-          t[j] = &pad.back();
-        }
+        const bool real = 8 * gi + j < P;
+        sd[j] = seeds[std::min(8 * gi + j, P - 1)];
+        d[j] = real ? &S[8 * gi + j]->d : &spare;
+        out[j] = real ? stream + (8 * gi + j) * rlen : pad_stream.data();
       }
-      for (size_t j = 0; j < 8 && 8 * gi + j < P; ++j)
-        Ps[pj[j]].V.assign(V.begin() + pj[j] * 2 * k, V.begin() + (pj[j] + 1) * 2 * k);
-      merlin::TranscriptX8 X;
-      if (!X.load(t)) {  // not in lockstep (cannot happen for one circuit): one at a time
-        for (size_t j = 0; j < 8 && 8 * gi + j < P; ++j) {
-          for (auto& e : Ps[pj[j]].V) t[j]->append_point("V", e.data());
-          S[pj[j]]->x_perm = t[j]->challenge_scalar("x_perm");
-        }
-        return;
+      perm::draw_prover_randomness_x8_stream(C, sd, out, d);
+      for (size_t j = 0; j < 8 && 8 * gi + j < P; ++j) {
+        S[8 * gi + j]->tr.arithmetic_domain_sep(n_p);
+        memcpy(pis + (8 * gi + j) * 4 * (size_t)k, S[8 * gi + j]->d.pi.data(), 4 * (size_t)k);
       }
-      for (uint32_t i = 0; i < 2 * k; ++i) {
-        for (size_t j = 0; j < 8; ++j) msg[j] = V[pj[j] * 2 * k + i].data();
-        X.append("V", msg, 32);
+#ifdef EXP_HOST_BURN_US  // timing experiment only: extra host CPU per proof
+      const auto t0 = std::chrono::steady_clock::now();
+      while (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(8 * EXP_HOST_BURN_US)) {
       }
-      hsc::Sc xp[8];
-      X.challenge_scalar("x_perm", xp);
-      X.store(t);
-      for (size_t j = 0; j < 8 && 8 * gi + j < P; ++j) S[pj[j]]->x_perm = xp[j];
+#endif
     });
+    BPP_TRY(ctx_h2d_staged(ctx, dst, stream, P * rlen));
+    BPP_TRY(ctx_h2d_staged(ctx, d_pi, pis, (size_t)P * k * 4));
+    BPP_TRY(draws_reduce_dev(ctx, C, (uint32_t)P, (const uint32_t*)dst, rlen, per, d_gamma, d_s));
   }
-  // V_2k = commit(x_perm, gamma_2k)
+  // V_0..V_2k-1 of every proof: one fixed-base launch over device inputs
+  // (values 1..k, pi + 1 and gamma, k_v_inputs), encodings back to the host
+  hs.reset(new HostScope(ctx, "pb_pedersen_V"));
+  uint32_t* d_gx_half = nullptr;  // gamma_2k / 2 for V_2k
+  {
+    void *dv = nullptr, *dg = nullptr, *dgx = nullptr, *denc = nullptr;
+    const size_t nv = (size_t)P * 2 * k;
+    BPP_TRY(ctx_ws(ctx, "pv_v", nv * 32, &dv));
+    BPP_TRY(ctx_ws(ctx, "pv_g", nv * 32, &dg));
+    BPP_TRY(ctx_ws(ctx, "pv_gx", (size_t)P * 32, &dgx));
+    BPP_TRY(ctx_ws(ctx, "pv_enc", nv * 32, &denc));
+    d_gx_half = (uint32_t*)dgx;
+    BPP_TRY(v_inputs_dev(ctx, C, (uint32_t)P, d_pi, d_gamma, (uint32_t*)dv, (uint32_t*)dg, d_gx_half));
+    {
+      HostScope hk(ctx, "ped_kernels");
+      BPP_TRY(pedersen_dev(ctx, G, (const uint32_t*)dv, (const uint32_t*)dg, nv, (uint32_t*)denc, nullptr));
+    }
+    std::vector<Enc32>& V = scr.V;
+    V.resize(nv);
+    {
+      HostScope hd(ctx, "ped_d2h");
+      BPP_TRY(ctx_d2h(ctx, V.data(), denc, nv * 32));
+    }
+    par::for_each(P, [&](size_t p) { Ps[p].V.assign(V.begin() + p * 2 * k, V.begin() + (p + 1) * 2 * k); });
+    // the 2k "V" appends and x_perm of eight proofs at a time in lockstep
+    // on the 8-way Keccak (byte-identical; 2.5x on this phase's ~26 us of
+    // permutations per proof)
+    merlin::lockstep_x8(
+        trs, for_groups,
+        [&](merlin::TranscriptX8& T8, const size_t* idx, size_t real) {
+          const uint8_t* msg[8];
+          for (uint32_t i = 0; i < 2 * k; ++i) {
+            for (size_t j = 0; j < 8; ++j) msg[j] = V[idx[j] * 2 * k + i].data();
+            T8.append("V", msg, 32);
+          }
+          hsc::Sc xp[8];
+          T8.challenge_scalar("x_perm", xp);
+          for (size_t j = 0; j < real; ++j) S[idx[j]]->x_perm = xp[j];
+        },
+        [&](size_t p) {
+          for (auto& e : Ps[p].V) S[p]->tr.append_point("V", e.data());
+          S[p]->x_perm = S[p]->tr.challenge_scalar("x_perm");
+        });
+  }
+  // V_2k = commit(x_perm, gamma_2k): halved scalars (x_perm / 2 from the
+  // host, gamma_2k / 2 from k_v_inputs), encoded as 2 (C / 2) on the host
   hs.reset(new HostScope(ctx, "pb_pedersen_Vx_witness"));
   {
-    std::vector<Sc> v(P), g(P);
-    for (size_t p = 0; p < P; ++p) {
-      v[p] = S[p]->x_perm;
-      g[p] = S[p]->d.gamma[2 * k];
-    }
-    std::vector<Enc32> Vx;
-    BPP_TRY(pedersen_host(ctx, G, v, g, Vx));
+    std::vector<Sc> vh(P);
+    for (size_t p = 0; p < P; ++p) vh[p] = hsc::half(S[p]->x_perm);
+    uint32_t* d_vh = nullptr;
+    BPP_TRY(upload_sc(ctx, vh, "pv_vx", &d_vh));
+    void* d_p3 = nullptr;
+    BPP_TRY(ctx_ws(ctx, "pp_p3", P * P3_BYTES, &d_p3));
+    BPP_TRY(pedersen_dev(ctx, G, d_vh, d_gx_half, P, nullptr, (uint32_t*)d_p3));
+    std::vector<Enc32> Vx(P);
+    BPP_TRY(points_double_encode_p3(ctx, (const uint32_t*)d_p3, P, Vx[0].data()));
     par::for_each(P, [&](size_t p) {
       Ps[p].V.push_back(Vx[p]);
       S[p]->tr.append_point("V", Vx[p].data());
@@ -310,28 +333,36 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
   }
   MsmPoints pts;
   BPP_TRY(gens_points(ctx, G, &pts));
-  const uint32_t per = 3 + 5 * n_p;  // A_I/A_O/S terms per proof
-  uint32_t* d_s = nullptr;           // their scalars, reused by the polynomial stage
-  // A_I, A_O, S of every proof: one batch of 3P MSMs
+  // A_I, A_O, S of every proof: one batch of 3P MSMs.  The host writes the
+  // first 3 + 3 n_p scalars of each proof (alpha, a_L, a_R, beta, a_O, rho)
+  // into the device array whose s_L / s_R slots k_draws_reduce filled.
   hs.reset(new HostScope(ctx, "pb_msm_AI_AO_S"));
   {
-    std::vector<Sc> sc((size_t)P * per);
-    std::vector<uint32_t> idx((size_t)P * per), off(3 * P + 1);
+    const uint32_t hostw = 3 + 3 * n_p;  // host-written scalars per proof
+    std::vector<uint32_t>& idx = scr.idx;
+    idx.resize((size_t)P * per);
+    std::vector<uint32_t> off(3 * P + 1);
+    uint8_t* stg = nullptr;  // written in place in the pinned arena
+    BPP_TRY(ctx_h2d_stage(ctx, (size_t)P * hostw * 32, &stg));
     par::for_each(P, [&](size_t p) {
       ProverState& st = *S[p];
-      size_t t = p * per;
-      auto add = [&](const Sc& s, uint32_t i) {
-        sc[t] = s;
-        idx[t++] = i;
-      };
-      add(st.d.alpha, G->bbidx());
-      for (uint32_t i = 0; i < n_p; ++i) add(st.aL[i], G->gidx(i));
-      for (uint32_t i = 0; i < n_p; ++i) add(st.aR[i], G->hidx(i));
-      add(st.d.beta, G->bbidx());
-      for (uint32_t i = 0; i < n_p; ++i) add(st.aO[i], G->gidx(i));
-      add(st.d.rho, G->bbidx());
-      for (uint32_t i = 0; i < n_p; ++i) add(st.d.sL[i], G->gidx(i));
-      for (uint32_t i = 0; i < n_p; ++i) add(st.d.sR[i], G->hidx(i));
+      Sc* o = reinterpret_cast<Sc*>(stg) + p * hostw;
+      o[0] = st.d.alpha;
+      std::copy(st.aL.begin(), st.aL.begin() + n_p, o + 1);
+      std::copy(st.aR.begin(), st.aR.begin() + n_p, o + 1 + n_p);
+      o[1 + 2 * n_p] = st.d.beta;
+      std::copy(st.aO.begin(), st.aO.begin() + n_p, o + 2 + 2 * n_p);
+      o[2 + 3 * n_p] = st.d.rho;
+      uint32_t* ix = &idx[p * per];
+      size_t t = 0;
+      ix[t++] = G->bbidx();
+      for (uint32_t i = 0; i < n_p; ++i) ix[t++] = G->gidx(i);
+      for (uint32_t i = 0; i < n_p; ++i) ix[t++] = G->hidx(i);
+      ix[t++] = G->bbidx();
+      for (uint32_t i = 0; i < n_p; ++i) ix[t++] = G->gidx(i);
+      ix[t++] = G->bbidx();
+      for (uint32_t i = 0; i < n_p; ++i) ix[t++] = G->gidx(i);
+      for (uint32_t i = 0; i < n_p; ++i) ix[t++] = G->hidx(i);
     });
     for (size_t p = 0; p < P; ++p) {
       off[3 * p] = (uint32_t)(p * per);
@@ -339,14 +370,15 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
       off[3 * p + 2] = (uint32_t)(p * per + 2 + 3 * n_p);
     }
     off[3 * P] = (uint32_t)(P * per);
-    BPP_TRY(upload_sc(ctx, sc, "mt_s", &d_s));
+    BPP_HIP(hipMemcpy2DAsync(d_s, (size_t)per * 32, stg, (size_t)hostw * 32, (size_t)hostw * 32, P,
+                             hipMemcpyHostToDevice, ctx->stream));
     void* d_i = nullptr;
     BPP_TRY(ctx_ws(ctx, "mt_i", idx.size() * 4 + 4, &d_i));
     BPP_TRY(ctx_h2d_const(ctx, "mt_i", d_i, idx.data(), idx.size() * 4));  // generator indices: same every batch
     // MSMs of the halved scalars, encoded as 2 * result (msm_multi_enc)
     void* d_sh = nullptr;
-    BPP_TRY(ctx_ws(ctx, "mt_s_half", sc.size() * 32 + 32, &d_sh));
-    BPP_TRY(sc_halve_dev(ctx, d_s, (uint32_t*)d_sh, sc.size()));
+    BPP_TRY(ctx_ws(ctx, "mt_s_half", (size_t)P * per * 32 + 32, &d_sh));
+    BPP_TRY(sc_halve_dev(ctx, d_s, (uint32_t*)d_sh, (size_t)P * per));
     std::vector<uint8_t> enc(3 * P * 32);
     BPP_TRY(msm_multi_enc(ctx, (const uint32_t*)d_sh, (const uint32_t*)d_i, off, pts, enc.data(), true));
     par::for_each(P, [&](size_t p) {

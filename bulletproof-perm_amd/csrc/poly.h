@@ -26,3 +26,14 @@ int poly_x_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const std::vect
 // count x (m + 8 + 2 lg) weighted proof-point scalars.
 int verify_scalars_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const std::vector<uint32_t>& rec,
                        uint32_t* d_sc);
+
+// The prover's SHAKE256 streams ([P][len] bytes on the device, len =
+// perm::randomness_bytes) -> gamma ([P][m], canonical) and s_L, s_R into
+// their slots of the A_I/A_O/S scalar array d_sc ([P][per]).
+int draws_reduce_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint32_t* d_stream, size_t len,
+                     uint32_t per, uint32_t* d_gamma, uint32_t* d_sc);
+
+// V commitment inputs on the device from pi ([P][k] u32) and gamma:
+// d_v, d_g [P][2k] and d_gx_half [P] = gamma_2k / 2.
+int v_inputs_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint32_t* d_pi, const uint32_t* d_gamma,
+                 uint32_t* d_v, uint32_t* d_g, uint32_t* d_gx_half);

@@ -290,6 +290,64 @@ __global__ void __launch_bounds__(POLY_T) k_verify_merge(uint32_t count, uint32_
   if (threadIdx.x == 0) sc_store(sc_out + 8 * i, acc[0]);
 }
 
+// ---------------------------------------------------------------------------
+// The prover's wide random draws reduced on the device.  stream = [P][len]
+// bytes of each proof's SHAKE256 stream (host/perm.h draw order: pi's u64s,
+// gamma[m], alpha beta rho, s_L[n_p], s_R[n_p], tau[5]); the host parses pi,
+// alpha, beta, rho and tau itself and never needs gamma, s_L, s_R: gamma goes
+// to [P][m] (V commitments, tau_x), s_L / s_R straight into their slots of the
+// A_I/A_O/S scalar array ([P][per], per = 3 + 5 n_p: s_L at 3 + 3 n_p).
+__global__ void __launch_bounds__(256) k_draws_reduce(uint32_t P, uint32_t len_w, uint32_t off_w, uint32_t m,
+                                                     uint32_t n_p, uint32_t per, const uint32_t* __restrict__ stream,
+                                                     uint32_t* __restrict__ gamma, uint32_t* __restrict__ sc_out) {
+  const uint32_t nw = m + 2 * n_p;
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (size_t)P * nw) return;
+  const uint32_t p = (uint32_t)(t / nw), j = (uint32_t)(t % nw);
+  const uint32_t slot = j < m ? j : j + 3;  // alpha, beta, rho sit between gamma and s_L
+  const sc x = sc_from_wide_w(stream + (size_t)p * len_w + off_w + 16 * slot);
+  if (j < m) sc_store(gamma + 8 * ((size_t)p * m + j), x);
+  else sc_store(sc_out + 8 * ((size_t)p * per + 3 + 3 * n_p + (j - m)), x);
+}
+
+// Inputs of the V commitments: v[p][i] = i + 1 (i < k), pi_p[i - k] + 1
+// (k <= i < 2k), g[p][i] = gamma[p][i]; gx[p] = gamma[p][2k] / 2 (V_2k is
+// committed with halved scalars and encoded as 2 (C / 2) on the host).
+__global__ void __launch_bounds__(256) k_v_inputs(uint32_t P, uint32_t k, uint32_t m, const uint32_t* __restrict__ pi,
+                                                 const uint32_t* __restrict__ gamma, uint32_t* __restrict__ v,
+                                                 uint32_t* __restrict__ g, uint32_t* __restrict__ gx_half) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (size_t)P * (2 * k + 1)) return;
+  const uint32_t p = (uint32_t)(t / (2 * k + 1)), i = (uint32_t)(t % (2 * k + 1));
+  const sc gm = sc_load(gamma + 8 * ((size_t)p * m + i));
+  if (i == 2 * k) {
+    sc_store(gx_half + 8 * (size_t)p, sc_half(gm));
+    return;
+  }
+  sc vv = sc_zero();
+  vv.v[0] = i < k ? i + 1 : pi[(size_t)p * k + (i - k)] + 1;
+  sc_store(v + 8 * ((size_t)p * 2 * k + i), vv);
+  sc_store(g + 8 * ((size_t)p * 2 * k + i), gm);
+}
+
+int draws_reduce_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint32_t* d_stream, size_t len,
+                     uint32_t per, uint32_t* d_gamma, uint32_t* d_sc) {
+  if (!P) return BPP_OK;
+  const size_t nt = (size_t)P * (C.m + 2 * C.n_p);
+  hipLaunchKernelGGL(k_draws_reduce, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, ctx->stream, P,
+                     (uint32_t)(len / 4), (uint32_t)(8 * (C.k - 1) / 4), C.m, C.n_p, per, d_stream, d_gamma, d_sc);
+  return ctx_check_launch(ctx, "k_draws_reduce");
+}
+
+int v_inputs_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint32_t* d_pi, const uint32_t* d_gamma,
+                 uint32_t* d_v, uint32_t* d_g, uint32_t* d_gx_half) {
+  if (!P) return BPP_OK;
+  const size_t nt = (size_t)P * (2 * C.k + 1);
+  hipLaunchKernelGGL(k_v_inputs, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, ctx->stream, P, C.k, C.m, d_pi,
+                     d_gamma, d_v, d_g, d_gx_half);
+  return ctx_check_launch(ctx, "k_v_inputs");
+}
+
 namespace {
 
 // Column-CSR of WL, WR, WO over the n_p gate columns: cp[3][n_p + 1],

@@ -138,6 +138,44 @@ FE_INLINE sc sc_from_mont(const sc& a) {
   return sc_mont(a, one);
 }
 
+// canonical w mod l for w < 2^256: w = q 2^252 + rest (q < 16), w - q l =
+// rest - q delta is in (-l, 2^252), one conditional addition of l
+FE_INLINE sc sc_reduce256(const uint32_t w[8]) {
+  const uint32_t q = w[7] >> 28;
+  sc r;
+  uint64_t pc = 0;   // q * l carry
+  uint32_t br = 0;   // borrow
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) {
+    const uint64_t pr = (uint64_t)q * SC_L[i] + pc;
+    pc = pr >> 32;
+    const uint64_t d = (uint64_t)w[i] - (uint32_t)pr - br;
+    r.v[i] = (uint32_t)d;
+    br = (uint32_t)(d >> 63);
+  }
+  if (br) {
+    uint64_t c = 0;
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) {
+      c += (uint64_t)r.v[i] + SC_L[i];
+      r.v[i] = (uint32_t)c;
+      c >>= 32;
+    }
+  }
+  return r;
+}
+
+// Scalar::from_bytes_mod_order_wide of 16 little-endian words, canonical:
+// x = lo + hi 2^256 = lo + hi R, and mont(hi, R^2) = hi R (mod l)
+FE_INLINE sc sc_from_wide_w(const uint32_t* __restrict__ w) {
+  sc hi, r2;
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) {
+    hi.v[i] = w[8 + i];
+    r2.v[i] = SC_R2[i];
+  }
+  uint32_t lo[8];
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) lo[i] = w[i];
+  return sc_add(sc_reduce256(lo), sc_mont(hi, r2));
+}
+
 // 64-lane wave reduction of a Montgomery scalar sum (result valid in lane 0)
 FE_INLINE sc sc_wave_sum(sc a) {
   _Pragma("unroll") for (int d = 32; d >= 1; d >>= 1) {

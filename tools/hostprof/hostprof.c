@@ -4,8 +4,10 @@
 // at that moment (state R in /proc/self/task/TID/stat); the handler records
 // its instruction pointer.  (ITIMER_PROF delivered only ~15 samples a
 // second to a 20-thread process.)  hp_stop() writes one line
-// per sample: "<object path> <offset in object> <symbol or ?>" (dladdr), to
-// be aggregated by tools/hostprof/report.py (nm resolves local symbols).
+// per sample: "<object path> <offset> <caller offset in libbpperm> <symbol or ?>", to
+// be aggregated by tools/hostprof/report.py (nm resolves local symbols);
+// for every sample the first word of the interrupted stack that points into
+// libbpperm.so's code is kept as a likely caller (libc / runtime samples).
 //   gcc -O2 -shared -fPIC tools/hostprof/hostprof.c -o tools/hostprof/libhostprof.so -ldl -lpthread
 #define _GNU_SOURCE
 #include <dlfcn.h>
@@ -23,8 +25,10 @@
 #include <time.h>
 #include <unistd.h>
 
-#define MAXS (1u << 21)
+#define MAXS (1u << 18)
+#define STACKW 48  // words copied from the stack top (caller heuristics)
 static uintptr_t samples[MAXS];
+static uintptr_t stacks[MAXS][STACKW];
 static atomic_uint nsamp;
 
 static void on_prof(int sig, siginfo_t* si, void* ucv) {
@@ -32,7 +36,11 @@ static void on_prof(int sig, siginfo_t* si, void* ucv) {
   (void)si;
   const ucontext_t* uc = (const ucontext_t*)ucv;
   const unsigned i = atomic_fetch_add(&nsamp, 1u);
-  if (i < MAXS) samples[i] = (uintptr_t)uc->uc_mcontext.gregs[REG_RIP];
+  if (i < MAXS) {
+    samples[i] = (uintptr_t)uc->uc_mcontext.gregs[REG_RIP];
+    const uintptr_t* sp = (const uintptr_t*)uc->uc_mcontext.gregs[REG_RSP];
+    for (int k = 0; k < STACKW; ++k) stacks[i][k] = sp[k];
+  }
 }
 
 static atomic_int running;
@@ -80,20 +88,55 @@ int hp_start(int hz) {
   return pthread_create(&sampler, NULL, sampler_main, NULL);
 }
 
+// executable mappings of libbpperm.so (caller candidates must point into code)
+static uintptr_t xlo[8], xhi[8];
+static int nx = 0;
+static void load_exec_ranges(void) {
+  FILE* m = fopen("/proc/self/maps", "r");
+  if (!m) return;
+  char line[512];
+  while (nx < 8 && fgets(line, sizeof line, m)) {
+    unsigned long lo, hi;
+    char perms[8];
+    if (sscanf(line, "%lx-%lx %7s", &lo, &hi, perms) == 3 && perms[2] == 'x' && strstr(line, "libbpperm")) {
+      xlo[nx] = lo;
+      xhi[nx] = hi;
+      ++nx;
+    }
+  }
+  fclose(m);
+}
+static int in_exec(uintptr_t a) {
+  for (int i = 0; i < nx; ++i)
+    if (a >= xlo[i] && a < xhi[i]) return 1;
+  return 0;
+}
+
 long hp_stop(const char* path) {
   atomic_store(&running, 0);
   pthread_join(sampler, NULL);
   unsigned n = atomic_load(&nsamp);
   if (n > MAXS) n = MAXS;
+  load_exec_ranges();
   FILE* f = fopen(path, "w");
   if (!f) return -1;
   for (unsigned i = 0; i < n; ++i) {
     Dl_info di;
+    // caller heuristic for samples outside libbpperm: the first stack word
+    // that points into libbpperm.so's code
+    unsigned long caller = 0;
+    for (int k = 0; k < STACKW; ++k) {
+      Dl_info dc;
+      if (in_exec(stacks[i][k]) && dladdr((void*)stacks[i][k], &dc) && dc.dli_fname) {
+        caller = (unsigned long)(stacks[i][k] - (uintptr_t)dc.dli_fbase);
+        break;
+      }
+    }
     if (dladdr((void*)samples[i], &di) && di.dli_fname) {
-      fprintf(f, "%s %lx %s\n", di.dli_fname, (unsigned long)(samples[i] - (uintptr_t)di.dli_fbase),
+      fprintf(f, "%s %lx %lx %s\n", di.dli_fname, (unsigned long)(samples[i] - (uintptr_t)di.dli_fbase), caller,
               di.dli_sname ? di.dli_sname : "?");
     } else {
-      fprintf(f, "? %lx ?\n", (unsigned long)samples[i]);
+      fprintf(f, "? %lx %lx ?\n", (unsigned long)samples[i], caller);
     }
   }
   fclose(f);

@@ -8,7 +8,13 @@ import sys
 
 path = sys.argv[1]
 top = int(sys.argv[2]) if len(sys.argv) > 2 else 40
-rows = [ln.split(" ", 2) for ln in open(path).read().splitlines() if ln]
+rows = []
+for ln in open(path).read().splitlines():
+    p = ln.split(" ", 3)
+    if len(p) == 4:
+        rows.append((p[0], p[1], p[3], p[2]))
+    elif len(p) == 3:  # (older format without the caller column)
+        rows.append((p[0], p[1], p[2], "0"))
 n = len(rows)
 by_obj = collections.Counter(os.path.basename(r[0]) for r in rows)
 print(f"{n} samples")
@@ -36,7 +42,7 @@ def table(obj):
 
 
 by_fn = collections.Counter()
-for obj, off, sname in rows:
+for obj, off, sname, _ in rows:
     name = sname.strip()
     if obj != "?":
         addrs, names = table(obj)
@@ -47,3 +53,18 @@ for obj, off, sname in rows:
 print("top functions")
 for (o, f), c in by_fn.most_common(top):
     print(f"  {c / n:6.1%}  {o:24s} {f}")
+
+# callers (first libbpperm return address on the interrupted stack) of the
+# samples outside libbpperm
+bp = next((r[0] for r in rows if r[0].endswith("libbpperm.so")), None)
+if bp:
+    addrs, names = table(bp)
+    by_caller = collections.Counter()
+    for obj, off, sname, caller in rows:
+        if obj.endswith("libbpperm.so") or caller == "0":
+            continue
+        i = bisect.bisect_right(addrs, int(caller, 16)) - 1
+        by_caller[(os.path.basename(obj), names[i][:80] if i >= 0 else "?")] += 1
+    print("callers in libbpperm of samples in other objects")
+    for (o, f), c in by_caller.most_common(top // 2):
+        print(f"  {c / n:6.1%}  {o:24s} <- {f}")

@@ -219,6 +219,9 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
   const auto for_groups = [](size_t n, const std::function<void(size_t)>& f) { par::for_each(n, f); };
 
   const uint32_t per = 3 + 5 * n_p;  // A_I/A_O/S terms per proof
+  // the witness on the device (k_witness) while its prefix products fit the
+  // workgroup's LDS; the host restatement beyond that
+  const bool dev_witness = (2 * (size_t)k + 512) * 32 <= 64 * 1024;
   // RNG draws (order fixed: pi, gamma, alpha beta rho, s_L, s_R, tau x5):
   // eight proofs' SHAKE256 streams per AVX-512 Keccak, written straight into
   // the pinned upload arena; the host parses pi, alpha, beta, rho, tau and
@@ -316,10 +319,14 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
   // host, gamma_2k / 2 from k_v_inputs), encoded as 2 (C / 2) on the host
   hs.reset(new HostScope(ctx, "pb_pedersen_Vx_witness"));
   {
-    std::vector<Sc> vh(P);
-    for (size_t p = 0; p < P; ++p) vh[p] = hsc::half(S[p]->x_perm);
+    std::vector<Sc> vh(2 * P);  // x_perm / 2 (V_2k), then x_perm (the device witness)
+    for (size_t p = 0; p < P; ++p) {
+      vh[p] = hsc::half(S[p]->x_perm);
+      vh[P + p] = S[p]->x_perm;
+    }
     uint32_t* d_vh = nullptr;
     BPP_TRY(upload_sc(ctx, vh, "pv_vx", &d_vh));
+    if (dev_witness) BPP_TRY(witness_dev(ctx, C, (uint32_t)P, d_pi, d_vh + 8 * P, per, d_s));
     void* d_p3 = nullptr;
     BPP_TRY(ctx_ws(ctx, "pp_p3", P * P3_BYTES, &d_p3));
     BPP_TRY(pedersen_dev(ctx, G, d_vh, d_gx_half, P, nullptr, (uint32_t*)d_p3));
@@ -328,7 +335,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     par::for_each(P, [&](size_t p) {
       Ps[p].V.push_back(Vx[p]);
       S[p]->tr.append_point("V", Vx[p].data());
-      perm::witness(C, S[p]->d.pi, S[p]->x_perm, S[p]->vals, S[p]->aL, S[p]->aR, S[p]->aO);
+      if (!dev_witness) perm::witness(C, S[p]->d.pi, S[p]->x_perm, S[p]->vals, S[p]->aL, S[p]->aR, S[p]->aO);
     });
   }
   MsmPoints pts;
@@ -342,17 +349,19 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     std::vector<uint32_t>& idx = scr.idx;
     idx.resize((size_t)P * per);
     std::vector<uint32_t> off(3 * P + 1);
-    uint8_t* stg = nullptr;  // written in place in the pinned arena
-    BPP_TRY(ctx_h2d_stage(ctx, (size_t)P * hostw * 32, &stg));
+    uint8_t* stg = nullptr;  // (host witness only) written in place in the pinned arena
+    if (!dev_witness) BPP_TRY(ctx_h2d_stage(ctx, (size_t)P * hostw * 32, &stg));
     par::for_each(P, [&](size_t p) {
       ProverState& st = *S[p];
-      Sc* o = reinterpret_cast<Sc*>(stg) + p * hostw;
-      o[0] = st.d.alpha;
-      std::copy(st.aL.begin(), st.aL.begin() + n_p, o + 1);
-      std::copy(st.aR.begin(), st.aR.begin() + n_p, o + 1 + n_p);
-      o[1 + 2 * n_p] = st.d.beta;
-      std::copy(st.aO.begin(), st.aO.begin() + n_p, o + 2 + 2 * n_p);
-      o[2 + 3 * n_p] = st.d.rho;
+      if (!dev_witness) {
+        Sc* o = reinterpret_cast<Sc*>(stg) + p * hostw;
+        o[0] = st.d.alpha;
+        std::copy(st.aL.begin(), st.aL.begin() + n_p, o + 1);
+        std::copy(st.aR.begin(), st.aR.begin() + n_p, o + 1 + n_p);
+        o[1 + 2 * n_p] = st.d.beta;
+        std::copy(st.aO.begin(), st.aO.begin() + n_p, o + 2 + 2 * n_p);
+        o[2 + 3 * n_p] = st.d.rho;
+      }
       uint32_t* ix = &idx[p * per];
       size_t t = 0;
       ix[t++] = G->bbidx();
@@ -370,8 +379,9 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
       off[3 * p + 2] = (uint32_t)(p * per + 2 + 3 * n_p);
     }
     off[3 * P] = (uint32_t)(P * per);
-    BPP_HIP(hipMemcpy2DAsync(d_s, (size_t)per * 32, stg, (size_t)hostw * 32, (size_t)hostw * 32, P,
-                             hipMemcpyHostToDevice, ctx->stream));
+    if (!dev_witness)
+      BPP_HIP(hipMemcpy2DAsync(d_s, (size_t)per * 32, stg, (size_t)hostw * 32, (size_t)hostw * 32, P,
+                               hipMemcpyHostToDevice, ctx->stream));
     void* d_i = nullptr;
     BPP_TRY(ctx_ws(ctx, "mt_i", idx.size() * 4 + 4, &d_i));
     BPP_TRY(ctx_h2d_const(ctx, "mt_i", d_i, idx.data(), idx.size() * 4));  // generator indices: same every batch

@@ -28,8 +28,8 @@ int verify_scalars_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, con
                        uint32_t* d_sc);
 
 // The prover's SHAKE256 streams ([P][len] bytes on the device, len =
-// perm::randomness_bytes) -> gamma ([P][m], canonical) and s_L, s_R into
-// their slots of the A_I/A_O/S scalar array d_sc ([P][per]).
+// perm::randomness_bytes) -> gamma ([P][m], canonical) and alpha, beta, rho,
+// s_L, s_R into their slots of the A_I/A_O/S scalar array d_sc ([P][per]).
 int draws_reduce_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint32_t* d_stream, size_t len,
                      uint32_t per, uint32_t* d_gamma, uint32_t* d_sc);
 
@@ -37,3 +37,8 @@ int draws_reduce_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uin
 // d_v, d_g [P][2k] and d_gx_half [P] = gamma_2k / 2.
 int v_inputs_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint32_t* d_pi, const uint32_t* d_gamma,
                  uint32_t* d_v, uint32_t* d_g, uint32_t* d_gx_half);
+
+// The witness a_L, a_R, a_O of every proof (x = x_perm [P] canonical, pi
+// [P][k]) into their slots of d_sc.
+int witness_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint32_t* d_pi, const uint32_t* d_x,
+                uint32_t per, uint32_t* d_sc);

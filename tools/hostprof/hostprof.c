@@ -29,6 +29,7 @@
 #define STACKW 48  // words copied from the stack top (caller heuristics)
 static uintptr_t samples[MAXS];
 static uintptr_t stacks[MAXS][STACKW];
+static int tids[MAXS];
 static atomic_uint nsamp;
 
 static void on_prof(int sig, siginfo_t* si, void* ucv) {
@@ -38,6 +39,7 @@ static void on_prof(int sig, siginfo_t* si, void* ucv) {
   const unsigned i = atomic_fetch_add(&nsamp, 1u);
   if (i < MAXS) {
     samples[i] = (uintptr_t)uc->uc_mcontext.gregs[REG_RIP];
+    tids[i] = (int)syscall(SYS_gettid);
     const uintptr_t* sp = (const uintptr_t*)uc->uc_mcontext.gregs[REG_RSP];
     for (int k = 0; k < STACKW; ++k) stacks[i][k] = sp[k];
   }
@@ -132,11 +134,21 @@ long hp_stop(const char* path) {
         break;
       }
     }
+    char comm[32] = "?";
+    {
+      char pth[64];
+      snprintf(pth, sizeof pth, "/proc/self/task/%d/comm", tids[i]);
+      FILE* c = fopen(pth, "r");
+      if (c) {
+        if (fgets(comm, sizeof comm, c)) comm[strcspn(comm, "\n ")] = 0;
+        fclose(c);
+      }
+    }
     if (dladdr((void*)samples[i], &di) && di.dli_fname) {
-      fprintf(f, "%s %lx %lx %s\n", di.dli_fname, (unsigned long)(samples[i] - (uintptr_t)di.dli_fbase), caller,
-              di.dli_sname ? di.dli_sname : "?");
+      fprintf(f, "%s %lx %lx %s %s\n", di.dli_fname, (unsigned long)(samples[i] - (uintptr_t)di.dli_fbase), caller,
+              comm, di.dli_sname ? di.dli_sname : "?");
     } else {
-      fprintf(f, "? %lx %lx ?\n", (unsigned long)samples[i], caller);
+      fprintf(f, "? %lx %lx %s ?\n", (unsigned long)samples[i], caller, comm);
     }
   }
   fclose(f);

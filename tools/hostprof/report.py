@@ -9,12 +9,15 @@ import sys
 path = sys.argv[1]
 top = int(sys.argv[2]) if len(sys.argv) > 2 else 40
 rows = []
+comms = []
 for ln in open(path).read().splitlines():
-    p = ln.split(" ", 3)
-    if len(p) == 4:
+    p = ln.split(" ", 4)
+    if len(p) == 5:  # object offset caller thread-name symbol
+        rows.append((p[0], p[1], p[4], p[2]))
+        comms.append(p[3])
+    elif len(p) == 4:
         rows.append((p[0], p[1], p[3], p[2]))
-    elif len(p) == 3:  # (older format without the caller column)
-        rows.append((p[0], p[1], p[2], "0"))
+        comms.append("?")
 n = len(rows)
 by_obj = collections.Counter(os.path.basename(r[0]) for r in rows)
 print(f"{n} samples")
@@ -68,3 +71,8 @@ if bp:
     print("callers in libbpperm of samples in other objects")
     for (o, f), c in by_caller.most_common(top // 2):
         print(f"  {c / n:6.1%}  {o:24s} <- {f}")
+
+if comms:
+    print("samples by thread name (object)")
+    for (c, o), k in collections.Counter((c, os.path.basename(r[0])) for c, r in zip(comms, rows)).most_common(12):
+        print(f"  {k / n:6.1%}  {c:16s} {o}")

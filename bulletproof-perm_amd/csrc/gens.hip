@@ -14,6 +14,8 @@
 #include <cstdlib>
 #include <cstring>
 
+#include <atomic>
+
 #include "ctx.h"
 #include "gens.h"
 #include "ge_io.cuh"
@@ -210,6 +212,8 @@ int pedersen_dev(bpp_ctx* ctx, const bpp_gens* g, const uint32_t* d_v, const uin
   return BPP_OK;
 }
 
+static std::atomic<size_t> g_dt_total{0};  // direct-table bytes of the live generator sets
+
 int gens_points(bpp_ctx* ctx, const bpp_gens* g, MsmPoints* out) {
   const uint32_t np = (uint32_t)(2 * g->n + 2);
   // First use builds the tables on this context's stream.  They are
@@ -240,8 +244,13 @@ int gens_points(bpp_ctx* ctx, const bpp_gens* g, MsmPoints* out) {
     // 258 generators of a 52-card proof, against W = 32 at c = 8.  Measured
     // in isolation (tools/ubench/dtbench, 8 batches' IPA rounds in one
     // launch): 446 / 376 / 337 / 312 / 294 us at c = 8 / 11 / 12 / 13 / 16.
+    // (and within what the process's other live generator sets leave of
+    // GENS_DT_TOTAL, so many sets -- tests, one per context -- fall back to
+    // narrower tables instead of exhausting HBM)
+    const size_t used = g_dt_total.load();
+    const size_t budget = std::min<size_t>(GENS_DT_BUDGET, used < GENS_DT_TOTAL ? GENS_DT_TOTAL - used : 0);
     uint32_t c = 8;
-    while (c < GENS_DT_CMAX && dt_bytes(np, c + 1) <= GENS_DT_BUDGET) ++c;
+    while (c < GENS_DT_CMAX && dt_bytes(np, c + 1) <= budget) ++c;
     uint32_t* d = nullptr;
     if (hipMalloc(&d, dt_bytes(np, c)) != hipSuccess) {
       ctx->err = "hipMalloc generator direct tables";
@@ -258,6 +267,7 @@ int gens_points(bpp_ctx* ctx, const bpp_gens* g, MsmPoints* out) {
     }
     g->d_dt = d;
     g->dt_c = c;
+    g_dt_total += dt_bytes(np, c);
   }
   *out = MsmPoints();
   out->tbl = g->d_tbl;
@@ -377,7 +387,10 @@ void bpp_gens_destroy(bpp_gens* g) {
   if (g->d_tbl) hipFree(g->d_tbl);
   if (g->d_fb) hipFree(g->d_fb);
   if (g->d_wt) hipFree(g->d_wt);
-  if (g->d_dt) hipFree(g->d_dt);
+  if (g->d_dt) {
+    hipFree(g->d_dt);
+    g_dt_total -= dt_bytes((uint32_t)(2 * g->n + 2), g->dt_c);
+  }
   delete g;
 }
 

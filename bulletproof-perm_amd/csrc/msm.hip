@@ -614,8 +614,8 @@ size_t dt_bytes(uint32_t npts, uint32_t c) {
 
 int dt_build(bpp_ctx* ctx, const uint32_t* d_wt, uint32_t npts, uint32_t c, uint32_t* d_dt) {
   if (!npts) return BPP_OK;
-  if (c < 8 || c > 13) {
-    ctx->err = "dt_build: window width must be 8..13";
+  if (c < 8 || c > 16) {
+    ctx->err = "dt_build: window width must be 8..16";
     return BPP_ERR_ARG;
   }
   const DtGeom g = dt_geom(c);

@@ -50,5 +50,7 @@ struct bpp_gens {
 // Builds g->d_wt if needed; fills a MsmPoints view (tbl = generators,
 // wt = their window tables).
 int gens_points(bpp_ctx* ctx, const bpp_gens* g, MsmPoints* out);
+// v_bound: 0, or a public bound every v is below (fewer positions for v)
 int pedersen_dev(bpp_ctx* ctx, const bpp_gens* g, const uint32_t* d_v, const uint32_t* d_gam, size_t m,
-                 uint32_t* d_out_enc, uint32_t* d_out_p3);
+                 uint32_t* d_out_enc, uint32_t* d_out_p3,
+                 uint64_t v_bound = 0);

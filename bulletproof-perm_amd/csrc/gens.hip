@@ -62,9 +62,15 @@ __global__ void __launch_bounds__(64) k_fb_tables(const uint32_t* __restrict__ t
 // G = 8 for large batches (13 312 V commitments per 128 proofs: fewest
 // partials), G = 32 for small ones (latency: 4 additions per lane).
 #define PED_T 256
+// v_groups: position groups that can hold nonzero digits of v (G in
+// general; 1 when a PUBLIC bound puts every v below 2^(4 P - 1), e.g. the V
+// commitments' values 1..k and pi + 1 <= k: their digits beyond group 0 are
+// all zero for every v under the bound, so skipping those groups depends on
+// k only, not on the secret values -- 72 instead of 128 table additions per
+// V commitment at G = 8).
 template <int G>
 __global__ void __launch_bounds__(PED_T) k_pedersen(const uint32_t* __restrict__ fb, const uint32_t* __restrict__ v,
-                                                    const uint32_t* __restrict__ gam, size_t m,
+                                                    const uint32_t* __restrict__ gam, size_t m, uint32_t v_groups,
                                                     uint32_t* __restrict__ part) {
   constexpr uint32_t PED_GPOS = FB_POS / G;    // positions per group
   constexpr uint32_t PED_ROWS = 2 * PED_GPOS * 8;  // table rows one block needs
@@ -81,7 +87,7 @@ __global__ void __launch_bounds__(PED_T) k_pedersen(const uint32_t* __restrict__
   const size_t j = (size_t)blockIdx.x * PED_T + threadIdx.x;
   if (j >= m) return;
   ge_p3 acc = ge_identity();
-  _Pragma("unroll 1") for (uint32_t which = 0; which < 2; ++which) {
+  _Pragma("unroll 1") for (uint32_t which = g < v_groups ? 0 : 1; which < 2; ++which) {
     // word Pg / 8 of s + K holds the nibbles of positions [Pg, Pg + P)
     const uint32_t* sp = (which ? gam : v) + 8 * j;
     const uint32_t wsel = PED_GPOS * g / 8, sh = 4 * (PED_GPOS * g % 8);
@@ -166,7 +172,7 @@ static int gens_finish(bpp_ctx* ctx, bpp_gens* g) {
 }
 
 int pedersen_dev(bpp_ctx* ctx, const bpp_gens* g, const uint32_t* d_v, const uint32_t* d_gam, size_t m,
-                 uint32_t* d_out_enc, uint32_t* d_out_p3) {
+                 uint32_t* d_out_enc, uint32_t* d_out_p3, uint64_t v_bound) {
   if (!m) return BPP_OK;
   uint32_t* p3 = d_out_p3;
   if (!p3) {
@@ -180,8 +186,16 @@ int pedersen_dev(bpp_ctx* ctx, const bpp_gens* g, const uint32_t* d_v, const uin
   // compete in L2 with the concurrent direct-table MSMs, while this kernel's
   // 128 KB radix-16 table stays resident)
   const uint32_t G = m <= 2048 ? 32 : 8;
+  // group 0 (P = FB_POS / G nibble positions) carries every v of the bound
+  // when v + 8 (16^P - 1) / 15 (the recoding offset K's low P nibbles) does
+  // not carry out of it: v < (7 16^P + 8) / 15 (2004318072 at P = 8, 120 at
+  // P = 2); nibble 63's top digit never sits in group 0
+  const uint32_t PG = FB_POS / G;
+  const uint64_t v_lim = PG < 16 ? (7 * (1ull << (4 * PG)) + 8) / 15 : 0;
+  const uint32_t v_groups = v_bound && v_bound <= v_lim ? 1u : G;
   ctx_work(ctx, "msm_terms", 2 * (uint64_t)m);
-  ctx_work(ctx, "madds", 2 * (uint64_t)FB_POS * m);  // constant time: every position of both scalars
+  // constant time: every position of gamma, every possible position of v
+  ctx_work(ctx, "madds", (uint64_t)(FB_POS + FB_POS / G * v_groups) * m);
   ctx_work(ctx, "padds", (uint64_t)(G - 1) * m);
   ctx_work(ctx, "msm_launches", 1);
   void* part = nullptr;
@@ -190,12 +204,12 @@ int pedersen_dev(bpp_ctx* ctx, const bpp_gens* g, const uint32_t* d_v, const uin
     ProfScope ps(ctx, "pedersen");
     if (G == 32) {
       hipLaunchKernelGGL(k_pedersen<32>, dim3(grid_for(m, PED_T), 32), dim3(PED_T), 0, ctx->stream, g->d_fb, d_v,
-                         d_gam, m, (uint32_t*)part);
+                         d_gam, m, v_groups, (uint32_t*)part);
       hipLaunchKernelGGL(k_pedersen_sum<32>, dim3(grid_for(m * 32, 256)), dim3(256), 0, ctx->stream,
                          (const uint32_t*)part, m, p3);
     } else {
       hipLaunchKernelGGL(k_pedersen<8>, dim3(grid_for(m, PED_T), 8), dim3(PED_T), 0, ctx->stream, g->d_fb, d_v,
-                         d_gam, m, (uint32_t*)part);
+                         d_gam, m, v_groups, (uint32_t*)part);
       hipLaunchKernelGGL(k_pedersen_sum<8>, dim3(grid_for(m * 8, 256)), dim3(256), 0, ctx->stream,
                          (const uint32_t*)part, m, p3);
     }

@@ -29,6 +29,8 @@ int points_compress_p3_dev(bpp_ctx* ctx, const uint32_t* d_p3, size_t n, uint8_t
 int points_double_encode_p3(bpp_ctx* ctx, const uint32_t* d_p3, size_t n, uint8_t* out_host);
 // d_out[i] = d_in[i] / 2 mod l (canonical scalars; in place allowed)
 int sc_halve_dev(bpp_ctx* ctx, const uint32_t* d_in, uint32_t* d_out, size_t n);
+// d_out[t] = d_in[d_map[t]] / 2 for t < n
+int sc_halve_gather_dev(bpp_ctx* ctx, const uint32_t* d_in, const uint32_t* d_map, uint32_t* d_out, size_t n);
 #include <vector>
 // Fixed-base window tables: entry k*FBW_W + w = 2^(FBW_C*w) * P_k (affine
 // Niels).  An MSM over such points needs no per-window Horner combine: all

@@ -184,7 +184,12 @@ int msm_terms(bpp_ctx* ctx, const std::vector<Sc>& sc, const std::vector<uint32_
 // size neither allocates nor zero-fills; every element is written before use).
 struct ProverScratch {
   std::vector<Enc32> V;
-  std::vector<uint32_t> idx;
+  // A_I/A_O/S MSM terms without the zero padding gates (a_L, a_R, a_O of
+  // gates 2k..n_p-1): generator index and source slot in the [P][per]
+  // scalar array per term, rebuilt when (P, k) changes
+  std::vector<uint32_t> idx, map, off;
+  size_t key_P = 0;
+  uint32_t key_k = 0;
 };
 
 struct ProverState {
@@ -286,7 +291,9 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     BPP_TRY(v_inputs_dev(ctx, C, (uint32_t)P, d_pi, d_gamma, (uint32_t*)dv, (uint32_t*)dg, d_gx_half));
     {
       HostScope hk(ctx, "ped_kernels");
-      BPP_TRY(pedersen_dev(ctx, G, (const uint32_t*)dv, (const uint32_t*)dg, nv, (uint32_t*)denc, nullptr));
+      // (values 1..k and pi + 1 <= k: the public bound k + 1)
+      BPP_TRY(pedersen_dev(ctx, G, (const uint32_t*)dv, (const uint32_t*)dg, nv, (uint32_t*)denc, nullptr,
+                           (uint64_t)k + 1));
     }
     std::vector<Enc32>& V = scr.V;
     V.resize(nv);
@@ -340,20 +347,49 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
   }
   MsmPoints pts;
   BPP_TRY(gens_points(ctx, G, &pts));
-  // A_I, A_O, S of every proof: one batch of 3P MSMs.  The host writes the
-  // first 3 + 3 n_p scalars of each proof (alpha, a_L, a_R, beta, a_O, rho)
-  // into the device array whose s_L / s_R slots k_draws_reduce filled.
+  // A_I, A_O, S of every proof: one batch of 3P MSMs over the [P][per]
+  // scalar array that k_draws_reduce (alpha, beta, rho, s_L, s_R) and
+  // k_witness (a_L, a_R, a_O) filled -- or, beyond the device witness's
+  // size, the host writes its first 3 + 3 n_p scalars.  The MSMs skip the
+  // padding gates' zero a_L, a_R, a_O (11 % of the terms at k = 52).
   hs.reset(new HostScope(ctx, "pb_msm_AI_AO_S"));
   {
     const uint32_t hostw = 3 + 3 * n_p;  // host-written scalars per proof
-    std::vector<uint32_t>& idx = scr.idx;
-    idx.resize((size_t)P * per);
-    std::vector<uint32_t> off(3 * P + 1);
+    std::vector<uint32_t>&idx = scr.idx, &map = scr.map, &off = scr.off;
+    const uint32_t n = C.n;                       // real gates; n_p - n padding gates are zero
+    const uint32_t per_c = 3 + 3 * n + 2 * n_p;  // MSM terms per proof
+    if (scr.key_P != P || scr.key_k != k) {
+      idx.resize((size_t)P * per_c);
+      map.resize((size_t)P * per_c);
+      off.resize(3 * P + 1);
+      for (size_t p = 0; p < P; ++p) {
+        size_t t = p * per_c;
+        const uint32_t b = (uint32_t)(p * per);
+        auto term = [&](uint32_t src, uint32_t gen) {
+          map[t] = b + src;
+          idx[t++] = gen;
+        };
+        off[3 * p] = (uint32_t)t;
+        term(0, G->bbidx());                                                  // alpha
+        for (uint32_t i = 0; i < n; ++i) term(1 + i, G->gidx(i));             // a_L
+        for (uint32_t i = 0; i < n; ++i) term(1 + n_p + i, G->hidx(i));       // a_R
+        off[3 * p + 1] = (uint32_t)t;
+        term(1 + 2 * n_p, G->bbidx());                                        // beta
+        for (uint32_t i = 0; i < n; ++i) term(2 + 2 * n_p + i, G->gidx(i));   // a_O
+        off[3 * p + 2] = (uint32_t)t;
+        term(2 + 3 * n_p, G->bbidx());                                        // rho
+        for (uint32_t i = 0; i < n_p; ++i) term(3 + 3 * n_p + i, G->gidx(i));  // s_L
+        for (uint32_t i = 0; i < n_p; ++i) term(3 + 4 * n_p + i, G->hidx(i));  // s_R
+      }
+      off[3 * P] = (uint32_t)(P * per_c);
+      scr.key_P = P;
+      scr.key_k = k;
+    }
     uint8_t* stg = nullptr;  // (host witness only) written in place in the pinned arena
-    if (!dev_witness) BPP_TRY(ctx_h2d_stage(ctx, (size_t)P * hostw * 32, &stg));
-    par::for_each(P, [&](size_t p) {
-      ProverState& st = *S[p];
-      if (!dev_witness) {
+    if (!dev_witness) {
+      BPP_TRY(ctx_h2d_stage(ctx, (size_t)P * hostw * 32, &stg));
+      par::for_each(P, [&](size_t p) {
+        ProverState& st = *S[p];
         Sc* o = reinterpret_cast<Sc*>(stg) + p * hostw;
         o[0] = st.d.alpha;
         std::copy(st.aL.begin(), st.aL.begin() + n_p, o + 1);
@@ -361,34 +397,19 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
         o[1 + 2 * n_p] = st.d.beta;
         std::copy(st.aO.begin(), st.aO.begin() + n_p, o + 2 + 2 * n_p);
         o[2 + 3 * n_p] = st.d.rho;
-      }
-      uint32_t* ix = &idx[p * per];
-      size_t t = 0;
-      ix[t++] = G->bbidx();
-      for (uint32_t i = 0; i < n_p; ++i) ix[t++] = G->gidx(i);
-      for (uint32_t i = 0; i < n_p; ++i) ix[t++] = G->hidx(i);
-      ix[t++] = G->bbidx();
-      for (uint32_t i = 0; i < n_p; ++i) ix[t++] = G->gidx(i);
-      ix[t++] = G->bbidx();
-      for (uint32_t i = 0; i < n_p; ++i) ix[t++] = G->gidx(i);
-      for (uint32_t i = 0; i < n_p; ++i) ix[t++] = G->hidx(i);
-    });
-    for (size_t p = 0; p < P; ++p) {
-      off[3 * p] = (uint32_t)(p * per);
-      off[3 * p + 1] = (uint32_t)(p * per + 1 + 2 * n_p);
-      off[3 * p + 2] = (uint32_t)(p * per + 2 + 3 * n_p);
-    }
-    off[3 * P] = (uint32_t)(P * per);
-    if (!dev_witness)
+      });
       BPP_HIP(hipMemcpy2DAsync(d_s, (size_t)per * 32, stg, (size_t)hostw * 32, (size_t)hostw * 32, P,
                                hipMemcpyHostToDevice, ctx->stream));
-    void* d_i = nullptr;
+    }
+    void *d_i = nullptr, *d_map = nullptr;
     BPP_TRY(ctx_ws(ctx, "mt_i", idx.size() * 4 + 4, &d_i));
     BPP_TRY(ctx_h2d_const(ctx, "mt_i", d_i, idx.data(), idx.size() * 4));  // generator indices: same every batch
-    // MSMs of the halved scalars, encoded as 2 * result (msm_multi_enc)
+    BPP_TRY(ctx_ws(ctx, "mt_map", map.size() * 4 + 4, &d_map));
+    BPP_TRY(ctx_h2d_const(ctx, "mt_map", d_map, map.data(), map.size() * 4));
+    // MSMs of the halved, compacted scalars, encoded as 2 * result (msm_multi_enc)
     void* d_sh = nullptr;
-    BPP_TRY(ctx_ws(ctx, "mt_s_half", (size_t)P * per * 32 + 32, &d_sh));
-    BPP_TRY(sc_halve_dev(ctx, d_s, (uint32_t*)d_sh, (size_t)P * per));
+    BPP_TRY(ctx_ws(ctx, "mt_s_half", map.size() * 32 + 32, &d_sh));
+    BPP_TRY(sc_halve_gather_dev(ctx, d_s, (const uint32_t*)d_map, (uint32_t*)d_sh, map.size()));
     std::vector<uint8_t> enc(3 * P * 32);
     BPP_TRY(msm_multi_enc(ctx, (const uint32_t*)d_sh, (const uint32_t*)d_i, off, pts, enc.data(), true));
     par::for_each(P, [&](size_t p) {
@@ -397,8 +418,8 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
       memcpy(Ps[p].S.data(), &enc[96 * p + 64], 32);
     });
   }
-  // challenges y, z (host transcripts), then the t(X) coefficients of every
-  // proof in one device launch (poly.hip); z^Q W_V stays on the host for tau_x
+  // challenges y, z (host transcripts), then the t(X) coefficients and
+  // tau_x's <z^Q W_V, gamma> of every proof in one device launch (poly.hip)
   hs.reset(new HostScope(ctx, "pb_host_poly"));
   std::vector<Sc> zwvg(P);  // <z^Q W_V, gamma> per proof (k_poly_coef)
   {

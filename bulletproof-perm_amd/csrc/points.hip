@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "ctx.h"
+#include "sc25519.cuh"
 #include "host/fe64.h"
 #include "host/par.h"
 #include "ge_io.cuh"
@@ -125,6 +126,21 @@ __global__ void __launch_bounds__(256) k_sc_halve(const uint32_t* __restrict__ i
   _Pragma("unroll") for (int k = 0; k < 7; ++k) s[k] = (s[k] >> 1) | (s[k + 1] << 31);
   s[7] >>= 1;  // s + l < 2^254: no carry out
   _Pragma("unroll") for (int k = 0; k < 8; ++k) out[8 * i + k] = s[k];
+}
+
+// out[t] = in[map[t]] / 2: halving with a gather (drops terms known to be zero)
+__global__ void __launch_bounds__(256) k_sc_halve_gather(const uint32_t* __restrict__ in,
+                                                        const uint32_t* __restrict__ map, uint32_t* __restrict__ out,
+                                                        size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  sc_store(out + 8 * i, sc_half(sc_load(in + 8 * (size_t)map[i])));
+}
+
+int sc_halve_gather_dev(bpp_ctx* ctx, const uint32_t* d_in, const uint32_t* d_map, uint32_t* d_out, size_t n) {
+  if (!n) return BPP_OK;
+  hipLaunchKernelGGL(k_sc_halve_gather, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, d_in, d_map, d_out, n);
+  return ctx_check_launch(ctx, "k_sc_halve_gather");
 }
 
 int sc_halve_dev(bpp_ctx* ctx, const uint32_t* d_in, uint32_t* d_out, size_t n) {

@@ -304,6 +304,10 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
                                       })
                             : ge_identity();
   __syncthreads();
+#ifdef EXP_IPA_NOTREE  // timing experiment only (wrong results): no block tree
+  if (tid == 0) store_p3(out_p3, blockIdx.x, acc);
+  return;
+#endif
   dt_block_tree(lds, acc, nt, out_p3, blockIdx.x);
 }
 

@@ -137,16 +137,77 @@ FE_INLINE ge_p3 lds_load_p3(const uint32_t* tl, uint32_t nslots, uint32_t j) {
   return r;
 }
 
-// Block tree in LDS (tl: blockDim.x extended points) whose waves retire as it
-// narrows; lane 0 writes the block's sum to out_p3[m].
+// Quad exchange: lane l reads lane (l & ~3) | ((l & 3) ^ X) of its own quad
+// (DPP quad_perm, no LDS round trip).
+template <int X>
+FE_INLINE fe fe_quad_xor(const fe& a) {
+  constexpr int ctrl = ((0 ^ X) << 0) | ((1 ^ X) << 2) | ((2 ^ X) << 4) | ((3 ^ X) << 6);
+  fe r;
+  _Pragma("unroll") for (int i = 0; i < FE_LIMBS; ++i) r.v[i] =
+      (uint32_t)__builtin_amdgcn_mov_dpp((int)a.v[i], ctrl, 0xf, 0xf, false);
+  return r;
+}
+FE_INLINE fe fe_pick(bool c, const fe& a, const fe& b) {
+  fe r;
+  _Pragma("unroll") for (int i = 0; i < FE_LIMBS; ++i) r.v[i] = c ? a.v[i] : b.v[i];
+  return r;
+}
+
+// p + q by the four lanes of a quad, lane c = lane & 3 returning coordinate c
+// (X, Y, Z, T) of the sum.  ge_add's nine multiplies are two rounds of four
+// independent products plus 2d * T1T2: lane c forms product c of the first
+// round (A = (Y1-X1)(Y2-X2), B = (Y1+X1)(Y2+X2), T1 T2, Z1 Z2), DPP hands each
+// lane the other three, every lane forms C = 2d T1T2 and E, F, G, H, and lane
+// c forms product c of the second round (EF, GH, GF, EH).  A wave spends 3
+// multiplies per addition instead of 9, with every lane on the same
+// instruction stream (the operands are selected, not branched on).  The
+// formulas and their bounds are ge_add_cached's.
+FE_INLINE fe ge_add_quad(const ge_p3& p, const ge_p3& q, uint32_t c) {
+  const fe a0 = fe_pick(c == 0, fe_sub_nc(p.Y, p.X), fe_pick(c == 1, fe_add_nc(p.Y, p.X), fe_pick(c == 2, p.T, p.Z)));
+  const fe b0 = fe_pick(c == 0, fe_sub_nc(q.Y, q.X), fe_pick(c == 1, fe_add_nc(q.Y, q.X), fe_pick(c == 2, q.T, q.Z)));
+  const fe m0 = fe_mul(a0, b0);
+  const fe m1 = fe_quad_xor<1>(m0), m2 = fe_quad_xor<2>(m0), m3 = fe_quad_xor<3>(m0);
+  // product of lane t = the exchange with lane distance t ^ c
+  auto prod = [&](uint32_t t) {
+    const uint32_t d = t ^ c;
+    return fe_pick(d == 0, m0, fe_pick(d == 1, m1, fe_pick(d == 2, m2, m3)));
+  };
+  const fe A = prod(0), B = prod(1), ZZ = prod(3);
+  const fe C = fe_mul(prod(2), fe_const(FE_D2));
+  const fe D = fe_add_nc(ZZ, ZZ);
+  const fe E = fe_sub_nc(B, A), F = fe_sub(D, C), G = fe_add_nc(D, C), H = fe_add_nc(B, A);
+  return fe_mul(fe_pick(c == 0 || c == 3, E, G), fe_pick(c == 0 || c == 2, F, H));
+}
+
+// Coordinate c (10 words) of slot j in lds_store_p3's layout.
+FE_INLINE void lds_store_coord(uint32_t* tl, uint32_t nslots, uint32_t j, uint32_t c, const fe& v) {
+  _Pragma("unroll") for (int i = 0; i < FE_LIMBS; ++i) {
+    const uint32_t w = 10 * c + i;
+    tl[((w >> 2) * nslots + j) * 4 + (w & 3)] = v.v[i];
+  }
+}
+
+// Block tree in LDS (tl: blockDim.x extended points); lane 0 writes the
+// block's sum to out_p3[m].  A level of s additions runs one lane per
+// addition while 4 s exceeds the block, then four lanes per addition
+// (ge_add_quad): a narrow level's latency is one wave's instruction stream,
+// which the quads cut by ~3x (the 8-level tree was ~29 us of each 80-us IPA
+// round at 256 lanes, measured with EXP_IPA_NOTREE).
 FE_INLINE void dt_block_tree(uint32_t* tl, const ge_p3& acc, uint32_t nt, uint32_t* __restrict__ out_p3, uint32_t m) {
   lds_store_p3(tl, nt, threadIdx.x, acc);
   __syncthreads();
   uint32_t p2 = 1;
   while (p2 < nt) p2 <<= 1;
   for (uint32_t s = p2 >> 1; s > 0; s >>= 1) {
-    if (threadIdx.x < s && threadIdx.x + s < nt)
-      lds_store_p3(tl, nt, threadIdx.x, ge_add(lds_load_p3(tl, nt, threadIdx.x), lds_load_p3(tl, nt, threadIdx.x + s)));
+    if (4 * s > nt) {
+      if (threadIdx.x < s && threadIdx.x + s < nt)
+        lds_store_p3(tl, nt, threadIdx.x, ge_add(lds_load_p3(tl, nt, threadIdx.x), lds_load_p3(tl, nt, threadIdx.x + s)));
+    } else if ((threadIdx.x & ~63u) < 4 * s) {  // wave-uniform: whole waves run the DPP exchange
+      const uint32_t j = threadIdx.x >> 2, c = threadIdx.x & 3;
+      const bool live = j < s && j + s < nt;
+      const fe r = ge_add_quad(lds_load_p3(tl, nt, live ? j : 0), lds_load_p3(tl, nt, live ? j + s : 0), c);
+      if (live) lds_store_coord(tl, nt, j, c, r);
+    }
     __syncthreads();
   }
   if (threadIdx.x == 0) store_p3(out_p3, m, lds_load_p3(tl, nt, 0));

@@ -205,6 +205,8 @@ __global__ void __launch_bounds__(256) k_ipa_fold(uint32_t n, uint32_t lg_n, uin
 //      on the GPU).
 // One launch per round instead of four: the latency of three small kernels
 // and their passes over the [P][n] arrays leave every round of a batch.
+// (512-lane blocks, half the walk per lane: 73.9 vs 70.8 us per round -- a
+// lone wave per SIMD already issues the walk at its rate)
 __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
     const uint32_t* __restrict__ dt, DtGeom dg, uint32_t n, uint32_t m, uint32_t lg_h, uint32_t fold,
     const uint32_t* __restrict__ am_in, const uint32_t* __restrict__ bm_in, const uint32_t* __restrict__ fG_in,
@@ -217,7 +219,7 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
   uint32_t* tgen = lds + 8 * (n + 1);            // n + 1 generator indices
   uint32_t* sa = tgen + ((n + 1 + 3) & ~3u);     // m x 8: a (Montgomery), this round
   uint32_t* sb = sa + 8 * m;                     // m x 8: b
-  uint32_t* red = sb + 8 * m;                    // 4 waves x 8 words
+  uint32_t* red = sb + 8 * m;                    // waves x 8 words
   const uint32_t nt = blockDim.x, tid = threadIdx.x;
   const uint32_t inst = blockIdx.x >> 1, side = blockIdx.x & 1u;
   const size_t ib = (size_t)inst * n;
@@ -227,50 +229,46 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
     um = sc_load(u + 16 * inst);
     uim = sc_load(u + 16 * inst + 8);
   }
-  // 1. a, b of this round (length m) into LDS
-  for (uint32_t p = tid; p < m; p += nt) {
-    sc a, b;
+  // 1. a, b of this round (length m) into LDS: item q < m is a_q, q >= m is
+  // b_{q-m} (one vector per lane, so a fold costs a lane two multiplies, not
+  // four, while 2 m <= blockDim)
+  for (uint32_t q = tid; q < 2 * m; q += nt) {
+    const bool isb = q >= m;
+    const uint32_t p = isb ? q - m : q;
+    const uint32_t* in = isb ? bm_in : am_in;
+    sc x;
     if (fold) {  // G' = u^-1 G_lo + u G_hi: a' = a_lo u + a_hi u^-1, b' = b_lo u^-1 + b_hi u
-      a = sc_add(sc_mont(sc_load(am_in + 8 * (ib + p)), um), sc_mont(sc_load(am_in + 8 * (ib + p + m)), uim));
-      b = sc_add(sc_mont(sc_load(bm_in + 8 * (ib + p)), uim), sc_mont(sc_load(bm_in + 8 * (ib + p + m)), um));
-      if (writer) {
-        sc_store(am_out + 8 * (ib + p), a);
-        sc_store(bm_out + 8 * (ib + p), b);
-      }
+      x = sc_add(sc_mont(sc_load(in + 8 * (ib + p)), isb ? uim : um),
+                 sc_mont(sc_load(in + 8 * (ib + p + m)), isb ? um : uim));
+      if (writer) sc_store((isb ? bm_out : am_out) + 8 * (ib + p), x);
     } else {
-      a = sc_load(am_in + 8 * (ib + p));
-      b = sc_load(bm_in + 8 * (ib + p));
+      x = sc_load(in + 8 * (ib + p));
     }
-    sc_store(sa + 8 * p, a);
-    sc_store(sb + 8 * p, b);
+    sc_store((isb ? sb : sa) + 8 * p, x);
   }
   __syncthreads();
   // 2. term scalars: every k gives one G term and one H term, to this side
-  // or the other
+  // or the other; item q < n is G_k, q >= n is H_{q-n}
   const uint32_t h = m >> 1;
-  for (uint32_t k = tid; k < n; k += nt) {
-    sc fg = sc_load(fG_in + 8 * (ib + k)), fh = sc_load(fH_in + 8 * (ib + k));
+  for (uint32_t q = tid; q < 2 * n; q += nt) {
+    const bool ish = q >= n;
+    const uint32_t k = ish ? q - n : q;
+    sc f = sc_load((ish ? fH_in : fG_in) + 8 * (ib + k));
     if (fold) {
       const bool hi_prev = (k & (2 * m - 1)) & m;
-      fg = sc_mont(fg, hi_prev ? um : uim);
-      fh = sc_mont(fh, hi_prev ? uim : um);
-      if (writer) {
-        sc_store(fG_out + 8 * (ib + k), fg);
-        sc_store(fH_out + 8 * (ib + k), fh);
-      }
+      f = sc_mont(f, hi_prev != ish ? um : uim);
+      if (writer) sc_store((ish ? fH_out : fG_out) + 8 * (ib + k), f);
     }
     const uint32_t r = k & (m - 1);
     const bool hi = (r & h) != 0;
-    const uint32_t p = r ^ h;
-    const uint32_t cidx = ((k >> (lg_h + 1)) << lg_h) | (k & (h - 1));
-    if (hi == (side == 0)) {
-      const sc x = sc_mont(sc_load(sa + 8 * p), fg);
-      sc_store(tsc + 8 * cidx, halve ? sc_half(x) : x);
-      tgen[cidx] = gbase + k;
-    } else {
-      const sc x = sc_mont(sc_load(sb + 8 * p), fh);
-      sc_store(tsc + 8 * ((n >> 1) + cidx), halve ? sc_half(x) : x);
-      tgen[(n >> 1) + cidx] = hbase + k;
+    // G_k's term is on side 0 (L) for hi k, H_k's on side 0 for lo k
+    if ((hi == (side == 0)) != ish) {
+      const uint32_t p = r ^ h;
+      const uint32_t cidx = ((k >> (lg_h + 1)) << lg_h) | (k & (h - 1));
+      const sc x = sc_mont(sc_load((ish ? sb : sa) + 8 * p), f);
+      const uint32_t slot = (ish ? (n >> 1) : 0) + cidx;
+      sc_store(tsc + 8 * slot, halve ? sc_half(x) : x);
+      tgen[slot] = (ish ? hbase : gbase) + k;
     }
   }
   // c_L = <a_lo, b_hi> (L) or c_R = <a_hi, b_lo> (R), Montgomery form
@@ -314,7 +312,7 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
 // LDS words of k_ipa_round_dt: terms + indices + a, b + wave partials, or
 // the block tree, whichever is larger
 static size_t ipa_round_lds_words(uint32_t n, uint32_t nt) {
-  const size_t prologue = 8 * (size_t)(n + 1) + ((n + 1 + 3) & ~3u) + 16 * (size_t)n + 32;
+  const size_t prologue = 8 * (size_t)(n + 1) + ((n + 1 + 3) & ~3u) + 16 * (size_t)n + 8 * ((nt + 63) / 64);
   return std::max(prologue, (size_t)nt * P3_WORDS);
 }
 

@@ -7,5 +7,5 @@ TAG=$1; shift
 for v in "$@"; do
   if [ "$v" = default ]; then lib=""; else lib="bulletproof-perm_amd/bpperm/variants/libbpperm_$v.so"; fi
   BPP_LIB=$lib timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/$TAG/$v -o run --output-format csv -- python3 tools/prove_batch_once.py 128 > gpurun_out/$TAG/$v.log 2>&1 || { echo "trace $v failed"; exit 1; }
-  echo "== $v"; python3 tools/kstats.py gpurun_out/$TAG/$v/run_kernel_stats.csv | head -14
+  echo "== $v"; python3 tools/kstats.py -n 16 gpurun_out/$TAG/$v/run_kernel_stats.csv
 done

@@ -44,6 +44,59 @@ FE_INLINE sc sc_pow_small(const sc& aR, uint32_t e, const sc& oneR) {
   return r;
 }
 
+// Doubling tables in LDS (every lane calls; ends with a barrier).  Table t
+// holds N_t >= 1 entries tab[e] = prod over the set bits b of e of f_b
+// (Montgomery), from tab[0] = 1 and either tab[1] = x (powers, f_b = x^(2^b);
+// pre = false) or every tab[2^b] = f_b written by the caller (pre = true);
+// the step for s = 1, 2, 4, ... fills (s, 2s], or (s, 2s) when preloaded, as
+// tab[e - s] tab[s] (e - s < s shares no bit with s).  A table costs log2(N)
+// dependent multiplies where sc_pow_small spends up to 2 log2(N) on each
+// entry, and all tables advance in the same steps.
+struct ScTable {
+  uint32_t* tab;
+  uint32_t N;
+  bool pre;
+};
+template <int T>
+FE_INLINE void sc_tables(const ScTable (&tb)[T]) {
+  uint32_t nmax = 0;
+  _Pragma("unroll") for (int t = 0; t < T; ++t) nmax = max(nmax, tb[t].N);
+  __syncthreads();  // the caller's preloads
+  for (uint32_t s = 1; s + 1 < nmax; s <<= 1) {
+    uint32_t cnt[T], tot = 0;
+    _Pragma("unroll") for (int t = 0; t < T; ++t) {
+      const uint32_t hi = min(2 * s - (tb[t].pre ? 1u : 0u), tb[t].N - 1);
+      cnt[t] = hi > s ? hi - s : 0;
+      tot += cnt[t];
+    }
+    for (uint32_t u = threadIdx.x; u < tot; u += blockDim.x) {
+      uint32_t off = u, t = 0;
+      _Pragma("unroll") for (int k = 0; k + 1 < T; ++k) if (t == (uint32_t)k && off >= cnt[k]) {
+          off -= cnt[k];
+          t = k + 1;
+        }
+      uint32_t* tab = tb[0].tab;
+      _Pragma("unroll") for (int k = 1; k < T; ++k) tab = t == (uint32_t)k ? tb[k].tab : tab;
+      const uint32_t e = s + 1 + off;
+      sc_store(tab + 8 * e, sc_mont(sc_load(tab + 8 * (e - s)), sc_load(tab + 8 * s)));
+    }
+    __syncthreads();
+  }
+}
+
+// Power-table preload (one lane): tab[0] = 1, tab[1] = x
+FE_INLINE void sc_table_pow_init(uint32_t* tab, uint32_t N, const sc& xR, const sc& oneR) {
+  sc_store(tab, oneR);
+  if (N > 1) sc_store(tab + 8, xR);
+}
+
+// Gates beyond the first POW_LO: lane tid handles gate i = tid + POW_LO r
+// (blockDim = POLY_T = POW_LO whenever n_p > POW_LO), so x^i = tab[tid]
+// (x^POW_LO)^r with the second factor kept as a running product
+#define POW_LO POLY_T
+#define POW_LO_LG 8
+static_assert(POW_LO == 1 << POW_LO_LG, "POW_LO");
+
 // Sum over the workgroup of K Montgomery scalars per lane; valid in lane 0.
 template <int K>
 FE_INLINE void sc_block_sum(sc (&v)[K], uint32_t* lds) {
@@ -83,7 +136,7 @@ FE_INLINE sc col_sum_block(const uint32_t* __restrict__ cp, const uint32_t* __re
   return v[0];
 }
 
-// grid = P proofs, block = poly_block(max(n_p, m)); dynamic LDS = Q * 32 + (POLY_T / 64) * 7 * 32
+// grid = P proofs, block = poly_block(max(n_p, m)); dynamic LDS = (Q + 1 + 2 min(n_p, POW_LO)) * 32 + (POLY_T / 64) * 7 * 32
 // t_out[p] = t_1..t_6, <z^Q W_V, gamma_p> (gamma: [P][m] canonical)
 #define POLY_NT 7
 __global__ void __launch_bounds__(POLY_T) k_poly_coef(uint32_t n_p, uint32_t m, uint32_t Q, uint32_t per,
@@ -93,14 +146,27 @@ __global__ void __launch_bounds__(POLY_T) k_poly_coef(uint32_t n_p, uint32_t m, 
                                                    const uint32_t* __restrict__ gamma, uint32_t* __restrict__ vec,
                                                    uint32_t* __restrict__ hf, uint32_t* __restrict__ t_out) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  uint32_t* zp = lds;           // [Q] z^(q+1)
-  uint32_t* red = lds + 8 * Q;  // reduction scratch
+  const uint32_t NY = min(n_p, (uint32_t)POW_LO);
+  uint32_t* zt = lds;               // [Q + 1] z^e
+  uint32_t* yt = zt + 8 * (Q + 1);  // [NY] y^i
+  uint32_t* yit = yt + 8 * NY;      // [NY] y^-i
+  uint32_t* red = yit + 8 * NY;     // reduction scratch
+  const uint32_t* zp = zt + 8;      // z^(q+1)
   const uint32_t p = blockIdx.x;
   const sc oneR = sc_one_mont();
   const sc yR = sc_to_mont(sc_load(ch + 24 * p)), yiR = sc_to_mont(sc_load(ch + 24 * p + 8)),
            zR = sc_to_mont(sc_load(ch + 24 * p + 16));
-  for (uint32_t q = threadIdx.x; q < Q; q += blockDim.x) sc_store(zp + 8 * q, sc_pow_small(zR, q + 1, oneR));
-  __syncthreads();
+  if (threadIdx.x == 0) {
+    sc_table_pow_init(zt, Q + 1, zR, oneR);
+    sc_table_pow_init(yt, NY, yR, oneR);
+    sc_table_pow_init(yit, NY, yiR, oneR);
+  }
+  sc_tables<3>({{zt, Q + 1, false}, {yt, NY, false}, {yit, NY, false}});
+  sc yhi = oneR, yihi = oneR, ystep = oneR, yistep = oneR;  // (y^POW_LO)^r
+  if (n_p > POW_LO) {
+    ystep = sc_mont(sc_load(yt + 8 * (POW_LO - 1)), yR);
+    yistep = sc_mont(sc_load(yit + 8 * (POW_LO - 1)), yiR);
+  }
   sc t[POLY_NT];
   _Pragma("unroll") for (int j = 0; j < POLY_NT; ++j) t[j] = sc_zero();
   for (uint32_t i = threadIdx.x; i < n_p; i += blockDim.x) {
@@ -110,7 +176,15 @@ __global__ void __launch_bounds__(POLY_T) k_poly_coef(uint32_t n_p, uint32_t m, 
     const sc l2 = sc_to_mont(sc_load(s + 8 * (2 + 2 * n_p + i)));  // a_O
     const sc l3 = sc_to_mont(sc_load(s + 8 * (3 + 3 * n_p + i)));  // s_L
     const sc sR = sc_to_mont(sc_load(s + 8 * (3 + 4 * n_p + i)));
-    const sc yp = sc_pow_small(yR, i, oneR), yip = sc_pow_small(yiR, i, oneR);
+    sc yp = sc_load(yt + 8 * (i % POW_LO)), yip = sc_load(yit + 8 * (i % POW_LO));
+    if (i >= POW_LO) {
+      yp = sc_mont(yp, yhi);
+      yip = sc_mont(yip, yihi);
+    }
+    if (n_p > POW_LO) {
+      yhi = sc_mont(yhi, ystep);
+      yihi = sc_mont(yihi, yistep);
+    }
     const sc zWL = col_sum(cp, ce, i, zp), zWR = col_sum(cp + (n_p + 1), ce, i, zp),
              zWO = col_sum(cp + 2 * (n_p + 1), ce, i, zp);
     const sc l1 = sc_add(aL, sc_mont(zWR, yip));
@@ -139,11 +213,12 @@ __global__ void __launch_bounds__(POLY_T) k_poly_coef(uint32_t n_p, uint32_t m, 
   const uint32_t* gam = gamma + 8 * (size_t)p * m;
   for (uint32_t j = threadIdx.x; j < m; j += blockDim.x)
     if (cpv[j + 1] - cpv[j] <= HEAVY_COL) t[6] = sc_add(t[6], sc_mont(col_sum(cpv, ce, j, zp), sc_to_mont(sc_load(gam + 8 * j))));
-  for (uint32_t j = 0; j < m; ++j)  // (uniform: every lane reads the same offsets)
-    if (cpv[j + 1] - cpv[j] > HEAVY_COL) {
-      const sc cs = col_sum_block(cpv, ce, j, zp, red);
-      if (threadIdx.x == 0) t[6] = sc_add(t[6], sc_mont(cs, sc_to_mont(sc_load(gam + 8 * j))));
-    }
+  const uint32_t* heavy = cpv + m + 1;  // [count, columns...] (build_csr)
+  for (uint32_t h = 0; h < heavy[0]; ++h) {
+    const uint32_t j = heavy[1 + h];
+    const sc cs = col_sum_block(cpv, ce, j, zp, red);
+    if (threadIdx.x == 0) t[6] = sc_add(t[6], sc_mont(cs, sc_to_mont(sc_load(gam + 8 * j))));
+  }
   sc_block_sum<POLY_NT>(t, red);
   if (threadIdx.x == 0)
     _Pragma("unroll") for (int j = 0; j < POLY_NT; ++j) sc_store(t_out + (POLY_NT * p + j) * 8, sc_from_mont(t[j]));
@@ -198,38 +273,56 @@ __global__ void __launch_bounds__(POLY_T) k_verify_scalars(
     const uint32_t* __restrict__ cp, const uint32_t* __restrict__ ce, const uint32_t* __restrict__ cR,
     uint32_t* __restrict__ gen, uint32_t* __restrict__ sc_out, uint32_t NG, uint32_t npt) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  uint32_t* zp = lds;           // [Q] z^(q+1), Montgomery
-  uint32_t* red = lds + 8 * Q;  // reduction scratch
+  const uint32_t NY = min(n_p, (uint32_t)POW_LO);
+  uint32_t* zt = lds;                // [Q + 1] z^e, Montgomery
+  uint32_t* yit = zt + 8 * (Q + 1);  // [NY] y^-i
+  uint32_t* st = yit + 8 * NY;       // [NY] s_i / s_0 (below)
+  uint32_t* red = st + 8 * NY;       // reduction scratch
+  const uint32_t* zp = zt + 8;       // z^(q+1)
   const uint32_t p = blockIdx.x, nrec = VREC_U + 2 * lg;
   const uint32_t* R = rec + (size_t)p * nrec * 8;
   const sc oneR = sc_one_mont();
   auto ldm = [&](uint32_t k) { return sc_to_mont(sc_load(R + 8 * k)); };
   const sc zR = ldm(VREC_Z), xR = ldm(VREC_X), yiR = ldm(VREC_YINV), aR = ldm(VREC_A), bR = ldm(VREC_B),
            wtR = ldm(VREC_WT), rR = ldm(VREC_R);
-  for (uint32_t q = threadIdx.x; q < Q; q += blockDim.x) sc_store(zp + 8 * q, sc_pow_small(zR, q + 1, oneR));
   // s_0 = prod u_j^-1; s_i = s_0 prod_{bit k of i} u_{lg-1-k}^2 (bulletproofs
-  // verification_scalars)
+  // verification_scalars): st[i] = s_i / s_0 for i < NY as a doubling table
+  // over the factors u_{lg-1-k}^2, the bits from POW_LO_LG up per lane
+  if (threadIdx.x == 0) {
+    sc_table_pow_init(zt, Q + 1, zR, oneR);
+    sc_table_pow_init(yit, NY, yiR, oneR);
+    sc_store(st, oneR);
+  }
+  for (uint32_t b = threadIdx.x; b < POW_LO_LG && (1u << b) < NY; b += blockDim.x) {
+    const sc u = ldm(VREC_U + lg - 1 - b);
+    sc_store(st + 8 * (1u << b), sc_mont(u, u));
+  }
   sc s0R = oneR;
   for (uint32_t j = 0; j < lg; ++j) s0R = sc_mont(s0R, ldm(VREC_U + lg + j));
-  __syncthreads();
-  auto s_of = [&](uint32_t i) {
-    sc v = s0R;
-    for (uint32_t k = 0; k < lg; ++k)
+  sc_tables<3>({{zt, Q + 1, false}, {yit, NY, false}, {st, NY, true}});
+  auto s_of = [&](uint32_t i) {  // s_i / s_0
+    sc v = sc_load(st + 8 * (i % POW_LO));
+    for (uint32_t k = POW_LO_LG; k < lg; ++k)
       if ((i >> k) & 1u) {
         const sc u = ldm(VREC_U + lg - 1 - k);
         v = sc_mont(v, sc_mont(u, u));
       }
     return v;
   };
+  const sc s0aR = sc_mont(s0R, aR), s0bR = sc_mont(s0R, bR);
+  sc yihi = oneR, yistep = oneR;  // (y^-POW_LO)^r, as k_poly_coef
+  if (n_p > POW_LO) yistep = sc_mont(sc_load(yit + 8 * (POW_LO - 1)), yiR);
   const size_t gb = (size_t)p * NG;
   sc acc[2] = {sc_zero(), sc_zero()};  // delta = sum y^-i zWR_i zWL_i, zc = <z^Q, c>
   for (uint32_t i = threadIdx.x; i < n_p; i += blockDim.x) {
-    const sc yi = sc_pow_small(yiR, i, oneR);
+    sc yi = sc_load(yit + 8 * (i % POW_LO));
+    if (i >= POW_LO) yi = sc_mont(yi, yihi);
+    if (n_p > POW_LO) yihi = sc_mont(yihi, yistep);
     const sc zWL = col_sum(cp, ce, i, zp), zWR = col_sum(cp + (n_p + 1), ce, i, zp),
              zWO = col_sum(cp + 2 * (n_p + 1), ce, i, zp);
     acc[0] = sc_add(acc[0], sc_mont(sc_mont(yi, zWR), zWL));
-    const sc gi = sc_sub(sc_mont(s_of(i), aR), sc_mont(sc_mont(zWR, xR), yi));
-    const sc hi = sc_add(sc_sub(sc_mont(sc_mont(s_of(n_p - 1 - i), bR), yi), sc_mont(sc_add(sc_mont(zWL, xR), zWO), yi)),
+    const sc gi = sc_sub(sc_mont(s_of(i), s0aR), sc_mont(sc_mont(zWR, xR), yi));
+    const sc hi = sc_add(sc_sub(sc_mont(sc_mont(s_of(n_p - 1 - i), s0bR), yi), sc_mont(sc_add(sc_mont(zWL, xR), zWO), yi)),
                          oneR);
     sc_store(gen + 8 * (gb + i), sc_from_mont(sc_mont(gi, wtR)));
     sc_store(gen + 8 * (gb + n_p + i), sc_from_mont(sc_mont(hi, wtR)));
@@ -247,11 +340,12 @@ __global__ void __launch_bounds__(POLY_T) k_verify_scalars(
   for (uint32_t j = threadIdx.x; j < m; j += blockDim.x)
     if (cpv[j + 1] - cpv[j] <= HEAVY_COL)
       sc_store(sc_out + 8 * (pb + j), sc_from_mont(sc_neg(sc_mont(col_sum(cpv, ce, j, zp), wrx2R))));
-  for (uint32_t j = 0; j < m; ++j)
-    if (cpv[j + 1] - cpv[j] > HEAVY_COL) {
-      const sc cs = col_sum_block(cpv, ce, j, zp, red);
-      if (threadIdx.x == 0) sc_store(sc_out + 8 * (pb + j), sc_from_mont(sc_neg(sc_mont(cs, wrx2R))));
-    }
+  const uint32_t* heavy = cpv + m + 1;  // [count, columns...] (build_csr)
+  for (uint32_t h = 0; h < heavy[0]; ++h) {
+    const uint32_t j = heavy[1 + h];
+    const sc cs = col_sum_block(cpv, ce, j, zp, red);
+    if (threadIdx.x == 0) sc_store(sc_out + 8 * (pb + j), sc_from_mont(sc_neg(sc_mont(cs, wrx2R))));
+  }
   // A_I, A_O, S: -wt x^(1,2,3); T_k: -wt r x^k (k = 1, 3..6); L_j: -wt u_j^2; R_j: -wt u_j^-2
   for (uint32_t j = threadIdx.x; j < 8 + 2 * lg; j += blockDim.x) {
     sc v;
@@ -445,7 +539,8 @@ namespace {
 
 // Column-CSR of WL, WR, WO over the n_p gate columns: cp[3][n_p + 1],
 // entries (q, valR[8]) as 9 words; with_v appends WV over its m columns at
-// cp[3 (n_p + 1)] (m + 1 offsets, the verifier's V scalars).
+// cp[3 (n_p + 1)] (m + 1 offsets, the verifier's V scalars), then the count
+// and list of its heavy columns.
 void build_csr(const perm::Circuit& C, std::vector<uint32_t>& cp, std::vector<uint32_t>& ce, bool with_v = false) {
   const uint32_t n_p = C.n_p;
   cp.assign(3 * (n_p + 1) + (with_v ? C.m + 1 : 0), 0);
@@ -468,6 +563,14 @@ void build_csr(const perm::Circuit& C, std::vector<uint32_t>& cp, std::vector<ui
     }
     cp[w * (n_p + 1) + ncol] = total;
   }
+  if (with_v) {  // then the V columns too long for one lane (col_sum_block)
+    const uint32_t* cpv = &cp[3 * (n_p + 1)];
+    std::vector<uint32_t> heavy;
+    for (uint32_t j = 0; j < C.m; ++j)
+      if (cpv[j + 1] - cpv[j] > HEAVY_COL) heavy.push_back(j);
+    cp.push_back((uint32_t)heavy.size());
+    cp.insert(cp.end(), heavy.begin(), heavy.end());
+  }
 }
 
 unsigned poly_block(uint32_t n_p) { return n_p < 64 ? 64u : (n_p > POLY_T ? POLY_T : n_p); }
@@ -489,7 +592,7 @@ int poly_coef_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint32
   BPP_TRY(ctx_h2d_const(ctx, "poly_ce", d_ce, ce.data(), ce.size() * 4));
   BPP_TRY(ctx_h2d(ctx, d_ch, ch.data(), ch.size() * 32));
   const unsigned nt = poly_block(std::max(C.n_p, C.m));
-  const size_t lds = (size_t)C.Q * 32 + (POLY_T / 64) * POLY_NT * 32;
+  const size_t lds = ((size_t)C.Q + 1 + 2 * std::min(C.n_p, (uint32_t)POW_LO)) * 32 + (POLY_T / 64) * POLY_NT * 32;
   {
     ProfScope ps(ctx, "poly_coef");
     hipLaunchKernelGGL(k_poly_coef, dim3(P), dim3(nt), lds, ctx->stream, C.n_p, C.m, C.Q, per, d_sc,
@@ -543,7 +646,7 @@ int verify_scalars_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, con
   BPP_TRY(ctx_h2d_const(ctx, "vs_c", d_c, cw.data(), cw.size() * 4));
   BPP_TRY(ctx_h2d(ctx, d_rec, rec.data(), rec.size() * 4));
   const unsigned nt = poly_block(std::max(C.n_p, C.m));
-  const size_t lds = (size_t)C.Q * 32 + (POLY_T / 64) * 2 * 32;
+  const size_t lds = ((size_t)C.Q + 1 + 2 * std::min(C.n_p, (uint32_t)POW_LO)) * 32 + (POLY_T / 64) * 2 * 32;
   {
     ProfScope ps(ctx, "verify_scalars");
     hipLaunchKernelGGL(k_verify_scalars, dim3(count), dim3(nt), lds, ctx->stream, C.n_p, C.m, C.Q, C.lg,

@@ -57,8 +57,9 @@ struct ScTable {
   uint32_t N;
   bool pre;
 };
-template <int T>
-FE_INLINE void sc_tables(const ScTable (&tb)[T]) {
+FE_INLINE void sc_tables3(const ScTable t0, const ScTable t1, const ScTable t2) {
+  constexpr int T = 3;
+  const ScTable tb[T] = {t0, t1, t2};
   uint32_t nmax = 0;
   _Pragma("unroll") for (int t = 0; t < T; ++t) nmax = max(nmax, tb[t].N);
   __syncthreads();  // the caller's preloads
@@ -161,7 +162,7 @@ __global__ void __launch_bounds__(POLY_T) k_poly_coef(uint32_t n_p, uint32_t m, 
     sc_table_pow_init(yt, NY, yR, oneR);
     sc_table_pow_init(yit, NY, yiR, oneR);
   }
-  sc_tables<3>({{zt, Q + 1, false}, {yt, NY, false}, {yit, NY, false}});
+  sc_tables3({zt, Q + 1, false}, {yt, NY, false}, {yit, NY, false});
   sc yhi = oneR, yihi = oneR, ystep = oneR, yistep = oneR;  // (y^POW_LO)^r
   if (n_p > POW_LO) {
     ystep = sc_mont(sc_load(yt + 8 * (POW_LO - 1)), yR);
@@ -185,18 +186,24 @@ __global__ void __launch_bounds__(POLY_T) k_poly_coef(uint32_t n_p, uint32_t m, 
       yhi = sc_mont(yhi, ystep);
       yihi = sc_mont(yihi, yistep);
     }
+#ifdef EXP_P_NOCS
+    const sc zWL = aL, zWR = aR, zWO = l2;
+#else
     const sc zWL = col_sum(cp, ce, i, zp), zWR = col_sum(cp + (n_p + 1), ce, i, zp),
              zWO = col_sum(cp + 2 * (n_p + 1), ce, i, zp);
+#endif
     const sc l1 = sc_add(aL, sc_mont(zWR, yip));
     const sc r0 = sc_sub(zWO, yp);
     const sc r1 = sc_add(sc_mont(aR, yp), zWL);
     const sc r3 = sc_mont(sR, yp);
+#ifndef EXP_P_NOT
     t[0] = sc_add(t[0], sc_mont(l1, r0));
     t[1] = sc_add(t[1], sc_add(sc_mont(l1, r1), sc_mont(l2, r0)));
     t[2] = sc_add(t[2], sc_add(sc_mont(l2, r1), sc_mont(l3, r0)));
     t[3] = sc_add(t[3], sc_add(sc_mont(l1, r3), sc_mont(l3, r1)));
     t[4] = sc_add(t[4], sc_mont(l2, r3));
     t[5] = sc_add(t[5], sc_mont(l3, r3));
+#endif
     uint32_t* v = vec + ((size_t)p * n_p + i) * POLY_SLOTS * 8;
     sc_store(v + 0, l1);
     sc_store(v + 8, r0);
@@ -211,6 +218,7 @@ __global__ void __launch_bounds__(POLY_T) k_poly_coef(uint32_t n_p, uint32_t m, 
   // the sum in the Montgomery domain of the other six
   const uint32_t* cpv = cp + 3 * (n_p + 1);
   const uint32_t* gam = gamma + 8 * (size_t)p * m;
+#ifndef EXP_P_NOV
   for (uint32_t j = threadIdx.x; j < m; j += blockDim.x)
     if (cpv[j + 1] - cpv[j] <= HEAVY_COL) t[6] = sc_add(t[6], sc_mont(col_sum(cpv, ce, j, zp), sc_to_mont(sc_load(gam + 8 * j))));
   const uint32_t* heavy = cpv + m + 1;  // [count, columns...] (build_csr)
@@ -219,6 +227,7 @@ __global__ void __launch_bounds__(POLY_T) k_poly_coef(uint32_t n_p, uint32_t m, 
     const sc cs = col_sum_block(cpv, ce, j, zp, red);
     if (threadIdx.x == 0) t[6] = sc_add(t[6], sc_mont(cs, sc_to_mont(sc_load(gam + 8 * j))));
   }
+#endif
   sc_block_sum<POLY_NT>(t, red);
   if (threadIdx.x == 0)
     _Pragma("unroll") for (int j = 0; j < POLY_NT; ++j) sc_store(t_out + (POLY_NT * p + j) * 8, sc_from_mont(t[j]));
@@ -299,7 +308,7 @@ __global__ void __launch_bounds__(POLY_T) k_verify_scalars(
   }
   sc s0R = oneR;
   for (uint32_t j = 0; j < lg; ++j) s0R = sc_mont(s0R, ldm(VREC_U + lg + j));
-  sc_tables<3>({{zt, Q + 1, false}, {yit, NY, false}, {st, NY, true}});
+  sc_tables3({zt, Q + 1, false}, {yit, NY, false}, {st, NY, true});
   auto s_of = [&](uint32_t i) {  // s_i / s_0
     sc v = sc_load(st + 8 * (i % POW_LO));
     for (uint32_t k = POW_LO_LG; k < lg; ++k)
@@ -417,50 +426,56 @@ __global__ void __launch_bounds__(256) k_draws_reduce(uint32_t P, uint32_t len_w
 // 2k-2 is (B[k-1], -1, -B[k-1]) and gate 2k-1 is (A[k-1] - B[k-1], 1, same);
 // padding gates are zero.  a_L, a_R, a_O go straight into the A_I/A_O/S
 // scalar array.  Prefix products: per-lane chunks, then a Hillis-Steele scan
-// of the chunk products in LDS.  dynamic LDS = (2 k + 2 blockDim) x 32 B.
+// of the chunk products in LDS.  dynamic LDS = (2 k + 4 blockDim) x 32 B.
 __global__ void __launch_bounds__(256) k_witness(uint32_t k, uint32_t n_p, uint32_t per, const uint32_t* __restrict__ pi,
                                                 const uint32_t* __restrict__ xs, uint32_t* __restrict__ sc_out) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  uint32_t* pref = lds;                 // [2][k] Montgomery prefix products (A then B)
-  uint32_t* scan = lds + 16 * k;        // [2][blockDim] chunk products
+  uint32_t* pref = lds;           // [2][k] prefix products (A then B): Montgomery, then canonical
+  uint32_t* scan = lds + 16 * k;  // [2 buffers][2][blockDim] chunk products
   const uint32_t p = blockIdx.x, nt = blockDim.x, t = threadIdx.x;
   const sc x = sc_load(xs + 8 * (size_t)p);
-  const sc oneR = sc_to_mont([] { sc o = sc_zero(); o.v[0] = 1; return o; }());
-  const uint32_t C = (k + nt - 1) / nt, i0 = t * C, i1 = min(i0 + C, k);
-  for (uint32_t c = 0; c < 2; ++c) {
-    sc run = oneR;
-    for (uint32_t i = i0; i < i1; ++i) {
-      sc v = sc_zero();
-      v.v[0] = c == 0 ? i + 1 : pi[(size_t)p * k + i] + 1;
-      run = sc_mont(run, sc_to_mont(sc_sub(v, x)));
-      sc_store(pref + 8 * (c * k + i), run);
-    }
-    sc_store(scan + 8 * (c * nt + t), run);
-  }
-  __syncthreads();
-  for (uint32_t d = 1; d < nt; d <<= 1) {  // inclusive scan of the chunk products
-    sc a[2];
-    for (uint32_t c = 0; c < 2; ++c) {
-      a[c] = sc_load(scan + 8 * (c * nt + t));
-      if (t >= d) a[c] = sc_mont(sc_load(scan + 8 * (c * nt + t - d)), a[c]);
-    }
-    __syncthreads();
-    for (uint32_t c = 0; c < 2; ++c) sc_store(scan + 8 * (c * nt + t), a[c]);
-    __syncthreads();
-  }
-  if (t > 0)
-    for (uint32_t c = 0; c < 2; ++c) {
-      const sc e = sc_load(scan + 8 * (c * nt + t - 1));
-      for (uint32_t i = i0; i < i1; ++i) sc_store(pref + 8 * (c * k + i), sc_mont(e, sc_load(pref + 8 * (c * k + i))));
-    }
-  __syncthreads();
-  uint32_t* o = sc_out + 8 * (size_t)p * per;
-  auto pr = [&](uint32_t c, uint32_t i) { return sc_from_mont(sc_load(pref + 8 * (c * k + i))); };
-  auto dd = [&](uint32_t c, uint32_t i) {
+  sc one = sc_zero();
+  one.v[0] = 1;
+  const sc oneR = sc_to_mont(one);
+  // lane t owns elements [i0, i1) of both chains; nch lanes own any
+  const uint32_t C = (k + nt - 1) / nt, nch = (k + C - 1) / C, i0 = t * C, i1 = min(i0 + C, k);
+  auto dd = [&](uint32_t c, uint32_t i) {  // v_i - x: v = i + 1 (A) or pi(i) + 1 (B)
     sc v = sc_zero();
     v.v[0] = c == 0 ? i + 1 : pi[(size_t)p * k + i] + 1;
     return sc_sub(v, x);
   };
+  sc run[2] = {oneR, oneR};
+  for (uint32_t i = i0; i < i1; ++i)
+    _Pragma("unroll") for (uint32_t c = 0; c < 2; ++c) {
+      run[c] = sc_mont(run[c], sc_to_mont(dd(c, i)));
+      sc_store(pref + 8 * (c * k + i), run[c]);
+    }
+  // inclusive Hillis-Steele scan of the chunk products, ping-pong buffers
+  uint32_t cur = 0;
+  _Pragma("unroll") for (uint32_t c = 0; c < 2; ++c) sc_store(scan + 8 * (c * nt + t), run[c]);
+  __syncthreads();
+  for (uint32_t d = 1; d < nch; d <<= 1) {
+    const uint32_t* src = scan + 16 * nt * cur;
+    uint32_t* dst = scan + 16 * nt * (cur ^ 1);
+    if (t < nch)
+      _Pragma("unroll") for (uint32_t c = 0; c < 2; ++c) {
+        sc a = sc_load(src + 8 * (c * nt + t));
+        if (t >= d) a = sc_mont(sc_load(src + 8 * (c * nt + t - d)), a);
+        sc_store(dst + 8 * (c * nt + t), a);
+      }
+    cur ^= 1;
+    __syncthreads();
+  }
+  // canonical prefixes: mont(e, P) for the canonical product e of the
+  // earlier chunks and Montgomery P is e P canonical (one multiply each)
+  if (t < nch)
+    _Pragma("unroll") for (uint32_t c = 0; c < 2; ++c) {
+      const sc e = t > 0 ? sc_from_mont(sc_load(scan + 16 * nt * cur + 8 * (c * nt + t - 1))) : one;
+      for (uint32_t i = i0; i < i1; ++i) sc_store(pref + 8 * (c * k + i), sc_mont(e, sc_load(pref + 8 * (c * k + i))));
+    }
+  __syncthreads();
+  uint32_t* o = sc_out + 8 * (size_t)p * per;
+  auto pr = [&](uint32_t c, uint32_t i) { return sc_load(pref + 8 * (c * k + i)); };
   for (uint32_t g = t; g < n_p; g += nt) {
     sc aL = sc_zero(), aR = sc_zero(), aO = sc_zero();
     if (g + 1 < k) {
@@ -474,12 +489,11 @@ __global__ void __launch_bounds__(256) k_witness(uint32_t k, uint32_t n_p, uint3
       aO = pr(1, h + 1);
     } else if (g == 2 * k - 2) {
       aL = pr(1, k - 1);
-      aR = sc_neg([] { sc o = sc_zero(); o.v[0] = 1; return o; }());
+      aR = sc_neg(one);
       aO = sc_neg(aL);
     } else if (g == 2 * k - 1) {
       aL = sc_sub(pr(0, k - 1), pr(1, k - 1));
-      aR = sc_zero();
-      aR.v[0] = 1;
+      aR = one;
       aO = aL;
     }
     sc_store(o + 8 * (1 + g), aL);
@@ -492,7 +506,7 @@ int witness_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint32_t
                 uint32_t per, uint32_t* d_sc) {
   if (!P) return BPP_OK;
   const unsigned nt = 256;
-  const size_t lds = (2 * (size_t)C.k + 2 * nt) * 32;
+  const size_t lds = (2 * (size_t)C.k + 4 * nt) * 32;
   hipLaunchKernelGGL(k_witness, dim3(P), dim3(nt), lds, ctx->stream, C.k, C.n_p, per, d_pi, d_x, d_sc);
   return ctx_check_launch(ctx, "k_witness");
 }

@@ -1,4 +1,4 @@
-// Scalar field Z/lZ on gfx950: Montgomery (CIOS, R = 2^256), 8 x 32-bit.
+// Scalar field Z/lZ on gfx950: Montgomery (R = 2^256), 8 x 32-bit storage.
 //
 // Device counterpart of dalek's `Scalar` for the data-parallel scalar work
 // of the inner-product argument (bulletproofs 4.0.0 InnerProductProof: the
@@ -67,8 +67,80 @@ FE_INLINE sc sc_sub(const sc& a, const sc& b) {
 
 FE_INLINE sc sc_neg(const sc& a) { return sc_sub(sc_zero(), a); }
 
-// a*b*R^-1 mod l; requires a*b < l*R (true for a, b < 2^256 when one is < l)
+// a*b*R^-1 mod l (R = 2^256); requires a*b < l*R (true for a, b < 2^256
+// when one is < l); canonical result.
+//
+// Radix 2^29 inside: 32 a and b as 9 limbs of 29 bits, the 17 product
+// columns as plain v_mad_u64_u32 sums (each < 18 * 2^58 with the reduction
+// terms: no carries while accumulating), then Montgomery reduction by 2^29
+// per step with R' = 2^261 -- mont'(32 a, b) = a b 2^-256.  The columns are
+// independent chains, and a reduction step waits only on the previous
+// step's carry, where sc_mont_cios's carries serialize all ~130
+// multiply-adds: a lone wave (the prover's per-proof scalar kernels) runs
+// the product several times faster (tools/ubench/scbench.hip).
+// l's 29-bit limbs 5..7 are zero, so a reduction step is 6 multiply-adds.
+__device__ __constant__ static const uint32_t SC_L29[9] = {0x1cf5d3edu, 0x009318d2u, 0x1de73596u, 0x1df3bd45u, 0x0000014du,
+                                                            0u, 0u, 0u, 0x00100000u};
+#define SC_M29 0x1fffffffu
+FE_INLINE void sc_to29(const uint32_t w[8], uint32_t sh, uint32_t r[9]) {  // (w << sh) in 29-bit limbs, sh < 29
+  _Pragma("unroll") for (int k = 0; k < 9; ++k) {
+    // bits [29 k - sh, 29 k - sh + 29) of w
+    const int lo = 29 * k - (int)sh;
+    uint64_t x;
+    if (lo < 0) {
+      x = (uint64_t)w[0] << (-lo);
+    } else {
+      const int q = lo >> 5, b = lo & 31;
+      x = (uint64_t)w[q] >> b;
+      if (q + 1 < 8) x |= (uint64_t)w[q + 1] << (32 - b);
+    }
+    r[k] = (uint32_t)x & SC_M29;
+  }
+}
 FE_INLINE sc sc_mont(const sc& a, const sc& b) {
+  uint32_t A[9], B[9];
+  sc_to29(a.v, 5, A);
+  sc_to29(b.v, 0, B);
+  uint64_t col[17];
+  _Pragma("unroll") for (int k = 0; k < 17; ++k) {
+    uint64_t c = 0;
+    _Pragma("unroll") for (int i = 0; i < 9; ++i) {
+      const int j = k - i;
+      if (j >= 0 && j < 9) c = (uint64_t)A[i] * B[j] + c;
+    }
+    col[k] = c;
+  }
+  _Pragma("unroll") for (int i = 0; i < 9; ++i) {
+    const uint32_t m = ((uint32_t)col[i] * SC_LINV) & SC_M29;
+    _Pragma("unroll") for (int j = 0; j < 9; ++j)
+      if (SC_L29[j] != 0 && i + j < 17) col[i + j] = (uint64_t)m * SC_L29[j] + col[i + j];
+    if (i + 1 < 17) col[i + 1] += col[i] >> 29;
+  }
+  // r = col[9..16] normalized (< 2 l < 2^254), as 8 x 32-bit words
+  uint32_t r29[9];
+  uint64_t c = 0;
+  _Pragma("unroll") for (int k = 0; k < 8; ++k) {
+    c += col[9 + k];
+    r29[k] = (uint32_t)c & SC_M29;
+    c >>= 29;
+  }
+  r29[8] = (uint32_t)c;
+  sc r;
+  _Pragma("unroll") for (int w = 0; w < 8; ++w) {
+    const int lo = 32 * w, k = lo / 29, b = lo % 29;
+    uint64_t x = (uint64_t)r29[k] >> b;
+    if (k + 1 < 9) x |= (uint64_t)r29[k + 1] << (29 - b);
+    if (k + 2 < 9 && 58 - b < 32) x |= (uint64_t)r29[k + 2] << (58 - b);
+    r.v[w] = (uint32_t)x;
+  }
+  if (sc_geq_l(r.v)) sc_sub_l(r.v);
+  return r;
+}
+
+// The same product by CIOS over 8 x 32-bit words (the round-1 form, kept as
+// the reference of tests / tools/ubench/scbench.hip): every multiply-add of
+// a row waits for the previous one's carry, a ~130-deep chain.
+FE_INLINE sc sc_mont_cios(const sc& a, const sc& b) {
   uint32_t t[10];
   _Pragma("unroll") for (int i = 0; i < 10; ++i) t[i] = 0;
   _Pragma("unroll") for (int i = 0; i < 8; ++i) {

@@ -128,99 +128,21 @@ void keccak_f1600_x8(uint64_t lanes[25][8]) {
 
 namespace perm {
 
-// Same draws as draw_prover_randomness, from a byte buffer holding the
-// stream (the fixed draw order consumes a fixed number of bytes).
-static void parse_randomness(const Circuit& C, const uint8_t* s, std::vector<uint32_t>& pi,
-                             std::vector<hsc::Sc>& gamma, hsc::Sc& alpha, hsc::Sc& beta, hsc::Sc& rho,
-                             std::vector<hsc::Sc>& sL, std::vector<hsc::Sc>& sR, std::vector<hsc::Sc>& taus) {
-  pi.resize(C.k);
-  for (uint32_t i = 0; i < C.k; ++i) pi[i] = i;
-  for (uint32_t i = C.k - 1; i > 0; --i) {
-    uint64_t x;
-    memcpy(&x, s, 8);
-    s += 8;
-    const uint32_t j = (uint32_t)(x % (uint64_t)(i + 1));
-    std::swap(pi[i], pi[j]);
-  }
-  auto scalar = [&]() {
-    const hsc::Sc v = hsc::from_wide(s);
-    s += 64;
-    return v;
-  };
-  gamma.resize(C.m);
-  for (auto& g : gamma) g = scalar();
-  alpha = scalar();
-  beta = scalar();
-  rho = scalar();
-  sL.resize(C.n_p);
-  sR.resize(C.n_p);
-  taus.resize(5);
-  for (auto& x : sL) x = scalar();
-  for (auto& x : sR) x = scalar();
-  for (auto& x : taus) x = scalar();
-}
-
-// pi, alpha, beta, rho, tau only (gamma, s_L, s_R skipped: device-reduced)
-static void parse_randomness_host_part(const Circuit& C, const uint8_t* s, std::vector<uint32_t>& pi,
-                                       hsc::Sc& alpha, hsc::Sc& beta, hsc::Sc& rho, std::vector<hsc::Sc>& taus) {
-  pi.resize(C.k);
-  for (uint32_t i = 0; i < C.k; ++i) pi[i] = i;
-  for (uint32_t i = C.k - 1; i > 0; --i) {
-    uint64_t x;
-    memcpy(&x, s, 8);
-    s += 8;
-    const uint32_t j = (uint32_t)(x % (uint64_t)(i + 1));
-    std::swap(pi[i], pi[j]);
-  }
-  s += 64 * (size_t)C.m;
-  alpha = hsc::from_wide(s);
-  beta = hsc::from_wide(s + 64);
-  rho = hsc::from_wide(s + 128);
-  s += 192 + 128 * (size_t)C.n_p;
-  taus.resize(5);
-  for (int i = 0; i < 5; ++i) taus[i] = hsc::from_wide(s + 64 * i);
-}
-
-size_t randomness_bytes(const Circuit& C) { return 8 * (size_t)(C.k - 1) + 64 * ((size_t)C.m + 3 + 2 * C.n_p + 5); }
-
-void draw_prover_randomness_x8(const Circuit& C, const Seed seeds[8], RandomDraws* const out[8]) {
-  const size_t len = randomness_bytes(C);
-  if (!merlin::keccak_x8_available()) {
-    for (int j = 0; j < 8; ++j)
-      draw_prover_randomness(C, seeds[j], out[j]->pi, out[j]->gamma, out[j]->alpha, out[j]->beta, out[j]->rho,
-                             out[j]->sL, out[j]->sR, out[j]->taus);
-    return;
-  }
-  static thread_local std::vector<uint8_t> buf;  // ~195 KB per call: reused, not re-mapped
-  buf.resize(8 * len);
-  uint8_t in[8][12 + 32];
-  const uint8_t* inp[8];
+// pi of eight proofs: Fisher-Yates over the first 8 (k - 1) bytes of their
+// SHAKE256("bpperm-prove" || seed) streams
+static void draw_pi_x8(const Circuit& C, const Seed seeds[8], RandomDraws* const out[8]) {
+  const size_t len = 8 * (size_t)(C.k - 1);
+  uint8_t st[8][8 * 1024];
+  static thread_local std::vector<uint8_t> big;  // (k > 1025)
   uint8_t* outp[8];
-  for (int j = 0; j < 8; ++j) {
-    memcpy(in[j], "bpperm-prove", 12);
-    memcpy(in[j] + 12, seeds[j].b, seeds[j].len);
-    inp[j] = in[j];
-    outp[j] = buf.data() + (size_t)j * len;
-  }
-  merlin::shake256_x8(inp, 12 + seeds[0].len, outp, len);
-  for (int j = 0; j < 8; ++j)
-    parse_randomness(C, outp[j], out[j]->pi, out[j]->gamma, out[j]->alpha, out[j]->beta, out[j]->rho, out[j]->sL,
-                     out[j]->sR, out[j]->taus);
-}
-
-}  // namespace perm
-
-namespace perm {
-
-void draw_prover_randomness_x8_stream(const Circuit& C, const Seed seeds[8], uint8_t* const stream[8],
-                                      RandomDraws* const out[8]) {
-  const size_t len = randomness_bytes(C);
+  if (len > sizeof st[0]) big.resize(8 * len);
+  for (int j = 0; j < 8; ++j) outp[j] = len > sizeof st[0] ? big.data() + (size_t)j * len : st[j];
   if (!merlin::keccak_x8_available()) {
     for (int j = 0; j < 8; ++j) {
       Rng rng("bpperm-prove", seeds[j]);
-      rng.bytes(stream[j], len);
+      rng.bytes(outp[j], len);
     }
-  } else {
+  } else if (len) {
     uint8_t in[8][12 + 32];
     const uint8_t* inp[8];
     for (int j = 0; j < 8; ++j) {
@@ -228,13 +150,84 @@ void draw_prover_randomness_x8_stream(const Circuit& C, const Seed seeds[8], uin
       memcpy(in[j] + 12, seeds[j].b, seeds[j].len);
       inp[j] = in[j];
     }
-    merlin::shake256_x8(inp, 12 + seeds[0].len, stream, len);
+    merlin::shake256_x8(inp, 12 + seeds[0].len, outp, len);
+  }
+  for (int j = 0; j < 8; ++j) {
+    std::vector<uint32_t>& pi = out[j]->pi;
+    pi.resize(C.k);
+    for (uint32_t i = 0; i < C.k; ++i) pi[i] = i;
+    const uint8_t* s = outp[j];
+    for (uint32_t i = C.k - 1; i > 0; --i) {
+      uint64_t x;
+      memcpy(&x, s, 8);
+      s += 8;
+      std::swap(pi[i], pi[(uint32_t)(x % (uint64_t)(i + 1))]);
+    }
+  }
+}
+
+// scalar draw `idx` of eight proofs (draw_scalar, 8-way)
+static void draw_scalar_x8(const Seed seeds[8], uint32_t idx, hsc::Sc* const out[8]) {
+  if (!merlin::keccak_x8_available()) {
+    for (int j = 0; j < 8; ++j) *out[j] = draw_scalar(seeds[j], idx);
+    return;
+  }
+  uint8_t in[8][BPP_DRAW_DOMAIN_LEN + 32 + 4], wide[8][64];
+  const uint8_t* inp[8];
+  uint8_t* outp[8];
+  const size_t sl = seeds[0].len;
+  for (int j = 0; j < 8; ++j) {
+    memcpy(in[j], BPP_DRAW_DOMAIN, BPP_DRAW_DOMAIN_LEN);
+    memcpy(in[j] + BPP_DRAW_DOMAIN_LEN, seeds[j].b, sl);
+    for (int b = 0; b < 4; ++b) in[j][BPP_DRAW_DOMAIN_LEN + sl + b] = (uint8_t)(idx >> (8 * b));
+    inp[j] = in[j];
+    outp[j] = wide[j];
+  }
+  merlin::shake256_x8(inp, BPP_DRAW_DOMAIN_LEN + sl + 4, outp, 64);
+  for (int j = 0; j < 8; ++j) *out[j] = hsc::from_wide(wide[j]);
+}
+
+void draw_prover_randomness_x8(const Circuit& C, const Seed seeds[8], RandomDraws* const out[8]) {
+  draw_pi_x8(C, seeds, out);
+  hsc::Sc* o[8];
+  uint32_t idx = 0;
+  auto vec = [&](std::vector<hsc::Sc> RandomDraws::*v, uint32_t n) {
+    for (int j = 0; j < 8; ++j) (out[j]->*v).resize(n);
+    for (uint32_t i = 0; i < n; ++i, ++idx) {
+      for (int j = 0; j < 8; ++j) o[j] = &(out[j]->*v)[i];
+      draw_scalar_x8(seeds, idx, o);
+    }
+  };
+  auto one = [&](hsc::Sc RandomDraws::*f) {
+    for (int j = 0; j < 8; ++j) o[j] = &(out[j]->*f);
+    draw_scalar_x8(seeds, idx++, o);
+  };
+  vec(&RandomDraws::gamma, C.m);
+  one(&RandomDraws::alpha);
+  one(&RandomDraws::beta);
+  one(&RandomDraws::rho);
+  vec(&RandomDraws::sL, C.n_p);
+  vec(&RandomDraws::sR, C.n_p);
+  vec(&RandomDraws::taus, 5);
+}
+
+void draw_prover_host_x8(const Circuit& C, const Seed seeds[8], RandomDraws* const out[8]) {
+  draw_pi_x8(C, seeds, out);
+  hsc::Sc* o[8];
+  hsc::Sc RandomDraws::*abr[3] = {&RandomDraws::alpha, &RandomDraws::beta, &RandomDraws::rho};
+  for (uint32_t i = 0; i < 3; ++i) {
+    for (int j = 0; j < 8; ++j) o[j] = &(out[j]->*abr[i]);
+    draw_scalar_x8(seeds, draw_alpha_index(C) + i, o);
   }
   for (int j = 0; j < 8; ++j) {
     out[j]->gamma.clear();
     out[j]->sL.clear();
     out[j]->sR.clear();
-    parse_randomness_host_part(C, stream[j], out[j]->pi, out[j]->alpha, out[j]->beta, out[j]->rho, out[j]->taus);
+    out[j]->taus.resize(5);
+  }
+  for (uint32_t i = 0; i < 5; ++i) {
+    for (int j = 0; j < 8; ++j) o[j] = &out[j]->taus[i];
+    draw_scalar_x8(seeds, draw_tau_index(C) + i, o);
   }
 }
 

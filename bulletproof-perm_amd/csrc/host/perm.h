@@ -83,32 +83,38 @@ struct Rng {
 
 std::vector<uint32_t> fisher_yates(uint32_t k, Rng& rng);
 
-// The prover's random draws from SHAKE256("bpperm-prove" || seed), in the
-// fixed order pi (Fisher-Yates), gamma[m], alpha, beta, rho, s_L[n_p],
-// s_R[n_p], tau[5] (the stand-in for thread_rng, circuit_lib.rs:175).
+// The prover's random draws (the stand-in for thread_rng,
+// circuit_lib.rs:175): pi by Fisher-Yates from the stream
+// SHAKE256("bpperm-prove" || seed), one u64 per step; the blinding scalars
+// by index j in the order gamma[m], alpha, beta, rho, s_L[n_p], s_R[n_p],
+// tau[5], scalar j = from_wide(SHAKE256("bpperm-prove-sc" || seed ||
+// le32 j)[0..64]) (draw_scalar; oracle/merlin.py indexed_scalar) -- one
+// sponge block per draw, so the GPU makes every draw in its own thread
+// (poly.h draws_dev).
 void draw_prover_randomness(const Circuit& C, const Seed& seed, std::vector<uint32_t>& pi, std::vector<hsc::Sc>& gamma,
                             hsc::Sc& alpha, hsc::Sc& beta, hsc::Sc& rho, std::vector<hsc::Sc>& sL,
                             std::vector<hsc::Sc>& sR, std::vector<hsc::Sc>& taus);
+#define BPP_DRAW_DOMAIN "bpperm-prove-sc"
+#define BPP_DRAW_DOMAIN_LEN 15
+hsc::Sc draw_scalar(const Seed& seed, uint32_t j);
+inline uint32_t draw_alpha_index(const Circuit& C) { return C.m; }            // then beta, rho
+inline uint32_t draw_tau_index(const Circuit& C) { return C.m + 3 + 2 * C.n_p; }  // tau[5]
+inline uint32_t draw_count(const Circuit& C) { return C.m + 3 + 2 * C.n_p + 5; }
 
 struct RandomDraws {
   std::vector<uint32_t> pi;
   std::vector<hsc::Sc> gamma, sL, sR, taus;
   hsc::Sc alpha, beta, rho;
 };
-// Bytes of the SHAKE256 stream one proof's draws consume (fixed: the
-// Fisher-Yates steps take one u64 each, every scalar 64 bytes).
-size_t randomness_bytes(const Circuit& C);
-// The draws of eight proofs at once: the eight SHAKE256 streams run through
-// an AVX-512 8-way Keccak (host/keccak_x8.cpp; scalar fallback without
-// AVX-512), byte-identical to draw_prover_randomness.
-// (the eight seeds must have the same length)
+// The draws of eight proofs at once: the eight pi streams and each index's
+// eight scalar sponges run through an AVX-512 8-way Keccak
+// (host/keccak_x8.cpp; scalar fallback without AVX-512), identical to
+// draw_prover_randomness.  (the eight seeds must have the same length)
 void draw_prover_randomness_x8(const Circuit& C, const Seed seeds[8], RandomDraws* const out[8]);
-// As above, but the eight streams are written to stream[j] (randomness_bytes
-// each) and only pi, alpha, beta, rho and tau are parsed on the host: gamma,
-// s_L and s_R stay in the streams (reduced on the GPU, poly.h
-// draws_reduce_dev) and out[j]'s vectors for them are left empty.
-void draw_prover_randomness_x8_stream(const Circuit& C, const Seed seeds[8], uint8_t* const stream[8],
-                                      RandomDraws* const out[8]);
+// As above, but only the host's share -- pi, alpha, beta, rho and tau: the
+// GPU draws gamma, s_L and s_R (and alpha, beta, rho again, into its scalar
+// arrays; poly.h draws_dev), and out[j]'s vectors for them are left empty.
+void draw_prover_host_x8(const Circuit& C, const Seed seeds[8], RandomDraws* const out[8]);
 
 size_t proof_len(uint32_t k);
 

@@ -112,22 +112,34 @@ std::vector<uint32_t> fisher_yates(uint32_t k, Rng& rng) {
   return p;
 }
 
+Sc draw_scalar(const Seed& seed, uint32_t j) {
+  merlin::Shake256 sh;
+  sh.update((const uint8_t*)BPP_DRAW_DOMAIN, BPP_DRAW_DOMAIN_LEN);
+  sh.update(seed.b, seed.len);
+  const uint8_t jb[4] = {(uint8_t)j, (uint8_t)(j >> 8), (uint8_t)(j >> 16), (uint8_t)(j >> 24)};
+  sh.update(jb, 4);
+  uint8_t b[64];
+  sh.read(b, 64);
+  return hsc::from_wide(b);
+}
+
 void draw_prover_randomness(const Circuit& C, const Seed& seed, std::vector<uint32_t>& pi, std::vector<Sc>& gamma,
                             Sc& alpha, Sc& beta, Sc& rho, std::vector<Sc>& sL, std::vector<Sc>& sR,
                             std::vector<Sc>& taus) {
   Rng rng("bpperm-prove", seed);
   pi = fisher_yates(C.k, rng);
+  uint32_t j = 0;
   gamma.resize(C.m);
-  for (auto& g : gamma) g = rng.scalar();
-  alpha = rng.scalar();
-  beta = rng.scalar();
-  rho = rng.scalar();
+  for (auto& g : gamma) g = draw_scalar(seed, j++);
+  alpha = draw_scalar(seed, j++);
+  beta = draw_scalar(seed, j++);
+  rho = draw_scalar(seed, j++);
   sL.resize(C.n_p);
   sR.resize(C.n_p);
   taus.resize(5);
-  for (auto& x : sL) x = rng.scalar();
-  for (auto& x : sR) x = rng.scalar();
-  for (auto& x : taus) x = rng.scalar();
+  for (auto& x : sL) x = draw_scalar(seed, j++);
+  for (auto& x : sR) x = draw_scalar(seed, j++);
+  for (auto& x : taus) x = draw_scalar(seed, j++);
 }
 
 size_t proof_len(uint32_t k) {

@@ -227,44 +227,50 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
   // the witness on the device (k_witness) while its prefix products fit the
   // workgroup's LDS; the host restatement beyond that
   const bool dev_witness = (2 * (size_t)k + 512) * 32 <= 64 * 1024;
-  // RNG draws (order fixed: pi, gamma, alpha beta rho, s_L, s_R, tau x5):
-  // eight proofs' SHAKE256 streams per AVX-512 Keccak, written straight into
-  // the pinned upload arena; the host parses pi, alpha, beta, rho, tau and
-  // the GPU reduces the 2 n_p + m wide draws it alone uses (gamma -> [P][m],
-  // s_L / s_R -> their slots of the A_I/A_O/S scalar array)
+  // RNG draws (perm.h draw_prover_randomness): the host makes pi (its short
+  // SHAKE256 streams, 8-way AVX-512 Keccak) and alpha, beta, rho, tau; the
+  // GPU makes the 2 n_p + m + 3 indexed scalar draws its kernels use (k_draws:
+  // gamma -> [P][m], alpha .. s_R -> their slots of the A_I/A_O/S scalar
+  // array) from per-proof sponge templates written straight into the pinned
+  // upload arena
   std::unique_ptr<HostScope> hs(new HostScope(ctx, "pb_rng"));
-  const size_t rlen = perm::randomness_bytes(C);
   uint32_t *d_gamma = nullptr, *d_s = nullptr, *d_pi = nullptr;
   {
     void *dg = nullptr, *dsc = nullptr, *dst = nullptr, *dpi = nullptr;
+    const size_t tlen = 7 * sizeof(uint64_t);  // draw template per proof
+    for (const perm::Seed& sd : seeds)
+      if (sd.len != seeds[0].len) {
+        ctx->err = "prove_batch: seeds of different lengths in one batch";
+        return BPP_ERR_ARG;
+      }
     BPP_TRY(ctx_ws(ctx, "pb_gamma", (size_t)P * m * 32, &dg));
     BPP_TRY(ctx_ws(ctx, "mt_s", (size_t)P * per * 32 + 32, &dsc));
-    BPP_TRY(ctx_ws(ctx, "pb_stream", P * rlen, &dst));
+    BPP_TRY(ctx_ws(ctx, "pb_tmpl", P * tlen, &dst));
     BPP_TRY(ctx_ws(ctx, "pb_pi", (size_t)P * k * 4, &dpi));
     d_gamma = (uint32_t*)dg;
     d_s = (uint32_t*)dsc;
     d_pi = (uint32_t*)dpi;
     // (one staging region: a second take could recycle the arena under the first)
-    uint8_t* stream = nullptr;
-    BPP_TRY(ctx_h2d_stage(ctx, P * rlen + (size_t)P * k * 4, &stream));
-    uint8_t* pis = stream + P * rlen;
+    uint8_t* stage = nullptr;
+    BPP_TRY(ctx_h2d_stage(ctx, P * tlen + (size_t)P * k * 4, &stage));
+    uint8_t* pis = stage + P * tlen;
     par::for_each((P + 7) / 8, [&](size_t gi) {
       perm::Seed sd[8];
       perm::RandomDraws* d[8];
-      uint8_t* out[8];
-      perm::RandomDraws spare;                 // a short last group's padding lanes
-      static thread_local std::vector<uint8_t> pad_stream;
-      pad_stream.resize(rlen);
+      perm::RandomDraws spare;  // a short last group's padding lanes
       for (size_t j = 0; j < 8; ++j) {
         const bool real = 8 * gi + j < P;
         sd[j] = seeds[std::min(8 * gi + j, P - 1)];
         d[j] = real ? &S[8 * gi + j]->d : &spare;
-        out[j] = real ? stream + (8 * gi + j) * rlen : pad_stream.data();
       }
-      perm::draw_prover_randomness_x8_stream(C, sd, out, d);
+      perm::draw_prover_host_x8(C, sd, d);
       for (size_t j = 0; j < 8 && 8 * gi + j < P; ++j) {
-        S[8 * gi + j]->tr.arithmetic_domain_sep(n_p);
-        memcpy(pis + (8 * gi + j) * 4 * (size_t)k, S[8 * gi + j]->d.pi.data(), 4 * (size_t)k);
+        const size_t i = 8 * gi + j;
+        S[i]->tr.arithmetic_domain_sep(n_p);
+        uint64_t tm[7];
+        draw_template(sd[j], tm);
+        memcpy(stage + i * tlen, tm, tlen);
+        memcpy(pis + i * 4 * (size_t)k, S[i]->d.pi.data(), 4 * (size_t)k);
       }
 #ifdef EXP_HOST_BURN_US  // timing experiment only: extra host CPU per proof
       const auto t0 = std::chrono::steady_clock::now();
@@ -272,9 +278,9 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
       }
 #endif
     });
-    BPP_TRY(ctx_h2d_staged(ctx, dst, stream, P * rlen));
+    BPP_TRY(ctx_h2d_staged(ctx, dst, stage, P * tlen));
     BPP_TRY(ctx_h2d_staged(ctx, d_pi, pis, (size_t)P * k * 4));
-    BPP_TRY(draws_reduce_dev(ctx, C, (uint32_t)P, (const uint32_t*)dst, rlen, per, d_gamma, d_s));
+    BPP_TRY(draws_dev(ctx, C, (uint32_t)P, (const uint64_t*)dst, P ? seeds[0].len : 0, per, d_gamma, d_s));
   }
   // V_0..V_2k-1 of every proof: one fixed-base launch over device inputs
   // (values 1..k, pi + 1 and gamma, k_v_inputs), encodings back to the host

@@ -27,11 +27,14 @@ int poly_x_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const std::vect
 int verify_scalars_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const std::vector<uint32_t>& rec,
                        uint32_t* d_sc);
 
-// The prover's SHAKE256 streams ([P][len] bytes on the device, len =
-// perm::randomness_bytes) -> gamma ([P][m], canonical) and alpha, beta, rho,
-// s_L, s_R into their slots of the A_I/A_O/S scalar array d_sc ([P][per]).
-int draws_reduce_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint32_t* d_stream, size_t len,
-                     uint32_t per, uint32_t* d_gamma, uint32_t* d_sc);
+// The prover's blinding draws on the device (perm.h draw_scalar, one
+// thread each) from per-proof sponge templates (d_tmpl [P][7] u64,
+// draw_template; seed_len uniform over the batch, <= 32) -> gamma ([P][m],
+// canonical) and alpha, beta, rho, s_L, s_R into their slots of the
+// A_I/A_O/S scalar array d_sc ([P][per]).
+int draws_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint64_t* d_tmpl, uint32_t seed_len,
+              uint32_t per, uint32_t* d_gamma, uint32_t* d_sc);
+void draw_template(const perm::Seed& seed, uint64_t tmpl[7]);
 
 // V commitment inputs on the device from pi ([P][k] u32) and gamma:
 // d_v, d_g [P][2k] and d_gx_half [P] = gamma_2k / 2.

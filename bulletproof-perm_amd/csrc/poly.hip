@@ -22,6 +22,7 @@
 
 #include "ctx.h"
 #include "poly.h"
+#include "keccak_dev.cuh"
 #include "sc25519.cuh"
 
 #define POLY_SLOTS 7  // l1 r0 r1 r3 l2 l3 (Montgomery) per gate
@@ -400,19 +401,39 @@ __global__ void __launch_bounds__(POLY_T) k_verify_merge(uint32_t count, uint32_
 // alpha, beta, rho and tau itself and never needs gamma, s_L, s_R: gamma goes
 // to [P][m] (V commitments, tau_x), s_L / s_R straight into their slots of the
 // A_I/A_O/S scalar array ([P][per], per = 3 + 5 n_p: s_L at 3 + 3 n_p).
-__global__ void __launch_bounds__(256) k_draws_reduce(uint32_t P, uint32_t len_w, uint32_t off_w, uint32_t m,
-                                                     uint32_t n_p, uint32_t per, const uint32_t* __restrict__ stream,
-                                                     uint32_t* __restrict__ gamma, uint32_t* __restrict__ sc_out) {
+// The blinding draws (perm.h draw_scalar) of P proofs, one thread per draw:
+// draw j's sponge block is the proof's template (tmpl [P][7] u64, host-built:
+// domain || seed with the 0x1F pad byte after the index) plus le32 j at byte
+// jo and the 0x80 that closes the 136-byte rate; one Keccak-f yields the 64
+// bytes that from_wide reduces.  gamma -> [P][m]; alpha, beta, rho, s_L, s_R
+// -> their slots of the A_I/A_O/S scalar array ([alpha, a_L, a_R, beta, a_O,
+// rho, s_L, s_R], per words x 8 a proof); the host draws tau itself.
+__global__ void __launch_bounds__(256) k_draws(uint32_t P, uint32_t m, uint32_t n_p, uint32_t per, uint32_t jo,
+                                              const uint64_t* __restrict__ tmpl, uint32_t* __restrict__ gamma,
+                                              uint32_t* __restrict__ sc_out) {
   const uint32_t nw = m + 3 + 2 * n_p;  // gamma[m], alpha, beta, rho, s_L[n_p], s_R[n_p]
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (size_t)P * nw) return;
   const uint32_t p = (uint32_t)(t / nw), j = (uint32_t)(t % nw);
-  const sc x = sc_from_wide_w(stream + (size_t)p * len_w + off_w + 16 * j);
+  uint64_t a[25];
+  _Pragma("unroll") for (int i = 0; i < 25; ++i) a[i] = i < 7 ? tmpl[7 * (size_t)p + i] : 0ull;
+  a[16] ^= 0x8000000000000000ull;
+  const uint32_t li = jo >> 3, sh = 8 * (jo & 7);
+  _Pragma("unroll") for (uint32_t i = 0; i < 7; ++i) {  // (static indices: no scratch)
+    if (i == li) a[i] ^= (uint64_t)j << sh;
+    if (i == li + 1 && sh > 32) a[i] ^= (uint64_t)j >> (64 - sh);
+  }
+  keccak_f1600_dev(a);
+  uint32_t w[16];
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) {
+    w[2 * i] = (uint32_t)a[i];
+    w[2 * i + 1] = (uint32_t)(a[i] >> 32);
+  }
+  const sc x = sc_from_wide_w(w);
   if (j < m) {
     sc_store(gamma + 8 * ((size_t)p * m + j), x);
     return;
   }
-  // A_I/A_O/S scalars [alpha, a_L, a_R, beta, a_O, rho, s_L, s_R]
   const uint32_t q = j - m;
   const uint32_t pos = q == 0 ? 0u : q == 1 ? 1 + 2 * n_p : q == 2 ? 2 + 3 * n_p : 3 + 3 * n_p + (q - 3);
   sc_store(sc_out + 8 * ((size_t)p * per + pos), x);
@@ -505,7 +526,9 @@ __global__ void __launch_bounds__(256) k_witness(uint32_t k, uint32_t n_p, uint3
 int witness_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint32_t* d_pi, const uint32_t* d_x,
                 uint32_t per, uint32_t* d_sc) {
   if (!P) return BPP_OK;
-  const unsigned nt = 256;
+  // (256 lanes while the prefixes and both scan buffers fit 64 KB, else 128:
+  // perm_api's dev_witness bound (2 k + 512) x 32 B)
+  const unsigned nt = (2 * (size_t)C.k + 4 * 256) * 32 <= 64 * 1024 ? 256 : 128;
   const size_t lds = (2 * (size_t)C.k + 4 * nt) * 32;
   hipLaunchKernelGGL(k_witness, dim3(P), dim3(nt), lds, ctx->stream, C.k, C.n_p, per, d_pi, d_x, d_sc);
   return ctx_check_launch(ctx, "k_witness");
@@ -531,13 +554,25 @@ __global__ void __launch_bounds__(256) k_v_inputs(uint32_t P, uint32_t k, uint32
   sc_store(g + 8 * ((size_t)p * 2 * k + i), gm);
 }
 
-int draws_reduce_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint32_t* d_stream, size_t len,
-                     uint32_t per, uint32_t* d_gamma, uint32_t* d_sc) {
+int draws_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint64_t* d_tmpl, uint32_t seed_len,
+              uint32_t per, uint32_t* d_gamma, uint32_t* d_sc) {
   if (!P) return BPP_OK;
+  if (seed_len > 32) {
+    ctx->err = "draws_dev: seed longer than 32 bytes";
+    return BPP_ERR_ARG;
+  }
   const size_t nt = (size_t)P * (C.m + 3 + 2 * C.n_p);
-  hipLaunchKernelGGL(k_draws_reduce, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, ctx->stream, P,
-                     (uint32_t)(len / 4), (uint32_t)(8 * (C.k - 1) / 4), C.m, C.n_p, per, d_stream, d_gamma, d_sc);
-  return ctx_check_launch(ctx, "k_draws_reduce");
+  hipLaunchKernelGGL(k_draws, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, ctx->stream, P, C.m, C.n_p, per,
+                     (uint32_t)(BPP_DRAW_DOMAIN_LEN + seed_len), d_tmpl, d_gamma, d_sc);
+  return ctx_check_launch(ctx, "k_draws");
+}
+
+void draw_template(const perm::Seed& seed, uint64_t tmpl[7]) {
+  uint8_t b[56] = {0};
+  memcpy(b, BPP_DRAW_DOMAIN, BPP_DRAW_DOMAIN_LEN);
+  memcpy(b + BPP_DRAW_DOMAIN_LEN, seed.b, seed.len);
+  b[BPP_DRAW_DOMAIN_LEN + seed.len + 4] = 0x1F;  // SHAKE's pad byte after le32 j
+  memcpy(tmpl, b, 56);
 }
 
 int v_inputs_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint32_t* d_pi, const uint32_t* d_gamma,

@@ -36,7 +36,7 @@ from __future__ import annotations
 from dataclasses import dataclass, field
 
 from . import ristretto as r255
-from .merlin import Rng, Transcript, bulletproof_gens, pedersen_gens_default
+from .merlin import Rng, Transcript, bulletproof_gens, indexed_scalar, pedersen_gens_default
 
 L = r255.L
 
@@ -294,8 +294,9 @@ def _vecpoly_eval(coeffs, x):
 
 
 def ac_prove(k: int, seed: int, gens=None, label: bytes = b"bp-perm"):
-    """Sound-mode arithmetic-circuit proof for a k-card permutation.  All
-    randomness from Rng(seed) in a fixed order."""
+    """Sound-mode arithmetic-circuit proof for a k-card permutation.  pi from
+    the stream Rng(seed, "bpperm-prove") (Fisher-Yates, one u64 per step), the
+    blinding scalars by index (indexed_scalar)."""
     rng = Rng(seed, b"bpperm-prove")
     C = perm_circuit(k)
     n, n_p, m = C.n, C.n_p, C.m
@@ -304,11 +305,13 @@ def ac_prove(k: int, seed: int, gens=None, label: bytes = b"bp-perm"):
     G, H = gens
     g, h = pedersen_gens_default()
     perm = fisher_yates(k, rng)
-    gamma = [rng.scalar() for _ in range(m)]
-    alpha, beta, rho = rng.scalar(), rng.scalar(), rng.scalar()
-    sL = [rng.scalar() for _ in range(n_p)]
-    sR = [rng.scalar() for _ in range(n_p)]
-    taus = [rng.scalar() for _ in range(5)]
+    # scalar draws by index: gamma[m], alpha, beta, rho, s_L[n_p], s_R[n_p], tau[5]
+    S = [indexed_scalar(seed, j) for j in range(m + 3 + 2 * n_p + 5)]
+    gamma = S[:m]
+    alpha, beta, rho = S[m], S[m + 1], S[m + 2]
+    sL = S[m + 3: m + 3 + n_p]
+    sR = S[m + 3 + n_p: m + 3 + 2 * n_p]
+    taus = S[m + 3 + 2 * n_p:]
 
     tr = Transcript(label)
     tr.arithmetic_domain_sep(n_p)

@@ -329,8 +329,19 @@ static void rng_init(rng_t* r, uint64_t seed) {
   sp_absorb(&r->x, (const uint8_t*)"bpperm-prove", 12);
   sp_absorb(&r->x, (const uint8_t*)&seed, 8);
 }
-static sc_t rng_scalar(rng_t* r) { uint8_t b[64]; sp_squeeze(&r->x, b, 64); return sc_from_wide(b); }
 static uint64_t rng_u64(rng_t* r) { uint64_t v; sp_squeeze(&r->x, (uint8_t*)&v, 8); return v; }
+/* blinding scalar j: from_wide(SHAKE256("bpperm-prove-sc" || seed || le32 j)[0..64])
+ * (oracle/merlin.py indexed_scalar) */
+static sc_t draw_sc(uint64_t seed, uint32_t j) {
+  sponge_t x;
+  uint8_t b[64], jb[4] = {(uint8_t)j, (uint8_t)(j >> 8), (uint8_t)(j >> 16), (uint8_t)(j >> 24)};
+  sp_init(&x, 136, 0x1F);
+  sp_absorb(&x, (const uint8_t*)"bpperm-prove-sc", 15);
+  sp_absorb(&x, (const uint8_t*)&seed, 8);
+  sp_absorb(&x, jb, 4);
+  sp_squeeze(&x, b, 64);
+  return sc_from_wide(b);
+}
 
 /* ================================================================ prover */
 static void enc_pt(uint8_t out[32], const ge_ext* p) { ristretto_encode(out, p); }
@@ -353,17 +364,18 @@ static int prove(const gens_t* G, const circuit_t* C, uint64_t seed, const uint8
     uint32_t j = (uint32_t)(rng_u64(&rng) % (uint64_t)(i + 1));
     uint32_t t = pi[i]; pi[i] = pi[j]; pi[j] = t;
   }
+  /* blinding scalars by index: gamma[m], alpha, beta, rho, s_L[n_p], s_R[n_p], tau[5] */
   sc_t* gamma = malloc(sizeof(sc_t) * m);
-  for (uint32_t i = 0; i < m; ++i) gamma[i] = rng_scalar(&rng);
-  sc_t alpha = rng_scalar(&rng), beta = rng_scalar(&rng), rho = rng_scalar(&rng);
+  for (uint32_t i = 0; i < m; ++i) gamma[i] = draw_sc(seed, i);
+  sc_t alpha = draw_sc(seed, m), beta = draw_sc(seed, m + 1), rho = draw_sc(seed, m + 2);
   sc_t* buf = calloc((size_t)n_p * 24 + 4 * C->Q + 64, sizeof(sc_t));
   sc_t *sL = buf, *sR = sL + n_p, *aL = sR + n_p, *aR = aL + n_p, *aO = aR + n_p, *y_n = aO + n_p,
        *y_inv = y_n + n_p, *zWL = y_inv + n_p, *zWR = zWL + n_p, *zWO = zWR + n_p, *l1 = zWO + n_p, *r0 = l1 + n_p,
        *r1 = r0 + n_p, *r3 = r1 + n_p, *l = r3 + n_p, *r = l + n_p, *zq = r + n_p, *zWV = zq + C->Q + 1;
-  for (uint32_t i = 0; i < n_p; ++i) sL[i] = rng_scalar(&rng);
-  for (uint32_t i = 0; i < n_p; ++i) sR[i] = rng_scalar(&rng);
+  for (uint32_t i = 0; i < n_p; ++i) sL[i] = draw_sc(seed, m + 3 + i);
+  for (uint32_t i = 0; i < n_p; ++i) sR[i] = draw_sc(seed, m + 3 + n_p + i);
   sc_t taus[5];
-  for (int i = 0; i < 5; ++i) taus[i] = rng_scalar(&rng);
+  for (int i = 0; i < 5; ++i) taus[i] = draw_sc(seed, m + 3 + 2 * n_p + (uint32_t)i);
 
   transcript_t tr;
   tr_init(&tr, label, llen);

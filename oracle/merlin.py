@@ -253,3 +253,12 @@ class Rng:
 
     def point(self):  # RistrettoPoint::random
         return r255.from_uniform_bytes(self.bytes(64))
+
+
+def indexed_scalar(seed, j: int, domain: bytes = b"bpperm-prove-sc") -> int:
+    """Draw j of a proof's blinding scalars: from_wide of the first 64 bytes of
+    SHAKE256(domain || seed || le32(j)) (seed bytes as in Rng).  Every draw is
+    its own one-block sponge, so the GPU makes each in its own thread
+    (poly.hip k_draws) where one sequential stream would serialize them."""
+    sb = bytes(seed) if isinstance(seed, (bytes, bytearray)) else struct.pack("<Q", seed)
+    return r255.scalar_from_wide(hashlib.shake_256(domain + sb + struct.pack("<I", j)).digest(64))

@@ -113,6 +113,17 @@ static int test_draws() {
       CHECK(memcmp(taus.data(), d[j].taus.data(), 32 * taus.size()) == 0);
       CHECK(memcmp(&rh, &d[j].rho, 32) == 0);
     }
+    perm::RandomDraws h[8];
+    perm::RandomDraws* hp[8];
+    for (int j = 0; j < 8; ++j) hp[j] = &h[j];
+    perm::draw_prover_host_x8(C, sd, hp);  // the host's share of the same draws
+    for (int j = 0; j < 8; ++j) {
+      CHECK(h[j].pi == d[j].pi);
+      CHECK(memcmp(&h[j].alpha, &d[j].alpha, 32) == 0 && memcmp(&h[j].beta, &d[j].beta, 32) == 0);
+      CHECK(memcmp(&h[j].rho, &d[j].rho, 32) == 0);
+      CHECK(h[j].taus.size() == 5 && memcmp(h[j].taus.data(), d[j].taus.data(), 32 * 5) == 0);
+      CHECK(h[j].gamma.empty() && h[j].sL.empty());
+    }
   }
   // sparse z^Q W over the circuit
   std::vector<hsc::Sc> zq(C.Q);

@@ -1,7 +1,7 @@
 // Host-side parallel-for over independent proofs (transcripts, challenge
 // scalars, witness polynomials).  A persistent pool (spawning threads per
 // call costs ~20 us each, more than a batch of transcript operations):
-// threads = BPP_HOST_THREADS or min(granted CPUs, 16) / 2; items are claimed
+// threads = BPP_HOST_THREADS or min(granted CPUs, 16) / 4; items are claimed
 // from an atomic counter; the calling thread works too.  Concurrent calls
 // share the workers; a call from inside a pool task runs inline.
 #pragma once
@@ -37,13 +37,16 @@ inline unsigned granted_cpus() {
 inline unsigned threads() {
   static const unsigned n = [] {
     const char* e = getenv("BPP_HOST_THREADS");
-    // Half the granted CPUs (8 of the box's 16): every batch in flight has
-    // its own driver thread that works on its jobs too, so 8 batches + 7
-    // workers fill the quota without oversubscribing it.  Measured on the
-    // box, 128-proof batches: 16 threads x 4 in flight 52-64 K proofs/s,
-    // 8 x 8 75-80 K, 8 x 12 80-83 K, 4 x 12 80-81 K; one batch alone
-    // 5.57 ms with 16 threads vs 5.60 ms with 8 (tools/EXPERIMENTS.md exp2-4).
-    const unsigned v = e ? (unsigned)atoi(e) : std::max(1u, std::min(16u, granted_cpus()) / 2);
+    // A quarter of the granted CPUs (4 of the box's 16): every batch in
+    // flight has its own driver thread that works on its jobs too, and the
+    // prover is GPU-bound, so more workers only spin.  Measured on the box
+    // (tools/gpu_batch_sweep.sh, 52-card proofs/s, two runs each): 256-proof
+    // batches x 8 in flight with 2 / 4 / 8 threads 196-206 K / 212-220 K /
+    // 206-213 K (8 threads: 9.4 cores busy, 45 us CPU per proof, against 6.5
+    // and 30 us with 4); 128 x 12 with 8 / 4 threads 138-144 K / 172-180 K.
+    // (round 1: 16 threads x 4 in flight 52-64 K, 8 x 8 75-80 K;
+    // tools/EXPERIMENTS.md exp2-4)
+    const unsigned v = e ? (unsigned)atoi(e) : std::max(1u, std::min(16u, granted_cpus()) / 4);
     return std::max(1u, v);
   }();
   return n;

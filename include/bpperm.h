@@ -210,8 +210,11 @@ int bpp_ipa_verify(bpp_ctx* ctx, const bpp_gens* g, bpp_transcript* tr, size_t n
  * Proof bytes (bpp_perm_proof_len(k)): A_I A_O S T1 T3 T4 T5 T6 | tau_x mu
  * t_hat | L_0 R_0 .. L_{lg-1} R_{lg-1} | a b.  The 2k+1 Pedersen
  * commitments V go to V_out (public inputs, 32 bytes each).  All prover
- * randomness (pi, blindings) comes from SHAKE256("bpperm-prove" || seed),
- * the injected stand-in for the reference's thread_rng (circuit_lib.rs:175). */
+ * randomness comes from the seed, the injected stand-in for the reference's
+ * thread_rng (circuit_lib.rs:175): pi from SHAKE256("bpperm-prove" || seed)
+ * (Fisher-Yates, one u64 per step), blinding scalar j (order gamma[2k+1],
+ * alpha, beta, rho, s_L[n_p], s_R[n_p], tau[5]) from the first 64 bytes of
+ * SHAKE256("bpperm-prove-sc" || seed || le32 j), reduced mod l. */
 size_t bpp_perm_proof_len(uint32_t k);
 int bpp_perm_prove(bpp_ctx* ctx, const bpp_gens* g, uint32_t k, uint64_t seed, const uint8_t* label, size_t llen,
                    uint8_t* proof_out, uint8_t* V_out, uint32_t* perm_out);
@@ -221,8 +224,8 @@ int bpp_perm_prove_batch(bpp_ctx* ctx, const bpp_gens* g, uint32_t k, size_t cou
  * a guessable seed reveals the witness).  Production proofs: 32 bytes of
  * entropy per proof from the caller (seeds32, count x 32 B), or seeds32 =
  * NULL to draw them from the OS CSPRNG (getrandom), as the reference draws
- * from thread_rng (circuit_lib.rs:175, weights.rs:39,59).  The blindings
- * are SHAKE256("bpperm-prove" || seed32) in the same draw order. */
+ * from thread_rng (circuit_lib.rs:175, weights.rs:39,59).  The draws are
+ * those above with the 32-byte seed32 in place of the 8-byte seed. */
 int bpp_perm_prove_batch_entropy(bpp_ctx* ctx, const bpp_gens* g, uint32_t k, size_t count, const uint8_t* seeds32,
                                  const uint8_t* label, size_t llen, uint8_t* proofs_out, uint8_t* V_out);
 /* BPP_OK or BPP_ERR_VERIFY (ProofError::VerificationError). One GPU MSM. */

@@ -57,7 +57,7 @@ def main():
         shutil.copy(stats, ROOT / "profiles" / f"{tag}_kernel_stats.csv")
     stats = src / "trace_proofs" / "run_kernel_stats.csv"
     if stats.exists():
-        shutil.copy(stats, ROOT / "profiles" / f"{tag}_prove_batch128_kernel_stats.csv")
+        shutil.copy(stats, ROOT / "profiles" / f"{tag}_prove_batch256_kernel_stats.csv")
     b = src / "bench.json"
     if b.exists():
         shutil.copy(b, ROOT / "profiles" / f"{tag}_bench.json")

@@ -614,8 +614,10 @@ size_t dt_bytes(uint32_t npts, uint32_t c) {
 
 int dt_build(bpp_ctx* ctx, const uint32_t* d_wt, uint32_t npts, uint32_t c, uint32_t* d_dt) {
   if (!npts) return BPP_OK;
-  if (c < 8 || c > 16) {
-    ctx->err = "dt_build: window width must be 8..16";
+  // (c <= 17: the top window's digit field of s + K < 2^254 stays below
+  // H = 2^(c-1) rows, and the row index below 2^32 for the generator sets)
+  if (c < 8 || c > 17) {
+    ctx->err = "dt_build: window width must be 8..17";
     return BPP_ERR_ARG;
   }
   const DtGeom g = dt_geom(c);

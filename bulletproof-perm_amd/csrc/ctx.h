@@ -21,6 +21,8 @@ struct bpp_ctx {
   // pinned host staging
   void* pinned = nullptr;
   size_t pinned_bytes = 0;
+  // named pinned host buffers that kernels read / write in place (ctx_host_buf)
+  std::map<std::string, std::pair<void*, size_t>> host_bufs;
   // pinned upload arena: bump-allocated, recycled after a stream sync
   uint8_t* stage = nullptr;
   size_t stage_cap = 0, stage_used = 0;
@@ -92,6 +94,11 @@ struct bpp_points {
 // Scratch buffer that grows on demand (never shrinks until ctx destroy).
 int ctx_ws(bpp_ctx* ctx, const char* name, size_t bytes, void** out);
 int ctx_pinned(bpp_ctx* ctx, size_t bytes, void** out);
+// A named pinned host buffer of at least `bytes` that kernels on this
+// context access in place (zero copy: no copy launch, and its values are
+// visible to the host once ctx_sync returns / to kernels launched after the
+// host writes them).  Grows on demand; freed by bpp_ctx_destroy.
+int ctx_host_buf(bpp_ctx* ctx, const char* name, size_t bytes, void** out);
 // Host->device copy staged through the ctx's pinned arena (pageable
 // hipMemcpyAsync measured up to ~25 ms on a 20 KB copy on the box); the host
 // buffer may be freed as soon as this returns.

@@ -61,6 +61,25 @@ int ctx_pinned(bpp_ctx* ctx, size_t bytes, void** out) {
   return BPP_OK;
 }
 
+int ctx_host_buf(bpp_ctx* ctx, const char* name, size_t bytes, void** out) {
+  auto& b = ctx->host_bufs[name];
+  if (b.second < bytes) {
+    if (b.first) BPP_HIP(hipHostFree(b.first));
+    b = {nullptr, 0};
+    void* h = nullptr;
+    BPP_HIP(hipHostMalloc(&h, bytes));
+    b = {h, bytes};
+  }
+  void* d = nullptr;
+  BPP_HIP(hipHostGetDevicePointer(&d, b.first, 0));
+  if (d != b.first) {  // (the kernels and the host share one pointer)
+    ctx->err = "ctx_host_buf: pinned buffer has a distinct device address";
+    return BPP_ERR_DEVICE;
+  }
+  *out = b.first;
+  return BPP_OK;
+}
+
 // The waiting thread polls an event with 5 us sleeps instead of
 // hipStreamSynchronize's spin: with 8-12 proof batches in flight, their
 // driver threads spinning in the HSA signal wait were ~25 % of the host CPU
@@ -235,6 +254,8 @@ void bpp_ctx_destroy(bpp_ctx* ctx) {
   for (auto& kv : ctx->ws)
     if (kv.second.p) hipFree(kv.second.p);
   if (ctx->pinned) hipHostFree(ctx->pinned);
+  for (auto& kv : ctx->host_bufs)
+    if (kv.second.first) hipHostFree(kv.second.first);
   if (ctx->stage) hipHostFree(ctx->stage);
   for (auto& p : ctx->pending) {
     hipEventDestroy(p.a);

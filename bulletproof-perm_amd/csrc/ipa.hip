@@ -414,6 +414,24 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
   // with no host round trip; L, R and the transcripts come back at the end.
   const char* dm_env = getenv("BPP_IPA_DEVICE_MERLIN");
   const bool dev_merlin = fused && dm_env && atoi(dm_env) != 0;
+  // Host round trip of the fused rounds without copy launches: the round
+  // kernel writes L/2, R/2 straight into pinned host memory and reads the
+  // challenges u, u^-1 from it (ctx_host_buf), where a device result buffer
+  // and a staged upload cost a copy launch each way per round.
+#ifdef EXP_IPA_NOZC
+  const bool zc = false;
+#else
+  const bool zc = fused && !dev_merlin;
+#endif
+  uint32_t* h_uw = nullptr;  // zc: the challenges' device words, in place
+  if (zc) {
+    void *hr = nullptr, *hu = nullptr;
+    BPP_TRY(ctx_host_buf(ctx, "ipa_res_h", (size_t)2 * P * P3_BYTES, &hr));
+    BPP_TRY(ctx_host_buf(ctx, "ipa_u_h", (size_t)P * 64, &hu));
+    d_res = hr;
+    d_u = hu;
+    h_uw = (uint32_t*)hu;
+  }
   void *d_states = nullptr, *d_lr = nullptr;
   if (dev_merlin) {
     std::vector<uint8_t> stt((size_t)P * MERLIN_DEV_STATE_BYTES);
@@ -450,6 +468,10 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
         uint8_t* lr = (uint8_t*)d_lr + (size_t)round * P * 64;
         BPP_TRY(points_compress_p3_dev(ctx, (const uint32_t*)d_res, 2 * (size_t)P, lr));
         BPP_TRY(ipa_transcript_step_dev(ctx, P, (uint8_t*)d_states, lr, (uint32_t*)d_u));
+      } else if (zc) {
+        HostScope hs(ctx, "ipa_msm");
+        BPP_TRY(ctx_sync(ctx));  // the kernel's L/2, R/2 are in host memory now
+        BPP_TRY(points_double_encode_host(ctx, (const uint32_t*)d_res, 2 * (size_t)P, enc.data()));
       } else {
         HostScope hs(ctx, "ipa_msm");
         BPP_TRY(points_double_encode_p3(ctx, (const uint32_t*)d_res, 2 * (size_t)P, enc.data()));
@@ -507,13 +529,14 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
     }
     ui = u;
     hsc::batch_invert(ui, false);
+    uint32_t* uwp = zc ? h_uw : uw.data();  // (zc: the device reads them in place)
     for (uint32_t p = 0; p < P; ++p) {  // device Montgomery forms u R, u^-1 R
       const sc um = to_dev_sc(hsc::to_mont(u[p]));
       const sc uim = to_dev_sc(hsc::to_mont(ui[p]));
-      memcpy(&uw[16 * (size_t)p], um.v, 32);
-      memcpy(&uw[16 * (size_t)p + 8], uim.v, 32);
+      memcpy(&uwp[16 * (size_t)p], um.v, 32);
+      memcpy(&uwp[16 * (size_t)p + 8], uim.v, 32);
     }
-    BPP_TRY(ctx_h2d(ctx, d_u, uw.data(), uw.size() * 4));
+    if (!zc) BPP_TRY(ctx_h2d(ctx, d_u, uw.data(), uw.size() * 4));
     }
     // the fused rounds fold inside the next round's launch; the last
     // challenge (and every challenge of the unfused path) is folded here

@@ -4,6 +4,7 @@
 
 #include <chrono>
 #include <map>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -23,6 +24,7 @@ struct bpp_ctx {
   size_t pinned_bytes = 0;
   // named pinned host buffers that kernels read / write in place (ctx_host_buf)
   std::map<std::string, std::pair<void*, size_t>> host_bufs;
+  std::set<std::string> zc_live;  // host buffers handed to kernels since the last ctx_sync
   // pinned upload arena: bump-allocated, recycled after a stream sync
   uint8_t* stage = nullptr;
   size_t stage_cap = 0, stage_used = 0;
@@ -99,6 +101,13 @@ int ctx_pinned(bpp_ctx* ctx, size_t bytes, void** out);
 // visible to the host once ctx_sync returns / to kernels launched after the
 // host writes them).  Grows on demand; freed by bpp_ctx_destroy.
 int ctx_host_buf(bpp_ctx* ctx, const char* name, size_t bytes, void** out);
+// Zero-copy exchange through such buffers, no copy launch: ctx_zc_in copies
+// `bytes` of host data into buffer `name` for kernels to read in place;
+// ctx_zc_out hands out buffer `name` for kernels to write, its contents valid
+// after the next ctx_sync.  A buffer handed out since the last ctx_sync is
+// waited for (ctx_sync) before it is handed out again.
+int ctx_zc_in(bpp_ctx* ctx, const char* name, const void* h, size_t bytes, uint32_t** d);
+int ctx_zc_out(bpp_ctx* ctx, const char* name, size_t bytes, uint32_t** d);
 // Host->device copy staged through the ctx's pinned arena (pageable
 // hipMemcpyAsync measured up to ~25 ms on a 20 KB copy on the box); the host
 // buffer may be freed as soon as this returns.

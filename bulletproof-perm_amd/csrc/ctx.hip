@@ -80,6 +80,21 @@ int ctx_host_buf(bpp_ctx* ctx, const char* name, size_t bytes, void** out) {
   return BPP_OK;
 }
 
+int ctx_zc_out(bpp_ctx* ctx, const char* name, size_t bytes, uint32_t** d) {
+  if (ctx->zc_live.count(name)) BPP_TRY(ctx_sync(ctx));
+  void* b = nullptr;
+  BPP_TRY(ctx_host_buf(ctx, name, std::max<size_t>(bytes, 32), &b));
+  ctx->zc_live.insert(name);
+  *d = (uint32_t*)b;
+  return BPP_OK;
+}
+
+int ctx_zc_in(bpp_ctx* ctx, const char* name, const void* h, size_t bytes, uint32_t** d) {
+  BPP_TRY(ctx_zc_out(ctx, name, bytes, d));
+  if (bytes) memcpy(*d, h, bytes);
+  return BPP_OK;
+}
+
 // The waiting thread polls an event with 5 us sleeps instead of
 // hipStreamSynchronize's spin: with 8-12 proof batches in flight, their
 // driver threads spinning in the HSA signal wait were ~25 % of the host CPU
@@ -99,6 +114,7 @@ int ctx_sync(bpp_ctx* ctx) {
     struct timespec ts = {0, 5000L};
     nanosleep(&ts, nullptr);
   }
+  ctx->zc_live.clear();
   ctx->stage_used = 0;
   return BPP_OK;
 }

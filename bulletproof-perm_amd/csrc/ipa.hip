@@ -357,7 +357,7 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
   BPP_TRY(ctx_ws(ctx, "ipa_fH", PN * 32, &fH));
   BPP_TRY(ctx_ws(ctx, "ipa_scal", PT * 32, &scal));
   BPP_TRY(ctx_ws(ctx, "ipa_pidx", PT * 4, &pidx));
-  BPP_TRY(ctx_ws(ctx, "ipa_qmul", (size_t)P * 32, &d_q));
+
   BPP_TRY(ctx_ws(ctx, "ipa_u", (size_t)P * 64, &d_u));
   // cross blocks per instance: enough lanes overall, at most 64
   const uint32_t cross_blocks =
@@ -373,7 +373,9 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
       const sc q = to_dev_sc(qmul[p]);
       memcpy(&qw[8 * (size_t)p], q.v, 32);
     }
-    BPP_TRY(ctx_h2d(ctx, d_q, qw.data(), qw.size() * 4));
+    uint32_t* hq = nullptr;  // read in place from pinned host memory (ctx_zc_in)
+    BPP_TRY(ctx_zc_in(ctx, "ipa_qmul_h", qw.data(), qw.size() * 4, &hq));
+    d_q = hq;
     hipLaunchKernelGGL(k_ipa_init, dim3(grid_for(PN, 256)), dim3(256), 0, ctx->stream, n, P, d_a, d_b, d_Gf, d_Hf,
                        (uint32_t*)am, (uint32_t*)bm, (uint32_t*)fG, (uint32_t*)fH);
     BPP_TRY(ctx_check_launch(ctx, "k_ipa_init"));

@@ -642,12 +642,16 @@ bool msm_use_dt(const MsmPoints& pts, uint32_t M, uint32_t T) {
 }
 
 static int msm_multi_dt_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx,
-                            const std::vector<uint32_t>& off, const MsmPoints& pts, uint32_t** d_res) {
+                            const std::vector<uint32_t>& off, const MsmPoints& pts, uint32_t** d_res,
+                            uint32_t* res_out = nullptr) {
   const uint32_t M = (uint32_t)off.size() - 1;
   const uint32_t T = off[M];
   void *d_off, *res;
   BPP_TRY(upload_offsets(ctx, off, &d_off));
-  BPP_TRY(ctx_ws(ctx, "dt_res", (size_t)M * P3_BYTES, &res));
+  if (res_out)
+    res = res_out;
+  else
+    BPP_TRY(ctx_ws(ctx, "dt_res", (size_t)M * P3_BYTES, &res));
   const DtGeom dg = dt_geom(pts.dt_c);
   // W lanes per term group: the largest multiple of W within DT_NT_MAX lanes
   // whose groups each still get about two terms (small MSMs: fewer lanes,
@@ -724,6 +728,13 @@ int msm_multi_enc(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, 
   // GPU lane per result, or (doubled) the host batch encoding of 2 R_m.
   if (M > 16 && T > 0 && (msm_use_dt(pts, M, T) || use_fb(pts, M, T))) {
     uint32_t* d_ws = nullptr;
+    if (msm_use_dt(pts, M, T) && doubled) {  // results written in place in host memory (ctx_zc_out)
+      uint32_t* h = nullptr;
+      BPP_TRY(ctx_zc_out(ctx, "multi_res_h", (size_t)M * P3_BYTES, &h));
+      BPP_TRY(msm_multi_dt_dev(ctx, d_scal, d_pidx, off, pts, &d_ws, h));
+      BPP_TRY(ctx_sync(ctx));
+      return points_double_encode_host(ctx, h, M, out_enc);
+    }
     if (msm_use_dt(pts, M, T))
       BPP_TRY(msm_multi_dt_dev(ctx, d_scal, d_pidx, off, pts, &d_ws));
     else

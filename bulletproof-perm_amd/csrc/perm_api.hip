@@ -106,13 +106,10 @@ std::vector<uint8_t> to_bytes(const std::vector<Sc>& v) {
   return b;
 }
 
+// (pinned host memory the kernels read in place: no copy launch, ctx_zc_in)
 int upload_sc(bpp_ctx* ctx, const std::vector<Sc>& v, const char* name, uint32_t** d) {
-  void* p = nullptr;
-  BPP_TRY(ctx_ws(ctx, name, v.size() * 32 + 32, &p));
   static_assert(sizeof(Sc) == 32, "Sc is the 32-byte little-endian scalar");
-  BPP_TRY(ctx_h2d(ctx, p, v.data(), v.size() * 32));  // canonical Sc == its byte encoding
-  *d = (uint32_t*)p;
-  return BPP_OK;
+  return ctx_zc_in(ctx, name, v.data(), v.size() * 32, d);  // canonical Sc == its byte encoding
 }
 
 // Fixed-base commitments v_i*B + g_i*Bb, returned compressed.
@@ -145,14 +142,15 @@ int pedersen_host(bpp_ctx* ctx, const bpp_gens* g, const std::vector<Sc>& v, con
   }
   out.resize(m);
   if (doubled) {
-    void* d_p3 = nullptr;
-    BPP_TRY(ctx_ws(ctx, "pp_p3", m * P3_BYTES, &d_p3));
+    uint32_t* h_p3 = nullptr;  // written in place by the kernel (ctx_zc_out)
+    BPP_TRY(ctx_zc_out(ctx, "pp_p3_h", m * P3_BYTES, &h_p3));
     {
       HostScope hs(ctx, "ped_kernels");
-      BPP_TRY(pedersen_dev(ctx, g, d_v, d_g, m, nullptr, (uint32_t*)d_p3));
+      BPP_TRY(pedersen_dev(ctx, g, d_v, d_g, m, nullptr, h_p3));
     }
     HostScope hs(ctx, "ped_d2h");
-    return points_double_encode_p3(ctx, (const uint32_t*)d_p3, m, out[0].data());
+    BPP_TRY(ctx_sync(ctx));
+    return points_double_encode_host(ctx, h_p3, m, out[0].data());
   }
   void* d_out = nullptr;
   BPP_TRY(ctx_ws(ctx, "pp_out", m * 32, &d_out));
@@ -245,8 +243,9 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
       }
     BPP_TRY(ctx_ws(ctx, "pb_gamma", (size_t)P * m * 32, &dg));
     BPP_TRY(ctx_ws(ctx, "mt_s", (size_t)P * per * 32 + 32, &dsc));
-    BPP_TRY(ctx_ws(ctx, "pb_tmpl", P * tlen, &dst));
-    BPP_TRY(ctx_ws(ctx, "pb_pi", (size_t)P * k * 4, &dpi));
+    // templates then pi, one device buffer filled by one copy
+    BPP_TRY(ctx_ws(ctx, "pb_rng_in", P * tlen + (size_t)P * k * 4, &dst));
+    dpi = (uint8_t*)dst + P * tlen;
     d_gamma = (uint32_t*)dg;
     d_s = (uint32_t*)dsc;
     d_pi = (uint32_t*)dpi;
@@ -278,8 +277,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
       }
 #endif
     });
-    BPP_TRY(ctx_h2d_staged(ctx, dst, stage, P * tlen));
-    BPP_TRY(ctx_h2d_staged(ctx, d_pi, pis, (size_t)P * k * 4));
+    BPP_TRY(ctx_h2d_staged(ctx, dst, stage, P * tlen + (size_t)P * k * 4));  // (pis follows the templates)
     BPP_TRY(draws_dev(ctx, C, (uint32_t)P, (const uint64_t*)dst, P ? seeds[0].len : 0, per, d_gamma, d_s));
   }
   // V_0..V_2k-1 of every proof: one fixed-base launch over device inputs
@@ -292,7 +290,11 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     BPP_TRY(ctx_ws(ctx, "pv_v", nv * 32, &dv));
     BPP_TRY(ctx_ws(ctx, "pv_g", nv * 32, &dg));
     BPP_TRY(ctx_ws(ctx, "pv_gx", (size_t)P * 32, &dgx));
-    BPP_TRY(ctx_ws(ctx, "pv_enc", nv * 32, &denc));
+    {
+      uint32_t* h = nullptr;  // encodings written in place by k_compress_p3 (ctx_zc_out)
+      BPP_TRY(ctx_zc_out(ctx, "pv_enc_h", nv * 32, &h));
+      denc = h;
+    }
     d_gx_half = (uint32_t*)dgx;
     BPP_TRY(v_inputs_dev(ctx, C, (uint32_t)P, d_pi, d_gamma, (uint32_t*)dv, (uint32_t*)dg, d_gx_half));
     {
@@ -305,7 +307,8 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     V.resize(nv);
     {
       HostScope hd(ctx, "ped_d2h");
-      BPP_TRY(ctx_d2h(ctx, V.data(), denc, nv * 32));
+      BPP_TRY(ctx_sync(ctx));
+      memcpy(V.data(), denc, nv * 32);
     }
     par::for_each(P, [&](size_t p) { Ps[p].V.assign(V.begin() + p * 2 * k, V.begin() + (p + 1) * 2 * k); });
     // the 2k "V" appends and x_perm of eight proofs at a time in lockstep
@@ -340,11 +343,12 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     uint32_t* d_vh = nullptr;
     BPP_TRY(upload_sc(ctx, vh, "pv_vx", &d_vh));
     if (dev_witness) BPP_TRY(witness_dev(ctx, C, (uint32_t)P, d_pi, d_vh + 8 * P, per, d_s));
-    void* d_p3 = nullptr;
-    BPP_TRY(ctx_ws(ctx, "pp_p3", P * P3_BYTES, &d_p3));
-    BPP_TRY(pedersen_dev(ctx, G, d_vh, d_gx_half, P, nullptr, (uint32_t*)d_p3));
+    uint32_t* h_p3 = nullptr;  // written in place by the kernel (ctx_zc_out)
+    BPP_TRY(ctx_zc_out(ctx, "pv_p3_h", P * P3_BYTES, &h_p3));
+    BPP_TRY(pedersen_dev(ctx, G, d_vh, d_gx_half, P, nullptr, h_p3));
     std::vector<Enc32> Vx(P);
-    BPP_TRY(points_double_encode_p3(ctx, (const uint32_t*)d_p3, P, Vx[0].data()));
+    BPP_TRY(ctx_sync(ctx));
+    BPP_TRY(points_double_encode_host(ctx, h_p3, P, Vx[0].data()));
     par::for_each(P, [&](size_t p) {
       Ps[p].V.push_back(Vx[p]);
       S[p]->tr.append_point("V", Vx[p].data());

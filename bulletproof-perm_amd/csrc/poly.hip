@@ -633,13 +633,18 @@ int poly_coef_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint32
   void *d_cp, *d_ce, *d_ch, *d_vec, *d_hf, *d_t;
   BPP_TRY(ctx_ws(ctx, "poly_cp", cp.size() * 4, &d_cp));
   BPP_TRY(ctx_ws(ctx, "poly_ce", ce.size() * 4 + 4, &d_ce));
-  BPP_TRY(ctx_ws(ctx, "poly_ch", ch.size() * 32, &d_ch));
+
   BPP_TRY(ctx_ws(ctx, "poly_vec", (size_t)P * C.n_p * POLY_SLOTS * 32, &d_vec));
   BPP_TRY(ctx_ws(ctx, "poly_hf", (size_t)P * C.n_p * 32, &d_hf));
-  BPP_TRY(ctx_ws(ctx, "poly_t", (size_t)P * POLY_NT * 32, &d_t));
+  {  // challenges in, t out: pinned host memory the kernel reads / writes in place
+    uint32_t *hc = nullptr, *ht = nullptr;
+    BPP_TRY(ctx_zc_in(ctx, "poly_ch_h", ch.data(), ch.size() * 32, &hc));
+    BPP_TRY(ctx_zc_out(ctx, "poly_t_h", (size_t)P * POLY_NT * 32, &ht));
+    d_ch = hc;
+    d_t = ht;
+  }
   BPP_TRY(ctx_h2d_const(ctx, "poly_cp", d_cp, cp.data(), cp.size() * 4));  // the circuit: same every batch
   BPP_TRY(ctx_h2d_const(ctx, "poly_ce", d_ce, ce.data(), ce.size() * 4));
-  BPP_TRY(ctx_h2d(ctx, d_ch, ch.data(), ch.size() * 32));
   const unsigned nt = poly_block(std::max(C.n_p, C.m));
   const size_t lds = ((size_t)C.Q + 1 + 2 * std::min(C.n_p, (uint32_t)POW_LO)) * 32 + (POLY_T / 64) * POLY_NT * 32;
   {
@@ -650,19 +655,26 @@ int poly_coef_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint32
   }
   BPP_TRY(ctx_check_launch(ctx, "k_poly_coef"));
   t.resize((size_t)P * POLY_NT);
-  return ctx_d2h(ctx, t.data(), d_t, (size_t)P * POLY_NT * 32);
+  BPP_TRY(ctx_sync(ctx));
+  memcpy(t.data(), d_t, (size_t)P * POLY_NT * 32);
+  return BPP_OK;
 }
 
 int poly_x_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const std::vector<hsc::Sc>& x, uint32_t** d_l,
                uint32_t** d_r, uint32_t** d_hf, std::vector<hsc::Sc>& t_hat) {
   void *d_x, *d_vec, *d_lo, *d_ro, *d_th, *hf;
-  BPP_TRY(ctx_ws(ctx, "poly_x", (size_t)P * 32, &d_x));
+
   BPP_TRY(ctx_ws(ctx, "poly_vec", (size_t)P * C.n_p * POLY_SLOTS * 32, &d_vec));
   BPP_TRY(ctx_ws(ctx, "poly_hf", (size_t)P * C.n_p * 32, &hf));
   BPP_TRY(ctx_ws(ctx, "pf_l", (size_t)P * C.n_p * 32 + 32, &d_lo));
   BPP_TRY(ctx_ws(ctx, "pf_r", (size_t)P * C.n_p * 32 + 32, &d_ro));
-  BPP_TRY(ctx_ws(ctx, "poly_that", (size_t)P * 32, &d_th));
-  BPP_TRY(ctx_h2d(ctx, d_x, x.data(), (size_t)P * 32));
+  {  // x in, t_hat out: in place in pinned host memory
+    uint32_t *hx = nullptr, *hth = nullptr;
+    BPP_TRY(ctx_zc_in(ctx, "poly_x_h", x.data(), (size_t)P * 32, &hx));
+    BPP_TRY(ctx_zc_out(ctx, "poly_that_h", (size_t)P * 32, &hth));
+    d_x = hx;
+    d_th = hth;
+  }
   {
     ProfScope ps(ctx, "poly_x");
     hipLaunchKernelGGL(k_poly_x, dim3(P), dim3(poly_block(C.n_p)), 0, ctx->stream, C.n_p, (const uint32_t*)d_x,
@@ -670,7 +682,8 @@ int poly_x_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const std::vect
   }
   BPP_TRY(ctx_check_launch(ctx, "k_poly_x"));
   t_hat.resize(P);
-  BPP_TRY(ctx_d2h(ctx, t_hat.data(), d_th, (size_t)P * 32));
+  BPP_TRY(ctx_sync(ctx));
+  memcpy(t_hat.data(), d_th, (size_t)P * 32);
   *d_l = (uint32_t*)d_lo;
   *d_r = (uint32_t*)d_ro;
   *d_hf = (uint32_t*)hf;

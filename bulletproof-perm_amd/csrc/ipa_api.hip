@@ -25,10 +25,13 @@ int decompress_ws(bpp_ctx* ctx, const uint8_t* enc, size_t count, const char* na
   BPP_TRY(ctx_ws(ctx, name, (count ? count : 1) * MSM_NIELS_WORDS * 4, &d_tbl));
   *d_out = (uint32_t*)d_tbl;
   if (!count) return BPP_OK;
-  BPP_TRY(ctx_ws(ctx, "dws_enc", count * 32, &d_enc));
+  {  // encodings read in place from pinned host memory (ctx_zc_in)
+    uint32_t* h = nullptr;
+    BPP_TRY(ctx_zc_in(ctx, "dws_enc_h", enc, count * 32, &h));
+    d_enc = h;
+  }
   BPP_TRY(ctx_ws(ctx, "dws_bad", 8, &d_bad));
   unsigned long long bad = ~0ull;
-  BPP_TRY(ctx_h2d(ctx, d_enc, enc, count * 32));
   BPP_TRY(ctx_h2d(ctx, d_bad, &bad, 8));
   hipLaunchKernelGGL(k_decompress, dim3(grid_for(count, 64)), dim3(64), 0, ctx->stream, (const uint32_t*)d_enc, count,
                      (uint32_t*)d_tbl, (unsigned long long*)d_bad);

@@ -701,12 +701,16 @@ int verify_scalars_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, con
   BPP_TRY(ctx_ws(ctx, "vs_cp", cp.size() * 4, &d_cp));
   BPP_TRY(ctx_ws(ctx, "vs_ce", ce.size() * 4 + 4, &d_ce));
   BPP_TRY(ctx_ws(ctx, "vs_c", cw.size() * 4, &d_c));
-  BPP_TRY(ctx_ws(ctx, "vs_rec", rec.size() * 4, &d_rec));
+
   BPP_TRY(ctx_ws(ctx, "vs_gen", (size_t)count * NG * 32, &d_gen));
   BPP_TRY(ctx_h2d_const(ctx, "vs_cp", d_cp, cp.data(), cp.size() * 4));  // the circuit: same every batch
   BPP_TRY(ctx_h2d_const(ctx, "vs_ce", d_ce, ce.data(), ce.size() * 4));
   BPP_TRY(ctx_h2d_const(ctx, "vs_c", d_c, cw.data(), cw.size() * 4));
-  BPP_TRY(ctx_h2d(ctx, d_rec, rec.data(), rec.size() * 4));
+  {  // per-proof records read in place from pinned host memory (ctx_zc_in)
+    uint32_t* h = nullptr;
+    BPP_TRY(ctx_zc_in(ctx, "vs_rec_h", rec.data(), rec.size() * 4, &h));
+    d_rec = h;
+  }
   const unsigned nt = poly_block(std::max(C.n_p, C.m));
   const size_t lds = ((size_t)C.Q + 1 + 2 * std::min(C.n_p, (uint32_t)POW_LO)) * 32 + (POLY_T / 64) * 2 * 32;
   {

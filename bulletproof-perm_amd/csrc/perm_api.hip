@@ -106,10 +106,18 @@ std::vector<uint8_t> to_bytes(const std::vector<Sc>& v) {
   return b;
 }
 
-// (pinned host memory the kernels read in place: no copy launch, ctx_zc_in)
+// Small vectors go to pinned host memory the kernels read in place (no copy
+// launch, ctx_zc_in); large ones (vector commitments of many terms, whose
+// scalars every window lane re-reads) are copied to the device.
+#define UPLOAD_ZC_MAX (256u << 10)
 int upload_sc(bpp_ctx* ctx, const std::vector<Sc>& v, const char* name, uint32_t** d) {
-  static_assert(sizeof(Sc) == 32, "Sc is the 32-byte little-endian scalar");
-  return ctx_zc_in(ctx, name, v.data(), v.size() * 32, d);  // canonical Sc == its byte encoding
+  static_assert(sizeof(Sc) == 32, "Sc is the 32-byte little-endian scalar");  // canonical Sc == its bytes
+  if (v.size() * 32 <= UPLOAD_ZC_MAX) return ctx_zc_in(ctx, name, v.data(), v.size() * 32, d);
+  void* p = nullptr;
+  BPP_TRY(ctx_ws(ctx, name, v.size() * 32 + 32, &p));
+  BPP_TRY(ctx_h2d(ctx, p, v.data(), v.size() * 32));
+  *d = (uint32_t*)p;
+  return BPP_OK;
 }
 
 // Fixed-base commitments v_i*B + g_i*Bb, returned compressed.
@@ -249,7 +257,8 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     d_gamma = (uint32_t*)dg;
     d_s = (uint32_t*)dsc;
     d_pi = (uint32_t*)dpi;
-    // (one staging region: a second take could recycle the arena under the first)
+    // (one staging region: a second take could recycle the arena under the first;
+    // read in place instead, by k_draws through LDS, measured within noise)
     uint8_t* stage = nullptr;
     BPP_TRY(ctx_h2d_stage(ctx, P * tlen + (size_t)P * k * 4, &stage));
     uint8_t* pis = stage + P * tlen;

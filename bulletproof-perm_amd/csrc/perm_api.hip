@@ -287,10 +287,17 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
 #endif
     });
     BPP_TRY(ctx_h2d_staged(ctx, dst, stage, P * tlen + (size_t)P * k * 4));  // (pis follows the templates)
-    BPP_TRY(draws_dev(ctx, C, (uint32_t)P, (const uint64_t*)dst, P ? seeds[0].len : 0, per, d_gamma, d_s));
+    // (the V commitments' inputs in the same launch: values 1..k and pi + 1,
+    // gamma copies and gamma_2k / 2, into the V phase's workspaces)
+    void *dv = nullptr, *dgv = nullptr, *dgx = nullptr;
+    BPP_TRY(ctx_ws(ctx, "pv_v", (size_t)P * 2 * k * 32, &dv));
+    BPP_TRY(ctx_ws(ctx, "pv_g", (size_t)P * 2 * k * 32, &dgv));
+    BPP_TRY(ctx_ws(ctx, "pv_gx", (size_t)P * 32, &dgx));
+    BPP_TRY(draws_dev(ctx, C, (uint32_t)P, (const uint64_t*)dst, P ? seeds[0].len : 0, per, d_gamma, d_s, d_pi,
+                      (uint32_t*)dv, (uint32_t*)dgv, (uint32_t*)dgx));
   }
   // V_0..V_2k-1 of every proof: one fixed-base launch over device inputs
-  // (values 1..k, pi + 1 and gamma, k_v_inputs), encodings back to the host
+  // (values 1..k, pi + 1 and gamma, written by k_draws), encodings back to the host
   hs.reset(new HostScope(ctx, "pb_pedersen_V"));
   uint32_t* d_gx_half = nullptr;  // gamma_2k / 2 for V_2k
   {
@@ -304,8 +311,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
       BPP_TRY(ctx_zc_out(ctx, "pv_enc_h", nv * 32, &h));
       denc = h;
     }
-    d_gx_half = (uint32_t*)dgx;
-    BPP_TRY(v_inputs_dev(ctx, C, (uint32_t)P, d_pi, d_gamma, (uint32_t*)dv, (uint32_t*)dg, d_gx_half));
+    d_gx_half = (uint32_t*)dgx;  // (filled by k_draws above)
     {
       HostScope hk(ctx, "ped_kernels");
       // (values 1..k and pi + 1 <= k: the public bound k + 1)
@@ -341,7 +347,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
         });
   }
   // V_2k = commit(x_perm, gamma_2k): halved scalars (x_perm / 2 from the
-  // host, gamma_2k / 2 from k_v_inputs), encoded as 2 (C / 2) on the host
+  // host, gamma_2k / 2 from k_draws), encoded as 2 (C / 2) on the host
   hs.reset(new HostScope(ctx, "pb_pedersen_Vx_witness"));
   {
     std::vector<Sc> vh(2 * P);  // x_perm / 2 (V_2k), then x_perm (the device witness)

@@ -32,14 +32,14 @@ int verify_scalars_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, con
 // draw_template; seed_len uniform over the batch, <= 32) -> gamma ([P][m],
 // canonical) and alpha, beta, rho, s_L, s_R into their slots of the
 // A_I/A_O/S scalar array d_sc ([P][per]).
+// With d_v non-null, also the V commitment inputs from pi ([P][k] u32):
+// d_v, d_g [P][2k] (values 1..k and pi + 1; gamma_0..2k-1) and d_gx_half [P]
+// = gamma_2k / 2, in the same launch.
 int draws_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint64_t* d_tmpl, uint32_t seed_len,
-              uint32_t per, uint32_t* d_gamma, uint32_t* d_sc);
+              uint32_t per, uint32_t* d_gamma, uint32_t* d_sc, const uint32_t* d_pi = nullptr,
+              uint32_t* d_v = nullptr, uint32_t* d_g = nullptr, uint32_t* d_gx_half = nullptr);
 void draw_template(const perm::Seed& seed, uint64_t tmpl[7]);
 
-// V commitment inputs on the device from pi ([P][k] u32) and gamma:
-// d_v, d_g [P][2k] and d_gx_half [P] = gamma_2k / 2.
-int v_inputs_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint32_t* d_pi, const uint32_t* d_gamma,
-                 uint32_t* d_v, uint32_t* d_g, uint32_t* d_gx_half);
 
 // The witness a_L, a_R, a_O of every proof (x = x_perm [P] canonical, pi
 // [P][k]) into their slots of d_sc.

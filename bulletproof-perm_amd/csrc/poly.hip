@@ -408,9 +408,15 @@ __global__ void __launch_bounds__(POLY_T) k_verify_merge(uint32_t count, uint32_
 // bytes that from_wide reduces.  gamma -> [P][m]; alpha, beta, rho, s_L, s_R
 // -> their slots of the A_I/A_O/S scalar array ([alpha, a_L, a_R, beta, a_O,
 // rho, s_L, s_R], per words x 8 a proof); the host draws tau itself.
+// With v (non-null) it also writes the V commitments' inputs (gamma_j's
+// thread, j <= 2k): v[p][i] = i + 1 (i < k) or pi_p[i - k] + 1 (k <= i < 2k),
+// g[p][i] = gamma_i, gx_half[p] = gamma_2k / 2 (V_2k is committed with halved
+// scalars and encoded as 2 (C / 2) on the host) -- no launch of its own.
 __global__ void __launch_bounds__(256) k_draws(uint32_t P, uint32_t m, uint32_t n_p, uint32_t per, uint32_t jo,
                                               const uint64_t* __restrict__ tmpl, uint32_t* __restrict__ gamma,
-                                              uint32_t* __restrict__ sc_out) {
+                                              uint32_t* __restrict__ sc_out, uint32_t k,
+                                              const uint32_t* __restrict__ pi, uint32_t* __restrict__ v,
+                                              uint32_t* __restrict__ g, uint32_t* __restrict__ gx_half) {
   const uint32_t nw = m + 3 + 2 * n_p;  // gamma[m], alpha, beta, rho, s_L[n_p], s_R[n_p]
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (size_t)P * nw) return;
@@ -432,6 +438,16 @@ __global__ void __launch_bounds__(256) k_draws(uint32_t P, uint32_t m, uint32_t 
   const sc x = sc_from_wide_w(w);
   if (j < m) {
     sc_store(gamma + 8 * ((size_t)p * m + j), x);
+    if (v) {
+      if (j == 2 * k) {
+        sc_store(gx_half + 8 * (size_t)p, sc_half(x));
+      } else if (j < 2 * k) {
+        sc vv = sc_zero();
+        vv.v[0] = j < k ? j + 1 : pi[(size_t)p * k + (j - k)] + 1;
+        sc_store(v + 8 * ((size_t)p * 2 * k + j), vv);
+        sc_store(g + 8 * ((size_t)p * 2 * k + j), x);
+      }
+    }
     return;
   }
   const uint32_t q = j - m;
@@ -534,28 +550,9 @@ int witness_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint32_t
   return ctx_check_launch(ctx, "k_witness");
 }
 
-// Inputs of the V commitments: v[p][i] = i + 1 (i < k), pi_p[i - k] + 1
-// (k <= i < 2k), g[p][i] = gamma[p][i]; gx[p] = gamma[p][2k] / 2 (V_2k is
-// committed with halved scalars and encoded as 2 (C / 2) on the host).
-__global__ void __launch_bounds__(256) k_v_inputs(uint32_t P, uint32_t k, uint32_t m, const uint32_t* __restrict__ pi,
-                                                 const uint32_t* __restrict__ gamma, uint32_t* __restrict__ v,
-                                                 uint32_t* __restrict__ g, uint32_t* __restrict__ gx_half) {
-  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (size_t)P * (2 * k + 1)) return;
-  const uint32_t p = (uint32_t)(t / (2 * k + 1)), i = (uint32_t)(t % (2 * k + 1));
-  const sc gm = sc_load(gamma + 8 * ((size_t)p * m + i));
-  if (i == 2 * k) {
-    sc_store(gx_half + 8 * (size_t)p, sc_half(gm));
-    return;
-  }
-  sc vv = sc_zero();
-  vv.v[0] = i < k ? i + 1 : pi[(size_t)p * k + (i - k)] + 1;
-  sc_store(v + 8 * ((size_t)p * 2 * k + i), vv);
-  sc_store(g + 8 * ((size_t)p * 2 * k + i), gm);
-}
-
 int draws_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint64_t* d_tmpl, uint32_t seed_len,
-              uint32_t per, uint32_t* d_gamma, uint32_t* d_sc) {
+              uint32_t per, uint32_t* d_gamma, uint32_t* d_sc, const uint32_t* d_pi, uint32_t* d_v, uint32_t* d_g,
+              uint32_t* d_gx_half) {
   if (!P) return BPP_OK;
   if (seed_len > 32) {
     ctx->err = "draws_dev: seed longer than 32 bytes";
@@ -563,7 +560,8 @@ int draws_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint64_t* 
   }
   const size_t nt = (size_t)P * (C.m + 3 + 2 * C.n_p);
   hipLaunchKernelGGL(k_draws, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, ctx->stream, P, C.m, C.n_p, per,
-                     (uint32_t)(BPP_DRAW_DOMAIN_LEN + seed_len), d_tmpl, d_gamma, d_sc);
+                     (uint32_t)(BPP_DRAW_DOMAIN_LEN + seed_len), d_tmpl, d_gamma, d_sc, C.k, d_pi, d_v, d_g,
+                     d_gx_half);
   return ctx_check_launch(ctx, "k_draws");
 }
 
@@ -575,14 +573,6 @@ void draw_template(const perm::Seed& seed, uint64_t tmpl[7]) {
   memcpy(tmpl, b, 56);
 }
 
-int v_inputs_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint32_t* d_pi, const uint32_t* d_gamma,
-                 uint32_t* d_v, uint32_t* d_g, uint32_t* d_gx_half) {
-  if (!P) return BPP_OK;
-  const size_t nt = (size_t)P * (2 * C.k + 1);
-  hipLaunchKernelGGL(k_v_inputs, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, ctx->stream, P, C.k, C.m, d_pi,
-                     d_gamma, d_v, d_g, d_gx_half);
-  return ctx_check_launch(ctx, "k_v_inputs");
-}
 
 namespace {
 

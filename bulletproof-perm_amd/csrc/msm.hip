@@ -643,7 +643,7 @@ bool msm_use_dt(const MsmPoints& pts, uint32_t M, uint32_t T) {
 
 static int msm_multi_dt_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx,
                             const std::vector<uint32_t>& off, const MsmPoints& pts, uint32_t** d_res,
-                            uint32_t* res_out = nullptr) {
+                            uint32_t* res_out = nullptr, const uint32_t* d_smap = nullptr) {
   const uint32_t M = (uint32_t)off.size() - 1;
   const uint32_t T = off[M];
   void *d_off, *res;
@@ -671,7 +671,7 @@ static int msm_multi_dt_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t
   {
     ProfScope ps(ctx, "msm_direct");
     hipLaunchKernelGGL(k_dt_msm, dim3(M), dim3(nt), (size_t)nt * P3_BYTES, ctx->stream, pts.dt, dg, d_scal, d_pidx,
-                       (const uint32_t*)d_off, (uint32_t*)res);
+                       (const uint32_t*)d_off, (uint32_t*)res, d_smap);
   }
   BPP_TRY(ctx_check_launch(ctx, "k_dt_msm"));
   *d_res = (uint32_t*)res;
@@ -720,10 +720,17 @@ int msm_multi(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, cons
 }
 
 int msm_multi_enc(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const std::vector<uint32_t>& off,
-                  const MsmPoints& pts, uint8_t* out_enc, bool doubled) {
+                  const MsmPoints& pts, uint8_t* out_enc, bool doubled, const uint32_t* d_smap) {
   const uint32_t M = (uint32_t)off.size() - 1;
   const uint32_t T = off[M];
   if (M == 0) return BPP_OK;
+  if (d_smap && !(doubled && M > 16 && T > 0 && msm_use_dt(pts, M, T))) {
+    // (only the direct-table kernel gathers and halves in place)
+    void* d_sh = nullptr;
+    BPP_TRY(ctx_ws(ctx, "mt_s_half", (size_t)T * 32 + 32, &d_sh));
+    BPP_TRY(sc_halve_gather_dev(ctx, d_scal, d_smap, (uint32_t*)d_sh, T));
+    return msm_multi_enc(ctx, (const uint32_t*)d_sh, d_pidx, off, pts, out_enc, doubled, nullptr);
+  }
   // Few results: host encoding beats a latency-bound GPU launch; many: one
   // GPU lane per result, or (doubled) the host batch encoding of 2 R_m.
   if (M > 16 && T > 0 && (msm_use_dt(pts, M, T) || use_fb(pts, M, T))) {
@@ -731,7 +738,7 @@ int msm_multi_enc(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, 
     if (msm_use_dt(pts, M, T) && doubled) {  // results written in place in host memory (ctx_zc_out)
       uint32_t* h = nullptr;
       BPP_TRY(ctx_zc_out(ctx, "multi_res_h", (size_t)M * P3_BYTES, &h));
-      BPP_TRY(msm_multi_dt_dev(ctx, d_scal, d_pidx, off, pts, &d_ws, h));
+      BPP_TRY(msm_multi_dt_dev(ctx, d_scal, d_pidx, off, pts, &d_ws, h, d_smap));
       BPP_TRY(ctx_sync(ctx));
       return points_double_encode_host(ctx, h, M, out_enc);
     }

@@ -69,8 +69,11 @@ int msm_multi(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, cons
 // doubled: d_scal holds halved scalars s/2 and out_enc gets the encodings of
 // 2 * result (host batch encoding, one inversion instead of a per-point
 // inverse square root)
+// d_smap (optional, with doubled): term t's scalar is d_scal[d_smap[t]] / 2
+// (gathered and halved inside the direct-table kernel; a gather pass first
+// on the other engines)
 int msm_multi_enc(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const std::vector<uint32_t>& off,
                   const MsmPoints& pts, uint8_t* out_enc,
-                  bool doubled = false);
+                  bool doubled = false, const uint32_t* d_smap = nullptr);
 int msm_multi(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const std::vector<uint32_t>& off,
               const uint32_t* d_tbl, const uint32_t* d_tbl1, uint32_t n0, std::vector<h25519::ge>& out);

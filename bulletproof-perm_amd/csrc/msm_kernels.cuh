@@ -856,11 +856,14 @@ __global__ void __launch_bounds__(RS_FT) k_rsort_fine(const uint32_t* __restrict
 // the W lanes sharing a term read the same 32 scalar bytes.  Then an LDS
 // tree over the block's lanes.
 #include "dt_walk.cuh"
+#include "sc25519.cuh"
 
+// smap (optional): term t's scalar is scalars[smap[t]] / 2 mod l (the
+// prover's halved, compacted A_I/A_O/S terms without a gather pass)
 __global__ void __launch_bounds__(DT_NT_MAX) k_dt_msm(const uint32_t* __restrict__ dt, DtGeom dg,
                                                     const uint32_t* __restrict__ scalars,
                                                     const uint32_t* __restrict__ pidx, const uint32_t* __restrict__ off,
-                                                    uint32_t* __restrict__ out_p3) {
+                                                    uint32_t* __restrict__ out_p3, const uint32_t* __restrict__ smap) {
   extern __shared__ uint32_t tl[];  // blockDim.x extended points (40 KB at 256 lanes)
   const uint32_t nt = blockDim.x, TG = nt / dg.W;
   const uint32_t m = blockIdx.x;
@@ -872,7 +875,12 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_dt_msm(const uint32_t* __restrict
 #endif
   const ge_p3 acc = tg < TG ? dt_walk(dt, dg, ln, off[m] + tg, off[m + 1], TG,
                                       [&](uint32_t t, uint32_t s[8], uint32_t& gen) {
-                                        load_scalar(scalars, t, s);
+                                        if (smap) {
+                                          const sc h = sc_half(sc_load(scalars + 8 * (size_t)smap[t]));
+                                          _Pragma("unroll") for (int i = 0; i < 8; ++i) s[i] = h.v[i];
+                                        } else {
+                                          load_scalar(scalars, t, s);
+                                        }
                                         gen = pidx ? pidx[t] : t;
                                       })
                             : ge_identity();

@@ -432,11 +432,9 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     BPP_TRY(ctx_ws(ctx, "mt_map", map.size() * 4 + 4, &d_map));
     BPP_TRY(ctx_h2d_const(ctx, "mt_map", d_map, map.data(), map.size() * 4));
     // MSMs of the halved, compacted scalars, encoded as 2 * result (msm_multi_enc)
-    void* d_sh = nullptr;
-    BPP_TRY(ctx_ws(ctx, "mt_s_half", map.size() * 32 + 32, &d_sh));
-    BPP_TRY(sc_halve_gather_dev(ctx, d_s, (const uint32_t*)d_map, (uint32_t*)d_sh, map.size()));
+    // (gathered and halved inside the direct-table kernel: d_map)
     std::vector<uint8_t> enc(3 * P * 32);
-    BPP_TRY(msm_multi_enc(ctx, (const uint32_t*)d_sh, (const uint32_t*)d_i, off, pts, enc.data(), true));
+    BPP_TRY(msm_multi_enc(ctx, d_s, (const uint32_t*)d_i, off, pts, enc.data(), true, (const uint32_t*)d_map));
     par::for_each(P, [&](size_t p) {
       memcpy(Ps[p].AI.data(), &enc[96 * p], 32);
       memcpy(Ps[p].AO.data(), &enc[96 * p + 32], 32);

@@ -213,7 +213,8 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
     const uint32_t* __restrict__ fH_in, uint32_t* __restrict__ am_out, uint32_t* __restrict__ bm_out,
     uint32_t* __restrict__ fG_out, uint32_t* __restrict__ fH_out, const uint32_t* __restrict__ u,
     const uint32_t* __restrict__ qmul, uint32_t gbase, uint32_t hbase, uint32_t qidx, uint32_t TG, uint32_t halve,
-    uint32_t* __restrict__ out_p3) {
+    uint32_t* __restrict__ out_p3, const uint32_t* __restrict__ a0, const uint32_t* __restrict__ b0,
+    const uint32_t* __restrict__ gf0, const uint32_t* __restrict__ hf0, uint32_t init) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* tsc = lds;                           // (n + 1) x 8 words: halved term scalars
   uint32_t* tgen = lds + 8 * (n + 1);            // n + 1 generator indices
@@ -223,7 +224,10 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
   const uint32_t nt = blockDim.x, tid = threadIdx.x;
   const uint32_t inst = blockIdx.x >> 1, side = blockIdx.x & 1u;
   const size_t ib = (size_t)inst * n;
-  const bool writer = fold && side == 0;
+  // init (the first round, no fold): a, b and the generator factors come
+  // from the caller's canonical arrays a0, b0, gf0, hf0 (null: all one), and
+  // side 0 writes the Montgomery state that round 1 folds (k_ipa_init's work)
+  const bool writer = (fold || init) && side == 0;
   sc um = sc_zero(), uim = sc_zero();
   if (fold) {
     um = sc_load(u + 16 * inst);
@@ -241,6 +245,9 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
       x = sc_add(sc_mont(sc_load(in + 8 * (ib + p)), isb ? uim : um),
                  sc_mont(sc_load(in + 8 * (ib + p + m)), isb ? um : uim));
       if (writer) sc_store((isb ? bm_out : am_out) + 8 * (ib + p), x);
+    } else if (init) {
+      x = sc_to_mont(sc_load((isb ? b0 : a0) + 8 * (ib + p)));
+      if (writer) sc_store((isb ? bm_out : am_out) + 8 * (ib + p), x);
     } else {
       x = sc_load(in + 8 * (ib + p));
     }
@@ -253,7 +260,19 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
   for (uint32_t q = tid; q < 2 * n; q += nt) {
     const bool ish = q >= n;
     const uint32_t k = ish ? q - n : q;
-    sc f = sc_load((ish ? fH_in : fG_in) + 8 * (ib + k));
+    sc f;
+    if (init) {
+      const uint32_t* r = ish ? hf0 : gf0;
+      if (r) {
+        f = sc_load(r + 8 * (ib + k));
+      } else {
+        f = sc_zero();
+        f.v[0] = 1;
+      }
+      if (writer) sc_store((ish ? fH_out : fG_out) + 8 * (ib + k), f);
+    } else {
+      f = sc_load((ish ? fH_in : fG_in) + 8 * (ib + k));
+    }
     if (fold) {
       const bool hi_prev = (k & (2 * m - 1)) & m;
       f = sc_mont(f, hi_prev != ish ? um : uim);
@@ -376,9 +395,6 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
     uint32_t* hq = nullptr;  // read in place from pinned host memory (ctx_zc_in)
     BPP_TRY(ctx_zc_in(ctx, "ipa_qmul_h", qw.data(), qw.size() * 4, &hq));
     d_q = hq;
-    hipLaunchKernelGGL(k_ipa_init, dim3(grid_for(PN, 256)), dim3(256), 0, ctx->stream, n, P, d_a, d_b, d_Gf, d_Hf,
-                       (uint32_t*)am, (uint32_t*)bm, (uint32_t*)fG, (uint32_t*)fH);
-    BPP_TRY(ctx_check_launch(ctx, "k_ipa_init"));
   }
   std::vector<uint32_t> off(2 * (size_t)P + 1);
   for (uint32_t p = 0; p < P; ++p) {
@@ -393,6 +409,11 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
   // tables: the state (a, b, fG, fH) alternates between two sets so that a
   // round's blocks read the previous state while side 0 writes the next.
   const bool fused = n >= 2 && n <= IPA_FUSED_NMAX && !g.pts.tbl1 && msm_use_dt(g.pts, 2 * P, (uint32_t)PT);
+  if (!fused) {  // (the fused first round converts the inputs itself)
+    hipLaunchKernelGGL(k_ipa_init, dim3(grid_for(PN, 256)), dim3(256), 0, ctx->stream, n, P, d_a, d_b, d_Gf, d_Hf,
+                       (uint32_t*)am, (uint32_t*)bm, (uint32_t*)fG, (uint32_t*)fH);
+    BPP_TRY(ctx_check_launch(ctx, "k_ipa_init"));
+  }
   uint32_t* S[2][4] = {{(uint32_t*)am, (uint32_t*)bm, (uint32_t*)fG, (uint32_t*)fH}, {nullptr, nullptr, nullptr, nullptr}};
   void* d_res = nullptr;
   DtGeom dg;
@@ -453,8 +474,10 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
         ProfScope ps(ctx, "msm_direct");
         hipLaunchKernelGGL(k_ipa_round_dt, dim3(2 * P), dim3(nt), ipa_round_lds_words(n, nt) * 4, ctx->stream,
                            g.pts.dt, dg, n, m, lg_h, round ? 1u : 0u, S[in][0], S[in][1], S[in][2], S[in][3],
-                           S[outs][0], S[outs][1], S[outs][2], S[outs][3], (const uint32_t*)d_u, (const uint32_t*)d_q,
-                           g.gbase, g.hbase, g.qidx, TG, dev_merlin ? 0u : 1u, (uint32_t*)d_res);
+                           S[round ? outs : in][0], S[round ? outs : in][1], S[round ? outs : in][2],
+                           S[round ? outs : in][3], (const uint32_t*)d_u, (const uint32_t*)d_q, g.gbase, g.hbase,
+                           g.qidx, TG, dev_merlin ? 0u : 1u, (uint32_t*)d_res, d_a, d_b, d_Gf, d_Hf,
+                           round ? 0u : 1u);
       }
       BPP_TRY(ctx_check_launch(ctx, "k_ipa_round_dt"));
       if (round) cur = outs;

@@ -189,6 +189,21 @@ __global__ void __launch_bounds__(256) k_ipa_fold(uint32_t n, uint32_t lg_n, uin
   }
 }
 
+// The last fold of the fused path, for element 0 only (the proof's a, b):
+// out[p] = (a_0 u + a_1 u^-1, b_0 u^-1 + b_1 u), Montgomery words, written
+// in place into pinned host memory -- one launch where k_ipa_fold over all n
+// elements and two copies stood.
+__global__ void __launch_bounds__(64) k_ipa_final(uint32_t P, uint32_t n, const uint32_t* __restrict__ am,
+                                                 const uint32_t* __restrict__ bm, const uint32_t* __restrict__ u,
+                                                 uint32_t* __restrict__ out) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  const size_t ib = (size_t)p * n;
+  const sc um = sc_load(u + 16 * p), uim = sc_load(u + 16 * p + 8);
+  sc_store(out + 16 * p, sc_add(sc_mont(sc_load(am + 8 * ib), um), sc_mont(sc_load(am + 8 * (ib + 1)), uim)));
+  sc_store(out + 16 * p + 8, sc_add(sc_mont(sc_load(bm + 8 * ib), uim), sc_mont(sc_load(bm + 8 * (ib + 1)), um)));
+}
+
 // One whole IPA round per launch over the direct tables (the fused form of
 // k_ipa_fold + k_ipa_terms + k_ipa_cross_final + k_dt_msm): block 2i + s is
 // instance i's L (s = 0) or R (s = 1).  The block
@@ -463,6 +478,7 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
     BPP_TRY(ctx_h2d(ctx, d_states, stt.data(), stt.size()));
     BPP_TRY(ctx_ws(ctx, "ipa_lr", (size_t)lg_n * P * 64, &d_lr));
   }
+  uint32_t* ab_host = nullptr;  // k_ipa_final's output (fused path)
   int cur = 0;  // set holding the state at the start of a round (before its fold)
   uint32_t m = n, round = 0;
   uint32_t lg_h = lg_n ? lg_n - 1 : 0;  // log2(m/2)
@@ -565,7 +581,13 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
     }
     // the fused rounds fold inside the next round's launch; the last
     // challenge (and every challenge of the unfused path) is folded here
-    if (!fused || h == 1) {
+    if (fused && h == 1 && n >= 2) {  // (the proof needs element 0 only)
+      uint32_t* hab = nullptr;
+      BPP_TRY(ctx_zc_out(ctx, "ipa_ab_h", (size_t)P * 64, &hab));
+      hipLaunchKernelGGL(k_ipa_final, dim3(grid_for(P, 64)), dim3(64), 0, ctx->stream, P, n, S[cur][0], S[cur][1],
+                         (const uint32_t*)d_u, hab);
+      ab_host = hab;
+    } else if (!fused || h == 1) {
       uint32_t** st = S[cur];
       ProfScope ps(ctx, "ipa_fold");
       hipLaunchKernelGGL(k_ipa_fold, dim3(grid_for(PN, 256)), dim3(256), 0, ctx->stream, n, lg_n, P, m, st[0], st[1],
@@ -595,7 +617,10 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
   }
   // a, b = element 0 of each instance
   std::vector<uint32_t> ab((size_t)P * 16);
-  {
+  if (ab_host) {  // k_ipa_final wrote them into host memory
+    BPP_TRY(ctx_sync(ctx));
+    memcpy(ab.data(), ab_host, ab.size() * 4);
+  } else {
     void* h = nullptr;
     BPP_TRY(ctx_pinned(ctx, ab.size() * 4, &h));
     BPP_HIP(hipMemcpy2DAsync(h, 64, am, (size_t)n * 32, 32, P, hipMemcpyDeviceToHost, ctx->stream));

@@ -466,9 +466,11 @@ class PermProver:
         check(rc, "bpp_perm_verify_batch", self.ctx.h)
         return True
 
-    def verify_job(self, proofs: Sequence[bytes], Vs: Sequence[bytes]) -> "VerifyJob":
-        """Host phase of a batch verification that may be split over GPUs."""
-        return VerifyJob(self.k, proofs, Vs, self.label)
+    def verify_job(self, proofs: Sequence[bytes], Vs: Sequence[bytes], device: bool = True) -> "VerifyJob":
+        """Replay phase of a batch verification that may be split over GPUs:
+        on this prover's context (device=True, bpp_perm_verify_begin_dev) or
+        on the host (bpp_perm_verify_begin)."""
+        return VerifyJob(self.k, proofs, Vs, self.label, ctx=self.ctx if device else None)
 
     def verify_partial(self, job: "VerifyJob", r_all: bytes, first: int, w_begin: int, w_end: int) -> bytes:
         """128-B raw partial of job's MSM over windows [w_begin, w_end) (see
@@ -481,23 +483,32 @@ class PermProver:
 
 
 class VerifyJob:
-    """Parsed proofs with their transcripts replayed (host only, no GPU):
-    bpp_perm_verify_begin.  `r` holds each proof's weight challenge; the
-    batch weights are derived from every rank's r (r_all)."""
+    """Parsed proofs with their transcripts replayed: on the host
+    (bpp_perm_verify_begin, ctx=None; no GPU) or on the GPU of `ctx`
+    (bpp_perm_verify_begin_dev: the job's records stay in that context's
+    workspaces, valid until its next device job).  `r` holds each proof's
+    weight challenge; the batch weights are derived from every rank's r
+    (r_all)."""
 
-    def __init__(self, k: int, proofs: Sequence[bytes], Vs: Sequence[bytes], label: bytes = b"bp-perm"):
+    def __init__(self, k: int, proofs: Sequence[bytes], Vs: Sequence[bytes], label: bytes = b"bp-perm",
+                 ctx: "Context | None" = None):
         self.lib = _lib.load()
         self.k = k
         self.count = len(proofs)
+        self.device = ctx is not None
         h = C.c_void_p()
         r = C.create_string_buffer(32 * self.count + 1)
-        rc = self.lib.bpp_perm_verify_begin(k, self.count, _buf(label), len(label), _buf(b"".join(proofs)),
-                                            _buf(b"".join(Vs)), r, C.byref(h))
+        pb, vb = _buf(b"".join(proofs)), _buf(b"".join(Vs))
+        if ctx is None:
+            rc = self.lib.bpp_perm_verify_begin(k, self.count, _buf(label), len(label), pb, vb, r, C.byref(h))
+        else:
+            rc = self.lib.bpp_perm_verify_begin_dev(ctx.h, k, self.count, _buf(label), len(label), pb, vb, r,
+                                                    C.byref(h))
         if rc == 6:
             self.h = None
             self.r = None
             return
-        check(rc, "bpp_perm_verify_begin")
+        check(rc, "bpp_perm_verify_begin" + ("_dev" if ctx is not None else ""), ctx.h if ctx is not None else None)
         self.h = h
         self.r = r.raw[:32 * self.count]
 

@@ -42,6 +42,7 @@ SIGNATURES = {
     "bpp_ctx_profile_reset": (None, [vp]),
     "bpp_ctx_work_get": (i32, [vp, C.c_char_p, C.POINTER(u64)]),
     "bpp_ctx_work_reset": (None, [vp]),
+    "bpp_host_tuning": (i32, [u32]),
     "bpp_dev_alloc": (i32, [vp, sz, C.POINTER(vp)]),
     "bpp_dev_free": (i32, [vp, vp]),
     "bpp_memcpy_htod": (i32, [vp, vp, vp, sz]),
@@ -85,6 +86,7 @@ SIGNATURES = {
     "bpp_perm_verify": (i32, [vp, vp, u32, vp, sz, vp, sz, vp]),
     "bpp_perm_verify_batch": (i32, [vp, vp, u32, sz, vp, sz, vp, vp]),
     "bpp_perm_verify_begin": (i32, [u32, sz, vp, sz, vp, vp, vp, C.POINTER(vp)]),
+    "bpp_perm_verify_begin_dev": (i32, [vp, u32, sz, vp, sz, vp, vp, vp, C.POINTER(vp)]),
     "bpp_perm_verify_terms": (i32, [vp, C.POINTER(sz)]),
     "bpp_perm_verify_scalars": (i32, [vp, vp, sz, sz, vp, vp]),
     "bpp_perm_verify_partial": (i32, [vp, vp, vp, vp, sz, sz, u32, u32, vp]),

@@ -17,7 +17,8 @@
 
 3. Batch verification (config 5): the weighted checks of all proofs form
    ONE MSM (bpp_perm_verify_*).  Window split (north_star): every rank
-   replays every proof and runs its window range; the 128-byte partials are
+   replays every proof (on its GPU, one lane per transcript) and runs its
+   window range; the 128-byte partials are
    all-gathered and must add up to the identity.  Proof split: each rank
    replays only its slice, the 32-byte weight challenges r are all-gathered
    (the batch weights depend on every proof), each rank runs all windows of
@@ -111,7 +112,7 @@ def distributed_verify(prover, proofs, Vs, rank: int, world: int, split: str = "
     import bpperm
 
     if split == "windows":
-        job = bpperm.VerifyJob(prover.k, proofs, Vs, prover.label)
+        job = bpperm.VerifyJob(prover.k, proofs, Vs, prover.label, ctx=prover.ctx)
         ok = job.ok
         if ok:
             wb, we = window_ranges(job.windows()[1], world)[rank]
@@ -121,7 +122,7 @@ def distributed_verify(prover, proofs, Vs, rank: int, world: int, split: str = "
         job.close()
     else:
         b, e = point_ranges(len(proofs), world)[rank]
-        job = bpperm.VerifyJob(prover.k, proofs[b:e], Vs[b:e], prover.label)
+        job = bpperm.VerifyJob(prover.k, proofs[b:e], Vs[b:e], prover.label, ctx=prover.ctx)
         ok = job.ok
         r_all = b"".join(torch_all_gather_bytes_var(job.r if ok else bytes(32 * (e - b)), device))
         part = prover.verify_partial(job, r_all, b, 0, job.windows()[1]) if ok else bytes(128)

@@ -28,10 +28,17 @@ def sources():
     return sorted(list(CSRC.glob("*.hip")) + list(CSRC.glob("host/*.cpp")))
 
 
+def dep_headers():
+    """Every file a source may include: a change to any of them rebuilds every
+    object (the generated csrc/fe10_ops.inc included, tools/gen_fe10.py)."""
+    return sorted(list(CSRC.glob("*.cuh")) + list(CSRC.glob("*.h")) + list(CSRC.glob("*.inc")) +
+                  list(CSRC.glob("host/*.h")) + list(CSRC.glob("host/*.inc")) +
+                  [ROOT.parent / "include" / "bpperm.h"])
+
+
 def _compile(src: Path, flags, bdir: Path = BUILD) -> Path:
     obj = bdir / (src.relative_to(CSRC).as_posix().replace("/", "_") + ".o")
-    deps = [src] + list(CSRC.glob("*.cuh")) + list(CSRC.glob("*.h")) + list(CSRC.glob("host/*.h")) + \
-        [ROOT.parent / "include" / "bpperm.h"]
+    deps = [src] + dep_headers()
     if obj.exists() and obj.stat().st_mtime >= max(d.stat().st_mtime for d in deps):
         return obj
     if src.suffix == ".hip":

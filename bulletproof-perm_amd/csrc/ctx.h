@@ -70,6 +70,10 @@ struct bpp_ctx {
   // "madds" (mixed additions of a table point), "padds" (additions of two
   // extended points: trees, bucket reductions), "msm_launches"
   std::map<std::string, uint64_t> work;
+  // device batch-verification jobs (bpp_perm_verify_begin_dev) keep their
+  // records and decompressed points in this context's "vj_*" workspaces; a
+  // job is valid while its generation is the context's latest
+  uint64_t vjob_gen = 0;
 };
 
 struct bpp_points {
@@ -112,6 +116,8 @@ int ctx_zc_out(bpp_ctx* ctx, const char* name, size_t bytes, uint32_t** d);
 // hipMemcpyAsync measured up to ~25 ms on a 20 KB copy on the box); the host
 // buffer may be freed as soon as this returns.
 int ctx_h2d(bpp_ctx* ctx, void* d, const void* h, size_t bytes);
+// Two host buffers copied back to back into d (one staging copy).
+int ctx_h2d2(bpp_ctx* ctx, void* d, const void* h0, size_t n0, const void* h1, size_t n1);
 // Two-step form for data produced straight into the pinned arena:
 // ctx_h2d_stage hands out `bytes` of staging (valid until the next
 // ctx_sync), ctx_h2d_staged enqueues its copy to d.

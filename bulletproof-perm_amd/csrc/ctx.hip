@@ -5,17 +5,6 @@
 #include <algorithm>
 #include <cstring>
 
-// glibc's dynamic mmap threshold makes every batch's few-hundred-KB to
-// few-MB host vectors (scalar arrays, encodings, staging) alternate between
-// mmap and trimmed arena tops: mprotect, munmap and fresh-page faults showed
-// up in a host profile of 8 batches in flight.  A fixed threshold and no
-// trimming keep that memory in the arenas (the process's steady footprint
-// is a few hundred MB).
-__attribute__((constructor)) static void bpp_tune_malloc() {
-  mallopt(M_MMAP_THRESHOLD, 64 << 20);
-  mallopt(M_TRIM_THRESHOLD, 1 << 30);
-}
-
 #include "ctx.h"
 #include "host/par.h"
 
@@ -153,6 +142,16 @@ int ctx_h2d(bpp_ctx* ctx, void* d, const void* h, size_t bytes) {
   return BPP_OK;
 }
 
+int ctx_h2d2(bpp_ctx* ctx, void* d, const void* h0, size_t n0, const void* h1, size_t n1) {
+  if (!n0 && !n1) return BPP_OK;
+  uint8_t* p = nullptr;
+  BPP_TRY(stage_take(ctx, n0 + n1, &p));
+  stage_copy(p, h0, n0);
+  stage_copy(p + n0, h1, n1);
+  BPP_HIP(hipMemcpyAsync(d, p, n0 + n1, hipMemcpyHostToDevice, ctx->stream));
+  return BPP_OK;
+}
+
 int ctx_h2d_const(bpp_ctx* ctx, const char* name, void* d, const void* h, size_t bytes) {
   auto& e = ctx->h2d_cache[name];
   if (e.first == d && e.second.size() == bytes && !memcmp(e.second.data(), h, bytes)) return BPP_OK;
@@ -245,6 +244,22 @@ static void prof_resolve(bpp_ctx* ctx) {
 }
 
 extern "C" {
+
+// glibc's dynamic mmap threshold makes every batch's few-hundred-KB to
+// few-MB host vectors (scalar arrays, encodings, staging) alternate between
+// mmap and trimmed arena tops: mprotect, munmap and fresh-page faults showed
+// up in a host profile of 8 batches in flight.  A fixed threshold and no
+// trimming keep that memory in the arenas.  This changes the allocator policy
+// of the whole host process, so it is opt-in (bench.py asks for it); loading
+// the library changes nothing.
+int bpp_host_tuning(uint32_t flags) {
+  if (flags & ~(uint32_t)BPP_TUNE_MALLOC) return BPP_ERR_ARG;
+  if (flags & BPP_TUNE_MALLOC) {
+    mallopt(M_MMAP_THRESHOLD, 64 << 20);
+    mallopt(M_TRIM_THRESHOLD, 1 << 30);
+  }
+  return BPP_OK;
+}
 
 int bpp_ctx_create(int device, bpp_ctx** out) {
   if (!out) return BPP_ERR_ARG;

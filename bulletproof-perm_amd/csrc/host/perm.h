@@ -118,4 +118,15 @@ void draw_prover_host_x8(const Circuit& C, const Seed seeds[8], RandomDraws* con
 
 size_t proof_len(uint32_t k);
 
+// Batch-verification weights over `total` proofs with weight challenges r
+// (each proof's transcript's "t-check-weight"):
+//   d_j  = SHAKE256("bp-perm-batch-r" || le64 total || le64 j || r[j total/8 ..
+//          (j+1) total/8))[0..32], j < 8
+//   seed = SHAKE256("bp-perm-batch-seed" || d_0 .. d_7)[0..32]
+//   w_p  = from_bytes_mod_order_wide(SHAKE256("bp-perm-batch-wt" || seed ||
+//          le64 p)[0..64])
+// (a single proof keeps weight one; callers special-case total <= 1).
+void batch_seed(const hsc::Sc* r, size_t total, uint8_t seed[32]);
+hsc::Sc batch_weight(const uint8_t seed[32], uint64_t p);
+
 }  // namespace perm

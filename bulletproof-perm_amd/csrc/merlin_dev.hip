@@ -13,8 +13,7 @@
 // LDS so that the byte-wise absorb/squeeze index them cheaply).
 #include "ctx.h"
 #include "merlin_dev.h"
-#include "keccak_dev.cuh"
-#include "sc25519.cuh"
+#include "merlin_lane.cuh"  // (sc_inv_vartime)
 
 #define STROBE_R_DEV 166
 #define ST_STRIDE 200  // bytes of one lane's sponge state in LDS (8-byte aligned)
@@ -97,63 +96,6 @@ FE_INLINE sc sc_from_wide_mont(const uint8_t b[64]) {
     r3.v[i] = SC_R3[i];
   }
   return sc_add(sc_mont(lo, r2), sc_mont(hi, r3));
-}
-
-FE_INLINE bool w8_is_one(const uint32_t a[8]) {
-  uint32_t o = a[0] ^ 1u;
-  _Pragma("unroll") for (int i = 1; i < 8; ++i) o |= a[i];
-  return o == 0;
-}
-FE_INLINE bool w8_geq(const uint32_t a[8], const uint32_t b[8]) {
-  for (int i = 7; i >= 0; --i)
-    if (a[i] != b[i]) return a[i] > b[i];
-  return true;
-}
-FE_INLINE void w8_sub(uint32_t a[8], const uint32_t b[8]) {
-  uint64_t br = 0;
-  _Pragma("unroll") for (int i = 0; i < 8; ++i) {
-    const uint64_t d = (uint64_t)a[i] - b[i] - br;
-    a[i] = (uint32_t)d;
-    br = (d >> 32) & 1u;
-  }
-}
-FE_INLINE void w8_shr1(uint32_t a[8]) {
-  _Pragma("unroll") for (int i = 0; i < 7; ++i) a[i] = (a[i] >> 1) | (a[i + 1] << 31);
-  a[7] >>= 1;
-}
-
-// a^-1 mod l for canonical a != 0 by the binary extended Euclidean algorithm
-// (variable time; the IPA challenges are public).  Bounded loop: every
-// outer step removes at least one bit from u + v.
-FE_INLINE sc sc_inv_vartime(const sc& a) {
-  uint32_t u[8], v[8];
-  sc x1 = sc_zero(), x2 = sc_zero();
-  x1.v[0] = 1;
-  bool zero = true;
-  _Pragma("unroll") for (int i = 0; i < 8; ++i) {
-    u[i] = a.v[i];
-    v[i] = SC_L[i];
-    zero &= a.v[i] == 0;
-  }
-  if (zero) return sc_zero();
-  for (int it = 0; it < 2048 && !w8_is_one(u) && !w8_is_one(v); ++it) {
-    while (!(u[0] & 1u)) {
-      w8_shr1(u);
-      x1 = sc_half(x1);
-    }
-    while (!(v[0] & 1u)) {
-      w8_shr1(v);
-      x2 = sc_half(x2);
-    }
-    if (w8_geq(u, v)) {
-      w8_sub(u, v);
-      x1 = sc_sub(x1, x2);
-    } else {
-      w8_sub(v, u);
-      x2 = sc_sub(x2, x1);
-    }
-  }
-  return w8_is_one(u) ? x1 : x2;
 }
 
 // One IPA round's transcript step for P proofs, one lane each.

@@ -33,10 +33,14 @@
 #include "msm_engine.h"
 #include "poly.h"
 #include "layout.h"
+#include "verify_dev.h"
 
 using hsc::Sc;
 
 int decompress_ws(bpp_ctx* ctx, const uint8_t* enc, size_t count, const char* name, uint32_t** d_out);
+// declared in points.hip
+__global__ void k_decompress(const uint32_t* __restrict__ enc, size_t n, uint32_t* __restrict__ tbl,
+                             unsigned long long* __restrict__ bad);
 
 namespace {
 
@@ -192,10 +196,15 @@ struct ProverScratch {
   std::vector<Enc32> V;
   // A_I/A_O/S MSM terms without the zero padding gates (a_L, a_R, a_O of
   // gates 2k..n_p-1): generator index and source slot in the [P][per]
-  // scalar array per term, rebuilt when (P, k) changes
+  // scalar array per term, rebuilt when (P, k, generator set) changes: the
+  // indices embed G->n (hidx(i) = n + i, bbidx() = 2n + 1), so one thread
+  // proving the same (P, k) against generator sets of different sizes must
+  // not reuse them
   std::vector<uint32_t> idx, map, off;
   size_t key_P = 0;
   uint32_t key_k = 0;
+  const bpp_gens* key_G = nullptr;
+  size_t key_n = 0;
 };
 
 struct ProverState {
@@ -383,7 +392,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     std::vector<uint32_t>&idx = scr.idx, &map = scr.map, &off = scr.off;
     const uint32_t n = C.n;                       // real gates; n_p - n padding gates are zero
     const uint32_t per_c = 3 + 3 * n + 2 * n_p;  // MSM terms per proof
-    if (scr.key_P != P || scr.key_k != k) {
+    if (scr.key_P != P || scr.key_k != k || scr.key_G != G || scr.key_n != G->n) {
       idx.resize((size_t)P * per_c);
       map.resize((size_t)P * per_c);
       off.resize(3 * P + 1);
@@ -409,6 +418,8 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
       off[3 * P] = (uint32_t)(P * per_c);
       scr.key_P = P;
       scr.key_k = k;
+      scr.key_G = G;
+      scr.key_n = G->n;
     }
     uint8_t* stg = nullptr;  // (host witness only) written in place in the pinned arena
     if (!dev_witness) {
@@ -717,6 +728,12 @@ struct bpp_verify_job {
   mutable std::mutex mu;
   mutable bool expanded = false;
   mutable std::vector<std::vector<Sc>> gen_p, pt_p;
+  // device job (bpp_perm_verify_begin_dev): the replay ran on the GPU and the
+  // records / decompressed proof points sit in dctx's "vj_*" workspaces
+  // (generation dgen); Ps, ch and inv stay empty
+  bool dev = false;
+  bpp_ctx* dctx = nullptr;
+  uint64_t dgen = 0;
 };
 
 namespace {
@@ -786,14 +803,16 @@ void job_expand_host(const bpp_verify_job& J) {
 // Terms of the job's MSM: merged generators (G, H, B, Bb) + every proof point.
 size_t verify_terms(const bpp_verify_job& J) { return 2 * (size_t)J.C.n_p + 2 + J.count * J.npt; }
 
-// Per-proof weights from a batch transcript over all `total` r challenges
-// (a single proof keeps weight one).
+// Per-proof weights from all `total` r challenges (perm::batch_seed /
+// batch_weight; a single proof keeps weight one).
 std::vector<Sc> batch_weights(const Sc* r_all, size_t total) {
   std::vector<Sc> wts(total, hsc::one());
   if (total > 1) {
-    merlin::Transcript batch((const uint8_t*)"bp-perm-batch-verify", 20);
-    for (size_t p = 0; p < total; ++p) batch.append_scalar("r", r_all[p]);
-    for (size_t p = 0; p < total; ++p) wts[p] = batch.challenge_scalar("proof-weight");
+    uint8_t seed[32];
+    perm::batch_seed(r_all, total, seed);
+    par::for_each((total + 63) / 64, [&](size_t b) {
+      for (size_t p = 64 * b; p < std::min(total, 64 * b + 64); ++p) wts[p] = perm::batch_weight(seed, p);
+    });
   }
   return wts;
 }
@@ -835,8 +854,38 @@ int verify_terms_weighted(const bpp_verify_job& J, const Sc* r_all, size_t total
   return BPP_OK;
 }
 
-// pass 2 (device): ONE MSM over the job's terms, windows [wb, we) of its
-// c-bit signed digits (c = msm_choose_c(terms)) -> raw partial point.
+// The batch's ONE MSM over windows [wb, we) of its c-bit signed digits (c =
+// msm_choose_c(terms)) -> raw partial point: scalars d_sv (2 n_p + 2 merged
+// generator scalars, then count x npt proof-point scalars), proof points d_x.
+int verify_msm(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, size_t count, const uint32_t* d_sv,
+               const uint32_t* d_x, uint32_t wb, uint32_t we, h25519::ge* out) {
+  const uint32_t n_p = C.n_p;
+  const size_t NG = 2 * (size_t)n_p + 2, T = NG + count * vpts_n(C);
+  // term t reads generator t of the resident table (G[0..n_p), H[0..n_p),
+  // B, Bb) or proof point t - NG; the index list is needed only when the
+  // generator set is longer than the padded circuit
+  const uint32_t n0 = (uint32_t)(2 * G->n + 2);
+  uint32_t* d_idx = nullptr;
+  if (G->n != n_p) {
+    std::vector<uint32_t> idx(T);
+    for (uint32_t i = 0; i < n_p; ++i) {
+      idx[i] = G->gidx(i);
+      idx[n_p + i] = G->hidx(i);
+    }
+    idx[2 * n_p] = G->bidx();
+    idx[2 * n_p + 1] = G->bbidx();
+    for (size_t j = NG; j < T; ++j) idx[j] = n0 + (uint32_t)(j - NG);
+    void* d = nullptr;
+    BPP_TRY(ctx_ws(ctx, "pv_idx", idx.size() * 4 + 4, &d));
+    BPP_TRY(ctx_h2d_const(ctx, "pv_idx", d, idx.data(), idx.size() * 4));
+    d_idx = (uint32_t*)d;
+  }
+  const uint32_t c = msm_choose_c((double)T);
+  return msm_single_dev(ctx, d_sv, d_idx, G->d_tbl, T, c, wb, we - wb, out, d_x, n0);
+}
+
+// pass 2 of a host job: per-proof records built on the host from the host
+// replay, then the same device scalars and MSM as a device job.
 int verify_partial(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J, const Sc* r_all, size_t total,
                    size_t first, uint32_t wb, uint32_t we, h25519::ge* out) {
   const uint32_t n_p = J.C.n_p;
@@ -891,38 +940,107 @@ int verify_partial(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J, con
   // term t reads generator t of the resident table (G[0..n_p), H[0..n_p),
   // B, Bb) or proof point t - NG; the index list is needed only when the
   // generator set is longer than the padded circuit
-  const uint32_t n0 = (uint32_t)(2 * G->n + 2);
-  uint32_t* d_idx = nullptr;
-  if (G->n != n_p) {
-    std::vector<uint32_t> idx(T);
-    for (uint32_t i = 0; i < n_p; ++i) {
-      idx[i] = G->gidx(i);
-      idx[n_p + i] = G->hidx(i);
-    }
-    idx[2 * n_p] = G->bidx();
-    idx[2 * n_p + 1] = G->bbidx();
-    for (size_t j = NG; j < T; ++j) idx[j] = n0 + (uint32_t)(j - NG);
-    void* d = nullptr;
-    BPP_TRY(ctx_ws(ctx, "pv_idx", idx.size() * 4 + 4, &d));
-    BPP_TRY(ctx_h2d(ctx, d, idx.data(), idx.size() * 4));
-    d_idx = (uint32_t*)d;
+  return verify_msm(ctx, G, J.C, count, (const uint32_t*)d_sv, d_x, wb, we, out);
+}
+
+// pass 1 on the device (bpp_perm_verify_begin_dev): upload the proofs and V,
+// replay every transcript on the GPU (k_verify_replay, one lane per proof),
+// decompress the proof points into the "vj_x" workspace, and return the r
+// challenges.  BPP_ERR_VERIFY if any proof is malformed.
+int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label, size_t llen, size_t count,
+                     const uint8_t* proofs, const uint8_t* V, std::unique_ptr<bpp_verify_job>& job) {
+  job.reset(new bpp_verify_job);
+  bpp_verify_job& J = *job;
+  J.C = C;
+  J.count = count;
+  J.npt = vpts_n(C);
+  J.rs.resize(count);
+  J.dev = true;
+  J.dctx = ctx;
+  J.dgen = ++ctx->vjob_gen;
+  if (!count) return BPP_OK;
+  if (count > (1u << 26)) return BPP_ERR_ARG;
+  const size_t plen = perm::proof_len(C.k), vbytes = (size_t)C.m * 32, npts = count * J.npt;
+  void *d_in = nullptr, *d_rec = nullptr, *d_enc = nullptr, *d_x = nullptr, *d_dbad = nullptr;
+  {
+    HostScope hs(ctx, "verify_upload");
+    BPP_TRY(ctx_ws(ctx, "vj_in", count * (plen + vbytes), &d_in));
+    BPP_TRY(ctx_h2d2(ctx, d_in, proofs, count * plen, V, count * vbytes));
   }
-  const uint32_t c = msm_choose_c((double)T);
-  return msm_single_dev(ctx, (const uint32_t*)d_sv, d_idx, G->d_tbl, T, c, wb, we - wb, out, d_x, n0);
+  HostScope hs(ctx, "verify_replay");
+  BPP_TRY(ctx_ws(ctx, "vj_rec", count * vrec_n(C) * 32, &d_rec));
+  BPP_TRY(ctx_ws(ctx, "vj_enc", npts * 32, &d_enc));
+  BPP_TRY(ctx_ws(ctx, "vj_x", npts * MSM_NIELS_WORDS * 4, &d_x));
+  BPP_TRY(ctx_ws(ctx, "vj_dbad", 8, &d_dbad));
+  uint32_t *h_init = nullptr, *h_r = nullptr, *h_bad = nullptr, *h_dbad = nullptr;
+  {
+    uint32_t init[52];
+    verify_init_state(C, label, llen, init);
+    BPP_TRY(ctx_zc_in(ctx, "vj_init", init, sizeof init, &h_init));
+  }
+  BPP_TRY(ctx_zc_out(ctx, "vj_r", count * 32, &h_r));
+  BPP_TRY(ctx_zc_out(ctx, "vj_bad", count * 4, &h_bad));
+  BPP_TRY(ctx_zc_out(ctx, "vj_dbad_h", 8, &h_dbad));
+  BPP_TRY(verify_replay_dev(ctx, C, (uint32_t)count, h_init, (const uint32_t*)d_in,
+                            (const uint32_t*)((uint8_t*)d_in + count * plen), (uint32_t*)d_rec, (uint32_t*)d_enc, h_r,
+                            h_bad));
+  BPP_HIP(hipMemsetAsync(d_dbad, 0xff, 8, ctx->stream));
+  {
+    ProfScope ps(ctx, "verify_decompress");
+    hipLaunchKernelGGL(k_decompress, dim3((unsigned)((npts + 63) / 64)), dim3(64), 0, ctx->stream,
+                       (const uint32_t*)d_enc, npts, (uint32_t*)d_x, (unsigned long long*)d_dbad);
+  }
+  BPP_TRY(ctx_check_launch(ctx, "k_decompress"));
+  BPP_HIP(hipMemcpyAsync(h_dbad, d_dbad, 8, hipMemcpyDeviceToHost, ctx->stream));
+  BPP_TRY(ctx_sync(ctx));
+  uint32_t any = 0;
+  for (size_t p = 0; p < count; ++p) any |= h_bad[p];
+  if (any || *(const unsigned long long*)h_dbad != ~0ull) return BPP_ERR_VERIFY;
+  memcpy(J.rs.data(), h_r, count * 32);
+  return BPP_OK;
+}
+
+// pass 2 of a device job: weights on the device from all `total` r
+// challenges, the unweighted-then-weighted scalars (k_verify_scalars) and the
+// MSM over windows [wb, we).
+int verify_partial_dev(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J, const Sc* r_all, size_t total,
+                       size_t first, uint32_t wb, uint32_t we, h25519::ge* out) {
+  if (J.dctx != ctx || J.dgen != ctx->vjob_gen) {
+    ctx->err = "device verify job belongs to another context or was superseded by a later begin";
+    return BPP_ERR_ARG;
+  }
+  if (G->n < J.C.n_p) {
+    ctx->err = "generators shorter than the padded circuit";
+    return BPP_ERR_LEN;
+  }
+  if (first > total || J.count > total - first) return BPP_ERR_ARG;
+  const size_t count = J.count, T = 2 * (size_t)J.C.n_p + 2 + count * J.npt;
+  void *d_rec = nullptr, *d_x = nullptr, *d_sv = nullptr;
+  BPP_TRY(ctx_ws(ctx, "vj_rec", count * vrec_n(J.C) * 32, &d_rec));
+  BPP_TRY(ctx_ws(ctx, "vj_x", count * J.npt * MSM_NIELS_WORDS * 4, &d_x));
+  BPP_TRY(ctx_ws(ctx, "pv_s", T * 32 + 32, &d_sv));
+  {
+    HostScope hs(ctx, "verify_terms");
+    uint8_t seed[32] = {0};
+    if (total > 1) perm::batch_seed(r_all, total, seed);
+    uint32_t* h_seed = nullptr;
+    BPP_TRY(ctx_zc_in(ctx, "vj_seed", seed, 32, &h_seed));
+    BPP_TRY(verify_weights_dev(ctx, J.C, (uint32_t)count, first, total, h_seed, (uint32_t*)d_rec));
+    BPP_TRY(verify_scalars_dev_rec(ctx, J.C, (uint32_t)count, (const uint32_t*)d_rec, (uint32_t*)d_sv));
+  }
+  return verify_msm(ctx, G, J.C, count, (const uint32_t*)d_sv, (const uint32_t*)d_x, wb, we, out);
 }
 
 // Verify `count` proofs with ONE MSM: generator scalars summed across proofs
-// with per-proof weights from a batch transcript.
+// with per-proof weights derived from every proof's r challenge; the
+// transcripts are replayed on the device.
 int verify_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const uint8_t* label, size_t llen,
-                 size_t count, const uint8_t* proofs, size_t proof_stride, const uint8_t* V) {
+                 size_t count, const uint8_t* proofs, const uint8_t* V) {
   std::unique_ptr<bpp_verify_job> job;
-  {
-    HostScope hs(ctx, "verify_replay");
-    BPP_TRY(verify_begin(C, label, llen, count, proofs, proof_stride, V, job));
-  }
+  BPP_TRY(verify_begin_dev(ctx, C, label, llen, count, proofs, V, job));
   const uint32_t c = msm_choose_c((double)verify_terms(*job));
   h25519::ge res;
-  BPP_TRY(verify_partial(ctx, G, *job, job->rs.data(), count, 0, 0, (254 + c - 1) / c, &res));
+  BPP_TRY(verify_partial_dev(ctx, G, *job, job->rs.data(), count, 0, 0, (254 + c - 1) / c, &res));
   uint8_t e[32];
   h25519::encode(e, res);
   static const uint8_t zero[32] = {0};
@@ -1056,7 +1174,7 @@ int bpp_perm_verify(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, const uint8_t* 
   if (proof_len != perm::proof_len(k)) return BPP_ERR_VERIFY;
   BPP_HIP(hipSetDevice(ctx->device));
   const perm::Circuit C = perm::build(k);
-  return verify_batch(ctx, G, C, label, llen, 1, proof, proof_len, V);
+  return verify_batch(ctx, G, C, label, llen, 1, proof, V);
 }
 
 int bpp_perm_verify_batch(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, size_t count, const uint8_t* label, size_t llen,
@@ -1065,7 +1183,7 @@ int bpp_perm_verify_batch(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, size_t co
   if (!count) return BPP_OK;
   BPP_HIP(hipSetDevice(ctx->device));
   const perm::Circuit C = perm::build(k);
-  return verify_batch(ctx, G, C, label, llen, count, proofs, perm::proof_len(k), V);
+  return verify_batch(ctx, G, C, label, llen, count, proofs, V);
 }
 
 int bpp_perm_verify_begin(uint32_t k, size_t count, const uint8_t* label, size_t llen, const uint8_t* proofs,
@@ -1077,6 +1195,19 @@ int bpp_perm_verify_begin(uint32_t k, size_t count, const uint8_t* label, size_t
   BPP_TRY(verify_begin(C, label, llen, count, proofs, perm::proof_len(k), V, job));
   if (r_out)
     for (size_t p = 0; p < count; ++p) hsc::to_bytes(r_out + 32 * p, job->rs[p]);
+  *out = job.release();
+  return BPP_OK;
+}
+
+int bpp_perm_verify_begin_dev(bpp_ctx* ctx, uint32_t k, size_t count, const uint8_t* label, size_t llen,
+                              const uint8_t* proofs, const uint8_t* V, uint8_t* r_out, bpp_verify_job** out) {
+  if (!ctx || !out || ((!proofs || !V) && count) || (!label && llen) || k < 2 || k > (1u << 20)) return BPP_ERR_ARG;
+  *out = nullptr;
+  BPP_HIP(hipSetDevice(ctx->device));
+  const perm::Circuit C = perm::build(k);
+  std::unique_ptr<bpp_verify_job> job;
+  BPP_TRY(verify_begin_dev(ctx, C, label, llen, count, proofs, V, job));
+  if (r_out && count) memcpy(r_out, job->rs.data(), 32 * count);
   *out = job.release();
   return BPP_OK;
 }
@@ -1097,6 +1228,7 @@ static int parse_rs(const uint8_t* r_all, size_t total, std::vector<Sc>& rs) {
 int bpp_perm_verify_scalars(const bpp_verify_job* job, const uint8_t* r_all, size_t total, size_t first,
                             uint8_t* scalars_out, uint8_t* points_out) {
   if (!job || (!r_all && total) || !scalars_out || (!points_out && job->count)) return BPP_ERR_ARG;
+  if (job->dev) return BPP_ERR_ARG;  // (a device job keeps no host replay to expand)
   std::vector<Sc> rs, sc;
   std::vector<uint8_t> enc;
   BPP_TRY(parse_rs(r_all, total, rs));
@@ -1116,7 +1248,12 @@ int bpp_perm_verify_partial(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_jo
   if (first > total || job->count > total - first) return BPP_ERR_ARG;
   BPP_HIP(hipSetDevice(ctx->device));
   h25519::ge r = h25519::ge_identity();
-  if (job->count) BPP_TRY(verify_partial(ctx, G, *job, rs.data(), total, first, w_begin, w_end, &r));
+  if (job->count) {
+    if (job->dev)
+      BPP_TRY(verify_partial_dev(ctx, G, *job, rs.data(), total, first, w_begin, w_end, &r));
+    else
+      BPP_TRY(verify_partial(ctx, G, *job, rs.data(), total, first, w_begin, w_end, &r));
+  }
   h25519::ge_to_words((uint32_t*)partial, r);
   return BPP_OK;
 }

@@ -22,6 +22,7 @@
 
 #include "ctx.h"
 #include "poly.h"
+#include "verify_dev.h"
 #include "keccak_dev.cuh"
 #include "sc25519.cuh"
 
@@ -262,19 +263,7 @@ __global__ void __launch_bounds__(POLY_T) k_poly_x(uint32_t n_p, const uint32_t*
 // circuit algebra, circuit_lib.rs:478-585 in sound form; host restatement
 // perm_api.hip verify_expand, which bpp_perm_verify_scalars still uses).
 // One workgroup per proof; rec[p] = VREC_N canonical scalars:
-#define VREC_XPERM 0
-#define VREC_YINV 1
-#define VREC_Z 2
-#define VREC_X 3
-#define VREC_W 4
-#define VREC_R 5
-#define VREC_A 6
-#define VREC_B 7
-#define VREC_THAT 8
-#define VREC_TAUX 9
-#define VREC_MU 10
-#define VREC_WT 11  // the proof's batch weight
-#define VREC_U 12   // u_j (lg), then u_j^-1 (lg)
+// (VREC_* slots: verify_dev.h)
 // Writes wt * (generator scalars) to gen[p][2 n_p + 2] (summed over proofs by
 // k_verify_merge) and wt * (proof-point scalars) to sc_out[NG + p npt + j]
 // (V_0..V_{m-1}, A_I, A_O, S, T1 T3 T4 T5 T6, L_0.., R_0..), canonical.
@@ -682,12 +671,19 @@ int poly_x_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const std::vect
 
 int verify_scalars_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const std::vector<uint32_t>& rec,
                        uint32_t* d_sc) {
+  uint32_t* h = nullptr;  // per-proof records read in place from pinned host memory (ctx_zc_in)
+  BPP_TRY(ctx_zc_in(ctx, "vs_rec_h", rec.data(), rec.size() * 4, &h));
+  return verify_scalars_dev_rec(ctx, C, count, h, d_sc);
+}
+
+int verify_scalars_dev_rec(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const uint32_t* d_rec,
+                           uint32_t* d_sc) {
   std::vector<uint32_t> cp, ce;
   build_csr(C, cp, ce, true);
   std::vector<uint32_t> cw((size_t)C.Q * 8);
   for (uint32_t q = 0; q < C.Q; ++q) memcpy(&cw[8 * (size_t)q], C.c[q].v, 32);
   const uint32_t NG = 2 * C.n_p + 2, npt = C.m + 8 + 2 * C.lg;
-  void *d_cp, *d_ce, *d_c, *d_rec, *d_gen;
+  void *d_cp, *d_ce, *d_c, *d_gen;
   BPP_TRY(ctx_ws(ctx, "vs_cp", cp.size() * 4, &d_cp));
   BPP_TRY(ctx_ws(ctx, "vs_ce", ce.size() * 4 + 4, &d_ce));
   BPP_TRY(ctx_ws(ctx, "vs_c", cw.size() * 4, &d_c));
@@ -696,18 +692,13 @@ int verify_scalars_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, con
   BPP_TRY(ctx_h2d_const(ctx, "vs_cp", d_cp, cp.data(), cp.size() * 4));  // the circuit: same every batch
   BPP_TRY(ctx_h2d_const(ctx, "vs_ce", d_ce, ce.data(), ce.size() * 4));
   BPP_TRY(ctx_h2d_const(ctx, "vs_c", d_c, cw.data(), cw.size() * 4));
-  {  // per-proof records read in place from pinned host memory (ctx_zc_in)
-    uint32_t* h = nullptr;
-    BPP_TRY(ctx_zc_in(ctx, "vs_rec_h", rec.data(), rec.size() * 4, &h));
-    d_rec = h;
-  }
   const unsigned nt = poly_block(std::max(C.n_p, C.m));
   const size_t lds = ((size_t)C.Q + 1 + 2 * std::min(C.n_p, (uint32_t)POW_LO)) * 32 + (POLY_T / 64) * 2 * 32;
   {
     ProfScope ps(ctx, "verify_scalars");
-    hipLaunchKernelGGL(k_verify_scalars, dim3(count), dim3(nt), lds, ctx->stream, C.n_p, C.m, C.Q, C.lg,
-                       (const uint32_t*)d_rec, (const uint32_t*)d_cp, (const uint32_t*)d_ce, (const uint32_t*)d_c,
-                       (uint32_t*)d_gen, d_sc, NG, npt);
+    hipLaunchKernelGGL(k_verify_scalars, dim3(count), dim3(nt), lds, ctx->stream, C.n_p, C.m, C.Q, C.lg, d_rec,
+                       (const uint32_t*)d_cp, (const uint32_t*)d_ce, (const uint32_t*)d_c, (uint32_t*)d_gen, d_sc,
+                       NG, npt);
     hipLaunchKernelGGL(k_verify_merge, dim3(NG), dim3(POLY_T), 0, ctx->stream, count, NG, (const uint32_t*)d_gen,
                        d_sc);
   }

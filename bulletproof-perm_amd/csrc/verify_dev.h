@@ -1,0 +1,47 @@
+// Batch verification on the device (verify_dev.hip, poly.hip k_verify_scalars).
+#pragma once
+#include <stdint.h>
+
+#include "ctx.h"
+#include "host/perm.h"
+
+// Per-proof verifier record: [12 + 2 lg] canonical scalars (8 words each)
+#define VREC_XPERM 0
+#define VREC_YINV 1
+#define VREC_Z 2
+#define VREC_X 3
+#define VREC_W 4
+#define VREC_R 5
+#define VREC_A 6
+#define VREC_B 7
+#define VREC_THAT 8
+#define VREC_TAUX 9
+#define VREC_MU 10
+#define VREC_WT 11  // the proof's batch weight
+#define VREC_U 12   // u_j (lg), then u_j^-1 (lg)
+inline uint32_t vrec_n(const perm::Circuit& C) { return VREC_U + 2 * C.lg; }
+// proof points per proof in MSM order: V_0..V_{m-1}, A_I, A_O, S, T1 T3 T4
+// T5 T6, L_0.., R_0..
+inline uint32_t vpts_n(const perm::Circuit& C) { return C.m + 8 + 2 * C.lg; }
+
+// Replays `count` transcripts on the device, one lane per proof
+// (k_verify_replay): d_proofs [count][proof_len] and d_V [count][m][32] on
+// the device; init = the 52-word transcript state every proof shares (the
+// label's Transcript::new and arithmetic_domain_sep(n_p); verify_init_state).
+// Writes d_rec (weights left zero), d_enc (the proof points' encodings,
+// [count][vpts_n][32]), r_out ([count][32], the t-check weight challenges)
+// and bad ([count] u32, nonzero where a point is the identity encoding, a
+// scalar is not canonical or a challenge is zero).  r_out and bad may be
+// pinned host memory (written in place).
+int verify_replay_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const uint32_t* d_init,
+                      const uint32_t* d_proofs, const uint32_t* d_V, uint32_t* d_rec, uint32_t* d_enc,
+                      uint32_t* r_out, uint32_t* bad);
+// The 52-word shared transcript prefix for verify_replay_dev.
+void verify_init_state(const perm::Circuit& C, const uint8_t* label, size_t llen, uint32_t out[52]);
+// rec[p][VREC_WT] = perm::batch_weight(seed, first + p) for p < count (one
+// for total <= 1).  seed: 8 words, may be pinned host memory.
+int verify_weights_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, uint64_t first, uint64_t total,
+                       const uint32_t* seed, uint32_t* d_rec);
+// k_verify_scalars + k_verify_merge over device records (poly.hip).
+int verify_scalars_dev_rec(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const uint32_t* d_rec,
+                           uint32_t* d_sc);

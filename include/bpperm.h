@@ -81,6 +81,14 @@ void bpp_ctx_profile_reset(bpp_ctx* ctx);
 int bpp_ctx_work_get(bpp_ctx* ctx, const char* name, uint64_t* value);
 void bpp_ctx_work_reset(bpp_ctx* ctx);
 
+/* Opt-in host-process tuning (process-wide, so never done implicitly):
+ * BPP_TUNE_MALLOC fixes glibc's mmap threshold at 64 MB and disables heap
+ * trimming, which keeps the prover's per-batch host vectors in the arenas
+ * (measured in a host profile of 8 batches in flight).
+ * BPP_ERR_ARG for unknown flags. */
+#define BPP_TUNE_MALLOC 1u
+int bpp_host_tuning(uint32_t flags);
+
 /* Device memory helpers, so callers can stage inputs resident in HBM. */
 int bpp_dev_alloc(bpp_ctx* ctx, size_t bytes, void** dptr);
 int bpp_dev_free(bpp_ctx* ctx, void* dptr);
@@ -231,8 +239,10 @@ int bpp_perm_prove_batch_entropy(bpp_ctx* ctx, const bpp_gens* g, uint32_t k, si
 /* BPP_OK or BPP_ERR_VERIFY (ProofError::VerificationError). One GPU MSM. */
 int bpp_perm_verify(bpp_ctx* ctx, const bpp_gens* g, uint32_t k, const uint8_t* label, size_t llen,
                     const uint8_t* proof, size_t proof_len, const uint8_t* V);
-/* Batch verification: all proofs' checks folded with transcript-derived
- * weights into ONE MSM (generator scalars merged across proofs). */
+/* Batch verification: all proofs' checks folded with weights derived from
+ * every proof's transcript into ONE MSM (generator scalars merged across
+ * proofs); the transcripts are replayed on the GPU.  Weights: DESIGN.md §5
+ * "Batch weights" (perm.h batch_seed / batch_weight). */
 int bpp_perm_verify_batch(bpp_ctx* ctx, const bpp_gens* g, uint32_t k, size_t count, const uint8_t* label,
                           size_t llen, const uint8_t* proofs, const uint8_t* V);
 
@@ -245,6 +255,16 @@ int bpp_perm_verify_batch(bpp_ctx* ctx, const bpp_gens* g, uint32_t k, size_t co
 typedef struct bpp_verify_job bpp_verify_job;
 int bpp_perm_verify_begin(uint32_t k, size_t count, const uint8_t* label, size_t llen, const uint8_t* proofs,
                           const uint8_t* V, uint8_t* r_out, bpp_verify_job** out);
+/* The same host interface with the replay on the GPU of ctx (one lane per
+ * proof, k_verify_replay): uploads the proofs and V, replays every
+ * transcript, decompresses the proof points and returns r (count x 32 B, may
+ * be NULL).  r is byte-identical to bpp_perm_verify_begin's.  The job keeps
+ * its records and points in ctx's workspaces: it is valid for
+ * bpp_perm_verify_partial on the same ctx until the next
+ * bpp_perm_verify_begin_dev there (BPP_ERR_ARG after that), and
+ * bpp_perm_verify_scalars rejects it (BPP_ERR_ARG). */
+int bpp_perm_verify_begin_dev(bpp_ctx* ctx, uint32_t k, size_t count, const uint8_t* label, size_t llen,
+                              const uint8_t* proofs, const uint8_t* V, uint8_t* r_out, bpp_verify_job** out);
 /* Terms of the job's MSM: 2 n_p + 2 merged generators + count x (m + 8 +
  * 2 log2 n_p) proof points.  bpp_msm_windows(terms) gives c and W. */
 int bpp_perm_verify_terms(const bpp_verify_job* job, size_t* terms);

@@ -222,6 +222,18 @@ class Context:
         return [raw[32 * i: 32 * i + 32] for i in range(count)]
 
 
+def host_tuning(malloc: bool = True):
+    """Opt-in process-wide host tuning (bpp_host_tuning): BPP_TUNE_MALLOC
+    fixes glibc's mmap threshold and disables heap trimming (the prover's
+    per-batch host vectors stay in the arenas)."""
+    check(_lib.load().bpp_host_tuning(1 if malloc else 0), "bpp_host_tuning")
+
+
+def host_pool_threads() -> int:
+    """Threads of the library's host pool (bpp_host_threads)."""
+    return int(_lib.load().bpp_host_threads())
+
+
 def msm_windows(n: int) -> tuple[int, int]:
     lib = _lib.load()
     c = C.c_uint32()
@@ -422,7 +434,10 @@ class PermProver:
         vraw = V.raw
         return pf.raw, [vraw[32 * j: 32 * j + 32] for j in range(self.m)], list(perm)
 
-    def prove_batch(self, seeds: Sequence[int]):
+    def prove_batch(self, seeds: Sequence[int], raw: bool = False):
+        """-> ([proof bytes], [V bytes of one proof]), or with raw=True the
+        two contiguous buffers (proofs, V) as the C ABI writes them (what
+        verify_batch takes without a join)."""
         cnt = len(seeds)
         pf = C.create_string_buffer(self.proof_len * cnt)
         V = C.create_string_buffer(32 * self.m * cnt)
@@ -430,6 +445,8 @@ class PermProver:
         check(self.ctx.lib.bpp_perm_prove_batch(self.ctx.h, self.gens.h, self.k, cnt, sd, _buf(self.label),
                                                 len(self.label), pf, V), "bpp_perm_prove_batch", self.ctx.h)
         praw, vraw = pf.raw, V.raw
+        if raw:
+            return praw, vraw
         return ([praw[i * self.proof_len:(i + 1) * self.proof_len] for i in range(cnt)],
                 [vraw[i * 32 * self.m:(i + 1) * 32 * self.m] for i in range(cnt)])
 
@@ -456,10 +473,17 @@ class PermProver:
         check(rc, "bpp_perm_verify", self.ctx.h)
         return True
 
-    def verify_batch(self, proofs: Sequence[bytes], Vs: Sequence[bytes]) -> bool:
-        pb = b"".join(proofs)
-        vb = b"".join(Vs)
-        rc = self.ctx.lib.bpp_perm_verify_batch(self.ctx.h, self.gens.h, self.k, len(proofs), _buf(self.label),
+    def verify_batch(self, proofs, Vs) -> bool:
+        """proofs / Vs: sequences of per-proof bytes, or the two contiguous
+        buffers (prove_batch(..., raw=True))."""
+        if isinstance(proofs, (bytes, bytearray)):
+            pb, vb = proofs, Vs
+            count = len(pb) // self.proof_len
+            if len(pb) != count * self.proof_len or len(vb) != count * 32 * self.m:
+                raise ValueError("contiguous proofs / V buffers of inconsistent length")
+        else:
+            pb, vb, count = b"".join(proofs), b"".join(Vs), len(proofs)
+        rc = self.ctx.lib.bpp_perm_verify_batch(self.ctx.h, self.gens.h, self.k, count, _buf(self.label),
                                                 len(self.label), _buf(pb), _buf(vb))
         if rc == 6:
             return False
@@ -474,11 +498,14 @@ class PermProver:
 
     def verify_partial(self, job: "VerifyJob", r_all: bytes, first: int, w_begin: int, w_end: int) -> bytes:
         """128-B raw partial of job's MSM over windows [w_begin, w_end) (see
-        bpp_perm_verify_partial); r_all = every rank's r challenges."""
+        bpp_perm_verify_partial); r_all = every rank's r challenges.  None
+        when a proof point does not decode (BPP_ERR_VERIFY)."""
         part = C.create_string_buffer(128)
-        check(self.ctx.lib.bpp_perm_verify_partial(self.ctx.h, self.gens.h, job.h, _buf(r_all), len(r_all) // 32,
-                                                   first, w_begin, w_end, part),
-              "bpp_perm_verify_partial", self.ctx.h)
+        rc = self.ctx.lib.bpp_perm_verify_partial(self.ctx.h, self.gens.h, job.h, _buf(r_all), len(r_all) // 32,
+                                                  first, w_begin, w_end, part)
+        if rc == 6:  # a proof point that does not decode: the batch cannot verify
+            return None
+        check(rc, "bpp_perm_verify_partial", self.ctx.h)
         return part.raw
 
 

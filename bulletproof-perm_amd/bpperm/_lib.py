@@ -43,6 +43,7 @@ SIGNATURES = {
     "bpp_ctx_work_get": (i32, [vp, C.c_char_p, C.POINTER(u64)]),
     "bpp_ctx_work_reset": (None, [vp]),
     "bpp_host_tuning": (i32, [u32]),
+    "bpp_host_threads": (u32, []),
     "bpp_dev_alloc": (i32, [vp, sz, C.POINTER(vp)]),
     "bpp_dev_free": (i32, [vp, vp]),
     "bpp_memcpy_htod": (i32, [vp, vp, vp, sz]),

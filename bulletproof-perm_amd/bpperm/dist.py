@@ -127,6 +127,8 @@ def distributed_verify(prover, proofs, Vs, rank: int, world: int, split: str = "
         r_all = b"".join(torch_all_gather_bytes_var(job.r if ok else bytes(32 * (e - b)), device))
         part = prover.verify_partial(job, r_all, b, 0, job.windows()[1]) if ok else bytes(128)
         job.close()
+    if part is None:  # a proof point did not decode
+        ok, part = False, bytes(128)
     parts = torch_all_gather_bytes(part, device)
     # a rank that rejected a proof in its replay vetoes the batch
     flags = torch_all_gather_bytes(bytes([1 if ok else 0]), device)

@@ -74,7 +74,14 @@ struct bpp_ctx {
   // records and decompressed points in this context's "vj_*" workspaces; a
   // job is valid while its generation is the context's latest
   uint64_t vjob_gen = 0;
+  // the device job's proof-point decompression runs on child context
+  // VJ_CHILD beside the replay: vj_ev_in (inputs uploaded, ctx stream) ->
+  // decompress -> vj_ev_dec (child stream), waited for before the MSM and
+  // before the next upload overwrites the inputs
+  hipEvent_t vj_ev_in = nullptr, vj_ev_dec = nullptr;
+  bool vj_dec_pending = false;
 };
+#define VJ_CHILD BPP_MSM_INFLIGHT
 
 struct bpp_points {
   bpp_ctx* ctx = nullptr;

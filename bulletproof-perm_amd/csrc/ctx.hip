@@ -261,6 +261,8 @@ int bpp_host_tuning(uint32_t flags) {
   return BPP_OK;
 }
 
+uint32_t bpp_host_threads(void) { return par::threads(); }
+
 int bpp_ctx_create(int device, bpp_ctx** out) {
   if (!out) return BPP_ERR_ARG;
   *out = nullptr;
@@ -294,6 +296,8 @@ void bpp_ctx_destroy(bpp_ctx* ctx) {
   }
   for (auto e : ctx->ev_pool) hipEventDestroy(e);
   if (ctx->sync_ev) hipEventDestroy(ctx->sync_ev);
+  if (ctx->vj_ev_in) hipEventDestroy(ctx->vj_ev_in);
+  if (ctx->vj_ev_dec) hipEventDestroy(ctx->vj_ev_dec);
   for (auto& sl : ctx->msm_slot)
     if (sl.done) hipEventDestroy(sl.done);
   hipStreamDestroy(ctx->stream);

@@ -1,7 +1,8 @@
 // Host-side parallel-for over independent proofs (transcripts, challenge
 // scalars, witness polynomials).  A persistent pool (spawning threads per
 // call costs ~20 us each, more than a batch of transcript operations):
-// threads = BPP_HOST_THREADS or min(granted CPUs, 16) / 4; items are claimed
+// threads = BPP_HOST_THREADS or min(granted CPUs / LOCAL_WORLD_SIZE, 16) / 4;
+// items are claimed
 // from an atomic counter; the calling thread works too.  Concurrent calls
 // share the workers; a call from inside a pool task runs inline.
 #pragma once
@@ -46,7 +47,11 @@ inline unsigned threads() {
     // and 30 us with 4); 128 x 12 with 8 / 4 threads 138-144 K / 172-180 K.
     // (round 1: 16 threads x 4 in flight 52-64 K, 8 x 8 75-80 K;
     // tools/EXPERIMENTS.md exp2-4)
-    const unsigned v = e ? (unsigned)atoi(e) : std::max(1u, std::min(16u, granted_cpus()) / 4);
+    // Several ranks on one node (torchrun's LOCAL_WORLD_SIZE) share the
+    // cgroup's CPUs: each sizes its pool from its share.
+    unsigned share = granted_cpus();
+    if (const char* lw = getenv("LOCAL_WORLD_SIZE")) share = std::max(1u, share / std::max(1, atoi(lw)));
+    const unsigned v = e ? (unsigned)atoi(e) : std::max(1u, std::min(16u, share) / 4);
     return std::max(1u, v);
   }();
   return n;

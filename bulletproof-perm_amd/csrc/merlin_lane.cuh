@@ -18,13 +18,18 @@
 #define LANE_STROBE_R 166
 #define LANE_ST_BYTES 200  // one lane's sponge in LDS (8-byte aligned rows)
 
-__device__ __noinline__ static void lane_keccak(uint8_t* st) {
+// (an LDS-typed pointer: through a generic one the out-of-line function's
+// loads and stores would be flat instructions)
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
+__device__ __noinline__ static void lane_keccak(lds_u64* st) {
+#ifdef EXP_NO_KECCAK  // timing experiment only (wrong results)
+  st[0] ^= 1;
+  return;
+#endif
   uint64_t a[25];
-  const uint64_t* w = reinterpret_cast<const uint64_t*>(st);
-  _Pragma("unroll") for (int i = 0; i < 25; ++i) a[i] = w[i];
+  _Pragma("unroll") for (int i = 0; i < 25; ++i) a[i] = st[i];
   keccak_f1600_dev(a);
-  uint64_t* o = reinterpret_cast<uint64_t*>(st);
-  _Pragma("unroll") for (int i = 0; i < 25; ++i) o[i] = a[i];
+  _Pragma("unroll") for (int i = 0; i < 25; ++i) st[i] = a[i];
 }
 
 struct LaneStrobe {
@@ -35,7 +40,7 @@ struct LaneStrobe {
     st[pos] ^= (uint8_t)pos_begin;
     st[pos + 1] ^= 0x04;
     st[LANE_STROBE_R + 1] ^= 0x80;
-    lane_keccak(st);
+    lane_keccak((lds_u64*)st);
     pos = 0;
     pos_begin = 0;
   }

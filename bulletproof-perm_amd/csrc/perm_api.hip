@@ -944,9 +944,12 @@ int verify_partial(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J, con
 }
 
 // pass 1 on the device (bpp_perm_verify_begin_dev): upload the proofs and V,
-// replay every transcript on the GPU (k_verify_replay, one lane per proof),
-// decompress the proof points into the "vj_x" workspace, and return the r
-// challenges.  BPP_ERR_VERIFY if any proof is malformed.
+// replay every transcript on the GPU (k_verify_replay, one lane per proof)
+// and return the r challenges; meanwhile the proof points are decompressed
+// on child stream VJ_CHILD into the "vj_x" workspace (k_verify_decompress,
+// independent of the replay: the 64 replay waves are latency-bound, the
+// decompression throughput-bound).  BPP_ERR_VERIFY if the replay rejects a
+// proof; an undecodable point is reported by verify_partial_dev.
 int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label, size_t llen, size_t count,
                      const uint8_t* proofs, const uint8_t* V, std::unique_ptr<bpp_verify_job>& job) {
   job.reset(new bpp_verify_job);
@@ -961,18 +964,31 @@ int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label,
   if (!count) return BPP_OK;
   if (count > (1u << 26)) return BPP_ERR_ARG;
   const size_t plen = perm::proof_len(C.k), vbytes = (size_t)C.m * 32, npts = count * J.npt;
-  void *d_in = nullptr, *d_rec = nullptr, *d_enc = nullptr, *d_x = nullptr, *d_dbad = nullptr;
+  bpp_ctx* kid = nullptr;
+  BPP_TRY(ctx_child(ctx, VJ_CHILD, &kid));
+  if (!ctx->vj_ev_in) BPP_HIP(hipEventCreateWithFlags(&ctx->vj_ev_in, hipEventDisableTiming));
+  if (!ctx->vj_ev_dec) BPP_HIP(hipEventCreateWithFlags(&ctx->vj_ev_dec, hipEventDisableTiming));
+  // (the previous job's decompression may still read "vj_in")
+  if (ctx->vj_dec_pending) BPP_HIP(hipStreamWaitEvent(ctx->stream, ctx->vj_ev_dec, 0));
+  void *d_in = nullptr, *d_rec = nullptr, *d_x = nullptr, *d_dbad = nullptr;
   {
     HostScope hs(ctx, "verify_upload");
     BPP_TRY(ctx_ws(ctx, "vj_in", count * (plen + vbytes), &d_in));
     BPP_TRY(ctx_h2d2(ctx, d_in, proofs, count * plen, V, count * vbytes));
   }
   HostScope hs(ctx, "verify_replay");
+  const uint32_t* d_pf = (const uint32_t*)d_in;
+  const uint32_t* d_V = (const uint32_t*)((uint8_t*)d_in + count * plen);
   BPP_TRY(ctx_ws(ctx, "vj_rec", count * vrec_n(C) * 32, &d_rec));
-  BPP_TRY(ctx_ws(ctx, "vj_enc", npts * 32, &d_enc));
   BPP_TRY(ctx_ws(ctx, "vj_x", npts * MSM_NIELS_WORDS * 4, &d_x));
   BPP_TRY(ctx_ws(ctx, "vj_dbad", 8, &d_dbad));
-  uint32_t *h_init = nullptr, *h_r = nullptr, *h_bad = nullptr, *h_dbad = nullptr;
+  BPP_HIP(hipMemsetAsync(d_dbad, 0xff, 8, ctx->stream));
+  BPP_HIP(hipEventRecord(ctx->vj_ev_in, ctx->stream));
+  BPP_HIP(hipStreamWaitEvent(kid->stream, ctx->vj_ev_in, 0));
+  BPP_TRY(verify_decompress_dev(kid, C, (uint32_t)count, d_pf, d_V, (uint32_t*)d_x, (unsigned long long*)d_dbad));
+  BPP_HIP(hipEventRecord(ctx->vj_ev_dec, kid->stream));
+  ctx->vj_dec_pending = true;
+  uint32_t *h_init = nullptr, *h_r = nullptr, *h_bad = nullptr;
   {
     uint32_t init[52];
     verify_init_state(C, label, llen, init);
@@ -980,29 +996,18 @@ int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label,
   }
   BPP_TRY(ctx_zc_out(ctx, "vj_r", count * 32, &h_r));
   BPP_TRY(ctx_zc_out(ctx, "vj_bad", count * 4, &h_bad));
-  BPP_TRY(ctx_zc_out(ctx, "vj_dbad_h", 8, &h_dbad));
-  BPP_TRY(verify_replay_dev(ctx, C, (uint32_t)count, h_init, (const uint32_t*)d_in,
-                            (const uint32_t*)((uint8_t*)d_in + count * plen), (uint32_t*)d_rec, (uint32_t*)d_enc, h_r,
-                            h_bad));
-  BPP_HIP(hipMemsetAsync(d_dbad, 0xff, 8, ctx->stream));
-  {
-    ProfScope ps(ctx, "verify_decompress");
-    hipLaunchKernelGGL(k_decompress, dim3((unsigned)((npts + 63) / 64)), dim3(64), 0, ctx->stream,
-                       (const uint32_t*)d_enc, npts, (uint32_t*)d_x, (unsigned long long*)d_dbad);
-  }
-  BPP_TRY(ctx_check_launch(ctx, "k_decompress"));
-  BPP_HIP(hipMemcpyAsync(h_dbad, d_dbad, 8, hipMemcpyDeviceToHost, ctx->stream));
+  BPP_TRY(verify_replay_dev(ctx, C, (uint32_t)count, h_init, d_pf, d_V, (uint32_t*)d_rec, h_r, h_bad));
   BPP_TRY(ctx_sync(ctx));
   uint32_t any = 0;
   for (size_t p = 0; p < count; ++p) any |= h_bad[p];
-  if (any || *(const unsigned long long*)h_dbad != ~0ull) return BPP_ERR_VERIFY;
+  if (any) return BPP_ERR_VERIFY;
   memcpy(J.rs.data(), h_r, count * 32);
   return BPP_OK;
 }
 
 // pass 2 of a device job: weights on the device from all `total` r
-// challenges, the unweighted-then-weighted scalars (k_verify_scalars) and the
-// MSM over windows [wb, we).
+// challenges, the weighted scalars (k_verify_scalars) and the MSM over
+// windows [wb, we); BPP_ERR_VERIFY if a proof point did not decode.
 int verify_partial_dev(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J, const Sc* r_all, size_t total,
                        size_t first, uint32_t wb, uint32_t we, h25519::ge* out) {
   if (J.dctx != ctx || J.dgen != ctx->vjob_gen) {
@@ -1015,9 +1020,10 @@ int verify_partial_dev(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J,
   }
   if (first > total || J.count > total - first) return BPP_ERR_ARG;
   const size_t count = J.count, T = 2 * (size_t)J.C.n_p + 2 + count * J.npt;
-  void *d_rec = nullptr, *d_x = nullptr, *d_sv = nullptr;
+  void *d_rec = nullptr, *d_x = nullptr, *d_sv = nullptr, *d_dbad = nullptr;
   BPP_TRY(ctx_ws(ctx, "vj_rec", count * vrec_n(J.C) * 32, &d_rec));
   BPP_TRY(ctx_ws(ctx, "vj_x", count * J.npt * MSM_NIELS_WORDS * 4, &d_x));
+  BPP_TRY(ctx_ws(ctx, "vj_dbad", 8, &d_dbad));
   BPP_TRY(ctx_ws(ctx, "pv_s", T * 32 + 32, &d_sv));
   {
     HostScope hs(ctx, "verify_terms");
@@ -1028,7 +1034,17 @@ int verify_partial_dev(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J,
     BPP_TRY(verify_weights_dev(ctx, J.C, (uint32_t)count, first, total, h_seed, (uint32_t*)d_rec));
     BPP_TRY(verify_scalars_dev_rec(ctx, J.C, (uint32_t)count, (const uint32_t*)d_rec, (uint32_t*)d_sv));
   }
-  return verify_msm(ctx, G, J.C, count, (const uint32_t*)d_sv, (const uint32_t*)d_x, wb, we, out);
+  uint64_t* h_dbad = nullptr;  // the decompression's verdict, copied behind the MSM
+  BPP_TRY(ctx_zc_out(ctx, "vj_dbad_h", 8, (uint32_t**)&h_dbad));
+  BPP_HIP(hipStreamWaitEvent(ctx->stream, ctx->vj_ev_dec, 0));
+  BPP_HIP(hipMemcpyAsync(h_dbad, d_dbad, 8, hipMemcpyDeviceToHost, ctx->stream));
+  BPP_TRY(verify_msm(ctx, G, J.C, count, (const uint32_t*)d_sv, (const uint32_t*)d_x, wb, we, out));
+  BPP_TRY(ctx_sync(ctx));  // (msm_single_dev has synchronised; this keeps h_dbad's contract)
+  if (*h_dbad != ~0ull) {
+    ctx->err = "undecodable proof point at index " + std::to_string(*h_dbad);
+    return BPP_ERR_VERIFY;
+  }
+  return BPP_OK;
 }
 
 // Verify `count` proofs with ONE MSM: generator scalars summed across proofs

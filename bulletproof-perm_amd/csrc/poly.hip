@@ -29,12 +29,6 @@
 #define POLY_SLOTS 7  // l1 r0 r1 r3 l2 l3 (Montgomery) per gate
 #define POLY_T 256    // lanes per proof; lane i handles gates i, i + POLY_T, ...
 
-FE_INLINE sc sc_one_mont() {
-  sc one = sc_zero();
-  one.v[0] = 1;
-  return sc_to_mont(one);
-}
-
 // aR^e (Montgomery in, Montgomery out), e < 2^31
 FE_INLINE sc sc_pow_small(const sc& aR, uint32_t e, const sc& oneR) {
   sc r = oneR;

@@ -210,6 +210,12 @@ FE_INLINE sc sc_from_mont(const sc& a) {
   return sc_mont(a, one);
 }
 
+FE_INLINE sc sc_one_mont() {
+  sc one = sc_zero();
+  one.v[0] = 1;
+  return sc_to_mont(one);
+}
+
 // canonical w mod l for w < 2^256: w = q 2^252 + rest (q < 16), w - q l =
 // rest - q delta is in (-l, 2^252), one conditional addition of l
 FE_INLINE sc sc_reduce256(const uint32_t w[8]) {

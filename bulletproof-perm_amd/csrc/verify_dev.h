@@ -28,14 +28,19 @@ inline uint32_t vpts_n(const perm::Circuit& C) { return C.m + 8 + 2 * C.lg; }
 // (k_verify_replay): d_proofs [count][proof_len] and d_V [count][m][32] on
 // the device; init = the 52-word transcript state every proof shares (the
 // label's Transcript::new and arithmetic_domain_sep(n_p); verify_init_state).
-// Writes d_rec (weights left zero), d_enc (the proof points' encodings,
-// [count][vpts_n][32]), r_out ([count][32], the t-check weight challenges)
-// and bad ([count] u32, nonzero where a point is the identity encoding, a
+// Writes d_rec (weights left zero), r_out ([count][32], the t-check
+// weight challenges) and bad ([count] u32, nonzero where a point is the identity encoding, a
 // scalar is not canonical or a challenge is zero).  r_out and bad may be
 // pinned host memory (written in place).
 int verify_replay_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const uint32_t* d_init,
-                      const uint32_t* d_proofs, const uint32_t* d_V, uint32_t* d_rec, uint32_t* d_enc,
-                      uint32_t* r_out, uint32_t* bad);
+                      const uint32_t* d_proofs, const uint32_t* d_V, uint32_t* d_rec, uint32_t* r_out,
+                      uint32_t* bad);
+// Decompresses every proof point of the uploaded proofs / V into d_tbl
+// ([count * vpts_n] Niels rows in MSM order); *d_bad = the smallest index of
+// an undecodable encoding (set to ~0 by the caller first).  Independent of
+// the replay (launched on another stream).
+int verify_decompress_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const uint32_t* d_proofs,
+                          const uint32_t* d_V, uint32_t* d_tbl, unsigned long long* d_bad);
 // The 52-word shared transcript prefix for verify_replay_dev.
 void verify_init_state(const perm::Circuit& C, const uint8_t* label, size_t llen, uint32_t out[52]);
 // rec[p][VREC_WT] = perm::batch_weight(seed, first + p) for p < count (one

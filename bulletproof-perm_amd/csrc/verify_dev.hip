@@ -11,6 +11,7 @@
 // the host's largest share of a 4096-proof batch verification (21.6 of 32.3
 // ms on the round-2 box, 4 host threads); here 4096 proofs are 64 waves.
 #include "ctx.h"
+#include "ge_io.cuh"
 #include "merlin_lane.cuh"
 #include "verify_dev.h"
 
@@ -29,6 +30,34 @@ FE_INLINE bool w8_zero(const uint32_t w[8]) {
   return o == 0;
 }
 
+// Per lane a^-1 (Montgomery in, Montgomery out) with one inversion per
+// wave: inclusive and exclusive products over the lanes (Hillis-Steele
+// scans, 6 shuffle steps each way), the wave's total inverted once
+// (uniform control flow), a^-1 = total^-1 * prefix * suffix.  A zero lane
+// value makes every lane's result wrong (its proof is rejected anyway).
+FE_INLINE sc sc_shfl(const sc& a, int src) {
+  sc r;
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) r.v[i] = __shfl(a.v[i], src, 64);
+  return r;
+}
+FE_INLINE sc sc_wave_inverse_mont(const sc& aR) {
+  const int lane = threadIdx.x & 63;
+  const sc oneR = sc_one_mont();
+  sc pre = aR, suf = aR;  // inclusive prefix / suffix products
+  _Pragma("unroll") for (int d = 1; d < 64; d <<= 1) {
+    const sc a = sc_shfl(pre, lane - d < 0 ? lane : lane - d);
+    const sc b = sc_shfl(suf, lane + d > 63 ? lane : lane + d);
+    if (lane >= d) pre = sc_mont(a, pre);
+    if (lane + d <= 63) suf = sc_mont(suf, b);
+  }
+  const sc total = sc_shfl(pre, 63);
+  const sc tinv = sc_to_mont(sc_inv_vartime(sc_from_mont(total)));  // (every lane: the same value)
+  const sc xp = sc_shfl(pre, lane ? lane - 1 : 0), xs = sc_shfl(suf, lane < 63 ? lane + 1 : 63);  // (all lanes shuffle)
+  const sc ex_pre = lane ? xp : oneR;
+  const sc ex_suf = lane < 63 ? xs : oneR;
+  return sc_mont(tinv, sc_mont(ex_pre, ex_suf));
+}
+
 // Proof layout (perm_api.hip serialize, bpp_perm_proof_len): A_I A_O S T1 T3
 // T4 T5 T6 (points), tau_x mu t_hat, L_0 R_0 .. L_{lg-1} R_{lg-1}, a b;
 // 8 words each.
@@ -36,11 +65,12 @@ __global__ void __launch_bounds__(64) k_verify_replay(uint32_t count, uint32_t k
                                                       const uint32_t* __restrict__ init,
                                                       const uint32_t* __restrict__ proofs, uint32_t pw,
                                                       const uint32_t* __restrict__ V, uint32_t* __restrict__ rec,
-                                                      uint32_t* __restrict__ enc, uint32_t npt,
                                                       uint32_t* __restrict__ r_out, uint32_t* __restrict__ bad) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[64 * LANE_ST_BYTES];
-  const uint32_t p = blockIdx.x * 64 + threadIdx.x;
-  if (p >= count) return;  // (no LDS is shared between lanes)
+  // every lane stays active for the wave-wide inversion below: lanes past
+  // the batch shadow the last proof and write nothing
+  const bool live = blockIdx.x * 64 + threadIdx.x < count;
+  const uint32_t p = live ? blockIdx.x * 64 + threadIdx.x : count - 1;
   LaneStrobe t;
   t.st = lds + threadIdx.x * LANE_ST_BYTES;
   {
@@ -51,7 +81,6 @@ __global__ void __launch_bounds__(64) k_verify_replay(uint32_t count, uint32_t k
   }
   const uint32_t m = 2 * k + 1, nrec = VREC_U + 2 * lg;
   uint32_t* __restrict__ R = rec + (size_t)p * nrec * 8;
-  uint32_t* __restrict__ E = enc + (size_t)p * npt * 8;
   const uint32_t* __restrict__ PV = V + (size_t)p * m * 8;
   const uint32_t* __restrict__ PP = proofs + (size_t)p * pw;
   uint32_t w[8];
@@ -59,25 +88,20 @@ __global__ void __launch_bounds__(64) k_verify_replay(uint32_t count, uint32_t k
   // V_0 .. V_{2k-1}, x_perm, V_2k
   for (uint32_t j = 0; j < 2 * k; ++j) {
     ld8(PV + 8 * j, w);
-    st8(E + 8 * j, w);
     t.append32("V", 1, w);
   }
   const sc x_perm = t.challenge_scalar("x_perm", 6);
   ld8(PV + 16 * k, w);
-  st8(E + 16 * k, w);
   t.append32("V", 1, w);
   // A_I, A_O, S (validated), y, z
   ld8(PP, w);
   ok &= !w8_zero(w);
-  st8(E + 8 * m, w);
   t.append32("A_I", 3, w);
   ld8(PP + 8, w);
   ok &= !w8_zero(w);
-  st8(E + 8 * (m + 1), w);
   t.append32("A_O", 3, w);
   ld8(PP + 16, w);
   ok &= !w8_zero(w);
-  st8(E + 8 * (m + 2), w);
   t.append32("S", 1, w);
   const sc y = t.challenge_scalar("y", 1);
   const sc z = t.challenge_scalar("z", 1);
@@ -85,7 +109,6 @@ __global__ void __launch_bounds__(64) k_verify_replay(uint32_t count, uint32_t k
   auto T_i = [&](int i, const char* lab) {
     ld8(PP + 24 + 8 * i, w);
     ok &= !w8_zero(w);
-    st8(E + 8 * (m + 3 + i), w);
     t.append32(lab, 2, w);
   };
   T_i(0, "T1");
@@ -111,11 +134,9 @@ __global__ void __launch_bounds__(64) k_verify_replay(uint32_t count, uint32_t k
   for (uint32_t j = 0; j < lg; ++j) {
     ld8(PL + 16 * j, w);
     ok &= !w8_zero(w);
-    st8(E + 8 * (m + 8 + j), w);
     t.append32("L", 1, w);
     ld8(PL + 16 * j + 8, w);
     ok &= !w8_zero(w);
-    st8(E + 8 * (m + 8 + lg + j), w);
     t.append32("R", 1, w);
     const sc u = t.challenge_scalar("u", 1);
     ok &= !w8_zero(u.v);  // (a zero challenge would fail the batch inversion)
@@ -127,19 +148,24 @@ __global__ void __launch_bounds__(64) k_verify_replay(uint32_t count, uint32_t k
   ok &= !sc_geq_l(a.v) && !sc_geq_l(b.v);
   const sc r = t.challenge_scalar("t-check-weight", 14);
   ok &= !w8_zero(y.v);
-  // y^-1 and u_j^-1 with one inversion (Montgomery's trick over the lane's
-  // own values; the u^-1 slots hold the prefix products meanwhile)
+  // y^-1 and u_j^-1: Montgomery's trick over the lane's own values (the u^-1
+  // slots hold the prefix products meanwhile), then over the wave's 64 lane
+  // products, so the wave runs ONE inversion with uniform control flow (a
+  // per-lane binary-Euclid inversion diverged and took 0.43 of the kernel's
+  // 1.08 ms at 4096 proofs)
   sc acc = sc_to_mont(y);
   for (uint32_t j = 0; j < lg; ++j) {
-    sc_store(R + 8 * (VREC_U + lg + j), acc);
+    if (live) sc_store(R + 8 * (VREC_U + lg + j), acc);
     acc = sc_mont(acc, sc_to_mont(sc_load(R + 8 * (VREC_U + j))));
   }
-  sc inv = sc_to_mont(sc_inv_vartime(sc_from_mont(acc)));
+  sc inv = sc_wave_inverse_mont(acc);
   for (uint32_t j = lg; j-- > 0;) {
-    const sc pre = sc_load(R + 8 * (VREC_U + lg + j));
-    sc_store(R + 8 * (VREC_U + lg + j), sc_from_mont(sc_mont(inv, pre)));
+    const sc pre = j ? sc_load(R + 8 * (VREC_U + lg + j)) : sc_to_mont(y);
+    const sc ui = sc_from_mont(sc_mont(inv, pre));
     inv = sc_mont(inv, sc_to_mont(sc_load(R + 8 * (VREC_U + j))));
+    if (live) sc_store(R + 8 * (VREC_U + lg + j), ui);
   }
+  if (!live) return;
   sc_store(R + 8 * VREC_XPERM, x_perm);
   sc_store(R + 8 * VREC_YINV, sc_from_mont(inv));
   sc_store(R + 8 * VREC_Z, z);
@@ -186,6 +212,36 @@ __global__ void __launch_bounds__(64) k_verify_weights(uint32_t count, uint64_t 
   sc_store(rec + ((size_t)p * nrec + VREC_WT) * 8, wt);
 }
 
+// Decompress every proof point straight from the uploaded proofs and V into
+// the MSM's Niels table (point i = p npt + j in vpts_n order), so that it
+// needs nothing from the replay and runs beside it on another stream.
+// *bad = the smallest index of an undecodable encoding (~0 if none).
+__global__ void __launch_bounds__(64) k_verify_decompress(uint32_t count, uint32_t m, uint32_t lg, uint32_t npt,
+                                                          const uint32_t* __restrict__ proofs, uint32_t pw,
+                                                          const uint32_t* __restrict__ V, uint32_t* __restrict__ tbl,
+                                                          unsigned long long* __restrict__ bad) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)count * npt) return;
+  const uint32_t p = (uint32_t)(i / npt), j = (uint32_t)(i % npt);
+  const uint32_t* src;
+  if (j < m)
+    src = V + ((size_t)p * m + j) * 8;
+  else if (j < m + 8)
+    src = proofs + (size_t)p * pw + 8 * (j - m);  // A_I A_O S T1 T3..T6
+  else if (j < m + 8 + lg)
+    src = proofs + (size_t)p * pw + 88 + 16 * (j - m - 8);  // L_j
+  else
+    src = proofs + (size_t)p * pw + 96 + 16 * (j - m - 8 - lg);  // R_j
+  uint32_t w[8];
+  ld8(src, w);
+  ge_p3 P;
+  if (!ge_ristretto_decode(w, P)) {
+    atomicMin(bad, (unsigned long long)i);
+    P = ge_identity();
+  }
+  store_niels(tbl, (uint32_t)i, ge_niels_from_affine(P.X, P.Y));  // (Z = 1 after decode)
+}
+
 static unsigned grid_for(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
 void verify_init_state(const perm::Circuit& C, const uint8_t* label, size_t llen, uint32_t out[52]) {
@@ -197,14 +253,14 @@ void verify_init_state(const perm::Circuit& C, const uint8_t* label, size_t llen
 }
 
 int verify_replay_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const uint32_t* d_init,
-                      const uint32_t* d_proofs, const uint32_t* d_V, uint32_t* d_rec, uint32_t* d_enc,
-                      uint32_t* r_out, uint32_t* bad) {
+                      const uint32_t* d_proofs, const uint32_t* d_V, uint32_t* d_rec, uint32_t* r_out,
+                      uint32_t* bad) {
   if (!count) return BPP_OK;
   const uint32_t pw = (uint32_t)(perm::proof_len(C.k) / 4);
   {
     ProfScope ps(ctx, "verify_replay_dev");
     hipLaunchKernelGGL(k_verify_replay, dim3(grid_for(count, 64)), dim3(64), 0, ctx->stream, count, C.k, C.lg, C.n_p,
-                       d_init, d_proofs, pw, d_V, d_rec, d_enc, vpts_n(C), r_out, bad);
+                       d_init, d_proofs, pw, d_V, d_rec, r_out, bad);
   }
   return ctx_check_launch(ctx, "k_verify_replay");
 }
@@ -218,4 +274,16 @@ int verify_weights_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, uin
                        seed, d_rec, vrec_n(C));
   }
   return ctx_check_launch(ctx, "k_verify_weights");
+}
+
+int verify_decompress_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const uint32_t* d_proofs,
+                          const uint32_t* d_V, uint32_t* d_tbl, unsigned long long* d_bad) {
+  const size_t n = (size_t)count * vpts_n(C);
+  if (!n) return BPP_OK;
+  {
+    ProfScope ps(ctx, "verify_decompress");
+    hipLaunchKernelGGL(k_verify_decompress, dim3(grid_for(n, 64)), dim3(64), 0, ctx->stream, count, C.m, C.lg,
+                       vpts_n(C), d_proofs, (uint32_t)(perm::proof_len(C.k) / 4), d_V, d_tbl, d_bad);
+  }
+  return ctx_check_launch(ctx, "k_verify_decompress");
 }

@@ -88,6 +88,11 @@ void bpp_ctx_work_reset(bpp_ctx* ctx);
  * BPP_ERR_ARG for unknown flags. */
 #define BPP_TUNE_MALLOC 1u
 int bpp_host_tuning(uint32_t flags);
+/* Threads of the library's host pool (transcripts, scalar bookkeeping),
+ * calling threads included: BPP_HOST_THREADS, else a quarter of this
+ * process's share of the granted CPUs (cgroup quota / LOCAL_WORLD_SIZE),
+ * at most 4. */
+uint32_t bpp_host_threads(void);
 
 /* Device memory helpers, so callers can stage inputs resident in HBM. */
 int bpp_dev_alloc(bpp_ctx* ctx, size_t bytes, void** dptr);
@@ -262,7 +267,9 @@ int bpp_perm_verify_begin(uint32_t k, size_t count, const uint8_t* label, size_t
  * its records and points in ctx's workspaces: it is valid for
  * bpp_perm_verify_partial on the same ctx until the next
  * bpp_perm_verify_begin_dev there (BPP_ERR_ARG after that), and
- * bpp_perm_verify_scalars rejects it (BPP_ERR_ARG). */
+ * bpp_perm_verify_scalars rejects it (BPP_ERR_ARG).  The proof points are
+ * decompressed beside the replay; one that does not decode makes
+ * bpp_perm_verify_partial return BPP_ERR_VERIFY. */
 int bpp_perm_verify_begin_dev(bpp_ctx* ctx, uint32_t k, size_t count, const uint8_t* label, size_t llen,
                               const uint8_t* proofs, const uint8_t* V, uint8_t* r_out, bpp_verify_job** out);
 /* Terms of the job's MSM: 2 n_p + 2 merged generators + count x (m + 8 +

@@ -120,6 +120,10 @@ def test_device_rejects(setup, ctx):
     ud = _tampered(proofs, 60, 11 * 32 + 31, 0x80)
     assert not pr.verify_batch(ud, Vs)
     assert not pr.verify(ud[60], Vs[60])
+    uj = bpperm.VerifyJob(K, ud, Vs, ctx=ctx)
+    assert uj.ok  # (the replay absorbs the bytes; the decompression beside it rejects)
+    assert pr.verify_partial(uj, uj.r, 0, 0, uj.windows()[1]) is None
+    uj.close()
     # the untampered batch still verifies on the same context afterwards
     assert pr.verify_batch(proofs, Vs)
 

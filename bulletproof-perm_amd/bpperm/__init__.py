@@ -205,6 +205,24 @@ class Context:
               "bpp_msm_submit", self.h)
         return t.value
 
+    def msm_submit_host(self, h_scalars, table: PointTable, n: int, w_begin: int = 0, w_end: int = 0) -> int:
+        """As msm_submit with host scalars: a pinned buffer address from
+        host_alloc (int; direct DMA on the MSM's stream) or bytes (staged)."""
+        t = C.c_uint64()
+        ptr = C.c_void_p(h_scalars) if isinstance(h_scalars, int) else _buf(h_scalars)
+        check(self.lib.bpp_msm_submit_host(self.h, ptr, table.handle, n, w_begin, w_end, C.byref(t)),
+              "bpp_msm_submit_host", self.h)
+        return t.value
+
+    def host_alloc(self, nbytes: int) -> int:
+        """Pinned host memory (bpp_host_alloc); free with host_free."""
+        p = C.c_void_p()
+        check(self.lib.bpp_host_alloc(self.h, nbytes, C.byref(p)), "bpp_host_alloc", self.h)
+        return p.value
+
+    def host_free(self, ptr: int):
+        check(self.lib.bpp_host_free(self.h, C.c_void_p(ptr)), "bpp_host_free", self.h)
+
     def msm_collect(self, ticket: int, partial: bool = False) -> bytes:
         out = C.create_string_buffer(128 if partial else 32)
         args = (None, out) if partial else (out, None)
@@ -477,7 +495,7 @@ class PermProver:
         """proofs / Vs: sequences of per-proof bytes, or the two contiguous
         buffers (prove_batch(..., raw=True))."""
         if isinstance(proofs, (bytes, bytearray)):
-            pb, vb = proofs, Vs
+            pb, vb = bytes(proofs), bytes(Vs)
             count = len(pb) // self.proof_len
             if len(pb) != count * self.proof_len or len(vb) != count * 32 * self.m:
                 raise ValueError("contiguous proofs / V buffers of inconsistent length")

@@ -61,6 +61,9 @@ SIGNATURES = {
     "bpp_msm_table_dev_partial": (i32, [vp, vp, vp, sz, u32, u32, vp]),
     "bpp_msm_submit": (i32, [vp, vp, vp, sz, u32, u32, C.POINTER(C.c_uint64)]),
     "bpp_msm_collect": (i32, [vp, C.c_uint64, vp, vp]),
+    "bpp_msm_submit_host": (i32, [vp, vp, vp, sz, u32, u32, C.POINTER(C.c_uint64)]),
+    "bpp_host_alloc": (i32, [vp, sz, C.POINTER(vp)]),
+    "bpp_host_free": (i32, [vp, vp]),
     "bpp_partials_finish": (i32, [vp, sz, vp]),
     "bpp_points_double_compress": (i32, [vp, sz, vp]),
     "bpp_msm_batch": (i32, [vp, sz, vp, vp, vp, vp, vp]),

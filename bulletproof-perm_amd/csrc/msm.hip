@@ -350,9 +350,39 @@ int bpp_msm_table_dev_partial(bpp_ctx* ctx, const void* d_scalars, const bpp_poi
   return BPP_OK;
 }
 
+static int msm_submit(bpp_ctx* ctx, const void* d_scalars, const void* h_scalars, const bpp_points* tbl, size_t n,
+                      uint32_t w_begin, uint32_t w_end, uint64_t* ticket);
+
 int bpp_msm_submit(bpp_ctx* ctx, const void* d_scalars, const bpp_points* tbl, size_t n, uint32_t w_begin,
                    uint32_t w_end, uint64_t* ticket) {
   if (!ctx || !tbl || !ticket || (!d_scalars && n)) return BPP_ERR_ARG;
+  return msm_submit(ctx, d_scalars, nullptr, tbl, n, w_begin, w_end, ticket);
+}
+
+int bpp_msm_submit_host(bpp_ctx* ctx, const void* h_scalars, const bpp_points* tbl, size_t n, uint32_t w_begin,
+                        uint32_t w_end, uint64_t* ticket) {
+  if (!ctx || !tbl || !ticket || (!h_scalars && n)) return BPP_ERR_ARG;
+  return msm_submit(ctx, nullptr, h_scalars, tbl, n, w_begin, w_end, ticket);
+}
+
+int bpp_host_alloc(bpp_ctx* ctx, size_t bytes, void** hptr) {
+  if (!ctx || !hptr) return BPP_ERR_ARG;
+  BPP_HIP(hipSetDevice(ctx->device));
+  BPP_HIP(hipHostMalloc(hptr, bytes ? bytes : 1));
+  return BPP_OK;
+}
+
+int bpp_host_free(bpp_ctx* ctx, void* hptr) {
+  if (!ctx) return BPP_ERR_ARG;
+  BPP_HIP(hipHostFree(hptr));
+  return BPP_OK;
+}
+
+// d_scalars (device) or h_scalars (host: copied on the slot's stream, so the
+// upload of MSM i+1 overlaps MSM i's kernels; a direct DMA from pinned
+// memory, through the slot's staging arena from pageable memory)
+static int msm_submit(bpp_ctx* ctx, const void* d_scalars, const void* h_scalars, const bpp_points* tbl, size_t n,
+                      uint32_t w_begin, uint32_t w_end, uint64_t* ticket) {
   if (n > tbl->n || n >= 0x80000000ull) return BPP_ERR_LEN;
   const uint32_t c = msm_choose_c((double)(n ? n : 1));
   const uint32_t W = (254 + c - 1) / c;
@@ -388,6 +418,31 @@ int bpp_msm_submit(bpp_ctx* ctx, const void* d_scalars, const bpp_points* tbl, s
   sl.wb = w_begin;
   sl.Wn = w_end - w_begin;
   sl.nterms = 1;
+  if (h_scalars && n && sl.Wn) {
+    void* d = nullptr;
+    int rc = ctx_ws(ch, "sub_sc", n * 32, &d);
+    if (!rc) {
+      hipPointerAttribute_t at;
+      const bool pinned = hipPointerGetAttributes(&at, h_scalars) == hipSuccess && at.type == hipMemoryTypeHost;
+      (void)hipGetLastError();  // (a pageable pointer leaves an error code behind)
+      // (measured at 2^20, 3 in flight, tools/host_msm_probe.py: resident
+      // scalars 0.875 ms per MSM; pinned + this DMA 1.226; pageable staged
+      // through the slot's arena 1.133; pinned read in place by the digit
+      // kernel (zero copy) 1.397 -- its PCIe-bound blocks held CUs the other
+      // MSMs' accumulations needed)
+      if (pinned) {
+        ProfScope ps(ch, "msm_upload");
+        if (hipMemcpyAsync(d, h_scalars, n * 32, hipMemcpyHostToDevice, ch->stream) != hipSuccess) rc = BPP_ERR_DEVICE;
+      } else {
+        rc = ctx_h2d(ch, d, h_scalars, n * 32);
+      }
+    }
+    if (rc) {
+      ctx->err = ch->err.empty() ? "bpp_msm_submit_host: scalar upload failed" : ch->err;
+      return rc;
+    }
+    d_scalars = d;
+  }
   if (n && sl.Wn) {
     // (in-flight MSMs share the device freely: serialising their
     // accumulations measured slower, 1.17 vs 1.04 ms per 2^20 MSM)

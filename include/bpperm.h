@@ -146,6 +146,18 @@ int bpp_msm_table_dev_partial(bpp_ctx* ctx, const void* d_scalars, const bpp_poi
 int bpp_msm_submit(bpp_ctx* ctx, const void* d_scalars, const bpp_points* tbl, size_t n, uint32_t w_begin,
                    uint32_t w_end, uint64_t* ticket);
 int bpp_msm_collect(bpp_ctx* ctx, uint64_t ticket, uint8_t out[32], uint8_t partial[128]);
+/* The same with host scalars (the shape of the reference's
+ * vartime_multiscalar_mul(scalars, points), circuit_lib.rs:187): the n x 32
+ * bytes are copied to the device on the MSM's own stream, so in a stream of
+ * submits the upload of one MSM overlaps the others' kernels.  From pinned
+ * memory (bpp_host_alloc) the copy is a direct DMA; pageable memory goes
+ * through a staging copy first.  h_scalars must stay valid and unchanged
+ * until collect. */
+int bpp_msm_submit_host(bpp_ctx* ctx, const void* h_scalars, const bpp_points* tbl, size_t n, uint32_t w_begin,
+                        uint32_t w_end, uint64_t* ticket);
+/* Pinned (page-locked) host memory for bpp_msm_submit_host inputs. */
+int bpp_host_alloc(bpp_ctx* ctx, size_t bytes, void** hptr);
+int bpp_host_free(bpp_ctx* ctx, void* hptr);
 /* Sum raw extended partial points (count x 128 bytes) and compress. */
 int bpp_partials_finish(const uint8_t* partials, size_t count, uint8_t out[32]);
 /* Host batch encoding of doubled points: out[i] = compress(2 * P_i) for raw
@@ -238,7 +250,13 @@ int bpp_perm_prove_batch(bpp_ctx* ctx, const bpp_gens* g, uint32_t k, size_t cou
  * entropy per proof from the caller (seeds32, count x 32 B), or seeds32 =
  * NULL to draw them from the OS CSPRNG (getrandom), as the reference draws
  * from thread_rng (circuit_lib.rs:175, weights.rs:39,59).  The draws are
- * those above with the 32-byte seed32 in place of the 8-byte seed. */
+ * those above with the 32-byte seed32 in place of the 8-byte seed.
+ * Secret lifetime: the seeds' draws, the witness and the blinding scalars
+ * stay in this process's memory after the call -- in the context's device
+ * workspaces and pinned staging arena and in the calling thread's reused
+ * prover states -- until they are overwritten by the next batch or freed by
+ * bpp_ctx_destroy / thread exit (the library does not wipe them between
+ * batches; the caller's own seeds32 buffer is the caller's to wipe). */
 int bpp_perm_prove_batch_entropy(bpp_ctx* ctx, const bpp_gens* g, uint32_t k, size_t count, const uint8_t* seeds32,
                                  const uint8_t* label, size_t llen, uint8_t* proofs_out, uint8_t* V_out);
 /* BPP_OK or BPP_ERR_VERIFY (ProofError::VerificationError). One GPU MSM. */

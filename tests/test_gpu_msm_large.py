@@ -117,6 +117,32 @@ def test_msm_async_submit_collect(ctx, big_table):
     ctx.dev_free(db)
 
 
+def test_msm_submit_host_scalars(ctx, big_table):
+    """bpp_msm_submit_host (host scalars, the reference's call shape): from
+    pinned memory (the H2D copy on the MSM's own stream) and from pageable
+    bytes (staged), several in flight, a window range; all equal the
+    resident-scalar MSM and the C port."""
+    import ctypes
+
+    import bpperm
+    from bpperm import dist as bdist
+    raw, tbl = big_table
+    n = 1 << 17
+    sa, sb_ = _sb(_scalars(n, 41)), _sb(_scalars(n, 42))
+    want_a = cport.msm(sa, cport.from_uniform(raw[: 64 * n]))
+    want_b = ctx.msm_table(sb_, tbl, n)
+    ha, hb = ctx.host_alloc(32 * n), ctx.host_alloc(32 * n)
+    ctypes.memmove(ha, sa, 32 * n)
+    ctypes.memmove(hb, sb_, 32 * n)
+    ticks = [ctx.msm_submit_host(ha, tbl, n), ctx.msm_submit_host(hb, tbl, n), ctx.msm_submit_host(sa, tbl, n)]
+    assert [ctx.msm_collect(t) for t in ticks] == [want_a, want_b, want_a]
+    c, W = bpperm.msm_windows(n)
+    parts = [ctx.msm_collect(ctx.msm_submit_host(hb, tbl, n, a, b), partial=True) for a, b in bdist.window_ranges(W, 2)]
+    assert bpperm.partials_finish(parts) == want_b
+    ctx.host_free(ha)
+    ctx.host_free(hb)
+
+
 def test_msm_2p22_config5_window_partition(ctx):
     """Config 5 shape (one 2^22-term batch-verify MSM, bucket windows
     partitioned over 8 GPUs), rehearsed on one GPU: the 8 ranks' window

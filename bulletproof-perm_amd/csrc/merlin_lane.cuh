@@ -184,3 +184,31 @@ FE_INLINE sc sc_inv_vartime(const sc& a) {
   }
   return w8_is_one(u) ? x1 : x2;
 }
+
+// Per lane a^-1 (Montgomery in, Montgomery out) with one inversion per
+// wave: inclusive and exclusive products over the lanes (Hillis-Steele
+// scans, 6 shuffle steps each way), the wave's total inverted once
+// (uniform control flow), a^-1 = total^-1 * prefix * suffix.  A zero lane
+// value makes every lane's result wrong (its proof is rejected anyway).
+FE_INLINE sc sc_shfl(const sc& a, int src) {
+  sc r;
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) r.v[i] = __shfl(a.v[i], src, 64);
+  return r;
+}
+FE_INLINE sc sc_wave_inverse_mont(const sc& aR) {
+  const int lane = threadIdx.x & 63;
+  const sc oneR = sc_one_mont();
+  sc pre = aR, suf = aR;  // inclusive prefix / suffix products
+  _Pragma("unroll") for (int d = 1; d < 64; d <<= 1) {
+    const sc a = sc_shfl(pre, lane - d < 0 ? lane : lane - d);
+    const sc b = sc_shfl(suf, lane + d > 63 ? lane : lane + d);
+    if (lane >= d) pre = sc_mont(a, pre);
+    if (lane + d <= 63) suf = sc_mont(suf, b);
+  }
+  const sc total = sc_shfl(pre, 63);
+  const sc tinv = sc_to_mont(sc_inv_vartime(sc_from_mont(total)));  // (every lane: the same value)
+  const sc xp = sc_shfl(pre, lane ? lane - 1 : 0), xs = sc_shfl(suf, lane < 63 ? lane + 1 : 63);  // (all lanes shuffle)
+  const sc ex_pre = lane ? xp : oneR;
+  const sc ex_suf = lane < 63 ? xs : oneR;
+  return sc_mont(tinv, sc_mont(ex_pre, ex_suf));
+}

@@ -80,6 +80,9 @@ struct bpp_ctx {
   // before the next upload overwrites the inputs
   hipEvent_t vj_ev_in = nullptr, vj_ev_dec = nullptr;
   bool vj_dec_pending = false;
+  // bpp_msm_submit_host: the uploaded scalars of this (child) context's MSM
+  void* up_sc = nullptr;
+  size_t up_sc_bytes = 0;
 };
 #define VJ_CHILD BPP_MSM_INFLIGHT
 

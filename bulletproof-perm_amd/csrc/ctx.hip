@@ -296,6 +296,7 @@ void bpp_ctx_destroy(bpp_ctx* ctx) {
   }
   for (auto e : ctx->ev_pool) hipEventDestroy(e);
   if (ctx->sync_ev) hipEventDestroy(ctx->sync_ev);
+  if (ctx->up_sc) hipFree(ctx->up_sc);
   if (ctx->vj_ev_in) hipEventDestroy(ctx->vj_ev_in);
   if (ctx->vj_ev_dec) hipEventDestroy(ctx->vj_ev_dec);
   for (auto& sl : ctx->msm_slot)

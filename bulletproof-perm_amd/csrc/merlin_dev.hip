@@ -61,6 +61,54 @@ __global__ void __launch_bounds__(64) k_ipa_transcript_step(uint32_t P, uint8_t*
   sc_store(u_out + 16 * (size_t)p + 8, uiR);
 }
 
+// The prover's V phase for P proofs, one lane each: from the shared state
+// after Transcript::new(label) + arithmetic_domain_sep(n_p) (init: 50 state
+// words + pos + pos_begin), append_point("V", V_i) for i < 2k and
+// x_perm = challenge_scalar("x_perm") (perm_api.hip prove_batch; the
+// reference's create, circuit_lib.rs:139-186, in sound form).  venc: [P][2k]
+// encodings on the device.  states_out: [P][MERLIN_DEV_STATE_BYTES],
+// xperm_out: [P][8] canonical words (both may be pinned host memory).
+__global__ void __launch_bounds__(64) k_prove_v_transcript(uint32_t P, uint32_t k, const uint32_t* __restrict__ init,
+                                                           const uint32_t* __restrict__ venc,
+                                                           uint8_t* __restrict__ states_out,
+                                                           uint32_t* __restrict__ xperm_out) {
+  __shared__ __attribute__((aligned(16))) uint8_t st_lds[64 * LANE_ST_BYTES];
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;  // (no LDS or shuffle shared between lanes)
+  LaneStrobe s;
+  s.st = st_lds + threadIdx.x * LANE_ST_BYTES;
+  {
+    uint32_t* d = reinterpret_cast<uint32_t*>(s.st);
+    for (int i = 0; i < 50; ++i) d[i] = init[i];
+    s.pos = init[50];
+    s.pos_begin = init[51];
+  }
+  const uint32_t* V = venc + (size_t)p * 2 * k * 8;
+  for (uint32_t j = 0; j < 2 * k; ++j) {
+    const uint4 a = reinterpret_cast<const uint4*>(V + 8 * j)[0], b = reinterpret_cast<const uint4*>(V + 8 * j)[1];
+    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    s.append32("V", 1, w);
+  }
+  const sc x = s.challenge_scalar("x_perm", 6);
+  uint8_t* g = states_out + (size_t)p * MERLIN_DEV_STATE_BYTES;
+  const uint2* src = reinterpret_cast<const uint2*>(s.st);
+  uint2* dst = reinterpret_cast<uint2*>(g);
+  for (int i = 0; i < 25; ++i) dst[i] = src[i];
+  reinterpret_cast<uint32_t*>(g)[50] = s.pos | (s.pos_begin << 8) | ((1u | 2u | 4u) << 16);  // pos, pos_begin, cur_flags
+  sc_store(xperm_out + 8 * (size_t)p, x);
+}
+
+int prove_v_transcript_dev(bpp_ctx* ctx, uint32_t P, uint32_t k, const uint32_t* init, const uint32_t* d_venc,
+                           uint8_t* states_out, uint32_t* xperm_out) {
+  if (!P) return BPP_OK;
+  {
+    ProfScope ps(ctx, "prove_v_transcript");
+    hipLaunchKernelGGL(k_prove_v_transcript, dim3((P + 63) / 64), dim3(64), 0, ctx->stream, P, k, init, d_venc,
+                       states_out, xperm_out);
+  }
+  return ctx_check_launch(ctx, "k_prove_v_transcript");
+}
+
 static unsigned grid_for(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
 int ipa_transcript_step_dev(bpp_ctx* ctx, uint32_t P, uint8_t* d_states, const uint8_t* d_enc, uint32_t* d_u) {

@@ -22,10 +22,6 @@
 // loads and stores would be flat instructions)
 typedef __attribute__((address_space(3))) uint64_t lds_u64;
 __device__ __noinline__ static void lane_keccak(lds_u64* st) {
-#ifdef EXP_NO_KECCAK  // timing experiment only (wrong results)
-  st[0] ^= 1;
-  return;
-#endif
   uint64_t a[25];
   _Pragma("unroll") for (int i = 0; i < 25; ++i) a[i] = st[i];
   keccak_f1600_dev(a);

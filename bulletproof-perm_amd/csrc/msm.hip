@@ -419,9 +419,25 @@ static int msm_submit(bpp_ctx* ctx, const void* d_scalars, const void* h_scalars
   sl.Wn = w_end - w_begin;
   sl.nterms = 1;
   if (h_scalars && n && sl.Wn) {
-    void* d = nullptr;
-    int rc = ctx_ws(ch, "sub_sc", n * 32, &d);
-    if (!rc) {
+    int rc = BPP_OK;
+    if (ch->up_sc_bytes < n * 32) {
+      if (ch->up_sc) BPP_HIP(hipFree(ch->up_sc));
+      ch->up_sc = nullptr;
+      ch->up_sc_bytes = 0;
+      // (BPP_MSM_UP_CACHED=1: an ordinary allocation; by default uncached,
+      // so that the upload's 32 B x n writes do not evict the point table
+      // the other MSMs' accumulations gather from the caches; the digit
+      // kernel reads each scalar once)
+      const bool cached = getenv("BPP_MSM_UP_CACHED") && atoi(getenv("BPP_MSM_UP_CACHED"));
+      if (cached) {
+        BPP_HIP(hipMalloc(&ch->up_sc, n * 32));
+      } else {
+        BPP_HIP(hipExtMallocWithFlags(&ch->up_sc, n * 32, hipDeviceMallocUncached));
+      }
+      ch->up_sc_bytes = n * 32;
+    }
+    void* d = ch->up_sc;
+    {
       hipPointerAttribute_t at;
       const bool pinned = hipPointerGetAttributes(&at, h_scalars) == hipSuccess && at.type == hipMemoryTypeHost;
       (void)hipGetLastError();  // (a pageable pointer leaves an error code behind)

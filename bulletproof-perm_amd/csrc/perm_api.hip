@@ -34,6 +34,7 @@
 #include "poly.h"
 #include "layout.h"
 #include "verify_dev.h"
+#include "merlin_dev.h"
 
 using hsc::Sc;
 
@@ -185,6 +186,17 @@ int msm_terms(bpp_ctx* ctx, const std::vector<Sc>& sc, const std::vector<uint32_
   return msm_multi(ctx, d_s, (const uint32_t*)d_i, off, pts, res);
 }
 
+// The prover's V transcript phase on the device (k_prove_v_transcript,
+// BPP_PROVE_DEV_V=1) instead of the host's 8-way lockstep Keccak.  Off:
+// measured 244-250 K vs 264-266 K proofs/s at 256 x 12 in flight (three
+// interleaved passes, tools/gpu_ab_env_prove.sh) -- the host is not the
+// bound (8 of 16 cores busy), and the 4-wave kernel's ~0.3 ms latency
+// lands on every batch's critical path.
+bool dev_v_transcript() {
+  const char* e = getenv("BPP_PROVE_DEV_V");
+  return e && atoi(e) != 0;
+}
+
 // Per-proof prover state carried between the lockstep phases.  The states
 // (and their vectors) persist per driver thread across batches: a host
 // profile of 8 batches in flight spent ~20 % of the host CPU in malloc /
@@ -321,11 +333,31 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
       denc = h;
     }
     d_gx_half = (uint32_t*)dgx;  // (filled by k_draws above)
+    // the 2k V appends and x_perm on the device (k_prove_v_transcript, one
+    // lane per proof; the host's share of a batch was ~10 us of CPU per
+    // proof here, its largest transcript phase): encodings to the device,
+    // copied back for the proofs, and the transcript states imported after
+    const bool dev_v = dev_v_transcript();
+    uint8_t* h_st = nullptr;
+    uint32_t* h_xp = nullptr;
     {
       HostScope hk(ctx, "ped_kernels");
+      void* dvenc = nullptr;
+      if (dev_v) BPP_TRY(ctx_ws(ctx, "pv_enc_d", nv * 32, &dvenc));
       // (values 1..k and pi + 1 <= k: the public bound k + 1)
-      BPP_TRY(pedersen_dev(ctx, G, (const uint32_t*)dv, (const uint32_t*)dg, nv, (uint32_t*)denc, nullptr,
-                           (uint64_t)k + 1));
+      BPP_TRY(pedersen_dev(ctx, G, (const uint32_t*)dv, (const uint32_t*)dg, nv,
+                           dev_v ? (uint32_t*)dvenc : (uint32_t*)denc, nullptr, (uint64_t)k + 1));
+      if (dev_v) {
+        BPP_HIP(hipMemcpyAsync(denc, dvenc, nv * 32, hipMemcpyDeviceToHost, ctx->stream));
+        uint32_t init[52], *h_init = nullptr;
+        verify_init_state(C, label, llen, init);  // (the same shared prefix as the verifier's)
+        BPP_TRY(ctx_zc_in(ctx, "pv_init", init, sizeof init, &h_init));
+        uint32_t* hs_ = nullptr;
+        BPP_TRY(ctx_zc_out(ctx, "pv_states", P * MERLIN_DEV_STATE_BYTES, &hs_));
+        BPP_TRY(ctx_zc_out(ctx, "pv_xperm", P * 32, &h_xp));
+        h_st = (uint8_t*)hs_;
+        BPP_TRY(prove_v_transcript_dev(ctx, (uint32_t)P, k, h_init, (const uint32_t*)dvenc, h_st, h_xp));
+      }
     }
     std::vector<Enc32>& V = scr.V;
     V.resize(nv);
@@ -334,26 +366,34 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
       BPP_TRY(ctx_sync(ctx));
       memcpy(V.data(), denc, nv * 32);
     }
-    par::for_each(P, [&](size_t p) { Ps[p].V.assign(V.begin() + p * 2 * k, V.begin() + (p + 1) * 2 * k); });
-    // the 2k "V" appends and x_perm of eight proofs at a time in lockstep
-    // on the 8-way Keccak (byte-identical; 2.5x on this phase's ~26 us of
-    // permutations per proof)
-    merlin::lockstep_x8(
-        trs, for_groups,
-        [&](merlin::TranscriptX8& T8, const size_t* idx, size_t real) {
-          const uint8_t* msg[8];
-          for (uint32_t i = 0; i < 2 * k; ++i) {
-            for (size_t j = 0; j < 8; ++j) msg[j] = V[idx[j] * 2 * k + i].data();
-            T8.append("V", msg, 32);
-          }
-          hsc::Sc xp[8];
-          T8.challenge_scalar("x_perm", xp);
-          for (size_t j = 0; j < real; ++j) S[idx[j]]->x_perm = xp[j];
-        },
-        [&](size_t p) {
-          for (auto& e : Ps[p].V) S[p]->tr.append_point("V", e.data());
-          S[p]->x_perm = S[p]->tr.challenge_scalar("x_perm");
-        });
+    par::for_each(P, [&](size_t p) {
+      Ps[p].V.assign(V.begin() + p * 2 * k, V.begin() + (p + 1) * 2 * k);
+      if (dev_v) {
+        merlin_state_import(S[p]->tr, h_st + p * MERLIN_DEV_STATE_BYTES);
+        memcpy(&S[p]->x_perm, h_xp + 8 * p, 32);  // (canonical Sc == its 32 bytes)
+      }
+    });
+    if (!dev_v) {
+      // the 2k "V" appends and x_perm of eight proofs at a time in lockstep
+      // on the 8-way Keccak (byte-identical; 2.5x on this phase's ~26 us of
+      // permutations per proof)
+      merlin::lockstep_x8(
+          trs, for_groups,
+          [&](merlin::TranscriptX8& T8, const size_t* idx, size_t real) {
+            const uint8_t* msg[8];
+            for (uint32_t i = 0; i < 2 * k; ++i) {
+              for (size_t j = 0; j < 8; ++j) msg[j] = V[idx[j] * 2 * k + i].data();
+              T8.append("V", msg, 32);
+            }
+            hsc::Sc xp[8];
+            T8.challenge_scalar("x_perm", xp);
+            for (size_t j = 0; j < real; ++j) S[idx[j]]->x_perm = xp[j];
+          },
+          [&](size_t p) {
+            for (auto& e : Ps[p].V) S[p]->tr.append_point("V", e.data());
+            S[p]->x_perm = S[p]->tr.challenge_scalar("x_perm");
+          });
+    }
   }
   // V_2k = commit(x_perm, gamma_2k): halved scalars (x_perm / 2 from the
   // host, gamma_2k / 2 from k_draws), encoded as 2 (C / 2) on the host

@@ -61,3 +61,22 @@ def test_device_transcript_proofs_match_host_path(gens128, monkeypatch):
         want, wv = cport.cpu_prove(52, seeds[i])
         assert dev_p[i] == want and dev_v[i] == b"".join(wv)
     assert pr.verify_batch(dev_p, dev_v)
+
+
+@pytest.mark.parametrize("k", [52, 5])
+def test_device_v_transcript_matches_host_path(gens128, monkeypatch, k):
+    """The prover's V phase on the device (BPP_PROVE_DEV_V=1,
+    k_prove_v_transcript: 2k V appends + x_perm per lane) gives the same
+    proof bytes as the host's 8-way lockstep transcripts (70 proofs: a
+    short last wave), also together with the device IPA transcript."""
+    import bpperm
+    pr = bpperm.PermProver(gens128, k)
+    seeds = list(range(4000, 4070))
+    monkeypatch.setenv("BPP_PROVE_DEV_V", "0")
+    host_p, host_v = pr.prove_batch(seeds)
+    monkeypatch.setenv("BPP_PROVE_DEV_V", "1")
+    dev_p, dev_v = pr.prove_batch(seeds)
+    assert dev_p == host_p and dev_v == host_v
+    monkeypatch.setenv("BPP_IPA_DEVICE_MERLIN", "1")
+    both_p, _ = pr.prove_batch(seeds)
+    assert both_p == host_p

@@ -6,5 +6,5 @@ export SHARED_GENS=1
 for rep in 1 2; do
 for cfg in "$@"; do
   T=${cfg%%:*}; H=${cfg##*:}
-  echo -n "T=$T threads=$H: "; BPP_HOST_THREADS=$H timeout -k 10 120 python tools/prove_inflight_exp.py 128 $T 24 || exit 1
+  echo -n "T=$T threads=$H: "; BPP_HOST_THREADS=$H timeout -k 10 120 python tools/prove_inflight_exp.py ${B:-256} $T ${R:-8} || exit 1
 done; done

@@ -1,7 +1,8 @@
 """Host-scalar MSM stream probe: per-call host time of bpp_msm_submit_host and
 bpp_msm_collect (does the submit block on the upload?), for pinned zero copy,
 pinned + copy (BPP_MSM_HOST_COPY=1) and pageable bytes, 2^20 pairs, 3 in
-flight.   python tools/host_msm_probe.py"""
+flight.   python tools/host_msm_probe.py
+(BPP_MSM_UP_CACHED=1: the upload buffer as an ordinary cached allocation)"""
 import ctypes
 import hashlib
 import os
@@ -27,11 +28,7 @@ def main():
     d = [ctx.dev_alloc(32 * n) for _ in sc]
     for p, x in zip(d, sc):
         ctx.htod(p, x)
-    for mode in ("resident", "pinned", "pinned-copy", "pageable"):
-        if mode == "pinned-copy":
-            os.environ["BPP_MSM_HOST_COPY"] = "1"
-        else:
-            os.environ.pop("BPP_MSM_HOST_COPY", None)
+    for mode in ("resident", "pinned", "pageable"):
 
         def sub(i):
             if mode == "resident":

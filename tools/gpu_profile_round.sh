@@ -1,8 +1,9 @@
 # One GPU call per round for the judged evidence: -m gpu tests + smoke, the
 # full bench line, kernel-trace stats (MSM stream traced one MSM at a time,
 # --inflight 1, so each launch is timed alone and its average matches the
-# bench line's kernel_ms; one 256-proof batch), FETCH_SIZE / WRITE_SIZE PMC
-# passes over the MSM bench, and the prover PMC passes (gpu_pmc_prover.sh).
+# bench line's kernel_ms; one 256-proof batch; three config-5 batch
+# verifications), FETCH_SIZE / WRITE_SIZE PMC passes over the MSM bench, and
+# the prover and MSM SQ counter passes (gpu_pmc_prover.sh, ... msm).
 # Usage (on the box): bash tools/gpu_profile_round.sh <tag>
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -17,7 +18,9 @@ timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail 
 python -c "import json;d=json.load(open('$OUT/bench.json'));p=d['proofs'];print(d['value'],d['ms_per_step'],d['result_ok'],p['value'],p['verify_batch_proofs_per_sec'],d['verify_batch']['value'])"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu --proofs-per-gpu 0 --verify-proofs 0 --inflight 1 > $OUT/trace_log.txt 2>&1 || { echo "trace failed"; exit 1; }
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace_proofs -o run --output-format csv -- python3 tools/prove_batch_once.py 256 > $OUT/trace_proofs_log.txt 2>&1 || { echo "proof trace failed"; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_verify -o run --output-format csv -- python3 tools/verify_stages.py --reps 3 > $OUT/trace_verify_log.txt 2>&1 || { echo "verify trace failed"; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu --proofs-per-gpu 0 --verify-proofs 0 > $OUT/pmc_fetch_log.txt 2>&1 || { echo "pmc fetch failed"; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu --proofs-per-gpu 0 --verify-proofs 0 > $OUT/pmc_write_log.txt 2>&1 || { echo "pmc write failed"; exit 1; }
 bash tools/gpu_pmc_prover.sh $TAG || exit 1
+bash tools/gpu_pmc_prover.sh $TAG msm || exit 1
 echo done

@@ -58,6 +58,9 @@ def main():
     stats = src / "trace_proofs" / "run_kernel_stats.csv"
     if stats.exists():
         shutil.copy(stats, ROOT / "profiles" / f"{tag}_prove_batch256_kernel_stats.csv")
+    stats = src / "trace_verify" / "run_kernel_stats.csv"
+    if stats.exists():
+        shutil.copy(stats, ROOT / "profiles" / f"{tag}_verify4096_kernel_stats.csv")
     b = src / "bench.json"
     if b.exists():
         shutil.copy(b, ROOT / "profiles" / f"{tag}_bench.json")

@@ -227,6 +227,49 @@ struct ProverState {
   Sc t[7];
 };
 
+std::vector<std::unique_ptr<ProverState>>& prover_states_tl() {
+  static thread_local std::vector<std::unique_ptr<ProverState>> S;
+  return S;
+}
+std::pair<uint8_t*, size_t>& last_stage_tl() {
+  static thread_local std::pair<uint8_t*, size_t> st{nullptr, 0};
+  return st;
+}
+std::vector<Proof>& proofs_tl();
+
+// Wipes what the last batch proved on this thread and context left of its
+// secrets: the draw templates and pi in the pinned staging arena
+// and on the device, the device workspaces holding blindings, witness and
+// the l / r vectors, the host buffers of the T-commitment inputs, and the
+// calling thread's reused prover states and proof objects (pi).  Called by
+// the production entry point (bpp_perm_prove_batch_entropy).
+int prove_wipe(bpp_ctx* ctx) {
+  static const char* dev[] = {"pb_rng_in", "pb_gamma", "mt_s", "pv_v", "pv_g", "pv_gx", "poly_vec", "poly_hf",
+                              "pf_l", "pf_r", "ipa_am", "ipa_bm", "ipa_am1", "ipa_bm1"};
+  for (const char* n : dev) {
+    auto it = ctx->ws.find(n);
+    if (it != ctx->ws.end() && it->second.p) BPP_HIP(hipMemsetAsync(it->second.p, 0, it->second.bytes, ctx->stream));
+  }
+  BPP_TRY(ctx_sync(ctx));
+  for (const char* n : {"pp_v", "pp_g"}) {
+    auto it = ctx->host_bufs.find(n);
+    if (it != ctx->host_bufs.end() && it->second.first) memset(it->second.first, 0, it->second.second);
+  }
+  auto& st = last_stage_tl();
+  if (st.first) memset(st.first, 0, st.second);
+  st = {nullptr, 0};
+  for (auto& S : prover_states_tl()) {
+    perm::RandomDraws& d = S->d;
+    std::fill(d.pi.begin(), d.pi.end(), 0u);
+    for (auto* v : {&d.gamma, &d.sL, &d.sR, &d.taus, &S->vals, &S->aL, &S->aR, &S->aO})
+      std::fill(v->begin(), v->end(), hsc::zero());
+    d.alpha = d.beta = d.rho = hsc::zero();
+    for (Sc& t : S->t) t = hsc::zero();
+  }
+  for (Proof& P : proofs_tl()) std::fill(P.pi.begin(), P.pi.end(), 0u);
+  return BPP_OK;
+}
+
 // Proves `seeds.size()` permutation proofs in lockstep: every GPU step
 // (Pedersen V, Pedersen V_2k, the A_I/A_O/S MSMs, Pedersen T, each IPA
 // round) is ONE launch sequence for the whole batch, and the per-proof host
@@ -240,8 +283,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
   if (!P) return BPP_OK;
   // (a plain reference: pool workers must reach THIS thread's states, a
   // thread_local named inside their lambdas would be their own)
-  static thread_local std::vector<std::unique_ptr<ProverState>> S_tl;
-  std::vector<std::unique_ptr<ProverState>>& S = S_tl;
+  std::vector<std::unique_ptr<ProverState>>& S = prover_states_tl();
   while (S.size() < P) S.emplace_back(new ProverState());
   par::for_each(P, [&](size_t p) { S[p]->tr = merlin::Transcript(label, llen); });
   static thread_local ProverScratch scr_tl;
@@ -282,6 +324,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     // read in place instead, by k_draws through LDS, measured within noise)
     uint8_t* stage = nullptr;
     BPP_TRY(ctx_h2d_stage(ctx, P * tlen + (size_t)P * k * 4, &stage));
+    last_stage_tl() = {stage, P * tlen + (size_t)P * k * 4};  // (prove_wipe)
     uint8_t* pis = stage + P * tlen;
     par::for_each((P + 7) / 8, [&](size_t gi) {
       perm::Seed sd[8];
@@ -1126,6 +1169,13 @@ int bpp_perm_prove(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, uint64_t seed, c
   return BPP_OK;
 }
 
+namespace {
+std::vector<Proof>& proofs_tl() {
+  static thread_local std::vector<Proof> Ps;
+  return Ps;
+}
+}  // namespace
+
 static int prove_batch_api(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, const std::vector<perm::Seed>& seeds,
                            const uint8_t* label, size_t llen, uint8_t* proofs_out, uint8_t* V_out) {
   const size_t count = seeds.size();
@@ -1137,8 +1187,7 @@ static int prove_batch_api(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, const st
   }
   BPP_HIP(hipSetDevice(ctx->device));
   const size_t pl = perm::proof_len(k);
-  static thread_local std::vector<Proof> Ps_tl;  // reused batch after batch (ProverState note)
-  std::vector<Proof>& Ps = Ps_tl;                // (the workers below must see this thread's)
+  std::vector<Proof>& Ps = proofs_tl();  // reused batch after batch (ProverState note; the workers see this thread's)
   Ps.resize(count);
   // Sub-batches in flight on S streams (child contexts), one host thread
   // each: while one sub-batch waits on transcripts / challenges on the host,
@@ -1219,9 +1268,11 @@ int bpp_perm_prove_batch_entropy(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, si
   }
   std::vector<perm::Seed> sd(count);
   for (size_t i = 0; i < count; ++i) sd[i] = perm::Seed::bytes32(seeds32 + 32 * i);
-  const int rc = prove_batch_api(ctx, G, k, sd, label, llen, proofs_out, V_out);
+  int rc = prove_batch_api(ctx, G, k, sd, label, llen, proofs_out, V_out);
   if (!ent.empty()) memset(ent.data(), 0, ent.size());
-  return rc;
+  for (perm::Seed& x : sd) memset(x.b, 0, sizeof x.b);
+  const int wrc = prove_wipe(ctx);
+  return rc ? rc : wrc;
 }
 
 int bpp_perm_verify(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, const uint8_t* label, size_t llen,

@@ -251,12 +251,11 @@ int bpp_perm_prove_batch(bpp_ctx* ctx, const bpp_gens* g, uint32_t k, size_t cou
  * NULL to draw them from the OS CSPRNG (getrandom), as the reference draws
  * from thread_rng (circuit_lib.rs:175, weights.rs:39,59).  The draws are
  * those above with the 32-byte seed32 in place of the 8-byte seed.
- * Secret lifetime: the seeds' draws, the witness and the blinding scalars
- * stay in this process's memory after the call -- in the context's device
- * workspaces and pinned staging arena and in the calling thread's reused
- * prover states -- until they are overwritten by the next batch or freed by
- * bpp_ctx_destroy / thread exit (the library does not wipe them between
- * batches; the caller's own seeds32 buffer is the caller's to wipe). */
+ * Secret lifetime: after the batch the library zeroes what it kept of it --
+ * the device workspaces holding draws, witness, blindings and the l / r
+ * vectors, the staged draw templates and pi, the T-commitment inputs, and the
+ * calling thread's reused prover states and permutations (the caller's own
+ * seeds32 buffer is the caller's to wipe). */
 int bpp_perm_prove_batch_entropy(bpp_ctx* ctx, const bpp_gens* g, uint32_t k, size_t count, const uint8_t* seeds32,
                                  const uint8_t* label, size_t llen, uint8_t* proofs_out, uint8_t* V_out);
 /* BPP_OK or BPP_ERR_VERIFY (ProofError::VerificationError). One GPU MSM. */

@@ -132,3 +132,19 @@ def test_prove_batch_entropy_seeds(gens):
     b, vb = pr.prove_batch_entropy(3)
     assert a != b and va != vb
     assert pr.verify_batch(a + b, va + vb)
+
+
+def test_entropy_batches_wipe_without_disturbing_later_batches(gens):
+    """bpp_perm_prove_batch_entropy zeroes the batch's secrets afterwards
+    (device workspaces, staged templates, the thread's prover states): the
+    same context and thread then prove a 52-card u64-seed batch byte-equal
+    to the one before, and both entropy batches verify."""
+    import bpperm
+    pr = bpperm.PermProver(gens, 52)
+    seeds = [11, 12, 13, 14, 15]
+    before, vb = pr.prove_batch(seeds)
+    e1, ve1 = pr.prove_batch_entropy(6)
+    after, va = pr.prove_batch(seeds)
+    e2, ve2 = pr.prove_batch_entropy(6)
+    assert before == after and vb == va
+    assert pr.verify_batch(e1 + e2 + after, ve1 + ve2 + va)

@@ -80,9 +80,14 @@ struct bpp_ctx {
   // before the next upload overwrites the inputs
   hipEvent_t vj_ev_in = nullptr, vj_ev_dec = nullptr;
   bool vj_dec_pending = false;
-  // bpp_msm_submit_host: the uploaded scalars of this (child) context's MSM
+  // bpp_msm_submit_host: the uploaded scalars of this (child) context's MSM,
+  // copied on the parent's upload streams (up_stream, created on first use;
+  // one per chunk of the copy) and signalled to this context's stream by
+  // up_ev
   void* up_sc = nullptr;
   size_t up_sc_bytes = 0;
+  hipStream_t up_stream[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t up_ev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 #define VJ_CHILD BPP_MSM_INFLIGHT
 
@@ -126,6 +131,8 @@ int ctx_zc_out(bpp_ctx* ctx, const char* name, size_t bytes, uint32_t** d);
 // hipMemcpyAsync measured up to ~25 ms on a 20 KB copy on the box); the host
 // buffer may be freed as soon as this returns.
 int ctx_h2d(bpp_ctx* ctx, void* d, const void* h, size_t bytes);
+// memcpy into / out of the pinned arena, split over the host pool above 512 KB
+void ctx_stage_copy(void* dst, const void* src, size_t bytes);
 // Two host buffers copied back to back into d (one staging copy).
 int ctx_h2d2(bpp_ctx* ctx, void* d, const void* h0, size_t n0, const void* h1, size_t n1);
 // Two-step form for data produced straight into the pinned arena:

@@ -10,7 +10,7 @@
 
 // memcpy to / from the pinned arena, split over the host pool above 512 KB
 // (a 2.6 MB scalar upload is ~0.25 ms on one core of the box)
-static void stage_copy(void* dst, const void* src, size_t bytes) {
+void ctx_stage_copy(void* dst, const void* src, size_t bytes) {
   const size_t chunk = 128u << 10;
   if (bytes < (512u << 10)) {
     memcpy(dst, src, bytes);
@@ -137,7 +137,7 @@ int ctx_h2d(bpp_ctx* ctx, void* d, const void* h, size_t bytes) {
   if (!bytes) return BPP_OK;
   uint8_t* p = nullptr;
   BPP_TRY(stage_take(ctx, bytes, &p));
-  stage_copy(p, h, bytes);
+  ctx_stage_copy(p, h, bytes);
   BPP_HIP(hipMemcpyAsync(d, p, bytes, hipMemcpyHostToDevice, ctx->stream));
   return BPP_OK;
 }
@@ -146,8 +146,8 @@ int ctx_h2d2(bpp_ctx* ctx, void* d, const void* h0, size_t n0, const void* h1, s
   if (!n0 && !n1) return BPP_OK;
   uint8_t* p = nullptr;
   BPP_TRY(stage_take(ctx, n0 + n1, &p));
-  stage_copy(p, h0, n0);
-  stage_copy(p + n0, h1, n1);
+  ctx_stage_copy(p, h0, n0);
+  ctx_stage_copy(p + n0, h1, n1);
   BPP_HIP(hipMemcpyAsync(d, p, n0 + n1, hipMemcpyHostToDevice, ctx->stream));
   return BPP_OK;
 }
@@ -167,7 +167,7 @@ int ctx_d2h(bpp_ctx* ctx, void* h, const void* d, size_t bytes) {
   BPP_TRY(stage_take(ctx, bytes, &p));
   BPP_HIP(hipMemcpyAsync(p, d, bytes, hipMemcpyDeviceToHost, ctx->stream));
   BPP_TRY(ctx_sync(ctx));
-  stage_copy(h, p, bytes);
+  ctx_stage_copy(h, p, bytes);
   return BPP_OK;
 }
 
@@ -297,6 +297,13 @@ void bpp_ctx_destroy(bpp_ctx* ctx) {
   for (auto e : ctx->ev_pool) hipEventDestroy(e);
   if (ctx->sync_ev) hipEventDestroy(ctx->sync_ev);
   if (ctx->up_sc) hipFree(ctx->up_sc);
+  for (auto e : ctx->up_ev)
+    if (e) hipEventDestroy(e);
+  for (auto s : ctx->up_stream)
+    if (s) {
+      hipStreamSynchronize(s);
+      hipStreamDestroy(s);
+    }
   if (ctx->vj_ev_in) hipEventDestroy(ctx->vj_ev_in);
   if (ctx->vj_ev_dec) hipEventDestroy(ctx->vj_ev_dec);
   for (auto& sl : ctx->msm_slot)

@@ -23,6 +23,19 @@ struct DtGeom {
 // a fourth spilled 124 B per lane and measured 104-120 K vs 147-151 K
 // proofs/s at 12 batches in flight)
 
+// Term groups per block (TG, lanes = TG * W): at most DT_NT_MAX / W, fewer
+// for short MSMs; BPP_DT_TG_MAX caps it (an A/B switch: fewer lanes per MSM
+// means a shallower block tree and less issue per MSM, but fewer waves).
+static inline uint32_t dt_term_groups(uint32_t W, double terms_per_msm) {
+  uint32_t TG = DT_NT_MAX / W;
+  if (const char* e = getenv("BPP_DT_TG_MAX")) {
+    const int v = atoi(e);
+    if (v >= 1 && (uint32_t)v < TG) TG = (uint32_t)v;
+  }
+  while (TG > 1 && terms_per_msm < 2.0 * TG) TG >>= 1;
+  return TG;
+}
+
 FE_INLINE uint32_t sel8(const uint32_t v[8], uint32_t i) {  // v[i], 0 for i >= 8 (no scratch)
   uint32_t r = 0;
   _Pragma("unroll") for (uint32_t k = 0; k < 8; ++k) r = i == k ? v[k] : r;

@@ -441,16 +441,53 @@ static int msm_submit(bpp_ctx* ctx, const void* d_scalars, const void* h_scalars
       hipPointerAttribute_t at;
       const bool pinned = hipPointerGetAttributes(&at, h_scalars) == hipSuccess && at.type == hipMemoryTypeHost;
       (void)hipGetLastError();  // (a pageable pointer leaves an error code behind)
-      // (measured at 2^20, 3 in flight, tools/host_msm_probe.py: resident
-      // scalars 0.875 ms per MSM; pinned + this DMA 1.226; pageable staged
-      // through the slot's arena 1.133; pinned read in place by the digit
-      // kernel (zero copy) 1.397 -- its PCIe-bound blocks held CUs the other
-      // MSMs' accumulations needed)
-      if (pinned) {
-        ProfScope ps(ch, "msm_upload");
-        if (hipMemcpyAsync(d, h_scalars, n * 32, hipMemcpyHostToDevice, ch->stream) != hipSuccess) rc = BPP_ERR_DEVICE;
-      } else {
-        rc = ctx_h2d(ch, d, h_scalars, n * 32);
+      // (pinned read in place by the digit kernel, zero copy, measured 1.397
+      // vs 0.875 ms per resident MSM: its PCIe-bound blocks held CUs the
+      // other MSMs' accumulations needed)
+      // The copy runs on the slot's own stream.  BPP_MSM_UP_STREAMS=k (1-4)
+      // splits it into k chunks on k upload streams of the parent that the
+      // slot's stream waits for by event (an A/B switch): the standalone
+      // probe (tools/host_msm_probe.py, 2^20 pinned, 3 in flight, three
+      // interleaved passes) measured 1.53-1.77 ms per MSM on the slot's
+      // stream, 1.11-1.24 with one upload stream and 1.10-1.12 with two,
+      // against 0.99 resident -- but inside bench.py (three interleaved full
+      // runs) two upload streams measured 1.35-1.82x resident vs 1.21-1.61x,
+      // the pageable leg 1.25-1.55x vs 1.16-1.22x, and the later prover leg
+      // 270-273 K vs 282-287 K proofs/s, so the default stays 0.  The
+      // pageable path is bound by its staging memcpy (1.6-1.9 ms of host time
+      // per 32 MB).  The slot's previous MSM has been collected, so nothing
+      // still reads up_sc.
+      const char* se = getenv("BPP_MSM_UP_STREAMS");
+      const int ns = se ? std::max(0, std::min(4, atoi(se))) : 0;
+      const size_t bytes = n * 32;
+      uint8_t* src = (uint8_t*)h_scalars;
+      if (!pinned) {  // staged through the slot's arena, recycled only by a
+                      // sync of the slot's stream -- which waits for the copies
+        uint8_t* p = nullptr;
+        rc = ctx_h2d_stage(ch, bytes, &p);
+        if (!rc) {
+          ctx_stage_copy(p, h_scalars, bytes);
+          src = p;
+        }
+      }
+      if (!rc && ns == 0) {
+        if (hipMemcpyAsync(d, src, bytes, hipMemcpyHostToDevice, ch->stream) != hipSuccess) rc = BPP_ERR_DEVICE;
+      } else if (!rc) {
+        const size_t part = ((bytes + ns - 1) / ns + 255) & ~(size_t)255;
+        for (int k = 0; k < ns && !rc; ++k) {
+          const size_t o = (size_t)k * part;
+          if (o >= bytes) break;
+          if (!ctx->up_stream[k]) BPP_HIP(hipStreamCreateWithFlags(&ctx->up_stream[k], hipStreamNonBlocking));
+          if (!ch->up_ev[k]) BPP_HIP(hipEventCreateWithFlags(&ch->up_ev[k], hipEventDisableTiming));
+          BPP_HIP(hipStreamWaitEvent(ctx->up_stream[k], sl.done, 0));  // (inputs written on ctx's stream)
+          if (hipMemcpyAsync((uint8_t*)d + o, src + o, std::min(part, bytes - o), hipMemcpyHostToDevice,
+                             ctx->up_stream[k]) != hipSuccess) {
+            rc = BPP_ERR_DEVICE;
+            break;
+          }
+          BPP_HIP(hipEventRecord(ch->up_ev[k], ctx->up_stream[k]));
+          BPP_HIP(hipStreamWaitEvent(ch->stream, ch->up_ev[k], 0));
+        }
       }
     }
     if (rc) {
@@ -729,8 +766,7 @@ static int msm_multi_dt_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t
   // a shallower tree); ~512 lanes measured slower at 8 proof batches in
   // flight
   const double t_avg = (double)T / (double)M;
-  uint32_t TG = DT_NT_MAX / dg.W;
-  while (TG > 1 && t_avg < 2.0 * TG) TG >>= 1;
+  const uint32_t TG = dt_term_groups(dg.W, t_avg);
   const uint32_t nt = TG * dg.W;
   ctx_work(ctx, "msm_terms", T);
   ctx_work(ctx, "madds", (uint64_t)T * dg.W);

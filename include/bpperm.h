@@ -149,10 +149,10 @@ int bpp_msm_collect(bpp_ctx* ctx, uint64_t ticket, uint8_t out[32], uint8_t part
 /* The same with host scalars (the shape of the reference's
  * vartime_multiscalar_mul(scalars, points), circuit_lib.rs:187): the n x 32
  * bytes are copied to the device on the MSM's own stream, so in a stream of
- * submits the upload of one MSM overlaps the others' kernels.  From pinned
- * memory (bpp_host_alloc) the copy is a direct DMA; pageable memory goes
- * through a staging copy first.  h_scalars must stay valid and unchanged
- * until collect. */
+ * submits the upload of one MSM overlaps the others' kernels.  From pinned memory (bpp_host_alloc)
+ * the copy is a direct DMA; pageable memory goes through a staging copy
+ * first (host memcpy inside the call).  h_scalars must stay valid and
+ * unchanged until collect. */
 int bpp_msm_submit_host(bpp_ctx* ctx, const void* h_scalars, const bpp_points* tbl, size_t n, uint32_t w_begin,
                         uint32_t w_end, uint64_t* ticket);
 /* Pinned (page-locked) host memory for bpp_msm_submit_host inputs. */

@@ -1150,7 +1150,7 @@ int verify_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const 
 
 extern "C" {
 
-size_t bpp_perm_proof_len(uint32_t k) { return k >= 2 ? perm::proof_len(k) : 0; }
+size_t bpp_perm_proof_len(uint32_t k) { return k >= 2 && k <= (1u << 20) ? perm::proof_len(k) : 0; }
 
 int bpp_perm_prove(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, uint64_t seed, const uint8_t* label, size_t llen,
                    uint8_t* proof_out, uint8_t* V_out, uint32_t* perm_out) {
@@ -1277,7 +1277,7 @@ int bpp_perm_prove_batch_entropy(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, si
 
 int bpp_perm_verify(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, const uint8_t* label, size_t llen,
                     const uint8_t* proof, size_t proof_len, const uint8_t* V) {
-  if (!ctx || !G || !proof || !V || (!label && llen) || k < 2) return BPP_ERR_ARG;
+  if (!ctx || !G || !proof || !V || (!label && llen) || k < 2 || k > (1u << 20)) return BPP_ERR_ARG;
   if (proof_len != perm::proof_len(k)) return BPP_ERR_VERIFY;
   BPP_HIP(hipSetDevice(ctx->device));
   const perm::Circuit C = perm::build(k);
@@ -1286,7 +1286,7 @@ int bpp_perm_verify(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, const uint8_t* 
 
 int bpp_perm_verify_batch(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, size_t count, const uint8_t* label, size_t llen,
                           const uint8_t* proofs, const uint8_t* V) {
-  if (!ctx || !G || ((!proofs || !V) && count) || (!label && llen) || k < 2) return BPP_ERR_ARG;
+  if (!ctx || !G || ((!proofs || !V) && count) || (!label && llen) || k < 2 || k > (1u << 20)) return BPP_ERR_ARG;
   if (!count) return BPP_OK;
   BPP_HIP(hipSetDevice(ctx->device));
   const perm::Circuit C = perm::build(k);

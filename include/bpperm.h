@@ -230,7 +230,8 @@ int bpp_ipa_verify(bpp_ctx* ctx, const bpp_gens* g, bpp_transcript* tr, size_t n
  * is a permutation of the first (ACProof::ArithmeticCircuitProof,
  * circuit_lib.rs:139-585 over the circuit of weights.rs:26-204), in sound
  * form (SURVEY.md §2.2 defects fixed; DESIGN.md "Protocol").  Gates are
- * padded to n_p = next_pow2(2k) <= bpp_gens_len(g).
+ * padded to n_p = next_pow2(2k) <= bpp_gens_len(g).  Every entry point takes
+ * 2 <= k <= 2^20 (BPP_ERR_ARG otherwise).
  *
  * Proof bytes (bpp_perm_proof_len(k)): A_I A_O S T1 T3 T4 T5 T6 | tau_x mu
  * t_hat | L_0 R_0 .. L_{lg-1} R_{lg-1} | a b.  The 2k+1 Pedersen

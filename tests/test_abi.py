@@ -41,3 +41,36 @@ def test_no_cpu_fallback_without_library(tmp_path):
     from bpperm import _lib
     with pytest.raises(RuntimeError):
         _lib.load(tmp_path / "missing.so")
+
+
+def test_argument_checks_without_device():
+    """Entry points reject bad arguments before any device call: a null
+    context, k outside [2, 2^20], a null job (BPP_ERR_ARG = 1)."""
+    from bpperm import _lib
+    lib = ctypes.CDLL(str(_lib.LIB_PATH))
+    ARG = 1
+    lib.bpp_perm_proof_len.restype = ctypes.c_size_t
+    assert lib.bpp_perm_proof_len(ctypes.c_uint32(1)) == 0
+    assert lib.bpp_perm_proof_len(ctypes.c_uint32(0x7FFFFFFF)) == 0  # (2k would wrap)
+    assert lib.bpp_perm_proof_len(ctypes.c_uint32((1 << 20) + 1)) == 0
+    assert lib.bpp_perm_proof_len(ctypes.c_uint32(52)) > 0
+    job = ctypes.c_void_p()
+    buf = ctypes.create_string_buffer(64)
+    for k in (0, 1, (1 << 20) + 1, 0xFFFFFFFF):
+        assert lib.bpp_perm_verify_begin(ctypes.c_uint32(k), ctypes.c_size_t(0), None, ctypes.c_size_t(0), None,
+                                         None, None, ctypes.byref(job)) == ARG
+    for k in (2, 52):  # a null context is refused before the device is touched
+        assert lib.bpp_perm_verify(None, None, ctypes.c_uint32(k), None, ctypes.c_size_t(0), buf,
+                                   ctypes.c_size_t(64), buf) == ARG
+        assert lib.bpp_perm_verify_batch(None, None, ctypes.c_uint32(k), ctypes.c_size_t(1), None,
+                                         ctypes.c_size_t(0), buf, buf) == ARG
+        assert lib.bpp_perm_prove(None, None, ctypes.c_uint32(k), ctypes.c_uint64(1), None, ctypes.c_size_t(0),
+                                  buf, buf, None) == ARG
+    assert lib.bpp_perm_verify_terms(None, ctypes.byref(ctypes.c_size_t())) == ARG
+    # the empty host job: zero proofs, replayed nowhere
+    assert lib.bpp_perm_verify_begin(ctypes.c_uint32(52), ctypes.c_size_t(0), None, ctypes.c_size_t(0), None, None,
+                                     None, ctypes.byref(job)) == 0
+    terms = ctypes.c_size_t()
+    assert lib.bpp_perm_verify_terms(job, ctypes.byref(terms)) == 0
+    assert terms.value == 2 * 128 + 2
+    lib.bpp_perm_verify_end(job)

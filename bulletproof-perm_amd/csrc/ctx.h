@@ -3,7 +3,9 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <exception>
 #include <map>
+#include <new>
 #include <set>
 #include <string>
 #include <vector>
@@ -91,6 +93,14 @@ struct bpp_ctx {
 };
 #define VJ_CHILD BPP_MSM_INFLIGHT
 
+inline void bpp_guard_note(bpp_ctx* ctx, const char* what) noexcept {
+  if (!ctx) return;
+  try {
+    ctx->err = what;
+  } catch (...) {
+  }
+}
+
 struct bpp_points {
   bpp_ctx* ctx = nullptr;
   uint32_t* d = nullptr;  // n x 24 words (affine Niels)
@@ -111,6 +121,26 @@ struct bpp_points {
     int _rc = (expr);            \
     if (_rc != BPP_OK) return _rc; \
   } while (0)
+
+// The C-ABI boundary: every int-returning bpp_* entry point runs its body
+// through bpp_guard, so no C++ exception (std::bad_alloc from a host vector
+// sized by the caller's arguments, a std::length_error, ...) unwinds into a
+// C, Rust or Python caller; it becomes BPP_ERR_NOMEM / BPP_ERR_DEVICE with
+// the text in bpp_ctx_last_error when the entry point has a context.
+template <class F>
+inline int bpp_guard(bpp_ctx* ctx, F&& body) noexcept {
+  try {
+    return body();
+  } catch (const std::bad_alloc&) {
+    bpp_guard_note(ctx, "out of host memory");
+    return BPP_ERR_NOMEM;
+  } catch (const std::exception& e) {
+    bpp_guard_note(ctx, e.what());
+  } catch (...) {
+    bpp_guard_note(ctx, "unexpected C++ exception");
+  }
+  return BPP_ERR_DEVICE;
+}
 
 // Scratch buffer that grows on demand (never shrinks until ctx destroy).
 int ctx_ws(bpp_ctx* ctx, const char* name, size_t bytes, void** out);

@@ -253,30 +253,34 @@ extern "C" {
 // of the whole host process, so it is opt-in (bench.py asks for it); loading
 // the library changes nothing.
 int bpp_host_tuning(uint32_t flags) {
-  if (flags & ~(uint32_t)BPP_TUNE_MALLOC) return BPP_ERR_ARG;
-  if (flags & BPP_TUNE_MALLOC) {
-    mallopt(M_MMAP_THRESHOLD, 64 << 20);
-    mallopt(M_TRIM_THRESHOLD, 1 << 30);
-  }
-  return BPP_OK;
+  return bpp_guard(nullptr, [&]() -> int {
+    if (flags & ~(uint32_t)BPP_TUNE_MALLOC) return BPP_ERR_ARG;
+    if (flags & BPP_TUNE_MALLOC) {
+      mallopt(M_MMAP_THRESHOLD, 64 << 20);
+      mallopt(M_TRIM_THRESHOLD, 1 << 30);
+    }
+    return BPP_OK;
+  });
 }
 
 uint32_t bpp_host_threads(void) { return par::threads(); }
 
 int bpp_ctx_create(int device, bpp_ctx** out) {
-  if (!out) return BPP_ERR_ARG;
-  *out = nullptr;
-  int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return BPP_ERR_DEVICE;
-  if (hipSetDevice(device) != hipSuccess) return BPP_ERR_DEVICE;
-  bpp_ctx* ctx = new bpp_ctx();
-  ctx->device = device;
-  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
-    delete ctx;
-    return BPP_ERR_DEVICE;
-  }
-  *out = ctx;
-  return BPP_OK;
+  return bpp_guard(nullptr, [&]() -> int {
+    if (!out) return BPP_ERR_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return BPP_ERR_DEVICE;
+    if (hipSetDevice(device) != hipSuccess) return BPP_ERR_DEVICE;
+    bpp_ctx* ctx = new bpp_ctx();
+    ctx->device = device;
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+      delete ctx;
+      return BPP_ERR_DEVICE;
+    }
+    *out = ctx;
+    return BPP_OK;
+  });
 }
 
 void bpp_ctx_destroy(bpp_ctx* ctx) {
@@ -317,19 +321,23 @@ const char* bpp_ctx_last_error(const bpp_ctx* ctx) { return ctx ? ctx->err.c_str
 void* bpp_ctx_stream(bpp_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 
 int bpp_ctx_profile(bpp_ctx* ctx, int enable) {
-  if (!ctx) return BPP_ERR_ARG;
-  ctx->prof = enable != 0;
-  for (bpp_ctx* c : ctx->children) bpp_ctx_profile(c, enable);
-  return BPP_OK;
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx) return BPP_ERR_ARG;
+    ctx->prof = enable != 0;
+    for (bpp_ctx* c : ctx->children) bpp_ctx_profile(c, enable);
+    return BPP_OK;
+  });
 }
 
 int bpp_ctx_profile_get(bpp_ctx* ctx, const char* stage, double* ms, uint64_t* launches) {
-  if (!ctx || !stage) return BPP_ERR_ARG;
-  prof_resolve(ctx);
-  auto it = ctx->prof_acc.find(stage);
-  if (ms) *ms = it == ctx->prof_acc.end() ? 0.0 : it->second.first;
-  if (launches) *launches = it == ctx->prof_acc.end() ? 0 : it->second.second;
-  return BPP_OK;
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !stage) return BPP_ERR_ARG;
+    prof_resolve(ctx);
+    auto it = ctx->prof_acc.find(stage);
+    if (ms) *ms = it == ctx->prof_acc.end() ? 0.0 : it->second.first;
+    if (launches) *launches = it == ctx->prof_acc.end() ? 0 : it->second.second;
+    return BPP_OK;
+  });
 }
 
 static void work_resolve(bpp_ctx* ctx) {
@@ -341,11 +349,13 @@ static void work_resolve(bpp_ctx* ctx) {
 }
 
 int bpp_ctx_work_get(bpp_ctx* ctx, const char* name, uint64_t* value) {
-  if (!ctx || !name || !value) return BPP_ERR_ARG;
-  work_resolve(ctx);
-  auto it = ctx->work.find(name);
-  *value = it == ctx->work.end() ? 0 : it->second;
-  return BPP_OK;
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !name || !value) return BPP_ERR_ARG;
+    work_resolve(ctx);
+    auto it = ctx->work.find(name);
+    *value = it == ctx->work.end() ? 0 : it->second;
+    return BPP_OK;
+  });
 }
 
 void bpp_ctx_work_reset(bpp_ctx* ctx) {
@@ -361,36 +371,46 @@ void bpp_ctx_profile_reset(bpp_ctx* ctx) {
 }
 
 int bpp_dev_alloc(bpp_ctx* ctx, size_t bytes, void** dptr) {
-  if (!ctx || !dptr) return BPP_ERR_ARG;
-  BPP_HIP(hipSetDevice(ctx->device));
-  BPP_HIP(hipMalloc(dptr, bytes ? bytes : 1));
-  return BPP_OK;
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !dptr) return BPP_ERR_ARG;
+    BPP_HIP(hipSetDevice(ctx->device));
+    BPP_HIP(hipMalloc(dptr, bytes ? bytes : 1));
+    return BPP_OK;
+  });
 }
 
 int bpp_dev_free(bpp_ctx* ctx, void* dptr) {
-  if (!ctx) return BPP_ERR_ARG;
-  BPP_HIP(hipFree(dptr));
-  return BPP_OK;
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx) return BPP_ERR_ARG;
+    BPP_HIP(hipFree(dptr));
+    return BPP_OK;
+  });
 }
 
 int bpp_memcpy_htod(bpp_ctx* ctx, void* dst, const void* src, size_t bytes) {
-  if (!ctx) return BPP_ERR_ARG;
-  BPP_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
-  BPP_HIP(hipStreamSynchronize(ctx->stream));
-  return BPP_OK;
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx) return BPP_ERR_ARG;
+    BPP_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    BPP_HIP(hipStreamSynchronize(ctx->stream));
+    return BPP_OK;
+  });
 }
 
 int bpp_memcpy_dtoh(bpp_ctx* ctx, void* dst, const void* src, size_t bytes) {
-  if (!ctx) return BPP_ERR_ARG;
-  BPP_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
-  BPP_HIP(hipStreamSynchronize(ctx->stream));
-  return BPP_OK;
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx) return BPP_ERR_ARG;
+    BPP_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    BPP_HIP(hipStreamSynchronize(ctx->stream));
+    return BPP_OK;
+  });
 }
 
 int bpp_synchronize(bpp_ctx* ctx) {
-  if (!ctx) return BPP_ERR_ARG;
-  BPP_HIP(hipStreamSynchronize(ctx->stream));
-  return BPP_OK;
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx) return BPP_ERR_ARG;
+    BPP_HIP(hipStreamSynchronize(ctx->stream));
+    return BPP_OK;
+  });
 }
 
 }  // extern "C"

@@ -306,96 +306,102 @@ void gens_chain_bytes(const char* label, uint32_t party, size_t n, uint8_t* out6
 extern "C" {
 
 int bpp_gens_create(bpp_ctx* ctx, size_t n, bpp_gens** out) {
-  if (!ctx || !out || n == 0 || n >= (1u << 28)) return BPP_ERR_ARG;
-  *out = nullptr;
-  BPP_HIP(hipSetDevice(ctx->device));
-  bpp_gens* g = nullptr;
-  BPP_TRY(gens_alloc(ctx, n, &g));
-  // uniform bytes: G chain, H chain, then B_blinding's SHA3-512(B) (as 64 B)
-  std::vector<uint8_t> uni((2 * n + 1) * 64);
-  gens_chain_bytes("G", 0, n, uni.data());
-  gens_chain_bytes("H", 0, n, uni.data() + 64 * n);
-  static const uint8_t B_ENC[32] = {0xe2, 0xf2, 0xae, 0x0a, 0x6a, 0xbc, 0x4e, 0x71, 0xa8, 0x84, 0xa9,
-                                    0x61, 0xc5, 0x00, 0x51, 0x5f, 0x58, 0xe3, 0x0b, 0x6a, 0xa5, 0x82,
-                                    0xdd, 0x8d, 0xb6, 0xa6, 0x59, 0x45, 0xe0, 0x8d, 0x2d, 0x76};
-  merlin::sha3_512(B_ENC, 32, uni.data() + 64 * 2 * n);
-  void *d_uni, *d_b, *d_bad;
-  int rc = ctx_ws(ctx, "gens_uni", uni.size(), &d_uni);
-  if (!rc) rc = ctx_ws(ctx, "gens_b", 32, &d_b);
-  if (!rc) rc = ctx_ws(ctx, "gens_bad", 8, &d_bad);
-  if (rc) {
-    bpp_gens_destroy(g);
-    return rc;
-  }
-  unsigned long long init = ~0ull;
-  BPP_HIP(hipMemcpyAsync(d_uni, uni.data(), uni.size(), hipMemcpyHostToDevice, ctx->stream));
-  BPP_HIP(hipMemcpyAsync(d_b, B_ENC, 32, hipMemcpyHostToDevice, ctx->stream));
-  BPP_HIP(hipMemcpyAsync(d_bad, &init, 8, hipMemcpyHostToDevice, ctx->stream));
-  hipLaunchKernelGGL(k_from_uniform, dim3(grid_for(2 * n, 64)), dim3(64), 0, ctx->stream, (const uint32_t*)d_uni, 2 * n,
-                     g->d_tbl);
-  hipLaunchKernelGGL(k_from_uniform, dim3(1), dim3(64), 0, ctx->stream, (const uint32_t*)d_uni + 16 * 2 * n, (size_t)1,
-                     g->d_tbl + (2 * n + 1) * MSM_NIELS_WORDS);
-  hipLaunchKernelGGL(k_decompress, dim3(1), dim3(64), 0, ctx->stream, (const uint32_t*)d_b, (size_t)1,
-                     g->d_tbl + 2 * n * MSM_NIELS_WORDS, (unsigned long long*)d_bad);
-  rc = ctx_check_launch(ctx, "gens kernels");
-  if (!rc) rc = gens_finish(ctx, g);
-  if (rc) {
-    bpp_gens_destroy(g);
-    return rc;
-  }
-  *out = g;
-  return BPP_OK;
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !out || n == 0 || n >= (1u << 28)) return BPP_ERR_ARG;
+    *out = nullptr;
+    BPP_HIP(hipSetDevice(ctx->device));
+    bpp_gens* g = nullptr;
+    BPP_TRY(gens_alloc(ctx, n, &g));
+    // uniform bytes: G chain, H chain, then B_blinding's SHA3-512(B) (as 64 B)
+    std::vector<uint8_t> uni((2 * n + 1) * 64);
+    gens_chain_bytes("G", 0, n, uni.data());
+    gens_chain_bytes("H", 0, n, uni.data() + 64 * n);
+    static const uint8_t B_ENC[32] = {0xe2, 0xf2, 0xae, 0x0a, 0x6a, 0xbc, 0x4e, 0x71, 0xa8, 0x84, 0xa9,
+                                      0x61, 0xc5, 0x00, 0x51, 0x5f, 0x58, 0xe3, 0x0b, 0x6a, 0xa5, 0x82,
+                                      0xdd, 0x8d, 0xb6, 0xa6, 0x59, 0x45, 0xe0, 0x8d, 0x2d, 0x76};
+    merlin::sha3_512(B_ENC, 32, uni.data() + 64 * 2 * n);
+    void *d_uni, *d_b, *d_bad;
+    int rc = ctx_ws(ctx, "gens_uni", uni.size(), &d_uni);
+    if (!rc) rc = ctx_ws(ctx, "gens_b", 32, &d_b);
+    if (!rc) rc = ctx_ws(ctx, "gens_bad", 8, &d_bad);
+    if (rc) {
+      bpp_gens_destroy(g);
+      return rc;
+    }
+    unsigned long long init = ~0ull;
+    BPP_HIP(hipMemcpyAsync(d_uni, uni.data(), uni.size(), hipMemcpyHostToDevice, ctx->stream));
+    BPP_HIP(hipMemcpyAsync(d_b, B_ENC, 32, hipMemcpyHostToDevice, ctx->stream));
+    BPP_HIP(hipMemcpyAsync(d_bad, &init, 8, hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_from_uniform, dim3(grid_for(2 * n, 64)), dim3(64), 0, ctx->stream, (const uint32_t*)d_uni, 2 * n,
+                       g->d_tbl);
+    hipLaunchKernelGGL(k_from_uniform, dim3(1), dim3(64), 0, ctx->stream, (const uint32_t*)d_uni + 16 * 2 * n, (size_t)1,
+                       g->d_tbl + (2 * n + 1) * MSM_NIELS_WORDS);
+    hipLaunchKernelGGL(k_decompress, dim3(1), dim3(64), 0, ctx->stream, (const uint32_t*)d_b, (size_t)1,
+                       g->d_tbl + 2 * n * MSM_NIELS_WORDS, (unsigned long long*)d_bad);
+    rc = ctx_check_launch(ctx, "gens kernels");
+    if (!rc) rc = gens_finish(ctx, g);
+    if (rc) {
+      bpp_gens_destroy(g);
+      return rc;
+    }
+    *out = g;
+    return BPP_OK;
+  });
 }
 
 int bpp_gens_from_points(bpp_ctx* ctx, const uint8_t* G_enc, const uint8_t* H_enc, size_t n, const uint8_t B_enc[32],
                          const uint8_t Bb_enc[32], bpp_gens** out) {
-  if (!ctx || !out || !G_enc || !H_enc || !B_enc || !Bb_enc || n == 0) return BPP_ERR_ARG;
-  *out = nullptr;
-  BPP_HIP(hipSetDevice(ctx->device));
-  bpp_gens* g = nullptr;
-  BPP_TRY(gens_alloc(ctx, n, &g));
-  std::vector<uint8_t> enc((2 * n + 2) * 32);
-  memcpy(enc.data(), G_enc, 32 * n);
-  memcpy(enc.data() + 32 * n, H_enc, 32 * n);
-  memcpy(enc.data() + 64 * n, B_enc, 32);
-  memcpy(enc.data() + 64 * n + 32, Bb_enc, 32);
-  void *d_enc, *d_bad;
-  int rc = ctx_ws(ctx, "gens_enc", enc.size(), &d_enc);
-  if (!rc) rc = ctx_ws(ctx, "gens_bad", 8, &d_bad);
-  if (rc) {
-    bpp_gens_destroy(g);
-    return rc;
-  }
-  unsigned long long bad = ~0ull;
-  BPP_HIP(hipMemcpyAsync(d_enc, enc.data(), enc.size(), hipMemcpyHostToDevice, ctx->stream));
-  BPP_HIP(hipMemcpyAsync(d_bad, &bad, 8, hipMemcpyHostToDevice, ctx->stream));
-  hipLaunchKernelGGL(k_decompress, dim3(grid_for(2 * n + 2, 64)), dim3(64), 0, ctx->stream, (const uint32_t*)d_enc,
-                     2 * n + 2, g->d_tbl, (unsigned long long*)d_bad);
-  BPP_HIP(hipMemcpyAsync(&bad, d_bad, 8, hipMemcpyDeviceToHost, ctx->stream));
-  BPP_HIP(hipStreamSynchronize(ctx->stream));
-  if (bad != ~0ull) {
-    ctx->err = "invalid generator encoding at index " + std::to_string(bad);
-    bpp_gens_destroy(g);
-    return BPP_ERR_DECOMPRESS;
-  }
-  rc = gens_finish(ctx, g);
-  if (rc) {
-    bpp_gens_destroy(g);
-    return rc;
-  }
-  *out = g;
-  return BPP_OK;
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !out || !G_enc || !H_enc || !B_enc || !Bb_enc || n == 0) return BPP_ERR_ARG;
+    *out = nullptr;
+    BPP_HIP(hipSetDevice(ctx->device));
+    bpp_gens* g = nullptr;
+    BPP_TRY(gens_alloc(ctx, n, &g));
+    std::vector<uint8_t> enc((2 * n + 2) * 32);
+    memcpy(enc.data(), G_enc, 32 * n);
+    memcpy(enc.data() + 32 * n, H_enc, 32 * n);
+    memcpy(enc.data() + 64 * n, B_enc, 32);
+    memcpy(enc.data() + 64 * n + 32, Bb_enc, 32);
+    void *d_enc, *d_bad;
+    int rc = ctx_ws(ctx, "gens_enc", enc.size(), &d_enc);
+    if (!rc) rc = ctx_ws(ctx, "gens_bad", 8, &d_bad);
+    if (rc) {
+      bpp_gens_destroy(g);
+      return rc;
+    }
+    unsigned long long bad = ~0ull;
+    BPP_HIP(hipMemcpyAsync(d_enc, enc.data(), enc.size(), hipMemcpyHostToDevice, ctx->stream));
+    BPP_HIP(hipMemcpyAsync(d_bad, &bad, 8, hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_decompress, dim3(grid_for(2 * n + 2, 64)), dim3(64), 0, ctx->stream, (const uint32_t*)d_enc,
+                       2 * n + 2, g->d_tbl, (unsigned long long*)d_bad);
+    BPP_HIP(hipMemcpyAsync(&bad, d_bad, 8, hipMemcpyDeviceToHost, ctx->stream));
+    BPP_HIP(hipStreamSynchronize(ctx->stream));
+    if (bad != ~0ull) {
+      ctx->err = "invalid generator encoding at index " + std::to_string(bad);
+      bpp_gens_destroy(g);
+      return BPP_ERR_DECOMPRESS;
+    }
+    rc = gens_finish(ctx, g);
+    if (rc) {
+      bpp_gens_destroy(g);
+      return rc;
+    }
+    *out = g;
+    return BPP_OK;
+  });
 }
 
 size_t bpp_gens_len(const bpp_gens* g) { return g ? g->n : 0; }
 
 int bpp_gens_export(bpp_ctx* ctx, const bpp_gens* g, uint8_t* out) {
-  if (!ctx || !g || !out) return BPP_ERR_ARG;
-  bpp_points view;
-  view.ctx = ctx;
-  view.d = g->d_tbl;
-  view.n = 2 * g->n + 2;
-  return bpp_points_compress(ctx, &view, out);
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !g || !out) return BPP_ERR_ARG;
+    bpp_points view;
+    view.ctx = ctx;
+    view.d = g->d_tbl;
+    view.n = 2 * g->n + 2;
+    return bpp_points_compress(ctx, &view, out);
+  });
 }
 
 void bpp_gens_destroy(bpp_gens* g) {
@@ -413,17 +419,19 @@ void bpp_gens_destroy(bpp_gens* g) {
 
 int bpp_pedersen_commit_batch(bpp_ctx* ctx, const bpp_gens* g, const uint8_t* v, const uint8_t* gamma, size_t m,
                               uint8_t* out) {
-  if (!ctx || !g || ((!v || !gamma || !out) && m)) return BPP_ERR_ARG;
-  if (!m) return BPP_OK;
-  BPP_HIP(hipSetDevice(ctx->device));
-  uint32_t *d_v, *d_g;
-  BPP_TRY(upload_scalars(ctx, v, m, "ped_v", &d_v));
-  BPP_TRY(upload_scalars(ctx, gamma, m, "ped_g", &d_g));
-  void* d_out = nullptr;
-  BPP_TRY(ctx_ws(ctx, "ped_out", m * 32, &d_out));
-  BPP_TRY(pedersen_dev(ctx, g, d_v, d_g, m, (uint32_t*)d_out, nullptr));
-  BPP_TRY(ctx_d2h(ctx, out, d_out, m * 32));
-  return BPP_OK;
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !g || ((!v || !gamma || !out) && m)) return BPP_ERR_ARG;
+    if (!m) return BPP_OK;
+    BPP_HIP(hipSetDevice(ctx->device));
+    uint32_t *d_v, *d_g;
+    BPP_TRY(upload_scalars(ctx, v, m, "ped_v", &d_v));
+    BPP_TRY(upload_scalars(ctx, gamma, m, "ped_g", &d_g));
+    void* d_out = nullptr;
+    BPP_TRY(ctx_ws(ctx, "ped_out", m * 32, &d_out));
+    BPP_TRY(pedersen_dev(ctx, g, d_v, d_g, m, (uint32_t*)d_out, nullptr));
+    BPP_TRY(ctx_d2h(ctx, out, d_out, m * 32));
+    return BPP_OK;
+  });
 }
 
 }  // extern "C"

@@ -63,149 +63,163 @@ bpp_transcript* bpp_transcript_clone(const bpp_transcript* t) { return t ? new b
 void bpp_transcript_destroy(bpp_transcript* t) { delete t; }
 int bpp_transcript_append_message(bpp_transcript* t, const uint8_t* label, size_t llen, const uint8_t* msg,
                                   size_t mlen) {
-  if (!t || (!label && llen) || (!msg && mlen)) return BPP_ERR_ARG;
-  t->t.append_message(label, llen, msg, mlen);
-  return BPP_OK;
+  return bpp_guard(nullptr, [&]() -> int {
+    if (!t || (!label && llen) || (!msg && mlen)) return BPP_ERR_ARG;
+    t->t.append_message(label, llen, msg, mlen);
+    return BPP_OK;
+  });
 }
 int bpp_transcript_append_u64(bpp_transcript* t, const uint8_t* label, size_t llen, uint64_t x) {
-  if (!t || (!label && llen)) return BPP_ERR_ARG;
-  uint8_t b[8];
-  memcpy(b, &x, 8);
-  t->t.append_message(label, llen, b, 8);
-  return BPP_OK;
+  return bpp_guard(nullptr, [&]() -> int {
+    if (!t || (!label && llen)) return BPP_ERR_ARG;
+    uint8_t b[8];
+    memcpy(b, &x, 8);
+    t->t.append_message(label, llen, b, 8);
+    return BPP_OK;
+  });
 }
 int bpp_transcript_challenge_bytes(bpp_transcript* t, const uint8_t* label, size_t llen, uint8_t* out, size_t n) {
-  if (!t || (!label && llen) || (!out && n)) return BPP_ERR_ARG;
-  std::string lab((const char*)label, llen);
-  t->t.challenge_bytes(lab.c_str(), out, n);
-  return BPP_OK;
+  return bpp_guard(nullptr, [&]() -> int {
+    if (!t || (!label && llen) || (!out && n)) return BPP_ERR_ARG;
+    std::string lab((const char*)label, llen);
+    t->t.challenge_bytes(lab.c_str(), out, n);
+    return BPP_OK;
+  });
 }
 int bpp_transcript_challenge_scalar(bpp_transcript* t, const uint8_t* label, size_t llen, uint8_t out[32]) {
-  if (!t || (!label && llen) || !out) return BPP_ERR_ARG;
-  std::string lab((const char*)label, llen);
-  hsc::to_bytes(out, t->t.challenge_scalar(lab.c_str()));
-  return BPP_OK;
+  return bpp_guard(nullptr, [&]() -> int {
+    if (!t || (!label && llen) || !out) return BPP_ERR_ARG;
+    std::string lab((const char*)label, llen);
+    hsc::to_bytes(out, t->t.challenge_scalar(lab.c_str()));
+    return BPP_OK;
+  });
 }
 
 int bpp_vec_commit(bpp_ctx* ctx, const bpp_gens* g, const uint8_t blind[32], const uint8_t* a, const uint8_t* b,
                    size_t n, uint8_t out[32]) {
-  if (!ctx || !g || !blind || !a || !out) return BPP_ERR_ARG;
-  if (n > g->n) return BPP_ERR_LEN;
-  BPP_HIP(hipSetDevice(ctx->device));
-  const size_t T = 1 + n + (b ? n : 0);
-  std::vector<uint8_t> sc(T * 32);
-  std::vector<uint32_t> idx(T);
-  memcpy(sc.data(), blind, 32);
-  idx[0] = g->bbidx();
-  memcpy(sc.data() + 32, a, 32 * n);
-  for (size_t i = 0; i < n; ++i) idx[1 + i] = g->gidx(i);
-  if (b) {
-    memcpy(sc.data() + 32 * (1 + n), b, 32 * n);
-    for (size_t i = 0; i < n; ++i) idx[1 + n + i] = g->hidx(i);
-  }
-  uint32_t* d_s = nullptr;
-  BPP_TRY(upload_scalars(ctx, sc.data(), T, "vc_s", &d_s));
-  void* d_i = nullptr;
-  BPP_TRY(ctx_ws(ctx, "vc_i", T * 4, &d_i));
-  BPP_TRY(ctx_h2d(ctx, d_i, idx.data(), T * 4));
-  std::vector<h25519::ge> res;
-  MsmPoints pts;
-  BPP_TRY(gens_points(ctx, g, &pts));
-  BPP_TRY(msm_multi(ctx, d_s, (const uint32_t*)d_i, {0, (uint32_t)T}, pts, res));
-  h25519::encode(out, res[0]);
-  return BPP_OK;
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !g || !blind || !a || !out) return BPP_ERR_ARG;
+    if (n > g->n) return BPP_ERR_LEN;
+    BPP_HIP(hipSetDevice(ctx->device));
+    const size_t T = 1 + n + (b ? n : 0);
+    std::vector<uint8_t> sc(T * 32);
+    std::vector<uint32_t> idx(T);
+    memcpy(sc.data(), blind, 32);
+    idx[0] = g->bbidx();
+    memcpy(sc.data() + 32, a, 32 * n);
+    for (size_t i = 0; i < n; ++i) idx[1 + i] = g->gidx(i);
+    if (b) {
+      memcpy(sc.data() + 32 * (1 + n), b, 32 * n);
+      for (size_t i = 0; i < n; ++i) idx[1 + n + i] = g->hidx(i);
+    }
+    uint32_t* d_s = nullptr;
+    BPP_TRY(upload_scalars(ctx, sc.data(), T, "vc_s", &d_s));
+    void* d_i = nullptr;
+    BPP_TRY(ctx_ws(ctx, "vc_i", T * 4, &d_i));
+    BPP_TRY(ctx_h2d(ctx, d_i, idx.data(), T * 4));
+    std::vector<h25519::ge> res;
+    MsmPoints pts;
+    BPP_TRY(gens_points(ctx, g, &pts));
+    BPP_TRY(msm_multi(ctx, d_s, (const uint32_t*)d_i, {0, (uint32_t)T}, pts, res));
+    h25519::encode(out, res[0]);
+    return BPP_OK;
+  });
 }
 
 int bpp_ipa_prove(bpp_ctx* ctx, const bpp_gens* g, bpp_transcript* tr, const uint8_t Q[32], const uint8_t* G_factors,
                   const uint8_t* H_factors, const uint8_t* a, const uint8_t* b, size_t n, uint8_t* L_out,
                   uint8_t* R_out, uint8_t a_out[32], uint8_t b_out[32]) {
-  if (!ctx || !g || !tr || !Q || !a || !b || !a_out || !b_out || ((!L_out || !R_out) && n > 1)) return BPP_ERR_ARG;
-  if (n == 0 || (n & (n - 1)) || n > g->n) return BPP_ERR_LEN;
-  BPP_HIP(hipSetDevice(ctx->device));
-  uint32_t *d_a, *d_b, *d_gf, *d_hf, *d_q;
-  BPP_TRY(upload_scalars(ctx, a, n, "ipa_in_a", &d_a));
-  BPP_TRY(upload_scalars(ctx, b, n, "ipa_in_b", &d_b));
-  BPP_TRY(upload_opt(ctx, G_factors, n, "ipa_in_gf", &d_gf));
-  BPP_TRY(upload_opt(ctx, H_factors, n, "ipa_in_hf", &d_hf));
-  BPP_TRY(decompress_ws(ctx, Q, 1, "ipa_q", &d_q));
-  IpaGens ig;
-  BPP_TRY(gens_points(ctx, g, &ig.pts));
-  BPP_TRY(msm_points_extra(ctx, &ig.pts, d_q, 1, (uint32_t)(2 * g->n + 2), "ipa_q_wt", (double)(n + 1)));
-  ig.gbase = 0;
-  ig.hbase = (uint32_t)g->n;
-  ig.qidx = ig.pts.n0;
-  IpaProofHost pf;
-  BPP_TRY(ipa_prove_dev(ctx, tr->t, ig, (uint32_t)n, d_gf, d_hf, d_a, d_b, pf));
-  for (size_t j = 0; j < pf.L.size(); ++j) {
-    memcpy(L_out + 32 * j, pf.L[j].data(), 32);
-    memcpy(R_out + 32 * j, pf.R[j].data(), 32);
-  }
-  hsc::to_bytes(a_out, pf.a);
-  hsc::to_bytes(b_out, pf.b);
-  return BPP_OK;
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !g || !tr || !Q || !a || !b || !a_out || !b_out || ((!L_out || !R_out) && n > 1)) return BPP_ERR_ARG;
+    if (n == 0 || (n & (n - 1)) || n > g->n) return BPP_ERR_LEN;
+    BPP_HIP(hipSetDevice(ctx->device));
+    uint32_t *d_a, *d_b, *d_gf, *d_hf, *d_q;
+    BPP_TRY(upload_scalars(ctx, a, n, "ipa_in_a", &d_a));
+    BPP_TRY(upload_scalars(ctx, b, n, "ipa_in_b", &d_b));
+    BPP_TRY(upload_opt(ctx, G_factors, n, "ipa_in_gf", &d_gf));
+    BPP_TRY(upload_opt(ctx, H_factors, n, "ipa_in_hf", &d_hf));
+    BPP_TRY(decompress_ws(ctx, Q, 1, "ipa_q", &d_q));
+    IpaGens ig;
+    BPP_TRY(gens_points(ctx, g, &ig.pts));
+    BPP_TRY(msm_points_extra(ctx, &ig.pts, d_q, 1, (uint32_t)(2 * g->n + 2), "ipa_q_wt", (double)(n + 1)));
+    ig.gbase = 0;
+    ig.hbase = (uint32_t)g->n;
+    ig.qidx = ig.pts.n0;
+    IpaProofHost pf;
+    BPP_TRY(ipa_prove_dev(ctx, tr->t, ig, (uint32_t)n, d_gf, d_hf, d_a, d_b, pf));
+    for (size_t j = 0; j < pf.L.size(); ++j) {
+      memcpy(L_out + 32 * j, pf.L[j].data(), 32);
+      memcpy(R_out + 32 * j, pf.R[j].data(), 32);
+    }
+    hsc::to_bytes(a_out, pf.a);
+    hsc::to_bytes(b_out, pf.b);
+    return BPP_OK;
+  });
 }
 
 int bpp_ipa_verify(bpp_ctx* ctx, const bpp_gens* g, bpp_transcript* tr, size_t n, const uint8_t* G_factors,
                    const uint8_t* H_factors, const uint8_t P[32], const uint8_t Q[32], const uint8_t* L,
                    const uint8_t* R, const uint8_t a[32], const uint8_t b[32]) {
-  if (!ctx || !g || !tr || !P || !Q || !a || !b || ((!L || !R) && n > 1)) return BPP_ERR_ARG;
-  if (n == 0 || (n & (n - 1)) || n > g->n) return BPP_ERR_LEN;
-  BPP_HIP(hipSetDevice(ctx->device));
-  uint32_t lg = 0;
-  while ((1u << lg) < n) ++lg;
-  std::vector<Enc32> Lv(lg), Rv(lg);
-  for (uint32_t j = 0; j < lg; ++j) {
-    memcpy(Lv[j].data(), L + 32 * j, 32);
-    memcpy(Rv[j].data(), R + 32 * j, 32);
-  }
-  hsc::Sc as, bs;
-  if (!hsc::from_canonical(as, a) || !hsc::from_canonical(bs, b)) return BPP_ERR_NONCANONICAL;
-  std::vector<hsc::Sc> gf(n, hsc::one()), hf(n, hsc::one());
-  for (size_t i = 0; i < n; ++i) {
-    if (G_factors && !hsc::from_canonical(gf[i], G_factors + 32 * i)) return BPP_ERR_NONCANONICAL;
-    if (H_factors && !hsc::from_canonical(hf[i], H_factors + 32 * i)) return BPP_ERR_NONCANONICAL;
-  }
-  std::vector<hsc::Sc> u_sq, uinv_sq, s;
-  if (!ipa_verification_scalars(tr->t, (uint32_t)n, Lv, Rv, u_sq, uinv_sq, s)) return BPP_ERR_VERIFY;
-  // extra points: Q, L_0.., R_0.., P
-  std::vector<uint8_t> extra((2 + 2 * lg) * 32);
-  memcpy(extra.data(), Q, 32);
-  memcpy(extra.data() + 32, L, 32 * lg);
-  memcpy(extra.data() + 32 * (1 + lg), R, 32 * lg);
-  memcpy(extra.data() + 32 * (1 + 2 * lg), P, 32);
-  uint32_t* d_x = nullptr;
-  int rc = decompress_ws(ctx, extra.data(), extra.size() / 32, "ipav_x", &d_x);
-  if (rc == BPP_ERR_DECOMPRESS) return BPP_ERR_VERIFY;
-  BPP_TRY(rc);
-  const uint32_t n0 = (uint32_t)(2 * g->n + 2);
-  const size_t T = 1 + 2 * n + 2 * lg + 1;
-  std::vector<uint8_t> sc(T * 32);
-  std::vector<uint32_t> idx(T);
-  size_t t = 0;
-  auto put = [&](const hsc::Sc& x, uint32_t i) {
-    hsc::to_bytes(sc.data() + 32 * t, x);
-    idx[t++] = i;
-  };
-  put(hsc::mul(as, bs), n0);
-  for (size_t i = 0; i < n; ++i) put(hsc::mul(hsc::mul(as, s[i]), gf[i]), g->gidx(i));
-  for (size_t i = 0; i < n; ++i) put(hsc::mul(hsc::mul(bs, s[n - 1 - i]), hf[i]), g->hidx(i));
-  for (uint32_t j = 0; j < lg; ++j) put(hsc::neg(u_sq[j]), n0 + 1 + j);
-  for (uint32_t j = 0; j < lg; ++j) put(hsc::neg(uinv_sq[j]), n0 + 1 + lg + j);
-  put(hsc::neg(hsc::one()), n0 + 1 + 2 * lg);
-  uint32_t* d_s = nullptr;
-  BPP_TRY(upload_scalars(ctx, sc.data(), T, "ipav_s", &d_s));
-  void* d_i = nullptr;
-  BPP_TRY(ctx_ws(ctx, "ipav_i", T * 4, &d_i));
-  BPP_TRY(ctx_h2d(ctx, d_i, idx.data(), T * 4));
-  std::vector<h25519::ge> res;
-  MsmPoints pts;
-  BPP_TRY(gens_points(ctx, g, &pts));
-  BPP_TRY(msm_points_extra(ctx, &pts, d_x, (uint32_t)(2 + 2 * lg), n0, "ipav_x_wt", (double)T));
-  BPP_TRY(msm_multi(ctx, d_s, (const uint32_t*)d_i, {0, (uint32_t)T}, pts, res));
-  uint8_t e[32];
-  h25519::encode(e, res[0]);
-  static const uint8_t zero[32] = {0};
-  return memcmp(e, zero, 32) == 0 ? BPP_OK : BPP_ERR_VERIFY;
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !g || !tr || !P || !Q || !a || !b || ((!L || !R) && n > 1)) return BPP_ERR_ARG;
+    if (n == 0 || (n & (n - 1)) || n > g->n) return BPP_ERR_LEN;
+    BPP_HIP(hipSetDevice(ctx->device));
+    uint32_t lg = 0;
+    while ((1u << lg) < n) ++lg;
+    std::vector<Enc32> Lv(lg), Rv(lg);
+    for (uint32_t j = 0; j < lg; ++j) {
+      memcpy(Lv[j].data(), L + 32 * j, 32);
+      memcpy(Rv[j].data(), R + 32 * j, 32);
+    }
+    hsc::Sc as, bs;
+    if (!hsc::from_canonical(as, a) || !hsc::from_canonical(bs, b)) return BPP_ERR_NONCANONICAL;
+    std::vector<hsc::Sc> gf(n, hsc::one()), hf(n, hsc::one());
+    for (size_t i = 0; i < n; ++i) {
+      if (G_factors && !hsc::from_canonical(gf[i], G_factors + 32 * i)) return BPP_ERR_NONCANONICAL;
+      if (H_factors && !hsc::from_canonical(hf[i], H_factors + 32 * i)) return BPP_ERR_NONCANONICAL;
+    }
+    std::vector<hsc::Sc> u_sq, uinv_sq, s;
+    if (!ipa_verification_scalars(tr->t, (uint32_t)n, Lv, Rv, u_sq, uinv_sq, s)) return BPP_ERR_VERIFY;
+    // extra points: Q, L_0.., R_0.., P
+    std::vector<uint8_t> extra((2 + 2 * lg) * 32);
+    memcpy(extra.data(), Q, 32);
+    memcpy(extra.data() + 32, L, 32 * lg);
+    memcpy(extra.data() + 32 * (1 + lg), R, 32 * lg);
+    memcpy(extra.data() + 32 * (1 + 2 * lg), P, 32);
+    uint32_t* d_x = nullptr;
+    int rc = decompress_ws(ctx, extra.data(), extra.size() / 32, "ipav_x", &d_x);
+    if (rc == BPP_ERR_DECOMPRESS) return BPP_ERR_VERIFY;
+    BPP_TRY(rc);
+    const uint32_t n0 = (uint32_t)(2 * g->n + 2);
+    const size_t T = 1 + 2 * n + 2 * lg + 1;
+    std::vector<uint8_t> sc(T * 32);
+    std::vector<uint32_t> idx(T);
+    size_t t = 0;
+    auto put = [&](const hsc::Sc& x, uint32_t i) {
+      hsc::to_bytes(sc.data() + 32 * t, x);
+      idx[t++] = i;
+    };
+    put(hsc::mul(as, bs), n0);
+    for (size_t i = 0; i < n; ++i) put(hsc::mul(hsc::mul(as, s[i]), gf[i]), g->gidx(i));
+    for (size_t i = 0; i < n; ++i) put(hsc::mul(hsc::mul(bs, s[n - 1 - i]), hf[i]), g->hidx(i));
+    for (uint32_t j = 0; j < lg; ++j) put(hsc::neg(u_sq[j]), n0 + 1 + j);
+    for (uint32_t j = 0; j < lg; ++j) put(hsc::neg(uinv_sq[j]), n0 + 1 + lg + j);
+    put(hsc::neg(hsc::one()), n0 + 1 + 2 * lg);
+    uint32_t* d_s = nullptr;
+    BPP_TRY(upload_scalars(ctx, sc.data(), T, "ipav_s", &d_s));
+    void* d_i = nullptr;
+    BPP_TRY(ctx_ws(ctx, "ipav_i", T * 4, &d_i));
+    BPP_TRY(ctx_h2d(ctx, d_i, idx.data(), T * 4));
+    std::vector<h25519::ge> res;
+    MsmPoints pts;
+    BPP_TRY(gens_points(ctx, g, &pts));
+    BPP_TRY(msm_points_extra(ctx, &pts, d_x, (uint32_t)(2 + 2 * lg), n0, "ipav_x_wt", (double)T));
+    BPP_TRY(msm_multi(ctx, d_s, (const uint32_t*)d_i, {0, (uint32_t)T}, pts, res));
+    uint8_t e[32];
+    h25519::encode(e, res[0]);
+    static const uint8_t zero[32] = {0};
+    return memcmp(e, zero, 32) == 0 ? BPP_OK : BPP_ERR_VERIFY;
+  });
 }
 
 }  // extern "C"

@@ -318,36 +318,42 @@ int upload_scalars(bpp_ctx* ctx, const uint8_t* scalars, size_t n, const char* n
 extern "C" {
 
 int bpp_msm_windows(size_t n, uint32_t* c, uint32_t* windows) {
-  uint32_t cc = msm_choose_c((double)(n ? n : 1));
-  if (c) *c = cc;
-  if (windows) *windows = (254 + cc - 1) / cc;
-  return BPP_OK;
+  return bpp_guard(nullptr, [&]() -> int {
+    uint32_t cc = msm_choose_c((double)(n ? n : 1));
+    if (c) *c = cc;
+    if (windows) *windows = (254 + cc - 1) / cc;
+    return BPP_OK;
+  });
 }
 
 int bpp_msm_table_dev(bpp_ctx* ctx, const void* d_scalars, const bpp_points* tbl, size_t n, uint8_t out[32]) {
-  if (!ctx || !tbl || !out || (!d_scalars && n)) return BPP_ERR_ARG;
-  if (n > tbl->n || n >= 0x80000000ull) return BPP_ERR_LEN;
-  BPP_HIP(hipSetDevice(ctx->device));
-  const uint32_t c = msm_choose_c((double)n);
-  const uint32_t W = (254 + c - 1) / c;
-  h25519::ge r;
-  BPP_TRY(msm_single_dev(ctx, (const uint32_t*)d_scalars, nullptr, tbl->d, n, c, 0, W, &r));
-  h25519::encode(out, r);
-  return BPP_OK;
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !tbl || !out || (!d_scalars && n)) return BPP_ERR_ARG;
+    if (n > tbl->n || n >= 0x80000000ull) return BPP_ERR_LEN;
+    BPP_HIP(hipSetDevice(ctx->device));
+    const uint32_t c = msm_choose_c((double)n);
+    const uint32_t W = (254 + c - 1) / c;
+    h25519::ge r;
+    BPP_TRY(msm_single_dev(ctx, (const uint32_t*)d_scalars, nullptr, tbl->d, n, c, 0, W, &r));
+    h25519::encode(out, r);
+    return BPP_OK;
+  });
 }
 
 int bpp_msm_table_dev_partial(bpp_ctx* ctx, const void* d_scalars, const bpp_points* tbl, size_t n, uint32_t w_begin,
                               uint32_t w_end, uint8_t partial[128]) {
-  if (!ctx || !tbl || !partial || (!d_scalars && n)) return BPP_ERR_ARG;
-  if (n > tbl->n || n >= 0x80000000ull) return BPP_ERR_LEN;
-  const uint32_t c = msm_choose_c((double)n);
-  const uint32_t W = (254 + c - 1) / c;
-  if (w_begin > w_end || w_end > W) return BPP_ERR_ARG;
-  BPP_HIP(hipSetDevice(ctx->device));
-  h25519::ge r;
-  BPP_TRY(msm_single_dev(ctx, (const uint32_t*)d_scalars, nullptr, tbl->d, n, c, w_begin, w_end - w_begin, &r));
-  h25519::ge_to_words((uint32_t*)partial, r);
-  return BPP_OK;
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !tbl || !partial || (!d_scalars && n)) return BPP_ERR_ARG;
+    if (n > tbl->n || n >= 0x80000000ull) return BPP_ERR_LEN;
+    const uint32_t c = msm_choose_c((double)n);
+    const uint32_t W = (254 + c - 1) / c;
+    if (w_begin > w_end || w_end > W) return BPP_ERR_ARG;
+    BPP_HIP(hipSetDevice(ctx->device));
+    h25519::ge r;
+    BPP_TRY(msm_single_dev(ctx, (const uint32_t*)d_scalars, nullptr, tbl->d, n, c, w_begin, w_end - w_begin, &r));
+    h25519::ge_to_words((uint32_t*)partial, r);
+    return BPP_OK;
+  });
 }
 
 static int msm_submit(bpp_ctx* ctx, const void* d_scalars, const void* h_scalars, const bpp_points* tbl, size_t n,
@@ -355,27 +361,35 @@ static int msm_submit(bpp_ctx* ctx, const void* d_scalars, const void* h_scalars
 
 int bpp_msm_submit(bpp_ctx* ctx, const void* d_scalars, const bpp_points* tbl, size_t n, uint32_t w_begin,
                    uint32_t w_end, uint64_t* ticket) {
-  if (!ctx || !tbl || !ticket || (!d_scalars && n)) return BPP_ERR_ARG;
-  return msm_submit(ctx, d_scalars, nullptr, tbl, n, w_begin, w_end, ticket);
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !tbl || !ticket || (!d_scalars && n)) return BPP_ERR_ARG;
+    return msm_submit(ctx, d_scalars, nullptr, tbl, n, w_begin, w_end, ticket);
+  });
 }
 
 int bpp_msm_submit_host(bpp_ctx* ctx, const void* h_scalars, const bpp_points* tbl, size_t n, uint32_t w_begin,
                         uint32_t w_end, uint64_t* ticket) {
-  if (!ctx || !tbl || !ticket || (!h_scalars && n)) return BPP_ERR_ARG;
-  return msm_submit(ctx, nullptr, h_scalars, tbl, n, w_begin, w_end, ticket);
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !tbl || !ticket || (!h_scalars && n)) return BPP_ERR_ARG;
+    return msm_submit(ctx, nullptr, h_scalars, tbl, n, w_begin, w_end, ticket);
+  });
 }
 
 int bpp_host_alloc(bpp_ctx* ctx, size_t bytes, void** hptr) {
-  if (!ctx || !hptr) return BPP_ERR_ARG;
-  BPP_HIP(hipSetDevice(ctx->device));
-  BPP_HIP(hipHostMalloc(hptr, bytes ? bytes : 1));
-  return BPP_OK;
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !hptr) return BPP_ERR_ARG;
+    BPP_HIP(hipSetDevice(ctx->device));
+    BPP_HIP(hipHostMalloc(hptr, bytes ? bytes : 1));
+    return BPP_OK;
+  });
 }
 
 int bpp_host_free(bpp_ctx* ctx, void* hptr) {
-  if (!ctx) return BPP_ERR_ARG;
-  BPP_HIP(hipHostFree(hptr));
-  return BPP_OK;
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx) return BPP_ERR_ARG;
+    BPP_HIP(hipHostFree(hptr));
+    return BPP_OK;
+  });
 }
 
 // d_scalars (device) or h_scalars (host: copied on the slot's stream, so the
@@ -523,120 +537,132 @@ static int msm_submit(bpp_ctx* ctx, const void* d_scalars, const void* h_scalars
 }
 
 int bpp_msm_collect(bpp_ctx* ctx, uint64_t ticket, uint8_t out[32], uint8_t partial[128]) {
-  if (!ctx) return BPP_ERR_ARG;
-  size_t s = BPP_MSM_INFLIGHT;
-  for (size_t i = 0; i < BPP_MSM_INFLIGHT; ++i)
-    if (ctx->msm_slot[i].busy && ctx->msm_slot[i].ticket == ticket) s = i;
-  if (s == BPP_MSM_INFLIGHT) {
-    ctx->err = "bpp_msm_collect: unknown or already collected ticket";
-    return BPP_ERR_ARG;
-  }
-  bpp_ctx::MsmSlot& sl = ctx->msm_slot[s];
-  BPP_HIP(hipSetDevice(ctx->device));
-  // the slot (its child stream and pinned buffer) is released only once the
-  // child's copies are known to be done; on a failed wait the child stream
-  // is drained before the slot can be reused
-  if (hipEventSynchronize(sl.done) != hipSuccess) {
-    bpp_ctx* ch = s < ctx->children.size() ? ctx->children[s] : nullptr;
-    if (ch) hipStreamSynchronize(ch->stream);
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx) return BPP_ERR_ARG;
+    size_t s = BPP_MSM_INFLIGHT;
+    for (size_t i = 0; i < BPP_MSM_INFLIGHT; ++i)
+      if (ctx->msm_slot[i].busy && ctx->msm_slot[i].ticket == ticket) s = i;
+    if (s == BPP_MSM_INFLIGHT) {
+      ctx->err = "bpp_msm_collect: unknown or already collected ticket";
+      return BPP_ERR_ARG;
+    }
+    bpp_ctx::MsmSlot& sl = ctx->msm_slot[s];
+    BPP_HIP(hipSetDevice(ctx->device));
+    // the slot (its child stream and pinned buffer) is released only once the
+    // child's copies are known to be done; on a failed wait the child stream
+    // is drained before the slot can be reused
+    if (hipEventSynchronize(sl.done) != hipSuccess) {
+      bpp_ctx* ch = s < ctx->children.size() ? ctx->children[s] : nullptr;
+      if (ch) hipStreamSynchronize(ch->stream);
+      sl.busy = false;
+      sl.h = nullptr;
+      ctx->err = "bpp_msm_collect: device error while waiting for the MSM";
+      return BPP_ERR_DEVICE;
+    }
     sl.busy = false;
+    h25519::ge r = h25519::ge_identity();
+    if (sl.h && sl.Wn) r = horner_host_terms((const uint32_t*)sl.h, sl.Wn, sl.nterms, sl.c, sl.wb);
     sl.h = nullptr;
-    ctx->err = "bpp_msm_collect: device error while waiting for the MSM";
-    return BPP_ERR_DEVICE;
-  }
-  sl.busy = false;
-  h25519::ge r = h25519::ge_identity();
-  if (sl.h && sl.Wn) r = horner_host_terms((const uint32_t*)sl.h, sl.Wn, sl.nterms, sl.c, sl.wb);
-  sl.h = nullptr;
-  if (out) h25519::encode(out, r);
-  if (partial) h25519::ge_to_words((uint32_t*)partial, r);
-  return BPP_OK;
+    if (out) h25519::encode(out, r);
+    if (partial) h25519::ge_to_words((uint32_t*)partial, r);
+    return BPP_OK;
+  });
 }
 
 int bpp_partials_finish(const uint8_t* partials, size_t count, uint8_t out[32]) {
-  if (!out || (!partials && count)) return BPP_ERR_ARG;
-  h25519::ge acc = h25519::ge_identity();
-  for (size_t i = 0; i < count; ++i) {
-    uint32_t w[32];
-    memcpy(w, partials + 128 * i, 128);
-    acc = h25519::ge_add(acc, h25519::ge_from_words(w));
-  }
-  h25519::encode(out, acc);
-  return BPP_OK;
+  return bpp_guard(nullptr, [&]() -> int {
+    if (!out || (!partials && count)) return BPP_ERR_ARG;
+    h25519::ge acc = h25519::ge_identity();
+    for (size_t i = 0; i < count; ++i) {
+      uint32_t w[32];
+      memcpy(w, partials + 128 * i, 128);
+      acc = h25519::ge_add(acc, h25519::ge_from_words(w));
+    }
+    h25519::encode(out, acc);
+    return BPP_OK;
+  });
 }
 
 int bpp_points_double_compress(const uint8_t* raw, size_t count, uint8_t* out) {
-  if ((!raw || !out) && count) return BPP_ERR_ARG;
-  std::vector<h25519::ge> pts(count);
-  for (size_t i = 0; i < count; ++i) {
-    uint32_t w[32];
-    memcpy(w, raw + 128 * i, 128);
-    pts[i] = h25519::ge_from_words(w);
-  }
-  h25519::encode_double_batch(pts.data(), count, out);
-  return BPP_OK;
+  return bpp_guard(nullptr, [&]() -> int {
+    if ((!raw || !out) && count) return BPP_ERR_ARG;
+    std::vector<h25519::ge> pts(count);
+    for (size_t i = 0; i < count; ++i) {
+      uint32_t w[32];
+      memcpy(w, raw + 128 * i, 128);
+      pts[i] = h25519::ge_from_words(w);
+    }
+    h25519::encode_double_batch(pts.data(), count, out);
+    return BPP_OK;
+  });
 }
 
 int bpp_msm_table(bpp_ctx* ctx, const uint8_t* scalars, const bpp_points* tbl, size_t n, uint8_t out[32]) {
-  if (!ctx || !tbl || !out || (!scalars && n)) return BPP_ERR_ARG;
-  if (n > tbl->n) return BPP_ERR_LEN;
-  BPP_HIP(hipSetDevice(ctx->device));
-  uint32_t* d_s = nullptr;
-  BPP_TRY(upload_scalars(ctx, scalars, n, "msm_scal", &d_s));
-  return bpp_msm_table_dev(ctx, d_s, tbl, n, out);
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !tbl || !out || (!scalars && n)) return BPP_ERR_ARG;
+    if (n > tbl->n) return BPP_ERR_LEN;
+    BPP_HIP(hipSetDevice(ctx->device));
+    uint32_t* d_s = nullptr;
+    BPP_TRY(upload_scalars(ctx, scalars, n, "msm_scal", &d_s));
+    return bpp_msm_table_dev(ctx, d_s, tbl, n, out);
+  });
 }
 
 int bpp_msm(bpp_ctx* ctx, const uint8_t* scalars, const uint8_t* points, size_t n, uint8_t out[32]) {
-  if (!ctx || !out || ((!scalars || !points) && n)) return BPP_ERR_ARG;
-  bpp_points* tbl = nullptr;
-  size_t bad = 0;
-  BPP_TRY(bpp_points_decompress(ctx, points, n, &tbl, &bad));
-  int rc = bpp_msm_table(ctx, scalars, tbl, n, out);
-  bpp_points_destroy(tbl);
-  return rc;
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !out || ((!scalars || !points) && n)) return BPP_ERR_ARG;
+    bpp_points* tbl = nullptr;
+    size_t bad = 0;
+    BPP_TRY(bpp_points_decompress(ctx, points, n, &tbl, &bad));
+    int rc = bpp_msm_table(ctx, scalars, tbl, n, out);
+    bpp_points_destroy(tbl);
+    return rc;
+  });
 }
 
 int bpp_msm_batch(bpp_ctx* ctx, size_t count, const uint64_t* offsets, const uint8_t* scalars,
                   const uint32_t* point_idx, const bpp_points* tbl, uint8_t* out) {
-  if (!ctx || !offsets || !tbl || (!out && count)) return BPP_ERR_ARG;
-  if (count == 0) return BPP_OK;
-  const uint64_t T = offsets[count];
-  if (offsets[0] != 0 || T >= 0x80000000ull) return BPP_ERR_LEN;
-  for (size_t j = 0; j < count; ++j)
-    if (offsets[j + 1] < offsets[j]) return BPP_ERR_LEN;
-  for (uint64_t t = 0; t < T; ++t)
-    if (point_idx[t] >= tbl->n) return BPP_ERR_LEN;
-  BPP_HIP(hipSetDevice(ctx->device));
-  uint32_t* d_s = nullptr;
-  BPP_TRY(upload_scalars(ctx, scalars, T, "msmb_scal", &d_s));
-  void *d_idx, *d_off, *d_res;
-  BPP_TRY(ctx_ws(ctx, "msmb_idx", T * 4 + 4, &d_idx));
-  BPP_TRY(ctx_ws(ctx, "msmb_off", (count + 1) * 4, &d_off));
-  BPP_TRY(ctx_ws(ctx, "msmb_res", count * P3_BYTES, &d_res));
-  std::vector<uint32_t> off32(count + 1);
-  for (size_t j = 0; j <= count; ++j) off32[j] = (uint32_t)offsets[j];
-  if (T) BPP_HIP(hipMemcpyAsync(d_idx, point_idx, T * 4, hipMemcpyHostToDevice, ctx->stream));
-  BPP_HIP(hipMemcpyAsync(d_off, off32.data(), (count + 1) * 4, hipMemcpyHostToDevice, ctx->stream));
-  const uint32_t c = msm_choose_c((double)T / (double)count);
-  const uint32_t W = (254 + c - 1) / c;
-  MsmGeom g;
-  g.M = (uint32_t)count;
-  g.T = (uint32_t)T;
-  g.c = c;
-  g.W = W;
-  g.wb = 0;
-  g.Wn = W;
-  g.B = 1u << (c - 1);
-  g.fb = 0;
-  uint32_t* d_ws = nullptr;
-  BPP_TRY(msm_engine(ctx, d_s, (const uint32_t*)d_idx, (const uint32_t*)d_off, g.M, g.T, c, 0, W, tbl->d, &d_ws));
-  {
-    ProfScope ps(ctx, "msm_horner");
-    hipLaunchKernelGGL(k_msm_horner, dim3(grid_for(count, 64)), dim3(64), 0, ctx->stream, (const uint32_t*)d_ws, g,
-                       (uint32_t*)d_res);
-  }
-  BPP_TRY(ctx_check_launch(ctx, "k_msm_horner"));
-  return points_compress_p3(ctx, (const uint32_t*)d_res, count, out);
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !offsets || !tbl || (!out && count)) return BPP_ERR_ARG;
+    if (count == 0) return BPP_OK;
+    const uint64_t T = offsets[count];
+    if (offsets[0] != 0 || T >= 0x80000000ull) return BPP_ERR_LEN;
+    for (size_t j = 0; j < count; ++j)
+      if (offsets[j + 1] < offsets[j]) return BPP_ERR_LEN;
+    for (uint64_t t = 0; t < T; ++t)
+      if (point_idx[t] >= tbl->n) return BPP_ERR_LEN;
+    BPP_HIP(hipSetDevice(ctx->device));
+    uint32_t* d_s = nullptr;
+    BPP_TRY(upload_scalars(ctx, scalars, T, "msmb_scal", &d_s));
+    void *d_idx, *d_off, *d_res;
+    BPP_TRY(ctx_ws(ctx, "msmb_idx", T * 4 + 4, &d_idx));
+    BPP_TRY(ctx_ws(ctx, "msmb_off", (count + 1) * 4, &d_off));
+    BPP_TRY(ctx_ws(ctx, "msmb_res", count * P3_BYTES, &d_res));
+    std::vector<uint32_t> off32(count + 1);
+    for (size_t j = 0; j <= count; ++j) off32[j] = (uint32_t)offsets[j];
+    if (T) BPP_HIP(hipMemcpyAsync(d_idx, point_idx, T * 4, hipMemcpyHostToDevice, ctx->stream));
+    BPP_HIP(hipMemcpyAsync(d_off, off32.data(), (count + 1) * 4, hipMemcpyHostToDevice, ctx->stream));
+    const uint32_t c = msm_choose_c((double)T / (double)count);
+    const uint32_t W = (254 + c - 1) / c;
+    MsmGeom g;
+    g.M = (uint32_t)count;
+    g.T = (uint32_t)T;
+    g.c = c;
+    g.W = W;
+    g.wb = 0;
+    g.Wn = W;
+    g.B = 1u << (c - 1);
+    g.fb = 0;
+    uint32_t* d_ws = nullptr;
+    BPP_TRY(msm_engine(ctx, d_s, (const uint32_t*)d_idx, (const uint32_t*)d_off, g.M, g.T, c, 0, W, tbl->d, &d_ws));
+    {
+      ProfScope ps(ctx, "msm_horner");
+      hipLaunchKernelGGL(k_msm_horner, dim3(grid_for(count, 64)), dim3(64), 0, ctx->stream, (const uint32_t*)d_ws, g,
+                         (uint32_t*)d_res);
+    }
+    BPP_TRY(ctx_check_launch(ctx, "k_msm_horner"));
+    return points_compress_p3(ctx, (const uint32_t*)d_res, count, out);
+  });
 }
 
 }  // extern "C"

@@ -1154,19 +1154,21 @@ size_t bpp_perm_proof_len(uint32_t k) { return k >= 2 && k <= (1u << 20) ? perm:
 
 int bpp_perm_prove(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, uint64_t seed, const uint8_t* label, size_t llen,
                    uint8_t* proof_out, uint8_t* V_out, uint32_t* perm_out) {
-  if (!ctx || !G || !proof_out || !V_out || (!label && llen) || k < 2 || k > (1u << 20)) return BPP_ERR_ARG;
-  const perm::Circuit C = perm::build(k);
-  if (G->n < C.n_p) {
-    ctx->err = "generators shorter than the padded circuit";
-    return BPP_ERR_LEN;
-  }
-  BPP_HIP(hipSetDevice(ctx->device));
-  std::vector<Proof> Ps;
-  BPP_TRY(prove_batch(ctx, G, C, {perm::Seed::u64(seed)}, label, llen, Ps));
-  serialize(C, Ps[0], proof_out);
-  for (uint32_t j = 0; j < C.m; ++j) memcpy(V_out + 32 * j, Ps[0].V[j].data(), 32);
-  if (perm_out) memcpy(perm_out, Ps[0].pi.data(), 4 * k);
-  return BPP_OK;
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !G || !proof_out || !V_out || (!label && llen) || k < 2 || k > (1u << 20)) return BPP_ERR_ARG;
+    const perm::Circuit C = perm::build(k);
+    if (G->n < C.n_p) {
+      ctx->err = "generators shorter than the padded circuit";
+      return BPP_ERR_LEN;
+    }
+    BPP_HIP(hipSetDevice(ctx->device));
+    std::vector<Proof> Ps;
+    BPP_TRY(prove_batch(ctx, G, C, {perm::Seed::u64(seed)}, label, llen, Ps));
+    serialize(C, Ps[0], proof_out);
+    for (uint32_t j = 0; j < C.m; ++j) memcpy(V_out + 32 * j, Ps[0].V[j].data(), 32);
+    if (perm_out) memcpy(perm_out, Ps[0].pi.data(), 4 * k);
+    return BPP_OK;
+  });
 }
 
 namespace {
@@ -1239,90 +1241,104 @@ static int prove_batch_api(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, const st
 
 int bpp_perm_prove_batch(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, size_t count, const uint64_t* seeds,
                          const uint8_t* label, size_t llen, uint8_t* proofs_out, uint8_t* V_out) {
-  if (!ctx || !G || (!seeds && count) || ((!proofs_out || !V_out) && count) || (!label && llen) || k < 2 ||
-      k > (1u << 20))
-    return BPP_ERR_ARG;
-  std::vector<perm::Seed> sd(count);
-  for (size_t i = 0; i < count; ++i) sd[i] = perm::Seed::u64(seeds[i]);
-  return prove_batch_api(ctx, G, k, sd, label, llen, proofs_out, V_out);
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !G || (!seeds && count) || ((!proofs_out || !V_out) && count) || (!label && llen) || k < 2 ||
+        k > (1u << 20))
+      return BPP_ERR_ARG;
+    std::vector<perm::Seed> sd(count);
+    for (size_t i = 0; i < count; ++i) sd[i] = perm::Seed::u64(seeds[i]);
+    return prove_batch_api(ctx, G, k, sd, label, llen, proofs_out, V_out);
+  });
 }
 
 int bpp_perm_prove_batch_entropy(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, size_t count, const uint8_t* seeds32,
                                  const uint8_t* label, size_t llen, uint8_t* proofs_out, uint8_t* V_out) {
-  if (!ctx || !G || ((!proofs_out || !V_out) && count) || (!label && llen) || k < 2 || k > (1u << 20))
-    return BPP_ERR_ARG;
-  std::vector<uint8_t> ent;
-  if (!seeds32 && count) {  // the OS CSPRNG, the reference's thread_rng() (circuit_lib.rs:175)
-    ent.resize(32 * count);
-    size_t got = 0;
-    while (got < ent.size()) {
-      const ssize_t r = getrandom(ent.data() + got, ent.size() - got, 0);
-      if (r < 0) {
-        if (errno == EINTR) continue;
-        ctx->err = "getrandom failed";
-        return BPP_ERR_DEVICE;
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !G || ((!proofs_out || !V_out) && count) || (!label && llen) || k < 2 || k > (1u << 20))
+      return BPP_ERR_ARG;
+    std::vector<uint8_t> ent;
+    if (!seeds32 && count) {  // the OS CSPRNG, the reference's thread_rng() (circuit_lib.rs:175)
+      ent.resize(32 * count);
+      size_t got = 0;
+      while (got < ent.size()) {
+        const ssize_t r = getrandom(ent.data() + got, ent.size() - got, 0);
+        if (r < 0) {
+          if (errno == EINTR) continue;
+          ctx->err = "getrandom failed";
+          return BPP_ERR_DEVICE;
+        }
+        got += (size_t)r;
       }
-      got += (size_t)r;
+      seeds32 = ent.data();
     }
-    seeds32 = ent.data();
-  }
-  std::vector<perm::Seed> sd(count);
-  for (size_t i = 0; i < count; ++i) sd[i] = perm::Seed::bytes32(seeds32 + 32 * i);
-  int rc = prove_batch_api(ctx, G, k, sd, label, llen, proofs_out, V_out);
-  if (!ent.empty()) memset(ent.data(), 0, ent.size());
-  for (perm::Seed& x : sd) memset(x.b, 0, sizeof x.b);
-  const int wrc = prove_wipe(ctx);
-  return rc ? rc : wrc;
+    std::vector<perm::Seed> sd(count);
+    for (size_t i = 0; i < count; ++i) sd[i] = perm::Seed::bytes32(seeds32 + 32 * i);
+    int rc = prove_batch_api(ctx, G, k, sd, label, llen, proofs_out, V_out);
+    if (!ent.empty()) memset(ent.data(), 0, ent.size());
+    for (perm::Seed& x : sd) memset(x.b, 0, sizeof x.b);
+    const int wrc = prove_wipe(ctx);
+    return rc ? rc : wrc;
+  });
 }
 
 int bpp_perm_verify(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, const uint8_t* label, size_t llen,
                     const uint8_t* proof, size_t proof_len, const uint8_t* V) {
-  if (!ctx || !G || !proof || !V || (!label && llen) || k < 2 || k > (1u << 20)) return BPP_ERR_ARG;
-  if (proof_len != perm::proof_len(k)) return BPP_ERR_VERIFY;
-  BPP_HIP(hipSetDevice(ctx->device));
-  const perm::Circuit C = perm::build(k);
-  return verify_batch(ctx, G, C, label, llen, 1, proof, V);
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !G || !proof || !V || (!label && llen) || k < 2 || k > (1u << 20)) return BPP_ERR_ARG;
+    if (proof_len != perm::proof_len(k)) return BPP_ERR_VERIFY;
+    BPP_HIP(hipSetDevice(ctx->device));
+    const perm::Circuit C = perm::build(k);
+    return verify_batch(ctx, G, C, label, llen, 1, proof, V);
+  });
 }
 
 int bpp_perm_verify_batch(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, size_t count, const uint8_t* label, size_t llen,
                           const uint8_t* proofs, const uint8_t* V) {
-  if (!ctx || !G || ((!proofs || !V) && count) || (!label && llen) || k < 2 || k > (1u << 20)) return BPP_ERR_ARG;
-  if (!count) return BPP_OK;
-  BPP_HIP(hipSetDevice(ctx->device));
-  const perm::Circuit C = perm::build(k);
-  return verify_batch(ctx, G, C, label, llen, count, proofs, V);
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !G || ((!proofs || !V) && count) || (!label && llen) || k < 2 || k > (1u << 20)) return BPP_ERR_ARG;
+    if (!count) return BPP_OK;
+    BPP_HIP(hipSetDevice(ctx->device));
+    const perm::Circuit C = perm::build(k);
+    return verify_batch(ctx, G, C, label, llen, count, proofs, V);
+  });
 }
 
 int bpp_perm_verify_begin(uint32_t k, size_t count, const uint8_t* label, size_t llen, const uint8_t* proofs,
                           const uint8_t* V, uint8_t* r_out, bpp_verify_job** out) {
-  if (!out || ((!proofs || !V) && count) || (!label && llen) || k < 2 || k > (1u << 20)) return BPP_ERR_ARG;
-  *out = nullptr;
-  const perm::Circuit C = perm::build(k);
-  std::unique_ptr<bpp_verify_job> job;
-  BPP_TRY(verify_begin(C, label, llen, count, proofs, perm::proof_len(k), V, job));
-  if (r_out)
-    for (size_t p = 0; p < count; ++p) hsc::to_bytes(r_out + 32 * p, job->rs[p]);
-  *out = job.release();
-  return BPP_OK;
+  return bpp_guard(nullptr, [&]() -> int {
+    if (!out || ((!proofs || !V) && count) || (!label && llen) || k < 2 || k > (1u << 20)) return BPP_ERR_ARG;
+    *out = nullptr;
+    const perm::Circuit C = perm::build(k);
+    std::unique_ptr<bpp_verify_job> job;
+    BPP_TRY(verify_begin(C, label, llen, count, proofs, perm::proof_len(k), V, job));
+    if (r_out)
+      for (size_t p = 0; p < count; ++p) hsc::to_bytes(r_out + 32 * p, job->rs[p]);
+    *out = job.release();
+    return BPP_OK;
+  });
 }
 
 int bpp_perm_verify_begin_dev(bpp_ctx* ctx, uint32_t k, size_t count, const uint8_t* label, size_t llen,
                               const uint8_t* proofs, const uint8_t* V, uint8_t* r_out, bpp_verify_job** out) {
-  if (!ctx || !out || ((!proofs || !V) && count) || (!label && llen) || k < 2 || k > (1u << 20)) return BPP_ERR_ARG;
-  *out = nullptr;
-  BPP_HIP(hipSetDevice(ctx->device));
-  const perm::Circuit C = perm::build(k);
-  std::unique_ptr<bpp_verify_job> job;
-  BPP_TRY(verify_begin_dev(ctx, C, label, llen, count, proofs, V, job));
-  if (r_out && count) memcpy(r_out, job->rs.data(), 32 * count);
-  *out = job.release();
-  return BPP_OK;
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !out || ((!proofs || !V) && count) || (!label && llen) || k < 2 || k > (1u << 20)) return BPP_ERR_ARG;
+    *out = nullptr;
+    BPP_HIP(hipSetDevice(ctx->device));
+    const perm::Circuit C = perm::build(k);
+    std::unique_ptr<bpp_verify_job> job;
+    BPP_TRY(verify_begin_dev(ctx, C, label, llen, count, proofs, V, job));
+    if (r_out && count) memcpy(r_out, job->rs.data(), 32 * count);
+    *out = job.release();
+    return BPP_OK;
+  });
 }
 
 int bpp_perm_verify_terms(const bpp_verify_job* job, size_t* terms) {
-  if (!job || !terms) return BPP_ERR_ARG;
-  *terms = verify_terms(*job);
-  return BPP_OK;
+  return bpp_guard(nullptr, [&]() -> int {
+    if (!job || !terms) return BPP_ERR_ARG;
+    *terms = verify_terms(*job);
+    return BPP_OK;
+  });
 }
 
 static int parse_rs(const uint8_t* r_all, size_t total, std::vector<Sc>& rs) {
@@ -1334,44 +1350,50 @@ static int parse_rs(const uint8_t* r_all, size_t total, std::vector<Sc>& rs) {
 
 int bpp_perm_verify_scalars(const bpp_verify_job* job, const uint8_t* r_all, size_t total, size_t first,
                             uint8_t* scalars_out, uint8_t* points_out) {
-  if (!job || (!r_all && total) || !scalars_out || (!points_out && job->count)) return BPP_ERR_ARG;
-  if (job->dev) return BPP_ERR_ARG;  // (a device job keeps no host replay to expand)
-  std::vector<Sc> rs, sc;
-  std::vector<uint8_t> enc;
-  BPP_TRY(parse_rs(r_all, total, rs));
-  BPP_TRY(verify_terms_weighted(*job, rs.data(), total, first, sc, enc));
-  for (size_t i = 0; i < sc.size(); ++i) hsc::to_bytes(scalars_out + 32 * i, sc[i]);
-  if (!enc.empty()) memcpy(points_out, enc.data(), enc.size());
-  return BPP_OK;
+  return bpp_guard(nullptr, [&]() -> int {
+    if (!job || (!r_all && total) || !scalars_out || (!points_out && job->count)) return BPP_ERR_ARG;
+    if (job->dev) return BPP_ERR_ARG;  // (a device job keeps no host replay to expand)
+    std::vector<Sc> rs, sc;
+    std::vector<uint8_t> enc;
+    BPP_TRY(parse_rs(r_all, total, rs));
+    BPP_TRY(verify_terms_weighted(*job, rs.data(), total, first, sc, enc));
+    for (size_t i = 0; i < sc.size(); ++i) hsc::to_bytes(scalars_out + 32 * i, sc[i]);
+    if (!enc.empty()) memcpy(points_out, enc.data(), enc.size());
+    return BPP_OK;
+  });
 }
 
 int bpp_perm_verify_partial(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job* job, const uint8_t* r_all,
                             size_t total, size_t first, uint32_t w_begin, uint32_t w_end, uint8_t partial[128]) {
-  if (!ctx || !G || !job || !partial || (!r_all && total)) return BPP_ERR_ARG;
-  const uint32_t c = msm_choose_c((double)verify_terms(*job));
-  if (w_begin > w_end || w_end > (254 + c - 1) / c) return BPP_ERR_ARG;
-  std::vector<Sc> rs;
-  BPP_TRY(parse_rs(r_all, total, rs));
-  if (first > total || job->count > total - first) return BPP_ERR_ARG;
-  BPP_HIP(hipSetDevice(ctx->device));
-  h25519::ge r = h25519::ge_identity();
-  if (job->count) {
-    if (job->dev)
-      BPP_TRY(verify_partial_dev(ctx, G, *job, rs.data(), total, first, w_begin, w_end, &r));
-    else
-      BPP_TRY(verify_partial(ctx, G, *job, rs.data(), total, first, w_begin, w_end, &r));
-  }
-  h25519::ge_to_words((uint32_t*)partial, r);
-  return BPP_OK;
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !G || !job || !partial || (!r_all && total)) return BPP_ERR_ARG;
+    const uint32_t c = msm_choose_c((double)verify_terms(*job));
+    if (w_begin > w_end || w_end > (254 + c - 1) / c) return BPP_ERR_ARG;
+    std::vector<Sc> rs;
+    BPP_TRY(parse_rs(r_all, total, rs));
+    if (first > total || job->count > total - first) return BPP_ERR_ARG;
+    BPP_HIP(hipSetDevice(ctx->device));
+    h25519::ge r = h25519::ge_identity();
+    if (job->count) {
+      if (job->dev)
+        BPP_TRY(verify_partial_dev(ctx, G, *job, rs.data(), total, first, w_begin, w_end, &r));
+      else
+        BPP_TRY(verify_partial(ctx, G, *job, rs.data(), total, first, w_begin, w_end, &r));
+    }
+    h25519::ge_to_words((uint32_t*)partial, r);
+    return BPP_OK;
+  });
 }
 
 void bpp_perm_verify_end(bpp_verify_job* job) { delete job; }
 
 int bpp_partials_is_identity(const uint8_t* partials, size_t count) {
-  uint8_t e[32];
-  BPP_TRY(bpp_partials_finish(partials, count, e));
-  static const uint8_t zero[32] = {0};
-  return memcmp(e, zero, 32) == 0 ? BPP_OK : BPP_ERR_VERIFY;
+  return bpp_guard(nullptr, [&]() -> int {
+    uint8_t e[32];
+    BPP_TRY(bpp_partials_finish(partials, count, e));
+    static const uint8_t zero[32] = {0};
+    return memcmp(e, zero, 32) == 0 ? BPP_OK : BPP_ERR_VERIFY;
+  });
 }
 
 }  // extern "C"

@@ -158,99 +158,105 @@ int sc_halve_dev(bpp_ctx* ctx, const uint32_t* d_in, uint32_t* d_out, size_t n) 
 extern "C" {
 
 int bpp_points_decompress(bpp_ctx* ctx, const uint8_t* enc, size_t n, bpp_points** out, size_t* bad_index) {
-  if (!ctx || !out || (!enc && n)) return BPP_ERR_ARG;
-  *out = nullptr;
-  BPP_HIP(hipSetDevice(ctx->device));
-  bpp_points* P = new bpp_points();
-  P->ctx = ctx;
-  P->n = n;
-  if (hipMalloc(&P->d, (n ? n : 1) * MSM_NIELS_WORDS * 4) != hipSuccess) {
-    delete P;
-    ctx->err = "hipMalloc point table";
-    return BPP_ERR_NOMEM;
-  }
-  void* d_enc = nullptr;
-  void* d_bad = nullptr;
-  int rc = BPP_OK;
-  if (n) {
-    rc = ctx_ws(ctx, "dec_in", n * 32, &d_enc);
-    if (!rc) rc = ctx_ws(ctx, "dec_bad", 8, &d_bad);
-    if (!rc) {
-      unsigned long long init = ~0ull;
-      hipMemcpyAsync(d_enc, enc, n * 32, hipMemcpyHostToDevice, ctx->stream);
-      hipMemcpyAsync(d_bad, &init, 8, hipMemcpyHostToDevice, ctx->stream);
-      {
-        ProfScope ps(ctx, "decompress");
-        hipLaunchKernelGGL(k_decompress, dim3(grid_for(n, 64)), dim3(64), 0, ctx->stream, (const uint32_t*)d_enc, n,
-                           P->d, (unsigned long long*)d_bad);
-      }
-      rc = ctx_check_launch(ctx, "k_decompress");
-      unsigned long long bad = ~0ull;
-      if (!rc && hipMemcpyAsync(&bad, d_bad, 8, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess) rc = BPP_ERR_DEVICE;
-      if (!rc && hipStreamSynchronize(ctx->stream) != hipSuccess) rc = BPP_ERR_DEVICE;
-      if (!rc && bad != ~0ull) {
-        if (bad_index) *bad_index = (size_t)bad;
-        ctx->err = "invalid ristretto encoding at index " + std::to_string(bad);
-        rc = BPP_ERR_DECOMPRESS;
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !out || (!enc && n)) return BPP_ERR_ARG;
+    *out = nullptr;
+    BPP_HIP(hipSetDevice(ctx->device));
+    bpp_points* P = new bpp_points();
+    P->ctx = ctx;
+    P->n = n;
+    if (hipMalloc(&P->d, (n ? n : 1) * MSM_NIELS_WORDS * 4) != hipSuccess) {
+      delete P;
+      ctx->err = "hipMalloc point table";
+      return BPP_ERR_NOMEM;
+    }
+    void* d_enc = nullptr;
+    void* d_bad = nullptr;
+    int rc = BPP_OK;
+    if (n) {
+      rc = ctx_ws(ctx, "dec_in", n * 32, &d_enc);
+      if (!rc) rc = ctx_ws(ctx, "dec_bad", 8, &d_bad);
+      if (!rc) {
+        unsigned long long init = ~0ull;
+        hipMemcpyAsync(d_enc, enc, n * 32, hipMemcpyHostToDevice, ctx->stream);
+        hipMemcpyAsync(d_bad, &init, 8, hipMemcpyHostToDevice, ctx->stream);
+        {
+          ProfScope ps(ctx, "decompress");
+          hipLaunchKernelGGL(k_decompress, dim3(grid_for(n, 64)), dim3(64), 0, ctx->stream, (const uint32_t*)d_enc, n,
+                             P->d, (unsigned long long*)d_bad);
+        }
+        rc = ctx_check_launch(ctx, "k_decompress");
+        unsigned long long bad = ~0ull;
+        if (!rc && hipMemcpyAsync(&bad, d_bad, 8, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess) rc = BPP_ERR_DEVICE;
+        if (!rc && hipStreamSynchronize(ctx->stream) != hipSuccess) rc = BPP_ERR_DEVICE;
+        if (!rc && bad != ~0ull) {
+          if (bad_index) *bad_index = (size_t)bad;
+          ctx->err = "invalid ristretto encoding at index " + std::to_string(bad);
+          rc = BPP_ERR_DECOMPRESS;
+        }
       }
     }
-  }
-  if (rc) {
-    hipFree(P->d);
-    delete P;
-    return rc;
-  }
-  *out = P;
-  return BPP_OK;
-}
-
-int bpp_points_from_uniform(bpp_ctx* ctx, const uint8_t* bytes64, size_t n, bpp_points** out) {
-  if (!ctx || !out || (!bytes64 && n)) return BPP_ERR_ARG;
-  *out = nullptr;
-  BPP_HIP(hipSetDevice(ctx->device));
-  bpp_points* P = new bpp_points();
-  P->ctx = ctx;
-  P->n = n;
-  if (hipMalloc(&P->d, (n ? n : 1) * MSM_NIELS_WORDS * 4) != hipSuccess) {
-    delete P;
-    ctx->err = "hipMalloc point table";
-    return BPP_ERR_NOMEM;
-  }
-  if (n) {
-    void* d_in = nullptr;
-    int rc = ctx_ws(ctx, "uni_in", n * 64, &d_in);
     if (rc) {
       hipFree(P->d);
       delete P;
       return rc;
     }
-    BPP_HIP(hipMemcpyAsync(d_in, bytes64, n * 64, hipMemcpyHostToDevice, ctx->stream));
-    {
-      ProfScope ps(ctx, "from_uniform");
-      hipLaunchKernelGGL(k_from_uniform, dim3(grid_for(n, 64)), dim3(64), 0, ctx->stream, (const uint32_t*)d_in, n,
-                         P->d);
+    *out = P;
+    return BPP_OK;
+  });
+}
+
+int bpp_points_from_uniform(bpp_ctx* ctx, const uint8_t* bytes64, size_t n, bpp_points** out) {
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !out || (!bytes64 && n)) return BPP_ERR_ARG;
+    *out = nullptr;
+    BPP_HIP(hipSetDevice(ctx->device));
+    bpp_points* P = new bpp_points();
+    P->ctx = ctx;
+    P->n = n;
+    if (hipMalloc(&P->d, (n ? n : 1) * MSM_NIELS_WORDS * 4) != hipSuccess) {
+      delete P;
+      ctx->err = "hipMalloc point table";
+      return BPP_ERR_NOMEM;
     }
-    BPP_TRY(ctx_check_launch(ctx, "k_from_uniform"));
-    BPP_TRY(ctx_sync(ctx));
-  }
-  *out = P;
-  return BPP_OK;
+    if (n) {
+      void* d_in = nullptr;
+      int rc = ctx_ws(ctx, "uni_in", n * 64, &d_in);
+      if (rc) {
+        hipFree(P->d);
+        delete P;
+        return rc;
+      }
+      BPP_HIP(hipMemcpyAsync(d_in, bytes64, n * 64, hipMemcpyHostToDevice, ctx->stream));
+      {
+        ProfScope ps(ctx, "from_uniform");
+        hipLaunchKernelGGL(k_from_uniform, dim3(grid_for(n, 64)), dim3(64), 0, ctx->stream, (const uint32_t*)d_in, n,
+                           P->d);
+      }
+      BPP_TRY(ctx_check_launch(ctx, "k_from_uniform"));
+      BPP_TRY(ctx_sync(ctx));
+    }
+    *out = P;
+    return BPP_OK;
+  });
 }
 
 int bpp_points_compress(bpp_ctx* ctx, const bpp_points* pts, uint8_t* out) {
-  if (!ctx || !pts || (!out && pts->n)) return BPP_ERR_ARG;
-  if (!pts->n) return BPP_OK;
-  void* d_out = nullptr;
-  BPP_TRY(ctx_ws(ctx, "compress_out", pts->n * 32, &d_out));
-  {
-    ProfScope ps(ctx, "compress");
-    hipLaunchKernelGGL(k_compress_niels, dim3(grid_for(pts->n, 64)), dim3(64), 0, ctx->stream, pts->d, pts->n,
-                       (uint32_t*)d_out);
-  }
-  BPP_TRY(ctx_check_launch(ctx, "k_compress_niels"));
-  BPP_HIP(hipMemcpyAsync(out, d_out, pts->n * 32, hipMemcpyDeviceToHost, ctx->stream));
-  BPP_TRY(ctx_sync(ctx));
-  return BPP_OK;
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !pts || (!out && pts->n)) return BPP_ERR_ARG;
+    if (!pts->n) return BPP_OK;
+    void* d_out = nullptr;
+    BPP_TRY(ctx_ws(ctx, "compress_out", pts->n * 32, &d_out));
+    {
+      ProfScope ps(ctx, "compress");
+      hipLaunchKernelGGL(k_compress_niels, dim3(grid_for(pts->n, 64)), dim3(64), 0, ctx->stream, pts->d, pts->n,
+                         (uint32_t*)d_out);
+    }
+    BPP_TRY(ctx_check_launch(ctx, "k_compress_niels"));
+    BPP_HIP(hipMemcpyAsync(out, d_out, pts->n * 32, hipMemcpyDeviceToHost, ctx->stream));
+    BPP_TRY(ctx_sync(ctx));
+    return BPP_OK;
+  });
 }
 
 size_t bpp_points_len(const bpp_points* pts) { return pts ? pts->n : 0; }

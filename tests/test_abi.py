@@ -74,3 +74,16 @@ def test_argument_checks_without_device():
     assert lib.bpp_perm_verify_terms(job, ctypes.byref(terms)) == 0
     assert terms.value == 2 * 128 + 2
     lib.bpp_perm_verify_end(job)
+
+
+def test_host_exceptions_do_not_cross_the_abi():
+    """A host allocation sized by the caller's arguments that cannot be met
+    comes back as BPP_ERR_NOMEM (7) instead of a C++ exception unwinding
+    into the caller (bpp_guard, csrc/ctx.h)."""
+    from bpperm import _lib
+    lib = ctypes.CDLL(str(_lib.LIB_PATH))
+    job = ctypes.c_void_p()
+    buf = ctypes.create_string_buffer(64)
+    rc = lib.bpp_perm_verify_begin(ctypes.c_uint32(52), ctypes.c_size_t(1 << 40), None, ctypes.c_size_t(0), buf,
+                                   buf, None, ctypes.byref(job))
+    assert rc == 7 and not job.value

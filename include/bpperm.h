@@ -44,6 +44,9 @@
 extern "C" {
 #endif
 
+/* Return codes.  No C++ exception leaves the library: a host allocation that
+ * cannot be met returns BPP_ERR_NOMEM, any other internal exception
+ * BPP_ERR_DEVICE (text in bpp_ctx_last_error when the call has a context). */
 enum {
   BPP_OK = 0,
   BPP_ERR_ARG = 1,

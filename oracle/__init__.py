@@ -10,6 +10,9 @@ vendored under /root/reference (pins from `bp-perm/Cargo.lock`):
   * bulletproofs 4.0.0 — PedersenGens, BulletproofGens (GeneratorsChain),
     InnerProductProof create / verify.
 
+`compat.py` restates the reference's own driver (test_first) as written,
+defects included (compat mode; test-only).
+
 Only `tests/`, `__graft_entry__.smoke()` and `bench.py`'s `cpu_baseline` leg
 may import anything from here, and only as the checker.  The product path
 (`bulletproof-perm_amd/`) never imports, links or executes this package.

@@ -140,7 +140,10 @@ __global__ void k_msm_scatter(const uint32_t* __restrict__ scalars, const uint32
 // without the bound the post-barrier fold lifts the kernel to 187 VGPRs.
 // (3 waves, with or without a software-pipelined row gather, measured equal
 // alone and slower in the pipelined stream: DESIGN.md §4)
-#define ACC_ATTR __attribute__((amdgpu_waves_per_eu(4, 8)))
+#ifndef ACC_WPE
+#define ACC_WPE 4
+#endif
+#define ACC_ATTR __attribute__((amdgpu_waves_per_eu(ACC_WPE, 8)))
 
 // Largest b with boff[b] <= i (boff non-decreasing, boff[0] = 0, i < boff[nb]).
 FE_INLINE uint32_t bucket_of(const uint32_t* __restrict__ boff, uint32_t nb, uint32_t i) {

@@ -159,7 +159,11 @@ FE_INLINE uint32_t bucket_of(const uint32_t* __restrict__ boff, uint32_t nb, uin
 // branch measured 1.5 % faster than ge_madd_signed's operand selects).
 FE_INLINE ge_niels fetch_entry(const uint32_t* __restrict__ tbl, const uint32_t* __restrict__ tbl1, uint32_t n0,
                                uint32_t e) {
+#ifdef EXP_ACC_L2ROWS  // timing experiment only (wrong results): every gather from 1024 L2-resident rows
+  const uint32_t pi = e & 0x3ffu;
+#else
   const uint32_t pi = e & 0x7fffffffu;
+#endif
   ge_niels q = pi < n0 ? load_niels(tbl, pi) : load_niels(tbl1, pi - n0);
   if (e & 0x80000000u) q = ge_niels_neg(q);
   return q;

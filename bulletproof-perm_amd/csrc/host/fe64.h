@@ -7,6 +7,7 @@
 // and of the oracle's C port.
 #pragma once
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <vector>
@@ -343,6 +344,19 @@ static inline void encode_double_batch(const ge* pts, size_t n, uint8_t* out) {
     if (fe_isneg(fe_mul(x, z_inv))) y = fe_neg(y);
     fe_to_bytes(o, fe_abs(fe_mul(den_inv, fe_sub(q.Z, y))));
   }
+}
+
+// The same on eight points per AVX-512 IFMA vector (host/encode_x8.cpp;
+// byte-identical).  encode_double_batch_auto takes it when the CPU has IFMA
+// and BPP_HOST_IFMA is not 0.
+bool encode_x8_available();
+void encode_double_batch_x8(const ge* pts, size_t n, uint8_t* out);
+static inline void encode_double_batch_auto(const ge* pts, size_t n, uint8_t* out) {
+  const char* e = getenv("BPP_HOST_IFMA");
+  if (n >= 8 && encode_x8_available() && !(e && e[0] == '0'))
+    encode_double_batch_x8(pts, n, out);
+  else
+    encode_double_batch(pts, n, out);
 }
 
 static inline bool decode(ge& out, const uint8_t in[32]) {

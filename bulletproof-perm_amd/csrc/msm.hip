@@ -592,7 +592,7 @@ int bpp_points_double_compress(const uint8_t* raw, size_t count, uint8_t* out) {
       memcpy(w, raw + 128 * i, 128);
       pts[i] = h25519::ge_from_words(w);
     }
-    h25519::encode_double_batch(pts.data(), count, out);
+    h25519::encode_double_batch_auto(pts.data(), count, out);
     return BPP_OK;
   });
 }
@@ -884,7 +884,7 @@ int msm_multi_enc(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, 
   std::vector<h25519::ge> res;
   BPP_TRY(msm_multi(ctx, d_scal, d_pidx, off, pts, res));
   if (doubled)
-    h25519::encode_double_batch(res.data(), M, out_enc);
+    h25519::encode_double_batch_auto(res.data(), M, out_enc);
   else
     for (uint32_t m = 0; m < M; ++m) h25519::encode(out_enc + 32 * (size_t)m, res[m]);
   return BPP_OK;

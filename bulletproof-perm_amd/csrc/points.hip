@@ -109,7 +109,7 @@ int points_double_encode_host(bpp_ctx* ctx, const uint32_t* raw, size_t n, uint8
     const size_t b = n * c / chunks, e = n * (c + 1) / chunks;
     std::vector<h25519::ge> pts(e - b);
     for (size_t i = b; i < e; ++i) pts[i - b] = h25519::ge_from_dev(raw + i * P3_WORDS);
-    h25519::encode_double_batch(pts.data(), e - b, out_host + 32 * b);
+    h25519::encode_double_batch_auto(pts.data(), e - b, out_host + 32 * b);
   });
   return BPP_OK;
 }

@@ -43,3 +43,22 @@ def test_double_compress_torsion_and_identity():
 def test_double_compress_empty():
     import bpperm
     assert bpperm.double_compress([]) == []
+
+
+def test_ifma_path_matches_scalar(monkeypatch):
+    """The 8-way AVX-512 IFMA batch encoder (host/encode_x8.cpp) against the
+    scalar one (BPP_HOST_IFMA=0) on every batch length 1..40 (padded last
+    vector, below-8 batches on the scalar path) with identity-torsion lanes
+    (W = 0) mixed into the vectors; both against the oracle."""
+    import bpperm
+    tors = [(0, 1, 1, 0), (0, R.P - 1, 1, 0), (R.SQRT_M1, 0, 1, 0)]
+    pts = _rand_points(37, 13)
+    pts = pts[:5] + tors[:1] + pts[5:20] + tors[1:] + pts[20:]
+    raw = [R.raw_point_bytes(p) for p in pts]
+    want = [R.encode(R.ed_double(p)) if i not in (5, 21, 22) else bytes(32) for i, p in enumerate(pts)]
+    for n in range(1, len(pts) + 1):
+        monkeypatch.setenv("BPP_HOST_IFMA", "1")
+        fast = bpperm.double_compress(raw[:n])
+        monkeypatch.setenv("BPP_HOST_IFMA", "0")
+        slow = bpperm.double_compress(raw[:n])
+        assert fast == slow == want[:n], n

@@ -14,6 +14,8 @@ if os.environ.get("WITH_TORCH"):
     import torch
 import bpperm  # noqa: E402
 
+if os.environ.get("HOST_TUNING", "1") != "0":  # as bench.py (bpp_host_tuning); HOST_TUNING=0 leaves malloc alone
+    bpperm.host_tuning(malloc=True)
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 128
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 6

@@ -381,23 +381,14 @@ static inline bool decode(ge& out, const uint8_t in[32]) {
 }
 
 // Device element: 10 u32 limbs at bit offsets ceil(25.5 i) (limbs may
-// exceed their nominal width; see csrc/fe25519.cuh) -> loose fe.
+// exceed their nominal width; see csrc/fe25519.cuh) -> loose fe.  Limb pair
+// (2k, 2k + 1) sits at offsets 51k and 51k + 26, so radix-2^51 limb k is
+// w[2k] + w[2k+1] 2^26 (< 2^59), and one carry pass (2^255 = 19) leaves the
+// same value mod p in carried limbs.
 static inline fe fe_from_dev(const uint32_t w[10]) {
-  static const int OFF[10] = {0, 26, 51, 77, 102, 128, 153, 179, 204, 230};
-  uint64_t t[5] = {0, 0, 0, 0, 0};
-  for (int i = 0; i < 10; ++i) {
-    const int q = OFF[i] >> 6, s = OFF[i] & 63;
-    const u128 x = (u128)w[i] << s;
-    u128 c = (u128)t[q] + (uint64_t)x;
-    t[q] = (uint64_t)c;
-    c = (u128)t[q + 1] + (uint64_t)(x >> 64) + (uint64_t)(c >> 64);
-    t[q + 1] = (uint64_t)c;
-    for (int k = q + 2; k < 5 && (c >> 64); ++k) {
-      c = (u128)t[k] + (uint64_t)(c >> 64);
-      t[k] = (uint64_t)c;
-    }
-  }
-  return fe_from_u256(t, t[4]);
+  fe r;
+  for (int k = 0; k < 5; ++k) r.v[k] = (uint64_t)w[2 * k] + ((uint64_t)w[2 * k + 1] << 26);
+  return fe_carry(r);
 }
 // device extended point (40 words, csrc/layout.h P3_WORDS) -> host point
 static inline ge ge_from_dev(const uint32_t* w) {

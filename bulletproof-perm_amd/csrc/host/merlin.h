@@ -275,9 +275,23 @@ struct TranscriptX8 {
     pos_begin = 0;
   }
   // d[j] = instance j's bytes (stride 0 when `same`: one buffer for all)
+  // (whole 64-bit words of the state where pos is word-aligned: a 32-byte
+  // point is mostly four word XORs per lane instead of 32 byte XORs)
   void absorb(const uint8_t* const d[8], size_t n) {
-    for (size_t i = 0; i < n; ++i) {
+    for (size_t i = 0; i < n;) {
+      if ((pos & 7) == 0 && n - i >= 8 && pos + 8 <= STROBE_R) {
+        uint64_t* row = L[pos >> 3];
+        for (int j = 0; j < 8; ++j) {
+          uint64_t x;
+          memcpy(&x, d[j] + i, 8);
+          row[j] ^= x;
+        }
+        i += 8;
+        pos += 8;  // (STROBE_R = 166 is not a multiple of 8: the last 6 bytes go below)
+        continue;
+      }
       for (int j = 0; j < 8; ++j) byte(j, pos) ^= d[j][i];
+      ++i;
       if (++pos == STROBE_R) run_f();
     }
   }
@@ -286,11 +300,22 @@ struct TranscriptX8 {
     absorb(dd, n);
   }
   void squeeze(uint8_t* const d[8], size_t n) {
-    for (size_t i = 0; i < n; ++i) {
+    for (size_t i = 0; i < n;) {
+      if ((pos & 7) == 0 && n - i >= 8 && pos + 8 <= STROBE_R) {
+        uint64_t* row = L[pos >> 3];
+        for (int j = 0; j < 8; ++j) {
+          memcpy(d[j] + i, &row[j], 8);
+          row[j] = 0;
+        }
+        i += 8;
+        pos += 8;
+        continue;
+      }
       for (int j = 0; j < 8; ++j) {
         d[j][i] = byte(j, pos);
         byte(j, pos) = 0;
       }
+      ++i;
       if (++pos == STROBE_R) run_f();
     }
   }

@@ -85,8 +85,9 @@ int bpp_ctx_work_get(bpp_ctx* ctx, const char* name, uint64_t* value);
 void bpp_ctx_work_reset(bpp_ctx* ctx);
 
 /* Opt-in host-process tuning (process-wide, so never done implicitly):
- * BPP_TUNE_MALLOC fixes glibc's mmap threshold at 64 MB and disables heap
- * trimming, which keeps the prover's per-batch host vectors in the arenas
+ * BPP_TUNE_MALLOC fixes glibc's mmap threshold at 64 MB, disables heap
+ * trimming and pads arena growth by 64 MB, which keeps the prover's
+ * per-batch host vectors in the arenas
  * (measured in a host profile of 8 batches in flight).
  * BPP_ERR_ARG for unknown flags. */
 #define BPP_TUNE_MALLOC 1u

@@ -117,12 +117,15 @@ def test_msm_async_submit_collect(ctx, big_table):
     ctx.dev_free(db)
 
 
-def test_msm_submit_host_scalars(ctx, big_table):
+@pytest.mark.parametrize("up_streams", ["0", "2"])
+def test_msm_submit_host_scalars(ctx, big_table, monkeypatch, up_streams):
     """bpp_msm_submit_host (host scalars, the reference's call shape): from
-    pinned memory (the H2D copy on the MSM's own stream) and from pageable
-    bytes (staged), several in flight, a window range; all equal the
+    pinned memory (the H2D copy on the MSM's own stream, or split over two
+    upload streams the MSM's stream waits for: BPP_MSM_UP_STREAMS) and from
+    pageable bytes (staged), several in flight, a window range; all equal the
     resident-scalar MSM and the C port."""
     import ctypes
+    monkeypatch.setenv("BPP_MSM_UP_STREAMS", up_streams)
 
     import bpperm
     from bpperm import dist as bdist

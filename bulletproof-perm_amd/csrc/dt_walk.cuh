@@ -23,14 +23,24 @@ struct DtGeom {
 // a fourth spilled 124 B per lane and measured 104-120 K vs 147-151 K
 // proofs/s at 12 batches in flight)
 
-// Term groups per block (TG, lanes = TG * W): at most DT_NT_MAX / W, fewer
-// for short MSMs; BPP_DT_TG_MAX caps it (an A/B switch: fewer lanes per MSM
-// means a shallower block tree and less issue per MSM, but fewer waves).
-static inline uint32_t dt_term_groups(uint32_t W, double terms_per_msm) {
+// Term groups per block (TG, lanes = TG * W) for a launch of `nmsm` MSMs:
+// at most DT_TG_DEFAULT (8: 128 lanes at c = 16) when the launch has blocks
+// enough to fill the device (>= 256 MSMs; a few long MSMs keep 16 groups for
+// latency), fewer for short MSMs; BPP_DT_TG_MAX overrides the cap (an A/B
+// switch).  Fewer lanes per MSM mean a shallower block tree and
+// less issue per MSM but a longer walk per lane.  256-proof batches, 52-card
+// proofs (tools/prove_inflight_exp.py): at 12 in flight with the host the
+// bottleneck, 16 / 8 / 4 / 2 groups measured 263-265 / 265 / 244 / 168-171 K
+// proofs/s; once the IFMA host encoder made the prover GPU-bound (16 in
+// flight), 8 groups beat 16 in three of three interleaved pairs (321-324 vs
+// 310-317 K) and 4 lost (285-287 K).
+#define DT_TG_DEFAULT 8
+static inline uint32_t dt_term_groups(uint32_t W, double terms_per_msm, uint32_t nmsm) {
   uint32_t TG = DT_NT_MAX / W;
+  if (nmsm >= 256 && TG > DT_TG_DEFAULT) TG = DT_TG_DEFAULT;
   if (const char* e = getenv("BPP_DT_TG_MAX")) {
     const int v = atoi(e);
-    if (v >= 1 && (uint32_t)v < TG) TG = (uint32_t)v;
+    if (v >= 1 && (uint32_t)v <= DT_NT_MAX / W) TG = (uint32_t)v;
   }
   while (TG > 1 && terms_per_msm < 2.0 * TG) TG >>= 1;
   return TG;

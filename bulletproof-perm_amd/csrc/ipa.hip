@@ -442,7 +442,7 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
     }
     BPP_TRY(ctx_ws(ctx, "ipa_res", (size_t)2 * P * P3_BYTES, &d_res));
     dg = dt_geom(g.pts.dt_c);
-    TG = dt_term_groups(dg.W, (double)(n + 1));  // as msm_multi_dt_dev for (n + 1)-term MSMs
+    TG = dt_term_groups(dg.W, (double)(n + 1), 2 * P);  // as msm_multi_dt_dev for (n + 1)-term MSMs
     nt = TG * dg.W;
   }
   // Device transcript path (an A/B experiment: see

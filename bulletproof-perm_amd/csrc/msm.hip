@@ -792,7 +792,7 @@ static int msm_multi_dt_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t
   // a shallower tree); ~512 lanes measured slower at 8 proof batches in
   // flight
   const double t_avg = (double)T / (double)M;
-  const uint32_t TG = dt_term_groups(dg.W, t_avg);
+  const uint32_t TG = dt_term_groups(dg.W, t_avg, M);
   const uint32_t nt = TG * dg.W;
   ctx_work(ctx, "msm_terms", T);
   ctx_work(ctx, "madds", (uint64_t)T * dg.W);

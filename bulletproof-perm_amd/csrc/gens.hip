@@ -74,7 +74,7 @@ __global__ void __launch_bounds__(64) k_fb_tables(const uint32_t* __restrict__ t
 template <int G>
 __global__ void __launch_bounds__(PED_T) k_pedersen(const uint32_t* __restrict__ fb, const uint32_t* __restrict__ v,
                                                     const uint32_t* __restrict__ gam, size_t m, uint32_t v_groups,
-                                                    uint32_t* __restrict__ part) {
+                                                    uint32_t v_npos, uint32_t* __restrict__ part) {
   constexpr uint32_t PED_GPOS = FB_POS / G;    // positions per group
   constexpr uint32_t PED_ROWS = 2 * PED_GPOS * 8;  // table rows one block needs
   __shared__ __attribute__((aligned(16))) uint32_t rows[PED_ROWS * MSM_NIELS_WORDS];
@@ -102,7 +102,9 @@ __global__ void __launch_bounds__(PED_T) k_pedersen(const uint32_t* __restrict__
       c >>= 32;
     }
     word >>= sh;
-    _Pragma("unroll 1") for (uint32_t b = 0; b < PED_GPOS; ++b) {
+    // (v: only the positions the public bound can reach, v_npos <= PED_GPOS)
+    const uint32_t npos = which == 0 ? v_npos : PED_GPOS;
+    _Pragma("unroll 1") for (uint32_t b = 0; b < npos; ++b) {
       const int nib = (int)((word >> (4 * b)) & 15u);
       const int d = PED_GPOS * g + b < FB_POS - 1 ? nib - 8 : nib;
       const int sg = d >> 31;  // 0 or -1
@@ -196,9 +198,19 @@ int pedersen_dev(bpp_ctx* ctx, const bpp_gens* g, const uint32_t* d_v, const uin
   const uint32_t PG = FB_POS / G;
   const uint64_t v_lim = PG < 16 ? (7 * (1ull << (4 * PG)) + 8) / 15 : 0;
   const uint32_t v_groups = v_bound && v_bound <= v_lim ? 1u : G;
+  // and within group 0 only the first v_npos positions: the least P' with
+  // v_bound < (7 16^P' + 8) / 15 (e.g. 2 for the 52-card values <= 53,
+  // 8 + 2 instead of 8 + 8 additions for v; still fixed by k alone)
+  uint32_t v_npos = PG;
+  if (v_groups == 1)
+    for (uint32_t q = 1; q < PG; ++q)
+      if (v_bound <= (7 * (1ull << (4 * q)) + 8) / 15) {
+        v_npos = q;
+        break;
+      }
   ctx_work(ctx, "msm_terms", 2 * (uint64_t)m);
   // constant time: every position of gamma, every possible position of v
-  ctx_work(ctx, "madds", (uint64_t)(FB_POS + FB_POS / G * v_groups) * m);
+  ctx_work(ctx, "madds", (uint64_t)(FB_POS + (v_groups == 1 ? v_npos : FB_POS)) * m);
   ctx_work(ctx, "padds", (uint64_t)(G - 1) * m);
   ctx_work(ctx, "msm_launches", 1);
   void* part = nullptr;
@@ -207,12 +219,12 @@ int pedersen_dev(bpp_ctx* ctx, const bpp_gens* g, const uint32_t* d_v, const uin
     ProfScope ps(ctx, "pedersen");
     if (G == 32) {
       hipLaunchKernelGGL(k_pedersen<32>, dim3(grid_for(m, PED_T), 32), dim3(PED_T), 0, ctx->stream, g->d_fb, d_v,
-                         d_gam, m, v_groups, (uint32_t*)part);
+                         d_gam, m, v_groups, v_npos, (uint32_t*)part);
       hipLaunchKernelGGL(k_pedersen_sum<32>, dim3(grid_for(m * 32, 256)), dim3(256), 0, ctx->stream,
                          (const uint32_t*)part, m, p3);
     } else {
       hipLaunchKernelGGL(k_pedersen<8>, dim3(grid_for(m, PED_T), 8), dim3(PED_T), 0, ctx->stream, g->d_fb, d_v,
-                         d_gam, m, v_groups, (uint32_t*)part);
+                         d_gam, m, v_groups, v_npos, (uint32_t*)part);
       hipLaunchKernelGGL(k_pedersen_sum<8>, dim3(grid_for(m * 8, 256)), dim3(256), 0, ctx->stream,
                          (const uint32_t*)part, m, p3);
     }

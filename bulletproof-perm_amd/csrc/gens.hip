@@ -67,7 +67,7 @@ __global__ void __launch_bounds__(64) k_fb_tables(const uint32_t* __restrict__ t
 // commitments' values 1..k and pi + 1 <= k: their digits beyond group 0 are
 // all zero for every v under the bound, so skipping those groups depends on
 // k only, not on the secret values -- 72 instead of 128 table additions per
-// V commitment at G = 8).  (Spreading v's P positions one per group, so no
+// V commitment at G = 8, 66 with v_npos below).  (Spreading v's P positions one per group, so no
 // group adds more than P + 1 rows, measured slower: 124 vs 117 us alone and
 // 206-218 K vs 208-222 K proofs/s at 256 x 8 -- the blocks are scheduled
 // dynamically, so group 0's longer blocks were not the kernel's tail.)

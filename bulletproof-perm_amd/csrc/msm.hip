@@ -91,7 +91,7 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
   BPP_TRY(ctx_ws(ctx, "msm_cnt", (NB + 1) * 4, &cnt));
   BPP_TRY(ctx_ws(ctx, "msm_cur", NB * 4, &cur));
   BPP_TRY(ctx_ws(ctx, "msm_boff", (NB + 1) * 4, &boff));
-  BPP_TRY(ctx_ws(ctx, "msm_entries", (size_t)T * Wn * 4 + 16, &entries));  // +16: 16-B reads past the end
+  BPP_TRY(ctx_ws(ctx, "msm_entries", (size_t)T * Wn * 4 + 48, &entries));  // +48: 16-B reads (and the next group's) past the end
   BPP_TRY(ctx_ws(ctx, "msm_bsum", NB * P3_BYTES, &bsum));
   BPP_TRY(ctx_ws(ctx, "msm_wsum", nseg * P3_BYTES, &wsum));
   // (tmpA packs the point index in 24 bits)

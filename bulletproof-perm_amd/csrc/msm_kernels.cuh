@@ -226,8 +226,25 @@ __global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_
     // loads touch the same 128-B line K times across a long loop and
     // re-fetch it once the table gathers have evicted it
     uint4 e4 = make_uint4(0, 0, 0, 0);
+#ifndef EXP_ACC_BOFF_CHAIN
+    // end of bucket b + 1, loaded one bucket ahead: when b closes, the next
+    // bucket (almost always non-empty: ~32 entries each at 2^20) starts at
+    // bend and ends at nbend, so the wave does not wait on dependent boff
+    // loads in the iteration that closes a run
+    uint32_t nbend = boff[min(b + 2, nbuckets)];
+#endif
+#ifdef EXP_ACC_E4_NEXT
+    uint4 e4n = *reinterpret_cast<const uint4*>(entries + i0);
+#endif
     for (uint32_t i = i0; i < i1; ++i) {
+#ifdef EXP_ACC_E4_NEXT
+      if (((i - i0) & 3u) == 0) {
+        e4 = e4n;
+        e4n = *reinterpret_cast<const uint4*>(entries + i + 4);
+      }
+#else
       if (((i - i0) & 3u) == 0) e4 = *reinterpret_cast<const uint4*>(entries + i);
+#endif
       const uint32_t q = (i - i0) & 3u;
       const uint32_t e = q == 0 ? e4.x : q == 1 ? e4.y : q == 2 ? e4.z : e4.w;
       if (i == bend) {  // close the run of bucket b
@@ -236,9 +253,22 @@ __global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_
         } else {
           park(acc, bstart, bend);  // first run, bucket started earlier
         }
+#ifndef EXP_ACC_BOFF_CHAIN
+        if (nbend > i) {  // bucket b + 1 is non-empty
+          ++b;
+          bstart = i;
+          bend = nbend;
+        } else {  // skip empty buckets
+          do { ++b; } while (boff[b + 1] <= i);
+          bstart = boff[b];
+          bend = boff[b + 1];
+        }
+        nbend = boff[min(b + 2, nbuckets)];
+#else
         do { ++b; } while (boff[b + 1] <= i);
         bstart = boff[b];
         bend = boff[b + 1];
+#endif
         if (((bend - 1) >> ks) - l >= FIX_MAX) heavy[1 + atomicAdd(&heavy[0], 1u)] = b;
         acc = ge_identity();
       }

@@ -233,18 +233,8 @@ __global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_
     // loads in the iteration that closes a run
     uint32_t nbend = boff[min(b + 2, nbuckets)];
 #endif
-#ifdef EXP_ACC_E4_NEXT
-    uint4 e4n = *reinterpret_cast<const uint4*>(entries + i0);
-#endif
     for (uint32_t i = i0; i < i1; ++i) {
-#ifdef EXP_ACC_E4_NEXT
-      if (((i - i0) & 3u) == 0) {
-        e4 = e4n;
-        e4n = *reinterpret_cast<const uint4*>(entries + i + 4);
-      }
-#else
       if (((i - i0) & 3u) == 0) e4 = *reinterpret_cast<const uint4*>(entries + i);
-#endif
       const uint32_t q = (i - i0) & 3u;
       const uint32_t e = q == 0 ? e4.x : q == 1 ? e4.y : q == 2 ? e4.z : e4.w;
       if (i == bend) {  // close the run of bucket b

@@ -58,7 +58,7 @@ static int upload_offsets(bpp_ctx* ctx, const std::vector<uint32_t>& off, void**
 
 int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const uint32_t* d_off, uint32_t M,
                uint32_t T, uint32_t c, uint32_t wb, uint32_t Wn, const uint32_t* d_tbl, uint32_t** d_wsum_out,
-               const uint32_t* d_tbl1, uint32_t n0, bool fb, uint32_t* terms_out) {
+               const uint32_t* d_tbl1, uint32_t n0, bool fb, uint32_t* terms_out, uint32_t rlog) {
   if (terms_out) *terms_out = 1;
   MsmGeom g;
   g.M = M;
@@ -218,9 +218,11 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
                          (const uint32_t*)heavy, (uint32_t*)bsum);
     }
     BPP_TRY(ctx_check_launch(ctx, "k_msm_fixup_heavy"));
-    if (terms_out && M == 1 && !fb && g.B >= (1u << RWAVE_SHIFT) && g.B <= (64u << RWAVE_SHIFT)) {
+    if (rlog != RWAVE_LOG && rlog != RWAVE_LOG_LONE) rlog = RWAVE_LOG;
+    const uint32_t rshift = rlog + 6;
+    if (terms_out && M == 1 && !fb && g.B >= (1u << rshift) && g.B <= ((uint32_t)RWAVE_NW_MAX << rshift)) {
       // power-of-two weights left to the host Horner (k_msm_reduce_wave)
-      const uint32_t nw = g.B >> RWAVE_SHIFT;
+      const uint32_t nw = g.B >> rshift;
       uint32_t J = 0;
       while ((1u << J) < nw) ++J;
       void* part = nullptr;
@@ -228,11 +230,19 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
       BPP_TRY(ctx_ws(ctx, "msm_wsum_terms", nseg * (1 + J) * P3_BYTES, &wsum));
       ProfScope ps(ctx, "msm_reduce");
 #ifndef EXP_NO_REDUCE  // (timing experiment only: results are wrong without it)
-      hipLaunchKernelGGL(k_msm_reduce_wave, dim3((unsigned)(nseg * nw)), dim3(64), 0, ctx->stream,
-                         (const uint32_t*)boff, ks, (const uint32_t*)head, (const uint32_t*)tail, (const uint32_t*)bsum,
-                         g, (uint32_t*)part);
-      hipLaunchKernelGGL(k_msm_reduce_bits, dim3((unsigned)(nseg * (1 + J))), dim3(64), 0, ctx->stream,
-                         (const uint32_t*)part, g, 1 + J, (uint32_t*)wsum);
+      if (rlog == RWAVE_LOG) {
+        hipLaunchKernelGGL(k_msm_reduce_wave<RWAVE_LOG>, dim3((unsigned)(nseg * nw)), dim3(64), 0, ctx->stream,
+                           (const uint32_t*)boff, ks, (const uint32_t*)head, (const uint32_t*)tail,
+                           (const uint32_t*)bsum, g, (uint32_t*)part);
+        hipLaunchKernelGGL(k_msm_reduce_bits<RWAVE_LOG>, dim3((unsigned)(nseg * (1 + J))), dim3(64), 0, ctx->stream,
+                           (const uint32_t*)part, g, 1 + J, (uint32_t*)wsum);
+      } else {
+        hipLaunchKernelGGL(k_msm_reduce_wave<RWAVE_LOG_LONE>, dim3((unsigned)(nseg * nw)), dim3(64), 0, ctx->stream,
+                           (const uint32_t*)boff, ks, (const uint32_t*)head, (const uint32_t*)tail,
+                           (const uint32_t*)bsum, g, (uint32_t*)part);
+        hipLaunchKernelGGL(k_msm_reduce_bits<RWAVE_LOG_LONE>, dim3((unsigned)(nseg * (1 + J))), dim3(64), 0,
+                           ctx->stream, (const uint32_t*)part, g, 1 + J, (uint32_t*)wsum);
+      }
 #endif
       BPP_TRY(ctx_check_launch(ctx, "k_msm_reduce_wave/bits"));
       *terms_out = 1 + J;
@@ -256,17 +266,18 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
   return BPP_OK;
 }
 
-// Window j = term 0 + sum_k 2^(RWAVE_SHIFT + k) term 1+k: one Horner pass
+// Window j = term 0 + sum_k 2^(rshift + k) term 1+k: one Horner pass
 // over all terms in descending bit position (the term offsets < c fall
 // between the doublings the window combine does anyway).
-h25519::ge horner_host_terms(const uint32_t* ws_words, uint32_t Wn, uint32_t nterms, uint32_t c, uint32_t wb) {
+h25519::ge horner_host_terms(const uint32_t* ws_words, uint32_t Wn, uint32_t nterms, uint32_t c, uint32_t wb,
+                             uint32_t rshift) {
   using namespace h25519;
   ge acc = ge_identity();
   bool started = false;
   uint32_t pos = 0;  // bit position acc is currently scaled to
   for (int j = (int)Wn - 1; j >= 0; --j) {
     for (int k = (int)nterms - 1; k >= 0; --k) {
-      const uint32_t off = c * (uint32_t)j + (k ? RWAVE_SHIFT + (uint32_t)(k - 1) : 0u);
+      const uint32_t off = c * (uint32_t)j + (k ? rshift + (uint32_t)(k - 1) : 0u);
       const ge v = ge_from_dev(ws_words + ((size_t)j * nterms + (size_t)k) * P3_WORDS);
       if (started)
         for (; pos > off; --pos) acc = ge_dbl(acc);
@@ -290,15 +301,21 @@ int msm_single_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx,
   // (window groups pipelined over two child streams measured slower: G = 2
   // 1.38 ms, G = 4 1.70 ms vs 1.26 ms at 2^20 -- the reduce and fixup are
   // latency-bound and would run G times)
+  // alone on the device: the latency-shaped bucket reduction (RWAVE_LOG_LONE;
+  // BPP_MSM_LONE_RLOG=4 selects the stream shape, for A/B runs)
+  static const uint32_t rlog = [] {
+    const char* e = getenv("BPP_MSM_LONE_RLOG");
+    return (e && atoi(e) == RWAVE_LOG) ? (uint32_t)RWAVE_LOG : (uint32_t)RWAVE_LOG_LONE;
+  }();
   uint32_t* d_ws = nullptr;
   uint32_t nterms = 1;
   BPP_TRY(msm_engine(ctx, d_scal, d_pidx, nullptr, 1, (uint32_t)n, c, wb, Wn, d_tbl, &d_ws, d_tbl1, n0, false,
-                     &nterms));
+                     &nterms, rlog));
   void* h = nullptr;
   BPP_TRY(ctx_pinned(ctx, (size_t)Wn * nterms * P3_BYTES, &h));
   BPP_HIP(hipMemcpyAsync(h, d_ws, (size_t)Wn * nterms * P3_BYTES, hipMemcpyDeviceToHost, ctx->stream));
   BPP_TRY(ctx_sync(ctx));
-  *out = horner_host_terms((const uint32_t*)h, Wn, nterms, c, wb);
+  *out = horner_host_terms((const uint32_t*)h, Wn, nterms, c, wb, rlog + 6);
   return BPP_OK;
 }
 

@@ -6,18 +6,27 @@
 #include "host/fe64.h"
 
 bool scalar_is_canonical(const uint8_t* s);
+// Buckets per lane of the single-MSM bucket reduction (k_msm_reduce_wave):
+// 2^RWAVE_LOG in MSM streams, 2^RWAVE_LOG_LONE for an MSM that runs alone
+#ifndef RWAVE_LOG
+#define RWAVE_LOG 4
+#endif
+#ifndef RWAVE_LOG_LONE
+#define RWAVE_LOG_LONE 2
+#endif
 uint32_t msm_choose_c(double n_per_msm);
 // Runs K1..K5 for M MSMs over T terms; returns the device array of M*Wn
 // window sums (extended points, 32 words each).
 int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const uint32_t* d_off, uint32_t M,
                uint32_t T, uint32_t c, uint32_t wb, uint32_t Wn, const uint32_t* d_tbl, uint32_t** d_wsum_out,
                const uint32_t* d_tbl1 = nullptr, uint32_t n0 = 0xffffffffu, bool fb = false,
-               uint32_t* terms_out = nullptr);
+               uint32_t* terms_out = nullptr, uint32_t rlog = RWAVE_LOG);
 // With terms_out (single MSMs only) the engine may return, per window, 1 + J
-// terms instead of one sum: the window sum is term 0 + sum_j 2^(9+j) term 1+j
-// (k_msm_reduce_wave); *terms_out = terms per window (1 = plain sums).
+// terms instead of one sum: the window sum is term 0 + sum_j 2^(rlog+6+j)
+// term 1+j (k_msm_reduce_wave); *terms_out = terms per window (1 = plain sums).
 // Host Horner over such terms: sum_j 2^(c (wb + j)) * window_j.
-h25519::ge horner_host_terms(const uint32_t* ws_words, uint32_t Wn, uint32_t nterms, uint32_t c, uint32_t wb);
+h25519::ge horner_host_terms(const uint32_t* ws_words, uint32_t Wn, uint32_t nterms, uint32_t c, uint32_t wb,
+                             uint32_t rshift = RWAVE_LOG + 6);
 int msm_single_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const uint32_t* d_tbl, size_t n,
                    uint32_t c, uint32_t wb, uint32_t Wn, h25519::ge* out, const uint32_t* d_tbl1 = nullptr,
                    uint32_t n0 = 0xffffffffu);

@@ -400,35 +400,43 @@ __global__ void __launch_bounds__(RED_T) k_msm_reduce_final(const uint32_t* __re
 //   6-step butterfly; writes V_w = sum_t v and R_w.
 // k_msm_reduce_bits: one wave per (segment, term): term 0 is X = sum_w V_w,
 //   term 1 + j is Y_j = sum_{w : bit j of w} R_w, so that
-//   sum_b (b+1) S_b = X + sum_j 2^(RWAVE_SHIFT+j) Y_j (horner_host_terms).
-// L = 16 (32 waves per 2^15-bucket window): 2^20 three in flight 0.888 /
+//   sum_b (b+1) S_b = X + sum_j 2^(log2(64 L)+j) Y_j (horner_host_terms).
+// In a stream of MSMs (bpp_msm_submit) L = 16 (32 waves per 2^15-bucket window): 2^20 three in flight 0.888 /
 // 0.892 ms per MSM against 0.913 / 0.899 at L = 8 (whose reduce costs more
 // issue slots: 12 scan / butterfly additions per 8 buckets instead of per
 // 16); alone the reduce takes 0.233 vs 0.170 ms and L = 32 0.339 ms
-// (0.899 / 0.904 pipelined).
+// (0.899 / 0.904 pipelined).  An MSM that runs alone (bpp_msm, the verifier's
+// single MSM) has idle SIMDs to spare and uses L = 4: four times the waves,
+// half the serial chain (msm_single_dev).
 #ifndef RWAVE_LOG
-#define RWAVE_LOG 4  // log2 buckets per lane
+#define RWAVE_LOG 4  // log2 buckets per lane (MSM streams)
+#endif
+#ifndef RWAVE_LOG_LONE
+#define RWAVE_LOG_LONE 2  // log2 buckets per lane when the MSM runs alone (latency)
 #endif
 #define RWAVE_L (1 << RWAVE_LOG)
 #define RWAVE_SHIFT (RWAVE_LOG + 6)  // log2(RWAVE_L * 64)
+#define RWAVE_NW_MAX 256             // waves per segment k_msm_reduce_bits folds
+template <int LOG>
 __global__ void __launch_bounds__(64) k_msm_reduce_wave(const uint32_t* __restrict__ boff, uint32_t ks,
                                                        const uint32_t* __restrict__ head,
                                                        const uint32_t* __restrict__ tail,
                                                        const uint32_t* __restrict__ bsum, MsmGeom g,
                                                        uint32_t* __restrict__ part) {
-  const uint32_t nw = g.B >> RWAVE_SHIFT;
+  constexpr uint32_t L = 1u << LOG;
+  const uint32_t nw = g.B >> (LOG + 6);
   const uint32_t seg = blockIdx.x / nw, w = blockIdx.x % nw;
   const uint32_t t = threadIdx.x;
-  const uint32_t lo = (w * 64 + t) * RWAVE_L;
+  const uint32_t lo = (w * 64 + t) * L;
   const size_t base = (size_t)seg * g.B + lo;
-  uint32_t bo[RWAVE_L + 1];
-  _Pragma("unroll") for (uint32_t k = 0; k <= RWAVE_L; ++k) bo[k] = boff[base + k];
+  uint32_t bo[L + 1];
+  _Pragma("unroll") for (uint32_t k = 0; k <= L; ++k) bo[k] = boff[base + k];
   ge_p3 run = ge_identity();
   ge_p3 acc = ge_identity();
   // a lane whose buckets are all empty (most of the narrow top window's)
   // keeps run = acc = identity without the additions
-  if (bo[0] != bo[RWAVE_L])
-    for (int i = RWAVE_L - 1; i >= 0; --i) {
+  if (bo[0] != bo[L])
+    for (int i = (int)L - 1; i >= 0; --i) {
       if (bo[i] != bo[i + 1]) run = ge_add(run, bucket_total(base + i, bo[i], bo[i + 1], ks, head, tail, bsum));
       acc = ge_add(acc, run);
     }
@@ -437,9 +445,9 @@ __global__ void __launch_bounds__(64) k_msm_reduce_wave(const uint32_t* __restri
     const ge_p3 s2 = ge_add(suf, ge_shfl_down(suf, d));
     if (t + d < 64) suf = s2;
   }
-  ge_p3 suf8 = suf;  // RWAVE_L * suf
-  _Pragma("unroll") for (int k = 0; k < RWAVE_LOG; ++k) suf8 = ge_dbl(suf8);
-  ge_p3 v = ge_add(acc, suf8);
+  ge_p3 sufL = suf;  // L * suf
+  _Pragma("unroll") for (int k = 0; k < LOG; ++k) sufL = ge_dbl(sufL);
+  ge_p3 v = ge_add(acc, sufL);
   if (t == 0) v = acc;
   _Pragma("unroll") for (int k = 1; k < 64; k <<= 1) v = ge_add(v, ge_shfl_xor(v, k));
   if (t == 0) {
@@ -448,16 +456,17 @@ __global__ void __launch_bounds__(64) k_msm_reduce_wave(const uint32_t* __restri
   }
 }
 
-// terms per segment = 1 + log2(nw)
+// terms per segment = 1 + log2(nw); lane t folds waves t, t + 64, ...
+template <int LOG>
 __global__ void __launch_bounds__(64) k_msm_reduce_bits(const uint32_t* __restrict__ part, MsmGeom g,
                                                        uint32_t nterms, uint32_t* __restrict__ out) {
-  const uint32_t nw = g.B >> RWAVE_SHIFT;
+  const uint32_t nw = g.B >> (LOG + 6);
   const uint32_t seg = blockIdx.x / nterms, term = blockIdx.x % nterms;
-  const uint32_t w = threadIdx.x;
-  const bool take = w < nw && (term == 0 || ((w >> (term - 1)) & 1u));
-  ge_p3 v = take ? load_p3(part, 2 * ((size_t)seg * nw + w) + (term ? 1 : 0)) : ge_identity();
+  ge_p3 v = ge_identity();
+  for (uint32_t w = threadIdx.x; w < nw; w += 64)
+    if (term == 0 || ((w >> (term - 1)) & 1u)) v = ge_add(v, load_p3(part, 2 * ((size_t)seg * nw + w) + (term ? 1 : 0)));
   _Pragma("unroll") for (int k = 1; k < 64; k <<= 1) v = ge_add(v, ge_shfl_xor(v, k));
-  if (w == 0) store_p3(out, blockIdx.x, v);
+  if (threadIdx.x == 0) store_p3(out, blockIdx.x, v);
 }
 
 // One lane per MSM: Horner over its W window sums.

@@ -101,14 +101,21 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
   const bool lds_sort = !fb && !radix_sort && (M == 1) && (c <= 16) && (T >= 16384);
   // entries per lane: enough lanes to fill the chip several times over
   const uint32_t E_max = T * Wn;
-  // K = entries per lane: about one round of lanes at the accumulate's
-  // 4 waves/SIMD occupancy (256 K lanes) -- fewer chunk borders, so fewer
-  // head/tail pieces (2^20: K = 64 measured best of 32/64/128)
-  uint32_t K = 4;
-  while (K < 128 && E_max / (2 * K) >= 256u * 1024u) K <<= 1;
+  // K = entries per lane (a multiple of 4, for the 16-B entry reads): at most
+  // one round of lanes at the accumulate's occupancy (4 workgroups of 256
+  // lanes per CU, LDS-bound: 256 K lanes on 256 CUs), since every lane does
+  // the same K additions and a partial second round of waves runs after the
+  // first as a tail (config 5's 8.85 M entries: K = 32 gave 4320 waves,
+  // 224 past the round; K = 36 gives 3841).  Fewer chunk borders also mean
+  // fewer head/tail pieces (2^20: K = 64 measured best of 32/64/128).
+  static const size_t round_lanes = [] {
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    return (size_t)std::max(1, ncu) * 4 * ACC_T;
+  }();
+  uint32_t K = (uint32_t)std::min<size_t>(128, std::max<size_t>(4, ((E_max + round_lanes - 1) / round_lanes + 3) & ~(size_t)3));
+  if (const char* ek = getenv("BPP_MSM_ACC_K")) K = (uint32_t)std::min(128, std::max(4, atoi(ek) & ~3));  // A/B runs
   const size_t lanes = (E_max + K - 1) / K + 1;
-  uint32_t ks = 0;
-  while ((1u << ks) < K) ++ks;
   // a heavy bucket spans > FIX_MAX chunks, so holds > (FIX_MAX - 1) K
   // entries: at most E / ((FIX_MAX - 1) K) + 1 of them
   const size_t max_heavy = std::min<size_t>(NB, E_max / ((size_t)(FIX_MAX - 1) * K) + 1);
@@ -232,13 +239,13 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
 #ifndef EXP_NO_REDUCE  // (timing experiment only: results are wrong without it)
       if (rlog == RWAVE_LOG) {
         hipLaunchKernelGGL(k_msm_reduce_wave<RWAVE_LOG>, dim3((unsigned)(nseg * nw)), dim3(64), 0, ctx->stream,
-                           (const uint32_t*)boff, ks, (const uint32_t*)head, (const uint32_t*)tail,
+                           (const uint32_t*)boff, K, (const uint32_t*)head, (const uint32_t*)tail,
                            (const uint32_t*)bsum, g, (uint32_t*)part);
         hipLaunchKernelGGL(k_msm_reduce_bits<RWAVE_LOG>, dim3((unsigned)(nseg * (1 + J))), dim3(64), 0, ctx->stream,
                            (const uint32_t*)part, g, 1 + J, (uint32_t*)wsum);
       } else {
         hipLaunchKernelGGL(k_msm_reduce_wave<RWAVE_LOG_LONE>, dim3((unsigned)(nseg * nw)), dim3(64), 0, ctx->stream,
-                           (const uint32_t*)boff, ks, (const uint32_t*)head, (const uint32_t*)tail,
+                           (const uint32_t*)boff, K, (const uint32_t*)head, (const uint32_t*)tail,
                            (const uint32_t*)bsum, g, (uint32_t*)part);
         hipLaunchKernelGGL(k_msm_reduce_bits<RWAVE_LOG_LONE>, dim3((unsigned)(nseg * (1 + J))), dim3(64), 0,
                            ctx->stream, (const uint32_t*)part, g, 1 + J, (uint32_t*)wsum);
@@ -255,7 +262,7 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
     if (BPS > 1) BPP_TRY(ctx_ws(ctx, "msm_rpart", nseg * BPS * P3_BYTES, &part));
     ProfScope ps(ctx, "msm_reduce");
     hipLaunchKernelGGL(k_msm_reduce_partial, dim3((unsigned)(nseg * BPS)), dim3(RED_T), 0, ctx->stream,
-                       (const uint32_t*)boff, ks, (const uint32_t*)head, (const uint32_t*)tail, (const uint32_t*)bsum,
+                       (const uint32_t*)boff, K, (const uint32_t*)head, (const uint32_t*)tail, (const uint32_t*)bsum,
                        g, L, BPS, (uint32_t*)part);
     if (BPS > 1)
       hipLaunchKernelGGL(k_msm_reduce_final, dim3((unsigned)nseg), dim3(RED_T), 0, ctx->stream,

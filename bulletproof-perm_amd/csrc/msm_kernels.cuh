@@ -196,9 +196,8 @@ __global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_
                                                        uint32_t K, uint32_t* __restrict__ bsum,
                                                        uint32_t* __restrict__ head, uint32_t* __restrict__ tail,
                                                        uint32_t* __restrict__ heavy) {
-  // K is a power of two (msm_engine)
+  // K is a multiple of 4 (msm_engine); lane of entry e = e / K
   __shared__ __attribute__((aligned(16))) uint32_t piece[ACC_T * P3_WORDS];
-  const uint32_t ks = 31 - __clz(K);
   const uint32_t l = blockIdx.x * ACC_T + threadIdx.x;
   const uint32_t lane_first = blockIdx.x * ACC_T, lane_last = lane_first + ACC_T - 1;
   const uint32_t E = boff[nbuckets];
@@ -207,8 +206,8 @@ __global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_
   // a later piece of a bucket that started in an earlier chunk: to LDS when
   // its owner is in this workgroup and will fold it, else to head[l]
   auto park = [&](const ge_p3& v, uint32_t s, uint32_t e) {
-    const uint32_t l0 = s >> ks;
-    uint32_t* dst = ((((e - 1) >> ks) - l0) < FIX_MAX && l0 >= lane_first) ? piece + threadIdx.x * P3_WORDS
+    const uint32_t l0 = s / K;
+    uint32_t* dst = ((((e - 1) / K) - l0) < FIX_MAX && l0 >= lane_first) ? piece + threadIdx.x * P3_WORDS
                                                                            : head + (size_t)l * P3_WORDS;
     store_p3(dst, 0, v);
   };
@@ -220,7 +219,7 @@ __global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_
     bstart = boff[b];
     bend = boff[b + 1];
     // the lane where a bucket starts lists it if it is heavy
-    if (bstart == i0 && ((bend - 1) >> ks) - l >= FIX_MAX) heavy[1 + atomicAdd(&heavy[0], 1u)] = b;
+    if (bstart == i0 && ((bend - 1) / K) - l >= FIX_MAX) heavy[1 + atomicAdd(&heavy[0], 1u)] = b;
     // entries are read 4 at a time (one 16-B load; K is a multiple of 4 and
     // the array is padded): a lane's chunk is contiguous, so per-entry 4-B
     // loads touch the same 128-B line K times across a long loop and
@@ -259,7 +258,7 @@ __global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_
         bstart = boff[b];
         bend = boff[b + 1];
 #endif
-        if (((bend - 1) >> ks) - l >= FIX_MAX) heavy[1 + atomicAdd(&heavy[0], 1u)] = b;
+        if (((bend - 1) / K) - l >= FIX_MAX) heavy[1 + atomicAdd(&heavy[0], 1u)] = b;
         acc = ge_identity();
       }
       acc = ge_madd(acc, fetch_entry(tbl, tbl1, n0, e));
@@ -276,7 +275,7 @@ __global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_
   }
   __syncthreads();
   if (owner) {
-    const uint32_t l1 = (bend - 1) >> ks;
+    const uint32_t l1 = (bend - 1) / K;
     if (l1 - l >= FIX_MAX) {  // heavy: k_msm_fixup_heavy's piece convention
       if (bstart == i0) store_p3(head, l, load_p3(tail, l));
       return;
@@ -293,9 +292,9 @@ __global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_
 // bsum[b] unless the bucket left its owner's workgroup without being heavy
 // (then the owner's partial tail[l0] plus the head pieces of the lanes of
 // later workgroups).
-FE_INLINE ge_p3 bucket_total(size_t b, uint32_t bs, uint32_t be, uint32_t ks, const uint32_t* __restrict__ head,
+FE_INLINE ge_p3 bucket_total(size_t b, uint32_t bs, uint32_t be, uint32_t K, const uint32_t* __restrict__ head,
                              const uint32_t* __restrict__ tail, const uint32_t* __restrict__ bsum) {
-  const uint32_t l0 = bs >> ks, l1 = (be - 1) >> ks;
+  const uint32_t l0 = bs / K, l1 = (be - 1) / K;
   const uint32_t next_wg = (l0 / ACC_T + 1) * ACC_T;
   if (l1 < next_wg || l1 - l0 >= FIX_MAX) return load_p3(bsum, b);
   ge_p3 v = load_p3(tail, l0);
@@ -343,7 +342,7 @@ FE_INLINE ge_p3 lds_tree_sum(uint32_t* lds, ge_p3 v) {
   return load_p3(lds, 0);
 }
 
-__global__ void __launch_bounds__(RED_T) k_msm_reduce_partial(const uint32_t* __restrict__ boff, uint32_t ks,
+__global__ void __launch_bounds__(RED_T) k_msm_reduce_partial(const uint32_t* __restrict__ boff, uint32_t K,
                                                              const uint32_t* __restrict__ head,
                                                              const uint32_t* __restrict__ tail,
                                                              const uint32_t* __restrict__ bsum, MsmGeom g,
@@ -362,7 +361,7 @@ __global__ void __launch_bounds__(RED_T) k_msm_reduce_partial(const uint32_t* __
   _Pragma("unroll") for (uint32_t k = 0; k <= RED_LMAX; ++k) bo[k] = (nb && k <= nb) ? boff[base + lo + k] : 0u;
   for (uint32_t b = hi; b > lo; --b) {
     const uint32_t bs = bo[b - 1 - lo], be = bo[b - lo];
-    if (bs != be) run = ge_add(run, bucket_total(base + b - 1, bs, be, ks, head, tail, bsum));
+    if (bs != be) run = ge_add(run, bucket_total(base + b - 1, bs, be, K, head, tail, bsum));
     acc = ge_add(acc, run);
   }
   if (lo < hi && lo > 0) {  // + lo * run
@@ -418,7 +417,7 @@ __global__ void __launch_bounds__(RED_T) k_msm_reduce_final(const uint32_t* __re
 #define RWAVE_SHIFT (RWAVE_LOG + 6)  // log2(RWAVE_L * 64)
 #define RWAVE_NW_MAX 256             // waves per segment k_msm_reduce_bits folds
 template <int LOG>
-__global__ void __launch_bounds__(64) k_msm_reduce_wave(const uint32_t* __restrict__ boff, uint32_t ks,
+__global__ void __launch_bounds__(64) k_msm_reduce_wave(const uint32_t* __restrict__ boff, uint32_t K,
                                                        const uint32_t* __restrict__ head,
                                                        const uint32_t* __restrict__ tail,
                                                        const uint32_t* __restrict__ bsum, MsmGeom g,
@@ -437,7 +436,7 @@ __global__ void __launch_bounds__(64) k_msm_reduce_wave(const uint32_t* __restri
   // keeps run = acc = identity without the additions
   if (bo[0] != bo[L])
     for (int i = (int)L - 1; i >= 0; --i) {
-      if (bo[i] != bo[i + 1]) run = ge_add(run, bucket_total(base + i, bo[i], bo[i + 1], ks, head, tail, bsum));
+      if (bo[i] != bo[i + 1]) run = ge_add(run, bucket_total(base + i, bo[i], bo[i + 1], K, head, tail, bsum));
       acc = ge_add(acc, run);
     }
   ge_p3 suf = run;  // inclusive suffix sum over lanes t..63

@@ -7,6 +7,8 @@
 #               build.py --variant ipanw -D EXP_IPA_NOWALK; bothnw adds
 #               -D EXP_DT_NOWALK; burn20 -D EXP_HOST_BURN_US=20)
 #   syncwait    hardware queues 4 vs 8, pool 8 vs 16 threads
+#   gaps        kernel + copy timeline of warm 128-proof batches
+#               (tools/trace_gaps.py reads it)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp SHARED_GENS=1
@@ -26,7 +28,10 @@ hostcpu)
   BPP_HOST_THREADS=1 BPP_POOL_SPIN_US=0 timeout -k 10 120 python tools/prove_phases.py 128 4 || exit 1
   for sp in 300 0; do echo -n "spin=$sp "; BPP_POOL_SPIN_US=$sp timeout -k 10 120 python tools/prove_inflight_exp.py 128 8 12 || exit 1; done ;;
 sensitivity)
-  bash tools/ab_prove.sh default ipanw bothnw burn20 || exit 1 ;;
+  B=128 T=12 bash tools/ab.sh prove LIB=default LIB=ipanw LIB=bothnw LIB=burn20 || exit 1 ;;
+gaps)
+  timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace -d $OUT -o run --output-format csv -- python3 tools/prove_phases.py 128 3 > $OUT/log.txt 2>&1 || exit 1
+  python3 tools/trace_gaps.py $OUT ;;
 syncwait)
   for rep in 1 2; do for cfg in "4 8" "8 8" "4 16"; do set -- $cfg
     echo -n "hwq=$1 threads=$2 "; GPU_MAX_HW_QUEUES=$1 BPP_HOST_THREADS=$2 timeout -k 10 120 python tools/prove_inflight_exp.py 128 8 12 || exit 1

@@ -1,5 +1,5 @@
 """GPU busy/idle timeline of the last prove_batch in a rocprofv3 kernel +
-memory-copy trace (tools/trace_prove.sh).  python tools/trace_gaps.py DIR"""
+memory-copy trace (tools/gpu_prover_study.sh gaps).  python tools/trace_gaps.py DIR"""
 import csv
 import sys
 

@@ -2,12 +2,14 @@
 // points: bpp_msm, bpp_msm_table, bpp_msm_table_dev, bpp_msm_batch and the
 // window-partitioned variants used for multi-GPU.
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
 
 #include "ctx.h"
 #include "host/fe64.h"
+#include "host/par.h"
 #include "msm_kernels.cuh"
 #include "msm_engine.h"
 
@@ -326,15 +328,41 @@ int msm_single_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx,
   return BPP_OK;
 }
 
+// Host scalars -> workspace `name`: staged into the pinned arena by the pool
+// in 4-MB pieces, each piece checked for canonical scalars while it is in
+// cache and its DMA queued as soon as it is staged, so the copy engine moves
+// piece k while the pool stages piece k + 1 (2^20 scalars: one serial check
+// pass, a parallel copy and then the whole DMA took ~1.7 ms before the MSM).
+// A non-canonical scalar fails the call (after the queued copies, which only
+// touch the workspace) with the first bad index.
 int upload_scalars(bpp_ctx* ctx, const uint8_t* scalars, size_t n, const char* name, uint32_t** d_out) {
-  for (size_t i = 0; i < n; ++i)
-    if (!scalar_is_canonical(scalars + 32 * i)) {
-      ctx->err = "non-canonical scalar at index " + std::to_string(i);
-      return BPP_ERR_NONCANONICAL;
-    }
   void* d = nullptr;
   BPP_TRY(ctx_ws(ctx, name, n * 32 + 32, &d));
-  BPP_TRY(ctx_h2d(ctx, d, scalars, n * 32));
+  if (n) {
+    uint8_t* p = nullptr;
+    BPP_TRY(ctx_h2d_stage(ctx, n * 32, &p));
+    constexpr size_t SUB = 4096, PIECE = 32 * SUB;  // scalars per pool task / per DMA
+    std::atomic<size_t> bad{n};
+    for (size_t p0 = 0; p0 < n; p0 += PIECE) {
+      const size_t pn = std::min(PIECE, n - p0);
+      par::for_each((pn + SUB - 1) / SUB, [&](size_t t) {
+        const size_t i0 = p0 + t * SUB, i1 = std::min(i0 + SUB, p0 + pn);
+        memcpy(p + 32 * i0, scalars + 32 * i0, 32 * (i1 - i0));
+        for (size_t i = i0; i < i1; ++i)
+          if (!scalar_is_canonical(p + 32 * i)) {
+            size_t cur = bad.load();
+            while (i < cur && !bad.compare_exchange_weak(cur, i)) {
+            }
+            break;
+          }
+      });
+      BPP_TRY(ctx_h2d_staged(ctx, (uint8_t*)d + 32 * p0, p + 32 * p0, 32 * pn));
+    }
+    if (bad.load() < n) {
+      ctx->err = "non-canonical scalar at index " + std::to_string(bad.load());
+      return BPP_ERR_NONCANONICAL;
+    }
+  }
   *d_out = (uint32_t*)d;
   return BPP_OK;
 }

@@ -245,3 +245,23 @@ def test_msm_2p21_both_partitions_exact(ctx):
         ctx.dev_free(ds)
         t.close()
     assert bpperm.partials_finish(parts).hex() == gold["result"]
+
+
+def test_host_scalar_upload_pieces_and_bad_index(ctx, big_table):
+    """Host scalars are staged, checked and copied in 4-MB pieces (131072
+    scalars, msm.hip upload_scalars): a 2^18 + 5-term MSM crosses two piece
+    borders and equals the same MSM over device-resident scalars; a
+    non-canonical scalar in the third piece fails the call with its index."""
+    _, tbl = big_table
+    n = (1 << 18) + 5
+    sb = _sb(_scalars(n, 18))
+    d = ctx.dev_alloc(32 * n)
+    ctx.htod(d, sb)
+    assert ctx.msm_table(sb, tbl, n) == ctx.msm_table_dev(d, tbl, n)
+    ctx.dev_free(d)
+    bad = 2 * 131072 + 3
+    sb2 = sb[: 32 * bad] + L.to_bytes(32, "little") + sb[32 * bad + 32:]
+    with pytest.raises(BppError) as ei:
+        ctx.msm_table(sb2, tbl, n)
+    assert ei.value.name == "BPP_ERR_NONCANONICAL"
+    assert f"index {bad}" in str(ei.value)

@@ -328,26 +328,31 @@ int msm_single_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx,
   return BPP_OK;
 }
 
-// Host scalars -> workspace `name`: staged into the pinned arena by the pool
-// in 4-MB pieces, each piece checked for canonical scalars while it is in
-// cache and its DMA queued as soon as it is staged, so the copy engine moves
-// piece k while the pool stages piece k + 1 (2^20 scalars: one serial check
-// pass, a parallel copy and then the whole DMA took ~1.7 ms before the MSM).
-// A non-canonical scalar fails the call (after the queued copies, which only
-// touch the workspace) with the first bad index.
-int upload_scalars(bpp_ctx* ctx, const uint8_t* scalars, size_t n, const char* name, uint32_t** d_out) {
-  void* d = nullptr;
-  BPP_TRY(ctx_ws(ctx, name, n * 32 + 32, &d));
-  if (n) {
-    uint8_t* p = nullptr;
-    BPP_TRY(ctx_h2d_stage(ctx, n * 32, &p));
-    constexpr size_t SUB = 4096, PIECE = 32 * SUB;  // scalars per pool task / per DMA
-    std::atomic<size_t> bad{n};
-    for (size_t p0 = 0; p0 < n; p0 += PIECE) {
-      const size_t pn = std::min(PIECE, n - p0);
-      par::for_each((pn + SUB - 1) / SUB, [&](size_t t) {
-        const size_t i0 = p0 + t * SUB, i1 = std::min(i0 + SUB, p0 + pn);
-        memcpy(p + 32 * i0, scalars + 32 * i0, 32 * (i1 - i0));
+// Host scalars -> device d on ctx's stream: staged into ctx's pinned arena by
+// the pool in pieces of 2^17 scalars (4 MB; BPP_UP_PIECE_SC overrides, for
+// A/B), each piece checked for canonical scalars while it is in cache (when
+// `check`) and its DMA queued as soon as it is staged, so the copy engine
+// moves piece k while the pool stages piece k + 1.  Returns the index of the
+// first non-canonical scalar, or n.  (2^20 one at a time: one serial check
+// pass, a parallel copy and then the whole DMA took ~1.7 ms before the MSM.)
+static int upload_pieces(bpp_ctx* ctx, void* d, const uint8_t* scalars, size_t n, bool check, size_t* bad_out) {
+  static const size_t PIECE = [] {
+    const char* e = getenv("BPP_UP_PIECE_SC");
+    const long v = e ? atol(e) : 0;
+    return v > 0 ? ((size_t)v + 4095) & ~(size_t)4095 : (size_t)1 << 17;
+  }();
+  constexpr size_t SUB = 4096;  // scalars per pool task
+  *bad_out = n;
+  if (!n) return BPP_OK;
+  uint8_t* p = nullptr;
+  BPP_TRY(ctx_h2d_stage(ctx, n * 32, &p));
+  std::atomic<size_t> bad{n};
+  for (size_t p0 = 0; p0 < n; p0 += PIECE) {
+    const size_t pn = std::min(PIECE, n - p0);
+    par::for_each((pn + SUB - 1) / SUB, [&](size_t t) {
+      const size_t i0 = p0 + t * SUB, i1 = std::min(i0 + SUB, p0 + pn);
+      memcpy(p + 32 * i0, scalars + 32 * i0, 32 * (i1 - i0));
+      if (check)
         for (size_t i = i0; i < i1; ++i)
           if (!scalar_is_canonical(p + 32 * i)) {
             size_t cur = bad.load();
@@ -355,13 +360,23 @@ int upload_scalars(bpp_ctx* ctx, const uint8_t* scalars, size_t n, const char* n
             }
             break;
           }
-      });
-      BPP_TRY(ctx_h2d_staged(ctx, (uint8_t*)d + 32 * p0, p + 32 * p0, 32 * pn));
-    }
-    if (bad.load() < n) {
-      ctx->err = "non-canonical scalar at index " + std::to_string(bad.load());
-      return BPP_ERR_NONCANONICAL;
-    }
+    });
+    BPP_TRY(ctx_h2d_staged(ctx, (uint8_t*)d + 32 * p0, p + 32 * p0, 32 * pn));
+  }
+  *bad_out = bad.load();
+  return BPP_OK;
+}
+
+// Host scalars -> workspace `name`; a non-canonical scalar fails the call
+// (after the queued copies, which only touch the workspace) with its index.
+int upload_scalars(bpp_ctx* ctx, const uint8_t* scalars, size_t n, const char* name, uint32_t** d_out) {
+  void* d = nullptr;
+  BPP_TRY(ctx_ws(ctx, name, n * 32 + 32, &d));
+  size_t bad = n;
+  BPP_TRY(upload_pieces(ctx, d, scalars, n, true, &bad));
+  if (bad < n) {
+    ctx->err = "non-canonical scalar at index " + std::to_string(bad);
+    return BPP_ERR_NONCANONICAL;
   }
   *d_out = (uint32_t*)d;
   return BPP_OK;
@@ -519,16 +534,22 @@ static int msm_submit(bpp_ctx* ctx, const void* d_scalars, const void* h_scalars
       // against 0.99 resident -- but inside bench.py (three interleaved full
       // runs) two upload streams measured 1.35-1.82x resident vs 1.21-1.61x,
       // the pageable leg 1.25-1.55x vs 1.16-1.22x, and the later prover leg
-      // 270-273 K vs 282-287 K proofs/s, so the default stays 0.  The
-      // pageable path is bound by its staging memcpy (1.6-1.9 ms of host time
-      // per 32 MB).  The slot's previous MSM has been collected, so nothing
-      // still reads up_sc.
+      // 270-273 K vs 282-287 K proofs/s, so the default stays 0.  Pageable
+      // scalars go piece by piece (upload_pieces): 1.16-1.30x resident vs
+      // 1.22-1.52x staged whole, within the box's noise.  The slot's previous
+      // MSM has been collected, so nothing still reads up_sc.
       const char* se = getenv("BPP_MSM_UP_STREAMS");
       const int ns = se ? std::max(0, std::min(4, atoi(se))) : 0;
       const size_t bytes = n * 32;
       uint8_t* src = (uint8_t*)h_scalars;
-      if (!pinned) {  // staged through the slot's arena, recycled only by a
-                      // sync of the slot's stream -- which waits for the copies
+      if (!pinned && ns == 0) {  // staged through the slot's arena (recycled
+        // only by a sync of the slot's stream, which waits for the copies)
+        // piece by piece, each piece's DMA queued on the slot's stream as
+        // soon as it is staged (the stream's scalars are not checked here:
+        // the submit contract, as for device scalars)
+        size_t bad = n;
+        rc = upload_pieces(ch, d, (const uint8_t*)h_scalars, n, false, &bad);
+      } else if (!pinned) {
         uint8_t* p = nullptr;
         rc = ctx_h2d_stage(ch, bytes, &p);
         if (!rc) {
@@ -536,9 +557,9 @@ static int msm_submit(bpp_ctx* ctx, const void* d_scalars, const void* h_scalars
           src = p;
         }
       }
-      if (!rc && ns == 0) {
+      if (pinned && !rc && ns == 0) {
         if (hipMemcpyAsync(d, src, bytes, hipMemcpyHostToDevice, ch->stream) != hipSuccess) rc = BPP_ERR_DEVICE;
-      } else if (!rc) {
+      } else if (!rc && ns > 0) {
         const size_t part = ((bytes + ns - 1) / ns + 255) & ~(size_t)255;
         for (int k = 0; k < ns && !rc; ++k) {
           const size_t o = (size_t)k * part;

@@ -24,7 +24,7 @@ ROOT = Path(__file__).resolve().parent.parent
 def per_kernel(path):
     d = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
-        d[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]))
+        d[r["Kernel_Name"].split("(")[0].replace("void ", "").split("<")[0]].append(float(r["Counter_Value"]))
     return d
 
 

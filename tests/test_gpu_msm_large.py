@@ -34,10 +34,15 @@ def big_table(ctx):
     t.close()
 
 
-@pytest.mark.parametrize("logn,lds", [(14, False), (17, False), (17, True)])
-def test_msm_exact_vs_cport(ctx, big_table, logn, lds, monkeypatch):
+@pytest.mark.parametrize("logn,lds,acc_k", [(14, False, None), (17, False, None), (17, True, None),
+                                            (17, False, "12"), (14, False, "36"), (17, False, "100")])
+def test_msm_exact_vs_cport(ctx, big_table, logn, lds, acc_k, monkeypatch):
+    """acc_k: entries per accumulation lane forced to a non-power-of-two
+    multiple of 4 (msm.hip picks one by size, e.g. 36 for config 5)."""
     if lds:
         monkeypatch.setenv("BPP_MSM_LDS_SORT", "1")
+    if acc_k:
+        monkeypatch.setenv("BPP_MSM_ACC_K", acc_k)
     raw, tbl = big_table
     n = 1 << logn
     sc = _sb(_scalars(n, logn))

@@ -490,7 +490,11 @@ static int msm_submit(bpp_ctx* ctx, const void* d_scalars, const void* h_scalars
   // would cost the accumulation ~8 % (BPP_ACC_LDS_PAD overrides the pad).
   bool others = false;
   for (size_t i = 0; i < BPP_MSM_INFLIGHT; ++i) others |= ctx->msm_slot[i].busy;
-  ch->acc_lds_pad = others ? (size_t)13000 : 0;
+  static const long pad_env = [] {
+    const char* e = getenv("BPP_ACC_LDS_PAD");
+    return e ? atol(e) : -1L;
+  }();
+  ch->acc_lds_pad = others ? (pad_env >= 0 ? (size_t)pad_env : (size_t)13000) : 0;
   if (!sl.done) BPP_HIP(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
   // inputs written on ctx's stream before this call are visible to the child
   BPP_HIP(hipEventRecord(sl.done, ctx->stream));

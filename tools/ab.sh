@@ -20,7 +20,7 @@
 #   bash tools/ab.sh prove "GPU_MAX_HW_QUEUES=8 T=12" "BPP_IPA_DEVICE_MERLIN=1"
 #   STEPS=120 bash tools/ab.sh msm "INFLIGHT=3" "INFLIGHT=4 GPU_MAX_HW_QUEUES=8"
 #   bash tools/ab.sh msmv "BENCH_ARGS=--verify-streams=2" "BENCH_ARGS=--verify-streams=3"
-# (BENCH_ARGS: extra bench.py arguments, one word)
+# (BENCH_ARGS: extra bench.py arguments, comma-separated)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp SHARED_GENS=1
@@ -65,7 +65,7 @@ for cfg in "$@"; do
         args="--no-cpu --steps ${STEPS:-20} --warmup ${WARMUP:-2} --inflight ${INFLIGHT:-3}"
         [ $LEG = full ] || args="$args --proofs-per-gpu 0"
         [ $LEG = msm ] && args="$args --verify-proofs 0"
-        args="$args $BENCH_ARGS"
+        args="$args ${BENCH_ARGS//,/ }"
         timeout -k 10 300 python bench.py $args > gpurun_out/ab.json 2> gpurun_out/ab.err || { tail -5 gpurun_out/ab.err; exit 1; }
         summ gpurun_out/ab.json "$cfg" ;;
       prove)

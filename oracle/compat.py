@@ -209,7 +209,11 @@ def compat_prove(k: int, seed: int, label: bytes = b"test", engine: Engine | Non
     # weights.rs:58-61 commit_variables: fresh blindings
     V_blind = [rng.scalar() for _ in range(m)]
     V = [eng.commit(vi, bl) for vi, bl in zip(v, V_blind)]
-    wl, wr, wo, wv = compat_create_weights(k)
+    # lib.rs:188 binds `let (w_r, w_l, w_o, w_v) = create_weights(k);` and
+    # passes W_L: w_l, W_R: w_r (:203-204): the reference's W_L is the matrix
+    # create_weights builds as w_r (its i >= n rows, weights.rs:153) and its
+    # W_R is create_weights' w_l (the i < n rows, :141)
+    wr, wl, wo, wv = compat_create_weights(k)
     WL, WR, WO, WV = _transpose(wl), _transpose(wr), _transpose(wo), _transpose(wv)  # Q2
     c = [0] * (Q - 2) + [L - 1, 1]  # weights.rs:26-35 create_constants
     aL, aR, aO = compat_create_a(v)  # Q3

@@ -56,27 +56,54 @@ def test_create_a_k4_by_hand():
     assert aO[2] == aO[5] == 3024 and aL[7] != 0
 
 
-def _violations(k, perm, x=1):
+def _violations(k, perm, x=1, bind_as_lib_rs=True):
+    """Violated linear / multiplication constraints of the reference's
+    witness.  lib.rs:188 binds `let (w_r, w_l, w_o, w_v) = create_weights(k)`
+    and passes W_L: w_l, W_R: w_r (:203-204), so the reference's W_L is
+    create_weights' SECOND return; bind_as_lib_rs=False reads the matrices
+    in create_weights' own order instead."""
     v = list(range(1, k + 1)) + [p + 1 for p in perm] + [x]
     aL, aR, aO = bp.compat_create_a(v)
-    wl, wr, wo, wv = bp.compat_create_weights(k)
+    first, second, wo, wv = bp.compat_create_weights(k)
+    wl, wr = (second, first) if bind_as_lib_rs else (first, second)
     Q, n = 4 * k, 2 * k
     c = [0] * (Q - 2) + [L - 1, 1]  # create_constants (weights.rs:26-36)
-    lin = 0
+    held = []
     for q in range(Q):
         lhs = sum(wl[q][i] * aL[i] + wr[q][i] * aR[i] + wo[q][i] * aO[i] for i in range(n)) % L
         rhs = (sum(wv[q][j] * v[j] for j in range(n + 1)) + c[q]) % L
-        lin += lhs != rhs
+        if lhs == rhs:
+            held.append(q)
     mul = sum((aL[i] * aR[i] - aO[i]) % L != 0 for i in range(n))
-    return lin, mul
+    return Q - len(held), mul, held
 
 
 def test_reference_witness_violates_its_constraints_k52():
-    """with x = 1 (weights.rs:50) every 52-card witness
-    violates tens of the 208 linear constraints (49-100 observed over random
-    permutations) and the last multiplication gate."""
+    """SURVEY.md §2.2 Q3, re-derived under the reference's actual binding
+    (lib.rs:188, 203-204): with x = 1 (weights.rs:50) every 52-card witness
+    violates 207 of the 208 linear constraints -- only row k/2 + 1 = 27
+    (create_weights' special a_L row, weights.rs:144-150) holds -- and the
+    last multiplication gate.  Read in create_weights' own order (the
+    binding SURVEY Q3 assumed) the same witnesses violate 49-100 rows."""
     rng = Rng(3, b"compat")
     for _ in range(6):
-        lin, mul = _violations(52, bp.fisher_yates(52, rng))
-        assert 49 <= lin <= 100
-        assert mul == 1
+        perm = bp.fisher_yates(52, rng)
+        lin, mul, held = _violations(52, perm)
+        assert (lin, mul, held) == (207, 1, [27])
+        lin_cw, mul_cw, _ = _violations(52, perm, bind_as_lib_rs=False)
+        assert 49 <= lin_cw <= 100 and mul_cw == 1
+
+
+def test_compat_restatement_binds_weights_as_lib_rs():
+    """oracle/compat.py's W_L is create_weights' w_r (ones in rows i >= n,
+    weights.rs:153) and its W_R is create_weights' w_l (ones in rows i < n,
+    weights.rs:141), both transposed for create() (Q2)."""
+    from oracle import compat
+    k = 3
+    run = compat.compat_prove(k, 0)
+    n, Q = 2 * k, 4 * k
+    first, second, _, _ = bp.compat_create_weights(k)
+    assert run.WL == [[second[q][i] for q in range(Q)] for i in range(n)]
+    assert run.WR == [[first[q][i] for q in range(Q)] for i in range(n)]
+    assert all(run.WL[i][q] == (1 if q == i + n else 0) for i in range(n) for q in range(Q))
+    assert all(run.WR[i][q] == (1 if q == i else 0) for i in range(n) for q in range(Q))

@@ -75,6 +75,54 @@ def test_config4_eight_batches_in_flight_bit_exact():
         c.close()
 
 
+def test_bench_shape_384_proof_batches_in_flight_bit_exact():
+    """bench.py's proofs leg shape: 384-proof lockstep batches, several in
+    flight on their own contexts and host threads over one shared generator
+    set.  Sampled proofs and V byte-exact against the serial C prover (first,
+    last, the 8-way lockstep group borders, the 128 / 256 borders of the
+    direct-table launch shapes); every batch verifies; one tampered proof and
+    one swapped V are rejected."""
+    import bpperm
+    B4, S4 = 384, 4
+    seeds = [[8_000_000 + 10_000 * s + i for i in range(B4)] for s in range(S4)]
+    ctxs = [bpperm.Context(0) for _ in range(S4)]
+    gens = bpperm.Gens(ctxs[0], 128)
+    provers = [bpperm.PermProver(gens, K, ctx=c) for c in ctxs]
+    out = [None] * S4
+    errs = []
+
+    def run(s):
+        try:
+            out[s] = provers[s].prove_batch(seeds[s])
+        except Exception as e:  # surfaced after the join
+            errs.append(e)
+
+    th = [threading.Thread(target=run, args=(s,)) for s in range(S4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    for s in range(S4):
+        proofs, Vs = out[s]
+        assert len(proofs) == B4 and all(len(p) == provers[s].proof_len for p in proofs)
+        picks = [0, 7, 8, 127, 128, 255, 256, 300 + 11 * s, B4 - 1] if s == 0 else [0, 129 + 17 * s, B4 - 1]
+        _check_sample(seeds[s], proofs, Vs, picks)
+        assert provers[s].verify_batch(proofs, Vs)
+    proofs, Vs = out[2]
+    bad = list(proofs)
+    b = bytearray(bad[333])
+    b[8 * 32 + 2 * 32 + 9] ^= 0x04
+    bad[333] = bytes(b)
+    assert not provers[2].verify_batch(bad, Vs)
+    Vbad = list(Vs)
+    Vbad[200], Vbad[201] = Vbad[201], Vbad[200]
+    assert not provers[2].verify_batch(proofs, Vbad)
+    gens.close()
+    for c in ctxs:
+        c.close()
+
+
 def test_changing_batch_shapes_on_one_context(ctx):
     """The per-context upload caches (generator indices, circuit CSR, MSM
     offsets: ctx_h2d_const / upload_offsets) see batch sizes 41 -> 128 -> 41

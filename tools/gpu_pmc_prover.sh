@@ -1,5 +1,5 @@
-# PMC counters of the prover's kernels under the bench's load shape (256-proof
-# batches, 12 contexts in flight; the profiler serialises dispatches, so each
+# PMC counters of the prover's kernels under the bench's load shape (384-proof
+# batches, 16 contexts in flight, PMC_SHAPE overrides; the profiler serialises dispatches, so each
 # kernel's counters are its own).  One counter pass per rocprofv3 run.
 # Usage (on the box): bash tools/gpu_pmc_prover.sh <tag> [msm]
 #   msm: the same passes over the 2^20 MSM bench stream instead
@@ -9,10 +9,10 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp SHARED_GENS=1
 TAG=${1:-r02}
 OUT=gpurun_out/pmc_prover_$TAG
-CMD="python3 tools/prove_inflight_exp.py 256 12 2"
+CMD="python3 tools/prove_inflight_exp.py ${PMC_SHAPE:-384 16 2}"
 if [ "$2" = "msm" ]; then
   OUT=gpurun_out/pmc_msm_$TAG
-  CMD="python3 bench.py --steps 6 --warmup 1 --no-cpu --proofs-per-gpu 0 --verify-proofs 0"
+  CMD="python3 bench.py --steps 6 --warmup 1 --no-cpu --proofs-per-gpu 0 --verify-proofs 0 --no-extra --no-extra"
 fi
 mkdir -p $OUT
 timeout -s KILL 60 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true

@@ -16,11 +16,11 @@ tail -1 $OUT/gpu_tests.txt
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.txt 2>&1 || { tail $OUT/smoke.txt; exit 1; }
 timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail $OUT/bench.err; exit 1; }
 python -c "import json;d=json.load(open('$OUT/bench.json'));p=d['proofs'];print(d['value'],d['ms_per_step'],d['result_ok'],p['value'],p['verify_batch_proofs_per_sec'],d['verify_batch']['value'])"
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu --proofs-per-gpu 0 --verify-proofs 0 --inflight 1 > $OUT/trace_log.txt 2>&1 || { echo "trace failed"; exit 1; }
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace_proofs -o run --output-format csv -- python3 tools/prove_batch_once.py 256 > $OUT/trace_proofs_log.txt 2>&1 || { echo "proof trace failed"; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu --proofs-per-gpu 0 --verify-proofs 0 --no-extra --no-extra --inflight 1 > $OUT/trace_log.txt 2>&1 || { echo "trace failed"; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace_proofs -o run --output-format csv -- python3 tools/prove_batch_once.py ${PROOF_BATCH:-384} > $OUT/trace_proofs_log.txt 2>&1 || { echo "proof trace failed"; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_verify -o run --output-format csv -- python3 tools/verify_stages.py --reps 3 > $OUT/trace_verify_log.txt 2>&1 || { echo "verify trace failed"; exit 1; }
-timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu --proofs-per-gpu 0 --verify-proofs 0 > $OUT/pmc_fetch_log.txt 2>&1 || { echo "pmc fetch failed"; exit 1; }
-timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu --proofs-per-gpu 0 --verify-proofs 0 > $OUT/pmc_write_log.txt 2>&1 || { echo "pmc write failed"; exit 1; }
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu --proofs-per-gpu 0 --verify-proofs 0 --no-extra --no-extra > $OUT/pmc_fetch_log.txt 2>&1 || { echo "pmc fetch failed"; exit 1; }
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu --proofs-per-gpu 0 --verify-proofs 0 --no-extra --no-extra > $OUT/pmc_write_log.txt 2>&1 || { echo "pmc write failed"; exit 1; }
 bash tools/gpu_pmc_prover.sh $TAG || exit 1
 bash tools/gpu_pmc_prover.sh $TAG msm || exit 1
 echo done

@@ -76,10 +76,19 @@ def main():
             e["any_issue_frac"] = mean["SQ_ACTIVE_INST_ANY"] / mean["SQ_WAVE_CYCLES"]
             e["wait_any_frac"] = mean["SQ_WAIT_ANY"] / mean["SQ_WAVE_CYCLES"]
             e["wait_inst_any_frac"] = mean["SQ_WAIT_INST_ANY"] / mean["SQ_WAVE_CYCLES"]
-            # SQ_WAVE_CYCLES and SQ_BUSY_CYCLES in quad-cycles summed over SEs:
-            # mean resident waves per SIMD over the kernel's busy time
-            e["mean_waves_per_cu"] = mean["SQ_WAVE_CYCLES"] / max(mean["SQ_BUSY_CYCLES"], 1) / 32.0
             e["eff_clock_ghz"] = mean["GRBM_GUI_ACTIVE"] / 8 / mean["_ns"] if mean["_ns"] > 0 else None
+            # mean resident waves per SIMD over the launch: SQ_WAVE_CYCLES is
+            # the sum over waves of their resident time in quad-cycles
+            # (MI355X_MICROARCH.md: SQ_WAVE_CYCLES counts quad-cycles), the
+            # launch spans GRBM_GUI_ACTIVE / 8 XCDs cycles, on 1024 SIMDs.
+            # Calibration: k_msm_accumulate holds 4 waves per SIMD by the
+            # compiler's report (128 VGPRs) and runs 4100 waves in one round,
+            # so this must read ~4 there (round 3's WAVE/BUSY/32 read 0.48).
+            cyc = mean["GRBM_GUI_ACTIVE"] / 8
+            e["waves_per_simd"] = 4.0 * mean["SQ_WAVE_CYCLES"] / max(cyc, 1) / 1024
+            e["launch_waves_per_simd"] = w / 1024
+            for c in ("SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE"):
+                e[c.lower()] = mean[c]
         for c in ("SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT",
                   "SQ_INSTS_BRANCH"):
             if c in mean and "SQ_WAVES" in mean:

@@ -101,6 +101,13 @@ class Context:
     def stream(self) -> int:
         return int(self.lib.bpp_ctx_stream(self.h) or 0)
 
+    def secret_residue(self) -> int:
+        """Nonzero bytes left in what the last production prover batch zeroed
+        (bpp_debug_secret_residue; a test hook)."""
+        nz = C.c_uint64()
+        check(self.lib.bpp_debug_secret_residue(self.h, C.byref(nz)), "bpp_debug_secret_residue", self.h)
+        return nz.value
+
     # ---------------------------------------------------------- profiling
     def profile(self, enable: bool = True):
         check(self.lib.bpp_ctx_profile(self.h, 1 if enable else 0), "bpp_ctx_profile", self.h)
@@ -514,6 +521,21 @@ class PermProver:
         on the host (bpp_perm_verify_begin)."""
         return VerifyJob(self.k, proofs, Vs, self.label, ctx=self.ctx if device else None)
 
+    def verify_partial_gathered(self, job: "VerifyJob", d_blocks: int, stride: int, counts: Sequence[int],
+                                w_begin: int, w_end: int) -> bytes:
+        """128-B raw partial of a sliced job's MSM over ALL its proofs, windows
+        [w_begin, w_end), from every slice's scalar block gathered at d_blocks
+        (block s at d_blocks + s * stride; bpp_perm_verify_partial_gathered).
+        None when a proof point does not decode."""
+        part = C.create_string_buffer(128)
+        cn = (C.c_size_t * max(len(counts), 1))(*counts)
+        rc = self.ctx.lib.bpp_perm_verify_partial_gathered(self.ctx.h, self.gens.h, job.h, d_blocks, stride, cn,
+                                                           len(counts), w_begin, w_end, part)
+        if rc == 6:
+            return None
+        check(rc, "bpp_perm_verify_partial_gathered", self.ctx.h)
+        return part.raw
+
     def verify_partial(self, job: "VerifyJob", r_all: bytes, first: int, w_begin: int, w_end: int) -> bytes:
         """128-B raw partial of job's MSM over windows [w_begin, w_end) (see
         bpp_perm_verify_partial); r_all = every rank's r challenges.  None
@@ -536,26 +558,47 @@ class VerifyJob:
     (r_all)."""
 
     def __init__(self, k: int, proofs: Sequence[bytes], Vs: Sequence[bytes], label: bytes = b"bp-perm",
-                 ctx: "Context | None" = None):
+                 ctx: "Context | None" = None, replay: "tuple[int, int] | None" = None):
+        """replay=(first, n): a sliced device job (bpp_perm_verify_begin_dev_slice):
+        every proof uploaded and decompressed, proofs [first, first + n)
+        replayed; `r` then holds the slice's n challenges."""
         self.lib = _lib.load()
         self.k = k
         self.count = len(proofs)
         self.device = ctx is not None
+        self.ctx = ctx
+        self.slice = replay
         h = C.c_void_p()
-        r = C.create_string_buffer(32 * self.count + 1)
+        nr = self.count if replay is None else replay[1]
+        r = C.create_string_buffer(32 * nr + 1)
         pb, vb = _buf(b"".join(proofs)), _buf(b"".join(Vs))
         if ctx is None:
             rc = self.lib.bpp_perm_verify_begin(k, self.count, _buf(label), len(label), pb, vb, r, C.byref(h))
-        else:
+            name = "bpp_perm_verify_begin"
+        elif replay is None:
             rc = self.lib.bpp_perm_verify_begin_dev(ctx.h, k, self.count, _buf(label), len(label), pb, vb, r,
                                                     C.byref(h))
+            name = "bpp_perm_verify_begin_dev"
+        else:
+            rc = self.lib.bpp_perm_verify_begin_dev_slice(ctx.h, k, self.count, _buf(label), len(label), pb, vb,
+                                                          replay[0], replay[1], r, C.byref(h))
+            name = "bpp_perm_verify_begin_dev_slice"
         if rc == 6:
             self.h = None
             self.r = None
             return
-        check(rc, "bpp_perm_verify_begin" + ("_dev" if ctx is not None else ""), ctx.h if ctx is not None else None)
+        check(rc, name, ctx.h if ctx is not None else None)
         self.h = h
-        self.r = r.raw[:32 * self.count]
+        self.r = r.raw[:32 * nr]
+
+    def slice_bytes(self) -> int:
+        return int(self.lib.bpp_perm_verify_slice_bytes(self.h))
+
+    def slice_scalars(self, r_all: bytes, d_out: int):
+        """The replayed slice's MSM scalars into device memory d_out
+        (slice_bytes() bytes; bpp_perm_verify_slice_scalars)."""
+        check(self.lib.bpp_perm_verify_slice_scalars(self.ctx.h, self.h, _buf(r_all), len(r_all) // 32, d_out),
+              "bpp_perm_verify_slice_scalars", self.ctx.h)
 
     @property
     def ok(self) -> bool:

@@ -22,7 +22,15 @@
    all-gathered and must add up to the identity.  Proof split: each rank
    replays only its slice, the 32-byte weight challenges r are all-gathered
    (the batch weights depend on every proof), each rank runs all windows of
-   its slice's MSM, then the same 128-byte exchange.
+   its slice's MSM, then the same 128-byte exchange.  Sharded window split
+   ("windows_sharded", VERDICT r3: the plain window split replays and
+   expands every proof on every rank, which bounds it at ~1.3x on 8 GPUs):
+   every rank uploads and decompresses all proofs but replays and expands
+   only its proof slice; the slices' r are all-gathered, each rank writes its
+   slice's MSM scalars (generator scalars summed over the slice, then the
+   slice's proof-point scalars) to one device block, the blocks are
+   all-gathered (RCCL all_gather_into_tensor; 16.7 MB in all for config 5),
+   and each rank runs the MSM of the whole batch over its window range.
 
 The functions take the collective as a callable so the same code runs over
 RCCL on GPUs (bench.py) and over gloo on CPU (tests/test_dist_gloo.py).
@@ -106,12 +114,80 @@ def torch_all_gather_bytes_var(payload: bytes, device=None) -> list[bytes]:
     return [o.cpu().numpy().tobytes()[:sz] for o, sz in zip(out, sizes)]
 
 
-def distributed_verify(prover, proofs, Vs, rank: int, world: int, split: str = "windows", device=None) -> bool:
-    """Batch-verify `proofs` (all of them, identical on every rank) with the
-    MSM partitioned over the ranks (split = "windows" or "proofs")."""
+def _slice_block_bytes(k: int, count: int) -> int:
+    """Bytes of one slice's scalar block (bpp_perm_verify_slice_bytes)."""
+    n_p = 1
+    while n_p < 2 * k:
+        n_p <<= 1
+    lg = n_p.bit_length() - 1
+    return (2 * n_p + 2 + count * (2 * k + 1 + 8 + 2 * lg)) * 32
+
+
+def gather_blocks(block, world: int, device=None):
+    """all_gather of equal-size uint8 device tensors into one device tensor
+    [world * len(block)]: all_gather_into_tensor over RCCL, through host
+    memory over gloo."""
+    import torch
+    import torch.distributed as dist
+
+    if world == 1:
+        return block
+    if dist.get_backend() == "nccl":
+        out = torch.empty(world * block.numel(), dtype=torch.uint8, device=block.device)
+        dist.all_gather_into_tensor(out, block)
+        return out
+    parts = [torch.empty(block.numel(), dtype=torch.uint8) for _ in range(world)]
+    dist.all_gather(parts, block.cpu())
+    return torch.cat(parts).to(block.device)
+
+
+def verify_sliced(prover, proofs, Vs, rank: int, world: int, all_gather_r, gather, device=None):
+    """The sharded window split of one batch (module doc, 3): returns (ok,
+    this rank's 128-B partial).  all_gather_r(bytes) -> every rank's r bytes
+    in rank order; gather(block tensor) -> the blocks of all ranks as one
+    device tensor (rank order)."""
+    import torch
+
     import bpperm
 
-    if split == "windows":
+    ranges = point_ranges(len(proofs), world)
+    b, e = ranges[rank]
+    counts = [hi - lo for lo, hi in ranges]
+    job = bpperm.VerifyJob(prover.k, proofs, Vs, prover.label, ctx=prover.ctx, replay=(b, e - b))
+    try:
+        ok = job.ok
+        r_all = b"".join(all_gather_r(job.r if ok else bytes(32 * (e - b))))
+        stride = (_slice_block_bytes(prover.k, max(counts)) + 15) // 16 * 16
+        dev = device if device is not None else torch.device("cuda", prover.ctx.device)
+        blk = torch.zeros(stride, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize(dev)  # (the fill runs on torch's stream, the library on its own)
+        if ok:
+            assert job.slice_bytes() <= stride
+            job.slice_scalars(r_all, blk.data_ptr())  # (synchronises the library's stream)
+        blocks = gather(blk)
+        torch.cuda.synchronize(dev)
+        part = None
+        if ok:
+            wb, we = window_ranges(job.windows()[1], world)[rank]
+            part = prover.verify_partial_gathered(job, blocks.data_ptr(), stride, counts, wb, we)
+        if part is None:  # a rejected replay, or a proof point that does not decode
+            ok, part = False, bytes(128)
+        return ok, part
+    finally:
+        job.close()
+
+
+def distributed_verify(prover, proofs, Vs, rank: int, world: int, split: str = "windows", device=None) -> bool:
+    """Batch-verify `proofs` (all of them, identical on every rank) with the
+    MSM partitioned over the ranks (split = "windows", "windows_sharded" or
+    "proofs")."""
+    import bpperm
+
+    if split == "windows_sharded":
+        ok, part = verify_sliced(prover, proofs, Vs, rank, world,
+                                 lambda r: torch_all_gather_bytes_var(r, device),
+                                 lambda blk: gather_blocks(blk, world, device), device)
+    elif split == "windows":
         job = bpperm.VerifyJob(prover.k, proofs, Vs, prover.label, ctx=prover.ctx)
         ok = job.ok
         if ok:
@@ -120,7 +196,7 @@ def distributed_verify(prover, proofs, Vs, rank: int, world: int, split: str = "
         else:
             part = bytes(128)
         job.close()
-    else:
+    else:  # "proofs"
         b, e = point_ranges(len(proofs), world)[rank]
         job = bpperm.VerifyJob(prover.k, proofs[b:e], Vs[b:e], prover.label, ctx=prover.ctx)
         ok = job.ok

@@ -90,6 +90,11 @@ struct bpp_ctx {
   size_t up_sc_bytes = 0;
   hipStream_t up_stream[4] = {nullptr, nullptr, nullptr, nullptr};
   hipEvent_t up_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  // spans of the pinned arena that the last prover batch on this context
+  // filled with secrets (draw templates and pi, the host-path witness), for
+  // prove_wipe; `wiped` keeps the spans of the last wipe for
+  // bpp_debug_secret_residue
+  std::vector<std::pair<uint8_t*, size_t>> secret_stage, wiped;
 };
 #define VJ_CHILD BPP_MSM_INFLIGHT
 

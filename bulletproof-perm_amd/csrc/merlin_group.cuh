@@ -1,0 +1,215 @@
+// Merlin transcripts on the device, one transcript per GROUP of 8 lanes
+// (merlin 3.0.0 / STROBE-128 over Keccak-f[1600]; the reference's
+// TranscriptProtocol, transcript_protocol.rs:26-67).  Byte-exact with
+// host/merlin.h and merlin_lane.cuh.
+//
+// Why groups: a batch of P proofs replays P independent transcripts of ~53
+// permutations each.  With one transcript per lane (merlin_lane.cuh) the
+// 4096 transcripts of config 5 are 64 waves, so the replay's time is one
+// wave's instruction stream: 24 rounds x ~190 VALU instructions per
+// permutation.  Here the five lanes of a group each own one column of the
+// state (Keccak lanes A[x][0..4], as lo / hi halves), so a round costs a lane
+// ~45 VALU and ~20 LDS instructions:
+//   theta   the column parity is the lane's own five words; C[x+1] and
+//           C[x-1] come from the neighbouring lanes by DPP (row_shl:1 /
+//           row_shr:1, no LDS);
+//   rho/pi  the lane rotates its five words by its own offsets (v_alignbit
+//           with per-lane shift registers; a rotation by >= 32 is a swap of
+//           the halves, folded into the LDS store addresses) and stores them
+//           at their pi destinations in the group's 200-byte scratch;
+//   chi     the lane reads back columns x, x+1, x+2 of the permuted state
+//           (ds_read2_b64) and forms its new column;
+//   iota    the lane of column 0 folds in the round constant.
+// Group lane gl holds column x = (gl + 4) mod 5 (gl 0..7 -> 4 0 1 2 3 4 0 1):
+// lanes 1..5 are the state's owners ("canonical", the only ones that store)
+// and every canonical lane finds C[x+1] at gl + 1 and C[x-1] at gl - 1 inside
+// the same 8-lane group, so the DPP row shifts never leave the group for
+// them; lanes 0, 6, 7 compute copies that nobody reads.
+// The 8 lanes of a group are in one wave and LDS instructions of one wave
+// execute in order, so the scratch needs no barrier -- only compiler fences
+// (the cross-lane dependence is invisible to the compiler).
+//
+// The STROBE byte operations (absorbs, the begin_op flags, the squeeze) are
+// the schedule of merlin_lane.cuh executed by the group's leader lane (gl 1)
+// on the group's sponge in LDS; every lane runs the same control flow (the
+// positions are uniform: a batch's transcripts have the same lengths), so the
+// whole wave enters each permutation together.
+#pragma once
+#include "keccak_dev.cuh"
+#include "merlin_lane.cuh"
+
+#define GRP_LANES 8
+#define GRP_ST_BYTES 200
+
+// rho offsets r[x][y] packed per y (6 bits per x) and the pi destination row
+// (2x + 3y) mod 5 packed per y (3 bits per x); pi's destination column is y
+__device__ __constant__ static const uint32_t GRP_RHO[5] = {
+    (0u << 0) | (1u << 6) | (62u << 12) | (28u << 18) | (27u << 24),
+    (36u << 0) | (44u << 6) | (6u << 12) | (55u << 18) | (20u << 24),
+    (3u << 0) | (10u << 6) | (43u << 12) | (25u << 18) | (39u << 24),
+    (41u << 0) | (45u << 6) | (15u << 12) | (21u << 18) | (8u << 24),
+    (18u << 0) | (2u << 6) | (61u << 12) | (56u << 18) | (14u << 24)};
+
+FE_INLINE uint32_t grp_dpp_next(uint32_t v) {  // lane i <- lane i + 1 (row_shl:1)
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x101, 0xf, 0xf, false);
+}
+FE_INLINE uint32_t grp_dpp_prev(uint32_t v) {  // lane i <- lane i - 1 (row_shr:1)
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+}
+#define GRP_FENCE() __asm__ volatile("" ::: "memory")
+
+// Keccak-f[1600] on the group's sponge st (25 x u64 in the standard x + 5y
+// order, LDS), with scr (200 B, LDS) as the pi scratch; called by all 8 lanes
+// of the group (gl = lane within the group).
+__device__ __noinline__ static void grp_keccak(lds_u64* st, lds_u64* scr, uint32_t gl) {
+  const uint32_t x = (gl + 4) % 5;
+  const bool canon = gl - 1u < 5u;
+  typedef __attribute__((address_space(3))) uint32_t lds_u32;
+  lds_u32* scr32 = (lds_u32*)scr;
+  uint32_t lo[5], hi[5], c[5], wl[5], wh[5];
+  _Pragma("unroll") for (int y = 0; y < 5; ++y) {
+    const uint64_t v = st[x + 5 * y];
+    lo[y] = (uint32_t)v;
+    hi[y] = (uint32_t)(v >> 32);
+    const uint32_t n = (GRP_RHO[y] >> (6 * x)) & 63u;
+    const uint32_t s = n & 31u, sw = (n >> 5) ^ (s == 0 ? 1u : 0u);
+    c[y] = (32u - s) & 31u;
+    const uint32_t Y = (2 * x + 3 * y) % 5;
+    const uint32_t off = 2 * (5 * y + Y);  // dword index of the destination word (column y, row Y)
+    wl[y] = off + sw;
+    wh[y] = off + (sw ^ 1u);
+  }
+  const uint32_t c0 = 5 * x, c1 = 5 * ((x + 1) % 5), c2 = 5 * ((x + 2) % 5);  // u64 index of columns
+  const uint32_t ms = x == 0 ? ~0u : 0u;
+  for (int r = 0; r < 24; ++r) {
+    // theta
+    const uint32_t cl = xor3(xor3(lo[0], lo[1], lo[2]), lo[3], lo[4]);
+    const uint32_t ch = xor3(xor3(hi[0], hi[1], hi[2]), hi[3], hi[4]);
+    const uint32_t nl = grp_dpp_next(cl), nh = grp_dpp_next(ch);
+    const uint32_t pl = grp_dpp_prev(cl), ph = grp_dpp_prev(ch);
+    const uint32_t dl = pl ^ __builtin_amdgcn_alignbit(nl, nh, 31);
+    const uint32_t dh = ph ^ __builtin_amdgcn_alignbit(nh, nl, 31);
+    // rho + pi: rotated words to their destinations (halves swapped there
+    // for rotations by >= 32)
+    GRP_FENCE();
+    if (canon) {
+      _Pragma("unroll") for (int y = 0; y < 5; ++y) {
+        const uint32_t a = lo[y] ^ dl, b = hi[y] ^ dh;
+        scr32[wl[y]] = __builtin_amdgcn_alignbit(a, b, c[y]);
+        scr32[wh[y]] = __builtin_amdgcn_alignbit(b, a, c[y]);
+      }
+    }
+    GRP_FENCE();
+    // chi over columns x, x + 1, x + 2 of the permuted state
+    _Pragma("unroll") for (int y = 0; y < 5; ++y) {
+      const uint64_t b0 = scr[c0 + y], b1 = scr[c1 + y], b2 = scr[c2 + y];
+      const uint32_t b0l = (uint32_t)b0, b0h = (uint32_t)(b0 >> 32), b1l = (uint32_t)b1, b1h = (uint32_t)(b1 >> 32),
+                     b2l = (uint32_t)b2, b2h = (uint32_t)(b2 >> 32);
+      lo[y] = b0l ^ (~b1l & b2l);
+      hi[y] = b0h ^ (~b1h & b2h);
+    }
+    GRP_FENCE();
+    // iota (column 0's lanes)
+    lo[0] ^= (uint32_t)KECCAK_RC[r] & ms;
+    hi[0] ^= (uint32_t)(KECCAK_RC[r] >> 32) & ms;
+  }
+  if (canon) {
+    _Pragma("unroll") for (int y = 0; y < 5; ++y) st[x + 5 * y] = ((uint64_t)hi[y] << 32) | lo[y];
+  }
+}
+
+// The STROBE-128 schedule of LaneStrobe (merlin_lane.cuh) for a group: byte
+// operations by the leader lane, permutations by the whole group.
+struct GroupStrobe {
+  uint8_t* st;   // the group's 200-byte sponge (LDS)
+  uint8_t* scr;  // the group's pi scratch (LDS)
+  uint32_t gl;   // lane within the group
+  bool leader;   // gl == 1
+  uint32_t pos, pos_begin;
+
+  FE_INLINE void run_f() {
+    if (leader) {
+      st[pos] ^= (uint8_t)pos_begin;
+      st[pos + 1] ^= 0x04;
+      st[LANE_STROBE_R + 1] ^= 0x80;
+    }
+    grp_keccak((lds_u64*)st, (lds_u64*)scr, gl);
+    pos = 0;
+    pos_begin = 0;
+  }
+  FE_INLINE void absorb_byte(uint32_t b) {
+    if (leader) st[pos] ^= (uint8_t)b;
+    if (++pos == LANE_STROBE_R) run_f();
+  }
+  FE_INLINE void absorb_bytes(const uint8_t* d, uint32_t n) {
+    for (uint32_t i = 0; i < n; ++i) absorb_byte(d[i]);
+  }
+  FE_INLINE void absorb_le32(uint32_t x) {
+    absorb_byte(x & 0xffu);
+    absorb_byte((x >> 8) & 0xffu);
+    absorb_byte((x >> 16) & 0xffu);
+    absorb_byte(x >> 24);
+  }
+  // 32 bytes as 8 little-endian words (valid in the leader lane)
+  FE_INLINE void absorb32(const uint32_t w[8]) {
+    if (pos + 32 < LANE_STROBE_R) {
+      if (leader) {
+        uint32_t* d = reinterpret_cast<uint32_t*>(st) + (pos >> 2);
+        const uint32_t sh = 8 * (pos & 3);
+        if (sh == 0) {
+          _Pragma("unroll") for (int i = 0; i < 8; ++i) d[i] ^= w[i];
+        } else {
+          d[0] ^= w[0] << sh;
+          _Pragma("unroll") for (int i = 1; i < 8; ++i) d[i] ^= __builtin_amdgcn_alignbit(w[i], w[i - 1], 32 - sh);
+          d[8] ^= w[7] >> (32 - sh);
+        }
+      }
+      pos += 32;
+      return;
+    }
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) absorb_le32(w[i]);
+  }
+  FE_INLINE void begin_op(uint32_t flags) {
+    const uint32_t old_begin = pos_begin;
+    pos_begin = pos + 1;
+    absorb_byte(old_begin);
+    absorb_byte(flags);
+    if ((flags & (4u | 32u)) && pos != 0) run_f();  // FLAG_C | FLAG_K
+  }
+  FE_INLINE void meta(const char* label, uint32_t ln, uint32_t n) {
+    begin_op(16u | 2u);  // FLAG_M | FLAG_A
+    absorb_bytes(reinterpret_cast<const uint8_t*>(label), ln);
+    absorb_le32(n);
+  }
+  FE_INLINE void append32(const char* label, uint32_t ln, const uint32_t w[8]) {
+    meta(label, ln, 32);
+    begin_op(2u);  // FLAG_A
+    absorb32(w);
+  }
+  FE_INLINE void append_bytes(const char* label, uint32_t ln, const uint8_t* msg, uint32_t n) {
+    meta(label, ln, n);
+    begin_op(2u);
+    absorb_bytes(msg, n);
+  }
+  FE_INLINE void append_u64(const char* label, uint32_t ln, uint64_t x) {
+    meta(label, ln, 8);
+    begin_op(2u);
+    absorb_le32((uint32_t)x);
+    absorb_le32((uint32_t)(x >> 32));
+  }
+  // challenge_bytes(label, 64): the 16 squeezed words to out (16 x u32,
+  // written by the leader; global memory), the rate's first 64 bytes cleared
+  FE_INLINE void challenge64_to(const char* label, uint32_t ln, uint32_t* __restrict__ out, bool store) {
+    meta(label, ln, 64);
+    begin_op(1u | 2u | 4u);  // FLAG_I | FLAG_A | FLAG_C
+    if (leader) {
+      uint4* d = reinterpret_cast<uint4*>(st);
+      _Pragma("unroll") for (int i = 0; i < 4; ++i) {
+        const uint4 v = d[i];
+        if (store) reinterpret_cast<uint4*>(out)[i] = v;
+        d[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+    pos = 64;
+  }
+};

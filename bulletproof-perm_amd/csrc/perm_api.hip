@@ -231,33 +231,32 @@ std::vector<std::unique_ptr<ProverState>>& prover_states_tl() {
   static thread_local std::vector<std::unique_ptr<ProverState>> S;
   return S;
 }
-std::pair<uint8_t*, size_t>& last_stage_tl() {
-  static thread_local std::pair<uint8_t*, size_t> st{nullptr, 0};
-  return st;
-}
 std::vector<Proof>& proofs_tl();
 
 // Wipes what the last batch proved on this thread and context left of its
-// secrets: the draw templates and pi in the pinned staging arena
-// and on the device, the device workspaces holding blindings, witness and
-// the l / r vectors, the host buffers of the T-commitment inputs, and the
-// calling thread's reused prover states and proof objects (pi).  Called by
-// the production entry point (bpp_perm_prove_batch_entropy).
+// secrets: the pinned-arena spans the batch staged secrets in
+// (draw templates and pi; the witness and blindings on the host-witness path,
+// k > 768), the device workspaces holding blindings, witness and the l / r
+// vectors, the host buffers of the T-commitment inputs, and the calling
+// thread's reused prover states and proof objects (pi).  Called by the
+// production entry point (bpp_perm_prove_batch_entropy) on its context, and
+// by each sub-batch thread on its child context (BPP_PROVE_STREAMS > 1).
+static const char* const kSecretWs[] = {"pb_rng_in", "pb_gamma", "mt_s",  "pv_v",   "pv_g",    "pv_gx",  "poly_vec",
+                                        "poly_hf",   "pf_l",     "pf_r",  "ipa_am", "ipa_bm",  "ipa_am1", "ipa_bm1"};
+static const char* const kSecretHost[] = {"pp_v", "pp_g"};
 int prove_wipe(bpp_ctx* ctx) {
-  static const char* dev[] = {"pb_rng_in", "pb_gamma", "mt_s", "pv_v", "pv_g", "pv_gx", "poly_vec", "poly_hf",
-                              "pf_l", "pf_r", "ipa_am", "ipa_bm", "ipa_am1", "ipa_bm1"};
-  for (const char* n : dev) {
+  for (const char* n : kSecretWs) {
     auto it = ctx->ws.find(n);
     if (it != ctx->ws.end() && it->second.p) BPP_HIP(hipMemsetAsync(it->second.p, 0, it->second.bytes, ctx->stream));
   }
   BPP_TRY(ctx_sync(ctx));
-  for (const char* n : {"pp_v", "pp_g"}) {
+  for (const char* n : kSecretHost) {
     auto it = ctx->host_bufs.find(n);
     if (it != ctx->host_bufs.end() && it->second.first) memset(it->second.first, 0, it->second.second);
   }
-  auto& st = last_stage_tl();
-  if (st.first) memset(st.first, 0, st.second);
-  st = {nullptr, 0};
+  for (auto& st : ctx->secret_stage) memset(st.first, 0, st.second);
+  ctx->wiped.swap(ctx->secret_stage);
+  ctx->secret_stage.clear();
   for (auto& S : prover_states_tl()) {
     perm::RandomDraws& d = S->d;
     std::fill(d.pi.begin(), d.pi.end(), 0u);
@@ -267,6 +266,31 @@ int prove_wipe(bpp_ctx* ctx) {
     for (Sc& t : S->t) t = hsc::zero();
   }
   for (Proof& P : proofs_tl()) std::fill(P.pi.begin(), P.pi.end(), 0u);
+  return BPP_OK;
+}
+
+// Test hook (bpp_debug_secret_residue): nonzero bytes left in what prove_wipe
+// zeroes on ctx and its child contexts (device workspaces, host buffers, the
+// arena spans of the last wipe).
+static int secret_residue(bpp_ctx* ctx, uint64_t* nz) {
+  std::vector<uint8_t> h;
+  for (const char* n : kSecretWs) {
+    auto it = ctx->ws.find(n);
+    if (it == ctx->ws.end() || !it->second.p) continue;
+    h.resize(it->second.bytes);
+    BPP_HIP(hipMemcpy(h.data(), it->second.p, h.size(), hipMemcpyDeviceToHost));
+    for (uint8_t b : h) *nz += b != 0;
+  }
+  for (const char* n : kSecretHost) {
+    auto it = ctx->host_bufs.find(n);
+    if (it == ctx->host_bufs.end() || !it->second.first) continue;
+    const uint8_t* b = (const uint8_t*)it->second.first;
+    for (size_t i = 0; i < it->second.second; ++i) *nz += b[i] != 0;
+  }
+  for (auto& st : ctx->wiped)
+    for (size_t i = 0; i < st.second; ++i) *nz += st.first[i] != 0;
+  for (bpp_ctx* kid : ctx->children)
+    if (kid) BPP_TRY(secret_residue(kid, nz));
   return BPP_OK;
 }
 
@@ -324,7 +348,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     // read in place instead, by k_draws through LDS, measured within noise)
     uint8_t* stage = nullptr;
     BPP_TRY(ctx_h2d_stage(ctx, P * tlen + (size_t)P * k * 4, &stage));
-    last_stage_tl() = {stage, P * tlen + (size_t)P * k * 4};  // (prove_wipe)
+    ctx->secret_stage.emplace_back(stage, P * tlen + (size_t)P * k * 4);  // (prove_wipe)
     uint8_t* pis = stage + P * tlen;
     par::for_each((P + 7) / 8, [&](size_t gi) {
       perm::Seed sd[8];
@@ -507,6 +531,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     uint8_t* stg = nullptr;  // (host witness only) written in place in the pinned arena
     if (!dev_witness) {
       BPP_TRY(ctx_h2d_stage(ctx, (size_t)P * hostw * 32, &stg));
+      ctx->secret_stage.emplace_back(stg, (size_t)P * hostw * 32);  // (prove_wipe)
       par::for_each(P, [&](size_t p) {
         ProverState& st = *S[p];
         Sc* o = reinterpret_cast<Sc*>(stg) + p * hostw;
@@ -817,6 +842,13 @@ struct bpp_verify_job {
   bool dev = false;
   bpp_ctx* dctx = nullptr;
   uint64_t dgen = 0;
+  // sliced device job (bpp_perm_verify_begin_dev_slice): all `count` proofs
+  // uploaded and their points decompressed, only [rfirst, rfirst + rcount)
+  // replayed (records and rs of that slice); a whole job has rcount = count
+  size_t rfirst = 0, rcount = 0;
+  // the inverses of the replay's wave products (one per 64 proofs of the
+  // replayed slice, canonical; verify_replay_dev's wtot, inverted on the host)
+  std::vector<Sc> winv;
 };
 
 namespace {
@@ -1033,19 +1065,26 @@ int verify_partial(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J, con
 // independent of the replay: the 64 replay waves are latency-bound, the
 // decompression throughput-bound).  BPP_ERR_VERIFY if the replay rejects a
 // proof; an undecodable point is reported by verify_partial_dev.
+// rfirst / rcount: replay only that slice (the points of all count proofs
+// are still decompressed; rcount = SIZE_MAX: all of them).
 int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label, size_t llen, size_t count,
-                     const uint8_t* proofs, const uint8_t* V, std::unique_ptr<bpp_verify_job>& job) {
+                     const uint8_t* proofs, const uint8_t* V, std::unique_ptr<bpp_verify_job>& job,
+                     size_t rfirst = 0, size_t rcount = SIZE_MAX) {
   job.reset(new bpp_verify_job);
   bpp_verify_job& J = *job;
+  if (rcount == SIZE_MAX) rcount = count;
   J.C = C;
   J.count = count;
   J.npt = vpts_n(C);
-  J.rs.resize(count);
+  J.rfirst = rfirst;
+  J.rcount = rcount;
+  J.rs.resize(rcount);
   J.dev = true;
   J.dctx = ctx;
+  // (before the generation: a refused call supersedes nothing)
+  if (count > (1u << 26) || rfirst > count || rcount > count - rfirst) return BPP_ERR_ARG;
   J.dgen = ++ctx->vjob_gen;
   if (!count) return BPP_OK;
-  if (count > (1u << 26)) return BPP_ERR_ARG;
   const size_t plen = perm::proof_len(C.k), vbytes = (size_t)C.m * 32, npts = count * J.npt;
   bpp_ctx* kid = nullptr;
   BPP_TRY(ctx_child(ctx, VJ_CHILD, &kid));
@@ -1062,29 +1101,151 @@ int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label,
   HostScope hs(ctx, "verify_replay");
   const uint32_t* d_pf = (const uint32_t*)d_in;
   const uint32_t* d_V = (const uint32_t*)((uint8_t*)d_in + count * plen);
-  BPP_TRY(ctx_ws(ctx, "vj_rec", count * vrec_n(C) * 32, &d_rec));
+  // (+1: the pad record of k_verify_replay's lanes past the batch)
+  BPP_TRY(ctx_ws(ctx, "vj_rec", (count + 1) * vrec_n(C) * 32, &d_rec));
   BPP_TRY(ctx_ws(ctx, "vj_x", npts * MSM_NIELS_WORDS * 4, &d_x));
   BPP_TRY(ctx_ws(ctx, "vj_dbad", 8, &d_dbad));
   BPP_HIP(hipMemsetAsync(d_dbad, 0xff, 8, ctx->stream));
-  BPP_HIP(hipEventRecord(ctx->vj_ev_in, ctx->stream));
-  BPP_HIP(hipStreamWaitEvent(kid->stream, ctx->vj_ev_in, 0));
-  BPP_TRY(verify_decompress_dev(kid, C, (uint32_t)count, d_pf, d_V, (uint32_t*)d_x, (unsigned long long*)d_dbad));
-  BPP_HIP(hipEventRecord(ctx->vj_ev_dec, kid->stream));
-  ctx->vj_dec_pending = true;
+  // decompression order (BPP_VERIFY_DEC, A/B): 0 = launched beside the
+  // replay before it, 1 = launched after the replay's launch (beside it),
+  // 2 = after the replay completes (it then overlaps the host weights and
+  // k_verify_scalars instead)
+  static const int dec_order = [] {
+    const char* e = getenv("BPP_VERIFY_DEC");
+    return e ? atoi(e) : 0;
+  }();
+  auto launch_dec = [&]() -> int {
+    BPP_HIP(hipEventRecord(ctx->vj_ev_in, ctx->stream));
+    BPP_HIP(hipStreamWaitEvent(kid->stream, ctx->vj_ev_in, 0));
+    BPP_TRY(verify_decompress_dev(kid, C, (uint32_t)count, d_pf, d_V, (uint32_t*)d_x, (unsigned long long*)d_dbad));
+    BPP_HIP(hipEventRecord(ctx->vj_ev_dec, kid->stream));
+    ctx->vj_dec_pending = true;
+    return BPP_OK;
+  };
+  if (dec_order == 0 || !rcount) BPP_TRY(launch_dec());
   uint32_t *h_init = nullptr, *h_r = nullptr, *h_bad = nullptr;
   {
     uint32_t init[52];
     verify_init_state(C, label, llen, init);
     BPP_TRY(ctx_zc_in(ctx, "vj_init", init, sizeof init, &h_init));
   }
-  BPP_TRY(ctx_zc_out(ctx, "vj_r", count * 32, &h_r));
-  BPP_TRY(ctx_zc_out(ctx, "vj_bad", count * 4, &h_bad));
-  BPP_TRY(verify_replay_dev(ctx, C, (uint32_t)count, h_init, d_pf, d_V, (uint32_t*)d_rec, h_r, h_bad));
+  if (!rcount) return ctx_sync(ctx);
+  const size_t nw = (rcount + 63) / 64;
+  void* d_inv = nullptr;
+  uint32_t* h_wtot = nullptr;
+  BPP_TRY(ctx_ws(ctx, "vj_inv", (rcount + 1) * (1 + (size_t)C.lg) * 32, &d_inv));
+  BPP_TRY(ctx_zc_out(ctx, "vj_wtot", nw * 32, &h_wtot));
+  BPP_TRY(ctx_zc_out(ctx, "vj_r", rcount * 32, &h_r));
+  BPP_TRY(ctx_zc_out(ctx, "vj_bad", rcount * 4, &h_bad));
+  if (dec_order == 1) {  // (the event is recorded before the replay: the decompression waits for the upload only)
+    BPP_HIP(hipEventRecord(ctx->vj_ev_in, ctx->stream));
+  }
+  BPP_TRY(verify_replay_dev(ctx, C, (uint32_t)rcount, h_init, d_pf + rfirst * (plen / 4),
+                            d_V + rfirst * (vbytes / 4), (uint32_t*)d_rec, (uint32_t*)d_inv, h_wtot, h_r, h_bad));
+  if (dec_order == 1) {
+    BPP_HIP(hipStreamWaitEvent(kid->stream, ctx->vj_ev_in, 0));
+    BPP_TRY(verify_decompress_dev(kid, C, (uint32_t)count, d_pf, d_V, (uint32_t*)d_x, (unsigned long long*)d_dbad));
+    BPP_HIP(hipEventRecord(ctx->vj_ev_dec, kid->stream));
+    ctx->vj_dec_pending = true;
+  } else if (dec_order == 2) {
+    BPP_TRY(launch_dec());
+  }
   BPP_TRY(ctx_sync(ctx));
   uint32_t any = 0;
-  for (size_t p = 0; p < count; ++p) any |= h_bad[p];
+  for (size_t p = 0; p < rcount; ++p) any |= h_bad[p];
   if (any) return BPP_ERR_VERIFY;
-  memcpy(J.rs.data(), h_r, count * 32);
+  memcpy(J.rs.data(), h_r, rcount * 32);
+  // the wave products' inverses: one host batch inversion for all waves
+  // (the products are nonzero: zero challenges entered them as 1)
+  J.winv.resize(nw);
+  memcpy(J.winv.data(), h_wtot, nw * 32);
+  hsc::batch_invert(J.winv, false);
+  return BPP_OK;
+}
+
+// The device inversion state of a device job for verify_weights_dev: the
+// replay's workspace and J's wave inverses in a zero-copy buffer.
+static int job_inv_state(bpp_ctx* ctx, const bpp_verify_job& J, uint32_t** d_inv, uint32_t** h_winv) {
+  void* d = nullptr;
+  BPP_TRY(ctx_ws(ctx, "vj_inv", (J.rcount + 1) * (1 + (size_t)J.C.lg) * 32, &d));
+  *d_inv = (uint32_t*)d;
+  return ctx_zc_in(ctx, "vj_winv", J.winv.data(), J.winv.size() * 32, h_winv);
+}
+
+// A sliced job's scalars (bpp_perm_verify_slice_scalars): weights of the
+// slice's proofs from all `total` r challenges (batch index rfirst + p), the
+// generator scalars summed over the slice and the slice's proof-point
+// scalars -> d_out = [NG | rcount x npt] x 32 B (device memory).
+int verify_slice_scalars_dev(bpp_ctx* ctx, const bpp_verify_job& J, const Sc* r_all, size_t total, uint32_t* d_out) {
+  if (J.dctx != ctx || J.dgen != ctx->vjob_gen) {
+    ctx->err = "device verify job belongs to another context or was superseded by a later begin";
+    return BPP_ERR_ARG;
+  }
+  if (total < J.rfirst + J.rcount) return BPP_ERR_ARG;
+  if (!J.rcount) {  // an empty slice adds nothing to the generator scalars
+    BPP_HIP(hipMemsetAsync(d_out, 0, (2 * (size_t)J.C.n_p + 2) * 32, ctx->stream));
+    return ctx_sync(ctx);
+  }
+  void* d_rec = nullptr;
+  BPP_TRY(ctx_ws(ctx, "vj_rec", J.rcount * vrec_n(J.C) * 32, &d_rec));
+  uint8_t seed[32] = {0};
+  if (total > 1) perm::batch_seed(r_all, total, seed);
+  uint32_t* h_seed = nullptr;
+  BPP_TRY(ctx_zc_in(ctx, "vj_seed", seed, 32, &h_seed));
+  uint32_t *d_inv = nullptr, *h_winv = nullptr;
+  BPP_TRY(job_inv_state(ctx, J, &d_inv, &h_winv));
+  BPP_TRY(verify_weights_dev(ctx, J.C, (uint32_t)J.rcount, J.rfirst, total, h_seed, (uint32_t*)d_rec, d_inv,
+                             h_winv));
+  BPP_TRY(verify_scalars_dev_rec(ctx, J.C, (uint32_t)J.rcount, (const uint32_t*)d_rec, d_out));
+  return ctx_sync(ctx);
+}
+
+// The MSM of a sliced job over windows [wb, we) with the scalars of every
+// slice gathered (bpp_perm_verify_partial_gathered): block r (stride bytes
+// apart) holds slice r's [NG | counts[r] x npt]; the generator scalars are
+// the sum of the blocks' NG heads, the proof-point scalars the blocks' tails
+// in slice (= proof) order.
+int verify_partial_gathered_dev(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J, const uint8_t* d_blocks,
+                                size_t stride, const size_t* counts, size_t nslices, uint32_t wb, uint32_t we,
+                                h25519::ge* out) {
+  if (J.dctx != ctx || J.dgen != ctx->vjob_gen) {
+    ctx->err = "device verify job belongs to another context or was superseded by a later begin";
+    return BPP_ERR_ARG;
+  }
+  if (G->n < J.C.n_p) {
+    ctx->err = "generators shorter than the padded circuit";
+    return BPP_ERR_LEN;
+  }
+  const size_t NG = 2 * (size_t)J.C.n_p + 2, npt = J.npt, T = NG + J.count * npt;
+  size_t sum = 0;
+  for (size_t r = 0; r < nslices; ++r) {
+    if ((NG + counts[r] * npt) * 32 > stride) return BPP_ERR_ARG;
+    sum += counts[r];
+  }
+  if (sum != J.count || stride % 16) return BPP_ERR_ARG;
+  void *d_sv = nullptr, *d_x = nullptr, *d_dbad = nullptr;
+  BPP_TRY(ctx_ws(ctx, "pv_s", T * 32 + 32, &d_sv));
+  BPP_TRY(ctx_ws(ctx, "vj_x", J.count * npt * MSM_NIELS_WORDS * 4, &d_x));
+  BPP_TRY(ctx_ws(ctx, "vj_dbad", 8, &d_dbad));
+  BPP_TRY(verify_sum_blocks_dev(ctx, (uint32_t)nslices, (uint32_t)NG, (const uint32_t*)d_blocks,
+                                (uint32_t)(stride / 4), (uint32_t*)d_sv));
+  size_t off = NG;
+  for (size_t r = 0; r < nslices; ++r) {
+    if (counts[r])
+      BPP_HIP(hipMemcpyAsync((uint8_t*)d_sv + off * 32, d_blocks + r * stride + NG * 32, counts[r] * npt * 32,
+                             hipMemcpyDeviceToDevice, ctx->stream));
+    off += counts[r] * npt;
+  }
+  uint64_t* h_dbad = nullptr;
+  BPP_TRY(ctx_zc_out(ctx, "vj_dbad_h", 8, (uint32_t**)&h_dbad));
+  BPP_HIP(hipStreamWaitEvent(ctx->stream, ctx->vj_ev_dec, 0));
+  BPP_HIP(hipMemcpyAsync(h_dbad, d_dbad, 8, hipMemcpyDeviceToHost, ctx->stream));
+  BPP_TRY(verify_msm(ctx, G, J.C, J.count, (const uint32_t*)d_sv, (const uint32_t*)d_x, wb, we, out));
+  BPP_TRY(ctx_sync(ctx));
+  if (*h_dbad != ~0ull) {
+    ctx->err = "undecodable proof point at index " + std::to_string(*h_dbad);
+    return BPP_ERR_VERIFY;
+  }
   return BPP_OK;
 }
 
@@ -1095,6 +1256,10 @@ int verify_partial_dev(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J,
                        size_t first, uint32_t wb, uint32_t we, h25519::ge* out) {
   if (J.dctx != ctx || J.dgen != ctx->vjob_gen) {
     ctx->err = "device verify job belongs to another context or was superseded by a later begin";
+    return BPP_ERR_ARG;
+  }
+  if (J.rcount != J.count) {
+    ctx->err = "a sliced verify job takes bpp_perm_verify_slice_scalars / _partial_gathered";
     return BPP_ERR_ARG;
   }
   if (G->n < J.C.n_p) {
@@ -1114,7 +1279,9 @@ int verify_partial_dev(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J,
     if (total > 1) perm::batch_seed(r_all, total, seed);
     uint32_t* h_seed = nullptr;
     BPP_TRY(ctx_zc_in(ctx, "vj_seed", seed, 32, &h_seed));
-    BPP_TRY(verify_weights_dev(ctx, J.C, (uint32_t)count, first, total, h_seed, (uint32_t*)d_rec));
+    uint32_t *d_inv = nullptr, *h_winv = nullptr;
+    BPP_TRY(job_inv_state(ctx, J, &d_inv, &h_winv));
+    BPP_TRY(verify_weights_dev(ctx, J.C, (uint32_t)count, first, total, h_seed, (uint32_t*)d_rec, d_inv, h_winv));
     BPP_TRY(verify_scalars_dev_rec(ctx, J.C, (uint32_t)count, (const uint32_t*)d_rec, (uint32_t*)d_sv));
   }
   uint64_t* h_dbad = nullptr;  // the decompression's verdict, copied behind the MSM
@@ -1178,8 +1345,11 @@ std::vector<Proof>& proofs_tl() {
 }
 }  // namespace
 
+// wipe: prove_wipe after the batch, on ctx (this thread) and on every child
+// context inside its sub-batch thread (whose prover states are its own)
 static int prove_batch_api(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, const std::vector<perm::Seed>& seeds,
-                           const uint8_t* label, size_t llen, uint8_t* proofs_out, uint8_t* V_out) {
+                           const uint8_t* label, size_t llen, uint8_t* proofs_out, uint8_t* V_out,
+                           bool wipe = false) {
   const size_t count = seeds.size();
   if (!count) return BPP_OK;
   const perm::Circuit C = perm::build(k);
@@ -1219,10 +1389,16 @@ static int prove_batch_api(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, const st
           return;
         }
         std::vector<Proof> sub;
-        rcs[s] = prove_batch(kc, G, C, std::vector<perm::Seed>(seeds.begin() + b, seeds.begin() + e), label,
-                             llen, sub);
+        std::vector<perm::Seed> part(seeds.begin() + b, seeds.begin() + e);
+        rcs[s] = prove_batch(kc, G, C, part, label, llen, sub);
         if (rcs[s] == BPP_OK)
           for (size_t i = b; i < e; ++i) Ps[i] = std::move(sub[i - b]);
+        if (wipe) {
+          for (perm::Seed& x : part) memset(x.b, 0, sizeof x.b);
+          for (Proof& q : sub) std::fill(q.pi.begin(), q.pi.end(), 0u);
+          const int w = prove_wipe(kc);
+          if (rcs[s] == BPP_OK) rcs[s] = w;
+        }
       });
     for (auto& t : th) t.join();
     // (the children's stage times fold into ctx's on its next profile query)
@@ -1273,11 +1449,21 @@ int bpp_perm_prove_batch_entropy(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, si
     }
     std::vector<perm::Seed> sd(count);
     for (size_t i = 0; i < count; ++i) sd[i] = perm::Seed::bytes32(seeds32 + 32 * i);
-    int rc = prove_batch_api(ctx, G, k, sd, label, llen, proofs_out, V_out);
+    int rc = prove_batch_api(ctx, G, k, sd, label, llen, proofs_out, V_out, true);
     if (!ent.empty()) memset(ent.data(), 0, ent.size());
     for (perm::Seed& x : sd) memset(x.b, 0, sizeof x.b);
     const int wrc = prove_wipe(ctx);
     return rc ? rc : wrc;
+  });
+}
+
+int bpp_debug_secret_residue(bpp_ctx* ctx, uint64_t* nonzero_bytes) {
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !nonzero_bytes) return BPP_ERR_ARG;
+    BPP_HIP(hipSetDevice(ctx->device));
+    BPP_TRY(ctx_sync(ctx));
+    *nonzero_bytes = 0;
+    return secret_residue(ctx, nonzero_bytes);
   });
 }
 
@@ -1359,6 +1545,57 @@ int bpp_perm_verify_scalars(const bpp_verify_job* job, const uint8_t* r_all, siz
     BPP_TRY(verify_terms_weighted(*job, rs.data(), total, first, sc, enc));
     for (size_t i = 0; i < sc.size(); ++i) hsc::to_bytes(scalars_out + 32 * i, sc[i]);
     if (!enc.empty()) memcpy(points_out, enc.data(), enc.size());
+    return BPP_OK;
+  });
+}
+
+int bpp_perm_verify_begin_dev_slice(bpp_ctx* ctx, uint32_t k, size_t count, const uint8_t* label, size_t llen,
+                                    const uint8_t* proofs, const uint8_t* V, size_t first, size_t n, uint8_t* r_out,
+                                    bpp_verify_job** out) {
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !out || ((!proofs || !V) && count) || (!label && llen) || k < 2 || k > (1u << 20) ||
+        first > count || n > count - first)
+      return BPP_ERR_ARG;
+    *out = nullptr;
+    BPP_HIP(hipSetDevice(ctx->device));
+    const perm::Circuit C = perm::build(k);
+    std::unique_ptr<bpp_verify_job> job;
+    BPP_TRY(verify_begin_dev(ctx, C, label, llen, count, proofs, V, job, first, n));
+    if (r_out && n) memcpy(r_out, job->rs.data(), 32 * n);
+    *out = job.release();
+    return BPP_OK;
+  });
+}
+
+size_t bpp_perm_verify_slice_bytes(const bpp_verify_job* job) {
+  return job ? (2 * (size_t)job->C.n_p + 2 + job->rcount * job->npt) * 32 : 0;
+}
+
+int bpp_perm_verify_slice_scalars(bpp_ctx* ctx, const bpp_verify_job* job, const uint8_t* r_all, size_t total,
+                                  void* d_out) {
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !job || !d_out || (!r_all && total) || !job->dev) return BPP_ERR_ARG;
+    std::vector<Sc> rs;
+    BPP_TRY(parse_rs(r_all, total, rs));
+    BPP_HIP(hipSetDevice(ctx->device));
+    return verify_slice_scalars_dev(ctx, *job, rs.data(), total, (uint32_t*)d_out);
+  });
+}
+
+int bpp_perm_verify_partial_gathered(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job* job,
+                                     const void* d_blocks, size_t stride, const size_t* counts, size_t nslices,
+                                     uint32_t w_begin, uint32_t w_end, uint8_t partial[128]) {
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !G || !job || !partial || !job->dev || (!d_blocks && nslices) || (!counts && nslices))
+      return BPP_ERR_ARG;
+    const uint32_t c = msm_choose_c((double)verify_terms(*job));
+    if (w_begin > w_end || w_end > (254 + c - 1) / c) return BPP_ERR_ARG;
+    BPP_HIP(hipSetDevice(ctx->device));
+    h25519::ge r = h25519::ge_identity();
+    if (job->count)
+      BPP_TRY(verify_partial_gathered_dev(ctx, G, *job, (const uint8_t*)d_blocks, stride, counts, nslices, w_begin,
+                                          w_end, &r));
+    h25519::ge_to_words((uint32_t*)partial, r);
     return BPP_OK;
   });
 }

@@ -28,13 +28,16 @@ inline uint32_t vpts_n(const perm::Circuit& C) { return C.m + 8 + 2 * C.lg; }
 // (k_verify_replay): d_proofs [count][proof_len] and d_V [count][m][32] on
 // the device; init = the 52-word transcript state every proof shares (the
 // label's Transcript::new and arithmetic_domain_sep(n_p); verify_init_state).
-// Writes d_rec (weights left zero), r_out ([count][32], the t-check
-// weight challenges) and bad ([count] u32, nonzero where a point is the identity encoding, a
-// scalar is not canonical or a challenge is zero).  r_out and bad may be
-// pinned host memory (written in place).
+// Writes d_rec (weights, y^-1 and the u_j^-1 left for verify_weights_dev),
+// d_inv ([count + 1][1 + lg] scalars: the inversion state), wtot
+// ([ceil(count / 64)][32]: each wave's product, for the host to invert),
+// r_out ([count][32], the t-check weight challenges) and bad ([count] u32,
+// nonzero where a point is the identity encoding, a scalar is not canonical
+// or a challenge is zero).  wtot, r_out and bad may be pinned host memory
+// (written in place).
 int verify_replay_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const uint32_t* d_init,
-                      const uint32_t* d_proofs, const uint32_t* d_V, uint32_t* d_rec, uint32_t* r_out,
-                      uint32_t* bad);
+                      const uint32_t* d_proofs, const uint32_t* d_V, uint32_t* d_rec, uint32_t* d_inv,
+                      uint32_t* wtot, uint32_t* r_out, uint32_t* bad);
 // Decompresses every proof point of the uploaded proofs / V into d_tbl
 // ([count * vpts_n] Niels rows in MSM order); *d_bad = the smallest index of
 // an undecodable encoding (set to ~0 by the caller first).  Independent of
@@ -44,9 +47,16 @@ int verify_decompress_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, 
 // The 52-word shared transcript prefix for verify_replay_dev.
 void verify_init_state(const perm::Circuit& C, const uint8_t* label, size_t llen, uint32_t out[52]);
 // rec[p][VREC_WT] = perm::batch_weight(seed, first + p) for p < count (one
-// for total <= 1).  seed: 8 words, may be pinned host memory.
+// for total <= 1); with d_inv / winv (a device replay: d_inv as
+// verify_replay_dev left it, winv = the inverses of its wave products) also
+// rec[p]'s y^-1 and u_j^-1.  seed and winv may be pinned host memory.
 int verify_weights_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, uint64_t first, uint64_t total,
-                       const uint32_t* seed, uint32_t* d_rec);
+                       const uint32_t* seed, uint32_t* d_rec, const uint32_t* d_inv = nullptr,
+                       const uint32_t* winv = nullptr);
+// out[i] = sum over the nb blocks (stride words apart) of block[b][i], i < n
+// (the generator scalars of a gathered sliced verification).
+int verify_sum_blocks_dev(bpp_ctx* ctx, uint32_t nb, uint32_t n, const uint32_t* d_blocks, uint32_t stride,
+                          uint32_t* d_out);
 // k_verify_scalars + k_verify_merge over device records (poly.hip).
 int verify_scalars_dev_rec(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const uint32_t* d_rec,
                            uint32_t* d_sc);

@@ -12,6 +12,7 @@
 // ms on the round-2 box, 4 host threads); here 4096 proofs are 64 waves.
 #include "ctx.h"
 #include "ge_io.cuh"
+#include "merlin_group.cuh"
 #include "merlin_lane.cuh"
 #include "verify_dev.h"
 
@@ -33,39 +34,71 @@ FE_INLINE bool w8_zero(const uint32_t w[8]) {
 // Proof layout (perm_api.hip serialize, bpp_perm_proof_len): A_I A_O S T1 T3
 // T4 T5 T6 (points), tau_x mu t_hat, L_0 R_0 .. L_{lg-1} R_{lg-1}, a b;
 // 8 words each.
-__global__ void __launch_bounds__(64) k_verify_replay(uint32_t count, uint32_t k, uint32_t lg, uint32_t n_p,
-                                                      const uint32_t* __restrict__ init,
-                                                      const uint32_t* __restrict__ proofs, uint32_t pw,
-                                                      const uint32_t* __restrict__ V, uint32_t* __restrict__ rec,
-                                                      uint32_t* __restrict__ r_out, uint32_t* __restrict__ bad) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[64 * LANE_ST_BYTES];
-  // every lane stays active for the wave-wide inversion below: lanes past
-  // the batch shadow the last proof and write nothing
-  const bool live = blockIdx.x * 64 + threadIdx.x < count;
-  const uint32_t p = live ? blockIdx.x * 64 + threadIdx.x : count - 1;
-  LaneStrobe t;
-  t.st = lds + threadIdx.x * LANE_ST_BYTES;
+// ---------------------------------------------------------------------------
+// Group replay (round 4, the default): one transcript per 8 lanes
+// (merlin_group.cuh), 8 transcripts per 64-lane block, so a 4096-proof batch
+// is 512 waves whose permutations cost ~65 instructions a round instead of
+// ~190.  The replay keeps only the transcript chain: every challenge's 64
+// squeezed bytes go to ch ([count + 1][6 + lg][16] words, the last a pad for
+// groups past the batch) and the proof's encoding / canonical-scalar checks to
+// okw[p]; k_verify_replay_post reduces the challenges, inverts y and the u_j
+// and writes the records, one lane per proof.  STAGED: the group's proof and
+// V bytes are first copied into LDS by its 8 lanes (one load latency instead
+// of one per absorbed item).
+#define RG_GROUPS 8
+#define RG_SP 208  // sponge / scratch stride (16-B aligned)
+template <bool STAGED>
+__global__ void __launch_bounds__(64) k_verify_replay_g(uint32_t count, uint32_t k, uint32_t lg, uint32_t n_p,
+                                                        const uint32_t* __restrict__ init,
+                                                        const uint32_t* __restrict__ proofs, uint32_t pw,
+                                                        const uint32_t* __restrict__ V, uint32_t* __restrict__ ch,
+                                                        uint32_t* __restrict__ okw) {
+  __shared__ __attribute__((aligned(16))) uint8_t sp[RG_GROUPS * 2 * RG_SP];
+  extern __shared__ __attribute__((aligned(16))) uint32_t stage[];  // STAGED: [8][pw + 8 m]
+  // the replay is a latency chain and the proof-point decompression runs
+  // beside it on the same SIMDs: win the issue arbitration
+  __builtin_amdgcn_s_setprio(3);
+  const uint32_t g = threadIdx.x >> 3, gl = threadIdx.x & 7;
+  const uint32_t pg = blockIdx.x * RG_GROUPS + g;
+  const bool live = pg < count;
+  const uint32_t p = live ? pg : count - 1;
+  const uint32_t m = 2 * k + 1, nch = 6 + lg;
+  GroupStrobe t;
+  t.st = sp + g * 2 * RG_SP;
+  t.scr = t.st + RG_SP;
+  t.gl = gl;
+  t.leader = gl == 1;
   {
     uint32_t* d = reinterpret_cast<uint32_t*>(t.st);
-    for (int i = 0; i < 50; ++i) d[i] = init[i];
+    for (uint32_t i = gl; i < 50; i += GRP_LANES) d[i] = init[i];
     t.pos = init[50];
     t.pos_begin = init[51];
   }
-  const uint32_t m = 2 * k + 1, nrec = VREC_U + 2 * lg;
-  uint32_t* __restrict__ R = rec + (size_t)p * nrec * 8;
-  const uint32_t* __restrict__ PV = V + (size_t)p * m * 8;
-  const uint32_t* __restrict__ PP = proofs + (size_t)p * pw;
+  const uint32_t* PV;
+  const uint32_t* PP;
+  if (STAGED) {
+    uint32_t* sg = stage + (size_t)g * (pw + 8 * m);
+    const uint4* sp4 = reinterpret_cast<const uint4*>(proofs + (size_t)p * pw);
+    for (uint32_t i = gl; i < pw / 4; i += GRP_LANES) reinterpret_cast<uint4*>(sg)[i] = sp4[i];
+    const uint4* sv4 = reinterpret_cast<const uint4*>(V + (size_t)p * m * 8);
+    for (uint32_t i = gl; i < 2 * m; i += GRP_LANES) reinterpret_cast<uint4*>(sg + pw)[i] = sv4[i];
+    PP = sg;
+    PV = sg + pw;
+  } else {
+    PP = proofs + (size_t)p * pw;
+    PV = V + (size_t)p * m * 8;
+  }
+  GRP_FENCE();
+  uint32_t* CH = ch + (size_t)(live ? p : count) * nch * 16;
   uint32_t w[8];
   bool ok = true;
-  // V_0 .. V_{2k-1}, x_perm, V_2k
   for (uint32_t j = 0; j < 2 * k; ++j) {
     ld8(PV + 8 * j, w);
     t.append32("V", 1, w);
   }
-  const sc x_perm = t.challenge_scalar("x_perm", 6);
+  t.challenge64_to("x_perm", 6, CH, true);
   ld8(PV + 16 * k, w);
   t.append32("V", 1, w);
-  // A_I, A_O, S (validated), y, z
   ld8(PP, w);
   ok &= !w8_zero(w);
   t.append32("A_I", 3, w);
@@ -75,9 +108,8 @@ __global__ void __launch_bounds__(64) k_verify_replay(uint32_t count, uint32_t k
   ld8(PP + 16, w);
   ok &= !w8_zero(w);
   t.append32("S", 1, w);
-  const sc y = t.challenge_scalar("y", 1);
-  const sc z = t.challenge_scalar("z", 1);
-  // T1, T3..T6 (validated), x
+  t.challenge64_to("y", 1, CH + 16, true);
+  t.challenge64_to("z", 1, CH + 32, true);
   auto T_i = [&](int i, const char* lab) {
     ld8(PP + 24 + 8 * i, w);
     ok &= !w8_zero(w);
@@ -88,18 +120,17 @@ __global__ void __launch_bounds__(64) k_verify_replay(uint32_t count, uint32_t k
   T_i(2, "T4");
   T_i(3, "T5");
   T_i(4, "T6");
-  const sc x = t.challenge_scalar("x", 1);
-  // tau_x, mu, t_hat (canonical scalars), w
-  sc taux, mu, that;
-  ld8(PP + 64, taux.v);
-  ld8(PP + 72, mu.v);
-  ld8(PP + 80, that.v);
-  ok &= !sc_geq_l(taux.v) && !sc_geq_l(mu.v) && !sc_geq_l(that.v);
-  t.append32("TX", 2, taux.v);
-  t.append32("mu", 2, mu.v);
-  t.append32("t", 1, that.v);
-  const sc wch = t.challenge_scalar("w", 1);
-  // bulletproofs InnerProductProof::verification_scalars, transcript part
+  t.challenge64_to("x", 1, CH + 48, true);
+  ld8(PP + 64, w);
+  ok &= !sc_geq_l(w);
+  t.append32("TX", 2, w);
+  ld8(PP + 72, w);
+  ok &= !sc_geq_l(w);
+  t.append32("mu", 2, w);
+  ld8(PP + 80, w);
+  ok &= !sc_geq_l(w);
+  t.append32("t", 1, w);
+  t.challenge64_to("w", 1, CH + 64, true);
   t.append_bytes("dom-sep", 7, reinterpret_cast<const uint8_t*>("ipp v1"), 6);
   t.append_u64("n", 1, n_p);
   const uint32_t* PL = PP + 88;
@@ -110,45 +141,90 @@ __global__ void __launch_bounds__(64) k_verify_replay(uint32_t count, uint32_t k
     ld8(PL + 16 * j + 8, w);
     ok &= !w8_zero(w);
     t.append32("R", 1, w);
-    const sc u = t.challenge_scalar("u", 1);
-    ok &= !w8_zero(u.v);  // (a zero challenge would fail the batch inversion)
-    sc_store(R + 8 * (VREC_U + j), u);
+    t.challenge64_to("u", 1, CH + 16 * (5 + j), true);
   }
-  sc a, b;
-  ld8(PL + 16 * lg, a.v);
-  ld8(PL + 16 * lg + 8, b.v);
-  ok &= !sc_geq_l(a.v) && !sc_geq_l(b.v);
-  const sc r = t.challenge_scalar("t-check-weight", 14);
+  ld8(PL + 16 * lg, w);
+  ok &= !sc_geq_l(w);
+  ld8(PL + 16 * lg + 8, w);
+  ok &= !sc_geq_l(w);
+  t.challenge64_to("t-check-weight", 14, CH + 16 * (5 + lg), true);
+  if (live && t.leader) okw[p] = ok ? 1u : 0u;
+}
+
+// One lane per proof: the challenges of k_verify_replay_g reduced mod l (the
+// verifier's challenge_scalar, transcript_protocol.rs:62-67) and the records
+// except y^-1 and the u_j^-1.  Those come from ONE inversion per wave of 64
+// proofs (Montgomery's trick: the lane's product y u_0 .. u_{lg-1}, then the
+// wave's): this kernel leaves the lane's prefix products and the product of
+// the other 63 lanes' totals in inv_st ([count + 1][1 + lg], Montgomery) and
+// the wave's total in wtot[wave] (canonical); the host inverts the wave
+// totals (one batch inversion, perm_api.hip verify_begin_dev) and
+// k_verify_weights finishes the inverses.  A binary-Euclid inversion on the
+// device cost a wave ~310 K cycles (129 us, tools/ubench/keccak_grp.hip), the
+// largest part of this step.  A zero y or u (a rejected proof) enters the
+// products as 1.  Lanes past the batch shadow the last proof and keep to the
+// pad entries.
+__global__ void __launch_bounds__(64) k_verify_replay_post(uint32_t count, uint32_t lg,
+                                                           const uint32_t* __restrict__ ch,
+                                                           const uint32_t* __restrict__ okw,
+                                                           const uint32_t* __restrict__ proofs, uint32_t pw,
+                                                           uint32_t* __restrict__ rec, uint32_t* __restrict__ inv_st,
+                                                           uint32_t* __restrict__ wtot, uint32_t* __restrict__ r_out,
+                                                           uint32_t* __restrict__ bad) {
+  const bool live = blockIdx.x * 64 + threadIdx.x < count;
+  const uint32_t p = live ? blockIdx.x * 64 + threadIdx.x : count - 1;
+  const uint32_t nch = 6 + lg, nrec = VREC_U + 2 * lg;
+  const uint32_t* __restrict__ CH = ch + (size_t)p * nch * 16;
+  uint32_t* __restrict__ R = rec + (size_t)(live ? p : count) * nrec * 8;
+  uint32_t* __restrict__ IS = inv_st + (size_t)(live ? p : count) * (1 + lg) * 8;
+  const uint32_t* __restrict__ PP = proofs + (size_t)p * pw;
+  bool ok = okw[p] != 0;
+  const sc y = sc_from_wide_w(CH + 16);
   ok &= !w8_zero(y.v);
-  // y^-1 and u_j^-1: Montgomery's trick over the lane's own values (the u^-1
-  // slots hold the prefix products meanwhile), then over the wave's 64 lane
-  // products, so the wave runs ONE inversion with uniform control flow (a
-  // per-lane binary-Euclid inversion diverged and took 0.43 of the kernel's
-  // 1.08 ms at 4096 proofs)
-  sc acc = sc_to_mont(y);
+  auto nz = [](const sc& v) {
+    sc o = v;
+    if (w8_zero(v.v)) o.v[0] = 1;
+    return o;
+  };
+  sc acc = sc_to_mont(nz(y));
   for (uint32_t j = 0; j < lg; ++j) {
-    if (live) sc_store(R + 8 * (VREC_U + lg + j), acc);
-    acc = sc_mont(acc, sc_to_mont(sc_load(R + 8 * (VREC_U + j))));
+    const sc u = sc_from_wide_w(CH + 16 * (5 + j));
+    ok &= !w8_zero(u.v);
+    sc_store(R + 8 * (VREC_U + j), u);
+    sc_store(IS + 8 * (1 + j), acc);  // prefix y u_0 .. u_{j-1}
+    acc = sc_mont(acc, sc_to_mont(nz(u)));
   }
-  sc inv = sc_wave_inverse_mont(acc);
-  for (uint32_t j = lg; j-- > 0;) {
-    const sc pre = j ? sc_load(R + 8 * (VREC_U + lg + j)) : sc_to_mont(y);
-    const sc ui = sc_from_mont(sc_mont(inv, pre));
-    inv = sc_mont(inv, sc_to_mont(sc_load(R + 8 * (VREC_U + j))));
-    if (live) sc_store(R + 8 * (VREC_U + lg + j), ui);
+  // the other lanes' product: inclusive prefix / suffix scans over the wave
+  const int lane = threadIdx.x & 63;
+  const sc oneR = sc_one_mont();
+  sc pre = acc, suf = acc;
+  _Pragma("unroll") for (int d = 1; d < 64; d <<= 1) {
+    const sc a = sc_shfl(pre, lane - d < 0 ? lane : lane - d);
+    const sc b = sc_shfl(suf, lane + d > 63 ? lane : lane + d);
+    if (lane >= d) pre = sc_mont(a, pre);
+    if (lane + d <= 63) suf = sc_mont(suf, b);
   }
+  const sc xp = sc_shfl(pre, lane ? lane - 1 : 0), xs = sc_shfl(suf, lane < 63 ? lane + 1 : 63);
+  sc_store(IS, sc_mont(lane ? xp : oneR, lane < 63 ? xs : oneR));
+  if (lane == 63) sc_store(wtot + 8 * (size_t)blockIdx.x, sc_from_mont(pre));
   if (!live) return;
-  sc_store(R + 8 * VREC_XPERM, x_perm);
-  sc_store(R + 8 * VREC_YINV, sc_from_mont(inv));
-  sc_store(R + 8 * VREC_Z, z);
-  sc_store(R + 8 * VREC_X, x);
-  sc_store(R + 8 * VREC_W, wch);
+  const sc r = sc_from_wide_w(CH + 16 * (5 + lg));
+  sc_store(R + 8 * VREC_XPERM, sc_from_wide_w(CH));
+  sc_store(R + 8 * VREC_Z, sc_from_wide_w(CH + 32));
+  sc_store(R + 8 * VREC_X, sc_from_wide_w(CH + 48));
+  sc_store(R + 8 * VREC_W, sc_from_wide_w(CH + 64));
   sc_store(R + 8 * VREC_R, r);
-  sc_store(R + 8 * VREC_A, a);
-  sc_store(R + 8 * VREC_B, b);
-  sc_store(R + 8 * VREC_THAT, that);
-  sc_store(R + 8 * VREC_TAUX, taux);
-  sc_store(R + 8 * VREC_MU, mu);
+  uint32_t w[8];
+  ld8(PP + 88 + 16 * lg, w);
+  st8(R + 8 * VREC_A, w);
+  ld8(PP + 88 + 16 * lg + 8, w);
+  st8(R + 8 * VREC_B, w);
+  ld8(PP + 80, w);
+  st8(R + 8 * VREC_THAT, w);
+  ld8(PP + 64, w);
+  st8(R + 8 * VREC_TAUX, w);
+  ld8(PP + 72, w);
+  st8(R + 8 * VREC_MU, w);
   sc_store(R + 8 * VREC_WT, sc_zero());
   sc_store(r_out + 8 * (size_t)p, r);
   bad[p] = ok ? 0u : 1u;
@@ -156,11 +232,30 @@ __global__ void __launch_bounds__(64) k_verify_replay(uint32_t count, uint32_t k
 
 // w_p = from_wide(SHAKE256("bp-perm-batch-wt" || seed || le64(first + p))
 // [0..64]) (perm::batch_weight): 56 bytes, one sponge block.
+// With inv_st / winv (a device replay's job): also y^-1 and u_j^-1 into the
+// record from k_verify_replay_post's prefix products, the other lanes'
+// product and the host-inverted wave total (canonical winv[wave]); inv_st is
+// only read, so a job's records can be finished again for another window
+// range.
 __global__ void __launch_bounds__(64) k_verify_weights(uint32_t count, uint64_t first, uint64_t total,
                                                        const uint32_t* __restrict__ seed, uint32_t* __restrict__ rec,
-                                                       uint32_t nrec) {
+                                                       uint32_t nrec, uint32_t lg,
+                                                       const uint32_t* __restrict__ inv_st,
+                                                       const uint32_t* __restrict__ winv) {
   const uint32_t p = blockIdx.x * 64 + threadIdx.x;
   if (p >= count) return;
+  if (inv_st) {
+    uint32_t* __restrict__ R = rec + (size_t)p * nrec * 8;
+    const uint32_t* __restrict__ IS = inv_st + (size_t)p * (1 + lg) * 8;
+    sc inv = sc_mont(sc_to_mont(sc_load(winv + 8 * (size_t)blockIdx.x)), sc_load(IS));  // (lane total)^-1
+    for (uint32_t j = lg; j-- > 0;) {
+      sc_store(R + 8 * (VREC_U + lg + j), sc_from_mont(sc_mont(inv, sc_load(IS + 8 * (1 + j)))));
+      sc u = sc_load(R + 8 * (VREC_U + j));
+      if (w8_zero(u.v)) u.v[0] = 1;
+      inv = sc_mont(inv, sc_to_mont(u));
+    }
+    sc_store(R + 8 * VREC_YINV, sc_from_mont(inv));
+  }
   sc wt = sc_zero();
   if (total <= 1) {
     wt.v[0] = 1;
@@ -225,28 +320,63 @@ void verify_init_state(const perm::Circuit& C, const uint8_t* label, size_t llen
 }
 
 int verify_replay_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const uint32_t* d_init,
-                      const uint32_t* d_proofs, const uint32_t* d_V, uint32_t* d_rec, uint32_t* r_out,
-                      uint32_t* bad) {
+                      const uint32_t* d_proofs, const uint32_t* d_V, uint32_t* d_rec, uint32_t* d_inv,
+                      uint32_t* wtot, uint32_t* r_out, uint32_t* bad) {
   if (!count) return BPP_OK;
   const uint32_t pw = (uint32_t)(perm::proof_len(C.k) / 4);
+  const uint32_t nch = 6 + C.lg;
+  void *d_ch = nullptr, *d_ok = nullptr;
+  BPP_TRY(ctx_ws(ctx, "vj_ch", ((size_t)count + 1) * nch * 64, &d_ch));
+  BPP_TRY(ctx_ws(ctx, "vj_ok", (size_t)count * 4, &d_ok));
+  // the proof and V bytes of the block's 8 proofs staged in LDS while they fit
+  const size_t stage = (size_t)RG_GROUPS * (pw + 8 * (size_t)C.m) * 4;
   {
     ProfScope ps(ctx, "verify_replay_dev");
-    hipLaunchKernelGGL(k_verify_replay, dim3(grid_for(count, 64)), dim3(64), 0, ctx->stream, count, C.k, C.lg, C.n_p,
-                       d_init, d_proofs, pw, d_V, d_rec, r_out, bad);
+    if (stage <= 48 * 1024)
+      hipLaunchKernelGGL(k_verify_replay_g<true>, dim3(grid_for(count, RG_GROUPS)), dim3(64), stage, ctx->stream,
+                         count, C.k, C.lg, C.n_p, d_init, d_proofs, pw, d_V, (uint32_t*)d_ch, (uint32_t*)d_ok);
+    else
+      hipLaunchKernelGGL(k_verify_replay_g<false>, dim3(grid_for(count, RG_GROUPS)), dim3(64), 0, ctx->stream,
+                         count, C.k, C.lg, C.n_p, d_init, d_proofs, pw, d_V, (uint32_t*)d_ch, (uint32_t*)d_ok);
   }
-  return ctx_check_launch(ctx, "k_verify_replay");
+  BPP_TRY(ctx_check_launch(ctx, "k_verify_replay_g"));
+  {
+    ProfScope ps(ctx, "verify_replay_post");
+    hipLaunchKernelGGL(k_verify_replay_post, dim3(grid_for(count, 64)), dim3(64), 0, ctx->stream, count, C.lg,
+                       (const uint32_t*)d_ch, (const uint32_t*)d_ok, d_proofs, pw, d_rec, d_inv, wtot, r_out, bad);
+  }
+  return ctx_check_launch(ctx, "k_verify_replay_post");
 }
 
 int verify_weights_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, uint64_t first, uint64_t total,
-                       const uint32_t* seed, uint32_t* d_rec) {
+                       const uint32_t* seed, uint32_t* d_rec, const uint32_t* d_inv, const uint32_t* winv) {
   if (!count) return BPP_OK;
   {
     ProfScope ps(ctx, "verify_weights");
     hipLaunchKernelGGL(k_verify_weights, dim3(grid_for(count, 64)), dim3(64), 0, ctx->stream, count, first, total,
-                       seed, d_rec, vrec_n(C));
+                       seed, d_rec, vrec_n(C), C.lg, d_inv, winv);
   }
   return ctx_check_launch(ctx, "k_verify_weights");
 }
+
+// out[i] = sum_b blocks[b * stride + 8 i] (mod l, canonical in and out)
+__global__ void __launch_bounds__(64) k_verify_sum_blocks(uint32_t nb, uint32_t n, const uint32_t* __restrict__ blocks,
+                                                          uint32_t stride, uint32_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  sc acc = sc_zero();
+  for (uint32_t b = 0; b < nb; ++b) acc = sc_add(acc, sc_load(blocks + (size_t)b * stride + 8 * (size_t)i));
+  sc_store(out + 8 * (size_t)i, acc);
+}
+
+int verify_sum_blocks_dev(bpp_ctx* ctx, uint32_t nb, uint32_t n, const uint32_t* d_blocks, uint32_t stride,
+                          uint32_t* d_out) {
+  if (!n) return BPP_OK;
+  hipLaunchKernelGGL(k_verify_sum_blocks, dim3(grid_for(n, 64)), dim3(64), 0, ctx->stream, nb, n, d_blocks, stride,
+                     d_out);
+  return ctx_check_launch(ctx, "k_verify_sum_blocks");
+}
+
 
 int verify_decompress_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const uint32_t* d_proofs,
                           const uint32_t* d_V, uint32_t* d_tbl, unsigned long long* d_bad) {

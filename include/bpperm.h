@@ -258,11 +258,19 @@ int bpp_perm_prove_batch(bpp_ctx* ctx, const bpp_gens* g, uint32_t k, size_t cou
  * those above with the 32-byte seed32 in place of the 8-byte seed.
  * Secret lifetime: after the batch the library zeroes what it kept of it --
  * the device workspaces holding draws, witness, blindings and the l / r
- * vectors, the staged draw templates and pi, the T-commitment inputs, and the
- * calling thread's reused prover states and permutations (the caller's own
- * seeds32 buffer is the caller's to wipe). */
+ * vectors, the staged draw templates, pi and (k > 768) host-path witness,
+ * the T-commitment inputs, and the calling thread's reused prover states and
+ * permutations; with BPP_PROVE_STREAMS > 1 each sub-batch thread does the same
+ * on its child context before it exits (the caller's own seeds32 buffer is
+ * the caller's to wipe). */
 int bpp_perm_prove_batch_entropy(bpp_ctx* ctx, const bpp_gens* g, uint32_t k, size_t count, const uint8_t* seeds32,
                                  const uint8_t* label, size_t llen, uint8_t* proofs_out, uint8_t* V_out);
+/* Test hook for the secret lifetime above: the number of nonzero bytes left
+ * in what the last bpp_perm_prove_batch_entropy zeroed on ctx and its child
+ * contexts (device workspaces, pinned buffers and staging spans, including
+ * the sub-batch contexts of BPP_PROVE_STREAMS > 1 and the host-witness
+ * staging of k > 768).  Synchronises ctx. */
+int bpp_debug_secret_residue(bpp_ctx* ctx, uint64_t* nonzero_bytes);
 /* BPP_OK or BPP_ERR_VERIFY (ProofError::VerificationError). One GPU MSM. */
 int bpp_perm_verify(bpp_ctx* ctx, const bpp_gens* g, uint32_t k, const uint8_t* label, size_t llen,
                     const uint8_t* proof, size_t proof_len, const uint8_t* V);
@@ -287,8 +295,11 @@ int bpp_perm_verify_begin(uint32_t k, size_t count, const uint8_t* label, size_t
  * transcript, decompresses the proof points and returns r (count x 32 B, may
  * be NULL).  r is byte-identical to bpp_perm_verify_begin's.  The job keeps
  * its records and points in ctx's workspaces: it is valid for
- * bpp_perm_verify_partial on the same ctx until the next
- * bpp_perm_verify_begin_dev there (BPP_ERR_ARG after that), and
+ * bpp_perm_verify_partial on the same ctx until the next verification on
+ * that ctx -- bpp_perm_verify_begin_dev, bpp_perm_verify or
+ * bpp_perm_verify_batch, which all replay through the same workspaces
+ * (BPP_ERR_ARG after that; a call refused for its arguments supersedes
+ * nothing) -- and
  * bpp_perm_verify_scalars rejects it (BPP_ERR_ARG).  The proof points are
  * decompressed beside the replay; one that does not decode makes
  * bpp_perm_verify_partial return BPP_ERR_VERIFY. */
@@ -311,6 +322,37 @@ int bpp_perm_verify_scalars(const bpp_verify_job* job, const uint8_t* r_all, siz
  * (bpp_partials_is_identity). */
 int bpp_perm_verify_partial(bpp_ctx* ctx, const bpp_gens* g, const bpp_verify_job* job, const uint8_t* r_all,
                             size_t total, size_t first, uint32_t w_begin, uint32_t w_end, uint8_t partial[128]);
+/* Window split with the per-proof work sharded by proof (config 5 over N
+ * GPUs, VERDICT r3: the plain window split replays and expands every proof
+ * on every rank).  Rank r of N:
+ *   1. bpp_perm_verify_begin_dev_slice: uploads all `count` proofs and
+ *      decompresses every proof point (the MSM's window range needs them
+ *      all), but replays only proofs [first, first + n), its slice; r_out =
+ *      the slice's r challenges (n x 32 B);
+ *   2. the r of all slices are all-gathered (r_all, count x 32 B, proof order);
+ *   3. bpp_perm_verify_slice_scalars writes the slice's MSM scalars to device
+ *      memory d_out (bpp_perm_verify_slice_bytes(job) bytes): the 2 n_p + 2
+ *      generator scalars summed over the slice, then the slice's n x
+ *      (m + 8 + 2 lg) proof-point scalars (32 B each, canonical); it
+ *      synchronises ctx, so d_out is complete for a collective on return;
+ *   4. the N blocks are all-gathered into one device buffer (block s at
+ *      d_blocks + s * stride; RCCL all_gather of equal-size padded blocks);
+ *   5. bpp_perm_verify_partial_gathered runs the MSM of ALL proofs over
+ *      windows [w_begin, w_end): generator scalars = the sum of the blocks'
+ *      heads, proof-point scalars = the blocks' tails in slice order (slices
+ *      contiguous, in proof order, counts[s] proofs each, summing to count);
+ *   6. the 128-B partials are exchanged as for bpp_perm_verify_partial.
+ * A sliced job is refused by bpp_perm_verify_partial (BPP_ERR_ARG); replay
+ * rejects (BPP_ERR_VERIFY from step 1) must veto the batch on every rank. */
+int bpp_perm_verify_begin_dev_slice(bpp_ctx* ctx, uint32_t k, size_t count, const uint8_t* label, size_t llen,
+                                    const uint8_t* proofs, const uint8_t* V, size_t first, size_t n, uint8_t* r_out,
+                                    bpp_verify_job** out);
+size_t bpp_perm_verify_slice_bytes(const bpp_verify_job* job);
+int bpp_perm_verify_slice_scalars(bpp_ctx* ctx, const bpp_verify_job* job, const uint8_t* r_all, size_t total,
+                                  void* d_out);
+int bpp_perm_verify_partial_gathered(bpp_ctx* ctx, const bpp_gens* g, const bpp_verify_job* job,
+                                     const void* d_blocks, size_t stride, const size_t* counts, size_t nslices,
+                                     uint32_t w_begin, uint32_t w_end, uint8_t partial[128]);
 void bpp_perm_verify_end(bpp_verify_job* job);
 /* BPP_OK if the partials add up to the identity, else BPP_ERR_VERIFY. */
 int bpp_partials_is_identity(const uint8_t* partials, size_t count);

@@ -151,6 +151,37 @@ def test_msm_submit_host_scalars(ctx, big_table, monkeypatch, up_streams):
     ctx.host_free(hb)
 
 
+def test_msm_submit_host_noncanonical_scalars(ctx, big_table):
+    """bpp_msm_submit_host does not check scalars for canonical
+    form (bpp_msm_table does); a non-canonical host scalar gives exactly what
+    bpp_msm_submit gives for the same bytes resident on the device -- pinned
+    and pageable, across the pageable path's staging pieces.  For a value
+    below 2^253 that is the MSM of the scalar reduced mod l (l * P is the
+    identity of the ristretto group)."""
+    import ctypes
+    raw, tbl = big_table
+    n = (1 << 17) + 5
+    sc = _scalars(n, 43)
+    sc[3] = L + 5          # non-canonical, < 2^253
+    sc[n - 2] = 2 * L + 1  # non-canonical near the end (last staging piece)
+    sb = _sb(sc)
+    want = ctx.msm_table(_sb([s % L for s in sc]), tbl, n)
+    d = ctx.dev_alloc(32 * n)
+    h = ctx.host_alloc(32 * n)
+    try:
+        ctx.htod(d, sb)
+        ctypes.memmove(h, sb, 32 * n)
+        dev = ctx.msm_collect(ctx.msm_submit(d, tbl, n))
+        pinned = ctx.msm_collect(ctx.msm_submit_host(h, tbl, n))
+        pageable = ctx.msm_collect(ctx.msm_submit_host(sb, tbl, n))
+        assert dev == pinned == pageable == want
+        with pytest.raises(BppError):  # the one-at-a-time host entry point checks
+            ctx.msm_table(sb, tbl, n)
+    finally:
+        ctx.dev_free(d)
+        ctx.host_free(h)
+
+
 def test_msm_2p22_config5_window_partition(ctx):
     """Config 5 shape (one 2^22-term batch-verify MSM, bucket windows
     partitioned over 8 GPUs), rehearsed on one GPU: the 8 ranks' window

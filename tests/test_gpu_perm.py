@@ -148,3 +148,26 @@ def test_entropy_batches_wipe_without_disturbing_later_batches(gens):
     e2, ve2 = pr.prove_batch_entropy(6)
     assert before == after and vb == va
     assert pr.verify_batch(e1 + e2 + after, ve1 + ve2 + va)
+
+
+@pytest.mark.parametrize("k,streams", [(52, 1), (52, 3), (769, 1)])
+def test_entropy_batch_leaves_no_secret_bytes(ctx, gens, monkeypatch, k, streams):
+    """after bpp_perm_prove_batch_entropy every workspace, pinned
+    buffer and staging span that held the batch's secrets reads back as zero:
+    the one-stream path, sub-batches on child contexts (BPP_PROVE_STREAMS),
+    and k > 768, where the witness and blindings are staged on the host."""
+    import bpperm
+    monkeypatch.setenv("BPP_PROVE_STREAMS", str(streams))
+    g = gens
+    if k > 768:
+        g = bpperm.Gens(ctx, 2048)
+    try:
+        pr = bpperm.PermProver(g, k)
+        proofs, Vs = pr.prove_batch([3, 4, 5])  # a test-hook batch leaves its secrets in place
+        assert ctx.secret_residue() > 0
+        e, ve = pr.prove_batch_entropy(6)
+        assert ctx.secret_residue() == 0
+        assert pr.verify_batch(e + proofs, ve + Vs)
+    finally:
+        if g is not gens:
+            g.close()

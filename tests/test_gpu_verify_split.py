@@ -152,3 +152,75 @@ def test_device_scalars_match_host_expansion(setup, ctx):
     want = cport.msm(b"".join(sc), b"".join(list(G) + list(H) + [B, Bb] + pts))
     assert got == want and got != bytes(32)
     job.close()
+
+
+def _sliced_partials(g, proofs, Vs, ranks, tamper_rank=None):
+    """The sharded window split (bpperm.dist.verify_sliced) rehearsed on one
+    GPU: one context per rank (its sliced job stays valid), r and the scalar
+    blocks gathered by concatenation in rank order."""
+    import torch
+
+    import bpperm
+    from bpperm import dist as bdist
+    ctxs = [bpperm.Context(0) for _ in range(ranks)]
+    prs = [bpperm.PermProver(g, K, ctx=c) for c in ctxs]
+    ranges = bdist.point_ranges(len(proofs), ranks)
+    counts = [e - b for b, e in ranges]
+    jobs = [bpperm.VerifyJob(K, proofs, Vs, prs[r].label, ctx=ctxs[r], replay=(b, e - b))
+            for r, (b, e) in enumerate(ranges)]
+    try:
+        if not all(j.ok for j in jobs):
+            return None
+        r_all = b"".join(j.r for j in jobs)
+        stride = (bdist._slice_block_bytes(K, max(counts)) + 15) // 16 * 16
+        blocks = torch.zeros(ranks * stride, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        for r, j in enumerate(jobs):
+            assert j.slice_bytes() == bdist._slice_block_bytes(K, counts[r])
+            j.slice_scalars(r_all, blocks.data_ptr() + r * stride)
+        if tamper_rank is not None:  # one rank's generator block perturbed after the fact
+            blocks[tamper_rank * stride] ^= 1
+            torch.cuda.synchronize()
+        W = jobs[0].windows()[1]
+        return [prs[r].verify_partial_gathered(jobs[r], blocks.data_ptr(), stride, counts, wb, we)
+                for r, (wb, we) in enumerate(bdist.window_ranges(W, ranks))]
+    finally:
+        for j in jobs:
+            j.close()
+        for c in ctxs:
+            c.close()
+
+
+@pytest.mark.parametrize("ranks,n", [(4, 64), (3, 100), (8, 64)])
+def test_sharded_window_split(setup, ranks, n):
+    """the window split with replay and scalar expansion sharded
+    by proof.  The ranks' window partials add up to the identity exactly when
+    the batch verifies, and to the same element as the plain window split's;
+    a tampered proof or a perturbed scalar block is rejected; a sliced job is
+    refused by bpp_perm_verify_partial."""
+    import bpperm
+    g, pr, proofs, Vs = setup
+    if n > len(proofs):
+        more, mv = pr.prove_batch(list(range(700, 700 + n - len(proofs))))
+        proofs, Vs = proofs + more, Vs + mv
+    proofs, Vs = proofs[:n], Vs[:n]
+    parts = _sliced_partials(g, proofs, Vs, ranks)
+    assert bpperm.partials_is_identity(parts)
+    assert not bpperm.partials_is_identity(parts[:-1])
+    bad = list(proofs)
+    b = bytearray(bad[n // 2])
+    b[40] ^= 1  # A_O's encoding: the replay rejects it or its point decodes to another
+    bad[n // 2] = bytes(b)
+    tp = _sliced_partials(g, bad, Vs, ranks)
+    assert tp is None or None in tp or not bpperm.partials_is_identity(tp)
+    badV = list(Vs)
+    v = bytearray(badV[1])
+    v[33] ^= 2
+    badV[1] = bytes(v)
+    tv = _sliced_partials(g, proofs, badV, ranks)
+    assert tv is None or None in tv or not bpperm.partials_is_identity(tv)
+    assert not bpperm.partials_is_identity(_sliced_partials(g, proofs, Vs, ranks, tamper_rank=ranks - 1))
+    job = bpperm.VerifyJob(K, proofs, Vs, pr.label, ctx=pr.ctx, replay=(0, n // 2))
+    with pytest.raises(bpperm.BppError):
+        pr.verify_partial(job, job.r, 0, 0, 1)
+    job.close()

@@ -65,7 +65,7 @@ for cfg in "$@"; do
         args="--no-cpu --steps ${STEPS:-20} --warmup ${WARMUP:-2} --inflight ${INFLIGHT:-3}"
         [ $LEG = full ] || args="$args --proofs-per-gpu 0"
         [ $LEG = msm ] && args="$args --verify-proofs 0"
-        args="$args ${BENCH_ARGS//,/ }"
+        args="$args --no-extra ${BENCH_ARGS//,/ }"
         timeout -k 10 300 python bench.py $args > gpurun_out/ab.json 2> gpurun_out/ab.err || { tail -5 gpurun_out/ab.err; exit 1; }
         summ gpurun_out/ab.json "$cfg" ;;
       prove)

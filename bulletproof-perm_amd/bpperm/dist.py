@@ -158,7 +158,8 @@ def verify_sliced(prover, proofs, Vs, rank: int, world: int, all_gather_r, gathe
         ok = job.ok
         r_all = b"".join(all_gather_r(job.r if ok else bytes(32 * (e - b))))
         stride = (_slice_block_bytes(prover.k, max(counts)) + 15) // 16 * 16
-        dev = device if device is not None else torch.device("cuda", prover.ctx.device)
+        # (the block lives on this rank's GPU whatever device the collectives use)
+        dev = torch.device("cuda", torch.cuda.current_device())
         blk = torch.zeros(stride, dtype=torch.uint8, device=dev)
         torch.cuda.synchronize(dev)  # (the fill runs on torch's stream, the library on its own)
         if ok:

@@ -1,6 +1,9 @@
 // Context, workspace, profiling and device-memory entry points of the C ABI.
+#include <execinfo.h>
 #include <malloc.h>
+#include <signal.h>
 #include <time.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstring>
@@ -280,7 +283,26 @@ int bpp_host_tuning(uint32_t flags) {
 
 uint32_t bpp_host_threads(void) { return par::threads(); }
 
+// BPP_SEGV_TRACE=1: a SIGSEGV prints the host backtrace (addresses of this
+// library's frames) before the process dies -- a diagnostic for host-side
+// faults on the GPU box, where no debugger may attach.
+static void segv_trace(int sig) {
+  void* fr[64];
+  const int n = backtrace(fr, 64);
+  static const char msg[] = "libbpperm: fatal signal, host backtrace:\n";
+  (void)!write(2, msg, sizeof msg - 1);
+  backtrace_symbols_fd(fr, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
 int bpp_ctx_create(int device, bpp_ctx** out) {
+  static const bool trace = [] {
+    const char* e = getenv("BPP_SEGV_TRACE");
+    if (e && e[0] == '1') signal(SIGSEGV, segv_trace);
+    return true;
+  }();
+  (void)trace;
   return bpp_guard(nullptr, [&]() -> int {
     if (!out) return BPP_ERR_ARG;
     *out = nullptr;

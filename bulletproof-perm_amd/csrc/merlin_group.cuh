@@ -16,12 +16,13 @@
 //   rho/pi  the lane rotates its five words by its own offsets (v_alignbit
 //           with per-lane shift registers; a rotation by >= 32 is a swap of
 //           the halves, folded into the LDS store addresses) and stores them
-//           at their pi destinations in the group's 200-byte scratch;
+//           at their pi destinations in the group's scratch (the copies'
+//           lanes into trash words past the state, so no branch);
 //   chi     the lane reads back columns x, x+1, x+2 of the permuted state
 //           (ds_read2_b64) and forms its new column;
 //   iota    the lane of column 0 folds in the round constant.
 // Group lane gl holds column x = (gl + 4) mod 5 (gl 0..7 -> 4 0 1 2 3 4 0 1):
-// lanes 1..5 are the state's owners ("canonical", the only ones that store)
+// lanes 1..5 are the state's owners ("canonical", the only ones whose stores land)
 // and every canonical lane finds C[x+1] at gl + 1 and C[x-1] at gl - 1 inside
 // the same 8-lane group, so the DPP row shifts never leave the group for
 // them; lanes 0, 6, 7 compute copies that nobody reads.
@@ -30,7 +31,7 @@
 // (the cross-lane dependence is invisible to the compiler).
 //
 // The STROBE byte operations (absorbs, the begin_op flags, the squeeze) are
-// the schedule of merlin_lane.cuh executed by the group's leader lane (gl 1)
+// the schedule of merlin_lane.cuh executed by the group's leader lane (GRP_LEADER)
 // on the group's sponge in LDS; every lane runs the same control flow (the
 // positions are uniform: a batch's transcripts have the same lengths), so the
 // whole wave enters each permutation together.
@@ -38,8 +39,11 @@
 #include "keccak_dev.cuh"
 #include "merlin_lane.cuh"
 
-#define GRP_LANES 8
+#ifndef GRP_LANES
+#define GRP_LANES 16  // lanes per transcript: 16 (grp_keccak16) or 8 (grp_keccak, A/B)
+#endif
 #define GRP_ST_BYTES 200
+#define GRP_SCR_BYTES 240  // the pi scratch: 200 bytes of state + the copies' trash words
 
 // rho offsets r[x][y] packed per y (6 bits per x) and the pi destination row
 // (2x + 3y) mod 5 packed per y (3 bits per x); pi's destination column is y
@@ -50,11 +54,13 @@ __device__ __constant__ static const uint32_t GRP_RHO[5] = {
     (41u << 0) | (45u << 6) | (15u << 12) | (21u << 18) | (8u << 24),
     (18u << 0) | (2u << 6) | (61u << 12) | (56u << 18) | (14u << 24)};
 
+// (mov_dpp with bound_ctrl: lanes whose source is outside the row read 0,
+// so no "old" value has to be materialised first)
 FE_INLINE uint32_t grp_dpp_next(uint32_t v) {  // lane i <- lane i + 1 (row_shl:1)
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x101, 0xf, 0xf, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x101, 0xf, 0xf, true);
 }
 FE_INLINE uint32_t grp_dpp_prev(uint32_t v) {  // lane i <- lane i - 1 (row_shr:1)
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x111, 0xf, 0xf, true);
 }
 #define GRP_FENCE() __asm__ volatile("" ::: "memory")
 
@@ -75,13 +81,15 @@ __device__ __noinline__ static void grp_keccak(lds_u64* st, lds_u64* scr, uint32
     const uint32_t s = n & 31u, sw = (n >> 5) ^ (s == 0 ? 1u : 0u);
     c[y] = (32u - s) & 31u;
     const uint32_t Y = (2 * x + 3 * y) % 5;
-    const uint32_t off = 2 * (5 * y + Y);  // dword index of the destination word (column y, row Y)
+    // dword index of the destination word (column y, row Y); the copies'
+    // lanes store into the trash words past the state (no branch per round)
+    const uint32_t off = canon ? 2 * (5 * y + Y) : 50 + 2 * y;
     wl[y] = off + sw;
     wh[y] = off + (sw ^ 1u);
   }
   const uint32_t c0 = 5 * x, c1 = 5 * ((x + 1) % 5), c2 = 5 * ((x + 2) % 5);  // u64 index of columns
   const uint32_t ms = x == 0 ? ~0u : 0u;
-  for (int r = 0; r < 24; ++r) {
+  _Pragma("unroll 2") for (int r = 0; r < 24; ++r) {
     // theta
     const uint32_t cl = xor3(xor3(lo[0], lo[1], lo[2]), lo[3], lo[4]);
     const uint32_t ch = xor3(xor3(hi[0], hi[1], hi[2]), hi[3], hi[4]);
@@ -92,12 +100,10 @@ __device__ __noinline__ static void grp_keccak(lds_u64* st, lds_u64* scr, uint32
     // rho + pi: rotated words to their destinations (halves swapped there
     // for rotations by >= 32)
     GRP_FENCE();
-    if (canon) {
-      _Pragma("unroll") for (int y = 0; y < 5; ++y) {
-        const uint32_t a = lo[y] ^ dl, b = hi[y] ^ dh;
-        scr32[wl[y]] = __builtin_amdgcn_alignbit(a, b, c[y]);
-        scr32[wh[y]] = __builtin_amdgcn_alignbit(b, a, c[y]);
-      }
+    _Pragma("unroll") for (int y = 0; y < 5; ++y) {
+      const uint32_t a = lo[y] ^ dl, b = hi[y] ^ dh;
+      scr32[wl[y]] = __builtin_amdgcn_alignbit(a, b, c[y]);
+      scr32[wh[y]] = __builtin_amdgcn_alignbit(b, a, c[y]);
     }
     GRP_FENCE();
     // chi over columns x, x + 1, x + 2 of the permuted state
@@ -118,13 +124,76 @@ __device__ __noinline__ static void grp_keccak(lds_u64* st, lds_u64* scr, uint32
   }
 }
 
+// The same permutation on 16-lane groups, each of the five columns on a PAIR
+// of lanes (lane 2j + h holds half h -- lo / hi -- of column x = (j + 4) mod
+// 5, pairs j = 1..5 canonical): a round costs a lane ~45 instructions instead
+// of ~68 (5 words' halves instead of 10 dwords; the rotation takes the other
+// half from the partner lane by DPP quad_perm), one transcript per 16 lanes.
+template <int CTRL>
+FE_INLINE uint32_t grp_dpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, true);
+}
+__device__ __noinline__ static void grp_keccak16(lds_u64* st, lds_u64* scr, uint32_t gl) {
+  const uint32_t j = gl >> 1, h = gl & 1u;
+  const uint32_t x = (j + 4) % 5;
+  const bool canon = j - 1u < 5u;
+  typedef __attribute__((address_space(3))) uint32_t lds_u32;
+  lds_u32* scr32 = (lds_u32*)scr;
+  const lds_u32* st32 = (const lds_u32*)st;
+  uint32_t a[5], c[5], w[5], rd[3];
+  const uint32_t cm = canon ? ~0u : 0u, hm = h ? ~0u : 0u;
+  _Pragma("unroll") for (int y = 0; y < 5; ++y) {
+    a[y] = st32[2 * (x + 5 * y) + h];
+    const uint32_t n = (GRP_RHO[y] >> (6 * x)) & 63u;
+    const uint32_t s = n & 31u, sw = (n >> 5) ^ (s == 0 ? 1u : 0u);
+    c[y] = (32u - s) & 31u;
+    const uint32_t Y = (2 * x + 3 * y) % 5;
+    const uint32_t wc = 2 * (5 * y + Y) + (sw ^ h), wt = 50 + 2 * y + h;  // (copies: trash dwords)
+    w[y] = (wc & cm) | (wt & ~cm);
+  }
+  rd[0] = 10 * x + h;
+  rd[1] = 10 * ((x + 1) % 5) + h;
+  rd[2] = 10 * ((x + 2) % 5) + h;
+  const uint32_t ms = x == 0 ? ~0u : 0u;
+  _Pragma("unroll 2") for (int r = 0; r < 24; ++r) {
+    // theta: this half's column parity; the neighbours' from the pairs beside
+    const uint32_t cc = xor3(xor3(a[0], a[1], a[2]), a[3], a[4]);
+    const uint32_t cp_same = grp_dpp<0x102>(cc);                      // lane + 2: C[x+1], this half
+    const uint32_t o1 = grp_dpp<0x101>(cc), o3 = grp_dpp<0x103>(cc);
+    const uint32_t cp_other = o3 ^ ((o1 ^ o3) & hm);  // C[x+1], the other half (lane + 1 or + 3)
+    const uint32_t cm_same = grp_dpp<0x112>(cc);                      // lane - 2: C[x-1], this half
+    const uint32_t d = cm_same ^ __builtin_amdgcn_alignbit(cp_same, cp_other, 31);
+    GRP_FENCE();
+    _Pragma("unroll") for (int y = 0; y < 5; ++y) {
+      const uint32_t v = a[y] ^ d;
+      const uint32_t pv = grp_dpp<0xB1>(v);  // the partner lane's half (quad_perm 1,0,3,2)
+      scr32[w[y]] = __builtin_amdgcn_alignbit(v, pv, c[y]);
+    }
+    GRP_FENCE();
+    _Pragma("unroll") for (int y = 0; y < 5; ++y) {
+      const uint32_t b0 = scr32[rd[0] + 2 * y], b1 = scr32[rd[1] + 2 * y], b2 = scr32[rd[2] + 2 * y];
+      a[y] = b0 ^ (~b1 & b2);
+    }
+    GRP_FENCE();
+    const uint64_t rc = KECCAK_RC[r];
+    const uint32_t rl = (uint32_t)rc, rh = (uint32_t)(rc >> 32);
+    a[0] ^= (rl ^ ((rl ^ rh) & hm)) & ms;
+  }
+  if (canon) {
+    lds_u32* stw = (lds_u32*)st;
+    _Pragma("unroll") for (int y = 0; y < 5; ++y) stw[2 * (x + 5 * y) + h] = a[y];
+  }
+}
+
+#define GRP_LEADER 2  // a canonical lane of either layout (8: gl 1..5, 16: gl 2..11)
+
 // The STROBE-128 schedule of LaneStrobe (merlin_lane.cuh) for a group: byte
 // operations by the leader lane, permutations by the whole group.
 struct GroupStrobe {
   uint8_t* st;   // the group's 200-byte sponge (LDS)
   uint8_t* scr;  // the group's pi scratch (LDS)
   uint32_t gl;   // lane within the group
-  bool leader;   // gl == 1
+  bool leader;   // gl == GRP_LEADER
   uint32_t pos, pos_begin;
 
   FE_INLINE void run_f() {
@@ -133,7 +202,11 @@ struct GroupStrobe {
       st[pos + 1] ^= 0x04;
       st[LANE_STROBE_R + 1] ^= 0x80;
     }
+#if GRP_LANES == 16
+    grp_keccak16((lds_u64*)st, (lds_u64*)scr, gl);
+#else
     grp_keccak((lds_u64*)st, (lds_u64*)scr, gl);
+#endif
     pos = 0;
     pos_begin = 0;
   }
@@ -181,7 +254,37 @@ struct GroupStrobe {
     absorb_bytes(reinterpret_cast<const uint8_t*>(label), ln);
     absorb_le32(n);
   }
+  // the framing bytes of append_message(label, n-byte message) before the
+  // message: begin_op(M | A), the label, le32(n), begin_op(A) -- when they
+  // and the message end before the rate, one branch-free run of byte XORs
+  // (the leader's LDS read-modify-writes then pipeline instead of paying the
+  // LDS latency byte by byte between the rate checks)
+  // (flags2: the second begin_op's flags, FLAG_A for a message; FLAG_I |
+  // FLAG_A | FLAG_C for a challenge, whose permutation the caller runs)
+  FE_INLINE bool frame_fast(const char* label, uint32_t ln, uint32_t n, uint32_t flags2 = 2u) {
+    const uint32_t fl = 2 + ln + 4 + 2;
+    if (pos + fl + (flags2 == 2u ? n : 0u) >= LANE_STROBE_R) return false;
+    if (leader) {
+      uint8_t* d = st + pos;
+      d[0] ^= (uint8_t)pos_begin;
+      d[1] ^= 18u;  // FLAG_M | FLAG_A
+      for (uint32_t i = 0; i < ln; ++i) d[2 + i] ^= (uint8_t)label[i];
+      d[2 + ln] ^= (uint8_t)n;
+      d[3 + ln] ^= (uint8_t)(n >> 8);
+      d[4 + ln] ^= (uint8_t)(n >> 16);
+      d[5 + ln] ^= (uint8_t)(n >> 24);
+      d[6 + ln] ^= (uint8_t)(pos + 1);  // the second begin_op: the old begin is this meta's
+      d[7 + ln] ^= (uint8_t)flags2;
+    }
+    pos_begin = pos + 7 + ln;  // (the second begin_op at byte pos + 6 + ln)
+    pos += fl;
+    return true;
+  }
   FE_INLINE void append32(const char* label, uint32_t ln, const uint32_t w[8]) {
+    if (frame_fast(label, ln, 32)) {
+      absorb32(w);
+      return;
+    }
     meta(label, ln, 32);
     begin_op(2u);  // FLAG_A
     absorb32(w);
@@ -200,8 +303,12 @@ struct GroupStrobe {
   // challenge_bytes(label, 64): the 16 squeezed words to out (16 x u32,
   // written by the leader; global memory), the rate's first 64 bytes cleared
   FE_INLINE void challenge64_to(const char* label, uint32_t ln, uint32_t* __restrict__ out, bool store) {
-    meta(label, ln, 64);
-    begin_op(1u | 2u | 4u);  // FLAG_I | FLAG_A | FLAG_C
+    if (frame_fast(label, ln, 64, 1u | 2u | 4u)) {
+      run_f();  // (begin_op(C) with pos != 0)
+    } else {
+      meta(label, ln, 64);
+      begin_op(1u | 2u | 4u);  // FLAG_I | FLAG_A | FLAG_C
+    }
     if (leader) {
       uint4* d = reinterpret_cast<uint4*>(st);
       _Pragma("unroll") for (int i = 0; i < 4; ++i) {

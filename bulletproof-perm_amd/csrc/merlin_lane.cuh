@@ -186,11 +186,6 @@ FE_INLINE sc sc_inv_vartime(const sc& a) {
 // scans, 6 shuffle steps each way), the wave's total inverted once
 // (uniform control flow), a^-1 = total^-1 * prefix * suffix.  A zero lane
 // value makes every lane's result wrong (its proof is rejected anyway).
-FE_INLINE sc sc_shfl(const sc& a, int src) {
-  sc r;
-  _Pragma("unroll") for (int i = 0; i < 8; ++i) r.v[i] = __shfl(a.v[i], src, 64);
-  return r;
-}
 FE_INLINE sc sc_wave_inverse_mont(const sc& aR) {
   const int lane = threadIdx.x & 63;
   const sc oneR = sc_one_mont();

@@ -261,6 +261,16 @@ __global__ void __launch_bounds__(POLY_T) k_poly_x(uint32_t n_p, const uint32_t*
 // Writes wt * (generator scalars) to gen[p][2 n_p + 2] (summed over proofs by
 // k_verify_merge) and wt * (proof-point scalars) to sc_out[NG + p npt + j]
 // (V_0..V_{m-1}, A_I, A_O, S, T1 T3 T4 T5 T6, L_0.., R_0..), canonical.
+#ifdef VS_TIMING  // phase stamps of k_verify_scalars (timing variant only: tools/vs_phases.py)
+__device__ unsigned long long vs_dbg[8192 * 8];
+#define VS_T(k) \
+  if (threadIdx.x == 0 && blockIdx.x < 8192) vs_dbg[blockIdx.x * 8 + (k)] = clock64()
+extern "C" int bpp_debug_vs_timing(unsigned long long* out, size_t n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(vs_dbg), n * 8) == hipSuccess ? 0 : 1;
+}
+#else
+#define VS_T(k)
+#endif
 __global__ void __launch_bounds__(POLY_T) k_verify_scalars(
     uint32_t n_p, uint32_t m, uint32_t Q, uint32_t lg, const uint32_t* __restrict__ rec,
     const uint32_t* __restrict__ cp, const uint32_t* __restrict__ ce, const uint32_t* __restrict__ cR,
@@ -276,6 +286,7 @@ __global__ void __launch_bounds__(POLY_T) k_verify_scalars(
   const uint32_t* R = rec + (size_t)p * nrec * 8;
   const sc oneR = sc_one_mont();
   auto ldm = [&](uint32_t k) { return sc_to_mont(sc_load(R + 8 * k)); };
+  VS_T(0);
   const sc zR = ldm(VREC_Z), xR = ldm(VREC_X), yiR = ldm(VREC_YINV), aR = ldm(VREC_A), bR = ldm(VREC_B),
            wtR = ldm(VREC_WT), rR = ldm(VREC_R);
   // s_0 = prod u_j^-1; s_i = s_0 prod_{bit k of i} u_{lg-1-k}^2 (bulletproofs
@@ -293,6 +304,7 @@ __global__ void __launch_bounds__(POLY_T) k_verify_scalars(
   sc s0R = oneR;
   for (uint32_t j = 0; j < lg; ++j) s0R = sc_mont(s0R, ldm(VREC_U + lg + j));
   sc_tables3({zt, Q + 1, false}, {yit, NY, false}, {st, NY, true});
+  VS_T(1);
   auto s_of = [&](uint32_t i) {  // s_i / s_0
     sc v = sc_load(st + 8 * (i % POW_LO));
     for (uint32_t k = POW_LO_LG; k < lg; ++k)
@@ -320,10 +332,12 @@ __global__ void __launch_bounds__(POLY_T) k_verify_scalars(
     sc_store(gen + 8 * (gb + i), sc_from_mont(sc_mont(gi, wtR)));
     sc_store(gen + 8 * (gb + n_p + i), sc_from_mont(sc_mont(hi, wtR)));
   }
+  VS_T(2);
   for (uint32_t q = threadIdx.x; q < Q; q += blockDim.x) {
     const sc c = q + 1 == Q ? sc_neg(ldm(VREC_XPERM)) : sc_to_mont(sc_load(cR + 8 * q));
     acc[1] = sc_add(acc[1], sc_mont(sc_load(zp + 8 * q), c));
   }
+  VS_T(3);
   const sc x2R = sc_mont(xR, xR);
   const sc wrx2R = sc_mont(sc_mont(wtR, rR), x2R);
   const size_t pb = NG + (size_t)p * npt;
@@ -339,6 +353,7 @@ __global__ void __launch_bounds__(POLY_T) k_verify_scalars(
     const sc cs = col_sum_block(cpv, ce, j, zp, red);
     if (threadIdx.x == 0) sc_store(sc_out + 8 * (pb + j), sc_from_mont(sc_neg(sc_mont(cs, wrx2R))));
   }
+  VS_T(4);
   // A_I, A_O, S: -wt x^(1,2,3); T_k: -wt r x^k (k = 1, 3..6); L_j: -wt u_j^2; R_j: -wt u_j^-2
   for (uint32_t j = threadIdx.x; j < 8 + 2 * lg; j += blockDim.x) {
     sc v;
@@ -354,16 +369,30 @@ __global__ void __launch_bounds__(POLY_T) k_verify_scalars(
     }
     sc_store(sc_out + 8 * (pb + m + j), sc_from_mont(sc_neg(sc_mont(v, wtR))));
   }
+  VS_T(5);
   sc_block_sum<2>(acc, red);
-  if (threadIdx.x == 0) {
-    // B: wt (r (t_hat - x^2 (delta + zc)) + w (a b - t_hat)); B_blinding: wt (r tau_x + mu)
+  VS_T(6);
+  // B = wt (r (t_hat - x^2 (delta + zc)) + w (a b - t_hat)) from lanes 0 and
+  // 1, B_blinding = wt (r tau_x + mu) on lane 2, at once (delta and zc are
+  // valid in lane 0; one lane ran all three chains before, ~11 % of a
+  // workgroup's cycles, tools/vs_phases.py)
+  if (threadIdx.x < 3) {
     const sc thR = ldm(VREC_THAT);
-    const sc tB = sc_mont(rR, sc_sub(thR, sc_mont(x2R, sc_add(acc[0], acc[1]))));
-    const sc iB = sc_mont(ldm(VREC_W), sc_sub(sc_mont(aR, bR), thR));
-    sc_store(gen + 8 * (gb + 2 * n_p), sc_from_mont(sc_mont(sc_add(tB, iB), wtR)));
-    const sc bb = sc_add(sc_mont(rR, ldm(VREC_TAUX)), ldm(VREC_MU));
-    sc_store(gen + 8 * (gb + 2 * n_p + 1), sc_from_mont(sc_mont(bb, wtR)));
+    sc v;
+    if (threadIdx.x == 0) v = sc_mont(rR, sc_sub(thR, sc_mont(x2R, sc_add(acc[0], acc[1]))));
+    else if (threadIdx.x == 1) v = sc_mont(ldm(VREC_W), sc_sub(sc_mont(aR, bR), thR));
+    else v = sc_add(sc_mont(rR, ldm(VREC_TAUX)), ldm(VREC_MU));
+    v = sc_mont(v, wtR);
+    if (threadIdx.x) sc_store(red + 8 * threadIdx.x, v);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (threadIdx.x == 0) {
+      sc_store(gen + 8 * (gb + 2 * n_p), sc_from_mont(sc_add(v, sc_load(red + 8))));
+      sc_store(gen + 8 * (gb + 2 * n_p + 1), sc_from_mont(sc_load(red + 16)));
+    }
   }
+  VS_T(7);
 }
 
 // sc_out[i] = sum_p gen[p][i] (one workgroup per generator column)

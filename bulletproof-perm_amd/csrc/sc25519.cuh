@@ -263,3 +263,10 @@ FE_INLINE sc sc_wave_sum(sc a) {
   }
   return a;
 }
+
+// value of lane src of the wave
+FE_INLINE sc sc_shfl(const sc& a, int src) {
+  sc r;
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) r.v[i] = __shfl(a.v[i], src, 64);
+  return r;
+}

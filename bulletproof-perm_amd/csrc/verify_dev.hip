@@ -38,15 +38,15 @@ FE_INLINE bool w8_zero(const uint32_t w[8]) {
 // Group replay (round 4, the default): one transcript per 8 lanes
 // (merlin_group.cuh), 8 transcripts per 64-lane block, so a 4096-proof batch
 // is 512 waves whose permutations cost ~65 instructions a round instead of
-// ~190.  The replay keeps only the transcript chain: every challenge's 64
+// ~190 (GRP_LANES = 16: 16 lanes, 4 transcripts per block, ~45).  The replay keeps only the transcript chain: every challenge's 64
 // squeezed bytes go to ch ([count + 1][6 + lg][16] words, the last a pad for
 // groups past the batch) and the proof's encoding / canonical-scalar checks to
 // okw[p]; k_verify_replay_post reduces the challenges, inverts y and the u_j
 // and writes the records, one lane per proof.  STAGED: the group's proof and
 // V bytes are first copied into LDS by its 8 lanes (one load latency instead
 // of one per absorbed item).
-#define RG_GROUPS 8
-#define RG_SP 208  // sponge / scratch stride (16-B aligned)
+#define RG_GROUPS (64 / GRP_LANES)
+#define RG_SP 240  // sponge / scratch stride (16-B aligned; the scratch holds GRP_SCR_BYTES)
 template <bool STAGED>
 __global__ void __launch_bounds__(64) k_verify_replay_g(uint32_t count, uint32_t k, uint32_t lg, uint32_t n_p,
                                                         const uint32_t* __restrict__ init,
@@ -58,7 +58,7 @@ __global__ void __launch_bounds__(64) k_verify_replay_g(uint32_t count, uint32_t
   // the replay is a latency chain and the proof-point decompression runs
   // beside it on the same SIMDs: win the issue arbitration
   __builtin_amdgcn_s_setprio(3);
-  const uint32_t g = threadIdx.x >> 3, gl = threadIdx.x & 7;
+  const uint32_t g = threadIdx.x / GRP_LANES, gl = threadIdx.x % GRP_LANES;
   const uint32_t pg = blockIdx.x * RG_GROUPS + g;
   const bool live = pg < count;
   const uint32_t p = live ? pg : count - 1;
@@ -67,7 +67,7 @@ __global__ void __launch_bounds__(64) k_verify_replay_g(uint32_t count, uint32_t
   t.st = sp + g * 2 * RG_SP;
   t.scr = t.st + RG_SP;
   t.gl = gl;
-  t.leader = gl == 1;
+  t.leader = gl == GRP_LEADER;
   {
     uint32_t* d = reinterpret_cast<uint32_t*>(t.st);
     for (uint32_t i = gl; i < 50; i += GRP_LANES) d[i] = init[i];

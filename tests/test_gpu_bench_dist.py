@@ -43,6 +43,6 @@ def test_bench_two_ranks_gloo(tmp_path):
     assert d["pipelined_matches_serial"] is True
     assert d["proofs"]["all_verified"] is True and d["proofs"]["n_gpus"] == 2
     v = d["verify_batch"]
-    assert set(v["splits"]) == {"windows", "proofs"}
+    assert set(v["splits"]) == {"windows", "windows_sharded", "proofs"}
     assert all(s["all_verified"] for s in v["splits"].values())
     assert v["rejects_tampered"] is True

@@ -157,9 +157,8 @@ def test_device_scalars_match_host_expansion(setup, ctx):
 def _sliced_partials(g, proofs, Vs, ranks, tamper_rank=None):
     """The sharded window split (bpperm.dist.verify_sliced) rehearsed on one
     GPU: one context per rank (its sliced job stays valid), r and the scalar
-    blocks gathered by concatenation in rank order."""
-    import torch
-
+    blocks gathered by concatenation in rank order (device memory from the
+    library: torch's own HIP runtime is not initialised in this process)."""
     import bpperm
     from bpperm import dist as bdist
     ctxs = [bpperm.Context(0) for _ in range(ranks)]
@@ -173,16 +172,18 @@ def _sliced_partials(g, proofs, Vs, ranks, tamper_rank=None):
             return None
         r_all = b"".join(j.r for j in jobs)
         stride = (bdist._slice_block_bytes(K, max(counts)) + 15) // 16 * 16
-        blocks = torch.zeros(ranks * stride, dtype=torch.uint8, device="cuda")
-        torch.cuda.synchronize()
+        blocks = ctxs[0].dev_alloc(ranks * stride)
+        ctxs[0].htod(blocks, bytes(ranks * stride))
         for r, j in enumerate(jobs):
             assert j.slice_bytes() == bdist._slice_block_bytes(K, counts[r])
-            j.slice_scalars(r_all, blocks.data_ptr() + r * stride)
+            j.slice_scalars(r_all, blocks + r * stride)
         if tamper_rank is not None:  # one rank's generator block perturbed after the fact
-            blocks[tamper_rank * stride] ^= 1
-            torch.cuda.synchronize()
+            at = blocks + tamper_rank * stride
+            b0 = bytearray(ctxs[0].dtoh(at, 16))
+            b0[0] ^= 1
+            ctxs[0].htod(at, bytes(b0))
         W = jobs[0].windows()[1]
-        return [prs[r].verify_partial_gathered(jobs[r], blocks.data_ptr(), stride, counts, wb, we)
+        return [prs[r].verify_partial_gathered(jobs[r], blocks, stride, counts, wb, we)
                 for r, (wb, we) in enumerate(bdist.window_ranges(W, ranks))]
     finally:
         for j in jobs:

@@ -3,6 +3,7 @@
 # kernel's counters are its own).  One counter pass per rocprofv3 run.
 # Usage (on the box): bash tools/gpu_pmc_prover.sh <tag> [msm]
 #   msm: the same passes over the 2^20 MSM bench stream instead
+#   verify: over config-5 batch verifications (tools/verify_stages.py)
 #        (-> gpurun_out/pmc_msm_<tag>; summarise with pmc_prover_summary.py)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -13,6 +14,10 @@ CMD="python3 tools/prove_inflight_exp.py ${PMC_SHAPE:-384 16 2}"
 if [ "$2" = "msm" ]; then
   OUT=gpurun_out/pmc_msm_$TAG
   CMD="python3 bench.py --steps 6 --warmup 1 --no-cpu --proofs-per-gpu 0 --verify-proofs 0 --no-extra --no-extra"
+fi
+if [ "$2" = "verify" ]; then  # one config-5 batch verification's kernels (tools/verify_stages.py)
+  OUT=gpurun_out/pmc_verify_$TAG
+  CMD="python3 tools/verify_stages.py --reps 2"
 fi
 mkdir -p $OUT
 timeout -s KILL 60 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true

@@ -25,16 +25,54 @@ __global__ void __launch_bounds__(64) k_lane(unsigned long long* cyc, uint32_t* 
 }
 
 __global__ void __launch_bounds__(64) k_group(unsigned long long* cyc, uint32_t* sink) {
-  __shared__ __attribute__((aligned(16))) uint8_t sp[8 * 2 * 208];
+  __shared__ __attribute__((aligned(16))) uint8_t sp[8 * 2 * 240];
   const uint32_t g = threadIdx.x >> 3, gl = threadIdx.x & 7;
-  uint8_t* st = sp + g * 416;
+  uint8_t* st = sp + g * 480;
   for (int i = gl; i < 25; i += 8) reinterpret_cast<uint64_t*>(st)[i] = i * 0x9e3779b97f4a7c15ull + g;
   __builtin_amdgcn_s_waitcnt(0);
   const unsigned long long t0 = clock64();
-  for (int n = 0; n < NPERM; ++n) grp_keccak((lds_u64*)st, (lds_u64*)(st + 208), gl);
+  for (int n = 0; n < NPERM; ++n) grp_keccak((lds_u64*)st, (lds_u64*)(st + 240), gl);
   const unsigned long long t1 = clock64();
   if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
   sink[blockIdx.x * 64 + threadIdx.x] = reinterpret_cast<uint32_t*>(st)[gl];
+}
+
+__global__ void __launch_bounds__(64) k_group16(unsigned long long* cyc, uint32_t* sink) {
+  __shared__ __attribute__((aligned(16))) uint8_t sp[4 * 2 * 240];
+  const uint32_t g = threadIdx.x >> 4, gl = threadIdx.x & 15;
+  uint8_t* st = sp + g * 480;
+  for (int i = gl; i < 25; i += 16) reinterpret_cast<uint64_t*>(st)[i] = i * 0x9e3779b97f4a7c15ull + g;
+  __builtin_amdgcn_s_waitcnt(0);
+  const unsigned long long t0 = clock64();
+  for (int n = 0; n < NPERM; ++n) grp_keccak16((lds_u64*)st, (lds_u64*)(st + 240), gl);
+  const unsigned long long t1 = clock64();
+  if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+  sink[blockIdx.x * 64 + threadIdx.x] = reinterpret_cast<uint32_t*>(st)[gl];
+}
+
+// the three permutations agree on the same inputs (8 states per block)
+__global__ void __launch_bounds__(64) k_check(uint32_t* bad) {
+  __shared__ __attribute__((aligned(16))) uint64_t ref[8 * 25];
+  __shared__ __attribute__((aligned(16))) uint8_t s8[8 * 2 * 240];
+  __shared__ __attribute__((aligned(16))) uint8_t s16[4 * 2 * 240];
+  for (int i = threadIdx.x; i < 8 * 25; i += 64) ref[i] = (i % 25) * 0x9e3779b97f4a7c15ull + (i / 25) * 0x1234567ull;
+  for (int i = threadIdx.x; i < 8 * 25; i += 64)
+    reinterpret_cast<uint64_t*>(s8 + (i / 25) * 480)[i % 25] = ref[i];
+  for (int i = threadIdx.x; i < 4 * 25; i += 64)
+    reinterpret_cast<uint64_t*>(s16 + (i / 25) * 480)[i % 25] = ref[i];
+  __syncthreads();
+  if (threadIdx.x < 8) lane_keccak((lds_u64*)(ref + 25 * threadIdx.x));
+  grp_keccak((lds_u64*)(s8 + (threadIdx.x >> 3) * 480), (lds_u64*)(s8 + (threadIdx.x >> 3) * 480 + 240),
+             threadIdx.x & 7);
+  grp_keccak16((lds_u64*)(s16 + (threadIdx.x >> 4) * 480), (lds_u64*)(s16 + (threadIdx.x >> 4) * 480 + 240),
+               threadIdx.x & 15);
+  __syncthreads();
+  uint32_t nb = 0;
+  for (int i = threadIdx.x; i < 8 * 25; i += 64) {
+    nb += reinterpret_cast<uint64_t*>(s8 + (i / 25) * 480)[i % 25] != ref[i];
+    if (i < 4 * 25) nb += reinterpret_cast<uint64_t*>(s16 + (i / 25) * 480)[i % 25] != ref[i];
+  }
+  atomicAdd(bad, nb);
 }
 
 // dependent VALU chain (v_xor) and dependent bitop3, DPP-fed chain, LDS round trip
@@ -125,9 +163,17 @@ static void report(const char* name, void (*k)(unsigned long long*, uint32_t*), 
 }
 
 int main() {
+  uint32_t* dbad;
+  hipMalloc(&dbad, 4);
+  hipMemset(dbad, 0, 4);
+  hipLaunchKernelGGL(k_check, dim3(1), dim3(64), 0, 0, dbad);
+  uint32_t hb = ~0u;
+  hipMemcpy(&hb, dbad, 4, hipMemcpyDeviceToHost);
+  printf("group permutations vs lane keccak: %u mismatching words\n", hb);
   for (int b : {1, 512}) {
     report("lane keccak (per perm)", k_lane, b, NPERM);
     report("group keccak (per perm)", k_group, b, NPERM);
+    report("group16 keccak (per perm)", k_group16, b, NPERM);
   }
   report("latency", k_lat, 1, 1);
   report("sc_inv_vartime on VGPRs", k_inv<false>, 1, 1);

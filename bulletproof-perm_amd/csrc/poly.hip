@@ -271,10 +271,59 @@ extern "C" int bpp_debug_vs_timing(unsigned long long* out, size_t n) {
 #else
 #define VS_T(k)
 #endif
+// Per-proof constants of k_verify_scalars (Montgomery form, VK_N x 8 words
+// a proof), one lane per proof: every product of two workgroup-uniform
+// values is formed here, on the vector unit.  Inside k_verify_scalars such
+// products ran on the scalar unit (uniform operands): 21 K SALU instructions
+// per wave next to 15 K VALU, ~400 spilled SGPRs, and the CU's one scalar
+// unit shared by its waves (r04 PMC, tools/vs_phases.py).
+#define VK_Z 0      // z
+#define VK_YI 1     // y^-1
+#define VK_X 2      // x
+#define VK_WT 3     // the proof's batch weight
+#define VK_S0A 4    // s_0 a  (s_0 = prod u_j^-1)
+#define VK_S0B 5    // s_0 b
+#define VK_WRX2 6   // wt r x^2
+#define VK_WRT 7    // wt r t_hat
+#define VK_IB 8     // wt w (a b - t_hat)
+#define VK_BB 9     // wt (r tau_x + mu)
+#define VK_R 10     // r
+#define VK_NXP 11   // -x_perm
+#define VK_N 12
+__global__ void __launch_bounds__(64) k_verify_consts(uint32_t count, uint32_t lg, const uint32_t* __restrict__ rec,
+                                                      uint32_t* __restrict__ kc) {
+  __builtin_amdgcn_s_setprio(3);  // (latency chain; the decompression runs beside it)
+  const uint32_t p = blockIdx.x * 64 + threadIdx.x;
+  if (p >= count) return;
+  const uint32_t nrec = VREC_U + 2 * lg;
+  const uint32_t* R = rec + (size_t)p * nrec * 8;
+  uint32_t* K = kc + (size_t)p * VK_N * 8;
+  auto ldm = [&](uint32_t k) { return sc_to_mont(sc_load(R + 8 * k)); };
+  const sc xR = ldm(VREC_X), wtR = ldm(VREC_WT), rR = ldm(VREC_R), aR = ldm(VREC_A), bR = ldm(VREC_B),
+           thR = ldm(VREC_THAT);
+  sc s0R = ldm(VREC_U + lg);
+  for (uint32_t j = 1; j < lg; ++j) s0R = sc_mont(s0R, ldm(VREC_U + lg + j));
+  const sc wrR = sc_mont(wtR, rR);
+  sc_store(K + 8 * VK_Z, ldm(VREC_Z));
+  sc_store(K + 8 * VK_YI, ldm(VREC_YINV));
+  sc_store(K + 8 * VK_X, xR);
+  sc_store(K + 8 * VK_WT, wtR);
+  sc_store(K + 8 * VK_S0A, sc_mont(s0R, aR));
+  sc_store(K + 8 * VK_S0B, sc_mont(s0R, bR));
+  sc_store(K + 8 * VK_WRX2, sc_mont(wrR, sc_mont(xR, xR)));
+  sc_store(K + 8 * VK_WRT, sc_mont(wrR, thR));
+  sc_store(K + 8 * VK_IB, sc_mont(wtR, sc_mont(ldm(VREC_W), sc_sub(sc_mont(aR, bR), thR))));
+  sc_store(K + 8 * VK_BB, sc_mont(wtR, sc_add(sc_mont(rR, ldm(VREC_TAUX)), ldm(VREC_MU))));
+  sc_store(K + 8 * VK_R, rR);
+  sc_store(K + 8 * VK_NXP, sc_neg(ldm(VREC_XPERM)));
+}
+
 __global__ void __launch_bounds__(POLY_T) k_verify_scalars(
     uint32_t n_p, uint32_t m, uint32_t Q, uint32_t lg, const uint32_t* __restrict__ rec,
-    const uint32_t* __restrict__ cp, const uint32_t* __restrict__ ce, const uint32_t* __restrict__ cR,
-    uint32_t* __restrict__ gen, uint32_t* __restrict__ sc_out, uint32_t NG, uint32_t npt) {
+    const uint32_t* __restrict__ kc, const uint32_t* __restrict__ cp, const uint32_t* __restrict__ ce,
+    const uint32_t* __restrict__ cR, uint32_t* __restrict__ gen, uint32_t* __restrict__ sc_out, uint32_t NG,
+    uint32_t npt) {
+  __builtin_amdgcn_s_setprio(2);  // (ahead of the proof-point decompression beside it)
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const uint32_t NY = min(n_p, (uint32_t)POW_LO);
   uint32_t* zt = lds;                // [Q + 1] z^e, Montgomery
@@ -284,25 +333,23 @@ __global__ void __launch_bounds__(POLY_T) k_verify_scalars(
   const uint32_t* zp = zt + 8;       // z^(q+1)
   const uint32_t p = blockIdx.x, nrec = VREC_U + 2 * lg;
   const uint32_t* R = rec + (size_t)p * nrec * 8;
+  const uint32_t* K = kc + (size_t)p * VK_N * 8;
   const sc oneR = sc_one_mont();
   auto ldm = [&](uint32_t k) { return sc_to_mont(sc_load(R + 8 * k)); };
+  auto ldk = [&](uint32_t k) { return sc_load(K + 8 * k); };
   VS_T(0);
-  const sc zR = ldm(VREC_Z), xR = ldm(VREC_X), yiR = ldm(VREC_YINV), aR = ldm(VREC_A), bR = ldm(VREC_B),
-           wtR = ldm(VREC_WT), rR = ldm(VREC_R);
-  // s_0 = prod u_j^-1; s_i = s_0 prod_{bit k of i} u_{lg-1-k}^2 (bulletproofs
+  // s_i = s_0 prod_{bit k of i} u_{lg-1-k}^2 (bulletproofs
   // verification_scalars): st[i] = s_i / s_0 for i < NY as a doubling table
   // over the factors u_{lg-1-k}^2, the bits from POW_LO_LG up per lane
   if (threadIdx.x == 0) {
-    sc_table_pow_init(zt, Q + 1, zR, oneR);
-    sc_table_pow_init(yit, NY, yiR, oneR);
+    sc_table_pow_init(zt, Q + 1, ldk(VK_Z), oneR);
+    sc_table_pow_init(yit, NY, ldk(VK_YI), oneR);
     sc_store(st, oneR);
   }
   for (uint32_t b = threadIdx.x; b < POW_LO_LG && (1u << b) < NY; b += blockDim.x) {
     const sc u = ldm(VREC_U + lg - 1 - b);
     sc_store(st + 8 * (1u << b), sc_mont(u, u));
   }
-  sc s0R = oneR;
-  for (uint32_t j = 0; j < lg; ++j) s0R = sc_mont(s0R, ldm(VREC_U + lg + j));
   sc_tables3({zt, Q + 1, false}, {yit, NY, false}, {st, NY, true});
   VS_T(1);
   auto s_of = [&](uint32_t i) {  // s_i / s_0
@@ -314,9 +361,9 @@ __global__ void __launch_bounds__(POLY_T) k_verify_scalars(
       }
     return v;
   };
-  const sc s0aR = sc_mont(s0R, aR), s0bR = sc_mont(s0R, bR);
+  const sc s0aR = ldk(VK_S0A), s0bR = ldk(VK_S0B), xR = ldk(VK_X), wtR = ldk(VK_WT);
   sc yihi = oneR, yistep = oneR;  // (y^-POW_LO)^r, as k_poly_coef
-  if (n_p > POW_LO) yistep = sc_mont(sc_load(yit + 8 * (POW_LO - 1)), yiR);
+  if (n_p > POW_LO) yistep = sc_mont(sc_load(yit + 8 * (POW_LO - 1)), ldk(VK_YI));
   const size_t gb = (size_t)p * NG;
   sc acc[2] = {sc_zero(), sc_zero()};  // delta = sum y^-i zWR_i zWL_i, zc = <z^Q, c>
   for (uint32_t i = threadIdx.x; i < n_p; i += blockDim.x) {
@@ -334,12 +381,11 @@ __global__ void __launch_bounds__(POLY_T) k_verify_scalars(
   }
   VS_T(2);
   for (uint32_t q = threadIdx.x; q < Q; q += blockDim.x) {
-    const sc c = q + 1 == Q ? sc_neg(ldm(VREC_XPERM)) : sc_to_mont(sc_load(cR + 8 * q));
+    const sc c = q + 1 == Q ? ldk(VK_NXP) : sc_to_mont(sc_load(cR + 8 * q));
     acc[1] = sc_add(acc[1], sc_mont(sc_load(zp + 8 * q), c));
   }
   VS_T(3);
-  const sc x2R = sc_mont(xR, xR);
-  const sc wrx2R = sc_mont(sc_mont(wtR, rR), x2R);
+  const sc wrx2R = ldk(VK_WRX2);
   const size_t pb = NG + (size_t)p * npt;
   // V_j: -wt r x^2 zWV_j (zWV from the fourth column-CSR, m columns; the
   // heavy x column summed by the whole workgroup)
@@ -362,7 +408,7 @@ __global__ void __launch_bounds__(POLY_T) k_verify_scalars(
       for (uint32_t e = 0; e < j; ++e) v = sc_mont(v, xR);
     } else if (j < 8) {
       const uint32_t e = j == 3 ? 1u : j - 1;  // T1, T3, T4, T5, T6
-      v = sc_mont(rR, sc_pow_small(xR, e, oneR));
+      v = sc_mont(ldk(VK_R), sc_pow_small(xR, e, oneR));
     } else {
       const sc u = ldm(j < 8 + lg ? VREC_U + (j - 8) : VREC_U + lg + (j - 8 - lg));
       v = sc_mont(u, u);
@@ -372,25 +418,11 @@ __global__ void __launch_bounds__(POLY_T) k_verify_scalars(
   VS_T(5);
   sc_block_sum<2>(acc, red);
   VS_T(6);
-  // B = wt (r (t_hat - x^2 (delta + zc)) + w (a b - t_hat)) from lanes 0 and
-  // 1, B_blinding = wt (r tau_x + mu) on lane 2, at once (delta and zc are
-  // valid in lane 0; one lane ran all three chains before, ~11 % of a
-  // workgroup's cycles, tools/vs_phases.py)
-  if (threadIdx.x < 3) {
-    const sc thR = ldm(VREC_THAT);
-    sc v;
-    if (threadIdx.x == 0) v = sc_mont(rR, sc_sub(thR, sc_mont(x2R, sc_add(acc[0], acc[1]))));
-    else if (threadIdx.x == 1) v = sc_mont(ldm(VREC_W), sc_sub(sc_mont(aR, bR), thR));
-    else v = sc_add(sc_mont(rR, ldm(VREC_TAUX)), ldm(VREC_MU));
-    v = sc_mont(v, wtR);
-    if (threadIdx.x) sc_store(red + 8 * threadIdx.x, v);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (threadIdx.x == 0) {
-      sc_store(gen + 8 * (gb + 2 * n_p), sc_from_mont(sc_add(v, sc_load(red + 8))));
-      sc_store(gen + 8 * (gb + 2 * n_p + 1), sc_from_mont(sc_load(red + 16)));
-    }
+  if (threadIdx.x == 0) {
+    // B: wt (r (t_hat - x^2 (delta + zc)) + w (a b - t_hat)); B_blinding: wt (r tau_x + mu)
+    const sc tB = sc_sub(ldk(VK_WRT), sc_mont(wrx2R, sc_add(acc[0], acc[1])));
+    sc_store(gen + 8 * (gb + 2 * n_p), sc_from_mont(sc_add(tB, ldk(VK_IB))));
+    sc_store(gen + 8 * (gb + 2 * n_p + 1), sc_from_mont(ldk(VK_BB)));
   }
   VS_T(7);
 }
@@ -717,11 +749,15 @@ int verify_scalars_dev_rec(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count,
   BPP_TRY(ctx_h2d_const(ctx, "vs_c", d_c, cw.data(), cw.size() * 4));
   const unsigned nt = poly_block(std::max(C.n_p, C.m));
   const size_t lds = ((size_t)C.Q + 1 + 2 * std::min(C.n_p, (uint32_t)POW_LO)) * 32 + (POLY_T / 64) * 2 * 32;
+  void* d_kc = nullptr;
+  BPP_TRY(ctx_ws(ctx, "vs_kc", (size_t)count * VK_N * 32, &d_kc));
   {
     ProfScope ps(ctx, "verify_scalars");
+    hipLaunchKernelGGL(k_verify_consts, dim3((count + 63) / 64), dim3(64), 0, ctx->stream, count, C.lg, d_rec,
+                       (uint32_t*)d_kc);
     hipLaunchKernelGGL(k_verify_scalars, dim3(count), dim3(nt), lds, ctx->stream, C.n_p, C.m, C.Q, C.lg, d_rec,
-                       (const uint32_t*)d_cp, (const uint32_t*)d_ce, (const uint32_t*)d_c, (uint32_t*)d_gen, d_sc,
-                       NG, npt);
+                       (const uint32_t*)d_kc, (const uint32_t*)d_cp, (const uint32_t*)d_ce, (const uint32_t*)d_c,
+                       (uint32_t*)d_gen, d_sc, NG, npt);
     hipLaunchKernelGGL(k_verify_merge, dim3(NG), dim3(POLY_T), 0, ctx->stream, count, NG, (const uint32_t*)d_gen,
                        d_sc);
   }

@@ -151,48 +151,67 @@ __global__ void __launch_bounds__(64) k_verify_replay_g(uint32_t count, uint32_t
   if (live && t.leader) okw[p] = ok ? 1u : 0u;
 }
 
-// One lane per proof: the challenges of k_verify_replay_g reduced mod l (the
-// verifier's challenge_scalar, transcript_protocol.rs:62-67) and the records
-// except y^-1 and the u_j^-1.  Those come from ONE inversion per wave of 64
-// proofs (Montgomery's trick: the lane's product y u_0 .. u_{lg-1}, then the
-// wave's): this kernel leaves the lane's prefix products and the product of
+// One lane per (proof, challenge): the 64 squeezed bytes of k_verify_replay_g
+// reduced mod l (the verifier's challenge_scalar, transcript_protocol.rs:62-67)
+// into the proof's record -- x_perm, z, x, w, u_j, r in their slots, y in
+// the y^-1 slot until k_verify_weights replaces it -- and r to r_out.  (One
+// lane per proof ran the 6 + lg reductions in a row, ~2.4 K cycles each.)
+__global__ void __launch_bounds__(64) k_verify_reduce(uint32_t count, uint32_t lg, const uint32_t* __restrict__ ch,
+                                                      uint32_t* __restrict__ rec, uint32_t* __restrict__ r_out) {
+  __builtin_amdgcn_s_setprio(3);  // (latency chain; the decompression runs beside it)
+  const uint32_t nch = 6 + lg, nrec = VREC_U + 2 * lg;
+  const size_t t = (size_t)blockIdx.x * 64 + threadIdx.x;
+  if (t >= (size_t)count * nch) return;
+  const uint32_t p = (uint32_t)(t / nch), c = (uint32_t)(t % nch);
+  const sc v = sc_from_wide_w(ch + t * 16);
+  const uint32_t slot = c == 0   ? VREC_XPERM
+                        : c == 1 ? VREC_YINV
+                        : c == 2 ? VREC_Z
+                        : c == 3 ? VREC_X
+                        : c == 4 ? VREC_W
+                        : c < 5 + lg ? VREC_U + (c - 5)
+                                     : VREC_R;
+  sc_store(rec + ((size_t)p * nrec + slot) * 8, v);
+  if (c == 5 + lg) sc_store(r_out + 8 * (size_t)p, v);
+}
+
+// One lane per proof, after k_verify_reduce: the checks, the record's proof
+// scalars, and ONE inversion per wave of 64 proofs for y^-1 and the u_j^-1
+// (Montgomery's trick: the lane's product y u_0 .. u_{lg-1}, then the
+// wave's).  This kernel leaves the lane's prefix products and the product of
 // the other 63 lanes' totals in inv_st ([count + 1][1 + lg], Montgomery) and
 // the wave's total in wtot[wave] (canonical); the host inverts the wave
 // totals (one batch inversion, perm_api.hip verify_begin_dev) and
 // k_verify_weights finishes the inverses.  A binary-Euclid inversion on the
-// device cost a wave ~310 K cycles (129 us, tools/ubench/keccak_grp.hip), the
-// largest part of this step.  A zero y or u (a rejected proof) enters the
-// products as 1.  Lanes past the batch shadow the last proof and keep to the
-// pad entries.
+// device cost a wave ~310 K cycles (129 us, tools/ubench/keccak_grp.hip).  A
+// zero y or u (a rejected proof) enters the products as 1.  Lanes past the
+// batch shadow the last proof and keep to the pad entries.
 __global__ void __launch_bounds__(64) k_verify_replay_post(uint32_t count, uint32_t lg,
-                                                           const uint32_t* __restrict__ ch,
                                                            const uint32_t* __restrict__ okw,
                                                            const uint32_t* __restrict__ proofs, uint32_t pw,
                                                            uint32_t* __restrict__ rec, uint32_t* __restrict__ inv_st,
-                                                           uint32_t* __restrict__ wtot, uint32_t* __restrict__ r_out,
-                                                           uint32_t* __restrict__ bad) {
+                                                           uint32_t* __restrict__ wtot, uint32_t* __restrict__ bad) {
+  __builtin_amdgcn_s_setprio(3);  // (latency chain; the decompression runs beside it)
   const bool live = blockIdx.x * 64 + threadIdx.x < count;
   const uint32_t p = live ? blockIdx.x * 64 + threadIdx.x : count - 1;
-  const uint32_t nch = 6 + lg, nrec = VREC_U + 2 * lg;
-  const uint32_t* __restrict__ CH = ch + (size_t)p * nch * 16;
+  const uint32_t nrec = VREC_U + 2 * lg;
+  const uint32_t* __restrict__ Rp = rec + (size_t)p * nrec * 8;  // (the shadowed proof's record: read only)
   uint32_t* __restrict__ R = rec + (size_t)(live ? p : count) * nrec * 8;
   uint32_t* __restrict__ IS = inv_st + (size_t)(live ? p : count) * (1 + lg) * 8;
   const uint32_t* __restrict__ PP = proofs + (size_t)p * pw;
   bool ok = okw[p] != 0;
-  const sc y = sc_from_wide_w(CH + 16);
-  ok &= !w8_zero(y.v);
-  auto nz = [](const sc& v) {
+  auto nz = [&](const sc& v) {
     sc o = v;
-    if (w8_zero(v.v)) o.v[0] = 1;
+    if (w8_zero(v.v)) {
+      ok = false;
+      o.v[0] = 1;
+    }
     return o;
   };
-  sc acc = sc_to_mont(nz(y));
+  sc acc = sc_to_mont(nz(sc_load(Rp + 8 * VREC_YINV)));  // (y, until k_verify_weights)
   for (uint32_t j = 0; j < lg; ++j) {
-    const sc u = sc_from_wide_w(CH + 16 * (5 + j));
-    ok &= !w8_zero(u.v);
-    sc_store(R + 8 * (VREC_U + j), u);
     sc_store(IS + 8 * (1 + j), acc);  // prefix y u_0 .. u_{j-1}
-    acc = sc_mont(acc, sc_to_mont(nz(u)));
+    acc = sc_mont(acc, sc_to_mont(nz(sc_load(Rp + 8 * (VREC_U + j)))));
   }
   // the other lanes' product: inclusive prefix / suffix scans over the wave
   const int lane = threadIdx.x & 63;
@@ -208,12 +227,6 @@ __global__ void __launch_bounds__(64) k_verify_replay_post(uint32_t count, uint3
   sc_store(IS, sc_mont(lane ? xp : oneR, lane < 63 ? xs : oneR));
   if (lane == 63) sc_store(wtot + 8 * (size_t)blockIdx.x, sc_from_mont(pre));
   if (!live) return;
-  const sc r = sc_from_wide_w(CH + 16 * (5 + lg));
-  sc_store(R + 8 * VREC_XPERM, sc_from_wide_w(CH));
-  sc_store(R + 8 * VREC_Z, sc_from_wide_w(CH + 32));
-  sc_store(R + 8 * VREC_X, sc_from_wide_w(CH + 48));
-  sc_store(R + 8 * VREC_W, sc_from_wide_w(CH + 64));
-  sc_store(R + 8 * VREC_R, r);
   uint32_t w[8];
   ld8(PP + 88 + 16 * lg, w);
   st8(R + 8 * VREC_A, w);
@@ -226,7 +239,6 @@ __global__ void __launch_bounds__(64) k_verify_replay_post(uint32_t count, uint3
   ld8(PP + 72, w);
   st8(R + 8 * VREC_MU, w);
   sc_store(R + 8 * VREC_WT, sc_zero());
-  sc_store(r_out + 8 * (size_t)p, r);
   bad[p] = ok ? 0u : 1u;
 }
 
@@ -242,6 +254,7 @@ __global__ void __launch_bounds__(64) k_verify_weights(uint32_t count, uint64_t 
                                                        uint32_t nrec, uint32_t lg,
                                                        const uint32_t* __restrict__ inv_st,
                                                        const uint32_t* __restrict__ winv) {
+  __builtin_amdgcn_s_setprio(3);  // (latency chain; the decompression runs beside it)
   const uint32_t p = blockIdx.x * 64 + threadIdx.x;
   if (p >= count) return;
   if (inv_st) {
@@ -342,10 +355,12 @@ int verify_replay_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, cons
   BPP_TRY(ctx_check_launch(ctx, "k_verify_replay_g"));
   {
     ProfScope ps(ctx, "verify_replay_post");
+    hipLaunchKernelGGL(k_verify_reduce, dim3(grid_for((size_t)count * nch, 64)), dim3(64), 0, ctx->stream, count,
+                       C.lg, (const uint32_t*)d_ch, d_rec, r_out);
     hipLaunchKernelGGL(k_verify_replay_post, dim3(grid_for(count, 64)), dim3(64), 0, ctx->stream, count, C.lg,
-                       (const uint32_t*)d_ch, (const uint32_t*)d_ok, d_proofs, pw, d_rec, d_inv, wtot, r_out, bad);
+                       (const uint32_t*)d_ok, d_proofs, pw, d_rec, d_inv, wtot, bad);
   }
-  return ctx_check_launch(ctx, "k_verify_replay_post");
+  return ctx_check_launch(ctx, "k_verify_reduce/post");
 }
 
 int verify_weights_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, uint64_t first, uint64_t total,

@@ -116,6 +116,11 @@ static int stage_take(bpp_ctx* ctx, size_t bytes, uint8_t** out) {
   if (ctx->stage_used + need > ctx->stage_cap) {
     BPP_TRY(ctx_sync(ctx));  // every staged copy has completed
     if (need > ctx->stage_cap) {
+      // secret spans recorded in the old arena (prove_wipe's list) are zeroed
+      // now and dropped: after the free they would point at unmapped memory
+      for (auto& st : ctx->secret_stage) memset(st.first, 0, st.second);
+      ctx->secret_stage.clear();
+      ctx->wiped.clear();
       if (ctx->stage) BPP_HIP(hipHostFree(ctx->stage));
       ctx->stage = nullptr;
       ctx->stage_cap = 0;
@@ -284,14 +289,21 @@ int bpp_host_tuning(uint32_t flags) {
 uint32_t bpp_host_threads(void) { return par::threads(); }
 
 // BPP_SEGV_TRACE=1: a SIGSEGV prints the host backtrace (addresses of this
-// library's frames) before the process dies -- a diagnostic for host-side
-// faults on the GPU box, where no debugger may attach.
-static void segv_trace(int sig) {
+// library's frames) and then runs the handler that was installed before
+// (Python's faulthandler under pytest) -- a diagnostic for host-side faults on
+// the GPU box, where no debugger may attach.
+static struct sigaction g_prev_segv;
+static void segv_trace(int sig, siginfo_t* si, void* uc) {
   void* fr[64];
   const int n = backtrace(fr, 64);
   static const char msg[] = "libbpperm: fatal signal, host backtrace:\n";
   (void)!write(2, msg, sizeof msg - 1);
   backtrace_symbols_fd(fr, n, 2);
+  if (g_prev_segv.sa_flags & SA_SIGINFO) {
+    if (g_prev_segv.sa_sigaction) return g_prev_segv.sa_sigaction(sig, si, uc);
+  } else if (g_prev_segv.sa_handler != SIG_DFL && g_prev_segv.sa_handler != SIG_IGN) {
+    return g_prev_segv.sa_handler(sig);
+  }
   signal(sig, SIG_DFL);
   raise(sig);
 }
@@ -299,7 +311,14 @@ static void segv_trace(int sig) {
 int bpp_ctx_create(int device, bpp_ctx** out) {
   static const bool trace = [] {
     const char* e = getenv("BPP_SEGV_TRACE");
-    if (e && e[0] == '1') signal(SIGSEGV, segv_trace);
+    if (e && e[0] == '1') {
+      struct sigaction sa;
+      memset(&sa, 0, sizeof sa);
+      sa.sa_sigaction = segv_trace;
+      sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+      sigemptyset(&sa.sa_mask);
+      sigaction(SIGSEGV, &sa, &g_prev_segv);
+    }
     return true;
   }();
   (void)trace;

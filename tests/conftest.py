@@ -7,6 +7,9 @@ from pathlib import Path
 import pytest
 
 ROOT = Path(__file__).resolve().parent.parent
+# a host-side fault inside libbpperm prints its native backtrace before
+# Python's faulthandler report (ctx.hip segv_trace)
+os.environ.setdefault("BPP_SEGV_TRACE", "1")
 sys.path.insert(0, str(ROOT / "bulletproof-perm_amd"))
 sys.path.insert(0, str(ROOT))
 

@@ -9,7 +9,7 @@ byte count: tools/ubench/gather_cal k_stream (268,435,456 B read -> 131,084
 KiB = exactly 1/2).  WRITE_SIZE is taken as exact (the guide's calibration;
 k_from_uniform here writes 2^20 x 96 B = 98,304 KiB, matched exactly).
 
-    python tools/pmc_summary.py gpurun_out/prof_r01c r01 20
+    python tools/pmc_summary.py gpurun_out/prof_r01c r01 20 [proof batch, 384]
 """
 import collections
 import csv
@@ -30,6 +30,7 @@ def per_kernel(path):
 
 def main():
     src, tag, log2n = Path(sys.argv[1]), sys.argv[2], int(sys.argv[3])
+    batch = int(sys.argv[4]) if len(sys.argv) > 4 else 384  # prove_batch_once.py size (PROOF_BATCH)
     fetch = per_kernel(src / "pmc_fetch" / "run_counter_collection.csv")
     write = per_kernel(src / "pmc_write" / "run_counter_collection.csv")
     out_p = ROOT / "profiles" / "pmc_summary.json"
@@ -57,7 +58,7 @@ def main():
         shutil.copy(stats, ROOT / "profiles" / f"{tag}_kernel_stats.csv")
     stats = src / "trace_proofs" / "run_kernel_stats.csv"
     if stats.exists():
-        shutil.copy(stats, ROOT / "profiles" / f"{tag}_prove_batch256_kernel_stats.csv")
+        shutil.copy(stats, ROOT / "profiles" / f"{tag}_prove_batch{batch}_kernel_stats.csv")
     stats = src / "trace_verify" / "run_kernel_stats.csv"
     if stats.exists():
         shutil.copy(stats, ROOT / "profiles" / f"{tag}_verify4096_kernel_stats.csv")

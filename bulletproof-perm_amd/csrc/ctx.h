@@ -82,6 +82,9 @@ struct bpp_ctx {
   // before the next upload overwrites the inputs
   hipEvent_t vj_ev_in = nullptr, vj_ev_dec = nullptr;
   bool vj_dec_pending = false;
+  // one event per upload chunk (verify_begin_dev: each chunk's points are
+  // decompressed as soon as its copy lands)
+  std::vector<hipEvent_t> vj_ev_chunk;
   // bpp_msm_submit_host: the uploaded scalars of this (child) context's MSM,
   // copied on the parent's upload streams (up_stream, created on first use;
   // one per chunk of the copy) and signalled to this context's stream by

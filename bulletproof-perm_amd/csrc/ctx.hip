@@ -366,6 +366,7 @@ void bpp_ctx_destroy(bpp_ctx* ctx) {
     }
   if (ctx->vj_ev_in) hipEventDestroy(ctx->vj_ev_in);
   if (ctx->vj_ev_dec) hipEventDestroy(ctx->vj_ev_dec);
+  for (auto e : ctx->vj_ev_chunk) hipEventDestroy(e);
   for (auto& sl : ctx->msm_slot)
     if (sl.done) hipEventDestroy(sl.done);
   hipStreamDestroy(ctx->stream);

@@ -43,7 +43,10 @@
 #define GRP_LANES 16  // lanes per transcript: 16 (grp_keccak16) or 8 (grp_keccak, A/B)
 #endif
 #define GRP_ST_BYTES 200
-#define GRP_SCR_BYTES 240  // the pi scratch: 200 bytes of state + the copies' trash words
+#ifndef GRP_TRASH
+#define GRP_TRASH 60  // first trash dword of grp_keccak16 (50: the former layout, A/B)
+#endif
+#define GRP_SCR_BYTES 280  // the pi scratch: 200 bytes of state + the copies' trash words (16-lane: dwords 60..69)
 
 // rho offsets r[x][y] packed per y (6 bits per x) and the pi destination row
 // (2x + 3y) mod 5 packed per y (3 bits per x); pi's destination column is y
@@ -148,7 +151,9 @@ __device__ __noinline__ static void grp_keccak16(lds_u64* st, lds_u64* scr, uint
     const uint32_t s = n & 31u, sw = (n >> 5) ^ (s == 0 ? 1u : 0u);
     c[y] = (32u - s) & 31u;
     const uint32_t Y = (2 * x + 3 * y) % 5;
-    const uint32_t wc = 2 * (5 * y + Y) + (sw ^ h), wt = 50 + 2 * y + h;  // (copies: trash dwords)
+    // (copies: trash dwords 60..69, placed so that they share no bank with
+    // the same instruction's state stores, tools/lds_banks.py)
+    const uint32_t wc = 2 * (5 * y + Y) + (sw ^ h), wt = GRP_TRASH + 2 * y + h;
     w[y] = (wc & cm) | (wt & ~cm);
   }
   rd[0] = 10 * x + h;

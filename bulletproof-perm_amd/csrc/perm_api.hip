@@ -1093,12 +1093,7 @@ int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label,
   // (the previous job's decompression may still read "vj_in")
   if (ctx->vj_dec_pending) BPP_HIP(hipStreamWaitEvent(ctx->stream, ctx->vj_ev_dec, 0));
   void *d_in = nullptr, *d_rec = nullptr, *d_x = nullptr, *d_dbad = nullptr;
-  {
-    HostScope hs(ctx, "verify_upload");
-    BPP_TRY(ctx_ws(ctx, "vj_in", count * (plen + vbytes), &d_in));
-    BPP_TRY(ctx_h2d2(ctx, d_in, proofs, count * plen, V, count * vbytes));
-  }
-  HostScope hs(ctx, "verify_replay");
+  BPP_TRY(ctx_ws(ctx, "vj_in", count * (plen + vbytes), &d_in));
   const uint32_t* d_pf = (const uint32_t*)d_in;
   const uint32_t* d_V = (const uint32_t*)((uint8_t*)d_in + count * plen);
   // (+1: the pad record of k_verify_replay's lanes past the batch)
@@ -1106,10 +1101,10 @@ int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label,
   BPP_TRY(ctx_ws(ctx, "vj_x", npts * MSM_NIELS_WORDS * 4, &d_x));
   BPP_TRY(ctx_ws(ctx, "vj_dbad", 8, &d_dbad));
   BPP_HIP(hipMemsetAsync(d_dbad, 0xff, 8, ctx->stream));
-  // decompression order (BPP_VERIFY_DEC, A/B): 0 = launched beside the
-  // replay before it, 1 = launched after the replay's launch (beside it),
-  // 2 = after the replay completes (it then overlaps the host weights and
-  // k_verify_scalars instead)
+  // decompression order (BPP_VERIFY_DEC, A/B): 0 = per upload chunk, beside
+  // the upload and then the replay, 1 = launched after the replay's launch
+  // (beside it), 2 = after the replay completes (it then overlaps the host
+  // weights and k_verify_scalars instead)
   static const int dec_order = [] {
     const char* e = getenv("BPP_VERIFY_DEC");
     return e ? atoi(e) : 0;
@@ -1122,7 +1117,48 @@ int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label,
     ctx->vj_dec_pending = true;
     return BPP_OK;
   };
-  if (dec_order == 0 || !rcount) BPP_TRY(launch_dec());
+  {
+    HostScope hs(ctx, "verify_upload");
+    if (dec_order == 0) {
+      // The proofs and V go up in chunks of proofs (each chunk's proof bytes
+      // and V bytes to their places in the [proofs][V] layout), and each
+      // chunk's points are decompressed on the child stream as soon as its
+      // copies land, so the decompression -- the longest stage beside the
+      // replay -- starts while later chunks are still being staged and copied
+      // (BPP_VERIFY_CHUNKS, default 4; 1 = one decompression after the whole
+      // upload).
+      static const size_t nchunk_env = [] {
+        const char* e = getenv("BPP_VERIFY_CHUNKS");
+        return (size_t)std::max(1, e ? atoi(e) : 4);
+      }();
+      const size_t nchunk = std::min(nchunk_env, std::max<size_t>(1, count / 256));
+      while (ctx->vj_ev_chunk.size() < nchunk) {
+        hipEvent_t e = nullptr;
+        BPP_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        ctx->vj_ev_chunk.push_back(e);
+      }
+      uint8_t* stg = nullptr;
+      BPP_TRY(ctx_h2d_stage(ctx, count * (plen + vbytes), &stg));
+      for (size_t q = 0; q < nchunk; ++q) {
+        const size_t p0 = count * q / nchunk, p1 = count * (q + 1) / nchunk;
+        const size_t po = p0 * plen, pn = (p1 - p0) * plen, vo = count * plen + p0 * vbytes, vn = (p1 - p0) * vbytes;
+        ctx_stage_copy(stg + po, proofs + po, pn);
+        BPP_TRY(ctx_h2d_staged(ctx, (uint8_t*)d_in + po, stg + po, pn));
+        ctx_stage_copy(stg + vo, V + p0 * vbytes, vn);
+        BPP_TRY(ctx_h2d_staged(ctx, (uint8_t*)d_in + vo, stg + vo, vn));
+        BPP_HIP(hipEventRecord(ctx->vj_ev_chunk[q], ctx->stream));
+        BPP_HIP(hipStreamWaitEvent(kid->stream, ctx->vj_ev_chunk[q], 0));
+        BPP_TRY(verify_decompress_dev(kid, C, (uint32_t)count, d_pf, d_V, (uint32_t*)d_x,
+                                      (unsigned long long*)d_dbad, (uint32_t)p0, (uint32_t)p1));
+      }
+      BPP_HIP(hipEventRecord(ctx->vj_ev_dec, kid->stream));
+      ctx->vj_dec_pending = true;
+    } else {
+      BPP_TRY(ctx_h2d2(ctx, d_in, proofs, count * plen, V, count * vbytes));
+    }
+  }
+  HostScope hs(ctx, "verify_replay");
+  if (dec_order != 0 && !rcount) BPP_TRY(launch_dec());
   uint32_t *h_init = nullptr, *h_r = nullptr, *h_bad = nullptr;
   {
     uint32_t init[52];

@@ -38,12 +38,14 @@ inline uint32_t vpts_n(const perm::Circuit& C) { return C.m + 8 + 2 * C.lg; }
 int verify_replay_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const uint32_t* d_init,
                       const uint32_t* d_proofs, const uint32_t* d_V, uint32_t* d_rec, uint32_t* d_inv,
                       uint32_t* wtot, uint32_t* r_out, uint32_t* bad);
-// Decompresses every proof point of the uploaded proofs / V into d_tbl
-// ([count * vpts_n] Niels rows in MSM order); *d_bad = the smallest index of
-// an undecodable encoding (set to ~0 by the caller first).  Independent of
-// the replay (launched on another stream).
+// Decompresses the proof points of proofs [p0, p1) (p1 = ~0u: count) of the
+// uploaded proofs / V into d_tbl ([count * vpts_n] Niels rows in MSM order);
+// *d_bad = the smallest index of an undecodable encoding (set to ~0 by the
+// caller first).  Independent of the replay (launched on another stream, one
+// launch per upload chunk).
 int verify_decompress_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const uint32_t* d_proofs,
-                          const uint32_t* d_V, uint32_t* d_tbl, unsigned long long* d_bad);
+                          const uint32_t* d_V, uint32_t* d_tbl, unsigned long long* d_bad, uint32_t p0 = 0,
+                          uint32_t p1 = ~0u);
 // The 52-word shared transcript prefix for verify_replay_dev.
 void verify_init_state(const perm::Circuit& C, const uint8_t* label, size_t llen, uint32_t out[52]);
 // rec[p][VREC_WT] = perm::batch_weight(seed, first + p) for p < count (one

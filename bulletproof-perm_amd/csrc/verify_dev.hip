@@ -1,3 +1,4 @@
+#include <algorithm>
 // Batch verifier, device side: every proof's Fiat-Shamir replay on the GPU,
 // one lane (one Merlin transcript) per proof, and the batch weights.
 //
@@ -46,14 +47,23 @@ FE_INLINE bool w8_zero(const uint32_t w[8]) {
 // V bytes are first copied into LDS by its 8 lanes (one load latency instead
 // of one per absorbed item).
 #define RG_GROUPS (64 / GRP_LANES)
-#define RG_SP 240  // sponge / scratch stride (16-B aligned; the scratch holds GRP_SCR_BYTES)
+// A group's sponge (200 B) and pi scratch (GRP_SCR_BYTES) at a stride of 576
+// B = 144 dwords = 16 mod 32: the two groups of a 32-lane half (the lanes whose
+// ds_read_b32 / ds_write_b32 share the 32 banks) then hit disjoint banks in
+// every chi load and all but 2 of a round's pi stores (tools/lds_banks.py: 2
+// extra LDS cycles a round against 20 at the former 480-B stride, where every
+// chi load was 2-way)
+#ifndef RG_GS  // (A/B: -DRG_GS=480 -DRG_SCR_OFF=240 -DGRP_TRASH=50 is the former layout)
+#define RG_GS 576
+#define RG_SCR_OFF 200
+#endif
 template <bool STAGED>
 __global__ void __launch_bounds__(64) k_verify_replay_g(uint32_t count, uint32_t k, uint32_t lg, uint32_t n_p,
                                                         const uint32_t* __restrict__ init,
                                                         const uint32_t* __restrict__ proofs, uint32_t pw,
                                                         const uint32_t* __restrict__ V, uint32_t* __restrict__ ch,
                                                         uint32_t* __restrict__ okw) {
-  __shared__ __attribute__((aligned(16))) uint8_t sp[RG_GROUPS * 2 * RG_SP];
+  __shared__ __attribute__((aligned(16))) uint8_t sp[RG_GROUPS * RG_GS];
   extern __shared__ __attribute__((aligned(16))) uint32_t stage[];  // STAGED: [8][pw + 8 m]
   // the replay is a latency chain and the proof-point decompression runs
   // beside it on the same SIMDs: win the issue arbitration
@@ -64,8 +74,8 @@ __global__ void __launch_bounds__(64) k_verify_replay_g(uint32_t count, uint32_t
   const uint32_t p = live ? pg : count - 1;
   const uint32_t m = 2 * k + 1, nch = 6 + lg;
   GroupStrobe t;
-  t.st = sp + g * 2 * RG_SP;
-  t.scr = t.st + RG_SP;
+  t.st = sp + g * RG_GS;
+  t.scr = t.st + RG_SCR_OFF;
   t.gl = gl;
   t.leader = gl == GRP_LEADER;
   {
@@ -296,12 +306,19 @@ __global__ void __launch_bounds__(64) k_verify_weights(uint32_t count, uint64_t 
 // the MSM's Niels table (point i = p npt + j in vpts_n order), so that it
 // needs nothing from the replay and runs beside it on another stream.
 // *bad = the smallest index of an undecodable encoding (~0 if none).
-__global__ void __launch_bounds__(64) k_verify_decompress(uint32_t count, uint32_t m, uint32_t lg, uint32_t npt,
-                                                          const uint32_t* __restrict__ proofs, uint32_t pw,
-                                                          const uint32_t* __restrict__ V, uint32_t* __restrict__ tbl,
-                                                          unsigned long long* __restrict__ bad) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (size_t)count * npt) return;
+// (VD_WPE waves per SIMD: unconstrained, the compiler takes 244 VGPRs for the
+// inverse square root, 2 waves per SIMD; config 5, interleaved A/B passes:
+// 0.594-0.607 ms unconstrained, 0.554-0.559 at 3 (167 VGPRs, spills outside
+// the squaring loops only), 0.62 at 4, 0.58-0.59 at 6)
+#ifndef VD_WPE
+#define VD_WPE 3
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(VD_WPE)))
+k_verify_decompress(size_t i0, size_t i1, uint32_t m, uint32_t lg, uint32_t npt, const uint32_t* __restrict__ proofs,
+                    uint32_t pw, const uint32_t* __restrict__ V, uint32_t* __restrict__ tbl,
+                    unsigned long long* __restrict__ bad) {
+  const size_t i = i0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= i1) return;
   const uint32_t p = (uint32_t)(i / npt), j = (uint32_t)(i % npt);
   const uint32_t* src;
   if (j < m)
@@ -394,13 +411,14 @@ int verify_sum_blocks_dev(bpp_ctx* ctx, uint32_t nb, uint32_t n, const uint32_t*
 
 
 int verify_decompress_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const uint32_t* d_proofs,
-                          const uint32_t* d_V, uint32_t* d_tbl, unsigned long long* d_bad) {
-  const size_t n = (size_t)count * vpts_n(C);
-  if (!n) return BPP_OK;
+                          const uint32_t* d_V, uint32_t* d_tbl, unsigned long long* d_bad, uint32_t p0, uint32_t p1) {
+  p1 = std::min(p1, count);
+  if (p0 >= p1) return BPP_OK;
+  const size_t npt = vpts_n(C), i0 = (size_t)p0 * npt, i1 = (size_t)p1 * npt;
   {
     ProfScope ps(ctx, "verify_decompress");
-    hipLaunchKernelGGL(k_verify_decompress, dim3(grid_for(n, 64)), dim3(64), 0, ctx->stream, count, C.m, C.lg,
-                       vpts_n(C), d_proofs, (uint32_t)(perm::proof_len(C.k) / 4), d_V, d_tbl, d_bad);
+    hipLaunchKernelGGL(k_verify_decompress, dim3(grid_for(i1 - i0, 64)), dim3(64), 0, ctx->stream, i0, i1, C.m, C.lg,
+                       (uint32_t)npt, d_proofs, (uint32_t)(perm::proof_len(C.k) / 4), d_V, d_tbl, d_bad);
   }
   return ctx_check_launch(ctx, "k_verify_decompress");
 }

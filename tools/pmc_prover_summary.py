@@ -82,9 +82,15 @@ def main():
             # the sum over waves of their resident time in quad-cycles
             # (MI355X_MICROARCH.md: SQ_WAVE_CYCLES counts quad-cycles), the
             # launch spans GRBM_GUI_ACTIVE / 8 XCDs cycles, on 1024 SIMDs.
-            # Calibration: k_msm_accumulate holds 4 waves per SIMD by the
-            # compiler's report (128 VGPRs) and runs 4100 waves in one round,
-            # so this must read ~4 there (round 3's WAVE/BUSY/32 read 0.48).
+            # Check (round 3's WAVE/BUSY/32 read 0.48 for the accumulate): a
+            # launch of more waves than fit reads at most its occupancy --
+            # k_verify_decompress (244 VGPRs, 2 waves per SIMD, 7.9 launched
+            # per SIMD) reads 1.78; the 2^20 accumulate (4100 waves) reads
+            # 1.77 in the bench stream, where it carries the 13 KB LDS pad
+            # beside another MSM (3 workgroups per CU: its 1025 workgroups
+            # take 1.33 rounds, ~2 waves per SIMD averaged over the launch),
+            # and config 5's lone one (961 workgroups) 2.24.  (rocprofv3's
+            # VGPR_Count column reads half the compiler's count on gfx950.)
             cyc = mean["GRBM_GUI_ACTIVE"] / 8
             e["waves_per_simd"] = 4.0 * mean["SQ_WAVE_CYCLES"] / max(cyc, 1) / 1024
             e["launch_waves_per_simd"] = w / 1024

@@ -116,6 +116,12 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
     return (size_t)std::max(1, ncu) * 4 * ACC_T;
   }();
   uint32_t K = (uint32_t)std::min<size_t>(128, std::max<size_t>(4, ((E_max + round_lanes - 1) / round_lanes + 3) & ~(size_t)3));
+  // an MSM alone on the device (the lone reduction shape) with K >= 32 takes
+  // K >= 48: fewer buckets cross lane borders, so its latency-bound reduction
+  // assembles fewer pieces (config 5, K 36 -> 48, three interleaved passes:
+  // reduce 0.216-0.218 -> 0.194-0.195 ms, accumulate 0.399 -> 0.394-0.398;
+  // profiles/r04_verify_k_ab.txt)
+  if (rlog == RWAVE_LOG_LONE && K >= 32) K = std::max<uint32_t>(K, 48);
   if (const char* ek = getenv("BPP_MSM_ACC_K")) K = (uint32_t)std::min(128, std::max(4, atoi(ek) & ~3));  // A/B runs
   const size_t lanes = (E_max + K - 1) / K + 1;
   // a heavy bucket spans > FIX_MAX chunks, so holds > (FIX_MAX - 1) K

@@ -89,7 +89,10 @@ def main():
             # 1.77 in the bench stream, where it carries the 13 KB LDS pad
             # beside another MSM (3 workgroups per CU: its 1025 workgroups
             # take 1.33 rounds, ~2 waves per SIMD averaged over the launch),
-            # and config 5's lone one (961 workgroups) 2.24.  (rocprofv3's
+            # and config 5's lone one (961 workgroups) 2.24 although 4 of its
+            # 40 KB workgroups fit a CU (tools/ubench/lds_occ.hip: 3.9
+            # resident at 40960 B, 3.0 at 41216) -- a launch-average that
+            # also counts the tail, read it relative.  (rocprofv3's
             # VGPR_Count column reads half the compiler's count on gfx950.)
             cyc = mean["GRBM_GUI_ACTIVE"] / 8
             e["waves_per_simd"] = 4.0 * mean["SQ_WAVE_CYCLES"] / max(cyc, 1) / 1024

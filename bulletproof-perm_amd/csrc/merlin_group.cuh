@@ -46,6 +46,9 @@
 #ifndef GRP_TRASH
 #define GRP_TRASH 60  // first trash dword of grp_keccak16 (50: the former layout, A/B)
 #endif
+#ifndef GRP_K16_FULL
+#define GRP_K16_FULL 1  // grp_keccak16 fully unrolled (0: the rolled loop, A/B)
+#endif
 #define GRP_SCR_BYTES 280  // the pi scratch: 200 bytes of state + the copies' trash words (16-lane: dwords 60..69)
 
 // rho offsets r[x][y] packed per y (6 bits per x) and the pi destination row
@@ -160,6 +163,42 @@ __device__ __noinline__ static void grp_keccak16(lds_u64* st, lds_u64* scr, uint
   rd[1] = 10 * ((x + 1) % 5) + h;
   rd[2] = 10 * ((x + 2) % 5) + h;
   const uint32_t ms = x == 0 ? ~0u : 0u;
+#if GRP_K16_FULL
+  // All 24 rounds unrolled with the round constants as literals: iota is one
+  // XOR on the chain (its lane-dependent constant is formed off the chain),
+  // and the rounds carry no scalar-memory load of KECCAK_RC -- whose
+  // s_load shared the lgkmcnt wait of the chi reads -- and no loop counter;
+  // rho/pi issues the five XORs, then the five DPP moves, then the rotates
+  // and stores, so no DPP waits on the XOR just before it (s_nop 1 each).
+  constexpr uint64_t RC[24] = {
+      0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808aull, 0x8000000080008000ull,
+      0x000000000000808bull, 0x0000000080000001ull, 0x8000000080008081ull, 0x8000000000008009ull,
+      0x000000000000008aull, 0x0000000000000088ull, 0x0000000080008009ull, 0x000000008000000aull,
+      0x000000008000808bull, 0x800000000000008bull, 0x8000000000008089ull, 0x8000000000008003ull,
+      0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800aull, 0x800000008000000aull,
+      0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
+  _Pragma("unroll") for (int r = 0; r < 24; ++r) {
+    const uint32_t cc = xor3(xor3(a[0], a[1], a[2]), a[3], a[4]);
+    const uint32_t cp_same = grp_dpp<0x102>(cc);
+    const uint32_t o1 = grp_dpp<0x101>(cc), o3 = grp_dpp<0x103>(cc);
+    const uint32_t cp_other = o3 ^ ((o1 ^ o3) & hm);
+    const uint32_t cm_same = grp_dpp<0x112>(cc);
+    const uint32_t d = cm_same ^ __builtin_amdgcn_alignbit(cp_same, cp_other, 31);
+    uint32_t v[5], pv[5];
+    _Pragma("unroll") for (int y = 0; y < 5; ++y) v[y] = a[y] ^ d;
+    _Pragma("unroll") for (int y = 0; y < 5; ++y) pv[y] = grp_dpp<0xB1>(v[y]);
+    GRP_FENCE();
+    _Pragma("unroll") for (int y = 0; y < 5; ++y) scr32[w[y]] = __builtin_amdgcn_alignbit(v[y], pv[y], c[y]);
+    GRP_FENCE();
+    _Pragma("unroll") for (int y = 0; y < 5; ++y) {
+      const uint32_t b0 = scr32[rd[0] + 2 * y], b1 = scr32[rd[1] + 2 * y], b2 = scr32[rd[2] + 2 * y];
+      a[y] = b0 ^ (~b1 & b2);
+    }
+    GRP_FENCE();
+    const uint32_t rl = (uint32_t)RC[r], rh = (uint32_t)(RC[r] >> 32);
+    a[0] ^= (rl ^ ((rl ^ rh) & hm)) & ms;
+  }
+#else
   _Pragma("unroll 2") for (int r = 0; r < 24; ++r) {
     // theta: this half's column parity; the neighbours' from the pairs beside
     const uint32_t cc = xor3(xor3(a[0], a[1], a[2]), a[3], a[4]);
@@ -184,6 +223,7 @@ __device__ __noinline__ static void grp_keccak16(lds_u64* st, lds_u64* scr, uint
     const uint32_t rl = (uint32_t)rc, rh = (uint32_t)(rc >> 32);
     a[0] ^= (rl ^ ((rl ^ rh) & hm)) & ms;
   }
+#endif
   if (canon) {
     lds_u32* stw = (lds_u32*)st;
     _Pragma("unroll") for (int y = 0; y < 5; ++y) stw[2 * (x + 5 * y) + h] = a[y];

@@ -318,7 +318,14 @@ __global__ void __launch_bounds__(64) k_verify_consts(uint32_t count, uint32_t l
   sc_store(K + 8 * VK_NXP, sc_neg(ldm(VREC_XPERM)));
 }
 
-__global__ void __launch_bounds__(POLY_T) k_verify_scalars(
+// (at 4 waves per SIMD: 128 VGPRs instead of 148, 108 B of spills, 8
+// workgroups per CU instead of 6 -- 2 rounds for 4096 proofs instead of 2.7;
+// three interleaved passes 0.281-0.283 vs 0.294-0.297 ms with the constants
+// and the merge, 0.309-0.312 at 5, profiles/r04_verify_vs_ab.txt)
+#ifndef VS_WPE
+#define VS_WPE 4
+#endif
+__global__ void __launch_bounds__(POLY_T) __attribute__((amdgpu_waves_per_eu(VS_WPE))) k_verify_scalars(
     uint32_t n_p, uint32_t m, uint32_t Q, uint32_t lg, const uint32_t* __restrict__ rec,
     const uint32_t* __restrict__ kc, const uint32_t* __restrict__ cp, const uint32_t* __restrict__ ce,
     const uint32_t* __restrict__ cR, uint32_t* __restrict__ gen, uint32_t* __restrict__ sc_out, uint32_t NG,

@@ -49,6 +49,9 @@
 #ifndef GRP_K16_FULL
 #define GRP_K16_FULL 1  // grp_keccak16 fully unrolled (0: the rolled loop, A/B)
 #endif
+#ifndef GRP_CHI128
+#define GRP_CHI128 0  // chi reads half-columns as 16-B + 4-B reads (A/B; needs RG_SCR_OFF 208, RG_GS 736)
+#endif
 #define GRP_SCR_BYTES 280  // the pi scratch: 200 bytes of state + the copies' trash words (16-lane: dwords 60..69)
 
 // rho offsets r[x][y] packed per y (6 bits per x) and the pi destination row
@@ -156,12 +159,24 @@ __device__ __noinline__ static void grp_keccak16(lds_u64* st, lds_u64* scr, uint
     const uint32_t Y = (2 * x + 3 * y) % 5;
     // (copies: trash dwords 60..69, placed so that they share no bank with
     // the same instruction's state stores, tools/lds_banks.py)
+#if GRP_CHI128
+    // (half-column layout: half h of column X at dwords 12 (2 X + h) + row;
+    // the copies' trash words past them)
+    const uint32_t wc = 12 * (2 * y + (sw ^ h)) + Y, wt = 120 + 2 * y + h;
+#else
     const uint32_t wc = 2 * (5 * y + Y) + (sw ^ h), wt = GRP_TRASH + 2 * y + h;
+#endif
     w[y] = (wc & cm) | (wt & ~cm);
   }
+#if GRP_CHI128
+  rd[0] = 12 * (2 * x + h);
+  rd[1] = 12 * (2 * ((x + 1) % 5) + h);
+  rd[2] = 12 * (2 * ((x + 2) % 5) + h);
+#else
   rd[0] = 10 * x + h;
   rd[1] = 10 * ((x + 1) % 5) + h;
   rd[2] = 10 * ((x + 2) % 5) + h;
+#endif
   const uint32_t ms = x == 0 ? ~0u : 0u;
 #if GRP_K16_FULL
   // All 24 rounds unrolled with the round constants as literals: iota is one
@@ -190,10 +205,28 @@ __device__ __noinline__ static void grp_keccak16(lds_u64* st, lds_u64* scr, uint
     GRP_FENCE();
     _Pragma("unroll") for (int y = 0; y < 5; ++y) scr32[w[y]] = __builtin_amdgcn_alignbit(v[y], pv[y], c[y]);
     GRP_FENCE();
+#if GRP_CHI128
+    {
+      // each half-column as one 16-B read (rows 0..3) and one dword (row 4)
+      typedef uint32_t grp_v4 __attribute__((ext_vector_type(4)));
+      typedef __attribute__((address_space(3))) grp_v4 lds_v4;
+      uint32_t b[3][5];
+      _Pragma("unroll") for (int k = 0; k < 3; ++k) {
+        const grp_v4 q = *(const lds_v4*)(scr32 + rd[k]);
+        b[k][0] = q.x;
+        b[k][1] = q.y;
+        b[k][2] = q.z;
+        b[k][3] = q.w;
+        b[k][4] = scr32[rd[k] + 4];
+      }
+      _Pragma("unroll") for (int y = 0; y < 5; ++y) a[y] = b[0][y] ^ (~b[1][y] & b[2][y]);
+    }
+#else
     _Pragma("unroll") for (int y = 0; y < 5; ++y) {
       const uint32_t b0 = scr32[rd[0] + 2 * y], b1 = scr32[rd[1] + 2 * y], b2 = scr32[rd[2] + 2 * y];
       a[y] = b0 ^ (~b1 & b2);
     }
+#endif
     GRP_FENCE();
     const uint32_t rl = (uint32_t)RC[r], rh = (uint32_t)(RC[r] >> 32);
     a[0] ^= (rl ^ ((rl ^ rh) & hm)) & ms;

@@ -187,6 +187,11 @@ int ctx_d2h(bpp_ctx* ctx, void* h, const void* d, size_t bytes);
 // Wait for ctx's stream (event poll with short sleeps, see ctx.hip) +
 // recycle the upload arena.
 int ctx_sync(bpp_ctx* ctx);
+// ctx_sync for a latency-bound single call (a lone MSM, a batch
+// verification's two round trips): polls the event without sleeping for up to
+// spin_us first (a 5 us nanosleep sleeps ~55 us under the default timer
+// slack, and these calls wait on the GPU twice or three times per result).
+int ctx_sync_latency(bpp_ctx* ctx, unsigned spin_us = 400);
 // i-th child context of ctx (created on first use, destroyed with ctx).
 int ctx_child(bpp_ctx* ctx, size_t i, bpp_ctx** out);
 

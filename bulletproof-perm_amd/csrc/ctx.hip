@@ -6,20 +6,23 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
 
 #include "ctx.h"
 #include "host/par.h"
 
-// memcpy to / from the pinned arena, split over the host pool above 512 KB
-// (a 2.6 MB scalar upload is ~0.25 ms on one core of the box)
+// memcpy to / from the pinned arena, split over the copy pool above 512 KB
+// (a 2.6 MB scalar upload is ~0.25 ms on one core of the box; par.h
+// copy_threads)
 void ctx_stage_copy(void* dst, const void* src, size_t bytes) {
   const size_t chunk = 128u << 10;
   if (bytes < (512u << 10)) {
     memcpy(dst, src, bytes);
     return;
   }
-  par::for_each((bytes + chunk - 1) / chunk, [&](size_t i) {
+  par::for_each_copy((bytes + chunk - 1) / chunk, [&](size_t i) {
     const size_t o = i * chunk;
     memcpy((uint8_t*)dst + o, (const uint8_t*)src + o, std::min(chunk, bytes - o));
   });
@@ -103,6 +106,29 @@ int ctx_sync(bpp_ctx* ctx) {
   BPP_HIP(hipEventRecord(ctx->sync_ev, ctx->stream));
   for (hipError_t r; (r = hipEventQuery(ctx->sync_ev)) != hipSuccess;) {
     if (r != hipErrorNotReady) BPP_HIP(r);
+    struct timespec ts = {0, 5000L};
+    nanosleep(&ts, nullptr);
+  }
+  ctx->zc_live.clear();
+  ctx->stage_used = 0;
+  return BPP_OK;
+}
+
+int ctx_sync_latency(bpp_ctx* ctx, unsigned spin_us) {
+  static const int spin_env = [] {  // (BPP_SYNC_SPIN_US overrides, for A/B; 0 = ctx_sync)
+    const char* e = getenv("BPP_SYNC_SPIN_US");
+    return e ? atoi(e) : -1;
+  }();
+  if (spin_env >= 0) spin_us = (unsigned)spin_env;
+  if (!ctx->sync_ev) BPP_HIP(hipEventCreateWithFlags(&ctx->sync_ev, hipEventDisableTiming));
+  BPP_HIP(hipEventRecord(ctx->sync_ev, ctx->stream));
+  const auto t0 = std::chrono::steady_clock::now();
+  for (hipError_t r; (r = hipEventQuery(ctx->sync_ev)) != hipSuccess;) {
+    if (r != hipErrorNotReady) BPP_HIP(r);
+    if (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(spin_us)) {
+      __builtin_ia32_pause();
+      continue;
+    }
     struct timespec ts = {0, 5000L};
     nanosleep(&ts, nullptr);
   }

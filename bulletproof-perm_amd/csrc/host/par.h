@@ -67,9 +67,9 @@ inline unsigned threads() {
 // the job and waits for the workers still inside it to leave.
 class Pool {
  public:
-  explicit Pool(unsigned workers) {
+  explicit Pool(unsigned workers, int spin_us = -1) {
     const char* e = getenv("BPP_POOL_SPIN_US");
-    spin_us_ = e ? atoi(e) : 300;
+    spin_us_ = spin_us >= 0 ? spin_us : e ? atoi(e) : 300;
     for (unsigned i = 0; i < workers; ++i)
       th_.emplace_back([this] {
         pthread_setname_np(pthread_self(), "bpp-pool");  // (host profiles tell workers from drivers)
@@ -184,6 +184,37 @@ class Pool {
 inline Pool& pool() {
   static Pool p(threads() - 1);
   return p;
+}
+
+// Threads for bulk host copies into the pinned staging arena (ctx_stage_copy):
+// BPP_COPY_THREADS or min(granted CPUs / LOCAL_WORLD_SIZE, 8).  A batch
+// verification stages 17 MB of proofs before its replay can start; on the
+// compute pool's 4 threads the staging ran at ~32 GB/s, below the copy
+// engine's rate, and paced the upload.  Its own pool: the workers sleep
+// between copies, so the prover's pool keeps its size.
+inline unsigned copy_threads() {
+  static const unsigned n = [] {
+    const char* e = getenv("BPP_COPY_THREADS");
+    unsigned share = granted_cpus();
+    if (const char* lw = getenv("LOCAL_WORLD_SIZE")) share = std::max(1u, share / std::max(1, atoi(lw)));
+    return std::max(1u, e ? (unsigned)atoi(e) : std::min(8u, share));
+  }();
+  return n;
+}
+
+inline Pool& copy_pool() {
+  static Pool p(copy_threads() - 1, 50);  // (copies come in bursts: a short spin)
+  return p;
+}
+
+template <class F>
+void for_each_copy(size_t n, F&& f) {
+  if (n <= 1 || copy_threads() <= 1 || Pool::in_worker()) {
+    for (size_t i = 0; i < n; ++i) f(i);
+    return;
+  }
+  const std::function<void(size_t)> fn = [&](size_t i) { f(i); };
+  copy_pool().run(n, fn);
 }
 
 template <class F>

@@ -50,7 +50,17 @@
 #define GRP_K16_FULL 1  // grp_keccak16 fully unrolled (0: the rolled loop, A/B)
 #endif
 #ifndef GRP_CHI128
-#define GRP_CHI128 0  // chi reads half-columns as 16-B + 4-B reads (A/B; needs RG_SCR_OFF 208, RG_GS 736)
+#define GRP_CHI128 1  // chi reads half-columns as 16-B + 4-B reads (0: the former dword layout, A/B)
+#endif
+#if GRP_CHI128 && !GRP_K16_FULL
+#error "GRP_CHI128 is implemented in the unrolled grp_keccak16 only"
+#endif
+#if GRP_CHI128
+#define GRP_SCR_OFF 208  // the pi scratch's offset in a group's block (16-B aligned for the chi reads)
+#define GRP_BLOCK 736    // a group's sponge + scratch block (130 scratch dwords)
+#else
+#define GRP_SCR_OFF 200
+#define GRP_BLOCK 576
 #endif
 #define GRP_SCR_BYTES 280  // the pi scratch: 200 bytes of state + the copies' trash words (16-lane: dwords 60..69)
 

@@ -329,7 +329,7 @@ int msm_single_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx,
   void* h = nullptr;
   BPP_TRY(ctx_pinned(ctx, (size_t)Wn * nterms * P3_BYTES, &h));
   BPP_HIP(hipMemcpyAsync(h, d_ws, (size_t)Wn * nterms * P3_BYTES, hipMemcpyDeviceToHost, ctx->stream));
-  BPP_TRY(ctx_sync(ctx));
+  BPP_TRY(ctx_sync_latency(ctx));
   *out = horner_host_terms((const uint32_t*)h, Wn, nterms, c, wb, rlog + 6);
   return BPP_OK;
 }

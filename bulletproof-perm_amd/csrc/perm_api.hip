@@ -1186,7 +1186,7 @@ int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label,
   } else if (dec_order == 2) {
     BPP_TRY(launch_dec());
   }
-  BPP_TRY(ctx_sync(ctx));
+  BPP_TRY(ctx_sync_latency(ctx));
   uint32_t any = 0;
   for (size_t p = 0; p < rcount; ++p) any |= h_bad[p];
   if (any) return BPP_ERR_VERIFY;
@@ -1325,7 +1325,7 @@ int verify_partial_dev(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J,
   BPP_HIP(hipStreamWaitEvent(ctx->stream, ctx->vj_ev_dec, 0));
   BPP_HIP(hipMemcpyAsync(h_dbad, d_dbad, 8, hipMemcpyDeviceToHost, ctx->stream));
   BPP_TRY(verify_msm(ctx, G, J.C, count, (const uint32_t*)d_sv, (const uint32_t*)d_x, wb, we, out));
-  BPP_TRY(ctx_sync(ctx));  // (msm_single_dev has synchronised; this keeps h_dbad's contract)
+  BPP_TRY(ctx_sync_latency(ctx));  // (msm_single_dev has synchronised; this keeps h_dbad's contract)
   if (*h_dbad != ~0ull) {
     ctx->err = "undecodable proof point at index " + std::to_string(*h_dbad);
     return BPP_ERR_VERIFY;

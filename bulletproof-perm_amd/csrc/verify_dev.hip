@@ -53,9 +53,9 @@ FE_INLINE bool w8_zero(const uint32_t w[8]) {
 // every chi load and all but 2 of a round's pi stores (tools/lds_banks.py: 2
 // extra LDS cycles a round against 20 at the former 480-B stride, where every
 // chi load was 2-way)
-#ifndef RG_GS  // (A/B: -DRG_GS=480 -DRG_SCR_OFF=240 -DGRP_TRASH=50 is the former layout)
-#define RG_GS 576
-#define RG_SCR_OFF 200
+#ifndef RG_GS  // (A/B: -DGRP_CHI128=0 -DRG_GS=480 -DRG_SCR_OFF=240 -DGRP_TRASH=50 is the round-3 layout)
+#define RG_GS GRP_BLOCK
+#define RG_SCR_OFF GRP_SCR_OFF
 #endif
 template <bool STAGED>
 __global__ void __launch_bounds__(64) k_verify_replay_g(uint32_t count, uint32_t k, uint32_t lg, uint32_t n_p,

@@ -25,26 +25,26 @@ __global__ void __launch_bounds__(64) k_lane(unsigned long long* cyc, uint32_t* 
 }
 
 __global__ void __launch_bounds__(64) k_group(unsigned long long* cyc, uint32_t* sink) {
-  __shared__ __attribute__((aligned(16))) uint8_t sp[8 * 576];
+  __shared__ __attribute__((aligned(16))) uint8_t sp[8 * GRP_BLOCK];
   const uint32_t g = threadIdx.x >> 3, gl = threadIdx.x & 7;
-  uint8_t* st = sp + g * 576;  // (verify_dev.hip RG_GS / RG_SCR_OFF)
+  uint8_t* st = sp + g * GRP_BLOCK;  // (merlin_group.cuh GRP_BLOCK / GRP_SCR_OFF)
   for (int i = gl; i < 25; i += 8) reinterpret_cast<uint64_t*>(st)[i] = i * 0x9e3779b97f4a7c15ull + g;
   __builtin_amdgcn_s_waitcnt(0);
   const unsigned long long t0 = clock64();
-  for (int n = 0; n < NPERM; ++n) grp_keccak((lds_u64*)st, (lds_u64*)(st + 200), gl);
+  for (int n = 0; n < NPERM; ++n) grp_keccak((lds_u64*)st, (lds_u64*)(st + GRP_SCR_OFF), gl);
   const unsigned long long t1 = clock64();
   if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
   sink[blockIdx.x * 64 + threadIdx.x] = reinterpret_cast<uint32_t*>(st)[gl];
 }
 
 __global__ void __launch_bounds__(64) k_group16(unsigned long long* cyc, uint32_t* sink) {
-  __shared__ __attribute__((aligned(16))) uint8_t sp[4 * 576];
+  __shared__ __attribute__((aligned(16))) uint8_t sp[4 * GRP_BLOCK];
   const uint32_t g = threadIdx.x >> 4, gl = threadIdx.x & 15;
-  uint8_t* st = sp + g * 576;
+  uint8_t* st = sp + g * GRP_BLOCK;
   for (int i = gl; i < 25; i += 16) reinterpret_cast<uint64_t*>(st)[i] = i * 0x9e3779b97f4a7c15ull + g;
   __builtin_amdgcn_s_waitcnt(0);
   const unsigned long long t0 = clock64();
-  for (int n = 0; n < NPERM; ++n) grp_keccak16((lds_u64*)st, (lds_u64*)(st + 200), gl);
+  for (int n = 0; n < NPERM; ++n) grp_keccak16((lds_u64*)st, (lds_u64*)(st + GRP_SCR_OFF), gl);
   const unsigned long long t1 = clock64();
   if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
   sink[blockIdx.x * 64 + threadIdx.x] = reinterpret_cast<uint32_t*>(st)[gl];
@@ -53,24 +53,24 @@ __global__ void __launch_bounds__(64) k_group16(unsigned long long* cyc, uint32_
 // the three permutations agree on the same inputs (8 states per block)
 __global__ void __launch_bounds__(64) k_check(uint32_t* bad) {
   __shared__ __attribute__((aligned(16))) uint64_t ref[8 * 25];
-  __shared__ __attribute__((aligned(16))) uint8_t s8[8 * 576];
-  __shared__ __attribute__((aligned(16))) uint8_t s16[4 * 576];
+  __shared__ __attribute__((aligned(16))) uint8_t s8[8 * GRP_BLOCK];
+  __shared__ __attribute__((aligned(16))) uint8_t s16[4 * GRP_BLOCK];
   for (int i = threadIdx.x; i < 8 * 25; i += 64) ref[i] = (i % 25) * 0x9e3779b97f4a7c15ull + (i / 25) * 0x1234567ull;
   for (int i = threadIdx.x; i < 8 * 25; i += 64)
-    reinterpret_cast<uint64_t*>(s8 + (i / 25) * 576)[i % 25] = ref[i];
+    reinterpret_cast<uint64_t*>(s8 + (i / 25) * GRP_BLOCK)[i % 25] = ref[i];
   for (int i = threadIdx.x; i < 4 * 25; i += 64)
-    reinterpret_cast<uint64_t*>(s16 + (i / 25) * 576)[i % 25] = ref[i];
+    reinterpret_cast<uint64_t*>(s16 + (i / 25) * GRP_BLOCK)[i % 25] = ref[i];
   __syncthreads();
   if (threadIdx.x < 8) lane_keccak((lds_u64*)(ref + 25 * threadIdx.x));
-  grp_keccak((lds_u64*)(s8 + (threadIdx.x >> 3) * 576), (lds_u64*)(s8 + (threadIdx.x >> 3) * 576 + 240),
+  grp_keccak((lds_u64*)(s8 + (threadIdx.x >> 3) * GRP_BLOCK), (lds_u64*)(s8 + (threadIdx.x >> 3) * GRP_BLOCK + GRP_SCR_OFF),
              threadIdx.x & 7);
-  grp_keccak16((lds_u64*)(s16 + (threadIdx.x >> 4) * 576), (lds_u64*)(s16 + (threadIdx.x >> 4) * 576 + 240),
+  grp_keccak16((lds_u64*)(s16 + (threadIdx.x >> 4) * GRP_BLOCK), (lds_u64*)(s16 + (threadIdx.x >> 4) * GRP_BLOCK + GRP_SCR_OFF),
                threadIdx.x & 15);
   __syncthreads();
   uint32_t nb = 0;
   for (int i = threadIdx.x; i < 8 * 25; i += 64) {
-    nb += reinterpret_cast<uint64_t*>(s8 + (i / 25) * 576)[i % 25] != ref[i];
-    if (i < 4 * 25) nb += reinterpret_cast<uint64_t*>(s16 + (i / 25) * 576)[i % 25] != ref[i];
+    nb += reinterpret_cast<uint64_t*>(s8 + (i / 25) * GRP_BLOCK)[i % 25] != ref[i];
+    if (i < 4 * 25) nb += reinterpret_cast<uint64_t*>(s16 + (i / 25) * GRP_BLOCK)[i % 25] != ref[i];
   }
   atomicAdd(bad, nb);
 }

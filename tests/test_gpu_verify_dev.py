@@ -196,6 +196,16 @@ def test_config5_full_size(ctx):
     assert bj.ok  # (well-formed: only the MSM check fails)
     assert not bpperm.partials_is_identity(_window_partials(pr, bj, 8))
     bj.close()
+    # the proof points are decompressed per upload chunk (4 chunks here, 3
+    # uneven ones of 333 / 333 / 334 proofs at 1000): an undecodable point
+    # in the last chunk, in a middle one, and in both is still caught
+    for n in (4096, 1000):
+        assert pr.verify_batch(proofs[:n], Vs[:n])
+        for where in ([n - 1], [n // 2], [n // 3, n - 2]):
+            ud = list(proofs[:n])
+            for i in where:
+                ud = _tampered(ud, i, 11 * 32 + 31, 0x80)  # L_0's top bit
+            assert not pr.verify_batch(ud, Vs[:n]), (n, where)
     g.close()
 
 

@@ -1059,7 +1059,7 @@ int verify_partial(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J, con
 }
 
 // pass 1 on the device (bpp_perm_verify_begin_dev): upload the proofs and V,
-// replay every transcript on the GPU (k_verify_replay, one lane per proof)
+// replay every transcript on the GPU (k_verify_replay_g, one 16-lane group per proof)
 // and return the r challenges; meanwhile the proof points are decompressed
 // on child stream VJ_CHILD into the "vj_x" workspace (k_verify_decompress,
 // independent of the replay: the 64 replay waves are latency-bound, the
@@ -1096,7 +1096,7 @@ int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label,
   BPP_TRY(ctx_ws(ctx, "vj_in", count * (plen + vbytes), &d_in));
   const uint32_t* d_pf = (const uint32_t*)d_in;
   const uint32_t* d_V = (const uint32_t*)((uint8_t*)d_in + count * plen);
-  // (+1: the pad record of k_verify_replay's lanes past the batch)
+  // (+1: the pad record of the replay's groups past the batch)
   BPP_TRY(ctx_ws(ctx, "vj_rec", (count + 1) * vrec_n(C) * 32, &d_rec));
   BPP_TRY(ctx_ws(ctx, "vj_x", npts * MSM_NIELS_WORDS * 4, &d_x));
   BPP_TRY(ctx_ws(ctx, "vj_dbad", 8, &d_dbad));

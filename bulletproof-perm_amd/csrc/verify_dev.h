@@ -24,8 +24,8 @@ inline uint32_t vrec_n(const perm::Circuit& C) { return VREC_U + 2 * C.lg; }
 // T5 T6, L_0.., R_0..
 inline uint32_t vpts_n(const perm::Circuit& C) { return C.m + 8 + 2 * C.lg; }
 
-// Replays `count` transcripts on the device, one lane per proof
-// (k_verify_replay): d_proofs [count][proof_len] and d_V [count][m][32] on
+// Replays `count` transcripts on the device, one per 16-lane group
+// (k_verify_replay_g, then k_verify_reduce and k_verify_replay_post): d_proofs [count][proof_len] and d_V [count][m][32] on
 // the device; init = the 52-word transcript state every proof shares (the
 // label's Transcript::new and arithmetic_domain_sep(n_p); verify_init_state).
 // Writes d_rec (weights, y^-1 and the u_j^-1 left for verify_weights_dev),

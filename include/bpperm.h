@@ -290,8 +290,8 @@ int bpp_perm_verify_batch(bpp_ctx* ctx, const bpp_gens* g, uint32_t k, size_t co
 typedef struct bpp_verify_job bpp_verify_job;
 int bpp_perm_verify_begin(uint32_t k, size_t count, const uint8_t* label, size_t llen, const uint8_t* proofs,
                           const uint8_t* V, uint8_t* r_out, bpp_verify_job** out);
-/* The same host interface with the replay on the GPU of ctx (one lane per
- * proof, k_verify_replay): uploads the proofs and V, replays every
+/* The same host interface with the replay on the GPU of ctx (one Merlin
+ * transcript per 16-lane group, k_verify_replay_g): uploads the proofs and V, replays every
  * transcript, decompresses the proof points and returns r (count x 32 B, may
  * be NULL).  r is byte-identical to bpp_perm_verify_begin's.  The job keeps
  * its records and points in ctx's workspaces: it is valid for

@@ -187,17 +187,17 @@ inline Pool& pool() {
 }
 
 // Threads for bulk host copies into the pinned staging arena (ctx_stage_copy):
-// BPP_COPY_THREADS or min(granted CPUs / LOCAL_WORLD_SIZE, 8).  A batch
-// verification stages 17 MB of proofs before its replay can start; on the
-// compute pool's 4 threads the staging ran at ~32 GB/s, below the copy
-// engine's rate, and paced the upload.  Its own pool: the workers sleep
-// between copies, so the prover's pool keeps its size.
+// BPP_COPY_THREADS or min(granted CPUs / LOCAL_WORLD_SIZE, 4).  Its own pool,
+// so that a batch verification's 17 MB of staging does not queue behind the
+// prover's host phases on the compute pool; 8 threads measured the same as 4
+// on the config-5 upload (0.23-0.28 ms either way: the copy engine paces it,
+// profiles/r04_copy_ab.txt).
 inline unsigned copy_threads() {
   static const unsigned n = [] {
     const char* e = getenv("BPP_COPY_THREADS");
     unsigned share = granted_cpus();
     if (const char* lw = getenv("LOCAL_WORLD_SIZE")) share = std::max(1u, share / std::max(1, atoi(lw)));
-    return std::max(1u, e ? (unsigned)atoi(e) : std::min(8u, share));
+    return std::max(1u, e ? (unsigned)atoi(e) : std::min(4u, share));
   }();
   return n;
 }

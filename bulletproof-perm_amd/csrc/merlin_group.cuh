@@ -49,6 +49,9 @@
 #ifndef GRP_K16_FULL
 #define GRP_K16_FULL 1  // grp_keccak16 fully unrolled (0: the rolled loop, A/B)
 #endif
+#ifndef GRP_PAR_APPEND
+#define GRP_PAR_APPEND 0  // append32 as one parallel XOR over the group (A/B)
+#endif
 #ifndef GRP_CHI128
 #define GRP_CHI128 1  // chi reads half-columns as 16-B + 4-B reads (0: the former dword layout, A/B)
 #endif
@@ -368,6 +371,45 @@ struct GroupStrobe {
     pos += fl;
     return true;
   }
+#if GRP_PAR_APPEND
+  // append_message(label, 32 bytes) when the framing and the message end
+  // before the rate, as ONE XOR of the 8 + ln framing bytes and the message
+  // into the sponge by the group's lanes, a dword each (lane gl: sponge dword
+  // (pos >> 2) + gl), instead of the leader's byte and dword read-modify-
+  // writes one after another; msg = the message's 8 words, readable by every
+  // lane (the staged proof bytes).  Byte-identical to frame_fast + absorb32.
+  FE_INLINE bool append32_par(const char* label, uint32_t ln, const uint32_t* msg) {
+    const uint32_t fl = 8 + ln;
+    if (pos + fl + 32 >= LANE_STROBE_R) return false;
+    uint32_t FD[3] = {0u, 0u, 0u};  // the framing bytes, little-endian
+    auto putb = [&](uint32_t i, uint32_t v) { FD[i >> 2] |= (v & 0xffu) << (8 * (i & 3)); };
+    putb(0, pos_begin);
+    putb(1, 18u);  // FLAG_M | FLAG_A
+    for (uint32_t i = 0; i < ln; ++i) putb(2 + i, (uint8_t)label[i]);
+    putb(2 + ln, 32u);   // le32(32)
+    putb(6 + ln, pos + 1);  // the second begin_op: the old begin is this meta's
+    putb(7 + ln, 2u);       // FLAG_A
+    const uint32_t o = pos & 3u, g = gl;
+    const uint32_t fcur = g == 0 ? FD[0] : g == 1 ? FD[1] : g == 2 ? FD[2] : 0u;
+    const uint32_t fprev = g == 1 ? FD[0] : g == 2 ? FD[1] : g == 3 ? FD[2] : 0u;
+    uint32_t M = o ? __builtin_amdgcn_alignbit(fcur, fprev, 32 - 8 * o) : fcur;
+    // the message bytes v .. v + 3 of this lane's dword (v may be negative)
+    const int v = (int)(4 * g) - (int)o - (int)fl;
+    const int qd = v >> 2;
+    const uint32_t r = (uint32_t)v & 3u;
+    const uint32_t lo = (qd >= 0 && qd < 8) ? msg[qd] : 0u;
+    const uint32_t hi = (qd + 1 >= 0 && qd + 1 < 8) ? msg[qd + 1] : 0u;
+    M |= __builtin_amdgcn_alignbit(hi, lo, 8 * r);
+    if (g < 12) {  // (8 + 3 + 32 bytes from offset pos & 3: at most 12 dwords)
+      typedef __attribute__((address_space(3))) uint32_t lds_u32;
+      lds_u32* d = (lds_u32*)st + (pos >> 2) + g;
+      *d ^= M;
+    }
+    pos_begin = pos + 7 + ln;
+    pos += fl + 32;
+    return true;
+  }
+#endif
   FE_INLINE void append32(const char* label, uint32_t ln, const uint32_t w[8]) {
     if (frame_fast(label, ln, 32)) {
       absorb32(w);

@@ -165,7 +165,20 @@ FE_INLINE ge_niels fetch_entry(const uint32_t* __restrict__ tbl, const uint32_t*
   const uint32_t pi = e & 0x7fffffffu;
 #endif
   ge_niels q = pi < n0 ? load_niels(tbl, pi) : load_niels(tbl1, pi - n0);
+#ifdef ACC_NEG_NC
+  // (A/B only) -2dxy uncarried (2p - limb < 2^27.6, a valid multiplier
+  // operand): 10 subtractions instead of a carried fe_neg, but the 2^20
+  // stream ran 1.09 vs 0.85 ms per MSM (accumulate 0.85 vs 0.67 ms; more
+  // spills around the branch), profiles/r04_acc_ab.txt
+  if (e & 0x80000000u) {
+    const fe t = q.ypx;
+    q.ypx = q.ymx;
+    q.ymx = t;
+    q.xy2d = fe_sub_nc(fe_zero(), q.xy2d);
+  }
+#else
   if (e & 0x80000000u) q = ge_niels_neg(q);
+#endif
   return q;
 }
 
@@ -213,13 +226,23 @@ __global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_
   };
   bool owner = false;
   uint32_t b = 0, bstart = 0, bend = 0;
+  // a bucket is heavy when it ends FIX_MAX or more lanes past this one:
+  // ((bend - 1) / K) - l >= FIX_MAX  <=>  bend - 1 >= (l + FIX_MAX) K (no
+  // division by the runtime K in the loop's bucket-close path: accumulate
+  // 0.668-0.671 vs 0.682-0.693 ms at 2^20, three interleaved passes,
+  // profiles/r04_acc_ab.txt; ACC_HEAVY_DIV = the division, A/B)
+  const uint32_t heavy_lim = (l + FIX_MAX) * K;
   ge_p3 acc = ge_identity();
   if (i0 < E) {
     b = bucket_of(boff, nbuckets, i0);
     bstart = boff[b];
     bend = boff[b + 1];
     // the lane where a bucket starts lists it if it is heavy
+#ifndef ACC_HEAVY_DIV
+    if (bstart == i0 && bend - 1 >= heavy_lim) heavy[1 + atomicAdd(&heavy[0], 1u)] = b;
+#else
     if (bstart == i0 && ((bend - 1) / K) - l >= FIX_MAX) heavy[1 + atomicAdd(&heavy[0], 1u)] = b;
+#endif
     // entries are read 4 at a time (one 16-B load; K is a multiple of 4 and
     // the array is padded): a lane's chunk is contiguous, so per-entry 4-B
     // loads touch the same 128-B line K times across a long loop and
@@ -258,7 +281,11 @@ __global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_
         bstart = boff[b];
         bend = boff[b + 1];
 #endif
+#ifndef ACC_HEAVY_DIV
+        if (bend - 1 >= heavy_lim) heavy[1 + atomicAdd(&heavy[0], 1u)] = b;
+#else
         if (((bend - 1) / K) - l >= FIX_MAX) heavy[1 + atomicAdd(&heavy[0], 1u)] = b;
+#endif
         acc = ge_identity();
       }
       acc = ge_madd(acc, fetch_entry(tbl, tbl1, n0, e));

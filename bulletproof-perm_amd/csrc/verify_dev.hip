@@ -99,31 +99,37 @@ __global__ void __launch_bounds__(64) k_verify_replay_g(uint32_t count, uint32_t
     PV = V + (size_t)p * m * 8;
   }
   GRP_FENCE();
+#if GRP_PAR_APPEND
+#define APPEND32(lab, ln, w, src) \
+  if (!t.append32_par(lab, ln, src)) t.append32(lab, ln, w)
+#else
+#define APPEND32(lab, ln, w, src) t.append32(lab, ln, w)
+#endif
   uint32_t* CH = ch + (size_t)(live ? p : count) * nch * 16;
   uint32_t w[8];
   bool ok = true;
   for (uint32_t j = 0; j < 2 * k; ++j) {
     ld8(PV + 8 * j, w);
-    t.append32("V", 1, w);
+    APPEND32("V", 1, w, PV + 8 * j);
   }
   t.challenge64_to("x_perm", 6, CH, true);
   ld8(PV + 16 * k, w);
-  t.append32("V", 1, w);
+  APPEND32("V", 1, w, PV + 16 * k);
   ld8(PP, w);
   ok &= !w8_zero(w);
-  t.append32("A_I", 3, w);
+  APPEND32("A_I", 3, w, PP);
   ld8(PP + 8, w);
   ok &= !w8_zero(w);
-  t.append32("A_O", 3, w);
+  APPEND32("A_O", 3, w, PP + 8);
   ld8(PP + 16, w);
   ok &= !w8_zero(w);
-  t.append32("S", 1, w);
+  APPEND32("S", 1, w, PP + 16);
   t.challenge64_to("y", 1, CH + 16, true);
   t.challenge64_to("z", 1, CH + 32, true);
   auto T_i = [&](int i, const char* lab) {
     ld8(PP + 24 + 8 * i, w);
     ok &= !w8_zero(w);
-    t.append32(lab, 2, w);
+    APPEND32(lab, 2, w, PP + 24 + 8 * i);
   };
   T_i(0, "T1");
   T_i(1, "T3");
@@ -133,13 +139,13 @@ __global__ void __launch_bounds__(64) k_verify_replay_g(uint32_t count, uint32_t
   t.challenge64_to("x", 1, CH + 48, true);
   ld8(PP + 64, w);
   ok &= !sc_geq_l(w);
-  t.append32("TX", 2, w);
+  APPEND32("TX", 2, w, PP + 64);
   ld8(PP + 72, w);
   ok &= !sc_geq_l(w);
-  t.append32("mu", 2, w);
+  APPEND32("mu", 2, w, PP + 72);
   ld8(PP + 80, w);
   ok &= !sc_geq_l(w);
-  t.append32("t", 1, w);
+  APPEND32("t", 1, w, PP + 80);
   t.challenge64_to("w", 1, CH + 64, true);
   t.append_bytes("dom-sep", 7, reinterpret_cast<const uint8_t*>("ipp v1"), 6);
   t.append_u64("n", 1, n_p);
@@ -147,10 +153,10 @@ __global__ void __launch_bounds__(64) k_verify_replay_g(uint32_t count, uint32_t
   for (uint32_t j = 0; j < lg; ++j) {
     ld8(PL + 16 * j, w);
     ok &= !w8_zero(w);
-    t.append32("L", 1, w);
+    APPEND32("L", 1, w, PL + 16 * j);
     ld8(PL + 16 * j + 8, w);
     ok &= !w8_zero(w);
-    t.append32("R", 1, w);
+    APPEND32("R", 1, w, PL + 16 * j + 8);
     t.challenge64_to("u", 1, CH + 16 * (5 + j), true);
   }
   ld8(PL + 16 * lg, w);

@@ -315,7 +315,10 @@ __global__ void __launch_bounds__(64) k_verify_weights(uint32_t count, uint64_t 
 // (VD_WPE waves per SIMD: unconstrained, the compiler takes 244 VGPRs for the
 // inverse square root, 2 waves per SIMD; config 5, interleaved A/B passes:
 // 0.594-0.607 ms unconstrained, 0.554-0.559 at 3 (167 VGPRs, spills outside
-// the squaring loops only), 0.62 at 4, 0.58-0.59 at 6)
+// the squaring loops only), 0.62 at 4, 0.58-0.59 at 6; with the chunked
+// upload, 4 -- so that a replay wave fits beside three decompression waves --
+// shortened the replay stage but not the batch: 2.11-2.15 vs 2.06-2.12 ms,
+// profiles/r04_verify_vd4_ab.txt)
 #ifndef VD_WPE
 #define VD_WPE 3
 #endif

@@ -122,7 +122,8 @@ class Context:
     def profile_reset(self):
         self.lib.bpp_ctx_profile_reset(self.h)
 
-    WORK_COUNTERS = ("msm_terms", "madds", "padds", "msm_launches", "dt_terms", "dt_madds", "dt_launches")
+    WORK_COUNTERS = ("msm_terms", "madds", "padds", "msm_launches", "dt_terms", "dt_madds", "dt_launches",
+                     "ipa_dt_terms", "ipa_dt_madds", "ipa_dt_launches")
 
     def work(self) -> dict:
         """Algorithmic work issued on this context since the last work_reset
@@ -475,9 +476,11 @@ class PermProver:
         return ([praw[i * self.proof_len:(i + 1) * self.proof_len] for i in range(cnt)],
                 [vraw[i * 32 * self.m:(i + 1) * 32 * self.m] for i in range(cnt)])
 
-    def prove_batch_entropy(self, count: int, seeds32: bytes | None = None):
+    def prove_batch_entropy(self, count: int, seeds32: bytes | None = None, raw: bool = False):
         """Production proving: 32 bytes of entropy per proof (seeds32) or,
-        when None, from the OS CSPRNG (bpp_perm_prove_batch_entropy)."""
+        when None, from the OS CSPRNG (bpp_perm_prove_batch_entropy); the
+        batch's secrets are wiped before it returns.  raw=True: the two
+        contiguous buffers (proofs, V), as prove_batch(..., raw=True)."""
         if seeds32 is not None and len(seeds32) != 32 * count:
             raise ValueError("seeds32 must hold 32 bytes per proof")
         pf = C.create_string_buffer(self.proof_len * count)
@@ -486,6 +489,8 @@ class PermProver:
                                                         _buf(self.label), len(self.label), pf, V),
               "bpp_perm_prove_batch_entropy", self.ctx.h)
         praw, vraw = pf.raw, V.raw
+        if raw:
+            return praw, vraw
         return ([praw[i * self.proof_len:(i + 1) * self.proof_len] for i in range(count)],
                 [vraw[i * 32 * self.m:(i + 1) * 32 * self.m] for i in range(count)])
 

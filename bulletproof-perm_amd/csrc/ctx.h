@@ -177,6 +177,12 @@ int ctx_h2d2(bpp_ctx* ctx, void* d, const void* h0, size_t n0, const void* h1, s
 // ctx_h2d_stage hands out `bytes` of staging (valid until the next
 // ctx_sync), ctx_h2d_staged enqueues its copy to d.
 int ctx_h2d_stage(bpp_ctx* ctx, size_t bytes, uint8_t** p);
+// Records [p, p + bytes) of the pinned arena as holding secrets (prove_wipe
+// zeroes the recorded spans).  Overlapping or touching spans are merged: the
+// arena is reused from offset 0 after every ctx_sync, so batches that are
+// never wiped (the u64-seed entry points) leave one span per distinct
+// region, not one per call.
+void ctx_secret_span(bpp_ctx* ctx, uint8_t* p, size_t bytes);
 int ctx_h2d_staged(bpp_ctx* ctx, void* d, const uint8_t* p, size_t bytes);
 // ctx_h2d that skips the copy when workspace `name` (at d) already holds
 // exactly these bytes: for arrays that repeat batch after batch (circuit

@@ -162,6 +162,24 @@ static int stage_take(bpp_ctx* ctx, size_t bytes, uint8_t** out) {
 
 int ctx_h2d_stage(bpp_ctx* ctx, size_t bytes, uint8_t** p) { return stage_take(ctx, bytes, p); }
 
+void ctx_secret_span(bpp_ctx* ctx, uint8_t* p, size_t bytes) {
+  if (!bytes) return;
+  uint8_t *lo = p, *hi = p + bytes;
+  auto& v = ctx->secret_stage;
+  for (size_t i = 0; i < v.size();) {  // absorb every span that overlaps or touches [lo, hi)
+    uint8_t *a = v[i].first, *b = v[i].first + v[i].second;
+    if (a <= hi && lo <= b) {
+      lo = std::min(lo, a);
+      hi = std::max(hi, b);
+      v[i] = v.back();
+      v.pop_back();
+    } else {
+      ++i;
+    }
+  }
+  v.emplace_back(lo, (size_t)(hi - lo));
+}
+
 int ctx_h2d_staged(bpp_ctx* ctx, void* d, const uint8_t* p, size_t bytes) {
   if (bytes) BPP_HIP(hipMemcpyAsync(d, p, bytes, hipMemcpyHostToDevice, ctx->stream));
   return BPP_OK;

@@ -486,7 +486,7 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
     if (fused) {
       const int in = cur, outs = cur ^ 1;
       {
-        ProfScope ps(ctx, "msm_direct");
+        ProfScope ps(ctx, "ipa_round_dt");  // (bench.py: this kernel's own roofline)
         hipLaunchKernelGGL(k_ipa_round_dt, dim3(2 * P), dim3(nt), ipa_round_lds_words(n, nt) * 4, ctx->stream,
                            g.pts.dt, dg, n, m, lg_h, round ? 1u : 0u, S[in][0], S[in][1], S[in][2], S[in][3],
                            S[round ? outs : in][0], S[round ? outs : in][1], S[round ? outs : in][2],
@@ -504,6 +504,9 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
       ctx_work(ctx, "dt_terms", terms);
       ctx_work(ctx, "dt_madds", terms * dg.W);
       ctx_work(ctx, "dt_launches", 1);
+      ctx_work(ctx, "ipa_dt_terms", terms);  // k_ipa_round_dt's share of the dt_* totals
+      ctx_work(ctx, "ipa_dt_madds", terms * dg.W);
+      ctx_work(ctx, "ipa_dt_launches", 1);
       if (dev_merlin) {
         uint8_t* lr = (uint8_t*)d_lr + (size_t)round * P * 64;
         BPP_TRY(points_compress_p3_dev(ctx, (const uint32_t*)d_res, 2 * (size_t)P, lr));

@@ -244,10 +244,37 @@ std::vector<Proof>& proofs_tl();
 static const char* const kSecretWs[] = {"pb_rng_in", "pb_gamma", "mt_s",  "pv_v",   "pv_g",    "pv_gx",  "poly_vec",
                                         "poly_hf",   "pf_l",     "pf_r",  "ipa_am", "ipa_bm",  "ipa_am1", "ipa_bm1"};
 static const char* const kSecretHost[] = {"pp_v", "pp_g"};
+// The device workspaces of kSecretWs zeroed by ONE launch (blockIdx.y = span)
+// instead of one hipMemsetAsync (a fill kernel each) per workspace.
+#define WIPE_MAX 16
+struct WipeSpans {
+  uint8_t* p[WIPE_MAX];
+  uint64_t n[WIPE_MAX];
+};
+static_assert(sizeof(kSecretWs) / sizeof(kSecretWs[0]) <= WIPE_MAX, "WipeSpans too small");
+__global__ void __launch_bounds__(256) k_wipe_spans(WipeSpans w) {
+  uint8_t* p = w.p[blockIdx.y];
+  const uint64_t n = w.n[blockIdx.y], n16 = n >> 4;  // (hipMalloc'd: 16-B aligned)
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x)
+    reinterpret_cast<uint4*>(p)[i] = make_uint4(0, 0, 0, 0);
+  if (blockIdx.x == 0 && threadIdx.x < (n & 15)) p[n16 * 16 + threadIdx.x] = 0;
+}
 int prove_wipe(bpp_ctx* ctx) {
+  WipeSpans w = {};
+  uint32_t cnt = 0;
+  uint64_t most = 0;
   for (const char* n : kSecretWs) {
     auto it = ctx->ws.find(n);
-    if (it != ctx->ws.end() && it->second.p) BPP_HIP(hipMemsetAsync(it->second.p, 0, it->second.bytes, ctx->stream));
+    if (it == ctx->ws.end() || !it->second.p || !it->second.bytes) continue;
+    w.p[cnt] = (uint8_t*)it->second.p;
+    w.n[cnt] = it->second.bytes;
+    most = std::max<uint64_t>(most, it->second.bytes);
+    ++cnt;
+  }
+  if (cnt) {
+    const uint32_t bx = (uint32_t)std::min<uint64_t>(64, (most / 16 + 255) / 256 + 1);
+    hipLaunchKernelGGL(k_wipe_spans, dim3(bx, cnt), dim3(256), 0, ctx->stream, w);
+    BPP_TRY(ctx_check_launch(ctx, "k_wipe_spans"));
   }
   BPP_TRY(ctx_sync(ctx));
   for (const char* n : kSecretHost) {
@@ -348,7 +375,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     // read in place instead, by k_draws through LDS, measured within noise)
     uint8_t* stage = nullptr;
     BPP_TRY(ctx_h2d_stage(ctx, P * tlen + (size_t)P * k * 4, &stage));
-    ctx->secret_stage.emplace_back(stage, P * tlen + (size_t)P * k * 4);  // (prove_wipe)
+    ctx_secret_span(ctx, stage, P * tlen + (size_t)P * k * 4);  // (prove_wipe)
     uint8_t* pis = stage + P * tlen;
     par::for_each((P + 7) / 8, [&](size_t gi) {
       perm::Seed sd[8];
@@ -531,7 +558,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
     uint8_t* stg = nullptr;  // (host witness only) written in place in the pinned arena
     if (!dev_witness) {
       BPP_TRY(ctx_h2d_stage(ctx, (size_t)P * hostw * 32, &stg));
-      ctx->secret_stage.emplace_back(stg, (size_t)P * hostw * 32);  // (prove_wipe)
+      ctx_secret_span(ctx, stg, (size_t)P * hostw * 32);  // (prove_wipe)
       par::for_each(P, [&](size_t p) {
         ProverState& st = *S[p];
         Sc* o = reinterpret_cast<Sc*>(stg) + p * hostw;

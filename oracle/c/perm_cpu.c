@@ -343,8 +343,71 @@ static sc_t draw_sc(uint64_t seed, uint32_t j) {
   return sc_from_wide(b);
 }
 
-/* ================================================================ prover */
 static void enc_pt(uint8_t out[32], const ge_ext* p) { ristretto_encode(out, p); }
+
+/* ================================================================ IPA */
+/* bulletproofs 4.0.0 InnerProductProof::create, folding form, G_factors = 1,
+ * H_factors = hf applied in the first round (App. B2).  a, b (n entries) are
+ * folded in place; writes L_0 R_0 ... L_{lg-1} R_{lg-1} a b (32 B each) to lr. */
+static void ipa_create(transcript_t* tr, const ge_ext* Qp, const ge_ext* G0, const ge_ext* H0, sc_t* a, sc_t* b,
+                       const sc_t* hf, uint32_t n_p, uint8_t* lr) {
+  const ge_ext Q = *Qp;
+  uint32_t nn = n_p;
+  ge_ext* Gv = malloc(sizeof(ge_ext) * n_p);
+  ge_ext* Hv = malloc(sizeof(ge_ext) * n_p);
+  memcpy(Gv, G0, sizeof(ge_ext) * n_p);
+  memcpy(Hv, H0, sizeof(ge_ext) * n_p);
+  sc_t* sv = malloc(sizeof(sc_t) * (n_p + 1));
+  ge_ext* pv = malloc(sizeof(ge_ext) * (n_p + 1));
+  tr_append(tr, "dom-sep", (const uint8_t*)"ipp v1", 6);
+  tr_u64(tr, "n", n_p);
+  int first = 1;
+  while (nn != 1) {
+    nn /= 2;
+    const sc_t cL = sc_inner(a, b + nn, nn), cR = sc_inner(a + nn, b, nn);
+    /* L = <a_lo, G_hi> + <b_hi * hf_lo, H_lo> + c_L Q */
+    for (uint32_t i = 0; i < nn; ++i) {
+      sv[i] = a[i];
+      pv[i] = Gv[nn + i];
+      sv[nn + i] = first ? sc_mul(b[nn + i], hf[i]) : b[nn + i];
+      pv[nn + i] = Hv[i];
+    }
+    sv[2 * nn] = cL;
+    pv[2 * nn] = Q;
+    ge_ext Lp = msm(sv, pv, 2 * nn + 1);
+    for (uint32_t i = 0; i < nn; ++i) {
+      sv[i] = a[nn + i];
+      pv[i] = Gv[i];
+      sv[nn + i] = first ? sc_mul(b[i], hf[nn + i]) : b[i];
+      pv[nn + i] = Hv[nn + i];
+    }
+    sv[2 * nn] = cR;
+    ge_ext Rp = msm(sv, pv, 2 * nn + 1);
+    enc_pt(lr, &Lp);
+    enc_pt(lr + 32, &Rp);
+    tr_append(tr, "L", lr, 32);
+    tr_append(tr, "R", lr + 32, 32);
+    lr += 64;
+    const sc_t u = tr_scalar(tr, "u"), ui = sc_inv(u);
+    for (uint32_t i = 0; i < nn; ++i) {
+      a[i] = sc_add(sc_mul(a[i], u), sc_mul(ui, a[nn + i]));
+      b[i] = sc_add(sc_mul(b[i], ui), sc_mul(u, b[nn + i]));
+      /* G'_i = u^-1 G_lo + u G_hi ; H'_i = u hf_lo H_lo + u^-1 hf_hi H_hi */
+      sc_t s2[2] = {ui, u};
+      ge_ext p2[2] = {Gv[i], Gv[nn + i]};
+      Gv[i] = msm(s2, p2, 2);
+      sc_t h2[2] = {first ? sc_mul(u, hf[i]) : u, first ? sc_mul(ui, hf[nn + i]) : ui};
+      ge_ext q2[2] = {Hv[i], Hv[nn + i]};
+      Hv[i] = msm(h2, q2, 2);
+    }
+    first = 0;
+  }
+  memcpy(lr, a[0].v, 32);
+  memcpy(lr + 32, b[0].v, 32);
+  free(Gv); free(Hv); free(sv); free(pv);
+}
+
+/* ================================================================ prover */
 static ge_ext commit2(const gens_t* g, sc_t v, sc_t gam) {
   sc_t s[2] = {v, gam};
   ge_ext P[2] = {g->B, g->Bb};
@@ -493,62 +556,7 @@ static int prove(const gens_t* G, const circuit_t* C, uint64_t seed, const uint8
     sc_t wq[1] = {w};
     ge_ext Bp[1] = {G->B};
     const ge_ext Q = msm(wq, Bp, 1);
-    uint32_t nn = n_p;
-    ge_ext* Gv = malloc(sizeof(ge_ext) * n_p);
-    ge_ext* Hv = malloc(sizeof(ge_ext) * n_p);
-    memcpy(Gv, G->G, sizeof(ge_ext) * n_p);
-    memcpy(Hv, G->H, sizeof(ge_ext) * n_p);
-    sc_t* a = l; sc_t* b = r;
-    sc_t* hf = y_inv;
-    sc_t* sv = malloc(sizeof(sc_t) * (n_p + 1));
-    ge_ext* pv = malloc(sizeof(ge_ext) * (n_p + 1));
-    tr_append(&tr, "dom-sep", (const uint8_t*)"ipp v1", 6);
-    tr_u64(&tr, "n", n_p);
-    uint8_t* lr = out + 352;
-    int first = 1;
-    while (nn != 1) {
-      nn /= 2;
-      const sc_t cL = sc_inner(a, b + nn, nn), cR = sc_inner(a + nn, b, nn);
-      /* L = <a_lo, G_hi> + <b_hi * hf_lo, H_lo> + c_L Q */
-      for (uint32_t i = 0; i < nn; ++i) {
-        sv[i] = a[i];
-        pv[i] = Gv[nn + i];
-        sv[nn + i] = first ? sc_mul(b[nn + i], hf[i]) : b[nn + i];
-        pv[nn + i] = Hv[i];
-      }
-      sv[2 * nn] = cL;
-      pv[2 * nn] = Q;
-      ge_ext Lp = msm(sv, pv, 2 * nn + 1);
-      for (uint32_t i = 0; i < nn; ++i) {
-        sv[i] = a[nn + i];
-        pv[i] = Gv[i];
-        sv[nn + i] = first ? sc_mul(b[i], hf[nn + i]) : b[i];
-        pv[nn + i] = Hv[nn + i];
-      }
-      sv[2 * nn] = cR;
-      ge_ext Rp = msm(sv, pv, 2 * nn + 1);
-      enc_pt(lr, &Lp);
-      enc_pt(lr + 32, &Rp);
-      tr_append(&tr, "L", lr, 32);
-      tr_append(&tr, "R", lr + 32, 32);
-      lr += 64;
-      const sc_t u = tr_scalar(&tr, "u"), ui = sc_inv(u);
-      for (uint32_t i = 0; i < nn; ++i) {
-        a[i] = sc_add(sc_mul(a[i], u), sc_mul(ui, a[nn + i]));
-        b[i] = sc_add(sc_mul(b[i], ui), sc_mul(u, b[nn + i]));
-        /* G'_i = u^-1 G_lo + u G_hi ; H'_i = u hf_lo H_lo + u^-1 hf_hi H_hi */
-        sc_t s2[2] = {ui, u};
-        ge_ext p2[2] = {Gv[i], Gv[nn + i]};
-        Gv[i] = msm(s2, p2, 2);
-        sc_t h2[2] = {first ? sc_mul(u, hf[i]) : u, first ? sc_mul(ui, hf[nn + i]) : ui};
-        ge_ext q2[2] = {Hv[i], Hv[nn + i]};
-        Hv[i] = msm(h2, q2, 2);
-      }
-      first = 0;
-    }
-    memcpy(lr, a[0].v, 32);
-    memcpy(lr + 32, b[0].v, 32);
-    free(Gv); free(Hv); free(sv); free(pv);
+    ipa_create(&tr, &Q, G->G, G->H, l, r, y_inv, n_p, out + 352);
   }
   free(pi); free(gamma); free(buf);
   return 0;
@@ -590,4 +598,63 @@ double cpu_perm_time(uint32_t k, uint64_t seed0, int count, const uint8_t* label
   free(proof);
   free(V);
   return (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+}
+
+/* Config 2: A = alpha B~ + <aL, G> + <aR, H> over GeneratorsChain(n),
+ * transcript `label` absorbs A ("A"), y = challenge "y", then the IPA on
+ * (aL, aR) with G_factors = 1, H_factors = y^-i and Q = from_uniform(q64)
+ * (tests/golden/make_golden.py config2_golden; bench.py bench_config2).
+ * sc: aL[n] || aR[n] || alpha, 32 B each.  out: A || L/R pairs || a || b. */
+static gens_t g_c2;
+static uint32_t g_c2_n = 0;
+int cpu_config2_setup(uint32_t n) {
+  if (n < 2 || (n & (n - 1))) return -1;
+  if (g_c2_n == n) return 0;
+  gens_make(&g_c2, n);
+  g_c2_n = n;
+  return 0;
+}
+int cpu_config2(uint32_t n, const uint8_t* sc, const uint8_t q64[64], const uint8_t* label, size_t llen,
+                uint8_t* out) {
+  if (g_c2_n != n) return -1;
+  const size_t T = 2 * (size_t)n + 1;
+  sc_t* s = malloc(sizeof(sc_t) * (T + 2 * (size_t)n));
+  ge_ext* P = malloc(sizeof(ge_ext) * T);
+  s[0] = *(const sc_t*)(sc + 64 * (size_t)n);  /* alpha */
+  P[0] = g_c2.Bb;
+  for (uint32_t i = 0; i < n; ++i) {
+    memcpy(&s[1 + i], sc + 32 * (size_t)i, 32);
+    memcpy(&s[1 + n + i], sc + 32 * ((size_t)n + i), 32);
+    P[1 + i] = g_c2.G[i];
+    P[1 + n + i] = g_c2.H[i];
+  }
+  ge_ext A = msm(s, P, T);
+  enc_pt(out, &A);
+  transcript_t tr;
+  tr_init(&tr, label, llen);
+  tr_append(&tr, "A", out, 32);
+  const sc_t y = tr_scalar(&tr, "y");
+  sc_t* a = s + T;
+  sc_t* b = a + n;
+  sc_t* hf = malloc(sizeof(sc_t) * n);
+  sc_powers(sc_inv(y), hf, n);
+  for (uint32_t i = 0; i < n; ++i) { a[i] = s[1 + i]; b[i] = s[1 + n + i]; }
+  const ge_ext Q = from_uniform(q64);
+  ipa_create(&tr, &Q, g_c2.G, g_c2.H, a, b, hf, n, out + 32);
+  free(s); free(P); free(hf);
+  return 0;
+}
+/* count config-2 runs on the same inputs; returns seconds */
+double cpu_config2_time(uint32_t n, const uint8_t* sc, const uint8_t q64[64], const uint8_t* label, size_t llen,
+                        int count) {
+  if (g_c2_n != n) return -1.0;
+  uint32_t lg = 0;
+  while ((1u << lg) < n) ++lg;
+  uint8_t* out = malloc(32 * (1 + 2 * (size_t)lg + 2));
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  for (int i = 0; i < count; ++i) cpu_config2(n, sc, q64, label, llen, out);
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  free(out);
+  return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }

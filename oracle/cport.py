@@ -205,3 +205,65 @@ def bench_msm_threads(log2n: int = 16, seconds: float = 10.0, threads: int = 1) 
     wall = max(secs)
     return {"value": threads * n * reps / wall, "unit": "pairs/s", "cores": threads, "kind": "port",
             "sample": f"{threads} threads x {reps} x 2^{log2n}-pair MSM, {wall:.1f} s"}
+
+
+# ------------------------------------------------------------ config 2 (commit + IPA)
+def config2_inputs(n: int = 1024, seed: int = 1):
+    """bench.py bench_config2's inputs (tests/golden/make_golden.py
+    config2_inputs): SHAKE256("config2" || le64 seed) read as 64-byte wide
+    scalars aL[n], aR[n], alpha, then 64 bytes for Q = from_uniform."""
+    xof = hashlib.shake_256(b"config2" + seed.to_bytes(8, "little")).digest((2 * n + 1) * 64 + 64)
+    sc = b"".join((int.from_bytes(xof[64 * i: 64 * i + 64], "little") % L).to_bytes(32, "little")
+                  for i in range(2 * n + 1))
+    return sc, xof[(2 * n + 1) * 64:]
+
+
+def _c2lib():
+    lib_ = perm_lib()
+    lib_.cpu_config2_setup.argtypes = [C.c_uint32]
+    lib_.cpu_config2.argtypes = [C.c_uint32, C.c_char_p, C.c_char_p, C.c_char_p, C.c_size_t, C.c_char_p]
+    lib_.cpu_config2_time.argtypes = [C.c_uint32, C.c_char_p, C.c_char_p, C.c_char_p, C.c_size_t, C.c_int]
+    lib_.cpu_config2_time.restype = C.c_double
+    return lib_
+
+
+def cpu_config2(n: int = 1024, seed: int = 1, label: bytes = b"config2") -> dict:
+    """Config 2 through the serial C port (dalek-style MSMs, bulletproofs'
+    folding IPA): A, L/R, a, b as hex (the fields of protocol.json config2)."""
+    lib_ = _c2lib()
+    assert lib_.cpu_config2_setup(n) == 0
+    sc, q = config2_inputs(n, seed)
+    lg = n.bit_length() - 1
+    out = C.create_string_buffer(32 * (1 + 2 * lg + 2))
+    assert lib_.cpu_config2(n, sc, q, label, len(label), out) == 0
+    raw = out.raw
+    return {"A": raw[:32].hex(), "L": [raw[32 + 64 * j: 64 + 64 * j].hex() for j in range(lg)],
+            "R": [raw[64 + 64 * j: 96 + 64 * j].hex() for j in range(lg)],
+            "a": raw[32 + 64 * lg: 64 + 64 * lg].hex(), "b": raw[64 + 64 * lg: 96 + 64 * lg].hex()}
+
+
+def bench_config2(n: int = 1024, seed: int = 1, seconds: float = 5.0, threads: int = 1,
+                  label: bytes = b"config2") -> dict:
+    """Config 2 runs/s of the serial C port on `threads` host cores (each
+    thread repeats the whole commit + IPA one at a time)."""
+    import threading
+    lib_ = _c2lib()
+    assert lib_.cpu_config2_setup(n) == 0
+    sc, q = config2_inputs(n, seed)
+    t1 = lib_.cpu_config2_time(n, sc, q, label, len(label), 1)
+    per = max(1, int(seconds / max(t1, 1e-6)))
+    secs = [0.0] * threads
+
+    def work(i):
+        secs[i] = lib_.cpu_config2_time(n, sc, q, label, len(label), per)
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    wall = max(secs)
+    return {"value": wall / per * 1e3, "unit": "ms", "runs_per_sec": threads * per / wall, "cores": threads,
+            "kind": "port",
+            "sample": f"{threads} x {per} runs of n = {n} vector commitment + IPA (dalek-ng Straus/Pippenger, "
+                      f"bulletproofs folding IPA, merlin, restated in C), {wall:.1f} s"}

@@ -283,6 +283,30 @@ def test_msm_2p21_both_partitions_exact(ctx):
     assert bpperm.partials_finish(parts).hex() == gold["result"]
 
 
+def test_msm_2p22_exact_vs_cport_golden_window_partition(ctx):
+    """Config 5 as BASELINE.json states it (one 2^22-term MSM, bucket windows
+    partitioned over 8 GPUs), exact: bench.py's msm_2e22 inputs (its four
+    2^20 slices) against the C port's result (tests/golden/bench_msm.json
+    world 4): the whole MSM one at a time and through the submit/collect
+    stream, and the 8 window-range partials (as bpperm.dist splits them for
+    8 ranks) added exactly (bpp_partials_finish)."""
+    import json
+    from pathlib import Path
+
+    import bpperm
+    from bpperm import dist as bdist
+    gold = json.loads((Path(__file__).parent / "golden" / "bench_msm.json").read_text())["world"]["4"]
+    tbl, d, n = _bench_inputs(ctx, 4)
+    assert n == 1 << 22
+    assert ctx.msm_table_dev(d, tbl, n).hex() == gold["result"]
+    assert ctx.msm_collect(ctx.msm_submit(d, tbl, n)).hex() == gold["result"]
+    c, W = bpperm.msm_windows(n)
+    parts = [ctx.msm_collect(ctx.msm_submit(d, tbl, n, a, b), partial=True) for a, b in bdist.window_ranges(W, 8)]
+    assert bpperm.partials_finish(parts).hex() == gold["result"]
+    ctx.dev_free(d)
+    tbl.close()
+
+
 def test_host_scalar_upload_pieces_and_bad_index(ctx, big_table):
     """Host scalars are staged, checked and copied in 4-MB pieces (131072
     scalars, msm.hip upload_scalars): a 2^18 + 5-term MSM crosses two piece

@@ -90,3 +90,13 @@ def test_bench_golden_is_prefix_consistent():
     pts = cport.from_uniform(bench.synth_point_bytes(n, 3))
     sc = bench.synth_scalars(n, 2)
     assert cport.msm_threads(sc, pts, threads=3) == cport.msm(sc, pts)
+
+
+def test_cpu_config2_matches_golden():
+    """The C port's config 2 (2049-term commitment + folding IPA at n = 1024,
+    bench.py's config2 cpu_baseline) reproduces tests/golden/protocol.json
+    config2, which the Python oracle generated: A, all 10 L/R pairs, a, b."""
+    gold = json.loads((Path(__file__).parent / "golden" / "protocol.json").read_text())["config2"]
+    got = cport.cpu_config2(gold["n"], gold["seed"])
+    for key in ("A", "L", "R", "a", "b"):
+        assert got[key] == gold[key], key

@@ -43,7 +43,7 @@ if os.environ.get("WITH_TORCH"):
     torch.cuda.synchronize()
 import resource  # noqa: E402
 PHASES = ["pb_rng", "pb_pedersen_V", "pb_pedersen_Vx_witness", "pb_msm_AI_AO_S", "pb_host_poly",
-          "pb_pedersen_T_lr", "pb_ipa", "ipa_host", "ipa_msm", "ped_d2h", "msm_direct", "double_encode"]
+          "pb_pedersen_T_lr", "pb_ipa", "ipa_host", "ipa_msm", "ped_d2h", "msm_direct", "ipa_round_dt", "double_encode"]
 if os.environ.get("PHASES"):  # per-phase wall time of a batch under the in-flight load
     for pr in provers:
         pr.ctx.profile(True)

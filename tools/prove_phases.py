@@ -13,7 +13,7 @@ import bpperm  # noqa: E402
 
 STAGES = ["pb_rng", "pb_pedersen_V", "pb_pedersen_Vx_witness", "pb_msm_AI_AO_S", "pb_host_poly",
           "pb_pedersen_T_lr", "pbT_pedersen", "pbT_host", "pb_ipa", "ipa_host", "ipa_msm", "ipa_terms",
-          "ipa_fold", "pedersen", "ped_upload", "ped_kernels", "ped_d2h", "msm_direct", "double_encode",
+          "ipa_fold", "pedersen", "ped_upload", "ped_kernels", "ped_d2h", "msm_direct", "ipa_round_dt", "double_encode",
           "compress", "poly_coef", "poly_x"]
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 128

@@ -175,40 +175,39 @@ def test_entropy_batch_leaves_no_secret_bytes(ctx, gens, monkeypatch, k, streams
             g.close()
 
 
-def test_entropy_wipe_after_staging_arena_growth(ctx, gens):
-    """VERDICT r4 item 5 (the round-4 segfault, fixed in ctx.hip stage_take):
-    a test-hook batch records secret spans in the pinned staging arena and
-    leaves them; one staging request larger than the arena (19.2 MB of host
-    scalars for bpp_msm_table, > the 16 MB first arena) frees and replaces
-    it; the next production batch's prove_wipe must not touch the freed
-    spans.  Then a second growth while the last wipe's spans are held for
-    bpp_debug_secret_residue.  No fault, nothing left unwiped, every proof
-    verifies."""
+def test_entropy_wipe_after_staging_arena_growth(gens):
+    """VERDICT r4 item 5 (the round-4 segfault, fixed in ctx.hip stage_take),
+    on a fresh context so that its pinned staging arena starts at 16 MB: a
+    test-hook batch records secret spans in the arena and leaves them; one
+    staging request larger than the arena (19.2 MB of host scalars for
+    bpp_msm_table) frees and replaces it; the next production batch's
+    prove_wipe must not touch the freed spans.  Then a second growth (25.6
+    MB) while the last wipe's spans are held for bpp_debug_secret_residue.
+    No fault, nothing left unwiped, every proof verifies."""
     import os
 
     import bpperm
-    pr = bpperm.PermProver(gens, 52)
-    proofs, Vs = pr.prove_batch([31, 32, 33])  # spans recorded, not wiped
-    n = 600_000
-    tbl = ctx.from_uniform(hashlib.shake_256(b"arena-growth").digest(64 * n))
+
+    def host_scalars(n):
+        sc = bytearray(os.urandom(32 * n))
+        sc[31::32] = bytes(n)  # < 2^248: canonical
+        return bytes(sc)
+
+    ctx2 = bpperm.Context(gens.ctx.device)
+    n, big = 600_000, 800_000
+    tbl = ctx2.from_uniform(hashlib.shake_256(b"arena-growth").digest(64 * big))  # (direct copy, no staging)
     try:
-        for it in range(2):  # the first request grows the arena (stale hook-batch spans live)
-            sc = bytearray(os.urandom(32 * n))
-            sc[31::32] = bytes(n)  # < 2^248: canonical
-            ctx.msm_table(bytes(sc), tbl, n)
-            e, ve = pr.prove_batch_entropy(5)
-            assert ctx.secret_residue() == 0
-            proofs += e
-            Vs += ve
-        big = (n * 4) // 3  # 25.6 MB: grows while the last wipe's spans are held
-        tbl2 = ctx.from_uniform(hashlib.shake_256(b"arena-growth-2").digest(64 * big))
-        sc = bytearray(os.urandom(32 * big))
-        sc[31::32] = bytes(big)
-        ctx.msm_table(bytes(sc), tbl2, big)
-        tbl2.close()
-        assert ctx.secret_residue() == 0
+        pr = bpperm.PermProver(gens, 52, ctx=ctx2)
+        proofs, Vs = pr.prove_batch([31, 32, 33])  # spans recorded in the 16 MB arena, not wiped
+        assert ctx2.secret_residue() > 0
+        ctx2.msm_table(host_scalars(n), tbl, n)  # 19.2 MB: the arena is replaced under the live spans
         e, ve = pr.prove_batch_entropy(5)
-        assert ctx.secret_residue() == 0
-        assert pr.verify_batch(proofs + e, Vs + ve)
+        assert ctx2.secret_residue() == 0
+        ctx2.msm_table(host_scalars(big), tbl, big)  # 25.6 MB: replaced under the last wipe's spans
+        assert ctx2.secret_residue() == 0
+        e2, ve2 = pr.prove_batch_entropy(5)
+        assert ctx2.secret_residue() == 0
+        assert pr.verify_batch(proofs + e + e2, Vs + ve + ve2)
     finally:
         tbl.close()
+        ctx2.close()

@@ -541,13 +541,15 @@ class PermProver:
         check(rc, "bpp_perm_verify_partial_gathered", self.ctx.h)
         return part.raw
 
-    def verify_partial(self, job: "VerifyJob", r_all: bytes, first: int, w_begin: int, w_end: int) -> bytes:
+    def verify_partial(self, job: "VerifyJob", seed: bytes, first: int, w_begin: int, w_end: int) -> bytes:
         """128-B raw partial of job's MSM over windows [w_begin, w_end) (see
-        bpp_perm_verify_partial); r_all = every rank's r challenges.  None
-        when a proof point does not decode (BPP_ERR_VERIFY)."""
+        bpp_perm_verify_partial); seed = the batch's 32 verifier-random bytes
+        (verify_seed(), the same on every rank), first = the batch index of
+        the job's first proof.  None when a proof point does not decode
+        (BPP_ERR_VERIFY)."""
         part = C.create_string_buffer(128)
-        rc = self.ctx.lib.bpp_perm_verify_partial(self.ctx.h, self.gens.h, job.h, _buf(r_all), len(r_all) // 32,
-                                                  first, w_begin, w_end, part)
+        rc = self.ctx.lib.bpp_perm_verify_partial(self.ctx.h, self.gens.h, job.h, _seed(seed), first, w_begin, w_end,
+                                                  part)
         if rc == 6:  # a proof point that does not decode: the batch cannot verify
             return None
         check(rc, "bpp_perm_verify_partial", self.ctx.h)
@@ -559,8 +561,8 @@ class VerifyJob:
     (bpp_perm_verify_begin, ctx=None; no GPU) or on the GPU of `ctx`
     (bpp_perm_verify_begin_dev: the job's records stay in that context's
     workspaces, valid until its next device job).  `r` holds each proof's
-    weight challenge; the batch weights are derived from every rank's r
-    (r_all)."""
+    weight challenge; proof p's batch weight mixes it with the batch's
+    verifier seed (bpp_perm_verify_scalars)."""
 
     def __init__(self, k: int, proofs: Sequence[bytes], Vs: Sequence[bytes], label: bytes = b"bp-perm",
                  ctx: "Context | None" = None, replay: "tuple[int, int] | None" = None):
@@ -599,10 +601,11 @@ class VerifyJob:
     def slice_bytes(self) -> int:
         return int(self.lib.bpp_perm_verify_slice_bytes(self.h))
 
-    def slice_scalars(self, r_all: bytes, d_out: int):
+    def slice_scalars(self, seed: bytes, d_out: int):
         """The replayed slice's MSM scalars into device memory d_out
-        (slice_bytes() bytes; bpp_perm_verify_slice_scalars)."""
-        check(self.lib.bpp_perm_verify_slice_scalars(self.ctx.h, self.h, _buf(r_all), len(r_all) // 32, d_out),
+        (slice_bytes() bytes; bpp_perm_verify_slice_scalars), weighted from
+        the batch's verifier seed."""
+        check(self.lib.bpp_perm_verify_slice_scalars(self.ctx.h, self.h, _seed(seed), d_out),
               "bpp_perm_verify_slice_scalars", self.ctx.h)
 
     @property
@@ -618,9 +621,11 @@ class VerifyJob:
     def windows(self) -> tuple[int, int]:
         return msm_windows(self.terms())
 
-    def scalars(self, r_all: bytes, first: int):
-        """(scalars, proof-point encodings) of the job's MSM (host): the
-        first 2 n_p + 2 scalars go to G[0..n_p), H[0..n_p), B, B_blinding."""
+    def scalars(self, seed: bytes, first: int):
+        """(scalars, proof-point encodings) of the job's MSM (host), its
+        proofs being batch proofs [first, first + count) weighted from the
+        batch's verifier seed: the first 2 n_p + 2 scalars go to G[0..n_p),
+        H[0..n_p), B, B_blinding."""
         T = self.terms()
         n_p = 1
         while n_p < 2 * self.k:
@@ -628,8 +633,7 @@ class VerifyJob:
         npts = T - (2 * n_p + 2)
         sc = C.create_string_buffer(32 * T)
         pts = C.create_string_buffer(32 * max(npts, 1))
-        check(self.lib.bpp_perm_verify_scalars(self.h, _buf(r_all), len(r_all) // 32, first, sc, pts),
-              "bpp_perm_verify_scalars")
+        check(self.lib.bpp_perm_verify_scalars(self.h, _seed(seed), first, sc, pts), "bpp_perm_verify_scalars")
         sraw, praw = sc.raw, pts.raw
         return ([sraw[32 * i: 32 * i + 32] for i in range(T)], [praw[32 * i: 32 * i + 32] for i in range(npts)])
 
@@ -643,6 +647,20 @@ class VerifyJob:
             self.close()
         except Exception:
             pass
+
+
+def verify_seed() -> bytes:
+    """32 bytes of verifier randomness for one batch (bpp_verify_seed: the OS
+    CSPRNG).  Every job / rank of the batch must use the same bytes."""
+    out = C.create_string_buffer(32)
+    check(_lib.load().bpp_verify_seed(out), "bpp_verify_seed")
+    return out.raw
+
+
+def _seed(seed: bytes):
+    if not isinstance(seed, (bytes, bytearray)) or len(seed) != 32:
+        raise ValueError("a batch-verification seed is 32 bytes")
+    return _buf(bytes(seed))
 
 
 def partials_is_identity(partials: Sequence[bytes]) -> bool:

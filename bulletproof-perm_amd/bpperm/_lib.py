@@ -93,11 +93,12 @@ SIGNATURES = {
     "bpp_perm_verify_begin": (i32, [u32, sz, vp, sz, vp, vp, vp, C.POINTER(vp)]),
     "bpp_perm_verify_begin_dev": (i32, [vp, u32, sz, vp, sz, vp, vp, vp, C.POINTER(vp)]),
     "bpp_perm_verify_terms": (i32, [vp, C.POINTER(sz)]),
-    "bpp_perm_verify_scalars": (i32, [vp, vp, sz, sz, vp, vp]),
-    "bpp_perm_verify_partial": (i32, [vp, vp, vp, vp, sz, sz, u32, u32, vp]),
+    "bpp_verify_seed": (i32, [vp]),
+    "bpp_perm_verify_scalars": (i32, [vp, vp, sz, vp, vp]),
+    "bpp_perm_verify_partial": (i32, [vp, vp, vp, vp, sz, u32, u32, vp]),
     "bpp_perm_verify_begin_dev_slice": (i32, [vp, u32, sz, vp, sz, vp, vp, sz, sz, vp, C.POINTER(vp)]),
     "bpp_perm_verify_slice_bytes": (sz, [vp]),
-    "bpp_perm_verify_slice_scalars": (i32, [vp, vp, vp, sz, vp]),
+    "bpp_perm_verify_slice_scalars": (i32, [vp, vp, vp, vp]),
     "bpp_perm_verify_partial_gathered": (i32, [vp, vp, vp, vp, sz, vp, sz, u32, u32, vp]),
     "bpp_perm_verify_end": (None, [vp]),
     "bpp_partials_is_identity": (i32, [vp, sz]),

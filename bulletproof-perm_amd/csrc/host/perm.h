@@ -118,15 +118,19 @@ void draw_prover_host_x8(const Circuit& C, const Seed seeds[8], RandomDraws* con
 
 size_t proof_len(uint32_t k);
 
-// Batch-verification weights over `total` proofs with weight challenges r
-// (each proof's transcript's "t-check-weight"):
-//   d_j  = SHAKE256("bp-perm-batch-r" || le64 total || le64 j || r[j total/8 ..
-//          (j+1) total/8))[0..32], j < 8
-//   seed = SHAKE256("bp-perm-batch-seed" || d_0 .. d_7)[0..32]
-//   w_p  = from_bytes_mod_order_wide(SHAKE256("bp-perm-batch-wt" || seed ||
-//          le64 p)[0..64])
-// (a single proof keeps weight one; callers special-case total <= 1).
-void batch_seed(const hsc::Sc* r, size_t total, uint8_t seed[32]);
-hsc::Sc batch_weight(const uint8_t seed[32], uint64_t p);
+// Batch-verification weight of proof p (its index in the batch) with weight
+// challenge r_p (its own transcript's "t-check-weight"):
+//   w_p = from_bytes_mod_order_wide(SHAKE256("bp-perm-batch-wt" || seed ||
+//         le64 p || r_p)[0..64])
+// seed = 32 bytes of the VERIFIER's randomness (getrandom; every rank of a
+// split batch uses the same seed), mixed with the proof's own transcript
+// challenge as bulletproofs' r1cs batch verifier mixes its external rng into
+// each proof's TranscriptRng.  The weights need nothing from the other
+// proofs, so they are made in each proof's own GPU lane right after its
+// replay (DESIGN.md §5 "Batch weights").  A seed the provers can predict
+// voids the batch's soundness.
+hsc::Sc batch_weight(const uint8_t seed[32], uint64_t p, const hsc::Sc& r);
+// 32 bytes from the OS CSPRNG (getrandom); false if it fails
+bool verify_seed(uint8_t seed[32]);
 
 }  // namespace perm

@@ -9,6 +9,8 @@
 // a_O[n-1] = a_L * a_R (weights.rs:108 squared a_L), and x is a transcript
 // challenge bound to the committed v_2k by the last row (weights.rs:50 fixed
 // x = 1).  Rows: a_L (2k), a_R (2k), a_O[n-1] = 0, v_2k = x  => Q = 4k + 2.
+#include <errno.h>
+#include <sys/random.h>
 #include "par.h"
 #include "perm.h"
 
@@ -153,35 +155,27 @@ size_t proof_len(uint32_t k) {
   return 32 * (8 + 3 + 2 * lg + 2);
 }
 
-// Batch-verification weights (DESIGN.md §5 "Batch weights"): a tree hash of
-// every proof's r challenge, so that the seed is cheap to compute and the
-// per-proof weights are independent one-block sponges (the device makes
-// them in its own thread each, verify_dev.hip k_verify_weights).
-void batch_seed(const hsc::Sc* r, size_t total, uint8_t seed[32]) {
-  uint8_t d[8][32];
-  par::for_each(8, [&](size_t j) {
-    merlin::Shake256 sh;
-    sh.update((const uint8_t*)"bp-perm-batch-r", 15);
-    const uint64_t hdr[2] = {(uint64_t)total, (uint64_t)j};
-    sh.update((const uint8_t*)hdr, 16);
-    const size_t b = j * total / 8, e = (j + 1) * total / 8;
-    if (e > b) sh.update((const uint8_t*)(r + b), 32 * (e - b));  // (canonical Sc == its 32 bytes)
-    sh.read(d[j], 32);
-  });
-  merlin::Shake256 sh;
-  sh.update((const uint8_t*)"bp-perm-batch-seed", 18);
-  sh.update(&d[0][0], sizeof d);
-  sh.read(seed, 32);
-}
-
-hsc::Sc batch_weight(const uint8_t seed[32], uint64_t p) {
+hsc::Sc batch_weight(const uint8_t seed[32], uint64_t p, const hsc::Sc& r) {
   merlin::Shake256 sh;
   sh.update((const uint8_t*)"bp-perm-batch-wt", 16);
   sh.update(seed, 32);
   sh.update((const uint8_t*)&p, 8);
+  sh.update((const uint8_t*)&r, 32);  // (canonical Sc == its 32 bytes)
   uint8_t o[64];
   sh.read(o, 64);
   return hsc::from_wide(o);
+}
+
+bool verify_seed(uint8_t seed[32]) {
+  size_t got = 0;
+  while (got < 32) {
+    const ssize_t n = getrandom(seed + got, 32 - got, 0);
+    if (n > 0)
+      got += (size_t)n;
+    else if (n < 0 && errno != EINTR)
+      return false;
+  }
+  return true;
 }
 
 }  // namespace perm

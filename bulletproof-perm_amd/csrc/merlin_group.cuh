@@ -65,7 +65,10 @@
 #define GRP_SCR_OFF 200
 #define GRP_BLOCK 576
 #endif
-#define GRP_SCR_BYTES 280  // the pi scratch: 200 bytes of state + the copies' trash words (16-lane: dwords 60..69)
+// the pi scratch: GRP_BLOCK - GRP_SCR_OFF bytes (CHI128: 528 = 130
+// half-column dwords (12 (2X + h) + row, X < 5, h < 2) + pad; the former
+// dword layout: 200 bytes of state + the copies' trash words, dwords 60..69)
+#define GRP_SCR_BYTES (GRP_BLOCK - GRP_SCR_OFF)
 
 // rho offsets r[x][y] packed per y (6 bits per x) and the pi destination row
 // (2x + 3y) mod 5 packed per y (3 bits per x); pi's destination column is y

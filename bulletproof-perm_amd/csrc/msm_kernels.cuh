@@ -155,6 +155,68 @@ FE_INLINE uint32_t bucket_of(const uint32_t* __restrict__ boff, uint32_t nb, uin
   return lo;
 }
 
+#ifndef ACC_ADDR_SWAP
+#define ACC_ADDR_SWAP 1
+#endif
+#ifndef ACC_RESET_Z
+#define ACC_RESET_Z 1
+#endif
+// Table row of entry e for ge_madd_fg: for a negative digit (-Q = (y-x,
+// y+x, -2dxy)) the (y+x, y-x) fields are read swapped -- the swap is in the
+// per-lane load addresses, so it costs no instruction -- and the sign of
+// 2dxy is left to ge_madd_fg (F and G exchanged).  The two swapped fields sit
+// at 40-byte offsets, so they are read as 8-byte loads.  This replaces the
+// divergent negation branch below (a register swap and a carried fe_neg that
+// the wave ran in almost every iteration).
+FE_INLINE ge_niels fetch_entry_sw(const uint32_t* __restrict__ tbl, const uint32_t* __restrict__ tbl1, uint32_t n0,
+                                  uint32_t e) {
+  const uint32_t pi = e & 0x7fffffffu;
+  const uint32_t neg = e >> 31;
+  const uint32_t* row = pi < n0 ? tbl + (size_t)pi * MSM_NIELS_WORDS : tbl1 + (size_t)(pi - n0) * MSM_NIELS_WORDS;
+  const uint2* pa = reinterpret_cast<const uint2*>(row + (neg ? 10u : 0u));  // -> ypx
+  const uint2* pb = reinterpret_cast<const uint2*>(row + (neg ? 0u : 10u));  // -> ymx
+  const uint4* pc = reinterpret_cast<const uint4*>(row + 20);
+  uint2 a[5], b[5];
+  _Pragma("unroll") for (int i = 0; i < 5; ++i) a[i] = pa[i];
+  _Pragma("unroll") for (int i = 0; i < 5; ++i) b[i] = pb[i];
+  const uint4 c0 = pc[0], c1 = pc[1];
+  const uint2 c2 = *reinterpret_cast<const uint2*>(row + 28);
+  ge_niels q;
+  _Pragma("unroll") for (int i = 0; i < 5; ++i) {
+    q.ypx.v[2 * i] = a[i].x;
+    q.ypx.v[2 * i + 1] = a[i].y;
+    q.ymx.v[2 * i] = b[i].x;
+    q.ymx.v[2 * i + 1] = b[i].y;
+  }
+  q.xy2d.v[0] = c0.x; q.xy2d.v[1] = c0.y; q.xy2d.v[2] = c0.z; q.xy2d.v[3] = c0.w;
+  q.xy2d.v[4] = c1.x; q.xy2d.v[5] = c1.y; q.xy2d.v[6] = c1.z; q.xy2d.v[7] = c1.w;
+  q.xy2d.v[8] = c2.x; q.xy2d.v[9] = c2.y;
+  return q;
+}
+// p + q (neg = false) or p - q (neg = true) for q from fetch_entry_sw (its
+// (y+x, y-x) already swapped for a negative digit): the sign of 2dxy only
+// exchanges F = D - C and G = D + C.
+FE_INLINE ge_p3 ge_madd_fg(const ge_p3& p, const ge_niels& q, bool neg) {
+  fe A = fe_mul(fe_sub_nc(p.Y, p.X), q.ymx);
+  fe B = fe_mul(fe_add_nc(p.Y, p.X), q.ypx);
+  fe C = fe_mul(p.T, q.xy2d);
+  fe D = fe_add_nc(p.Z, p.Z);
+  fe E = fe_sub_nc(B, A);
+  fe H = fe_add_nc(B, A);
+  const fe Dm = fe_sub(D, C), Dp = fe_add_nc(D, C);
+  fe F, G;
+  _Pragma("unroll") for (int i = 0; i < FE_LIMBS; ++i) {
+    F.v[i] = neg ? Dp.v[i] : Dm.v[i];
+    G.v[i] = neg ? Dm.v[i] : Dp.v[i];
+  }
+  ge_p3 r;
+  r.X = fe_mul(E, F);
+  r.Y = fe_mul(G, H);
+  r.Z = fe_mul(G, F);  // F as the second operand in X and Z: its 19x limbs are shared
+  r.T = fe_mul(E, H);
+  return r;
+}
+
 // Table point of entry e, negated for a negative digit (in this kernel the
 // branch measured 1.5 % faster than ge_madd_signed's operand selects).
 FE_INLINE ge_niels fetch_entry(const uint32_t* __restrict__ tbl, const uint32_t* __restrict__ tbl1, uint32_t n0,
@@ -286,9 +348,21 @@ __global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_
 #else
         if (((bend - 1) / K) - l >= FIX_MAX) heavy[1 + atomicAdd(&heavy[0], 1u)] = b;
 #endif
+#if ACC_RESET_Z
+        // the identity as (0 : Z : Z : 0) with the accumulator's own Z (never
+        // zero): 30 moves instead of materialising (0 : 1 : 1 : 0)'s 40 words
+        acc.Y = acc.Z;
+        acc.X = fe_zero();
+        acc.T = fe_zero();
+#else
         acc = ge_identity();
+#endif
       }
+#if ACC_ADDR_SWAP
+      acc = ge_madd_fg(acc, fetch_entry_sw(tbl, tbl1, n0, e), (e >> 31) != 0);
+#else
       acc = ge_madd(acc, fetch_entry(tbl, tbl1, n0, e));
+#endif
     }
     // last run [max(bstart, i0), i1)
     if (bstart >= i0 && bend <= i1) {

@@ -769,68 +769,75 @@ bool verify_replay(const perm::Circuit& C, const Proof& P, merlin::Transcript& t
   return true;
 }
 
-// Verifier, phase 2: the proof's unweighted MSM scalars from its challenges
-// and the inverses y^-1, u_j^-1 (batch-inverted across proofs by the
-// caller).  gen_sc (2n_p + 2: G, H, B, Bb) is set; proof-point scalars
-// (m + 8 + 2lg, order V, A_I, A_O, S, T1..T6, L.., R..) are appended.
-void verify_expand(const perm::Circuit& C, const Proof& P, const VerifyChallenges& ch, const Sc& y_inv,
-                   const Sc* u_inv, std::vector<Sc>& gen_sc, std::vector<Sc>& pt_sc) {
+// Verifier, phase 2: the proof's unweighted MSM scalars from its
+// challenges, scaled by F = U^2 Y (U = prod u_j, Y = y^(n_p - 1)) so that no
+// inverse is needed -- the same scalars as k_verify_consts / k_verify_scalars
+// (formulas there).  gen_sc (2n_p + 2: G, H, B, Bb) is set; proof-point
+// scalars (m + 8 + 2lg, order V, A_I, A_O, S, T1..T6, L.., R..) are appended.
+void verify_expand(const perm::Circuit& C, const Proof& P, const VerifyChallenges& ch, std::vector<Sc>& gen_sc,
+                   std::vector<Sc>& pt_sc) {
   const uint32_t n_p = C.n_p, m = C.m, lg = C.lg;
   using hsc::add;
   using hsc::mul;
   using hsc::neg;
   using hsc::sub;
-  // s_i = prod_j u_j^(+-1) (bulletproofs verification_scalars)
-  std::vector<Sc> u_sq(lg), uinv_sq(lg), s(n_p);
-  Sc allinv = hsc::one();
+  // st[i] = s_i / s_0 = prod over the bits of i of u^2 (bulletproofs
+  // verification_scalars' s_i with s_0 = prod u_j^-1 factored out)
+  std::vector<Sc> u_sq(lg), st(n_p);
+  Sc U = hsc::one();
   for (uint32_t j = 0; j < lg; ++j) {
     u_sq[j] = hsc::sq(ch.u[j]);
-    uinv_sq[j] = hsc::sq(u_inv[j]);
-    allinv = mul(allinv, u_inv[j]);
+    U = mul(U, ch.u[j]);
   }
-  s[0] = allinv;
+  st[0] = hsc::one();
   for (uint32_t i = 1; i < n_p; ++i) {
     const uint32_t lg_i = 31 - __builtin_clz(i), kk = 1u << lg_i;
-    s[i] = mul(s[i - kk], u_sq[lg - 1 - lg_i]);
+    st[i] = mul(st[i - kk], u_sq[lg - 1 - lg_i]);
   }
   const Sc x = ch.x, r = ch.r, w = ch.w;
   std::vector<Sc> xp = hsc::powers(x, 7);
-  std::vector<Sc> y_inv_n = hsc::powers(y_inv, n_p);
+  std::vector<Sc> y_n = hsc::powers(ch.y, n_p);  // y^e, e < n_p
+  const Sc Y = y_n[n_p - 1], U2 = hsc::sq(U), F = mul(U2, Y);
   std::vector<Sc> zq = hsc::powers(ch.z, C.Q + 1);
   zq.erase(zq.begin());
   const std::vector<Sc> zWL = perm::zW(C.WL, zq, n_p), zWR = perm::zW(C.WR, zq, n_p), zWO = perm::zW(C.WO, zq, n_p),
                         zWV = perm::zW(C.WV, zq, m);
   std::vector<Sc> c = C.c;
   c[C.Q - 1] = hsc::neg(ch.x_perm);
-  Sc delta = hsc::zero();
-  for (uint32_t i = 0; i < n_p; ++i) delta = add(delta, mul(mul(y_inv_n[i], zWR[i]), zWL[i]));
-  const Sc aR_ = hsc::to_mont(P.ipa.a), bR_ = hsc::to_mont(P.ipa.b), xR_ = hsc::to_mont(x);
-  const Sc zc = hsc::inner_product(zq, c);
   const Sc a = P.ipa.a, b = P.ipa.b;
-  // generators (merged t-check and IPA-check scalars)
+  const Sc uyaR = hsc::to_mont(mul(mul(U, Y), a)), ubR = hsc::to_mont(mul(U, b)), xR_ = hsc::to_mont(x),
+           u2R = hsc::to_mont(U2);
+  Sc delta = hsc::zero();  // sum_i U^2 yr_i zWR_i zWL_i (= F delta)
   for (uint32_t i = 0; i < n_p; ++i) {
-    const Sc yiR = hsc::to_mont(y_inv_n[i]);
-    const Sc gi = sub(hsc::mulm(s[i], aR_), hsc::mulm(hsc::mulm(zWR[i], xR_), yiR));
-    const Sc hi = add(sub(hsc::mulm(hsc::mulm(s[n_p - 1 - i], bR_), yiR),
-                          hsc::mulm(add(hsc::mulm(zWL[i], xR_), zWO[i]), yiR)),
-                      hsc::one());
-    gen_sc[i] = gi;
-    gen_sc[n_p + i] = hi;
+    const Sc yr = y_n[n_p - 1 - i];  // y^(n_p - 1 - i) = Y y^-i
+    const Sc yu = hsc::mulm(yr, u2R);
+    const Sc yuR = hsc::to_mont(yu), yrR = hsc::to_mont(yr);
+    delta = add(delta, mul(mul(yu, zWR[i]), zWL[i]));
+    gen_sc[i] = sub(hsc::mulm(st[i], uyaR), hsc::mulm(hsc::mulm(zWR[i], xR_), yuR));
+    gen_sc[n_p + i] = add(sub(hsc::mulm(hsc::mulm(st[n_p - 1 - i], ubR), yrR),
+                              hsc::mulm(add(hsc::mulm(zWL[i], xR_), zWO[i]), yuR)),
+                          F);
   }
-  const Sc tcheck_B = mul(r, sub(P.t_hat, mul(xp[2], add(delta, zc))));
-  const Sc ipa_B = mul(w, sub(mul(a, b), P.t_hat));
+  const Sc zc = hsc::inner_product(zq, c);
+  const Sc tcheck_B = mul(r, sub(mul(F, P.t_hat), mul(xp[2], add(delta, mul(F, zc)))));
+  const Sc ipa_B = mul(mul(w, F), sub(mul(a, b), P.t_hat));
   gen_sc[2 * n_p] = add(tcheck_B, ipa_B);
-  gen_sc[2 * n_p + 1] = add(mul(r, P.tau_x), P.mu);
+  gen_sc[2 * n_p + 1] = mul(F, add(mul(r, P.tau_x), P.mu));
   // proof points
-  const Sc rx2R = hsc::to_mont(mul(r, xp[2]));
-  for (uint32_t j = 0; j < m; ++j) pt_sc.push_back(neg(hsc::mulm(zWV[j], rx2R)));
-  pt_sc.push_back(neg(x));
-  pt_sc.push_back(neg(xp[2]));
-  pt_sc.push_back(neg(xp[3]));
+  const Sc rx2FR = hsc::to_mont(mul(mul(r, xp[2]), F));
+  for (uint32_t j = 0; j < m; ++j) pt_sc.push_back(neg(hsc::mulm(zWV[j], rx2FR)));
+  pt_sc.push_back(neg(mul(F, x)));
+  pt_sc.push_back(neg(mul(F, xp[2])));
+  pt_sc.push_back(neg(mul(F, xp[3])));
   const int tidx[5] = {1, 3, 4, 5, 6};
-  for (int i = 0; i < 5; ++i) pt_sc.push_back(neg(mul(r, xp[tidx[i]])));
-  for (uint32_t j = 0; j < lg; ++j) pt_sc.push_back(neg(u_sq[j]));
-  for (uint32_t j = 0; j < lg; ++j) pt_sc.push_back(neg(uinv_sq[j]));
+  for (int i = 0; i < 5; ++i) pt_sc.push_back(neg(mul(F, mul(r, xp[tidx[i]]))));
+  for (uint32_t j = 0; j < lg; ++j) pt_sc.push_back(neg(mul(F, u_sq[j])));
+  for (uint32_t j = 0; j < lg; ++j) {  // -Y prod_{k != j} u_k^2 (= -F u_j^-2)
+    Sc v = Y;
+    for (uint32_t k = 0; k < lg; ++k)
+      if (k != j) v = mul(v, u_sq[k]);
+    pt_sc.push_back(neg(v));
+  }
 }
 
 void proof_points(const Proof& P, std::vector<uint8_t>& enc) {
@@ -856,7 +863,6 @@ struct bpp_verify_job {
   std::vector<Proof> Ps;
   std::vector<Sc> rs;                 // per-proof weight challenges
   std::vector<VerifyChallenges> ch;   // every proof's transcript challenges
-  std::vector<Sc> inv;                // per proof: y^-1, u_0^-1 .. u_{lg-1}^-1
   // unweighted generator / proof-point scalars, expanded on the host only
   // when asked for (bpp_perm_verify_scalars); the GPU path expands them on
   // the device (k_verify_scalars)
@@ -865,7 +871,10 @@ struct bpp_verify_job {
   mutable std::vector<std::vector<Sc>> gen_p, pt_p;
   // device job (bpp_perm_verify_begin_dev): the replay ran on the GPU and the
   // records / decompressed proof points sit in dctx's "vj_*" workspaces
-  // (generation dgen); Ps, ch and inv stay empty
+  // (generation dgen); Ps and ch stay empty.  An asynchronous begin
+  // (verify_batch) leaves the replay's verdicts in bad_h (pinned, rcount
+  // words) for the partial to check after its own synchronisation.
+  const uint32_t* bad_h = nullptr;
   bool dev = false;
   bpp_ctx* dctx = nullptr;
   uint64_t dgen = 0;
@@ -873,16 +882,13 @@ struct bpp_verify_job {
   // uploaded and their points decompressed, only [rfirst, rfirst + rcount)
   // replayed (records and rs of that slice); a whole job has rcount = count
   size_t rfirst = 0, rcount = 0;
-  // the inverses of the replay's wave products (one per 64 proofs of the
-  // replayed slice, canonical; verify_replay_dev's wtot, inverted on the host)
-  std::vector<Sc> winv;
 };
 
 namespace {
 
-// pass 1 (parallel over chunks of proofs): parse, replay each transcript
-// (all challenges and the proof's weight challenge r), and invert every y
-// and u of a chunk with ONE inversion (Montgomery's trick)
+// pass 1 (parallel over chunks of proofs): parse and replay each transcript
+// (all challenges and the proof's weight challenge r); a zero y or u_j
+// rejects the proof (the checks are scaled by a product of them)
 // (circuit_lib.rs:478-585 restated in sound mode)
 int verify_begin(const perm::Circuit& C, const uint8_t* label, size_t llen, size_t count, const uint8_t* proofs,
                  size_t proof_stride, const uint8_t* V, std::unique_ptr<bpp_verify_job>& job) {
@@ -894,33 +900,17 @@ int verify_begin(const perm::Circuit& C, const uint8_t* label, size_t llen, size
   J.Ps.resize(count);
   J.rs.resize(count);
   J.ch.resize(count);
-  J.inv.resize(count * (1 + C.lg));
   std::vector<uint8_t> ok(count, 0);
-  const size_t chunks = std::max<size_t>(1, std::min<size_t>(count, 64));
-  par::for_each(chunks, [&](size_t chk) {
-    const size_t p0 = chk * count / chunks, p1 = (chk + 1) * count / chunks;
-    std::vector<Sc> inv;
-    inv.reserve((p1 - p0) * (1 + C.lg));
-    for (size_t p = p0; p < p1; ++p) {
-      if (!deserialize(C, proofs + p * proof_stride, perm::proof_len(C.k), V + p * 32 * C.m, J.Ps[p])) return;
-      merlin::Transcript tr(label, llen);
-      VerifyChallenges& ch = J.ch[p];
-      if (!verify_replay(C, J.Ps[p], tr, ch)) return;
-      // a zero challenge has negligible probability; it would make the
-      // batch inversion fail, so such a proof is rejected
-      if (hsc::is_zero(ch.y)) return;
-      inv.push_back(ch.y);
-      for (const Sc& u : ch.u) {
-        if (hsc::is_zero(u)) return;
-        inv.push_back(u);
-      }
-    }
-    hsc::batch_invert(inv, false);
-    std::copy(inv.begin(), inv.end(), J.inv.begin() + p0 * (1 + C.lg));
-    for (size_t p = p0; p < p1; ++p) {
-      J.rs[p] = J.ch[p].r;
-      ok[p] = 1;
-    }
+  par::for_each(count, [&](size_t p) {
+    if (!deserialize(C, proofs + p * proof_stride, perm::proof_len(C.k), V + p * 32 * C.m, J.Ps[p])) return;
+    merlin::Transcript tr(label, llen);
+    VerifyChallenges& ch = J.ch[p];
+    if (!verify_replay(C, J.Ps[p], tr, ch)) return;
+    if (hsc::is_zero(ch.y)) return;
+    for (const Sc& u : ch.u)
+      if (hsc::is_zero(u)) return;
+    J.rs[p] = ch.r;
+    ok[p] = 1;
   });
   for (size_t p = 0; p < count; ++p)
     if (!ok[p]) return BPP_ERR_VERIFY;
@@ -936,8 +926,7 @@ void job_expand_host(const bpp_verify_job& J) {
   J.pt_p.assign(J.count, std::vector<Sc>());
   par::for_each(J.count, [&](size_t p) {
     J.gen_p[p].assign(2 * C.n_p + 2, hsc::zero());
-    const Sc* iv = &J.inv[p * (1 + C.lg)];
-    verify_expand(C, J.Ps[p], J.ch[p], iv[0], iv + 1, J.gen_p[p], J.pt_p[p]);
+    verify_expand(C, J.Ps[p], J.ch[p], J.gen_p[p], J.pt_p[p]);
   });
   J.expanded = true;
 }
@@ -945,33 +934,19 @@ void job_expand_host(const bpp_verify_job& J) {
 // Terms of the job's MSM: merged generators (G, H, B, Bb) + every proof point.
 size_t verify_terms(const bpp_verify_job& J) { return 2 * (size_t)J.C.n_p + 2 + J.count * J.npt; }
 
-// Per-proof weights from all `total` r challenges (perm::batch_seed /
-// batch_weight; a single proof keeps weight one).
-std::vector<Sc> batch_weights(const Sc* r_all, size_t total) {
-  std::vector<Sc> wts(total, hsc::one());
-  if (total > 1) {
-    uint8_t seed[32];
-    perm::batch_seed(r_all, total, seed);
-    par::for_each((total + 63) / 64, [&](size_t b) {
-      for (size_t p = 64 * b; p < std::min(total, 64 * b + 64); ++p) wts[p] = perm::batch_weight(seed, p);
-    });
-  }
-  return wts;
-}
-
-// pass 2 (host): the job's MSM terms with its proofs weighted by
-// wts[first + p] -- generator scalars merged across its proofs (G[0..n_p),
-// H[0..n_p), B, Bb), then each proof's points (V, A_I, A_O, S, T1..T6, L..,
-// R..) weighted by their proof's weight; enc = those points' encodings.
-int verify_terms_weighted(const bpp_verify_job& J, const Sc* r_all, size_t total, size_t first, std::vector<Sc>& sc,
+// pass 2 (host): the job's MSM terms with proof p weighted by
+// perm::batch_weight(seed, first + p, r_p) -- generator scalars merged across
+// its proofs (G[0..n_p), H[0..n_p), B, Bb), then each proof's points (V,
+// A_I, A_O, S, T1..T6, L.., R..) weighted by their proof's weight; enc =
+// those points' encodings.
+int verify_terms_weighted(const bpp_verify_job& J, const uint8_t seed[32], size_t first, std::vector<Sc>& sc,
                           std::vector<uint8_t>& enc) {
   const uint32_t n_p = J.C.n_p;
   const size_t count = J.count, npt = J.npt;
-  if (first > total || count > total - first) return BPP_ERR_ARG;
   job_expand_host(J);
-  std::vector<Sc> wR = batch_weights(r_all, total);  // -> Montgomery form (one step per product)
-  for (auto& w : wR) w = hsc::to_mont(w);
-  const Sc* wts = wR.data() + first;
+  std::vector<Sc> wR(count);  // Montgomery form (one step per product)
+  par::for_each(count, [&](size_t p) { wR[p] = hsc::to_mont(perm::batch_weight(seed, first + p, J.rs[p])); });
+  const Sc* wts = wR.data();
   const size_t NG = 2 * (size_t)n_p + 2;
   sc.assign(NG + count * npt, hsc::zero());
   enc.assign(count * npt * 32, 0);
@@ -1028,44 +1003,39 @@ int verify_msm(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, size_t c
 
 // pass 2 of a host job: per-proof records built on the host from the host
 // replay, then the same device scalars and MSM as a device job.
-int verify_partial(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J, const Sc* r_all, size_t total,
-                   size_t first, uint32_t wb, uint32_t we, h25519::ge* out) {
+int verify_partial(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J, const uint8_t seed[32], size_t first,
+                   uint32_t wb, uint32_t we, h25519::ge* out) {
   const uint32_t n_p = J.C.n_p;
   if (G->n < n_p) {
     ctx->err = "generators shorter than the padded circuit";
     return BPP_ERR_LEN;
   }
   const size_t NG = 2 * (size_t)n_p + 2, count = J.count, npt = J.npt, T = NG + count * npt;
-  if (first > total || count > total - first) return BPP_ERR_ARG;
-  const uint32_t lg = J.C.lg, nrec = 12 + 2 * lg;
-  // per-proof records for k_verify_scalars and the proof points' encodings
+  const uint32_t lg = J.C.lg, nrec = vrec_n(J.C);
+  // per-proof records for k_verify_consts / k_verify_scalars and the proof
+  // points' encodings
   std::vector<uint32_t> rec(count * nrec * 8);
   std::vector<uint8_t> enc(count * npt * 32);
   {
     HostScope hs(ctx, "verify_terms");
-    const std::vector<Sc> wts = batch_weights(r_all, total);
     par::for_each(count, [&](size_t p) {
       const VerifyChallenges& ch = J.ch[p];
       const Proof& P = J.Ps[p];
-      const Sc* iv = &J.inv[p * (1 + lg)];
       uint32_t* r = &rec[p * nrec * 8];
       auto put = [&](uint32_t k, const Sc& v) { hsc::to_bytes((uint8_t*)(r + 8 * k), v); };
-      put(0, ch.x_perm);
-      put(1, iv[0]);
-      put(2, ch.z);
-      put(3, ch.x);
-      put(4, ch.w);
-      put(5, ch.r);
-      put(6, P.ipa.a);
-      put(7, P.ipa.b);
-      put(8, P.t_hat);
-      put(9, P.tau_x);
-      put(10, P.mu);
-      put(11, wts[first + p]);
-      for (uint32_t j = 0; j < lg; ++j) {
-        put(12 + j, ch.u[j]);
-        put(12 + lg + j, iv[1 + j]);
-      }
+      put(VREC_XPERM, ch.x_perm);
+      put(VREC_Y, ch.y);
+      put(VREC_Z, ch.z);
+      put(VREC_X, ch.x);
+      put(VREC_W, ch.w);
+      put(VREC_R, ch.r);
+      put(VREC_A, P.ipa.a);
+      put(VREC_B, P.ipa.b);
+      put(VREC_THAT, P.t_hat);
+      put(VREC_TAUX, P.tau_x);
+      put(VREC_MU, P.mu);
+      put(VREC_WT, hsc::zero());
+      for (uint32_t j = 0; j < lg; ++j) put(VREC_U + j, ch.u[j]);
       std::vector<uint8_t> e;
       e.reserve(npt * 32);
       proof_points(P, e);
@@ -1074,7 +1044,7 @@ int verify_partial(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J, con
   }
   void* d_sv = nullptr;
   BPP_TRY(ctx_ws(ctx, "pv_s", T * 32 + 32, &d_sv));
-  BPP_TRY(verify_scalars_dev(ctx, J.C, (uint32_t)count, rec, (uint32_t*)d_sv));
+  BPP_TRY(verify_scalars_dev(ctx, J.C, (uint32_t)count, rec, seed, first, (uint32_t*)d_sv));
   uint32_t* d_x = nullptr;
   int rc = decompress_ws(ctx, enc.data(), enc.size() / 32, "pv_x", &d_x);
   if (rc == BPP_ERR_DECOMPRESS) return BPP_ERR_VERIFY;
@@ -1094,9 +1064,13 @@ int verify_partial(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J, con
 // proof; an undecodable point is reported by verify_partial_dev.
 // rfirst / rcount: replay only that slice (the points of all count proofs
 // are still decompressed; rcount = SIZE_MAX: all of them).
+// sync = false (verify_batch): nothing waits here -- the replay's verdicts
+// stay in J.bad_h for verify_partial_dev to check after its own
+// synchronisation, so the weights, scalars and MSM are queued right behind
+// the replay with no host round trip (J.rs stays empty).
 int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label, size_t llen, size_t count,
                      const uint8_t* proofs, const uint8_t* V, std::unique_ptr<bpp_verify_job>& job,
-                     size_t rfirst = 0, size_t rcount = SIZE_MAX) {
+                     size_t rfirst = 0, size_t rcount = SIZE_MAX, bool sync = true) {
   job.reset(new bpp_verify_job);
   bpp_verify_job& J = *job;
   if (rcount == SIZE_MAX) rcount = count;
@@ -1193,18 +1167,13 @@ int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label,
     BPP_TRY(ctx_zc_in(ctx, "vj_init", init, sizeof init, &h_init));
   }
   if (!rcount) return ctx_sync(ctx);
-  const size_t nw = (rcount + 63) / 64;
-  void* d_inv = nullptr;
-  uint32_t* h_wtot = nullptr;
-  BPP_TRY(ctx_ws(ctx, "vj_inv", (rcount + 1) * (1 + (size_t)C.lg) * 32, &d_inv));
-  BPP_TRY(ctx_zc_out(ctx, "vj_wtot", nw * 32, &h_wtot));
   BPP_TRY(ctx_zc_out(ctx, "vj_r", rcount * 32, &h_r));
   BPP_TRY(ctx_zc_out(ctx, "vj_bad", rcount * 4, &h_bad));
   if (dec_order == 1) {  // (the event is recorded before the replay: the decompression waits for the upload only)
     BPP_HIP(hipEventRecord(ctx->vj_ev_in, ctx->stream));
   }
   BPP_TRY(verify_replay_dev(ctx, C, (uint32_t)rcount, h_init, d_pf + rfirst * (plen / 4),
-                            d_V + rfirst * (vbytes / 4), (uint32_t*)d_rec, (uint32_t*)d_inv, h_wtot, h_r, h_bad));
+                            d_V + rfirst * (vbytes / 4), (uint32_t*)d_rec, h_r, h_bad));
   if (dec_order == 1) {
     BPP_HIP(hipStreamWaitEvent(kid->stream, ctx->vj_ev_in, 0));
     BPP_TRY(verify_decompress_dev(kid, C, (uint32_t)count, d_pf, d_V, (uint32_t*)d_x, (unsigned long long*)d_dbad));
@@ -1213,53 +1182,37 @@ int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label,
   } else if (dec_order == 2) {
     BPP_TRY(launch_dec());
   }
+  if (!sync) {
+    J.bad_h = h_bad;
+    J.rs.clear();
+    return BPP_OK;
+  }
   BPP_TRY(ctx_sync_latency(ctx));
   uint32_t any = 0;
   for (size_t p = 0; p < rcount; ++p) any |= h_bad[p];
   if (any) return BPP_ERR_VERIFY;
   memcpy(J.rs.data(), h_r, rcount * 32);
-  // the wave products' inverses: one host batch inversion for all waves
-  // (the products are nonzero: zero challenges entered them as 1)
-  J.winv.resize(nw);
-  memcpy(J.winv.data(), h_wtot, nw * 32);
-  hsc::batch_invert(J.winv, false);
   return BPP_OK;
 }
 
-// The device inversion state of a device job for verify_weights_dev: the
-// replay's workspace and J's wave inverses in a zero-copy buffer.
-static int job_inv_state(bpp_ctx* ctx, const bpp_verify_job& J, uint32_t** d_inv, uint32_t** h_winv) {
-  void* d = nullptr;
-  BPP_TRY(ctx_ws(ctx, "vj_inv", (J.rcount + 1) * (1 + (size_t)J.C.lg) * 32, &d));
-  *d_inv = (uint32_t*)d;
-  return ctx_zc_in(ctx, "vj_winv", J.winv.data(), J.winv.size() * 32, h_winv);
-}
-
-// A sliced job's scalars (bpp_perm_verify_slice_scalars): weights of the
-// slice's proofs from all `total` r challenges (batch index rfirst + p), the
-// generator scalars summed over the slice and the slice's proof-point
-// scalars -> d_out = [NG | rcount x npt] x 32 B (device memory).
-int verify_slice_scalars_dev(bpp_ctx* ctx, const bpp_verify_job& J, const Sc* r_all, size_t total, uint32_t* d_out) {
+// A sliced job's scalars (bpp_perm_verify_slice_scalars): the slice's
+// proofs weighted by perm::batch_weight(seed, rfirst + p, r_p), the generator
+// scalars summed over the slice and the slice's proof-point scalars ->
+// d_out = [NG | rcount x npt] x 32 B (device memory).
+int verify_slice_scalars_dev(bpp_ctx* ctx, const bpp_verify_job& J, const uint8_t seed[32], uint32_t* d_out) {
   if (J.dctx != ctx || J.dgen != ctx->vjob_gen) {
     ctx->err = "device verify job belongs to another context or was superseded by a later begin";
     return BPP_ERR_ARG;
   }
-  if (total < J.rfirst + J.rcount) return BPP_ERR_ARG;
   if (!J.rcount) {  // an empty slice adds nothing to the generator scalars
     BPP_HIP(hipMemsetAsync(d_out, 0, (2 * (size_t)J.C.n_p + 2) * 32, ctx->stream));
     return ctx_sync(ctx);
   }
   void* d_rec = nullptr;
-  BPP_TRY(ctx_ws(ctx, "vj_rec", J.rcount * vrec_n(J.C) * 32, &d_rec));
-  uint8_t seed[32] = {0};
-  if (total > 1) perm::batch_seed(r_all, total, seed);
+  BPP_TRY(ctx_ws(ctx, "vj_rec", (J.rcount + 1) * vrec_n(J.C) * 32, &d_rec));
   uint32_t* h_seed = nullptr;
   BPP_TRY(ctx_zc_in(ctx, "vj_seed", seed, 32, &h_seed));
-  uint32_t *d_inv = nullptr, *h_winv = nullptr;
-  BPP_TRY(job_inv_state(ctx, J, &d_inv, &h_winv));
-  BPP_TRY(verify_weights_dev(ctx, J.C, (uint32_t)J.rcount, J.rfirst, total, h_seed, (uint32_t*)d_rec, d_inv,
-                             h_winv));
-  BPP_TRY(verify_scalars_dev_rec(ctx, J.C, (uint32_t)J.rcount, (const uint32_t*)d_rec, d_out));
+  BPP_TRY(verify_scalars_dev_rec(ctx, J.C, (uint32_t)J.rcount, (const uint32_t*)d_rec, h_seed, J.rfirst, d_out));
   return ctx_sync(ctx);
 }
 
@@ -1281,11 +1234,17 @@ int verify_partial_gathered_dev(bpp_ctx* ctx, const bpp_gens* G, const bpp_verif
   }
   const size_t NG = 2 * (size_t)J.C.n_p + 2, npt = J.npt, T = NG + J.count * npt;
   size_t sum = 0;
+  bool mine = false;  // this job's replayed slice sits at its place among the blocks
   for (size_t r = 0; r < nslices; ++r) {
     if ((NG + counts[r] * npt) * 32 > stride) return BPP_ERR_ARG;
+    mine |= sum == J.rfirst && counts[r] == J.rcount;
     sum += counts[r];
   }
   if (sum != J.count || stride % 16) return BPP_ERR_ARG;
+  if (!mine) {
+    ctx->err = "the gathered blocks do not hold this job's slice at its proof offset";
+    return BPP_ERR_ARG;
+  }
   void *d_sv = nullptr, *d_x = nullptr, *d_dbad = nullptr;
   BPP_TRY(ctx_ws(ctx, "pv_s", T * 32 + 32, &d_sv));
   BPP_TRY(ctx_ws(ctx, "vj_x", J.count * npt * MSM_NIELS_WORDS * 4, &d_x));
@@ -1312,10 +1271,12 @@ int verify_partial_gathered_dev(bpp_ctx* ctx, const bpp_gens* G, const bpp_verif
   return BPP_OK;
 }
 
-// pass 2 of a device job: weights on the device from all `total` r
-// challenges, the weighted scalars (k_verify_scalars) and the MSM over
-// windows [wb, we); BPP_ERR_VERIFY if a proof point did not decode.
-int verify_partial_dev(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J, const Sc* r_all, size_t total,
+// pass 2 of a device job: each proof's weight perm::batch_weight(seed,
+// first + p, r_p) and constants (k_verify_consts), the weighted scalars
+// (k_verify_scalars) and the MSM over windows [wb, we); BPP_ERR_VERIFY if a
+// proof point did not decode or (an asynchronous begin) the replay rejected a
+// proof.
+int verify_partial_dev(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J, const uint8_t seed[32],
                        size_t first, uint32_t wb, uint32_t we, h25519::ge* out) {
   if (J.dctx != ctx || J.dgen != ctx->vjob_gen) {
     ctx->err = "device verify job belongs to another context or was superseded by a later begin";
@@ -1329,23 +1290,18 @@ int verify_partial_dev(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J,
     ctx->err = "generators shorter than the padded circuit";
     return BPP_ERR_LEN;
   }
-  if (first > total || J.count > total - first) return BPP_ERR_ARG;
   const size_t count = J.count, T = 2 * (size_t)J.C.n_p + 2 + count * J.npt;
   void *d_rec = nullptr, *d_x = nullptr, *d_sv = nullptr, *d_dbad = nullptr;
-  BPP_TRY(ctx_ws(ctx, "vj_rec", count * vrec_n(J.C) * 32, &d_rec));
+  BPP_TRY(ctx_ws(ctx, "vj_rec", (count + 1) * vrec_n(J.C) * 32, &d_rec));
   BPP_TRY(ctx_ws(ctx, "vj_x", count * J.npt * MSM_NIELS_WORDS * 4, &d_x));
   BPP_TRY(ctx_ws(ctx, "vj_dbad", 8, &d_dbad));
   BPP_TRY(ctx_ws(ctx, "pv_s", T * 32 + 32, &d_sv));
   {
     HostScope hs(ctx, "verify_terms");
-    uint8_t seed[32] = {0};
-    if (total > 1) perm::batch_seed(r_all, total, seed);
     uint32_t* h_seed = nullptr;
     BPP_TRY(ctx_zc_in(ctx, "vj_seed", seed, 32, &h_seed));
-    uint32_t *d_inv = nullptr, *h_winv = nullptr;
-    BPP_TRY(job_inv_state(ctx, J, &d_inv, &h_winv));
-    BPP_TRY(verify_weights_dev(ctx, J.C, (uint32_t)count, first, total, h_seed, (uint32_t*)d_rec, d_inv, h_winv));
-    BPP_TRY(verify_scalars_dev_rec(ctx, J.C, (uint32_t)count, (const uint32_t*)d_rec, (uint32_t*)d_sv));
+    BPP_TRY(verify_scalars_dev_rec(ctx, J.C, (uint32_t)count, (const uint32_t*)d_rec, h_seed, first,
+                                   (uint32_t*)d_sv));
   }
   uint64_t* h_dbad = nullptr;  // the decompression's verdict, copied behind the MSM
   BPP_TRY(ctx_zc_out(ctx, "vj_dbad_h", 8, (uint32_t**)&h_dbad));
@@ -1353,6 +1309,14 @@ int verify_partial_dev(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J,
   BPP_HIP(hipMemcpyAsync(h_dbad, d_dbad, 8, hipMemcpyDeviceToHost, ctx->stream));
   BPP_TRY(verify_msm(ctx, G, J.C, count, (const uint32_t*)d_sv, (const uint32_t*)d_x, wb, we, out));
   BPP_TRY(ctx_sync_latency(ctx));  // (msm_single_dev has synchronised; this keeps h_dbad's contract)
+  if (J.bad_h) {  // an asynchronous begin's replay verdicts (the stream has passed them)
+    uint32_t any = 0;
+    for (size_t p = 0; p < J.rcount; ++p) any |= J.bad_h[p];
+    if (any) {
+      ctx->err = "a proof's transcript replay rejected it";
+      return BPP_ERR_VERIFY;
+    }
+  }
   if (*h_dbad != ~0ull) {
     ctx->err = "undecodable proof point at index " + std::to_string(*h_dbad);
     return BPP_ERR_VERIFY;
@@ -1365,11 +1329,16 @@ int verify_partial_dev(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J,
 // transcripts are replayed on the device.
 int verify_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const uint8_t* label, size_t llen,
                  size_t count, const uint8_t* proofs, const uint8_t* V) {
+  uint8_t seed[32];  // the verifier's own randomness for the batch weights
+  if (!perm::verify_seed(seed)) {
+    ctx->err = "getrandom failed";
+    return BPP_ERR_DEVICE;
+  }
   std::unique_ptr<bpp_verify_job> job;
-  BPP_TRY(verify_begin_dev(ctx, C, label, llen, count, proofs, V, job));
+  BPP_TRY(verify_begin_dev(ctx, C, label, llen, count, proofs, V, job, 0, SIZE_MAX, false));
   const uint32_t c = msm_choose_c((double)verify_terms(*job));
   h25519::ge res;
-  BPP_TRY(verify_partial_dev(ctx, G, *job, job->rs.data(), count, 0, 0, (254 + c - 1) / c, &res));
+  BPP_TRY(verify_partial_dev(ctx, G, *job, seed, 0, 0, (254 + c - 1) / c, &res));
   uint8_t e[32];
   h25519::encode(e, res);
   static const uint8_t zero[32] = {0};
@@ -1590,22 +1559,21 @@ int bpp_perm_verify_terms(const bpp_verify_job* job, size_t* terms) {
   });
 }
 
-static int parse_rs(const uint8_t* r_all, size_t total, std::vector<Sc>& rs) {
-  rs.resize(total);
-  for (size_t p = 0; p < total; ++p)
-    if (!hsc::from_canonical(rs[p], r_all + 32 * p)) return BPP_ERR_NONCANONICAL;
-  return BPP_OK;
+int bpp_verify_seed(uint8_t seed[32]) {
+  return bpp_guard(nullptr, [&]() -> int {
+    if (!seed) return BPP_ERR_ARG;
+    return perm::verify_seed(seed) ? BPP_OK : BPP_ERR_DEVICE;
+  });
 }
 
-int bpp_perm_verify_scalars(const bpp_verify_job* job, const uint8_t* r_all, size_t total, size_t first,
-                            uint8_t* scalars_out, uint8_t* points_out) {
+int bpp_perm_verify_scalars(const bpp_verify_job* job, const uint8_t seed[32], size_t first, uint8_t* scalars_out,
+                            uint8_t* points_out) {
   return bpp_guard(nullptr, [&]() -> int {
-    if (!job || (!r_all && total) || !scalars_out || (!points_out && job->count)) return BPP_ERR_ARG;
+    if (!job || !seed || !scalars_out || (!points_out && job->count)) return BPP_ERR_ARG;
     if (job->dev) return BPP_ERR_ARG;  // (a device job keeps no host replay to expand)
-    std::vector<Sc> rs, sc;
+    std::vector<Sc> sc;
     std::vector<uint8_t> enc;
-    BPP_TRY(parse_rs(r_all, total, rs));
-    BPP_TRY(verify_terms_weighted(*job, rs.data(), total, first, sc, enc));
+    BPP_TRY(verify_terms_weighted(*job, seed, first, sc, enc));
     for (size_t i = 0; i < sc.size(); ++i) hsc::to_bytes(scalars_out + 32 * i, sc[i]);
     if (!enc.empty()) memcpy(points_out, enc.data(), enc.size());
     return BPP_OK;
@@ -1634,14 +1602,11 @@ size_t bpp_perm_verify_slice_bytes(const bpp_verify_job* job) {
   return job ? (2 * (size_t)job->C.n_p + 2 + job->rcount * job->npt) * 32 : 0;
 }
 
-int bpp_perm_verify_slice_scalars(bpp_ctx* ctx, const bpp_verify_job* job, const uint8_t* r_all, size_t total,
-                                  void* d_out) {
+int bpp_perm_verify_slice_scalars(bpp_ctx* ctx, const bpp_verify_job* job, const uint8_t seed[32], void* d_out) {
   return bpp_guard(ctx, [&]() -> int {
-    if (!ctx || !job || !d_out || (!r_all && total) || !job->dev) return BPP_ERR_ARG;
-    std::vector<Sc> rs;
-    BPP_TRY(parse_rs(r_all, total, rs));
+    if (!ctx || !job || !d_out || !seed || !job->dev) return BPP_ERR_ARG;
     BPP_HIP(hipSetDevice(ctx->device));
-    return verify_slice_scalars_dev(ctx, *job, rs.data(), total, (uint32_t*)d_out);
+    return verify_slice_scalars_dev(ctx, *job, seed, (uint32_t*)d_out);
   });
 }
 
@@ -1663,22 +1628,19 @@ int bpp_perm_verify_partial_gathered(bpp_ctx* ctx, const bpp_gens* G, const bpp_
   });
 }
 
-int bpp_perm_verify_partial(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job* job, const uint8_t* r_all,
-                            size_t total, size_t first, uint32_t w_begin, uint32_t w_end, uint8_t partial[128]) {
+int bpp_perm_verify_partial(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job* job, const uint8_t seed[32],
+                            size_t first, uint32_t w_begin, uint32_t w_end, uint8_t partial[128]) {
   return bpp_guard(ctx, [&]() -> int {
-    if (!ctx || !G || !job || !partial || (!r_all && total)) return BPP_ERR_ARG;
+    if (!ctx || !G || !job || !partial || !seed) return BPP_ERR_ARG;
     const uint32_t c = msm_choose_c((double)verify_terms(*job));
     if (w_begin > w_end || w_end > (254 + c - 1) / c) return BPP_ERR_ARG;
-    std::vector<Sc> rs;
-    BPP_TRY(parse_rs(r_all, total, rs));
-    if (first > total || job->count > total - first) return BPP_ERR_ARG;
     BPP_HIP(hipSetDevice(ctx->device));
     h25519::ge r = h25519::ge_identity();
     if (job->count) {
       if (job->dev)
-        BPP_TRY(verify_partial_dev(ctx, G, *job, rs.data(), total, first, w_begin, w_end, &r));
+        BPP_TRY(verify_partial_dev(ctx, G, *job, seed, first, w_begin, w_end, &r));
       else
-        BPP_TRY(verify_partial(ctx, G, *job, rs.data(), total, first, w_begin, w_end, &r));
+        BPP_TRY(verify_partial(ctx, G, *job, seed, first, w_begin, w_end, &r));
     }
     h25519::ge_to_words((uint32_t*)partial, r);
     return BPP_OK;

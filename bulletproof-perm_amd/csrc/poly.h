@@ -19,13 +19,15 @@ int poly_coef_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const uint32
 int poly_x_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const std::vector<hsc::Sc>& x, uint32_t** d_l,
                uint32_t** d_r, uint32_t** d_hf, std::vector<hsc::Sc>& t_hat);
 
-// The batch verifier's MSM scalars for `count` proofs (k_verify_scalars +
-// k_verify_merge): rec = [count][12 + 2 lg] canonical scalars (x_perm,
-// y^-1, z, x, w, r, a, b, t_hat, tau_x, mu, weight, u_j.., u_j^-1..);
-// d_sc (device) receives the 2 n_p + 2 merged generator scalars then
-// count x (m + 8 + 2 lg) weighted proof-point scalars.
+// The batch verifier's MSM scalars for `count` proofs (k_verify_consts +
+// k_verify_scalars + k_verify_merge): rec = [count][12 + lg] canonical
+// scalars (x_perm, y, z, x, w, r, a, b, t_hat, tau_x, mu, -, u_j..); proof p
+// is weighted by perm::batch_weight(seed, first + p, r_p); d_sc (device)
+// receives the 2 n_p + 2 merged generator scalars then count x (m + 8 + 2 lg)
+// weighted proof-point scalars, every proof's check scaled by
+// (prod u_j)^2 y^(n_p - 1) (verify_dev.h).
 int verify_scalars_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const std::vector<uint32_t>& rec,
-                       uint32_t* d_sc);
+                       const uint8_t seed[32], uint64_t first, uint32_t* d_sc);
 
 // The prover's blinding draws on the device (perm.h draw_scalar, one
 // thread each) from per-proof sponge templates (d_tmpl [P][7] u64,

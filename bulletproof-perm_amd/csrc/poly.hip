@@ -277,45 +277,96 @@ extern "C" int bpp_debug_vs_timing(unsigned long long* out, size_t n) {
 // products ran on the scalar unit (uniform operands): 21 K SALU instructions
 // per wave next to 15 K VALU, ~400 spilled SGPRs, and the CU's one scalar
 // unit shared by its waves (r04 PMC, tools/vs_phases.py).
+//
+// No inverses: proof p's check is scaled by F = U^2 Y, U = prod u_j, Y =
+// y^(n_p - 1) (nonzero: a zero y or u_j rejects the proof in the replay), so
+// that with s_i / s_0 = prod over the bits of i of u^2 (st below) and yr_i =
+// y^(n_p - 1 - i):
+//   G_i: st[i] U Y a - x zWR_i U^2 yr_i
+//   H_i: st[n_p-1-i] U b yr_i - (x zWL_i + zWO_i) U^2 yr_i + F
+//   B:   r F t_hat - r x^2 (delta' + F <z^Q, c>) + w F (a b - t_hat),
+//        delta' = sum_i U^2 yr_i zWR_i zWL_i
+//   B~:  F (r tau_x + mu)
+//   V_j: -r x^2 F zWV_j;  A_I A_O S: -F x^(1,2,3);  T_k: -F r x^k
+//   L_j: -F u_j^2;  R_j: -Y prod_{k != j} u_k^2
+// (F times bulletproofs' verification_scalars / the t-check), all times the
+// proof's batch weight w_p = perm::batch_weight(seed, first + p, r_p).
 #define VK_Z 0      // z
-#define VK_YI 1     // y^-1
+#define VK_Y 1      // y
 #define VK_X 2      // x
-#define VK_WT 3     // the proof's batch weight
-#define VK_S0A 4    // s_0 a  (s_0 = prod u_j^-1)
-#define VK_S0B 5    // s_0 b
-#define VK_WRX2 6   // wt r x^2
-#define VK_WRT 7    // wt r t_hat
-#define VK_IB 8     // wt w (a b - t_hat)
-#define VK_BB 9     // wt (r tau_x + mu)
+#define VK_WT 3     // w_p, the proof's batch weight
+#define VK_UYA 4    // U Y a
+#define VK_UB 5     // U b
+#define VK_WRX2 6   // w_p r x^2
+#define VK_WRFT 7   // w_p r F t_hat
+#define VK_IB 8     // w_p w F (a b - t_hat)
+#define VK_BB 9     // w_p F (r tau_x + mu)
 #define VK_R 10     // r
 #define VK_NXP 11   // -x_perm
-#define VK_N 12
-__global__ void __launch_bounds__(64) k_verify_consts(uint32_t count, uint32_t lg, const uint32_t* __restrict__ rec,
-                                                      uint32_t* __restrict__ kc) {
+#define VK_U2 12    // U^2
+#define VK_F 13     // F
+#define VK_WTF 14   // w_p F
+#define VK_WRX2F 15 // w_p r x^2 F
+#define VK_WTY 16   // w_p Y
+#define VK_N 17
+__global__ void __launch_bounds__(64) k_verify_consts(uint32_t count, uint32_t lg, uint64_t first,
+                                                      const uint32_t* __restrict__ seed,
+                                                      const uint32_t* __restrict__ rec, uint32_t* __restrict__ kc) {
   __builtin_amdgcn_s_setprio(3);  // (latency chain; the decompression runs beside it)
   const uint32_t p = blockIdx.x * 64 + threadIdx.x;
   if (p >= count) return;
-  const uint32_t nrec = VREC_U + 2 * lg;
+  const uint32_t nrec = VREC_U + lg;
   const uint32_t* R = rec + (size_t)p * nrec * 8;
   uint32_t* K = kc + (size_t)p * VK_N * 8;
+  // w_p = from_wide(SHAKE256("bp-perm-batch-wt" || seed || le64(first + p) ||
+  // r_p)[0..64]): 88 bytes, one sponge block (perm::batch_weight)
+  sc wt;
+  {
+    uint64_t a[25];
+    _Pragma("unroll") for (int i = 0; i < 25; ++i) a[i] = 0;
+    a[0] = 0x6d7265702d7062ull | (0x2dull << 56);  // "bp-perm-"
+    a[1] = 0x74772d6863746162ull;                 // "batch-wt"
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) a[2 + i] = (uint64_t)seed[2 * i] | ((uint64_t)seed[2 * i + 1] << 32);
+    a[6] = first + p;
+    const uint32_t* rp = R + 8 * VREC_R;
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) a[7 + i] = (uint64_t)rp[2 * i] | ((uint64_t)rp[2 * i + 1] << 32);
+    a[11] = 0x1full;         // SHAKE domain byte at 88
+    a[16] = 0x80ull << 56;   // last byte of the 136-byte rate
+    keccak_f1600_dev(a);
+    uint32_t o[16];
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) {
+      o[2 * i] = (uint32_t)a[i];
+      o[2 * i + 1] = (uint32_t)(a[i] >> 32);
+    }
+    wt = sc_from_wide_w(o);
+  }
   auto ldm = [&](uint32_t k) { return sc_to_mont(sc_load(R + 8 * k)); };
-  const sc xR = ldm(VREC_X), wtR = ldm(VREC_WT), rR = ldm(VREC_R), aR = ldm(VREC_A), bR = ldm(VREC_B),
-           thR = ldm(VREC_THAT);
-  sc s0R = ldm(VREC_U + lg);
-  for (uint32_t j = 1; j < lg; ++j) s0R = sc_mont(s0R, ldm(VREC_U + lg + j));
-  const sc wrR = sc_mont(wtR, rR);
+  const sc xR = ldm(VREC_X), yR = ldm(VREC_Y), wtR = sc_to_mont(wt), rR = ldm(VREC_R), aR = ldm(VREC_A),
+           bR = ldm(VREC_B), thR = ldm(VREC_THAT);
+  sc UR = ldm(VREC_U);
+  for (uint32_t j = 1; j < lg; ++j) UR = sc_mont(UR, ldm(VREC_U + j));
+  sc YR = yR;  // y^(2^lg - 1) = y^(n_p - 1)
+  for (uint32_t j = 1; j < lg; ++j) YR = sc_mont(sc_mont(YR, YR), yR);
+  const sc U2R = sc_mont(UR, UR), FR = sc_mont(U2R, YR);
+  const sc wrR = sc_mont(wtR, rR), wtfR = sc_mont(wtR, FR);
+  const sc wrx2R = sc_mont(wrR, sc_mont(xR, xR));
   sc_store(K + 8 * VK_Z, ldm(VREC_Z));
-  sc_store(K + 8 * VK_YI, ldm(VREC_YINV));
+  sc_store(K + 8 * VK_Y, yR);
   sc_store(K + 8 * VK_X, xR);
   sc_store(K + 8 * VK_WT, wtR);
-  sc_store(K + 8 * VK_S0A, sc_mont(s0R, aR));
-  sc_store(K + 8 * VK_S0B, sc_mont(s0R, bR));
-  sc_store(K + 8 * VK_WRX2, sc_mont(wrR, sc_mont(xR, xR)));
-  sc_store(K + 8 * VK_WRT, sc_mont(wrR, thR));
-  sc_store(K + 8 * VK_IB, sc_mont(wtR, sc_mont(ldm(VREC_W), sc_sub(sc_mont(aR, bR), thR))));
-  sc_store(K + 8 * VK_BB, sc_mont(wtR, sc_add(sc_mont(rR, ldm(VREC_TAUX)), ldm(VREC_MU))));
+  sc_store(K + 8 * VK_UYA, sc_mont(sc_mont(UR, YR), aR));
+  sc_store(K + 8 * VK_UB, sc_mont(UR, bR));
+  sc_store(K + 8 * VK_WRX2, wrx2R);
+  sc_store(K + 8 * VK_WRFT, sc_mont(sc_mont(wrR, FR), thR));
+  sc_store(K + 8 * VK_IB, sc_mont(wtfR, sc_mont(ldm(VREC_W), sc_sub(sc_mont(aR, bR), thR))));
+  sc_store(K + 8 * VK_BB, sc_mont(wtfR, sc_add(sc_mont(rR, ldm(VREC_TAUX)), ldm(VREC_MU))));
   sc_store(K + 8 * VK_R, rR);
   sc_store(K + 8 * VK_NXP, sc_neg(ldm(VREC_XPERM)));
+  sc_store(K + 8 * VK_U2, U2R);
+  sc_store(K + 8 * VK_F, FR);
+  sc_store(K + 8 * VK_WTF, wtfR);
+  sc_store(K + 8 * VK_WRX2F, sc_mont(wrx2R, FR));
+  sc_store(K + 8 * VK_WTY, sc_mont(wtR, YR));
 }
 
 // (at 4 waves per SIMD: 128 VGPRs instead of 148, 108 B of spills, 8
@@ -334,11 +385,11 @@ __global__ void __launch_bounds__(POLY_T) __attribute__((amdgpu_waves_per_eu(VS_
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const uint32_t NY = min(n_p, (uint32_t)POW_LO);
   uint32_t* zt = lds;                // [Q + 1] z^e, Montgomery
-  uint32_t* yit = zt + 8 * (Q + 1);  // [NY] y^-i
-  uint32_t* st = yit + 8 * NY;       // [NY] s_i / s_0 (below)
+  uint32_t* yt = zt + 8 * (Q + 1);   // [NY] y^e
+  uint32_t* st = yt + 8 * NY;        // [NY] s_i / s_0 (below)
   uint32_t* red = st + 8 * NY;       // reduction scratch
   const uint32_t* zp = zt + 8;       // z^(q+1)
-  const uint32_t p = blockIdx.x, nrec = VREC_U + 2 * lg;
+  const uint32_t p = blockIdx.x, nrec = VREC_U + lg;
   const uint32_t* R = rec + (size_t)p * nrec * 8;
   const uint32_t* K = kc + (size_t)p * VK_N * 8;
   const sc oneR = sc_one_mont();
@@ -350,14 +401,14 @@ __global__ void __launch_bounds__(POLY_T) __attribute__((amdgpu_waves_per_eu(VS_
   // over the factors u_{lg-1-k}^2, the bits from POW_LO_LG up per lane
   if (threadIdx.x == 0) {
     sc_table_pow_init(zt, Q + 1, ldk(VK_Z), oneR);
-    sc_table_pow_init(yit, NY, ldk(VK_YI), oneR);
+    sc_table_pow_init(yt, NY, ldk(VK_Y), oneR);
     sc_store(st, oneR);
   }
   for (uint32_t b = threadIdx.x; b < POW_LO_LG && (1u << b) < NY; b += blockDim.x) {
     const sc u = ldm(VREC_U + lg - 1 - b);
     sc_store(st + 8 * (1u << b), sc_mont(u, u));
   }
-  sc_tables3({zt, Q + 1, false}, {yit, NY, false}, {st, NY, true});
+  sc_tables3({zt, Q + 1, false}, {yt, NY, false}, {st, NY, true});
   VS_T(1);
   auto s_of = [&](uint32_t i) {  // s_i / s_0
     sc v = sc_load(st + 8 * (i % POW_LO));
@@ -368,21 +419,25 @@ __global__ void __launch_bounds__(POLY_T) __attribute__((amdgpu_waves_per_eu(VS_
       }
     return v;
   };
-  const sc s0aR = ldk(VK_S0A), s0bR = ldk(VK_S0B), xR = ldk(VK_X), wtR = ldk(VK_WT);
-  sc yihi = oneR, yistep = oneR;  // (y^-POW_LO)^r, as k_poly_coef
-  if (n_p > POW_LO) yistep = sc_mont(sc_load(yit + 8 * (POW_LO - 1)), ldk(VK_YI));
+  const sc uyaR = ldk(VK_UYA), ubR = ldk(VK_UB), xR = ldk(VK_X), wtR = ldk(VK_WT), u2R = ldk(VK_U2), fR = ldk(VK_F);
+  // gate i = n_p - 1 - e with e ascending per lane: yr_i = y^e = yt[e mod
+  // POW_LO] (y^POW_LO)^(e / POW_LO), the second factor a running product
+  // (blockDim = POW_LO whenever n_p > POW_LO)
+  sc yhi = oneR, ystep = oneR;
+  if (n_p > POW_LO) ystep = sc_mont(sc_load(yt + 8 * (POW_LO - 1)), ldk(VK_Y));
   const size_t gb = (size_t)p * NG;
-  sc acc[2] = {sc_zero(), sc_zero()};  // delta = sum y^-i zWR_i zWL_i, zc = <z^Q, c>
-  for (uint32_t i = threadIdx.x; i < n_p; i += blockDim.x) {
-    sc yi = sc_load(yit + 8 * (i % POW_LO));
-    if (i >= POW_LO) yi = sc_mont(yi, yihi);
-    if (n_p > POW_LO) yihi = sc_mont(yihi, yistep);
+  sc acc[2] = {sc_zero(), sc_zero()};  // delta' = sum U^2 yr_i zWR_i zWL_i, zc = <z^Q, c>
+  for (uint32_t e = threadIdx.x; e < n_p; e += blockDim.x) {
+    const uint32_t i = n_p - 1 - e;
+    sc yr = sc_load(yt + 8 * (e % POW_LO));
+    if (e >= POW_LO) yr = sc_mont(yr, yhi);
+    if (n_p > POW_LO) yhi = sc_mont(yhi, ystep);
+    const sc yu = sc_mont(u2R, yr);
     const sc zWL = col_sum(cp, ce, i, zp), zWR = col_sum(cp + (n_p + 1), ce, i, zp),
              zWO = col_sum(cp + 2 * (n_p + 1), ce, i, zp);
-    acc[0] = sc_add(acc[0], sc_mont(sc_mont(yi, zWR), zWL));
-    const sc gi = sc_sub(sc_mont(s_of(i), s0aR), sc_mont(sc_mont(zWR, xR), yi));
-    const sc hi = sc_add(sc_sub(sc_mont(sc_mont(s_of(n_p - 1 - i), s0bR), yi), sc_mont(sc_add(sc_mont(zWL, xR), zWO), yi)),
-                         oneR);
+    acc[0] = sc_add(acc[0], sc_mont(sc_mont(yu, zWR), zWL));
+    const sc gi = sc_sub(sc_mont(s_of(i), uyaR), sc_mont(sc_mont(zWR, xR), yu));
+    const sc hi = sc_add(sc_sub(sc_mont(sc_mont(s_of(e), ubR), yr), sc_mont(sc_add(sc_mont(zWL, xR), zWO), yu)), fR);
     sc_store(gen + 8 * (gb + i), sc_from_mont(sc_mont(gi, wtR)));
     sc_store(gen + 8 * (gb + n_p + i), sc_from_mont(sc_mont(hi, wtR)));
   }
@@ -392,42 +447,52 @@ __global__ void __launch_bounds__(POLY_T) __attribute__((amdgpu_waves_per_eu(VS_
     acc[1] = sc_add(acc[1], sc_mont(sc_load(zp + 8 * q), c));
   }
   VS_T(3);
-  const sc wrx2R = ldk(VK_WRX2);
+  const sc wrx2fR = ldk(VK_WRX2F);
   const size_t pb = NG + (size_t)p * npt;
-  // V_j: -wt r x^2 zWV_j (zWV from the fourth column-CSR, m columns; the
+  // V_j: -wt r x^2 F zWV_j (zWV from the fourth column-CSR, m columns; the
   // heavy x column summed by the whole workgroup)
   const uint32_t* cpv = cp + 3 * (n_p + 1);
   for (uint32_t j = threadIdx.x; j < m; j += blockDim.x)
     if (cpv[j + 1] - cpv[j] <= HEAVY_COL)
-      sc_store(sc_out + 8 * (pb + j), sc_from_mont(sc_neg(sc_mont(col_sum(cpv, ce, j, zp), wrx2R))));
+      sc_store(sc_out + 8 * (pb + j), sc_from_mont(sc_neg(sc_mont(col_sum(cpv, ce, j, zp), wrx2fR))));
   const uint32_t* heavy = cpv + m + 1;  // [count, columns...] (build_csr)
   for (uint32_t h = 0; h < heavy[0]; ++h) {
     const uint32_t j = heavy[1 + h];
     const sc cs = col_sum_block(cpv, ce, j, zp, red);
-    if (threadIdx.x == 0) sc_store(sc_out + 8 * (pb + j), sc_from_mont(sc_neg(sc_mont(cs, wrx2R))));
+    if (threadIdx.x == 0) sc_store(sc_out + 8 * (pb + j), sc_from_mont(sc_neg(sc_mont(cs, wrx2fR))));
   }
   VS_T(4);
-  // A_I, A_O, S: -wt x^(1,2,3); T_k: -wt r x^k (k = 1, 3..6); L_j: -wt u_j^2; R_j: -wt u_j^-2
+  // A_I, A_O, S: -wt F x^(1,2,3); T_k: -wt F r x^k (k = 1, 3..6); L_j:
+  // -wt F u_j^2; R_j: -wt Y prod_{k != j} u_k^2
   for (uint32_t j = threadIdx.x; j < 8 + 2 * lg; j += blockDim.x) {
-    sc v;
+    sc v, f = ldk(VK_WTF);
     if (j < 3) {
       v = xR;
       for (uint32_t e = 0; e < j; ++e) v = sc_mont(v, xR);
     } else if (j < 8) {
       const uint32_t e = j == 3 ? 1u : j - 1;  // T1, T3, T4, T5, T6
       v = sc_mont(ldk(VK_R), sc_pow_small(xR, e, oneR));
-    } else {
-      const sc u = ldm(j < 8 + lg ? VREC_U + (j - 8) : VREC_U + lg + (j - 8 - lg));
+    } else if (j < 8 + lg) {
+      const sc u = ldm(VREC_U + (j - 8));
       v = sc_mont(u, u);
+    } else {
+      const uint32_t jj = j - 8 - lg;
+      v = oneR;
+      for (uint32_t k = 0; k < lg; ++k)
+        if (k != jj) {
+          const sc u = ldm(VREC_U + k);
+          v = sc_mont(v, sc_mont(u, u));
+        }
+      f = ldk(VK_WTY);
     }
-    sc_store(sc_out + 8 * (pb + m + j), sc_from_mont(sc_neg(sc_mont(v, wtR))));
+    sc_store(sc_out + 8 * (pb + m + j), sc_from_mont(sc_neg(sc_mont(v, f))));
   }
   VS_T(5);
   sc_block_sum<2>(acc, red);
   VS_T(6);
   if (threadIdx.x == 0) {
-    // B: wt (r (t_hat - x^2 (delta + zc)) + w (a b - t_hat)); B_blinding: wt (r tau_x + mu)
-    const sc tB = sc_sub(ldk(VK_WRT), sc_mont(wrx2R, sc_add(acc[0], acc[1])));
+    // B: wt (r F t_hat - r x^2 (delta' + F zc) + w F (a b - t_hat)); B_blinding: wt F (r tau_x + mu)
+    const sc tB = sc_sub(ldk(VK_WRFT), sc_mont(ldk(VK_WRX2), sc_add(acc[0], sc_mont(fR, acc[1]))));
     sc_store(gen + 8 * (gb + 2 * n_p), sc_from_mont(sc_add(tB, ldk(VK_IB))));
     sc_store(gen + 8 * (gb + 2 * n_p + 1), sc_from_mont(ldk(VK_BB)));
   }
@@ -732,14 +797,15 @@ int poly_x_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t P, const std::vect
 }
 
 int verify_scalars_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const std::vector<uint32_t>& rec,
-                       uint32_t* d_sc) {
-  uint32_t* h = nullptr;  // per-proof records read in place from pinned host memory (ctx_zc_in)
+                       const uint8_t seed[32], uint64_t first, uint32_t* d_sc) {
+  uint32_t *h = nullptr, *hs = nullptr;  // per-proof records read in place from pinned host memory (ctx_zc_in)
   BPP_TRY(ctx_zc_in(ctx, "vs_rec_h", rec.data(), rec.size() * 4, &h));
-  return verify_scalars_dev_rec(ctx, C, count, h, d_sc);
+  BPP_TRY(ctx_zc_in(ctx, "vs_seed_h", seed, 32, &hs));
+  return verify_scalars_dev_rec(ctx, C, count, h, hs, first, d_sc);
 }
 
 int verify_scalars_dev_rec(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const uint32_t* d_rec,
-                           uint32_t* d_sc) {
+                           const uint32_t* seed, uint64_t first, uint32_t* d_sc) {
   std::vector<uint32_t> cp, ce;
   build_csr(C, cp, ce, true);
   std::vector<uint32_t> cw((size_t)C.Q * 8);
@@ -760,8 +826,8 @@ int verify_scalars_dev_rec(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count,
   BPP_TRY(ctx_ws(ctx, "vs_kc", (size_t)count * VK_N * 32, &d_kc));
   {
     ProfScope ps(ctx, "verify_scalars");
-    hipLaunchKernelGGL(k_verify_consts, dim3((count + 63) / 64), dim3(64), 0, ctx->stream, count, C.lg, d_rec,
-                       (uint32_t*)d_kc);
+    hipLaunchKernelGGL(k_verify_consts, dim3((count + 63) / 64), dim3(64), 0, ctx->stream, count, C.lg, first, seed,
+                       d_rec, (uint32_t*)d_kc);
     hipLaunchKernelGGL(k_verify_scalars, dim3(count), dim3(nt), lds, ctx->stream, C.n_p, C.m, C.Q, C.lg, d_rec,
                        (const uint32_t*)d_kc, (const uint32_t*)d_cp, (const uint32_t*)d_ce, (const uint32_t*)d_c,
                        (uint32_t*)d_gen, d_sc, NG, npt);

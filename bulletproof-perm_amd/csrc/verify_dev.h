@@ -5,9 +5,13 @@
 #include "ctx.h"
 #include "host/perm.h"
 
-// Per-proof verifier record: [12 + 2 lg] canonical scalars (8 words each)
+// Per-proof verifier record: [12 + lg] canonical scalars (8 words each).
+// The verifier needs no inverse (DESIGN.md §5 "No inversions"): every
+// proof's check is scaled by F = (u_0 .. u_{lg-1})^2 y^(n_p - 1), so y^-i,
+// s_0 = prod u_j^-1 and u_j^-2 become y^(n_p-1-i), prod u_j and
+// prod_{k != j} u_k^2.
 #define VREC_XPERM 0
-#define VREC_YINV 1
+#define VREC_Y 1
 #define VREC_Z 2
 #define VREC_X 3
 #define VREC_W 4
@@ -17,9 +21,9 @@
 #define VREC_THAT 8
 #define VREC_TAUX 9
 #define VREC_MU 10
-#define VREC_WT 11  // the proof's batch weight
-#define VREC_U 12   // u_j (lg), then u_j^-1 (lg)
-inline uint32_t vrec_n(const perm::Circuit& C) { return VREC_U + 2 * C.lg; }
+#define VREC_WT 11  // (unused: the weight is made by k_verify_consts)
+#define VREC_U 12   // u_j (lg)
+inline uint32_t vrec_n(const perm::Circuit& C) { return VREC_U + C.lg; }
 // proof points per proof in MSM order: V_0..V_{m-1}, A_I, A_O, S, T1 T3 T4
 // T5 T6, L_0.., R_0..
 inline uint32_t vpts_n(const perm::Circuit& C) { return C.m + 8 + 2 * C.lg; }
@@ -28,16 +32,12 @@ inline uint32_t vpts_n(const perm::Circuit& C) { return C.m + 8 + 2 * C.lg; }
 // (k_verify_replay_g, then k_verify_reduce and k_verify_replay_post): d_proofs [count][proof_len] and d_V [count][m][32] on
 // the device; init = the 52-word transcript state every proof shares (the
 // label's Transcript::new and arithmetic_domain_sep(n_p); verify_init_state).
-// Writes d_rec (weights, y^-1 and the u_j^-1 left for verify_weights_dev),
-// d_inv ([count + 1][1 + lg] scalars: the inversion state), wtot
-// ([ceil(count / 64)][32]: each wave's product, for the host to invert),
-// r_out ([count][32], the t-check weight challenges) and bad ([count] u32,
-// nonzero where a point is the identity encoding, a scalar is not canonical
-// or a challenge is zero).  wtot, r_out and bad may be pinned host memory
-// (written in place).
+// Writes d_rec (the challenges and the proof's scalars), r_out ([count][32],
+// the t-check weight challenges) and bad ([count] u32, nonzero where a point
+// is the identity encoding, a scalar is not canonical or a challenge is
+// zero).  r_out and bad may be pinned host memory (written in place).
 int verify_replay_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const uint32_t* d_init,
-                      const uint32_t* d_proofs, const uint32_t* d_V, uint32_t* d_rec, uint32_t* d_inv,
-                      uint32_t* wtot, uint32_t* r_out, uint32_t* bad);
+                      const uint32_t* d_proofs, const uint32_t* d_V, uint32_t* d_rec, uint32_t* r_out, uint32_t* bad);
 // Decompresses the proof points of proofs [p0, p1) (p1 = ~0u: count) of the
 // uploaded proofs / V into d_tbl ([count * vpts_n] Niels rows in MSM order);
 // *d_bad = the smallest index of an undecodable encoding (set to ~0 by the
@@ -48,17 +48,12 @@ int verify_decompress_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, 
                           uint32_t p1 = ~0u);
 // The 52-word shared transcript prefix for verify_replay_dev.
 void verify_init_state(const perm::Circuit& C, const uint8_t* label, size_t llen, uint32_t out[52]);
-// rec[p][VREC_WT] = perm::batch_weight(seed, first + p) for p < count (one
-// for total <= 1); with d_inv / winv (a device replay: d_inv as
-// verify_replay_dev left it, winv = the inverses of its wave products) also
-// rec[p]'s y^-1 and u_j^-1.  seed and winv may be pinned host memory.
-int verify_weights_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, uint64_t first, uint64_t total,
-                       const uint32_t* seed, uint32_t* d_rec, const uint32_t* d_inv = nullptr,
-                       const uint32_t* winv = nullptr);
 // out[i] = sum over the nb blocks (stride words apart) of block[b][i], i < n
 // (the generator scalars of a gathered sliced verification).
 int verify_sum_blocks_dev(bpp_ctx* ctx, uint32_t nb, uint32_t n, const uint32_t* d_blocks, uint32_t stride,
                           uint32_t* d_out);
-// k_verify_scalars + k_verify_merge over device records (poly.hip).
+// k_verify_consts (each proof's weight perm::batch_weight(seed, first + p,
+// r_p) and its constants) + k_verify_scalars + k_verify_merge over device
+// records (poly.hip).  seed: 8 words, may be pinned host memory.
 int verify_scalars_dev_rec(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const uint32_t* d_rec,
-                           uint32_t* d_sc);
+                           const uint32_t* seed, uint64_t first, uint32_t* d_sc);

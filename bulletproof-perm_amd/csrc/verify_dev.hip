@@ -47,12 +47,14 @@ FE_INLINE bool w8_zero(const uint32_t w[8]) {
 // V bytes are first copied into LDS by its 8 lanes (one load latency instead
 // of one per absorbed item).
 #define RG_GROUPS (64 / GRP_LANES)
-// A group's sponge (200 B) and pi scratch (GRP_SCR_BYTES) at a stride of 576
-// B = 144 dwords = 16 mod 32: the two groups of a 32-lane half (the lanes whose
-// ds_read_b32 / ds_write_b32 share the 32 banks) then hit disjoint banks in
-// every chi load and all but 2 of a round's pi stores (tools/lds_banks.py: 2
-// extra LDS cycles a round against 20 at the former 480-B stride, where every
-// chi load was 2-way)
+// A group's sponge (200 B) and pi scratch (GRP_SCR_BYTES) at a stride of
+// GRP_BLOCK: 736 B = 184 dwords (24 mod 32) with the default half-column chi
+// layout (GRP_CHI128), whose reads are one 16-B and one 4-B read per column;
+// the former dword layout used 576 B = 144 dwords (16 mod 32), chosen with
+// tools/lds_banks.py so that the two groups of a 32-lane half hit disjoint
+// banks in every chi load (2 extra LDS cycles a round against 20 at 480 B).
+// The 736-B stride has not been re-modelled: the replay measured the same
+// with the conflicts gone (r04_verify_pmc_final.json), it is not LDS-bound.
 #ifndef RG_GS  // (A/B: -DGRP_CHI128=0 -DRG_GS=480 -DRG_SCR_OFF=240 -DGRP_TRASH=50 is the round-3 layout)
 #define RG_GS GRP_BLOCK
 #define RG_SCR_OFF GRP_SCR_OFF
@@ -169,19 +171,19 @@ __global__ void __launch_bounds__(64) k_verify_replay_g(uint32_t count, uint32_t
 
 // One lane per (proof, challenge): the 64 squeezed bytes of k_verify_replay_g
 // reduced mod l (the verifier's challenge_scalar, transcript_protocol.rs:62-67)
-// into the proof's record -- x_perm, z, x, w, u_j, r in their slots, y in
-// the y^-1 slot until k_verify_weights replaces it -- and r to r_out.  (One
-// lane per proof ran the 6 + lg reductions in a row, ~2.4 K cycles each.)
+// into the proof's record -- x_perm, y, z, x, w, u_j, r in their slots -- and
+// r to r_out.  (One lane per proof ran the 6 + lg reductions in a row, ~2.4 K
+// cycles each.)
 __global__ void __launch_bounds__(64) k_verify_reduce(uint32_t count, uint32_t lg, const uint32_t* __restrict__ ch,
                                                       uint32_t* __restrict__ rec, uint32_t* __restrict__ r_out) {
   __builtin_amdgcn_s_setprio(3);  // (latency chain; the decompression runs beside it)
-  const uint32_t nch = 6 + lg, nrec = VREC_U + 2 * lg;
+  const uint32_t nch = 6 + lg, nrec = VREC_U + lg;
   const size_t t = (size_t)blockIdx.x * 64 + threadIdx.x;
   if (t >= (size_t)count * nch) return;
   const uint32_t p = (uint32_t)(t / nch), c = (uint32_t)(t % nch);
   const sc v = sc_from_wide_w(ch + t * 16);
   const uint32_t slot = c == 0   ? VREC_XPERM
-                        : c == 1 ? VREC_YINV
+                        : c == 1 ? VREC_Y
                         : c == 2 ? VREC_Z
                         : c == 3 ? VREC_X
                         : c == 4 ? VREC_W
@@ -191,59 +193,28 @@ __global__ void __launch_bounds__(64) k_verify_reduce(uint32_t count, uint32_t l
   if (c == 5 + lg) sc_store(r_out + 8 * (size_t)p, v);
 }
 
-// One lane per proof, after k_verify_reduce: the checks, the record's proof
-// scalars, and ONE inversion per wave of 64 proofs for y^-1 and the u_j^-1
-// (Montgomery's trick: the lane's product y u_0 .. u_{lg-1}, then the
-// wave's).  This kernel leaves the lane's prefix products and the product of
-// the other 63 lanes' totals in inv_st ([count + 1][1 + lg], Montgomery) and
-// the wave's total in wtot[wave] (canonical); the host inverts the wave
-// totals (one batch inversion, perm_api.hip verify_begin_dev) and
-// k_verify_weights finishes the inverses.  A binary-Euclid inversion on the
-// device cost a wave ~310 K cycles (129 us, tools/ubench/keccak_grp.hip).  A
-// zero y or u (a rejected proof) enters the products as 1.  Lanes past the
-// batch shadow the last proof and keep to the pad entries.
+// One lane per proof, after k_verify_reduce: the checks (a zero y or u_j
+// rejects the proof: the verifier's scaling by (prod u_j)^2 y^(n_p - 1) must
+// not vanish) and the record's proof scalars.  No inversions: the checks are
+// scaled instead (poly.hip k_verify_consts).
 __global__ void __launch_bounds__(64) k_verify_replay_post(uint32_t count, uint32_t lg,
                                                            const uint32_t* __restrict__ okw,
                                                            const uint32_t* __restrict__ proofs, uint32_t pw,
-                                                           uint32_t* __restrict__ rec, uint32_t* __restrict__ inv_st,
-                                                           uint32_t* __restrict__ wtot, uint32_t* __restrict__ bad) {
+                                                           uint32_t* __restrict__ rec, uint32_t* __restrict__ bad) {
   __builtin_amdgcn_s_setprio(3);  // (latency chain; the decompression runs beside it)
-  const bool live = blockIdx.x * 64 + threadIdx.x < count;
-  const uint32_t p = live ? blockIdx.x * 64 + threadIdx.x : count - 1;
-  const uint32_t nrec = VREC_U + 2 * lg;
-  const uint32_t* __restrict__ Rp = rec + (size_t)p * nrec * 8;  // (the shadowed proof's record: read only)
-  uint32_t* __restrict__ R = rec + (size_t)(live ? p : count) * nrec * 8;
-  uint32_t* __restrict__ IS = inv_st + (size_t)(live ? p : count) * (1 + lg) * 8;
+  const uint32_t p = blockIdx.x * 64 + threadIdx.x;
+  if (p >= count) return;
+  const uint32_t nrec = VREC_U + lg;
+  uint32_t* __restrict__ R = rec + (size_t)p * nrec * 8;
   const uint32_t* __restrict__ PP = proofs + (size_t)p * pw;
   bool ok = okw[p] != 0;
-  auto nz = [&](const sc& v) {
-    sc o = v;
-    if (w8_zero(v.v)) {
-      ok = false;
-      o.v[0] = 1;
-    }
-    return o;
-  };
-  sc acc = sc_to_mont(nz(sc_load(Rp + 8 * VREC_YINV)));  // (y, until k_verify_weights)
-  for (uint32_t j = 0; j < lg; ++j) {
-    sc_store(IS + 8 * (1 + j), acc);  // prefix y u_0 .. u_{j-1}
-    acc = sc_mont(acc, sc_to_mont(nz(sc_load(Rp + 8 * (VREC_U + j)))));
-  }
-  // the other lanes' product: inclusive prefix / suffix scans over the wave
-  const int lane = threadIdx.x & 63;
-  const sc oneR = sc_one_mont();
-  sc pre = acc, suf = acc;
-  _Pragma("unroll") for (int d = 1; d < 64; d <<= 1) {
-    const sc a = sc_shfl(pre, lane - d < 0 ? lane : lane - d);
-    const sc b = sc_shfl(suf, lane + d > 63 ? lane : lane + d);
-    if (lane >= d) pre = sc_mont(a, pre);
-    if (lane + d <= 63) suf = sc_mont(suf, b);
-  }
-  const sc xp = sc_shfl(pre, lane ? lane - 1 : 0), xs = sc_shfl(suf, lane < 63 ? lane + 1 : 63);
-  sc_store(IS, sc_mont(lane ? xp : oneR, lane < 63 ? xs : oneR));
-  if (lane == 63) sc_store(wtot + 8 * (size_t)blockIdx.x, sc_from_mont(pre));
-  if (!live) return;
   uint32_t w[8];
+  ld8(R + 8 * VREC_Y, w);
+  ok &= !w8_zero(w);
+  for (uint32_t j = 0; j < lg; ++j) {
+    ld8(R + 8 * (VREC_U + j), w);
+    ok &= !w8_zero(w);
+  }
   ld8(PP + 88 + 16 * lg, w);
   st8(R + 8 * VREC_A, w);
   ld8(PP + 88 + 16 * lg + 8, w);
@@ -254,58 +225,7 @@ __global__ void __launch_bounds__(64) k_verify_replay_post(uint32_t count, uint3
   st8(R + 8 * VREC_TAUX, w);
   ld8(PP + 72, w);
   st8(R + 8 * VREC_MU, w);
-  sc_store(R + 8 * VREC_WT, sc_zero());
   bad[p] = ok ? 0u : 1u;
-}
-
-// w_p = from_wide(SHAKE256("bp-perm-batch-wt" || seed || le64(first + p))
-// [0..64]) (perm::batch_weight): 56 bytes, one sponge block.
-// With inv_st / winv (a device replay's job): also y^-1 and u_j^-1 into the
-// record from k_verify_replay_post's prefix products, the other lanes'
-// product and the host-inverted wave total (canonical winv[wave]); inv_st is
-// only read, so a job's records can be finished again for another window
-// range.
-__global__ void __launch_bounds__(64) k_verify_weights(uint32_t count, uint64_t first, uint64_t total,
-                                                       const uint32_t* __restrict__ seed, uint32_t* __restrict__ rec,
-                                                       uint32_t nrec, uint32_t lg,
-                                                       const uint32_t* __restrict__ inv_st,
-                                                       const uint32_t* __restrict__ winv) {
-  __builtin_amdgcn_s_setprio(3);  // (latency chain; the decompression runs beside it)
-  const uint32_t p = blockIdx.x * 64 + threadIdx.x;
-  if (p >= count) return;
-  if (inv_st) {
-    uint32_t* __restrict__ R = rec + (size_t)p * nrec * 8;
-    const uint32_t* __restrict__ IS = inv_st + (size_t)p * (1 + lg) * 8;
-    sc inv = sc_mont(sc_to_mont(sc_load(winv + 8 * (size_t)blockIdx.x)), sc_load(IS));  // (lane total)^-1
-    for (uint32_t j = lg; j-- > 0;) {
-      sc_store(R + 8 * (VREC_U + lg + j), sc_from_mont(sc_mont(inv, sc_load(IS + 8 * (1 + j)))));
-      sc u = sc_load(R + 8 * (VREC_U + j));
-      if (w8_zero(u.v)) u.v[0] = 1;
-      inv = sc_mont(inv, sc_to_mont(u));
-    }
-    sc_store(R + 8 * VREC_YINV, sc_from_mont(inv));
-  }
-  sc wt = sc_zero();
-  if (total <= 1) {
-    wt.v[0] = 1;
-  } else {
-    uint64_t a[25];
-    _Pragma("unroll") for (int i = 0; i < 25; ++i) a[i] = 0;
-    a[0] = 0x6d7265702d7062ull | (0x2dull << 56);  // "bp-perm-"
-    a[1] = 0x74772d6863746162ull;                 // "batch-wt"
-    _Pragma("unroll") for (int i = 0; i < 4; ++i) a[2 + i] = (uint64_t)seed[2 * i] | ((uint64_t)seed[2 * i + 1] << 32);
-    a[6] = first + p;
-    a[7] = 0x1full;              // SHAKE domain byte at 56
-    a[16] = 0x80ull << 56;       // last byte of the 136-byte rate
-    keccak_f1600_dev(a);
-    uint32_t o[16];
-    _Pragma("unroll") for (int i = 0; i < 8; ++i) {
-      o[2 * i] = (uint32_t)a[i];
-      o[2 * i + 1] = (uint32_t)(a[i] >> 32);
-    }
-    wt = sc_from_wide_w(o);
-  }
-  sc_store(rec + ((size_t)p * nrec + VREC_WT) * 8, wt);
 }
 
 // Decompress every proof point straight from the uploaded proofs and V into
@@ -359,8 +279,7 @@ void verify_init_state(const perm::Circuit& C, const uint8_t* label, size_t llen
 }
 
 int verify_replay_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const uint32_t* d_init,
-                      const uint32_t* d_proofs, const uint32_t* d_V, uint32_t* d_rec, uint32_t* d_inv,
-                      uint32_t* wtot, uint32_t* r_out, uint32_t* bad) {
+                      const uint32_t* d_proofs, const uint32_t* d_V, uint32_t* d_rec, uint32_t* r_out, uint32_t* bad) {
   if (!count) return BPP_OK;
   const uint32_t pw = (uint32_t)(perm::proof_len(C.k) / 4);
   const uint32_t nch = 6 + C.lg;
@@ -384,20 +303,9 @@ int verify_replay_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, cons
     hipLaunchKernelGGL(k_verify_reduce, dim3(grid_for((size_t)count * nch, 64)), dim3(64), 0, ctx->stream, count,
                        C.lg, (const uint32_t*)d_ch, d_rec, r_out);
     hipLaunchKernelGGL(k_verify_replay_post, dim3(grid_for(count, 64)), dim3(64), 0, ctx->stream, count, C.lg,
-                       (const uint32_t*)d_ok, d_proofs, pw, d_rec, d_inv, wtot, bad);
+                       (const uint32_t*)d_ok, d_proofs, pw, d_rec, bad);
   }
   return ctx_check_launch(ctx, "k_verify_reduce/post");
-}
-
-int verify_weights_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, uint64_t first, uint64_t total,
-                       const uint32_t* seed, uint32_t* d_rec, const uint32_t* d_inv, const uint32_t* winv) {
-  if (!count) return BPP_OK;
-  {
-    ProfScope ps(ctx, "verify_weights");
-    hipLaunchKernelGGL(k_verify_weights, dim3(grid_for(count, 64)), dim3(64), 0, ctx->stream, count, first, total,
-                       seed, d_rec, vrec_n(C), C.lg, d_inv, winv);
-  }
-  return ctx_check_launch(ctx, "k_verify_weights");
 }
 
 // out[i] = sum_b blocks[b * stride + 8 i] (mod l, canonical in and out)

@@ -274,10 +274,14 @@ int bpp_debug_secret_residue(bpp_ctx* ctx, uint64_t* nonzero_bytes);
 /* BPP_OK or BPP_ERR_VERIFY (ProofError::VerificationError). One GPU MSM. */
 int bpp_perm_verify(bpp_ctx* ctx, const bpp_gens* g, uint32_t k, const uint8_t* label, size_t llen,
                     const uint8_t* proof, size_t proof_len, const uint8_t* V);
-/* Batch verification: all proofs' checks folded with weights derived from
- * every proof's transcript into ONE MSM (generator scalars merged across
- * proofs); the transcripts are replayed on the GPU.  Weights: DESIGN.md §5
- * "Batch weights" (perm.h batch_seed / batch_weight). */
+/* Batch verification: all proofs' checks folded into ONE MSM (generator
+ * scalars merged across proofs) with random weights w_p =
+ * from_wide(SHAKE256("bp-perm-batch-wt" || seed || le64 p || r_p)[0..64]):
+ * seed = 32 bytes of the verifier's own randomness (getrandom), mixed with
+ * each proof's transcript challenge r_p as bulletproofs' r1cs batch verifier
+ * mixes its rng into a TranscriptRng.  The transcripts are replayed on the
+ * GPU and the whole batch runs with no host round trip (DESIGN.md §5 "Batch
+ * weights", "No inversions"). */
 int bpp_perm_verify_batch(bpp_ctx* ctx, const bpp_gens* g, uint32_t k, size_t count, const uint8_t* label,
                           size_t llen, const uint8_t* proofs, const uint8_t* V);
 
@@ -308,20 +312,27 @@ int bpp_perm_verify_begin_dev(bpp_ctx* ctx, uint32_t k, size_t count, const uint
 /* Terms of the job's MSM: 2 n_p + 2 merged generators + count x (m + 8 +
  * 2 log2 n_p) proof points.  bpp_msm_windows(terms) gives c and W. */
 int bpp_perm_verify_terms(const bpp_verify_job* job, size_t* terms);
-/* The job's MSM terms (host): proof weights come from a batch transcript
- * over all `total` r challenges (r_all, every rank's in proof order), this
- * job's proofs being [first, first + count).  scalars_out: terms x 32 B
+/* 32 bytes of verifier randomness for a batch (the OS CSPRNG).  Every job,
+ * slice and rank of ONE batch takes the same seed (rank 0 draws it and
+ * broadcasts the 32 bytes); a seed the provers can predict voids the batch's
+ * soundness. */
+int bpp_verify_seed(uint8_t seed[32]);
+/* The job's MSM terms (host): proof p of the job is batch proof first + p,
+ * weighted by w = from_wide(SHAKE256("bp-perm-batch-wt" || seed || le64(first
+ * + p) || r_p)[0..64]) (bpp_perm_verify_batch).  scalars_out: terms x 32 B
  * (G[0..n_p), H[0..n_p), B, B_blinding, then the proof points'); points_out:
- * the proof points' encodings ((terms - 2 n_p - 2) x 32 B). */
-int bpp_perm_verify_scalars(const bpp_verify_job* job, const uint8_t* r_all, size_t total, size_t first,
-                            uint8_t* scalars_out, uint8_t* points_out);
+ * the proof points' encodings ((terms - 2 n_p - 2) x 32 B).  Every proof's
+ * check is scaled by (prod u_j)^2 y^(n_p - 1), so no inverse is formed. */
+int bpp_perm_verify_scalars(const bpp_verify_job* job, const uint8_t seed[32], size_t first, uint8_t* scalars_out,
+                            uint8_t* points_out);
 /* The job's MSM over bucket windows [w_begin, w_end) on this GPU -> 128-B
- * raw partial point.  The batch verifies iff the partials of every window
- * range (window split: every rank's job holds all proofs) or of every proof
- * slice (proof split: all windows each) sum to the identity
- * (bpp_partials_is_identity). */
-int bpp_perm_verify_partial(bpp_ctx* ctx, const bpp_gens* g, const bpp_verify_job* job, const uint8_t* r_all,
-                            size_t total, size_t first, uint32_t w_begin, uint32_t w_end, uint8_t partial[128]);
+ * raw partial point, its proofs being batch proofs [first, first + count)
+ * weighted from `seed` as bpp_perm_verify_scalars.  The batch verifies iff
+ * the partials of every window range (window split: every rank's job holds
+ * all proofs) or of every proof slice (proof split: all windows each, no
+ * exchange before the MSM) sum to the identity (bpp_partials_is_identity). */
+int bpp_perm_verify_partial(bpp_ctx* ctx, const bpp_gens* g, const bpp_verify_job* job, const uint8_t seed[32],
+                            size_t first, uint32_t w_begin, uint32_t w_end, uint8_t partial[128]);
 /* Window split with the per-proof work sharded by proof (config 5 over N
  * GPUs, VERDICT r3: the plain window split replays and expands every proof
  * on every rank).  Rank r of N:
@@ -329,7 +340,7 @@ int bpp_perm_verify_partial(bpp_ctx* ctx, const bpp_gens* g, const bpp_verify_jo
  *      decompresses every proof point (the MSM's window range needs them
  *      all), but replays only proofs [first, first + n), its slice; r_out =
  *      the slice's r challenges (n x 32 B);
- *   2. the r of all slices are all-gathered (r_all, count x 32 B, proof order);
+ *   2. (every rank holds the batch's seed, bpp_verify_seed)
  *   3. bpp_perm_verify_slice_scalars writes the slice's MSM scalars to device
  *      memory d_out (bpp_perm_verify_slice_bytes(job) bytes): the 2 n_p + 2
  *      generator scalars summed over the slice, then the slice's n x
@@ -348,8 +359,7 @@ int bpp_perm_verify_begin_dev_slice(bpp_ctx* ctx, uint32_t k, size_t count, cons
                                     const uint8_t* proofs, const uint8_t* V, size_t first, size_t n, uint8_t* r_out,
                                     bpp_verify_job** out);
 size_t bpp_perm_verify_slice_bytes(const bpp_verify_job* job);
-int bpp_perm_verify_slice_scalars(bpp_ctx* ctx, const bpp_verify_job* job, const uint8_t* r_all, size_t total,
-                                  void* d_out);
+int bpp_perm_verify_slice_scalars(bpp_ctx* ctx, const bpp_verify_job* job, const uint8_t seed[32], void* d_out);
 int bpp_perm_verify_partial_gathered(bpp_ctx* ctx, const bpp_gens* g, const bpp_verify_job* job,
                                      const void* d_blocks, size_t stride, const size_t* counts, size_t nslices,
                                      uint32_t w_begin, uint32_t w_end, uint8_t partial[128]);

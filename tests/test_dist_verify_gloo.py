@@ -1,9 +1,10 @@
 """World-size-2 gloo test of the multi-GPU batch verifier (CPU only).
 
 The product's host phase runs on every rank: bpp_perm_verify_begin parses
-and replays the transcripts of the rank's proofs and returns their weight
-challenges r; the r's are all-gathered; bpp_perm_verify_scalars builds the
-rank's weighted MSM terms.  Only the MSM itself (bpp_perm_verify_partial on
+and replays the transcripts of the rank's proofs; rank 0 draws the batch's
+verifier seed and sends it to every rank (bpperm.dist.shared_seed, the one
+exchange before the partials); bpp_perm_verify_scalars builds the rank's
+weighted MSM terms (every proof's weight mixes the seed with its own r).  Only the MSM itself (bpp_perm_verify_partial on
 a GPU) is replaced here by the oracle, so partition + exchange + combine
 (bpp_partials_is_identity) are checked end to end without a GPU, for both
 splits of SURVEY.md §8(e):
@@ -63,8 +64,8 @@ def _worker(rank, world, port, tamper, q):
         B, Bb = pedersen_gens_default()
         gens = list(G) + list(H) + [B, Bb]
 
-        def partial(job, r_all, first, wb=None, we=None):
-            sc, pts = job.scalars(r_all, first)
+        def partial(job, seed, first, wb=None, we=None):
+            sc, pts = job.scalars(seed, first)
             s_int = [int.from_bytes(x, "little") for x in sc]
             P = gens + [r255.decode(p) for p in pts]
             if wb is None:
@@ -72,19 +73,20 @@ def _worker(rank, world, port, tamper, q):
             c, W = job.windows()
             return r255.raw_point_bytes(r255.msm_window_partial(s_int, P, c, W, wb, we))
 
-        # proof split: this rank's slice, r's exchanged, all windows
+        seed = bdist.shared_seed(rank)
+        assert bdist.torch_all_gather_bytes(seed) == [seed] * world
+        # proof split: this rank's slice, all windows, no exchange before the partials
         b, e = bdist.point_ranges(COUNT, world)[rank]
         job = bpperm.VerifyJob(K, proofs[b:e], Vs[b:e])
         assert job.ok
-        r_all = b"".join(bdist.torch_all_gather_bytes_var(job.r))
-        ok_split = bpperm.partials_is_identity(bdist.torch_all_gather_bytes(partial(job, r_all, b)))
+        ok_split = bpperm.partials_is_identity(bdist.torch_all_gather_bytes(partial(job, seed, b)))
         job.close()
 
         # window split: every proof on every rank, a window range each
         job = bpperm.VerifyJob(K, proofs, Vs)
         c, W = job.windows()
         wb, we = bdist.window_ranges(W, world)[rank]
-        ok_win = bpperm.partials_is_identity(bdist.torch_all_gather_bytes(partial(job, job.r, 0, wb, we)))
+        ok_win = bpperm.partials_is_identity(bdist.torch_all_gather_bytes(partial(job, seed, 0, wb, we)))
         job.close()
         q.put((rank, ok_split, ok_win))
     finally:
@@ -128,11 +130,16 @@ def test_verify_job_host_phase_matches_oracle():
     assert job.ok and len(job.r) == 96
     T = job.terms()
     assert T == 2 * 4 + 2 + 3 * (2 * K + 1 + 8 + 2 * 2)
-    sc, pts = job.scalars(job.r, 0)
     G, H = bulletproof_gens(4)
     B, Bb = pedersen_gens_default()
+    seed = bpperm.verify_seed()
+    sc, pts = job.scalars(seed, 0)
     P = list(G) + list(H) + [B, Bb] + [r255.decode(p) for p in pts]
     assert r255.equal(r255.msm([int.from_bytes(x, "little") for x in sc], P), r255.IDENTITY)
+    # the same job as batch proofs 5..7: other weights, still the identity
+    sc2, _ = job.scalars(seed, 5)
+    assert sc2 != sc
+    assert r255.equal(r255.msm([int.from_bytes(x, "little") for x in sc2], P), r255.IDENTITY)
     job.close()
     # A_I = the identity encoding: validate_and_append_point rejects it
     # (transcript_protocol.rs:48-60); undecodable points fail later, in the

@@ -1,7 +1,8 @@
 """GPU batch verification with the Fiat-Shamir replay on the device
-(bpp_perm_verify_begin_dev / bpp_perm_verify_batch: k_verify_replay, one lane
-per proof; k_verify_weights; reference verify, circuit_lib.rs:478-585;
-transcript_protocol.rs:48-67).
+(bpp_perm_verify_begin_dev / bpp_perm_verify_batch: k_verify_replay_g, one
+16-lane group per proof; k_verify_consts makes each proof's weight from the
+batch's verifier seed and its own r; no inverses, no host round trip;
+reference verify, circuit_lib.rs:478-585; transcript_protocol.rs:48-67).
 
 Parity: every proof's r challenge from the device replay is byte-equal to the
 host replay (host/merlin.h, itself KAT-pinned against merlin 3.0.0), and a
@@ -29,10 +30,13 @@ def setup(ctx):
     g.close()
 
 
-def _window_partials(pr, job, ranks):
+SEED = bytes(range(32))  # (a fixed verifier seed: tests compare partials across jobs)
+
+
+def _window_partials(pr, job, ranks, seed=SEED):
     from bpperm.dist import window_ranges
     c, W = job.windows()
-    return [pr.verify_partial(job, job.r, 0, wb, we) for wb, we in window_ranges(W, ranks)]
+    return [pr.verify_partial(job, seed, 0, wb, we) for wb, we in window_ranges(W, ranks)]
 
 
 def test_device_r_equals_host_r(setup, ctx):
@@ -122,7 +126,7 @@ def test_device_rejects(setup, ctx):
     assert not pr.verify(ud[60], Vs[60])
     uj = bpperm.VerifyJob(K, ud, Vs, ctx=ctx)
     assert uj.ok  # (the replay absorbs the bytes; the decompression beside it rejects)
-    assert pr.verify_partial(uj, uj.r, 0, 0, uj.windows()[1]) is None
+    assert pr.verify_partial(uj, SEED, 0, 0, uj.windows()[1]) is None
     uj.close()
     # the untampered batch still verifies on the same context afterwards
     assert pr.verify_batch(proofs, Vs)
@@ -141,7 +145,7 @@ def test_device_proof_split(setup, ctx):
                 for (b, e), c in zip(point_ranges(len(bad), 4), ctxs)]
         r_all = b"".join(j.r for _, j in jobs)
         prs = [bpperm.PermProver(gens, K, ctx=c) for c in ctxs]
-        parts = [p.verify_partial(j, r_all, b, 0, j.windows()[1]) for p, (b, j) in zip(prs, jobs)]
+        parts = [p.verify_partial(j, SEED, b, 0, j.windows()[1]) for p, (b, j) in zip(prs, jobs)]
         whole = bpperm.VerifyJob(K, bad, Vs, ctx=ctx)
         assert whole.r == r_all
         wparts = _window_partials(pr, whole, 8)
@@ -161,8 +165,8 @@ def test_superseded_device_job_is_refused(setup, ctx):
     j1 = bpperm.VerifyJob(K, proofs[:8], Vs[:8], ctx=ctx)
     j2 = bpperm.VerifyJob(K, proofs[8:16], Vs[8:16], ctx=ctx)
     with pytest.raises(BppError):
-        pr.verify_partial(j1, j1.r, 0, 0, j1.windows()[1])
-    assert bpperm.partials_is_identity([pr.verify_partial(j2, j2.r, 0, 0, j2.windows()[1])])
+        pr.verify_partial(j1, SEED, 0, 0, j1.windows()[1])
+    assert bpperm.partials_is_identity([pr.verify_partial(j2, SEED, 0, 0, j2.windows()[1])])
     j1.close()
     j2.close()
 
@@ -222,3 +226,24 @@ def test_prover_scratch_keyed_on_generators(ctx):
         assert pr.verify_batch(proofs, Vs)
     g1.close()
     g2.close()
+
+
+def test_weights_follow_the_seed(setup, ctx):
+    """The batch weights come from the verifier's seed (and each proof's own
+    r): an honest batch verifies under any seed, a tampered one under none
+    of several, and two seeds give different partials for the same window
+    range (the weights are not fixed by the proofs)."""
+    import bpperm
+    _, pr, proofs, Vs = setup
+    dj = bpperm.VerifyJob(K, proofs, Vs, ctx=ctx)
+    s1, s2 = bpperm.verify_seed(), bpperm.verify_seed()
+    assert s1 != s2
+    p1, p2 = _window_partials(pr, dj, 2, s1), _window_partials(pr, dj, 2, s2)
+    assert bpperm.partials_is_identity(p1) and bpperm.partials_is_identity(p2)
+    assert bpperm.partials_finish(p1[:1]) != bpperm.partials_finish(p2[:1])
+    dj.close()
+    bad = _tampered(proofs, 9, 8 * 32 + 70, 1)
+    bj = bpperm.VerifyJob(K, bad, Vs, ctx=ctx)
+    for _ in range(3):
+        assert not bpperm.partials_is_identity(_window_partials(pr, bj, 2, bpperm.verify_seed()))
+    bj.close()

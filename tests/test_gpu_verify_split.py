@@ -2,8 +2,8 @@
 verifier MSM partitions its bucket windows across GPUs"; config 5 shape).
 
 On one GPU the batch's single MSM is split as several ranks would split it:
-8 window ranges (every "rank" holds every proof) and 4 proof slices (r
-challenges exchanged, all windows each).  The partials must add up to the
+8 window ranges (every "rank" holds every proof) and 4 proof slices (all
+windows each, nothing exchanged but the batch's verifier seed).  The partials must add up to the
 identity exactly when bpp_perm_verify_batch accepts, the partial sums of both
 splits must be the same group element, and a tampered proof must be rejected
 by every split.  Reference: verify, circuit_lib.rs:478-585."""
@@ -12,6 +12,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 K = 52
+SEED = bytes(range(100, 132))  # (a fixed verifier seed: tests compare partials across splits)
 
 
 @pytest.fixture(scope="module")
@@ -30,7 +31,7 @@ def _window_partials(pr, proofs, Vs, ranks):
     job = bpperm.VerifyJob(K, proofs, Vs)
     assert job.ok
     c, W = job.windows()
-    parts = [pr.verify_partial(job, job.r, 0, wb, we) for wb, we in window_ranges(W, ranks)]
+    parts = [pr.verify_partial(job, SEED, 0, wb, we) for wb, we in window_ranges(W, ranks)]
     job.close()
     return parts
 
@@ -39,8 +40,7 @@ def _proof_partials(pr, proofs, Vs, ranks):
     import bpperm
     from bpperm.dist import point_ranges
     jobs = [(b, bpperm.VerifyJob(K, proofs[b:e], Vs[b:e])) for b, e in point_ranges(len(proofs), ranks)]
-    r_all = b"".join(j.r for _, j in jobs)
-    parts = [pr.verify_partial(j, r_all, b, 0, j.windows()[1]) for b, j in jobs]
+    parts = [pr.verify_partial(j, SEED, b, 0, j.windows()[1]) for b, j in jobs]
     for _, j in jobs:
         j.close()
     return parts
@@ -104,7 +104,7 @@ def _window_partials_k(pr, proofs, Vs, k, ranks):
     import bpperm
     from bpperm.dist import window_ranges
     job = bpperm.VerifyJob(k, proofs, Vs)
-    parts = [pr.verify_partial(job, job.r, 0, wb, we) for wb, we in window_ranges(job.windows()[1], ranks)]
+    parts = [pr.verify_partial(job, SEED, 0, wb, we) for wb, we in window_ranges(job.windows()[1], ranks)]
     job.close()
     return parts
 
@@ -142,12 +142,11 @@ def test_device_scalars_match_host_expansion(setup, ctx):
     bad[9] = bytes(b)
     job = bpperm.VerifyJob(K, bad[:24], Vs[:24])
     first = 5
-    # the job as a slice [first, first + 24) of a larger batch: the weights
-    # come from every r (the others' stand-ins are small canonical scalars)
-    r_all = b"".join(bytes([(i * 7 + 1) % 251]) + bytes(31) for i in range(first)) + job.r
+    # the job as a slice [first, first + 24) of a larger batch: proof p's
+    # weight mixes the seed, its batch index first + p and its own r
     c, W = job.windows()
-    got = bpperm.partials_finish([pr.verify_partial(job, r_all, first, 0, W)])
-    sc, pts = job.scalars(r_all, first)
+    got = bpperm.partials_finish([pr.verify_partial(job, SEED, first, 0, W)])
+    sc, pts = job.scalars(SEED, first)
     G, H, B, Bb = gens.export()  # n = n_p = 128: G[0..n_p), H[0..n_p), B, B_blinding
     want = cport.msm(b"".join(sc), b"".join(list(G) + list(H) + [B, Bb] + pts))
     assert got == want and got != bytes(32)
@@ -170,13 +169,12 @@ def _sliced_partials(g, proofs, Vs, ranks, tamper_rank=None):
     try:
         if not all(j.ok for j in jobs):
             return None
-        r_all = b"".join(j.r for j in jobs)
         stride = (bdist._slice_block_bytes(K, max(counts)) + 15) // 16 * 16
         blocks = ctxs[0].dev_alloc(ranks * stride)
         ctxs[0].htod(blocks, bytes(ranks * stride))
         for r, j in enumerate(jobs):
             assert j.slice_bytes() == bdist._slice_block_bytes(K, counts[r])
-            j.slice_scalars(r_all, blocks + r * stride)
+            j.slice_scalars(SEED, blocks + r * stride)
         if tamper_rank is not None:  # one rank's generator block perturbed after the fact
             at = blocks + tamper_rank * stride
             b0 = bytearray(ctxs[0].dtoh(at, 16))
@@ -198,7 +196,8 @@ def test_sharded_window_split(setup, ranks, n):
     by proof.  The ranks' window partials add up to the identity exactly when
     the batch verifies, and to the same element as the plain window split's;
     a tampered proof or a perturbed scalar block is rejected; a sliced job is
-    refused by bpp_perm_verify_partial."""
+    refused by bpp_perm_verify_partial; blocks gathered out of slice order are
+    refused."""
     import bpperm
     g, pr, proofs, Vs = setup
     if n > len(proofs):
@@ -223,5 +222,31 @@ def test_sharded_window_split(setup, ranks, n):
     assert not bpperm.partials_is_identity(_sliced_partials(g, proofs, Vs, ranks, tamper_rank=ranks - 1))
     job = bpperm.VerifyJob(K, proofs, Vs, pr.label, ctx=pr.ctx, replay=(0, n // 2))
     with pytest.raises(bpperm.BppError):
-        pr.verify_partial(job, job.r, 0, 0, 1)
+        pr.verify_partial(job, SEED, 0, 0, 1)
     job.close()
+
+
+def test_gathered_blocks_out_of_order_refused(setup):
+    """bpp_perm_verify_partial_gathered checks that the job's own
+    slice sits at its proof offset among the gathered blocks: counts listed
+    in another order are an argument error, not a silent rejection."""
+    import bpperm
+    from bpperm import dist as bdist
+    g, pr, proofs, Vs = setup
+    ranges = bdist.point_ranges(len(proofs), 3)
+    counts = [e - b for b, e in ranges]
+    assert counts == [21, 21, 22]
+    b, e = ranges[0]
+    job = bpperm.VerifyJob(K, proofs, Vs, pr.label, ctx=pr.ctx, replay=(b, e - b))
+    stride = (bdist._slice_block_bytes(K, max(counts)) + 15) // 16 * 16
+    blocks = pr.ctx.dev_alloc(3 * stride)
+    try:
+        pr.ctx.htod(blocks, bytes(3 * stride))
+        job.slice_scalars(SEED, blocks)
+        W = job.windows()[1]
+        # the job's slice is proofs [0, 21); counts [22, 21, 21] put 22 there
+        with pytest.raises(bpperm.BppError):
+            pr.verify_partial_gathered(job, blocks, stride, counts[::-1], 0, W)
+    finally:
+        pr.ctx.dev_free(blocks)
+        job.close()

@@ -520,6 +520,17 @@ class PermProver:
         check(rc, "bpp_perm_verify_batch", self.ctx.h)
         return True
 
+    def verify_batch_ptr(self, proofs_ptr: int, V_ptr: int, count: int) -> bool:
+        """verify_batch over `count` proofs and their V already in host
+        memory at two addresses -- e.g. pinned buffers from
+        Context.host_alloc, which go up by DMA without the staging copy."""
+        rc = self.ctx.lib.bpp_perm_verify_batch(self.ctx.h, self.gens.h, self.k, count, _buf(self.label),
+                                                len(self.label), C.c_void_p(proofs_ptr), C.c_void_p(V_ptr))
+        if rc == 6:
+            return False
+        check(rc, "bpp_perm_verify_batch", self.ctx.h)
+        return True
+
     def verify_job(self, proofs: Sequence[bytes], Vs: Sequence[bytes], device: bool = True) -> "VerifyJob":
         """Replay phase of a batch verification that may be split over GPUs:
         on this prover's context (device=True, bpp_perm_verify_begin_dev) or

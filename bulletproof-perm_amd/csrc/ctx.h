@@ -85,6 +85,10 @@ struct bpp_ctx {
   // one event per upload chunk (verify_begin_dev: each chunk's points are
   // decompressed as soon as its copy lands)
   std::vector<hipEvent_t> vj_ev_chunk;
+  // the split replay (BPP_VERIFY_SPLIT): the proof-byte chunks' events, and
+  // the end of the V-part replays on their child stream
+  std::vector<hipEvent_t> vj_ev_chunk2;
+  hipEvent_t vj_ev_vrep = nullptr;
   // bpp_msm_submit_host: the uploaded scalars of this (child) context's MSM,
   // copied on the parent's upload streams (up_stream, created on first use;
   // one per chunk of the copy) and signalled to this context's stream by

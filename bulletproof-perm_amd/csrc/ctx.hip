@@ -411,6 +411,8 @@ void bpp_ctx_destroy(bpp_ctx* ctx) {
   if (ctx->vj_ev_in) hipEventDestroy(ctx->vj_ev_in);
   if (ctx->vj_ev_dec) hipEventDestroy(ctx->vj_ev_dec);
   for (auto e : ctx->vj_ev_chunk) hipEventDestroy(e);
+  for (auto e : ctx->vj_ev_chunk2) hipEventDestroy(e);
+  if (ctx->vj_ev_vrep) hipEventDestroy(ctx->vj_ev_vrep);
   for (auto& sl : ctx->msm_slot)
     if (sl.done) hipEventDestroy(sl.done);
   hipStreamDestroy(ctx->stream);

@@ -16,6 +16,12 @@
 // challenge on the host, and the scalar fold (k_ipa_fold).  L, R, a, b are
 // identical group elements / scalars to the folding form (same transcript).
 #include <cstdlib>
+#include <chrono>
+#include <thread>
+#include <condition_variable>
+#include <mutex>
+#include <memory>
+#include <map>
 #include <functional>
 #include <cstring>
 
@@ -222,22 +228,45 @@ __global__ void __launch_bounds__(64) k_ipa_final(uint32_t P, uint32_t n, const 
 // and their passes over the [P][n] arrays leave every round of a batch.
 // (512-lane blocks, half the walk per lane: 73.9 vs 70.8 us per round -- a
 // lone wave per SIMD already issues the walk at its rate)
-__global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
-    const uint32_t* __restrict__ dt, DtGeom dg, uint32_t n, uint32_t m, uint32_t lg_h, uint32_t fold,
-    const uint32_t* __restrict__ am_in, const uint32_t* __restrict__ bm_in, const uint32_t* __restrict__ fG_in,
-    const uint32_t* __restrict__ fH_in, uint32_t* __restrict__ am_out, uint32_t* __restrict__ bm_out,
-    uint32_t* __restrict__ fG_out, uint32_t* __restrict__ fH_out, const uint32_t* __restrict__ u,
-    const uint32_t* __restrict__ qmul, uint32_t gbase, uint32_t hbase, uint32_t qidx, uint32_t TG, uint32_t halve,
-    uint32_t* __restrict__ out_p3, const uint32_t* __restrict__ a0, const uint32_t* __restrict__ b0,
-    const uint32_t* __restrict__ gf0, const uint32_t* __restrict__ hf0, uint32_t init) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+// One batch's round as the fused kernel sees it (k_ipa_round_dt's
+// arguments; k_ipa_round_dt_multi runs several batches' rounds in one launch).
+struct IpaRoundArgs {
+  const uint32_t *am_in, *bm_in, *fG_in, *fH_in;
+  uint32_t *am_out, *bm_out, *fG_out, *fH_out;
+  const uint32_t *u, *qmul;
+  uint32_t* out_p3;
+  const uint32_t *a0, *b0, *gf0, *hf0;
+  uint32_t m, lg_h, fold, init, halve, gbase, hbase, qidx;
+  uint32_t blocks;  // 2 P (k_ipa_round_dt_multi)
+  uint32_t pad_;
+};
+
+FE_INLINE void ipa_round_body(const uint32_t* __restrict__ dt, const DtGeom& dg, uint32_t n, uint32_t TG,
+                              const IpaRoundArgs& A, uint32_t bidx, uint32_t* lds) {
+  const uint32_t m = A.m, lg_h = A.lg_h, fold = A.fold, init = A.init, halve = A.halve, gbase = A.gbase,
+                 hbase = A.hbase, qidx = A.qidx;
+  const uint32_t* __restrict__ am_in = A.am_in;
+  const uint32_t* __restrict__ bm_in = A.bm_in;
+  const uint32_t* __restrict__ fG_in = A.fG_in;
+  const uint32_t* __restrict__ fH_in = A.fH_in;
+  uint32_t* __restrict__ am_out = A.am_out;
+  uint32_t* __restrict__ bm_out = A.bm_out;
+  uint32_t* __restrict__ fG_out = A.fG_out;
+  uint32_t* __restrict__ fH_out = A.fH_out;
+  const uint32_t* __restrict__ u = A.u;
+  const uint32_t* __restrict__ qmul = A.qmul;
+  uint32_t* __restrict__ out_p3 = A.out_p3;
+  const uint32_t* __restrict__ a0 = A.a0;
+  const uint32_t* __restrict__ b0 = A.b0;
+  const uint32_t* __restrict__ gf0 = A.gf0;
+  const uint32_t* __restrict__ hf0 = A.hf0;
   uint32_t* tsc = lds;                           // (n + 1) x 8 words: halved term scalars
   uint32_t* tgen = lds + 8 * (n + 1);            // n + 1 generator indices
   uint32_t* sa = tgen + ((n + 1 + 3) & ~3u);     // m x 8: a (Montgomery), this round
   uint32_t* sb = sa + 8 * m;                     // m x 8: b
   uint32_t* red = sb + 8 * m;                    // waves x 8 words
   const uint32_t nt = blockDim.x, tid = threadIdx.x;
-  const uint32_t inst = blockIdx.x >> 1, side = blockIdx.x & 1u;
+  const uint32_t inst = bidx >> 1, side = bidx & 1u;
   const size_t ib = (size_t)inst * n;
   // init (the first round, no fold): a, b and the generator factors come
   // from the caller's canonical arrays a0, b0, gf0, hf0 (null: all one), and
@@ -325,7 +354,7 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
   const uint32_t tg = tid / dg.W;
   const DtLane ln = DtLane::make(dg, tid % dg.W);
 #ifdef EXP_IPA_NOWALK  // timing experiment only (wrong results): no walk, no tree
-  if (tid == 0) store_p3(out_p3, blockIdx.x, ge_identity());
+  if (tid == 0) store_p3(out_p3, bidx, ge_identity());
   return;
 #endif
   const ge_p3 acc = tg < TG ? dt_walk(dt, dg, ln, tg, n + 1, TG,
@@ -337,11 +366,164 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
                             : ge_identity();
   __syncthreads();
 #ifdef EXP_IPA_NOTREE  // timing experiment only (wrong results): no block tree
-  if (tid == 0) store_p3(out_p3, blockIdx.x, acc);
+  if (tid == 0) store_p3(out_p3, bidx, acc);
   return;
 #endif
-  dt_block_tree(lds, acc, nt, out_p3, blockIdx.x);
+  dt_block_tree(lds, acc, nt, out_p3, bidx);
 }
+
+__global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
+    const uint32_t* __restrict__ dt, DtGeom dg, uint32_t n, uint32_t m, uint32_t lg_h, uint32_t fold,
+    const uint32_t* __restrict__ am_in, const uint32_t* __restrict__ bm_in, const uint32_t* __restrict__ fG_in,
+    const uint32_t* __restrict__ fH_in, uint32_t* __restrict__ am_out, uint32_t* __restrict__ bm_out,
+    uint32_t* __restrict__ fG_out, uint32_t* __restrict__ fH_out, const uint32_t* __restrict__ u,
+    const uint32_t* __restrict__ qmul, uint32_t gbase, uint32_t hbase, uint32_t qidx, uint32_t TG, uint32_t halve,
+    uint32_t* __restrict__ out_p3, const uint32_t* __restrict__ a0, const uint32_t* __restrict__ b0,
+    const uint32_t* __restrict__ gf0, const uint32_t* __restrict__ hf0, uint32_t init) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  IpaRoundArgs A;
+  A.am_in = am_in; A.bm_in = bm_in; A.fG_in = fG_in; A.fH_in = fH_in;
+  A.am_out = am_out; A.bm_out = bm_out; A.fG_out = fG_out; A.fH_out = fH_out;
+  A.u = u; A.qmul = qmul; A.out_p3 = out_p3;
+  A.a0 = a0; A.b0 = b0; A.gf0 = gf0; A.hf0 = hf0;
+  A.m = m; A.lg_h = lg_h; A.fold = fold; A.init = init; A.halve = halve;
+  A.gbase = gbase; A.hbase = hbase; A.qidx = qidx;
+  ipa_round_body(dt, dg, n, TG, A, blockIdx.x, lds);
+}
+
+// Several batches' rounds in one launch (BPP_IPA_MERGE, the shared-launch
+// round scheduler below): block b runs block b - prefix of batch j.  args:
+// nargs structs in pinned host memory, read once per block into LDS.
+#define IPA_MERGE_MAX 16
+__global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt_multi(const uint32_t* __restrict__ dt, DtGeom dg,
+                                                                 uint32_t n, uint32_t TG,
+                                                                 const IpaRoundArgs* __restrict__ args,
+                                                                 uint32_t nargs) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ IpaRoundArgs sA;
+  __shared__ uint32_t sb;
+  if (threadIdx.x == 0) {
+    uint32_t b = blockIdx.x, j = 0;
+    while (j + 1 < nargs && b >= args[j].blocks) b -= args[j++].blocks;
+    sA = args[j];
+    sb = b;
+  }
+  __syncthreads();
+  ipa_round_body(dt, dg, n, TG, sA, sb, lds);
+}
+
+// The shared-launch round scheduler (BPP_IPA_MERGE=1; an
+// A/B switch): the batches in flight on one device hand their fused IPA
+// rounds to one merger, which issues ONE k_ipa_round_dt_multi over every
+// round pending at the time on its own stream, after each batch's stream has
+// reached the round (an event per request).  Combining: the first thread to
+// arrive leads -- it waits BPP_IPA_MERGE_US (default 0) for others, takes
+// every pending request with the same shape (n, TG, tables), launches, and
+// wakes them; each then waits for the launch's event.  A batch's round thus
+// runs as part of a larger grid (more waves per SIMD for the latency-bound
+// walk and tree) instead of on its own queue beside the others.
+namespace {
+struct IpaMergeReq {
+  IpaRoundArgs a;
+  hipEvent_t ready = nullptr;  // recorded on the batch's stream
+  const uint32_t* dt = nullptr;
+  DtGeom dg;
+  uint32_t n = 0, TG = 0, nt = 0;
+  size_t lds = 0;
+  uint64_t gen = 0;            // set when launched
+  hipEvent_t done = nullptr;   // the launch's completion
+  int err = BPP_OK;
+};
+struct IpaMerger {
+  std::mutex mu;
+  std::condition_variable cv;
+  bool leading = false;
+  uint64_t gen = 0;
+  std::vector<IpaMergeReq*> pending;
+  hipStream_t stream = nullptr;
+  static constexpr int RING = 64;
+  IpaRoundArgs* ring = nullptr;  // pinned: RING x IPA_MERGE_MAX argument blocks
+  hipEvent_t ring_ev[RING] = {};
+  bool ring_used[RING] = {};
+  int ring_pos = 0;
+  uint64_t launches = 0, rounds = 0;
+};
+IpaMerger& ipa_merger(int dev) {
+  static std::mutex mu;
+  static std::map<int, std::unique_ptr<IpaMerger>> all;
+  std::lock_guard<std::mutex> g(mu);
+  auto& p = all[dev];
+  if (!p) p.reset(new IpaMerger);
+  return *p;
+}
+bool same_shape(const IpaMergeReq& a, const IpaMergeReq& b) {
+  return a.dt == b.dt && a.n == b.n && a.TG == b.TG && a.nt == b.nt && a.dg.c == b.dg.c;
+}
+// the leader's launch of `reqs` (same shape); sets their gen / done
+int merger_launch(bpp_ctx* ctx, IpaMerger& M, std::vector<IpaMergeReq*>& reqs) {
+  if (!M.stream) BPP_HIP(hipStreamCreateWithFlags(&M.stream, hipStreamNonBlocking));
+  if (!M.ring) BPP_HIP(hipHostMalloc((void**)&M.ring, sizeof(IpaRoundArgs) * IPA_MERGE_MAX * IpaMerger::RING));
+  const int slot = M.ring_pos;
+  M.ring_pos = (M.ring_pos + 1) % IpaMerger::RING;
+  if (!M.ring_ev[slot]) BPP_HIP(hipEventCreateWithFlags(&M.ring_ev[slot], hipEventDisableTiming));
+  if (M.ring_used[slot]) BPP_HIP(hipEventSynchronize(M.ring_ev[slot]));  // (its last launch has read the slot)
+  IpaRoundArgs* args = M.ring + (size_t)slot * IPA_MERGE_MAX;
+  uint32_t blocks = 0;
+  for (size_t i = 0; i < reqs.size(); ++i) {
+    args[i] = reqs[i]->a;
+    blocks += reqs[i]->a.blocks;
+    BPP_HIP(hipStreamWaitEvent(M.stream, reqs[i]->ready, 0));
+  }
+  const IpaMergeReq& r0 = *reqs[0];
+  hipLaunchKernelGGL(k_ipa_round_dt_multi, dim3(blocks), dim3(r0.nt), r0.lds, M.stream, r0.dt, r0.dg, r0.n, r0.TG,
+                     (const IpaRoundArgs*)args, (uint32_t)reqs.size());
+  BPP_HIP(hipGetLastError());
+  BPP_HIP(hipEventRecord(M.ring_ev[slot], M.stream));
+  M.ring_used[slot] = true;
+  ++M.launches;
+  M.rounds += reqs.size();
+  for (IpaMergeReq* r : reqs) r->done = M.ring_ev[slot];
+  return BPP_OK;
+}
+// Blocks until the request's round has been launched; returns the event to
+// wait for (or an error).
+int merger_submit(bpp_ctx* ctx, IpaMergeReq& req) {
+  IpaMerger& M = ipa_merger(ctx->device);
+  static const int wait_us = [] {
+    const char* e = getenv("BPP_IPA_MERGE_US");
+    return e ? std::max(0, atoi(e)) : 0;
+  }();
+  std::unique_lock<std::mutex> lk(M.mu);
+  M.pending.push_back(&req);
+  for (;;) {
+    if (req.gen) return req.err;
+    if (!M.leading) break;
+    M.cv.wait(lk);
+  }
+  // lead: gather, launch every pending request of this shape, wake them
+  M.leading = true;
+  if (wait_us > 0) {
+    lk.unlock();
+    std::this_thread::sleep_for(std::chrono::microseconds(wait_us));
+    lk.lock();
+  }
+  std::vector<IpaMergeReq*> take{&req}, keep;  // (the leader's own request first)
+  for (IpaMergeReq* r : M.pending)
+    if (r != &req) (same_shape(*r, req) && take.size() < IPA_MERGE_MAX ? take : keep).push_back(r);
+  M.pending.swap(keep);
+  lk.unlock();
+  const int rc = merger_launch(ctx, M, take);
+  lk.lock();
+  const uint64_t g = ++M.gen;
+  for (IpaMergeReq* r : take) {
+    r->gen = g;
+    r->err = rc;
+  }
+  M.leading = false;
+  M.cv.notify_all();
+  return req.err;
+}
+}  // namespace
 
 // LDS words of k_ipa_round_dt: terms + indices + a, b + wave partials, or
 // the block tree, whichever is larger
@@ -460,6 +642,12 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
 #else
   const bool zc = fused && !dev_merlin;
 #endif
+  // the shared-launch round scheduler (A/B switch, off by default)
+  static const bool merge_env = [] {
+    const char* e = getenv("BPP_IPA_MERGE");
+    return e && atoi(e) != 0;
+  }();
+  const bool merge = merge_env && zc;
   uint32_t* h_uw = nullptr;  // zc: the challenges' device words, in place
   if (zc) {
     void *hr = nullptr, *hu = nullptr;
@@ -485,7 +673,31 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
     const uint32_t h = m >> 1;
     if (fused) {
       const int in = cur, outs = cur ^ 1;
-      {
+      if (merge) {  // one launch with the other batches' pending rounds (the merger's stream)
+        static thread_local hipEvent_t ready = nullptr;
+        if (!ready) BPP_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+        IpaMergeReq req;
+        IpaRoundArgs& A = req.a;
+        A.am_in = S[in][0]; A.bm_in = S[in][1]; A.fG_in = S[in][2]; A.fH_in = S[in][3];
+        A.am_out = S[round ? outs : in][0]; A.bm_out = S[round ? outs : in][1];
+        A.fG_out = S[round ? outs : in][2]; A.fH_out = S[round ? outs : in][3];
+        A.u = (const uint32_t*)d_u; A.qmul = (const uint32_t*)d_q; A.out_p3 = (uint32_t*)d_res;
+        A.a0 = d_a; A.b0 = d_b; A.gf0 = d_Gf; A.hf0 = d_Hf;
+        A.m = m; A.lg_h = lg_h; A.fold = round ? 1u : 0u; A.init = round ? 0u : 1u; A.halve = 1u;
+        A.gbase = g.gbase; A.hbase = g.hbase; A.qidx = g.qidx;
+        A.blocks = 2 * P;
+        A.pad_ = 0;
+        req.dt = g.pts.dt;
+        req.dg = dg;
+        req.n = n;
+        req.TG = TG;
+        req.nt = nt;
+        req.lds = ipa_round_lds_words(n, nt) * 4;
+        BPP_HIP(hipEventRecord(ready, ctx->stream));
+        req.ready = ready;
+        BPP_TRY(merger_submit(ctx, req));
+        BPP_HIP(hipStreamWaitEvent(ctx->stream, req.done, 0));  // (ctx_sync below then covers the round)
+      } else {
         ProfScope ps(ctx, "ipa_round_dt");  // (bench.py: this kernel's own roofline)
         hipLaunchKernelGGL(k_ipa_round_dt, dim3(2 * P), dim3(nt), ipa_round_lds_words(n, nt) * 4, ctx->stream,
                            g.pts.dt, dg, n, m, lg_h, round ? 1u : 0u, S[in][0], S[in][1], S[in][2], S[in][3],

@@ -1118,9 +1118,89 @@ int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label,
     ctx->vj_dec_pending = true;
     return BPP_OK;
   };
+  // BPP_VERIFY_SPLIT=1 (whole jobs): the V bytes of every chunk go up first
+  // and each chunk's transcripts run their V part (2k V appends, x_perm,
+  // V_2k: ~60 % of a transcript's permutations) on a second child stream as
+  // soon as its V bytes land, while the proof bytes are still being copied;
+  // the proof part follows the last copy.  Each chunk's V points and then its
+  // proof points are decompressed as they land.
+  static const bool split_env = [] {
+    const char* e = getenv("BPP_VERIFY_SPLIT");
+    return e && atoi(e) != 0;
+  }();
+  const bool split = split_env && dec_order == 0 && rfirst == 0 && rcount == count && count >= 256;
+  uint32_t* d_stt = nullptr;
+  uint32_t* h_init = nullptr;  // the shared transcript prefix, read in place (zero copy)
+  if (split) {
+    void* d = nullptr;
+    BPP_TRY(ctx_ws(ctx, "vj_stt", count * 52 * 4, &d));
+    d_stt = (uint32_t*)d;
+  }
   {
     HostScope hs(ctx, "verify_upload");
-    if (dec_order == 0) {
+    if (split) {
+      bpp_ctx* kv = nullptr;
+      BPP_TRY(ctx_child(ctx, VJ_CHILD + 1, &kv));
+      {
+        uint32_t init[52];
+        verify_init_state(C, label, llen, init);
+        BPP_TRY(ctx_zc_in(ctx, "vj_init", init, sizeof init, &h_init));
+      }
+      static const size_t nchunk_env = [] {
+        const char* e = getenv("BPP_VERIFY_CHUNKS");
+        return (size_t)std::max(1, e ? atoi(e) : 4);
+      }();
+      const size_t nchunk = std::min(nchunk_env, std::max<size_t>(1, count / 256));
+      for (auto* evs : {&ctx->vj_ev_chunk, &ctx->vj_ev_chunk2})
+        while (evs->size() < nchunk) {
+          hipEvent_t e = nullptr;
+          BPP_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+          evs->push_back(e);
+        }
+      if (!ctx->vj_ev_vrep) BPP_HIP(hipEventCreateWithFlags(&ctx->vj_ev_vrep, hipEventDisableTiming));
+      auto is_pinned = [](const void* h) {
+        hipPointerAttribute_t at;
+        const bool pin = hipPointerGetAttributes(&at, h) == hipSuccess && at.type == hipMemoryTypeHost;
+        (void)hipGetLastError();
+        return pin;
+      };
+      const bool direct = is_pinned(proofs) && is_pinned(V);
+      uint8_t* stg = nullptr;
+      if (!direct) BPP_TRY(ctx_h2d_stage(ctx, count * (plen + vbytes), &stg));
+      auto up = [&](size_t off, const uint8_t* src, size_t n) -> int {
+        if (direct) {
+          BPP_HIP(hipMemcpyAsync((uint8_t*)d_in + off, src, n, hipMemcpyHostToDevice, ctx->stream));
+        } else {
+          ctx_stage_copy(stg + off, src, n);
+          BPP_TRY(ctx_h2d_staged(ctx, (uint8_t*)d_in + off, stg + off, n));
+        }
+        return BPP_OK;
+      };
+      const uint32_t m = C.m, npt = (uint32_t)J.npt;
+      for (size_t q = 0; q < nchunk; ++q) {  // V bytes, V-part replays, V points
+        const size_t p0 = count * q / nchunk, p1 = count * (q + 1) / nchunk;
+        BPP_TRY(up(count * plen + p0 * vbytes, V + p0 * vbytes, (p1 - p0) * vbytes));
+        BPP_HIP(hipEventRecord(ctx->vj_ev_chunk[q], ctx->stream));
+        BPP_HIP(hipStreamWaitEvent(kv->stream, ctx->vj_ev_chunk[q], 0));
+        BPP_TRY(verify_replay_v_dev(ctx, kv->stream, C, (uint32_t)p0, (uint32_t)p1, (uint32_t)count, h_init, d_V,
+                                    d_stt));
+        BPP_HIP(hipStreamWaitEvent(kid->stream, ctx->vj_ev_chunk[q], 0));
+        BPP_TRY(verify_decompress_dev(kid, C, (uint32_t)count, d_pf, d_V, (uint32_t*)d_x, (unsigned long long*)d_dbad,
+                                      (uint32_t)p0, (uint32_t)p1, 0, m));
+      }
+      BPP_HIP(hipEventRecord(ctx->vj_ev_vrep, kv->stream));
+      for (size_t q = 0; q < nchunk; ++q) {  // proof bytes, proof points
+        const size_t p0 = count * q / nchunk, p1 = count * (q + 1) / nchunk;
+        BPP_TRY(up(p0 * plen, proofs + p0 * plen, (p1 - p0) * plen));
+        BPP_HIP(hipEventRecord(ctx->vj_ev_chunk2[q], ctx->stream));
+        BPP_HIP(hipStreamWaitEvent(kid->stream, ctx->vj_ev_chunk2[q], 0));
+        BPP_TRY(verify_decompress_dev(kid, C, (uint32_t)count, d_pf, d_V, (uint32_t*)d_x, (unsigned long long*)d_dbad,
+                                      (uint32_t)p0, (uint32_t)p1, m, npt - m));
+      }
+      BPP_HIP(hipEventRecord(ctx->vj_ev_dec, kid->stream));
+      ctx->vj_dec_pending = true;
+      BPP_HIP(hipStreamWaitEvent(ctx->stream, ctx->vj_ev_vrep, 0));
+    } else if (dec_order == 0) {
       // The proofs and V go up in chunks of proofs (each chunk's proof bytes
       // and V bytes to their places in the [proofs][V] layout), and each
       // chunk's points are decompressed on the child stream as soon as its
@@ -1138,15 +1218,31 @@ int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label,
         BPP_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         ctx->vj_ev_chunk.push_back(e);
       }
+      // proofs and V already in pinned host memory (bpp_host_alloc, or
+      // registered by the caller) go up by DMA from where they are; pageable
+      // buffers are staged through the pinned arena first (the host copy
+      // then paces the upload)
+      auto pinned = [](const void* h) {
+        hipPointerAttribute_t at;
+        const bool pin = hipPointerGetAttributes(&at, h) == hipSuccess && at.type == hipMemoryTypeHost;
+        (void)hipGetLastError();  // (a pageable pointer leaves an error code behind)
+        return pin;
+      };
+      const bool direct = pinned(proofs) && pinned(V);
       uint8_t* stg = nullptr;
-      BPP_TRY(ctx_h2d_stage(ctx, count * (plen + vbytes), &stg));
+      if (!direct) BPP_TRY(ctx_h2d_stage(ctx, count * (plen + vbytes), &stg));
       for (size_t q = 0; q < nchunk; ++q) {
         const size_t p0 = count * q / nchunk, p1 = count * (q + 1) / nchunk;
         const size_t po = p0 * plen, pn = (p1 - p0) * plen, vo = count * plen + p0 * vbytes, vn = (p1 - p0) * vbytes;
-        ctx_stage_copy(stg + po, proofs + po, pn);
-        BPP_TRY(ctx_h2d_staged(ctx, (uint8_t*)d_in + po, stg + po, pn));
-        ctx_stage_copy(stg + vo, V + p0 * vbytes, vn);
-        BPP_TRY(ctx_h2d_staged(ctx, (uint8_t*)d_in + vo, stg + vo, vn));
+        if (direct) {
+          BPP_HIP(hipMemcpyAsync((uint8_t*)d_in + po, proofs + po, pn, hipMemcpyHostToDevice, ctx->stream));
+          BPP_HIP(hipMemcpyAsync((uint8_t*)d_in + vo, V + p0 * vbytes, vn, hipMemcpyHostToDevice, ctx->stream));
+        } else {
+          ctx_stage_copy(stg + po, proofs + po, pn);
+          BPP_TRY(ctx_h2d_staged(ctx, (uint8_t*)d_in + po, stg + po, pn));
+          ctx_stage_copy(stg + vo, V + p0 * vbytes, vn);
+          BPP_TRY(ctx_h2d_staged(ctx, (uint8_t*)d_in + vo, stg + vo, vn));
+        }
         BPP_HIP(hipEventRecord(ctx->vj_ev_chunk[q], ctx->stream));
         BPP_HIP(hipStreamWaitEvent(kid->stream, ctx->vj_ev_chunk[q], 0));
         BPP_TRY(verify_decompress_dev(kid, C, (uint32_t)count, d_pf, d_V, (uint32_t*)d_x,
@@ -1160,8 +1256,8 @@ int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label,
   }
   HostScope hs(ctx, "verify_replay");
   if (dec_order != 0 && !rcount) BPP_TRY(launch_dec());
-  uint32_t *h_init = nullptr, *h_r = nullptr, *h_bad = nullptr;
-  {
+  uint32_t *h_r = nullptr, *h_bad = nullptr;
+  if (!h_init) {
     uint32_t init[52];
     verify_init_state(C, label, llen, init);
     BPP_TRY(ctx_zc_in(ctx, "vj_init", init, sizeof init, &h_init));
@@ -1173,7 +1269,7 @@ int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label,
     BPP_HIP(hipEventRecord(ctx->vj_ev_in, ctx->stream));
   }
   BPP_TRY(verify_replay_dev(ctx, C, (uint32_t)rcount, h_init, d_pf + rfirst * (plen / 4),
-                            d_V + rfirst * (vbytes / 4), (uint32_t*)d_rec, h_r, h_bad));
+                            d_V + rfirst * (vbytes / 4), (uint32_t*)d_rec, h_r, h_bad, d_stt));
   if (dec_order == 1) {
     BPP_HIP(hipStreamWaitEvent(kid->stream, ctx->vj_ev_in, 0));
     BPP_TRY(verify_decompress_dev(kid, C, (uint32_t)count, d_pf, d_V, (uint32_t*)d_x, (unsigned long long*)d_dbad));

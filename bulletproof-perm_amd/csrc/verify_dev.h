@@ -36,16 +36,29 @@ inline uint32_t vpts_n(const perm::Circuit& C) { return C.m + 8 + 2 * C.lg; }
 // the t-check weight challenges) and bad ([count] u32, nonzero where a point
 // is the identity encoding, a scalar is not canonical or a challenge is
 // zero).  r_out and bad may be pinned host memory (written in place).
+// d_stt (optional): the transcripts' V parts already replayed by
+// verify_replay_v_dev into d_stt ([count][52] words); the replay then starts
+// from each proof's state there and reads only the proof bytes.
 int verify_replay_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const uint32_t* d_init,
-                      const uint32_t* d_proofs, const uint32_t* d_V, uint32_t* d_rec, uint32_t* r_out, uint32_t* bad);
+                      const uint32_t* d_proofs, const uint32_t* d_V, uint32_t* d_rec, uint32_t* r_out, uint32_t* bad,
+                      const uint32_t* d_stt = nullptr);
+// The V part of the transcripts of proofs [p0, p1) of a batch of `total`
+// (2k V appends, x_perm, V_2k): needs only their V bytes; leaves each
+// proof's sponge in d_stt[p] (52 words) and its x_perm challenge bytes in
+// the replay's challenge workspace.
+// Launched on stream st (the workspaces are ctx's).
+int verify_replay_v_dev(bpp_ctx* ctx, hipStream_t st, const perm::Circuit& C, uint32_t p0, uint32_t p1,
+                        uint32_t total, const uint32_t* d_init, const uint32_t* d_V, uint32_t* d_stt);
 // Decompresses the proof points of proofs [p0, p1) (p1 = ~0u: count) of the
 // uploaded proofs / V into d_tbl ([count * vpts_n] Niels rows in MSM order);
 // *d_bad = the smallest index of an undecodable encoding (set to ~0 by the
 // caller first).  Independent of the replay (launched on another stream, one
 // launch per upload chunk).
+// [jlo, jlo + jn): the points of each proof to decode (V_0..V_{m-1} are
+// points 0..m-1, the proof's own m..npt-1; default all of them).
 int verify_decompress_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const uint32_t* d_proofs,
                           const uint32_t* d_V, uint32_t* d_tbl, unsigned long long* d_bad, uint32_t p0 = 0,
-                          uint32_t p1 = ~0u);
+                          uint32_t p1 = ~0u, uint32_t jlo = 0, uint32_t jn = ~0u);
 // The 52-word shared transcript prefix for verify_replay_dev.
 void verify_init_state(const perm::Circuit& C, const uint8_t* label, size_t llen, uint32_t out[52]);
 // out[i] = sum over the nb blocks (stride words apart) of block[b][i], i < n

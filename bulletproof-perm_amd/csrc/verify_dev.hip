@@ -59,21 +59,27 @@ FE_INLINE bool w8_zero(const uint32_t w[8]) {
 #define RG_GS GRP_BLOCK
 #define RG_SCR_OFF GRP_SCR_OFF
 #endif
-template <bool STAGED>
-__global__ void __launch_bounds__(64) k_verify_replay_g(uint32_t count, uint32_t k, uint32_t lg, uint32_t n_p,
-                                                        const uint32_t* __restrict__ init,
+// PH: 0 = the whole transcript; 1 = its V part (the 2k V appends, x_perm,
+// V_2k), the sponge left in stt[p] (52 words: state, pos, pos_begin); 2 =
+// the rest, from stt[p].  The split lets the V part of a chunk of proofs run
+// as soon as that chunk's V bytes land (verify_begin_dev, BPP_VERIFY_SPLIT),
+// while the proof bytes are still on their way.  Proofs [p0, p1) of a batch
+// of `total` (ch and okw indexed by batch proof; ch[total] is the pad).
+template <bool STAGED, int PH>
+__global__ void __launch_bounds__(64) k_verify_replay_g(uint32_t p0, uint32_t p1, uint32_t total, uint32_t k,
+                                                        uint32_t lg, uint32_t n_p, const uint32_t* __restrict__ init,
                                                         const uint32_t* __restrict__ proofs, uint32_t pw,
                                                         const uint32_t* __restrict__ V, uint32_t* __restrict__ ch,
-                                                        uint32_t* __restrict__ okw) {
+                                                        uint32_t* __restrict__ okw, uint32_t* __restrict__ stt) {
   __shared__ __attribute__((aligned(16))) uint8_t sp[RG_GROUPS * RG_GS];
   extern __shared__ __attribute__((aligned(16))) uint32_t stage[];  // STAGED: [8][pw + 8 m]
   // the replay is a latency chain and the proof-point decompression runs
   // beside it on the same SIMDs: win the issue arbitration
   __builtin_amdgcn_s_setprio(3);
   const uint32_t g = threadIdx.x / GRP_LANES, gl = threadIdx.x % GRP_LANES;
-  const uint32_t pg = blockIdx.x * RG_GROUPS + g;
-  const bool live = pg < count;
-  const uint32_t p = live ? pg : count - 1;
+  const uint32_t pg = p0 + blockIdx.x * RG_GROUPS + g;
+  const bool live = pg < p1;
+  const uint32_t p = live ? pg : p1 - 1;
   const uint32_t m = 2 * k + 1, nch = 6 + lg;
   GroupStrobe t;
   t.st = sp + g * RG_GS;
@@ -81,21 +87,23 @@ __global__ void __launch_bounds__(64) k_verify_replay_g(uint32_t count, uint32_t
   t.gl = gl;
   t.leader = gl == GRP_LEADER;
   {
+    const uint32_t* src = PH == 2 ? stt + (size_t)p * 52 : init;
     uint32_t* d = reinterpret_cast<uint32_t*>(t.st);
-    for (uint32_t i = gl; i < 50; i += GRP_LANES) d[i] = init[i];
-    t.pos = init[50];
-    t.pos_begin = init[51];
+    for (uint32_t i = gl; i < 50; i += GRP_LANES) d[i] = src[i];
+    t.pos = src[50];
+    t.pos_begin = src[51];
   }
-  const uint32_t* PV;
-  const uint32_t* PP;
+  const uint32_t* PV = nullptr;
+  const uint32_t* PP = nullptr;
   if (STAGED) {
-    uint32_t* sg = stage + (size_t)g * (pw + 8 * m);
+    const uint32_t pwh = PH == 1 ? 0u : pw, vw = PH == 2 ? 0u : 8 * m;  // the words this phase reads
+    uint32_t* sg = stage + (size_t)g * (pwh + vw);
     const uint4* sp4 = reinterpret_cast<const uint4*>(proofs + (size_t)p * pw);
-    for (uint32_t i = gl; i < pw / 4; i += GRP_LANES) reinterpret_cast<uint4*>(sg)[i] = sp4[i];
+    for (uint32_t i = gl; i < pwh / 4; i += GRP_LANES) reinterpret_cast<uint4*>(sg)[i] = sp4[i];
     const uint4* sv4 = reinterpret_cast<const uint4*>(V + (size_t)p * m * 8);
-    for (uint32_t i = gl; i < 2 * m; i += GRP_LANES) reinterpret_cast<uint4*>(sg + pw)[i] = sv4[i];
+    for (uint32_t i = gl; i < vw / 4; i += GRP_LANES) reinterpret_cast<uint4*>(sg + pwh)[i] = sv4[i];
     PP = sg;
-    PV = sg + pw;
+    PV = sg + pwh;
   } else {
     PP = proofs + (size_t)p * pw;
     PV = V + (size_t)p * m * 8;
@@ -107,16 +115,30 @@ __global__ void __launch_bounds__(64) k_verify_replay_g(uint32_t count, uint32_t
 #else
 #define APPEND32(lab, ln, w, src) t.append32(lab, ln, w)
 #endif
-  uint32_t* CH = ch + (size_t)(live ? p : count) * nch * 16;
+  uint32_t* CH = ch + (size_t)(live ? p : total) * nch * 16;
   uint32_t w[8];
   bool ok = true;
-  for (uint32_t j = 0; j < 2 * k; ++j) {
-    ld8(PV + 8 * j, w);
-    APPEND32("V", 1, w, PV + 8 * j);
+  if (PH != 2) {
+    for (uint32_t j = 0; j < 2 * k; ++j) {
+      ld8(PV + 8 * j, w);
+      APPEND32("V", 1, w, PV + 8 * j);
+    }
+    t.challenge64_to("x_perm", 6, CH, true);
+    ld8(PV + 16 * k, w);
+    APPEND32("V", 1, w, PV + 16 * k);
   }
-  t.challenge64_to("x_perm", 6, CH, true);
-  ld8(PV + 16 * k, w);
-  APPEND32("V", 1, w, PV + 16 * k);
+  if (PH == 1) {
+    if (live) {
+      const uint32_t* d = reinterpret_cast<const uint32_t*>(t.st);
+      uint32_t* o = stt + (size_t)p * 52;
+      for (uint32_t i = gl; i < 50; i += GRP_LANES) o[i] = d[i];
+      if (t.leader) {
+        o[50] = t.pos;
+        o[51] = t.pos_begin;
+      }
+    }
+    return;
+  }
   ld8(PP, w);
   ok &= !w8_zero(w);
   APPEND32("A_I", 3, w, PP);
@@ -243,12 +265,15 @@ __global__ void __launch_bounds__(64) k_verify_replay_post(uint32_t count, uint3
 #define VD_WPE 3
 #endif
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(VD_WPE)))
-k_verify_decompress(size_t i0, size_t i1, uint32_t m, uint32_t lg, uint32_t npt, const uint32_t* __restrict__ proofs,
-                    uint32_t pw, const uint32_t* __restrict__ V, uint32_t* __restrict__ tbl,
-                    unsigned long long* __restrict__ bad) {
-  const size_t i = i0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= i1) return;
-  const uint32_t p = (uint32_t)(i / npt), j = (uint32_t)(i % npt);
+k_verify_decompress(size_t i0, size_t i1, uint32_t jlo, uint32_t jn, uint32_t m, uint32_t lg, uint32_t npt,
+                    const uint32_t* __restrict__ proofs, uint32_t pw, const uint32_t* __restrict__ V,
+                    uint32_t* __restrict__ tbl, unsigned long long* __restrict__ bad) {
+  // lane -> (proof p, point j = jlo + j' with j' < jn): the V points (jlo =
+  // 0, jn = m) or the proof's own points (jlo = m) can go separately
+  const size_t t = i0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= i1) return;
+  const uint32_t p = (uint32_t)(t / jn), j = jlo + (uint32_t)(t % jn);
+  const size_t i = (size_t)p * npt + j;
   const uint32_t* src;
   if (j < m)
     src = V + ((size_t)p * m + j) * 8;
@@ -278,24 +303,50 @@ void verify_init_state(const perm::Circuit& C, const uint8_t* label, size_t llen
   out[51] = tr.s.pos_begin;
 }
 
+template <int PH>
+static void launch_replay(hipStream_t st, const perm::Circuit& C, uint32_t p0, uint32_t p1, uint32_t total,
+                          const uint32_t* d_init, const uint32_t* d_proofs, const uint32_t* d_V, uint32_t* d_ch,
+                          uint32_t* d_ok, uint32_t* d_stt) {
+  const uint32_t pw = (uint32_t)(perm::proof_len(C.k) / 4);
+  // the bytes the phase reads, of the block's groups, staged in LDS while they fit
+  const size_t words = (PH == 1 ? 0 : pw) + (PH == 2 ? 0 : 8 * (size_t)C.m);
+  const size_t stage = (size_t)RG_GROUPS * words * 4;
+  if (stage <= 48 * 1024)
+    hipLaunchKernelGGL((k_verify_replay_g<true, PH>), dim3(grid_for(p1 - p0, RG_GROUPS)), dim3(64), stage, st,
+                       p0, p1, total, C.k, C.lg, C.n_p, d_init, d_proofs, pw, d_V, d_ch, d_ok, d_stt);
+  else
+    hipLaunchKernelGGL((k_verify_replay_g<false, PH>), dim3(grid_for(p1 - p0, RG_GROUPS)), dim3(64), 0, st,
+                       p0, p1, total, C.k, C.lg, C.n_p, d_init, d_proofs, pw, d_V, d_ch, d_ok, d_stt);
+}
+
+int verify_replay_v_dev(bpp_ctx* ctx, hipStream_t st, const perm::Circuit& C, uint32_t p0, uint32_t p1,
+                        uint32_t total, const uint32_t* d_init, const uint32_t* d_V, uint32_t* d_stt) {
+  if (p0 >= p1) return BPP_OK;
+  const uint32_t nch = 6 + C.lg;
+  void *d_ch = nullptr, *d_ok = nullptr;
+  BPP_TRY(ctx_ws(ctx, "vj_ch", ((size_t)total + 1) * nch * 64, &d_ch));
+  BPP_TRY(ctx_ws(ctx, "vj_ok", (size_t)total * 4, &d_ok));
+  launch_replay<1>(st, C, p0, p1, total, d_init, nullptr, d_V, (uint32_t*)d_ch, (uint32_t*)d_ok, d_stt);
+  return ctx_check_launch(ctx, "k_verify_replay_g<V>");
+}
+
 int verify_replay_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const uint32_t* d_init,
-                      const uint32_t* d_proofs, const uint32_t* d_V, uint32_t* d_rec, uint32_t* r_out, uint32_t* bad) {
+                      const uint32_t* d_proofs, const uint32_t* d_V, uint32_t* d_rec, uint32_t* r_out, uint32_t* bad,
+                      const uint32_t* d_stt) {
   if (!count) return BPP_OK;
   const uint32_t pw = (uint32_t)(perm::proof_len(C.k) / 4);
   const uint32_t nch = 6 + C.lg;
   void *d_ch = nullptr, *d_ok = nullptr;
   BPP_TRY(ctx_ws(ctx, "vj_ch", ((size_t)count + 1) * nch * 64, &d_ch));
   BPP_TRY(ctx_ws(ctx, "vj_ok", (size_t)count * 4, &d_ok));
-  // the proof and V bytes of the block's 8 proofs staged in LDS while they fit
-  const size_t stage = (size_t)RG_GROUPS * (pw + 8 * (size_t)C.m) * 4;
   {
     ProfScope ps(ctx, "verify_replay_dev");
-    if (stage <= 48 * 1024)
-      hipLaunchKernelGGL(k_verify_replay_g<true>, dim3(grid_for(count, RG_GROUPS)), dim3(64), stage, ctx->stream,
-                         count, C.k, C.lg, C.n_p, d_init, d_proofs, pw, d_V, (uint32_t*)d_ch, (uint32_t*)d_ok);
+    if (d_stt)
+      launch_replay<2>(ctx->stream, C, 0, count, count, nullptr, d_proofs, d_V, (uint32_t*)d_ch, (uint32_t*)d_ok,
+                       (uint32_t*)d_stt);
     else
-      hipLaunchKernelGGL(k_verify_replay_g<false>, dim3(grid_for(count, RG_GROUPS)), dim3(64), 0, ctx->stream,
-                         count, C.k, C.lg, C.n_p, d_init, d_proofs, pw, d_V, (uint32_t*)d_ch, (uint32_t*)d_ok);
+      launch_replay<0>(ctx->stream, C, 0, count, count, d_init, d_proofs, d_V, (uint32_t*)d_ch, (uint32_t*)d_ok,
+                       nullptr);
   }
   BPP_TRY(ctx_check_launch(ctx, "k_verify_replay_g"));
   {
@@ -328,14 +379,18 @@ int verify_sum_blocks_dev(bpp_ctx* ctx, uint32_t nb, uint32_t n, const uint32_t*
 
 
 int verify_decompress_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const uint32_t* d_proofs,
-                          const uint32_t* d_V, uint32_t* d_tbl, unsigned long long* d_bad, uint32_t p0, uint32_t p1) {
+                          const uint32_t* d_V, uint32_t* d_tbl, unsigned long long* d_bad, uint32_t p0, uint32_t p1,
+                          uint32_t jlo, uint32_t jn) {
   p1 = std::min(p1, count);
-  if (p0 >= p1) return BPP_OK;
-  const size_t npt = vpts_n(C), i0 = (size_t)p0 * npt, i1 = (size_t)p1 * npt;
+  const uint32_t npt = vpts_n(C);
+  if (jlo >= npt) return BPP_OK;
+  jn = std::min(jn, npt - jlo);
+  if (p0 >= p1 || !jn) return BPP_OK;
+  const size_t i0 = (size_t)p0 * jn, i1 = (size_t)p1 * jn;
   {
     ProfScope ps(ctx, "verify_decompress");
-    hipLaunchKernelGGL(k_verify_decompress, dim3(grid_for(i1 - i0, 64)), dim3(64), 0, ctx->stream, i0, i1, C.m, C.lg,
-                       (uint32_t)npt, d_proofs, (uint32_t)(perm::proof_len(C.k) / 4), d_V, d_tbl, d_bad);
+    hipLaunchKernelGGL(k_verify_decompress, dim3(grid_for(i1 - i0, 64)), dim3(64), 0, ctx->stream, i0, i1, jlo, jn, C.m,
+                       C.lg, npt, d_proofs, (uint32_t)(perm::proof_len(C.k) / 4), d_V, d_tbl, d_bad);
   }
   return ctx_check_launch(ctx, "k_verify_decompress");
 }

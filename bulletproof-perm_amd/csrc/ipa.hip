@@ -237,14 +237,14 @@ struct IpaRoundArgs {
   uint32_t* out_p3;
   const uint32_t *a0, *b0, *gf0, *hf0;
   uint32_t m, lg_h, fold, init, halve, gbase, hbase, qidx;
-  uint32_t blocks;  // 2 P (k_ipa_round_dt_multi)
-  uint32_t pad_;
+  uint32_t blocks;  // 2 P J (k_ipa_round_dt_multi)
+  uint32_t split;   // J: blocks per L / R MSM, each walking a slice of its n + 1 terms
 };
 
 FE_INLINE void ipa_round_body(const uint32_t* __restrict__ dt, const DtGeom& dg, uint32_t n, uint32_t TG,
                               const IpaRoundArgs& A, uint32_t bidx, uint32_t* lds) {
   const uint32_t m = A.m, lg_h = A.lg_h, fold = A.fold, init = A.init, halve = A.halve, gbase = A.gbase,
-                 hbase = A.hbase, qidx = A.qidx;
+                 hbase = A.hbase, qidx = A.qidx, J = A.split;
   const uint32_t* __restrict__ am_in = A.am_in;
   const uint32_t* __restrict__ bm_in = A.bm_in;
   const uint32_t* __restrict__ fG_in = A.fG_in;
@@ -266,12 +266,14 @@ FE_INLINE void ipa_round_body(const uint32_t* __restrict__ dt, const DtGeom& dg,
   uint32_t* sb = sa + 8 * m;                     // m x 8: b
   uint32_t* red = sb + 8 * m;                    // waves x 8 words
   const uint32_t nt = blockDim.x, tid = threadIdx.x;
-  const uint32_t inst = bidx >> 1, side = bidx & 1u;
+  // block bidx: slice jp of J of MSM bidx / J = instance inst's L (side 0) or R
+  const uint32_t msm = bidx / J, jp = bidx - msm * J;
+  const uint32_t inst = msm >> 1, side = msm & 1u;
   const size_t ib = (size_t)inst * n;
   // init (the first round, no fold): a, b and the generator factors come
   // from the caller's canonical arrays a0, b0, gf0, hf0 (null: all one), and
   // side 0 writes the Montgomery state that round 1 folds (k_ipa_init's work)
-  const bool writer = (fold || init) && side == 0;
+  const bool writer = (fold || init) && side == 0 && jp == 0;
   sc um = sc_zero(), uim = sc_zero();
   if (fold) {
     um = sc_load(u + 16 * inst);
@@ -357,7 +359,8 @@ FE_INLINE void ipa_round_body(const uint32_t* __restrict__ dt, const DtGeom& dg,
   if (tid == 0) store_p3(out_p3, bidx, ge_identity());
   return;
 #endif
-  const ge_p3 acc = tg < TG ? dt_walk(dt, dg, ln, tg, n + 1, TG,
+  const uint32_t t0 = (uint32_t)((uint64_t)jp * (n + 1) / J), t1 = (uint32_t)((uint64_t)(jp + 1) * (n + 1) / J);
+  const ge_p3 acc = tg < TG ? dt_walk(dt, dg, ln, t0 + tg, t1, TG,
                                       [&](uint32_t t, uint32_t s[8], uint32_t& gen) {
                                         const sc v = sc_load(tsc + 8 * t);
                                         _Pragma("unroll") for (int i = 0; i < 8; ++i) s[i] = v.v[i];
@@ -379,7 +382,7 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
     uint32_t* __restrict__ fG_out, uint32_t* __restrict__ fH_out, const uint32_t* __restrict__ u,
     const uint32_t* __restrict__ qmul, uint32_t gbase, uint32_t hbase, uint32_t qidx, uint32_t TG, uint32_t halve,
     uint32_t* __restrict__ out_p3, const uint32_t* __restrict__ a0, const uint32_t* __restrict__ b0,
-    const uint32_t* __restrict__ gf0, const uint32_t* __restrict__ hf0, uint32_t init) {
+    const uint32_t* __restrict__ gf0, const uint32_t* __restrict__ hf0, uint32_t init, uint32_t J) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   IpaRoundArgs A;
   A.am_in = am_in; A.bm_in = bm_in; A.fG_in = fG_in; A.fH_in = fH_in;
@@ -388,6 +391,7 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
   A.a0 = a0; A.b0 = b0; A.gf0 = gf0; A.hf0 = hf0;
   A.m = m; A.lg_h = lg_h; A.fold = fold; A.init = init; A.halve = halve;
   A.gbase = gbase; A.hbase = hbase; A.qidx = qidx;
+  A.split = J;
   ipa_round_body(dt, dg, n, TG, A, blockIdx.x, lds);
 }
 
@@ -648,10 +652,26 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
     return e && atoi(e) != 0;
   }();
   const bool merge = merge_env && zc;
+  // J blocks per L / R MSM when the batch is small (config 2: P = 1, two
+  // blocks of one wave per SIMD walking ~64 of the 1025 terms per lane in a
+  // row): each block walks a slice of the terms and the host adds the J
+  // partials before it encodes (zero-copy path only; BPP_IPA_SPLIT overrides)
+  uint32_t J = 1;
+  if (zc && nt) {
+    static const int split_env = [] {
+      const char* e = getenv("BPP_IPA_SPLIT");
+      return e ? atoi(e) : -1;
+    }();
+    if (split_env >= 1) {
+      J = (uint32_t)split_env;
+    } else if (split_env < 0) {
+      while (J < 16 && 2 * P * (2 * J) <= 512 && (n + 1) / (2 * J) >= 2 * TG) J *= 2;
+    }
+  }
   uint32_t* h_uw = nullptr;  // zc: the challenges' device words, in place
   if (zc) {
     void *hr = nullptr, *hu = nullptr;
-    BPP_TRY(ctx_host_buf(ctx, "ipa_res_h", (size_t)2 * P * P3_BYTES, &hr));
+    BPP_TRY(ctx_host_buf(ctx, "ipa_res_h", (size_t)2 * P * J * P3_BYTES, &hr));
     BPP_TRY(ctx_host_buf(ctx, "ipa_u_h", (size_t)P * 64, &hu));
     d_res = hr;
     d_u = hu;
@@ -685,8 +705,8 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
         A.a0 = d_a; A.b0 = d_b; A.gf0 = d_Gf; A.hf0 = d_Hf;
         A.m = m; A.lg_h = lg_h; A.fold = round ? 1u : 0u; A.init = round ? 0u : 1u; A.halve = 1u;
         A.gbase = g.gbase; A.hbase = g.hbase; A.qidx = g.qidx;
-        A.blocks = 2 * P;
-        A.pad_ = 0;
+        A.blocks = 2 * P * J;
+        A.split = J;
         req.dt = g.pts.dt;
         req.dg = dg;
         req.n = n;
@@ -699,12 +719,12 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
         BPP_HIP(hipStreamWaitEvent(ctx->stream, req.done, 0));  // (ctx_sync below then covers the round)
       } else {
         ProfScope ps(ctx, "ipa_round_dt");  // (bench.py: this kernel's own roofline)
-        hipLaunchKernelGGL(k_ipa_round_dt, dim3(2 * P), dim3(nt), ipa_round_lds_words(n, nt) * 4, ctx->stream,
+        hipLaunchKernelGGL(k_ipa_round_dt, dim3(2 * P * J), dim3(nt), ipa_round_lds_words(n, nt) * 4, ctx->stream,
                            g.pts.dt, dg, n, m, lg_h, round ? 1u : 0u, S[in][0], S[in][1], S[in][2], S[in][3],
                            S[round ? outs : in][0], S[round ? outs : in][1], S[round ? outs : in][2],
                            S[round ? outs : in][3], (const uint32_t*)d_u, (const uint32_t*)d_q, g.gbase, g.hbase,
                            g.qidx, TG, dev_merlin ? 0u : 1u, (uint32_t*)d_res, d_a, d_b, d_Gf, d_Hf,
-                           round ? 0u : 1u);
+                           round ? 0u : 1u, J);
       }
       BPP_TRY(ctx_check_launch(ctx, "k_ipa_round_dt"));
       if (round) cur = outs;
@@ -726,7 +746,7 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
       } else if (zc) {
         HostScope hs(ctx, "ipa_msm");
         BPP_TRY(ctx_sync(ctx));  // the kernel's L/2, R/2 are in host memory now
-        BPP_TRY(points_double_encode_host(ctx, (const uint32_t*)d_res, 2 * (size_t)P, enc.data()));
+        BPP_TRY(points_double_encode_host(ctx, (const uint32_t*)d_res, 2 * (size_t)P, enc.data(), J));
       } else {
         HostScope hs(ctx, "ipa_msm");
         BPP_TRY(points_double_encode_p3(ctx, (const uint32_t*)d_res, 2 * (size_t)P, enc.data()));

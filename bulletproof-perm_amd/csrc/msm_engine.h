@@ -37,7 +37,8 @@ int points_compress_p3_dev(bpp_ctx* ctx, const uint32_t* d_p3, size_t n, uint8_t
 // out = encodings of 2 * P_i (host batch encoding; see points.hip)
 int points_double_encode_p3(bpp_ctx* ctx, const uint32_t* d_p3, size_t n, uint8_t* out_host);
 // same for n points already in host memory (P3 words)
-int points_double_encode_host(bpp_ctx* ctx, const uint32_t* raw, size_t n, uint8_t* out_host);
+// raw: n x J device-layout points; point i = the sum of raw[i J .. i J + J)
+int points_double_encode_host(bpp_ctx* ctx, const uint32_t* raw, size_t n, uint8_t* out_host, uint32_t J = 1);
 // d_out[i] = d_in[i] / 2 mod l (canonical scalars; in place allowed)
 int sc_halve_dev(bpp_ctx* ctx, const uint32_t* d_in, uint32_t* d_out, size_t n);
 // d_out[t] = d_in[d_map[t]] / 2 for t < n

@@ -93,7 +93,7 @@ int points_compress_p3(bpp_ctx* ctx, const uint32_t* d_p3, size_t n, uint8_t* ou
 // (h25519::encode_double_batch).  For small batches this beats the
 // per-point inverse-square-root chain of k_compress_p3 (~70 us of serial
 // field ops on one lane); callers compute P_i = C_i / 2 from halved scalars.
-int points_double_encode_host(bpp_ctx* ctx, const uint32_t* raw, size_t n, uint8_t* out_host);
+int points_double_encode_host(bpp_ctx* ctx, const uint32_t* raw, size_t n, uint8_t* out_host, uint32_t J = 1);
 int points_double_encode_p3(bpp_ctx* ctx, const uint32_t* d_p3, size_t n, uint8_t* out_host) {
   if (!n) return BPP_OK;
   std::vector<uint32_t> raw(n * P3_WORDS);
@@ -101,14 +101,18 @@ int points_double_encode_p3(bpp_ctx* ctx, const uint32_t* d_p3, size_t n, uint8_
   return points_double_encode_host(ctx, raw.data(), n, out_host);
 }
 
-int points_double_encode_host(bpp_ctx* ctx, const uint32_t* raw, size_t n, uint8_t* out_host) {
+int points_double_encode_host(bpp_ctx* ctx, const uint32_t* raw, size_t n, uint8_t* out_host, uint32_t J) {
   if (!n) return BPP_OK;
   HostScope hs(ctx, "double_encode");
   const size_t chunks = std::min<size_t>(par::threads(), (n + 7) / 8);
   par::for_each(chunks, [&](size_t c) {
     const size_t b = n * c / chunks, e = n * (c + 1) / chunks;
     std::vector<h25519::ge> pts(e - b);
-    for (size_t i = b; i < e; ++i) pts[i - b] = h25519::ge_from_dev(raw + i * P3_WORDS);
+    for (size_t i = b; i < e; ++i) {
+      pts[i - b] = h25519::ge_from_dev(raw + i * J * P3_WORDS);
+      for (uint32_t j = 1; j < J; ++j)
+        pts[i - b] = h25519::ge_add(pts[i - b], h25519::ge_from_dev(raw + (i * J + j) * P3_WORDS));
+    }
     h25519::encode_double_batch_auto(pts.data(), e - b, out_host + 32 * b);
   });
   return BPP_OK;

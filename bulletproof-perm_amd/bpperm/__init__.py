@@ -660,6 +660,20 @@ class VerifyJob:
             pass
 
 
+def scalar_invert(x: bytes) -> bytes:
+    """Scalar::invert of a canonical 32-byte scalar (bpp_scalar_invert)."""
+    out = C.create_string_buffer(32)
+    check(_lib.load().bpp_scalar_invert(_buf(bytes(x)), out), "bpp_scalar_invert")
+    return out.raw
+
+
+def scalar_powers(x: bytes, n: int) -> bytes:
+    """x^0 .. x^(n-1) as n x 32 bytes (bpp_scalar_powers; util.rs exp_iter)."""
+    out = C.create_string_buffer(32 * max(n, 1))
+    check(_lib.load().bpp_scalar_powers(_buf(bytes(x)), n, out), "bpp_scalar_powers")
+    return out.raw[:32 * n]
+
+
 def verify_seed() -> bytes:
     """32 bytes of verifier randomness for one batch (bpp_verify_seed: the OS
     CSPRNG).  Every job / rank of the batch must use the same bytes."""

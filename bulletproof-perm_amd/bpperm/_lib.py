@@ -94,6 +94,8 @@ SIGNATURES = {
     "bpp_perm_verify_begin_dev": (i32, [vp, u32, sz, vp, sz, vp, vp, vp, C.POINTER(vp)]),
     "bpp_perm_verify_terms": (i32, [vp, C.POINTER(sz)]),
     "bpp_verify_seed": (i32, [vp]),
+    "bpp_scalar_invert": (i32, [vp, vp]),
+    "bpp_scalar_powers": (i32, [vp, sz, vp]),
     "bpp_perm_verify_scalars": (i32, [vp, vp, sz, vp, vp]),
     "bpp_perm_verify_partial": (i32, [vp, vp, vp, vp, sz, u32, u32, vp]),
     "bpp_perm_verify_begin_dev_slice": (i32, [vp, u32, sz, vp, sz, vp, vp, sz, sz, vp, C.POINTER(vp)]),

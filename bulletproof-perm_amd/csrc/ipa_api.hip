@@ -95,6 +95,28 @@ int bpp_transcript_challenge_scalar(bpp_transcript* t, const uint8_t* label, siz
   });
 }
 
+int bpp_scalar_invert(const uint8_t x[32], uint8_t out[32]) {
+  return bpp_guard(nullptr, [&]() -> int {
+    if (!x || !out) return BPP_ERR_ARG;
+    hsc::Sc v;
+    if (!hsc::from_canonical(v, x)) return BPP_ERR_NONCANONICAL;
+    if (hsc::is_zero(v)) return BPP_ERR_ARG;
+    hsc::to_bytes(out, hsc::invert(v));
+    return BPP_OK;
+  });
+}
+
+int bpp_scalar_powers(const uint8_t x[32], size_t n, uint8_t* out) {
+  return bpp_guard(nullptr, [&]() -> int {
+    if (!x || (!out && n)) return BPP_ERR_ARG;
+    hsc::Sc v;
+    if (!hsc::from_canonical(v, x)) return BPP_ERR_NONCANONICAL;
+    const std::vector<hsc::Sc> p = hsc::powers(v, n);
+    for (size_t i = 0; i < n; ++i) hsc::to_bytes(out + 32 * i, p[i]);
+    return BPP_OK;
+  });
+}
+
 int bpp_vec_commit(bpp_ctx* ctx, const bpp_gens* g, const uint8_t blind[32], const uint8_t* a, const uint8_t* b,
                    size_t n, uint8_t out[32]) {
   return bpp_guard(ctx, [&]() -> int {
@@ -120,8 +142,16 @@ int bpp_vec_commit(bpp_ctx* ctx, const bpp_gens* g, const uint8_t blind[32], con
     std::vector<h25519::ge> res;
     MsmPoints pts;
     BPP_TRY(gens_points(ctx, g, &pts));
-    BPP_TRY(msm_multi(ctx, d_s, (const uint32_t*)d_i, {0, (uint32_t)T}, pts, res));
-    h25519::encode(out, res[0]);
+    // one long MSM alone runs as one block (one wave per SIMD walking ~T/16
+    // terms per lane in a row): cut it into J slices, J blocks side by side,
+    // and add the J results here (config 2's 2049 terms: 16 slices)
+    const uint32_t J = (uint32_t)std::max<size_t>(1, std::min<size_t>(16, T / 128));
+    std::vector<uint32_t> off(J + 1);
+    for (uint32_t j = 0; j <= J; ++j) off[j] = (uint32_t)((uint64_t)T * j / J);
+    BPP_TRY(msm_multi(ctx, d_s, (const uint32_t*)d_i, off, pts, res));
+    h25519::ge acc = res[0];
+    for (uint32_t j = 1; j < J; ++j) acc = h25519::ge_add(acc, res[j]);
+    h25519::encode(out, acc);
     return BPP_OK;
   });
 }

@@ -307,8 +307,9 @@ extern "C" int bpp_debug_vs_timing(unsigned long long* out, size_t n) {
 #define VK_F 13     // F
 #define VK_WTF 14   // w_p F
 #define VK_WRX2F 15 // w_p r x^2 F
-#define VK_WTY 16   // w_p Y
-#define VK_N 17
+#define VK_XU2 16   // x U^2
+#define VK_RC 17    // lg values: -w_p Y prod_{k != j} u_k^2 (R_j's scalar)
+#define VK_N(lg) (VK_RC + (lg))
 __global__ void __launch_bounds__(64) k_verify_consts(uint32_t count, uint32_t lg, uint64_t first,
                                                       const uint32_t* __restrict__ seed,
                                                       const uint32_t* __restrict__ rec, uint32_t* __restrict__ kc) {
@@ -317,7 +318,7 @@ __global__ void __launch_bounds__(64) k_verify_consts(uint32_t count, uint32_t l
   if (p >= count) return;
   const uint32_t nrec = VREC_U + lg;
   const uint32_t* R = rec + (size_t)p * nrec * 8;
-  uint32_t* K = kc + (size_t)p * VK_N * 8;
+  uint32_t* K = kc + (size_t)p * VK_N(lg) * 8;
   // w_p = from_wide(SHAKE256("bp-perm-batch-wt" || seed || le64(first + p) ||
   // r_p)[0..64]): 88 bytes, one sponge block (perm::batch_weight)
   sc wt;
@@ -345,6 +346,18 @@ __global__ void __launch_bounds__(64) k_verify_consts(uint32_t count, uint32_t l
            bR = ldm(VREC_B), thR = ldm(VREC_THAT);
   sc UR = ldm(VREC_U);
   for (uint32_t j = 1; j < lg; ++j) UR = sc_mont(UR, ldm(VREC_U + j));
+  // R_j's scalar -w_p Y prod_{k != j} u_k^2 from prefix and suffix products
+  // of the u_k^2 (here, one lane per proof, instead of a 13-multiply chain on
+  // one lane of every k_verify_scalars workgroup); the prefixes wait in the
+  // slots, the suffix runs downwards
+  {
+    sc pre = sc_one_mont();
+    for (uint32_t j = 0; j < lg; ++j) {
+      sc_store(K + 8 * (VK_RC + j), pre);
+      const sc u = ldm(VREC_U + j);
+      pre = sc_mont(pre, sc_mont(u, u));
+    }
+  }
   sc YR = yR;  // y^(2^lg - 1) = y^(n_p - 1)
   for (uint32_t j = 1; j < lg; ++j) YR = sc_mont(sc_mont(YR, YR), yR);
   const sc U2R = sc_mont(UR, UR), FR = sc_mont(U2R, YR);
@@ -366,7 +379,16 @@ __global__ void __launch_bounds__(64) k_verify_consts(uint32_t count, uint32_t l
   sc_store(K + 8 * VK_F, FR);
   sc_store(K + 8 * VK_WTF, wtfR);
   sc_store(K + 8 * VK_WRX2F, sc_mont(wrx2R, FR));
-  sc_store(K + 8 * VK_WTY, sc_mont(wtR, YR));
+  sc_store(K + 8 * VK_XU2, sc_mont(xR, U2R));
+  {
+    const sc nwy = sc_neg(sc_mont(wtR, YR));
+    sc suf = sc_one_mont();
+    for (uint32_t j = lg; j-- > 0;) {
+      sc_store(K + 8 * (VK_RC + j), sc_mont(sc_mont(sc_load(K + 8 * (VK_RC + j)), suf), nwy));
+      const sc u = ldm(VREC_U + j);
+      suf = sc_mont(suf, sc_mont(u, u));
+    }
+  }
 }
 
 // (at 4 waves per SIMD: 128 VGPRs instead of 148, 108 B of spills, 8
@@ -391,7 +413,7 @@ __global__ void __launch_bounds__(POLY_T) __attribute__((amdgpu_waves_per_eu(VS_
   const uint32_t* zp = zt + 8;       // z^(q+1)
   const uint32_t p = blockIdx.x, nrec = VREC_U + lg;
   const uint32_t* R = rec + (size_t)p * nrec * 8;
-  const uint32_t* K = kc + (size_t)p * VK_N * 8;
+  const uint32_t* K = kc + (size_t)p * VK_N(lg) * 8;
   const sc oneR = sc_one_mont();
   auto ldm = [&](uint32_t k) { return sc_to_mont(sc_load(R + 8 * k)); };
   auto ldk = [&](uint32_t k) { return sc_load(K + 8 * k); };
@@ -419,25 +441,29 @@ __global__ void __launch_bounds__(POLY_T) __attribute__((amdgpu_waves_per_eu(VS_
       }
     return v;
   };
-  const sc uyaR = ldk(VK_UYA), ubR = ldk(VK_UB), xR = ldk(VK_X), wtR = ldk(VK_WT), u2R = ldk(VK_U2), fR = ldk(VK_F);
+  const sc uyaR = ldk(VK_UYA), ubR = ldk(VK_UB), xu2R = ldk(VK_XU2), wtR = ldk(VK_WT), u2R = ldk(VK_U2), fR = ldk(VK_F);
   // gate i = n_p - 1 - e with e ascending per lane: yr_i = y^e = yt[e mod
   // POW_LO] (y^POW_LO)^(e / POW_LO), the second factor a running product
   // (blockDim = POW_LO whenever n_p > POW_LO)
   sc yhi = oneR, ystep = oneR;
   if (n_p > POW_LO) ystep = sc_mont(sc_load(yt + 8 * (POW_LO - 1)), ldk(VK_Y));
   const size_t gb = (size_t)p * NG;
-  sc acc[2] = {sc_zero(), sc_zero()};  // delta' = sum U^2 yr_i zWR_i zWL_i, zc = <z^Q, c>
+  // acc[0]: delta'' = sum yr_i zWR_i zWL_i (delta' = U^2 delta'', applied
+  // once below); acc[1]: zc = <z^Q, c>
+  sc acc[2] = {sc_zero(), sc_zero()};
   for (uint32_t e = threadIdx.x; e < n_p; e += blockDim.x) {
     const uint32_t i = n_p - 1 - e;
     sc yr = sc_load(yt + 8 * (e % POW_LO));
     if (e >= POW_LO) yr = sc_mont(yr, yhi);
     if (n_p > POW_LO) yhi = sc_mont(yhi, ystep);
-    const sc yu = sc_mont(u2R, yr);
     const sc zWL = col_sum(cp, ce, i, zp), zWR = col_sum(cp + (n_p + 1), ce, i, zp),
              zWO = col_sum(cp + 2 * (n_p + 1), ce, i, zp);
-    acc[0] = sc_add(acc[0], sc_mont(sc_mont(yu, zWR), zWL));
-    const sc gi = sc_sub(sc_mont(s_of(i), uyaR), sc_mont(sc_mont(zWR, xR), yu));
-    const sc hi = sc_add(sc_sub(sc_mont(sc_mont(s_of(e), ubR), yr), sc_mont(sc_add(sc_mont(zWL, xR), zWO), yu)), fR);
+    const sc rw = sc_mont(zWR, yr);
+    acc[0] = sc_add(acc[0], sc_mont(rw, zWL));
+    // G_i: st[i] U Y a - (zWR yr) x U^2;  H_i: (st[e] U b - zWL x U^2 - zWO U^2) yr + F
+    const sc gi = sc_sub(sc_mont(s_of(i), uyaR), sc_mont(rw, xu2R));
+    const sc hi = sc_add(sc_mont(sc_sub(sc_sub(sc_mont(s_of(e), ubR), sc_mont(zWL, xu2R)), sc_mont(zWO, u2R)), yr),
+                         fR);
     sc_store(gen + 8 * (gb + i), sc_from_mont(sc_mont(gi, wtR)));
     sc_store(gen + 8 * (gb + n_p + i), sc_from_mont(sc_mont(hi, wtR)));
   }
@@ -463,36 +489,32 @@ __global__ void __launch_bounds__(POLY_T) __attribute__((amdgpu_waves_per_eu(VS_
   }
   VS_T(4);
   // A_I, A_O, S: -wt F x^(1,2,3); T_k: -wt F r x^k (k = 1, 3..6); L_j:
-  // -wt F u_j^2; R_j: -wt Y prod_{k != j} u_k^2
+  // -wt F u_j^2; R_j: -wt Y prod_{k != j} u_k^2 (k_verify_consts)
   for (uint32_t j = threadIdx.x; j < 8 + 2 * lg; j += blockDim.x) {
-    sc v, f = ldk(VK_WTF);
+    if (j >= 8 + lg) {
+      sc_store(sc_out + 8 * (pb + m + j), sc_from_mont(ldk(VK_RC + (j - 8 - lg))));
+      continue;
+    }
+    sc v;
     if (j < 3) {
+      const sc xR = ldk(VK_X);
       v = xR;
       for (uint32_t e = 0; e < j; ++e) v = sc_mont(v, xR);
     } else if (j < 8) {
       const uint32_t e = j == 3 ? 1u : j - 1;  // T1, T3, T4, T5, T6
-      v = sc_mont(ldk(VK_R), sc_pow_small(xR, e, oneR));
-    } else if (j < 8 + lg) {
+      v = sc_mont(ldk(VK_R), sc_pow_small(ldk(VK_X), e, oneR));
+    } else {
       const sc u = ldm(VREC_U + (j - 8));
       v = sc_mont(u, u);
-    } else {
-      const uint32_t jj = j - 8 - lg;
-      v = oneR;
-      for (uint32_t k = 0; k < lg; ++k)
-        if (k != jj) {
-          const sc u = ldm(VREC_U + k);
-          v = sc_mont(v, sc_mont(u, u));
-        }
-      f = ldk(VK_WTY);
     }
-    sc_store(sc_out + 8 * (pb + m + j), sc_from_mont(sc_neg(sc_mont(v, f))));
+    sc_store(sc_out + 8 * (pb + m + j), sc_from_mont(sc_neg(sc_mont(v, ldk(VK_WTF)))));
   }
   VS_T(5);
   sc_block_sum<2>(acc, red);
   VS_T(6);
   if (threadIdx.x == 0) {
     // B: wt (r F t_hat - r x^2 (delta' + F zc) + w F (a b - t_hat)); B_blinding: wt F (r tau_x + mu)
-    const sc tB = sc_sub(ldk(VK_WRFT), sc_mont(ldk(VK_WRX2), sc_add(acc[0], sc_mont(fR, acc[1]))));
+    const sc tB = sc_sub(ldk(VK_WRFT), sc_mont(ldk(VK_WRX2), sc_add(sc_mont(u2R, acc[0]), sc_mont(fR, acc[1]))));
     sc_store(gen + 8 * (gb + 2 * n_p), sc_from_mont(sc_add(tB, ldk(VK_IB))));
     sc_store(gen + 8 * (gb + 2 * n_p + 1), sc_from_mont(ldk(VK_BB)));
   }
@@ -823,7 +845,7 @@ int verify_scalars_dev_rec(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count,
   const unsigned nt = poly_block(std::max(C.n_p, C.m));
   const size_t lds = ((size_t)C.Q + 1 + 2 * std::min(C.n_p, (uint32_t)POW_LO)) * 32 + (POLY_T / 64) * 2 * 32;
   void* d_kc = nullptr;
-  BPP_TRY(ctx_ws(ctx, "vs_kc", (size_t)count * VK_N * 32, &d_kc));
+  BPP_TRY(ctx_ws(ctx, "vs_kc", (size_t)count * VK_N(C.lg) * 32, &d_kc));
   {
     ProfScope ps(ctx, "verify_scalars");
     hipLaunchKernelGGL(k_verify_consts, dim3((count + 63) / 64), dim3(64), 0, ctx->stream, count, C.lg, first, seed,

@@ -216,6 +216,14 @@ int bpp_transcript_challenge_bytes(bpp_transcript* t, const uint8_t* label, size
  * (transcript_protocol.rs:62-67). */
 int bpp_transcript_challenge_scalar(bpp_transcript* t, const uint8_t* label, size_t llen, uint8_t out[32]);
 
+/* ------------------------------------------------- scalar helpers (host) */
+/* The caller-side scalar algebra the IPA's factors need: Scalar::invert
+ * (circuit_lib.rs:274; BPP_ERR_ARG for zero) and x^0 .. x^(n-1) (util.rs:
+ * 138-157 exp_iter; e.g. H_factors = powers of y^-1).  Canonical 32-byte
+ * scalars in and out (BPP_ERR_NONCANONICAL otherwise). */
+int bpp_scalar_invert(const uint8_t x[32], uint8_t out[32]);
+int bpp_scalar_powers(const uint8_t x[32], size_t n, uint8_t* out);
+
 /* ------------------------------------------------ inner-product argument */
 /* bulletproofs 4.0.0 InnerProductProof::create over G[0..n), H[0..n) of g
  * (n a power of two, n <= bpp_gens_len): L_out, R_out receive log2(n)

@@ -87,3 +87,26 @@ def test_host_exceptions_do_not_cross_the_abi():
     rc = lib.bpp_perm_verify_begin(ctypes.c_uint32(52), ctypes.c_size_t(1 << 40), None, ctypes.c_size_t(0), buf,
                                    buf, None, ctypes.byref(job))
     assert rc == 7 and not job.value
+
+
+def test_scalar_helpers_match_python():
+    """bpp_scalar_invert / bpp_scalar_powers (the caller-side algebra of the
+    IPA's H_factors, circuit_lib.rs:274 and util.rs:138-157 exp_iter) equal
+    Python big-integer arithmetic; zero and non-canonical inputs are refused
+    (host-only entry points: no GPU)."""
+    import hashlib
+
+    import bpperm
+    from bpperm._lib import BppError
+    L = 2**252 + 27742317777372353535851937790883648493
+    for i in range(8):
+        x = int.from_bytes(hashlib.sha256(b"scalar-%d" % i).digest(), "little") % L
+        xb = x.to_bytes(32, "little")
+        assert int.from_bytes(bpperm.scalar_invert(xb), "little") == pow(x, -1, L)
+        pw = bpperm.scalar_powers(xb, 37)
+        assert [int.from_bytes(pw[32 * j: 32 * j + 32], "little") for j in range(37)] == [pow(x, j, L) for j in range(37)]
+    assert bpperm.scalar_powers((5).to_bytes(32, "little"), 0) == b""
+    with pytest.raises(BppError):
+        bpperm.scalar_invert(bytes(32))
+    with pytest.raises(BppError):
+        bpperm.scalar_powers(L.to_bytes(32, "little"), 3)

@@ -4,7 +4,7 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
 tail -1 $O/gpu_tests.txt
 BPP_LIB=bulletproof-perm_amd/bpperm/variants/libbpperm_vst.so timeout -k 10 300 python tools/vs_phases.py > $O/vs_phases.txt 2>&1 || { tail $O/vs_phases.txt; exit 1; }
 cat $O/vs_phases.txt
-for rep in 1 2; do for cfg in "" "BPP_VERIFY_SPLIT=1" "BPP_LIB=bulletproof-perm_amd/bpperm/variants/libbpperm_vs3.so"; do
+for rep in 1 2; do for cfg in "X=1"; do
   env $cfg timeout -k 10 300 python bench.py --no-cpu --proofs-per-gpu 0 --no-extra --steps 10 > $O/bv.json 2> $O/bv.err || { tail $O/bv.err; exit 1; }
   python3 -c "import json;d=json.load(open('$O/bv.json'));v=d['verify_batch'];print('$cfg'.ljust(60),{k:round(x['ms_per_batch'],3) for k,x in v['splits'].items()}, round(v['stage_ms']['verify_scalars'],3))"
 done; done

@@ -28,6 +28,11 @@ bool scalar_is_canonical(const uint8_t* s) {
 }
 
 uint32_t msm_choose_c(double n_per_msm) {
+  static const int c_env = [] {  // (A/B runs: one window size for every MSM)
+    const char* e = getenv("BPP_MSM_C");
+    return e ? atoi(e) : 0;
+  }();
+  if (c_env >= 2 && c_env <= 16) return (uint32_t)c_env;
   uint32_t best = 4;
   double bestc = 1e300;
   // c <= 16: a window's bucket histogram (2^(c-1) x 4 B) fits in LDS

@@ -1233,6 +1233,11 @@ int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label,
       const bool direct = pinned(proofs) && pinned(V);
       uint8_t* stg = nullptr;
       if (!direct) BPP_TRY(ctx_h2d_stage(ctx, count * (plen + vbytes), &stg));
+      static const size_t stage_piece = [] {  // (BPP_VERIFY_PIECE_KB, A/B; 0 = whole parts)
+        const char* e = getenv("BPP_VERIFY_PIECE_KB");
+        const long kb = e ? atol(e) : 1024;
+        return kb > 0 ? (size_t)kb << 10 : SIZE_MAX;
+      }();
       for (size_t q = 0; q < nchunk; ++q) {
         const size_t p0 = count * q / nchunk, p1 = count * (q + 1) / nchunk;
         const size_t po = p0 * plen, pn = (p1 - p0) * plen, vo = count * plen + p0 * vbytes, vn = (p1 - p0) * vbytes;
@@ -1240,10 +1245,18 @@ int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label,
           BPP_HIP(hipMemcpyAsync((uint8_t*)d_in + po, proofs + po, pn, hipMemcpyHostToDevice, ctx->stream));
           BPP_HIP(hipMemcpyAsync((uint8_t*)d_in + vo, V + p0 * vbytes, vn, hipMemcpyHostToDevice, ctx->stream));
         } else {
-          ctx_stage_copy(stg + po, proofs + po, pn);
-          BPP_TRY(ctx_h2d_staged(ctx, (uint8_t*)d_in + po, stg + po, pn));
-          ctx_stage_copy(stg + vo, V + p0 * vbytes, vn);
-          BPP_TRY(ctx_h2d_staged(ctx, (uint8_t*)d_in + vo, stg + vo, vn));
+          // staged in pieces, each piece's DMA behind its host copy: the
+          // copy engine starts after one piece instead of a whole chunk
+          auto staged = [&](size_t o, const uint8_t* src, size_t n) -> int {
+            for (size_t a = 0; a < n; a += stage_piece) {
+              const size_t b = std::min(n, a + stage_piece);
+              ctx_stage_copy(stg + o + a, src + a, b - a);
+              BPP_TRY(ctx_h2d_staged(ctx, (uint8_t*)d_in + o + a, stg + o + a, b - a));
+            }
+            return BPP_OK;
+          };
+          BPP_TRY(staged(po, proofs + po, pn));
+          BPP_TRY(staged(vo, V + p0 * vbytes, vn));
         }
         BPP_HIP(hipEventRecord(ctx->vj_ev_chunk[q], ctx->stream));
         BPP_HIP(hipStreamWaitEvent(kid->stream, ctx->vj_ev_chunk[q], 0));

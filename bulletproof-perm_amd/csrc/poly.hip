@@ -272,11 +272,11 @@ extern "C" int bpp_debug_vs_timing(unsigned long long* out, size_t n) {
 #define VS_T(k)
 #endif
 // Per-proof constants of k_verify_scalars (Montgomery form, VK_N x 8 words
-// a proof), one lane per proof: every product of two workgroup-uniform
-// values is formed here, on the vector unit.  Inside k_verify_scalars such
-// products ran on the scalar unit (uniform operands): 21 K SALU instructions
-// per wave next to 15 K VALU, ~400 spilled SGPRs, and the CU's one scalar
-// unit shared by its waves (r04 PMC, tools/vs_phases.py).
+// a proof): every product of two workgroup-uniform values is formed here, on
+// the vector unit.  Inside k_verify_scalars such products ran on the scalar
+// unit (uniform operands): 21 K SALU instructions per wave next to 15 K VALU,
+// ~400 spilled SGPRs, and the CU's one scalar unit shared by its waves (r04
+// PMC, tools/vs_phases.py).
 //
 // No inverses: proof p's check is scaled by F = U^2 Y, U = prod u_j, Y =
 // y^(n_p - 1) (nonzero: a zero y or u_j rejects the proof in the replay), so
@@ -291,103 +291,180 @@ extern "C" int bpp_debug_vs_timing(unsigned long long* out, size_t n) {
 //   L_j: -F u_j^2;  R_j: -Y prod_{k != j} u_k^2
 // (F times bulletproofs' verification_scalars / the t-check), all times the
 // proof's batch weight w_p = perm::batch_weight(seed, first + p, r_p).
-#define VK_Z 0      // z
-#define VK_Y 1      // y
-#define VK_X 2      // x
-#define VK_WT 3     // w_p, the proof's batch weight
-#define VK_UYA 4    // U Y a
-#define VK_UB 5     // U b
-#define VK_WRX2 6   // w_p r x^2
-#define VK_WRFT 7   // w_p r F t_hat
-#define VK_IB 8     // w_p w F (a b - t_hat)
-#define VK_BB 9     // w_p F (r tau_x + mu)
-#define VK_R 10     // r
-#define VK_NXP 11   // -x_perm
-#define VK_U2 12    // U^2
-#define VK_F 13     // F
-#define VK_WTF 14   // w_p F
-#define VK_WRX2F 15 // w_p r x^2 F
-#define VK_XU2 16   // x U^2
-#define VK_RC 17    // lg values: -w_p Y prod_{k != j} u_k^2 (R_j's scalar)
+#define VK_Z 0       // z
+#define VK_Y 1       // y
+#define VK_X 2       // x
+#define VK_WT 3      // w_p, the proof's batch weight
+#define VK_UYA 4     // w_p U Y a
+#define VK_UB 5      // w_p U b
+#define VK_WRX2 6    // w_p r x^2
+#define VK_WRFT 7    // w_p r F t_hat
+#define VK_IB 8      // w_p w F (a b - t_hat)
+#define VK_BB 9      // w_p F (r tau_x + mu)
+#define VK_R 10      // r
+#define VK_NXP 11    // -x_perm
+#define VK_U2 12     // U^2
+#define VK_F 13      // F
+#define VK_WTF 14    // w_p F
+#define VK_WRX2F 15  // w_p r x^2 F
+#define VK_XU2 16    // w_p x U^2
+#define VK_U2W 17    // w_p U^2
+#define VK_RC 18     // lg values: -w_p Y prod_{k != j} u_k^2 (R_j's scalar)
 #define VK_N(lg) (VK_RC + (lg))
-__global__ void __launch_bounds__(64) k_verify_consts(uint32_t count, uint32_t lg, uint64_t first,
-                                                      const uint32_t* __restrict__ seed,
-                                                      const uint32_t* __restrict__ rec, uint32_t* __restrict__ kc) {
+
+// k_verify_consts works on 16 lanes a proof, 4 proofs a wave, VC_W such
+// waves and one Keccak wave a workgroup.  One lane a proof (round 5's first
+// version) ran every product of a proof on one lane: ~100 dependent scalar
+// multiplies plus the sponge, 67 us for 4096 proofs on 64 waves.  Here the
+// proof's multiplies are spread over its 16 lanes in dependency levels: the
+// R_j products prod_{k != j} u_k^2, U = prod u_k and Y = y^(2^lg - 1) as one
+// lg-step loop (one lane each), the named constants in four levels of at most
+// 10 independent products (a table of (op, dst, a, b) per lane), and the
+// batch weight's SHAKE256 on the Keccak wave while the loop runs.  Values
+// travel through LDS slots (VC_*), the first VK_RC of which are the VK_*
+// outputs.
+#define VC_W 2
+#define VC_P (4 * VC_W)  // proofs a workgroup
+#define VC_LGMAX 32
+#define VC_T_U 18
+#define VC_T_YR 19
+#define VC_T_A 20
+#define VC_T_B 21
+#define VC_T_TH 22
+#define VC_T_W 23
+#define VC_T_TAUX 24
+#define VC_T_MU 25
+#define VC_T_WR 26
+#define VC_T_X2 27
+#define VC_T_AB 28
+#define VC_T_RT 29
+#define VC_T_WU 30
+#define VC_T_WY 31
+#define VC_T_WX 32
+#define VC_T_RTH 33
+#define VC_T_ABT 34
+#define VC_T_RTM 35
+#define VC_T_NWY 36
+#define VC_T_WUA 37
+#define VC_T_IBT 38
+#define VC_NV 39
+enum : uint8_t { VC_NOP = 0, VC_MUL, VC_ADD, VC_SUB, VC_NEG };
+// level l, lane k: {op, dst, a, b}
+__constant__ uint8_t vc_prog[4][16][4] = {
+    {{VC_MUL, VK_U2, VC_T_U, VC_T_U},
+     {VC_MUL, VC_T_WR, VK_WT, VK_R},
+     {VC_MUL, VC_T_X2, VK_X, VK_X},
+     {VC_MUL, VC_T_AB, VC_T_A, VC_T_B},
+     {VC_MUL, VC_T_RT, VK_R, VC_T_TAUX},
+     {VC_MUL, VC_T_WU, VK_WT, VC_T_U},
+     {VC_MUL, VC_T_WY, VK_WT, VC_T_YR},
+     {VC_MUL, VC_T_WX, VK_WT, VK_X},
+     {VC_MUL, VC_T_RTH, VK_R, VC_T_TH}},
+    {{VC_MUL, VK_F, VK_U2, VC_T_YR},
+     {VC_MUL, VK_WRX2, VC_T_WR, VC_T_X2},
+     {VC_MUL, VC_T_WUA, VC_T_WU, VC_T_A},
+     {VC_MUL, VK_UB, VC_T_WU, VC_T_B},
+     {VC_MUL, VK_XU2, VC_T_WX, VK_U2},
+     {VC_MUL, VK_U2W, VK_WT, VK_U2},
+     {VC_MUL, VK_WTF, VC_T_WY, VK_U2},
+     {VC_SUB, VC_T_ABT, VC_T_AB, VC_T_TH},
+     {VC_ADD, VC_T_RTM, VC_T_RT, VC_T_MU},
+     {VC_NEG, VC_T_NWY, VC_T_WY, 0}},
+    {{VC_MUL, VK_UYA, VC_T_WUA, VC_T_YR},
+     {VC_MUL, VK_WRFT, VK_WTF, VC_T_RTH},
+     {VC_MUL, VC_T_IBT, VC_T_W, VC_T_ABT},
+     {VC_MUL, VK_BB, VK_WTF, VC_T_RTM},
+     {VC_MUL, VK_WRX2F, VK_WRX2, VK_F}},
+    {{VC_MUL, VK_IB, VK_WTF, VC_T_IBT}},
+};
+// (record slot, value slot) of the loaded proof values
+__constant__ uint8_t vc_load[11][2] = {{VREC_Z, VK_Z},     {VREC_Y, VK_Y},         {VREC_X, VK_X},
+                                       {VREC_R, VK_R},     {VREC_XPERM, VK_NXP},   {VREC_A, VC_T_A},
+                                       {VREC_B, VC_T_B},   {VREC_THAT, VC_T_TH},   {VREC_W, VC_T_W},
+                                       {VREC_TAUX, VC_T_TAUX}, {VREC_MU, VC_T_MU}};
+__global__ void __launch_bounds__(64 * (VC_W + 1)) k_verify_consts(uint32_t count, uint32_t lg, uint64_t first,
+                                                                   const uint32_t* __restrict__ seed,
+                                                                   const uint32_t* __restrict__ rec,
+                                                                   uint32_t* __restrict__ kc) {
   __builtin_amdgcn_s_setprio(3);  // (latency chain; the decompression runs beside it)
-  const uint32_t p = blockIdx.x * 64 + threadIdx.x;
-  if (p >= count) return;
+  __shared__ __attribute__((aligned(16))) uint32_t vs[VC_P][VC_NV * 8];
+  __shared__ __attribute__((aligned(16))) uint32_t ut[VC_P][VC_LGMAX * 8], u2t[VC_P][VC_LGMAX * 8],
+      pjt[VC_P][VC_LGMAX * 8];
   const uint32_t nrec = VREC_U + lg;
+  const bool kwave = threadIdx.x >= 64 * VC_W;
+  const uint32_t g = (threadIdx.x >> 4) & (VC_P - 1), l = threadIdx.x & 15u;
+  const uint32_t p = blockIdx.x * VC_P + g;
+  const bool live = !kwave && p < count;
   const uint32_t* R = rec + (size_t)p * nrec * 8;
-  uint32_t* K = kc + (size_t)p * VK_N(lg) * 8;
-  // w_p = from_wide(SHAKE256("bp-perm-batch-wt" || seed || le64(first + p) ||
-  // r_p)[0..64]): 88 bytes, one sponge block (perm::batch_weight)
-  sc wt;
-  {
+  uint32_t* V = vs[g];
+  const sc oneR = sc_one_mont();
+  auto ldv = [&](uint32_t k) { return sc_load(V + 8 * k); };
+  if (live) {
+    if (l < 11) {
+      sc v = sc_to_mont(sc_load(R + 8 * vc_load[l][0]));
+      if (vc_load[l][1] == VK_NXP) v = sc_neg(v);
+      sc_store(V + 8 * vc_load[l][1], v);
+    }
+    for (uint32_t j = l; j < lg; j += 16) {
+      const sc u = sc_to_mont(sc_load(R + 8 * (VREC_U + j)));
+      sc_store(ut[g] + 8 * j, u);
+      sc_store(u2t[g] + 8 * j, sc_mont(u, u));
+    }
+  }
+  __syncthreads();
+  if (live) {
+    // lanes j < lg: prod_{k != j} u_k^2; lane lg: U; lane lg + 1: Y
+    const sc yR = ldv(VK_Y);
+    for (uint32_t jj = l; jj < lg + 2; jj += 16) {
+      const bool isY = jj == lg + 1, isU = jj == lg;
+      sc v = oneR;
+      for (uint32_t k = 0; k < lg; ++k) {
+        const sc f = isY ? v : isU ? sc_load(ut[g] + 8 * k) : k == jj ? oneR : sc_load(u2t[g] + 8 * k);
+        v = sc_mont(v, f);
+        if (isY) v = sc_mont(v, yR);
+      }
+      sc_store(isY ? V + 8 * VC_T_YR : isU ? V + 8 * VC_T_U : pjt[g] + 8 * jj, v);
+    }
+  } else if (kwave && (threadIdx.x & 63u) < VC_P && blockIdx.x * VC_P + (threadIdx.x & 63u) < count) {
+    // w_p = from_wide(SHAKE256("bp-perm-batch-wt" || seed || le64(first + p) ||
+    // r_p)[0..64]): 88 bytes, one sponge block (perm::batch_weight)
+    const uint32_t q = threadIdx.x & 63u, pq = blockIdx.x * VC_P + q;
     uint64_t a[25];
     _Pragma("unroll") for (int i = 0; i < 25; ++i) a[i] = 0;
     a[0] = 0x6d7265702d7062ull | (0x2dull << 56);  // "bp-perm-"
     a[1] = 0x74772d6863746162ull;                 // "batch-wt"
     _Pragma("unroll") for (int i = 0; i < 4; ++i) a[2 + i] = (uint64_t)seed[2 * i] | ((uint64_t)seed[2 * i + 1] << 32);
-    a[6] = first + p;
-    const uint32_t* rp = R + 8 * VREC_R;
+    a[6] = first + pq;
+    const uint32_t* rp = rec + ((size_t)pq * nrec + VREC_R) * 8;
     _Pragma("unroll") for (int i = 0; i < 4; ++i) a[7 + i] = (uint64_t)rp[2 * i] | ((uint64_t)rp[2 * i + 1] << 32);
-    a[11] = 0x1full;         // SHAKE domain byte at 88
-    a[16] = 0x80ull << 56;   // last byte of the 136-byte rate
+    a[11] = 0x1full;        // SHAKE domain byte at 88
+    a[16] = 0x80ull << 56;  // last byte of the 136-byte rate
     keccak_f1600_dev(a);
     uint32_t o[16];
     _Pragma("unroll") for (int i = 0; i < 8; ++i) {
       o[2 * i] = (uint32_t)a[i];
       o[2 * i + 1] = (uint32_t)(a[i] >> 32);
     }
-    wt = sc_from_wide_w(o);
+    sc_store(vs[q] + 8 * VK_WT, sc_to_mont(sc_from_wide_w(o)));
   }
-  auto ldm = [&](uint32_t k) { return sc_to_mont(sc_load(R + 8 * k)); };
-  const sc xR = ldm(VREC_X), yR = ldm(VREC_Y), wtR = sc_to_mont(wt), rR = ldm(VREC_R), aR = ldm(VREC_A),
-           bR = ldm(VREC_B), thR = ldm(VREC_THAT);
-  sc UR = ldm(VREC_U);
-  for (uint32_t j = 1; j < lg; ++j) UR = sc_mont(UR, ldm(VREC_U + j));
-  // R_j's scalar -w_p Y prod_{k != j} u_k^2 from prefix and suffix products
-  // of the u_k^2 (here, one lane per proof, instead of a 13-multiply chain on
-  // one lane of every k_verify_scalars workgroup); the prefixes wait in the
-  // slots, the suffix runs downwards
-  {
-    sc pre = sc_one_mont();
-    for (uint32_t j = 0; j < lg; ++j) {
-      sc_store(K + 8 * (VK_RC + j), pre);
-      const sc u = ldm(VREC_U + j);
-      pre = sc_mont(pre, sc_mont(u, u));
+  __syncthreads();
+  for (uint32_t lv = 0; lv < 4; ++lv) {
+    if (live && vc_prog[lv][l][0] != VC_NOP) {
+      const uint8_t op = vc_prog[lv][l][0];
+      const sc x = ldv(vc_prog[lv][l][2]), y = ldv(vc_prog[lv][l][3]);
+      const sc r = op == VC_MUL ? sc_mont(x, y) : op == VC_ADD ? sc_add(x, y) : op == VC_SUB ? sc_sub(x, y) : sc_neg(x);
+      sc_store(V + 8 * vc_prog[lv][l][1], r);
     }
+    if (lv == 2 && live) {
+      const sc nwy = ldv(VC_T_NWY);
+      for (uint32_t j = l; j < lg; j += 16) sc_store(kc + ((size_t)p * VK_N(lg) + VK_RC + j) * 8,
+                                                     sc_mont(sc_load(pjt[g] + 8 * j), nwy));
+    }
+    __syncthreads();
   }
-  sc YR = yR;  // y^(2^lg - 1) = y^(n_p - 1)
-  for (uint32_t j = 1; j < lg; ++j) YR = sc_mont(sc_mont(YR, YR), yR);
-  const sc U2R = sc_mont(UR, UR), FR = sc_mont(U2R, YR);
-  const sc wrR = sc_mont(wtR, rR), wtfR = sc_mont(wtR, FR);
-  const sc wrx2R = sc_mont(wrR, sc_mont(xR, xR));
-  sc_store(K + 8 * VK_Z, ldm(VREC_Z));
-  sc_store(K + 8 * VK_Y, yR);
-  sc_store(K + 8 * VK_X, xR);
-  sc_store(K + 8 * VK_WT, wtR);
-  sc_store(K + 8 * VK_UYA, sc_mont(sc_mont(UR, YR), aR));
-  sc_store(K + 8 * VK_UB, sc_mont(UR, bR));
-  sc_store(K + 8 * VK_WRX2, wrx2R);
-  sc_store(K + 8 * VK_WRFT, sc_mont(sc_mont(wrR, FR), thR));
-  sc_store(K + 8 * VK_IB, sc_mont(wtfR, sc_mont(ldm(VREC_W), sc_sub(sc_mont(aR, bR), thR))));
-  sc_store(K + 8 * VK_BB, sc_mont(wtfR, sc_add(sc_mont(rR, ldm(VREC_TAUX)), ldm(VREC_MU))));
-  sc_store(K + 8 * VK_R, rR);
-  sc_store(K + 8 * VK_NXP, sc_neg(ldm(VREC_XPERM)));
-  sc_store(K + 8 * VK_U2, U2R);
-  sc_store(K + 8 * VK_F, FR);
-  sc_store(K + 8 * VK_WTF, wtfR);
-  sc_store(K + 8 * VK_WRX2F, sc_mont(wrx2R, FR));
-  sc_store(K + 8 * VK_XU2, sc_mont(xR, U2R));
-  {
-    const sc nwy = sc_neg(sc_mont(wtR, YR));
-    sc suf = sc_one_mont();
-    for (uint32_t j = lg; j-- > 0;) {
-      sc_store(K + 8 * (VK_RC + j), sc_mont(sc_mont(sc_load(K + 8 * (VK_RC + j)), suf), nwy));
-      const sc u = ldm(VREC_U + j);
-      suf = sc_mont(suf, sc_mont(u, u));
-    }
+  if (live) {
+    uint32_t* K = kc + (size_t)p * VK_N(lg) * 8;
+    for (uint32_t w = l; w < VK_RC * 8; w += 16) K[w] = V[w];
   }
 }
 
@@ -441,7 +518,8 @@ __global__ void __launch_bounds__(POLY_T) __attribute__((amdgpu_waves_per_eu(VS_
       }
     return v;
   };
-  const sc uyaR = ldk(VK_UYA), ubR = ldk(VK_UB), xu2R = ldk(VK_XU2), wtR = ldk(VK_WT), u2R = ldk(VK_U2), fR = ldk(VK_F);
+  // (weighted: w_p folded into the constants)
+  const sc uyaR = ldk(VK_UYA), ubR = ldk(VK_UB), xu2R = ldk(VK_XU2), u2R = ldk(VK_U2W), fR = ldk(VK_WTF);
   // gate i = n_p - 1 - e with e ascending per lane: yr_i = y^e = yt[e mod
   // POW_LO] (y^POW_LO)^(e / POW_LO), the second factor a running product
   // (blockDim = POW_LO whenever n_p > POW_LO)
@@ -464,8 +542,8 @@ __global__ void __launch_bounds__(POLY_T) __attribute__((amdgpu_waves_per_eu(VS_
     const sc gi = sc_sub(sc_mont(s_of(i), uyaR), sc_mont(rw, xu2R));
     const sc hi = sc_add(sc_mont(sc_sub(sc_sub(sc_mont(s_of(e), ubR), sc_mont(zWL, xu2R)), sc_mont(zWO, u2R)), yr),
                          fR);
-    sc_store(gen + 8 * (gb + i), sc_from_mont(sc_mont(gi, wtR)));
-    sc_store(gen + 8 * (gb + n_p + i), sc_from_mont(sc_mont(hi, wtR)));
+    sc_store(gen + 8 * (gb + i), sc_from_mont(gi));
+    sc_store(gen + 8 * (gb + n_p + i), sc_from_mont(hi));
   }
   VS_T(2);
   for (uint32_t q = threadIdx.x; q < Q; q += blockDim.x) {
@@ -514,7 +592,8 @@ __global__ void __launch_bounds__(POLY_T) __attribute__((amdgpu_waves_per_eu(VS_
   VS_T(6);
   if (threadIdx.x == 0) {
     // B: wt (r F t_hat - r x^2 (delta' + F zc) + w F (a b - t_hat)); B_blinding: wt F (r tau_x + mu)
-    const sc tB = sc_sub(ldk(VK_WRFT), sc_mont(ldk(VK_WRX2), sc_add(sc_mont(u2R, acc[0]), sc_mont(fR, acc[1]))));
+    const sc tB =
+        sc_sub(ldk(VK_WRFT), sc_mont(ldk(VK_WRX2), sc_add(sc_mont(ldk(VK_U2), acc[0]), sc_mont(ldk(VK_F), acc[1]))));
     sc_store(gen + 8 * (gb + 2 * n_p), sc_from_mont(sc_add(tB, ldk(VK_IB))));
     sc_store(gen + 8 * (gb + 2 * n_p + 1), sc_from_mont(ldk(VK_BB)));
   }
@@ -844,11 +923,13 @@ int verify_scalars_dev_rec(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count,
   BPP_TRY(ctx_h2d_const(ctx, "vs_c", d_c, cw.data(), cw.size() * 4));
   const unsigned nt = poly_block(std::max(C.n_p, C.m));
   const size_t lds = ((size_t)C.Q + 1 + 2 * std::min(C.n_p, (uint32_t)POW_LO)) * 32 + (POLY_T / 64) * 2 * 32;
+  if (C.lg > VC_LGMAX) return BPP_ERR_LEN;  // (k_verify_consts' LDS tables)
   void* d_kc = nullptr;
   BPP_TRY(ctx_ws(ctx, "vs_kc", (size_t)count * VK_N(C.lg) * 32, &d_kc));
   {
     ProfScope ps(ctx, "verify_scalars");
-    hipLaunchKernelGGL(k_verify_consts, dim3((count + 63) / 64), dim3(64), 0, ctx->stream, count, C.lg, first, seed,
+    hipLaunchKernelGGL(k_verify_consts, dim3((count + VC_P - 1) / VC_P), dim3(64 * (VC_W + 1)), 0, ctx->stream, count,
+                       C.lg, first, seed,
                        d_rec, (uint32_t*)d_kc);
     hipLaunchKernelGGL(k_verify_scalars, dim3(count), dim3(nt), lds, ctx->stream, C.n_p, C.m, C.Q, C.lg, d_rec,
                        (const uint32_t*)d_kc, (const uint32_t*)d_cp, (const uint32_t*)d_ce, (const uint32_t*)d_c,

@@ -552,6 +552,20 @@ class PermProver:
         check(rc, "bpp_perm_verify_partial_gathered", self.ctx.h)
         return part.raw
 
+    def verify_partial_sharded(self, job: "VerifyJob", first: int, d_blocks: int, stride: int, d_pblocks: int,
+                               pstride: int, counts: Sequence[int], w_begin: int, w_end: int) -> bytes:
+        """128-B raw partial of the whole batch's MSM over windows [w_begin,
+        w_end), from every slice's scalar block (d_blocks + s * stride) and
+        decompressed point block (d_pblocks + s * pstride) gathered in slice
+        order; job = this rank's job over its own slice, batch proofs [first,
+        first + job.count) (bpp_perm_verify_partial_sharded)."""
+        part = C.create_string_buffer(128)
+        cn = (C.c_size_t * max(len(counts), 1))(*counts)
+        check(self.ctx.lib.bpp_perm_verify_partial_sharded(self.ctx.h, self.gens.h, job.h, first, d_blocks, stride,
+                                                           d_pblocks, pstride, cn, len(counts), w_begin, w_end, part),
+              "bpp_perm_verify_partial_sharded", self.ctx.h)
+        return part.raw
+
     def verify_partial(self, job: "VerifyJob", seed: bytes, first: int, w_begin: int, w_end: int) -> bytes:
         """128-B raw partial of job's MSM over windows [w_begin, w_end) (see
         bpp_perm_verify_partial); seed = the batch's 32 verifier-random bytes
@@ -612,12 +626,27 @@ class VerifyJob:
     def slice_bytes(self) -> int:
         return int(self.lib.bpp_perm_verify_slice_bytes(self.h))
 
-    def slice_scalars(self, seed: bytes, d_out: int):
+    def slice_scalars(self, seed: bytes, d_out: int, first: int = 0):
         """The replayed slice's MSM scalars into device memory d_out
-        (slice_bytes() bytes; bpp_perm_verify_slice_scalars), weighted from
-        the batch's verifier seed."""
-        check(self.lib.bpp_perm_verify_slice_scalars(self.ctx.h, self.h, _seed(seed), d_out),
-              "bpp_perm_verify_slice_scalars", self.ctx.h)
+        (slice_bytes() bytes; bpp_perm_verify_slice_scalars_at), weighted from
+        the batch's verifier seed; first = the batch index of the job's first
+        proof (0 for a job over the whole batch with a replay slice)."""
+        check(self.lib.bpp_perm_verify_slice_scalars_at(self.ctx.h, self.h, _seed(seed), first, d_out),
+              "bpp_perm_verify_slice_scalars_at", self.ctx.h)
+
+    def point_bytes(self) -> int:
+        """Bytes of the job's decompressed proof points (128 per point)."""
+        return int(self.lib.bpp_perm_verify_slice_point_bytes(self.h))
+
+    def slice_points(self, d_out: int) -> bool:
+        """The job's decompressed proof points into device memory d_out
+        (point_bytes() bytes; bpp_perm_verify_slice_points); False if a
+        point did not decode."""
+        rc = self.lib.bpp_perm_verify_slice_points(self.ctx.h, self.h, d_out)
+        if rc == 6:
+            return False
+        check(rc, "bpp_perm_verify_slice_points", self.ctx.h)
+        return True
 
     @property
     def ok(self) -> bool:

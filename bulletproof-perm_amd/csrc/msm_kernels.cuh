@@ -506,13 +506,17 @@ __global__ void __launch_bounds__(RED_T) k_msm_reduce_final(const uint32_t* __re
 // issue slots: 12 scan / butterfly additions per 8 buckets instead of per
 // 16); alone the reduce takes 0.233 vs 0.170 ms and L = 32 0.339 ms
 // (0.899 / 0.904 pipelined).  An MSM that runs alone (bpp_msm, the verifier's
-// single MSM) has idle SIMDs to spare and uses L = 4: four times the waves,
-// half the serial chain (msm_single_dev).
+// single MSM) has idle SIMDs to spare and uses L = 8: twice the waves of the
+// stream shape, 2/3 of its serial chain (msm_single_dev; config 5's 17 x 2^14
+// buckets, two interleaved passes: reduce 0.159-0.166 ms at L = 8 against
+// 0.205-0.209 at L = 4, 0.231-0.234 at 2, 0.228-0.231 at 16, 0.363-0.387 at
+// 32 -- the 12 scan / butterfly additions per lane, not the chain, set the
+// cost; profiles/r05_reduce_l_ab.txt).
 #ifndef RWAVE_LOG
 #define RWAVE_LOG 4  // log2 buckets per lane (MSM streams)
 #endif
 #ifndef RWAVE_LOG_LONE
-#define RWAVE_LOG_LONE 2  // log2 buckets per lane when the MSM runs alone (latency)
+#define RWAVE_LOG_LONE 3  // log2 buckets per lane when the MSM runs alone (latency)
 #endif
 #define RWAVE_L (1 << RWAVE_LOG)
 #define RWAVE_SHIFT (RWAVE_LOG + 6)  // log2(RWAVE_L * 64)

@@ -1310,7 +1310,8 @@ int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label,
 // proofs weighted by perm::batch_weight(seed, rfirst + p, r_p), the generator
 // scalars summed over the slice and the slice's proof-point scalars ->
 // d_out = [NG | rcount x npt] x 32 B (device memory).
-int verify_slice_scalars_dev(bpp_ctx* ctx, const bpp_verify_job& J, const uint8_t seed[32], uint32_t* d_out) {
+int verify_slice_scalars_dev(bpp_ctx* ctx, const bpp_verify_job& J, const uint8_t seed[32], size_t first,
+                             uint32_t* d_out) {
   if (J.dctx != ctx || J.dgen != ctx->vjob_gen) {
     ctx->err = "device verify job belongs to another context or was superseded by a later begin";
     return BPP_ERR_ARG;
@@ -1323,8 +1324,35 @@ int verify_slice_scalars_dev(bpp_ctx* ctx, const bpp_verify_job& J, const uint8_
   BPP_TRY(ctx_ws(ctx, "vj_rec", (J.rcount + 1) * vrec_n(J.C) * 32, &d_rec));
   uint32_t* h_seed = nullptr;
   BPP_TRY(ctx_zc_in(ctx, "vj_seed", seed, 32, &h_seed));
-  BPP_TRY(verify_scalars_dev_rec(ctx, J.C, (uint32_t)J.rcount, (const uint32_t*)d_rec, h_seed, J.rfirst, d_out));
+  BPP_TRY(verify_scalars_dev_rec(ctx, J.C, (uint32_t)J.rcount, (const uint32_t*)d_rec, h_seed, first + J.rfirst,
+                                 d_out));
   return ctx_sync(ctx);
+}
+
+// A job's decompressed proof points (bpp_perm_verify_slice_points): count x
+// npt extended-Niels records (MSM_NIELS_WORDS words each, proof-major) ->
+// d_out, after the job's decompression; BPP_ERR_VERIFY if a point did not
+// decode.  Synchronises ctx.
+int verify_slice_points_dev(bpp_ctx* ctx, const bpp_verify_job& J, void* d_out) {
+  if (J.dctx != ctx || J.dgen != ctx->vjob_gen) {
+    ctx->err = "device verify job belongs to another context or was superseded by a later begin";
+    return BPP_ERR_ARG;
+  }
+  if (!J.count) return BPP_OK;
+  void *d_x = nullptr, *d_dbad = nullptr;
+  BPP_TRY(ctx_ws(ctx, "vj_x", J.count * J.npt * MSM_NIELS_WORDS * 4, &d_x));
+  BPP_TRY(ctx_ws(ctx, "vj_dbad", 8, &d_dbad));
+  uint64_t* h_dbad = nullptr;
+  BPP_TRY(ctx_zc_out(ctx, "vj_dbad_h", 8, (uint32_t**)&h_dbad));
+  BPP_HIP(hipStreamWaitEvent(ctx->stream, ctx->vj_ev_dec, 0));
+  BPP_HIP(hipMemcpyAsync(h_dbad, d_dbad, 8, hipMemcpyDeviceToHost, ctx->stream));
+  BPP_HIP(hipMemcpyAsync(d_out, d_x, J.count * J.npt * MSM_NIELS_WORDS * 4, hipMemcpyDeviceToDevice, ctx->stream));
+  BPP_TRY(ctx_sync(ctx));
+  if (*h_dbad != ~0ull) {
+    ctx->err = "undecodable proof point at index " + std::to_string(*h_dbad);
+    return BPP_ERR_VERIFY;
+  }
+  return BPP_OK;
 }
 
 // The MSM of a sliced job over windows [wb, we) with the scalars of every
@@ -1380,6 +1408,66 @@ int verify_partial_gathered_dev(bpp_ctx* ctx, const bpp_gens* G, const bpp_verif
     return BPP_ERR_VERIFY;
   }
   return BPP_OK;
+}
+
+// The MSM of a sharded batch over windows [wb, we) (bpp_perm_verify_partial_sharded):
+// slice s's scalar block at d_blocks + s stride ([NG | counts[s] x npt], as
+// verify_partial_gathered_dev) and its decompressed points at d_pblocks + s
+// pstride (counts[s] x npt Niels records, bpp_perm_verify_slice_points); J is
+// this rank's job over its own slice, batch proofs [first, first + J.count).
+int verify_partial_sharded_dev(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J, size_t first,
+                               const uint8_t* d_blocks, size_t stride, const uint8_t* d_pblocks, size_t pstride,
+                               const size_t* counts, size_t nslices, uint32_t wb, uint32_t we, h25519::ge* out) {
+  if (J.dctx != ctx || J.dgen != ctx->vjob_gen) {
+    ctx->err = "device verify job belongs to another context or was superseded by a later begin";
+    return BPP_ERR_ARG;
+  }
+  if (J.rcount != J.count) {
+    ctx->err = "a sharded batch takes one whole job per slice (bpp_perm_verify_begin_dev on the slice)";
+    return BPP_ERR_ARG;
+  }
+  if (G->n < J.C.n_p) {
+    ctx->err = "generators shorter than the padded circuit";
+    return BPP_ERR_LEN;
+  }
+  const size_t NG = 2 * (size_t)J.C.n_p + 2, npt = J.npt, prec = (size_t)MSM_NIELS_WORDS * 4;
+  size_t total = 0;
+  bool mine = false, tight = true;  // (tight: the point blocks already lie end to end)
+  for (size_t r = 0; r < nslices; ++r) {
+    if ((NG + counts[r] * npt) * 32 > stride || counts[r] * npt * prec > pstride) return BPP_ERR_ARG;
+    mine |= total == first && counts[r] == J.count;
+    tight &= r + 1 == nslices || counts[r] * npt * prec == pstride;
+    total += counts[r];
+  }
+  if (stride % 16 || pstride % 16 || total > (1u << 26)) return BPP_ERR_ARG;
+  if (!mine) {
+    ctx->err = "the gathered blocks do not hold this job's slice at its proof offset";
+    return BPP_ERR_ARG;
+  }
+  const size_t T = NG + total * npt;
+  void* d_sv = nullptr;
+  BPP_TRY(ctx_ws(ctx, "pv_s", T * 32 + 32, &d_sv));
+  BPP_TRY(verify_sum_blocks_dev(ctx, (uint32_t)nslices, (uint32_t)NG, (const uint32_t*)d_blocks,
+                                (uint32_t)(stride / 4), (uint32_t*)d_sv));
+  const uint8_t* d_x = d_pblocks;
+  if (!tight) {
+    void* d = nullptr;
+    BPP_TRY(ctx_ws(ctx, "vj_xg", total * npt * prec, &d));
+    d_x = (const uint8_t*)d;
+  }
+  size_t off = 0;
+  for (size_t r = 0; r < nslices; ++r) {
+    if (counts[r]) {
+      BPP_HIP(hipMemcpyAsync((uint8_t*)d_sv + (NG + off * npt) * 32, d_blocks + r * stride + NG * 32,
+                             counts[r] * npt * 32, hipMemcpyDeviceToDevice, ctx->stream));
+      if (!tight)
+        BPP_HIP(hipMemcpyAsync((uint8_t*)d_x + off * npt * prec, d_pblocks + r * pstride, counts[r] * npt * prec,
+                               hipMemcpyDeviceToDevice, ctx->stream));
+    }
+    off += counts[r];
+  }
+  BPP_TRY(verify_msm(ctx, G, J.C, total, (const uint32_t*)d_sv, (const uint32_t*)d_x, wb, we, out));
+  return ctx_sync(ctx);
 }
 
 // pass 2 of a device job: each proof's weight perm::batch_weight(seed,
@@ -1714,10 +1802,48 @@ size_t bpp_perm_verify_slice_bytes(const bpp_verify_job* job) {
 }
 
 int bpp_perm_verify_slice_scalars(bpp_ctx* ctx, const bpp_verify_job* job, const uint8_t seed[32], void* d_out) {
+  return bpp_perm_verify_slice_scalars_at(ctx, job, seed, 0, d_out);
+}
+
+int bpp_perm_verify_slice_scalars_at(bpp_ctx* ctx, const bpp_verify_job* job, const uint8_t seed[32], size_t first,
+                                     void* d_out) {
   return bpp_guard(ctx, [&]() -> int {
-    if (!ctx || !job || !d_out || !seed || !job->dev) return BPP_ERR_ARG;
+    if (!ctx || !job || !d_out || !seed || !job->dev || first > (1u << 26)) return BPP_ERR_ARG;
     BPP_HIP(hipSetDevice(ctx->device));
-    return verify_slice_scalars_dev(ctx, *job, seed, (uint32_t*)d_out);
+    return verify_slice_scalars_dev(ctx, *job, seed, first, (uint32_t*)d_out);
+  });
+}
+
+size_t bpp_perm_verify_slice_point_bytes(const bpp_verify_job* job) {
+  return job ? job->count * job->npt * MSM_NIELS_WORDS * 4 : 0;
+}
+
+int bpp_perm_verify_slice_points(bpp_ctx* ctx, const bpp_verify_job* job, void* d_out) {
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !job || (!d_out && job->count) || !job->dev) return BPP_ERR_ARG;
+    BPP_HIP(hipSetDevice(ctx->device));
+    return verify_slice_points_dev(ctx, *job, d_out);
+  });
+}
+
+int bpp_perm_verify_partial_sharded(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job* job, size_t first,
+                                    const void* d_blocks, size_t stride, const void* d_pblocks, size_t pstride,
+                                    const size_t* counts, size_t nslices, uint32_t w_begin, uint32_t w_end,
+                                    uint8_t partial[128]) {
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !G || !job || !partial || !job->dev || !nslices || !d_blocks || !d_pblocks || !counts)
+      return BPP_ERR_ARG;
+    size_t total = 0;
+    for (size_t r = 0; r < nslices; ++r) total += counts[r];
+    const uint32_t c = msm_choose_c((double)(2 * (size_t)job->C.n_p + 2 + total * job->npt));
+    if (w_begin > w_end || w_end > (254 + c - 1) / c) return BPP_ERR_ARG;
+    BPP_HIP(hipSetDevice(ctx->device));
+    h25519::ge r = h25519::ge_identity();
+    if (total)
+      BPP_TRY(verify_partial_sharded_dev(ctx, G, *job, first, (const uint8_t*)d_blocks, stride,
+                                         (const uint8_t*)d_pblocks, pstride, counts, nslices, w_begin, w_end, &r));
+    h25519::ge_to_words((uint32_t*)partial, r);
+    return BPP_OK;
   });
 }
 

@@ -371,6 +371,34 @@ int bpp_perm_verify_slice_scalars(bpp_ctx* ctx, const bpp_verify_job* job, const
 int bpp_perm_verify_partial_gathered(bpp_ctx* ctx, const bpp_gens* g, const bpp_verify_job* job,
                                      const void* d_blocks, size_t stride, const size_t* counts, size_t nslices,
                                      uint32_t w_begin, uint32_t w_end, uint8_t partial[128]);
+/* Window split with the upload and decompression sharded too (config 5
+ * over N GPUs, "windows_sharded").  Rank r of N, slice
+ * [first, first + n) of the batch:
+ *   1. bpp_perm_verify_begin_dev over the slice's proofs and V only (each
+ *      rank uploads, decompresses and replays 1/N of the batch);
+ *   2. bpp_perm_verify_slice_points copies the slice's decompressed points
+ *      (bpp_perm_verify_slice_point_bytes(job): n x npt records of 128 B,
+ *      proof-major) to device memory d_out; BPP_ERR_VERIFY if one did not
+ *      decode; synchronises ctx;
+ *   3. bpp_perm_verify_slice_scalars_at(job, seed, first) writes the slice's
+ *      scalar block as bpp_perm_verify_slice_scalars, the proofs weighted as
+ *      batch proofs first + p;
+ *   4. the point blocks (pstride bytes apart) and the scalar blocks (stride
+ *      apart) of all slices are all-gathered into device memory (RCCL
+ *      all_gather over xGMI), slices contiguous and in proof order;
+ *   5. bpp_perm_verify_partial_sharded runs the MSM of ALL proofs over windows
+ *      [w_begin, w_end) from the gathered blocks (job: this rank's slice job,
+ *      which must sit at proof offset `first` among counts[]);
+ *   6. the 128-B partials are exchanged as for bpp_perm_verify_partial;
+ *      a replay reject or an undecodable point on any rank vetoes the batch. */
+int bpp_perm_verify_slice_scalars_at(bpp_ctx* ctx, const bpp_verify_job* job, const uint8_t seed[32], size_t first,
+                                     void* d_out);
+size_t bpp_perm_verify_slice_point_bytes(const bpp_verify_job* job);
+int bpp_perm_verify_slice_points(bpp_ctx* ctx, const bpp_verify_job* job, void* d_out);
+int bpp_perm_verify_partial_sharded(bpp_ctx* ctx, const bpp_gens* g, const bpp_verify_job* job, size_t first,
+                                    const void* d_blocks, size_t stride, const void* d_pblocks, size_t pstride,
+                                    const size_t* counts, size_t nslices, uint32_t w_begin, uint32_t w_end,
+                                    uint8_t partial[128]);
 void bpp_perm_verify_end(bpp_verify_job* job);
 /* BPP_OK if the partials add up to the identity, else BPP_ERR_VERIFY. */
 int bpp_partials_is_identity(const uint8_t* partials, size_t count);

@@ -11,7 +11,9 @@ splits of SURVEY.md §8(e):
 
 * proof split: rank r holds proofs [first, first + count), all windows;
 * window split (north_star): every rank holds every proof, windows
-  window_ranges(W, world)[rank].
+  window_ranges(W, world)[rank];
+* sharded window split: rank r expands its slice only, the slices' scalars
+  and points are all-gathered, then windows window_ranges(W, world)[rank].
 
 Proofs come from the serial C prover (oracle/c/perm_cpu.c, byte-equal to the
 GPU prover in tests/test_gpu_perm.py).  Reference: verify,
@@ -88,7 +90,33 @@ def _worker(rank, world, port, tamper, q):
         wb, we = bdist.window_ranges(W, world)[rank]
         ok_win = bpperm.partials_is_identity(bdist.torch_all_gather_bytes(partial(job, seed, 0, wb, we)))
         job.close()
-        q.put((rank, ok_split, ok_win))
+
+        # sharded window split (bdist.verify_sliced's exchange): each rank
+        # expands its slice only; the slices' scalars (generator part summed,
+        # proof-point part concatenated) and decoded points are all-gathered,
+        # then each rank takes its window range of the whole batch's MSM
+        job = bpperm.VerifyJob(K, proofs[b:e], Vs[b:e])
+        sc, pts = job.scalars(seed, b)
+        job.close()
+        NG = 2 * n_p + 2
+        blob = b"".join(sc) + b"".join(pts)
+        blobs = bdist.torch_all_gather_bytes_var(blob)
+        gen_sum = [0] * NG
+        s_all, p_all = [], []
+        for bl in blobs:
+            n_t = len(bl) // 64 - NG // 2  # (scalar count = NG + points; the blob holds both, 32 B each)
+            sc_r = [bl[32 * i: 32 * i + 32] for i in range(NG + n_t)]
+            pts_r = [bl[32 * (NG + n_t) + 32 * i: 32 * (NG + n_t) + 32 * i + 32] for i in range(n_t)]
+            gen_sum = [(a + int.from_bytes(x, "little")) % r255.L for a, x in zip(gen_sum, sc_r[:NG])]
+            s_all += [int.from_bytes(x, "little") for x in sc_r[NG:]]
+            p_all += pts_r
+        c, W = bpperm.msm_windows(NG + len(p_all))
+        assert W == bdist._batch_windows(K, COUNT)
+        wb, we = bdist.window_ranges(W, world)[rank]
+        P = gens + [r255.decode(p) for p in p_all]
+        part = r255.raw_point_bytes(r255.msm_window_partial(gen_sum + s_all, P, c, W, wb, we))
+        ok_shard = bpperm.partials_is_identity(bdist.torch_all_gather_bytes(part))
+        q.put((rank, ok_split, ok_win, ok_shard))
     finally:
         dist.destroy_process_group()
 
@@ -106,9 +134,10 @@ def test_verify_split_over_gloo(tamper):
         p.join(300)
         assert p.exitcode == 0
     results = sorted(q.get() for _ in range(world))
-    for _, ok_split, ok_win in results:
+    for _, ok_split, ok_win, ok_shard in results:
         assert ok_split == (not tamper)
         assert ok_win == (not tamper)
+        assert ok_shard == (not tamper)
 
 
 def test_verify_job_host_phase_matches_oracle():

@@ -250,3 +250,121 @@ def test_gathered_blocks_out_of_order_refused(setup):
     finally:
         pr.ctx.dev_free(blocks)
         job.close()
+
+
+def _sharded_partials(g, proofs, Vs, ranks, tamper_rank=None, equal_stride=False):
+    """The upload-sharded window split (bpperm.dist.verify_sliced, VERDICT r4
+    item 2) rehearsed on one GPU: one context per rank, each job over its
+    own slice only (its upload, decompression and replay); the point blocks
+    and scalar blocks gathered by concatenation in rank order.  Returns None
+    if a rank's job failed (replay reject or undecodable point)."""
+    import bpperm
+    from bpperm import dist as bdist
+    ctxs = [bpperm.Context(0) for _ in range(ranks)]
+    prs = [bpperm.PermProver(g, K, ctx=c) for c in ctxs]
+    ranges = bdist.point_ranges(len(proofs), ranks)
+    counts = [e - b for b, e in ranges]
+    jobs = [bpperm.VerifyJob(K, proofs[b:e], Vs[b:e], prs[r].label, ctx=ctxs[r]) for r, (b, e) in enumerate(ranges)]
+    blocks = pblocks = None
+    try:
+        if not all(j.ok for j in jobs):
+            return None
+        stride = (bdist._slice_block_bytes(K, max(counts)) + 15) // 16 * 16
+        pstride = max(counts) * bdist._points_per_proof(K) * 128
+        blocks = ctxs[0].dev_alloc(ranks * stride)
+        pblocks = ctxs[0].dev_alloc(ranks * pstride)
+        ctxs[0].htod(blocks, bytes(ranks * stride))
+        for r, (j, (b, e)) in enumerate(zip(jobs, ranges)):
+            assert j.point_bytes() == counts[r] * bdist._points_per_proof(K) * 128
+            if not j.slice_points(pblocks + r * pstride):
+                return None
+            j.slice_scalars(SEED, blocks + r * stride, first=b)
+        if tamper_rank is not None:  # one rank's first point record perturbed after the fact
+            at = pblocks + tamper_rank * pstride
+            b0 = bytearray(ctxs[0].dtoh(at, 16))
+            b0[0] ^= 1
+            ctxs[0].htod(at, bytes(b0))
+        W = bdist._batch_windows(K, len(proofs))
+        return [prs[r].verify_partial_sharded(jobs[r], ranges[r][0], blocks, stride, pblocks, pstride, counts, wb, we)
+                for r, (wb, we) in enumerate(bdist.window_ranges(W, ranks))]
+    finally:
+        if blocks is not None:
+            ctxs[0].dev_free(blocks)
+            ctxs[0].dev_free(pblocks)
+        for j in jobs:
+            j.close()
+        for c in ctxs:
+            c.close()
+
+
+@pytest.mark.parametrize("ranks,n", [(4, 64), (3, 100), (8, 64)])
+def test_upload_sharded_window_split(setup, ranks, n):
+    """the window split with the upload, decompression,
+    replay and scalar expansion all sharded by proof.  The partials add up
+    to the identity exactly when the batch verifies and to the same group
+    element as the plain window split's (unequal slices, n = 100 over 3,
+    exercise the compaction of padded point blocks); a tampered proof, a
+    tampered V or a perturbed gathered point is rejected."""
+    import bpperm
+    g, pr, proofs, Vs = setup
+    if n > len(proofs):
+        more, mv = pr.prove_batch(list(range(700, 700 + n - len(proofs))))
+        proofs, Vs = proofs + more, Vs + mv
+    proofs, Vs = proofs[:n], Vs[:n]
+    parts = _sharded_partials(g, proofs, Vs, ranks)
+    assert bpperm.partials_is_identity(parts)
+    assert not bpperm.partials_is_identity(parts[:-1])
+    # the same element as the plain window split's partial sums, window range by window range
+    plain = _window_partials(pr, proofs, Vs, ranks)
+    assert [bpperm.partials_finish([x]) for x in parts] == [bpperm.partials_finish([x]) for x in plain]
+    bad = list(proofs)
+    b = bytearray(bad[n // 2])
+    b[40] ^= 1  # A_O's encoding: the replay rejects it or its point decodes to another
+    bad[n // 2] = bytes(b)
+    tp = _sharded_partials(g, bad, Vs, ranks)
+    assert tp is None or not bpperm.partials_is_identity(tp)
+    badV = list(Vs)
+    v = bytearray(badV[1])
+    v[33] ^= 2
+    badV[1] = bytes(v)
+    tv = _sharded_partials(g, proofs, badV, ranks)
+    assert tv is None or not bpperm.partials_is_identity(tv)
+    assert not bpperm.partials_is_identity(_sharded_partials(g, proofs, Vs, ranks, tamper_rank=ranks - 1))
+
+
+def test_sharded_blocks_out_of_order_refused(setup):
+    """bpp_perm_verify_partial_sharded checks that the job's slice sits at
+    its proof offset among the gathered blocks, and refuses a sliced-replay
+    job (those take bpp_perm_verify_partial_gathered)."""
+    import bpperm
+    from bpperm import dist as bdist
+    g, pr, proofs, Vs = setup
+    ranges = bdist.point_ranges(len(proofs), 3)
+    counts = [e - b for b, e in ranges]
+    assert counts == [21, 21, 22]
+    b, e = ranges[0]
+    job = bpperm.VerifyJob(K, proofs[b:e], Vs[b:e], pr.label, ctx=pr.ctx)
+    stride = (bdist._slice_block_bytes(K, max(counts)) + 15) // 16 * 16
+    pstride = max(counts) * bdist._points_per_proof(K) * 128
+    blocks = pr.ctx.dev_alloc(3 * stride)
+    pblocks = pr.ctx.dev_alloc(3 * pstride)
+    sliced = None
+    try:
+        pr.ctx.htod(blocks, bytes(3 * stride))
+        pr.ctx.htod(pblocks, bytes(3 * pstride))
+        assert job.slice_points(pblocks)
+        job.slice_scalars(SEED, blocks, first=0)
+        W = bdist._batch_windows(K, len(proofs))
+        with pytest.raises(bpperm.BppError):  # the slice [0, 21) listed as 22 proofs
+            pr.verify_partial_sharded(job, 0, blocks, stride, pblocks, pstride, counts[::-1], 0, W)
+        with pytest.raises(bpperm.BppError):  # the slice claimed at offset 5 (no slice starts there)
+            pr.verify_partial_sharded(job, 5, blocks, stride, pblocks, pstride, counts, 0, W)
+        sliced = bpperm.VerifyJob(K, proofs, Vs, pr.label, ctx=pr.ctx, replay=(0, 21))
+        with pytest.raises(bpperm.BppError):
+            pr.verify_partial_sharded(sliced, 0, blocks, stride, pblocks, pstride, counts, 0, W)
+    finally:
+        pr.ctx.dev_free(blocks)
+        pr.ctx.dev_free(pblocks)
+        if sliced is not None:
+            sliced.close()
+        job.close()

@@ -590,10 +590,13 @@ class VerifyJob:
     verifier seed (bpp_perm_verify_scalars)."""
 
     def __init__(self, k: int, proofs: Sequence[bytes], Vs: Sequence[bytes], label: bytes = b"bp-perm",
-                 ctx: "Context | None" = None, replay: "tuple[int, int] | None" = None):
+                 ctx: "Context | None" = None, replay: "tuple[int, int] | None" = None, wait: bool = True):
         """replay=(first, n): a sliced device job (bpp_perm_verify_begin_dev_slice):
         every proof uploaded and decompressed, proofs [first, first + n)
-        replayed; `r` then holds the slice's n challenges."""
+        replayed; `r` then holds the slice's n challenges.  wait=False (a
+        device job over all its proofs): bpp_perm_verify_begin_dev_async --
+        returns before the replay ends, `r` is None and a rejected proof
+        surfaces as False from slice_scalars / verify_partial."""
         self.lib = _lib.load()
         self.k = k
         self.count = len(proofs)
@@ -607,6 +610,12 @@ class VerifyJob:
         if ctx is None:
             rc = self.lib.bpp_perm_verify_begin(k, self.count, _buf(label), len(label), pb, vb, r, C.byref(h))
             name = "bpp_perm_verify_begin"
+        elif replay is None and not wait:
+            self._keep = (pb, vb)  # (pinned inputs are read after the return; these are staged, but keep them)
+            rc = self.lib.bpp_perm_verify_begin_dev_async(ctx.h, k, self.count, _buf(label), len(label), pb, vb,
+                                                          C.byref(h))
+            name = "bpp_perm_verify_begin_dev_async"
+            nr = 0
         elif replay is None:
             rc = self.lib.bpp_perm_verify_begin_dev(ctx.h, k, self.count, _buf(label), len(label), pb, vb, r,
                                                     C.byref(h))
@@ -621,18 +630,22 @@ class VerifyJob:
             return
         check(rc, name, ctx.h if ctx is not None else None)
         self.h = h
-        self.r = r.raw[:32 * nr]
+        self.r = r.raw[:32 * nr] if nr else (None if not wait else b"")
 
     def slice_bytes(self) -> int:
         return int(self.lib.bpp_perm_verify_slice_bytes(self.h))
 
-    def slice_scalars(self, seed: bytes, d_out: int, first: int = 0):
+    def slice_scalars(self, seed: bytes, d_out: int, first: int = 0) -> bool:
         """The replayed slice's MSM scalars into device memory d_out
         (slice_bytes() bytes; bpp_perm_verify_slice_scalars_at), weighted from
         the batch's verifier seed; first = the batch index of the job's first
-        proof (0 for a job over the whole batch with a replay slice)."""
-        check(self.lib.bpp_perm_verify_slice_scalars_at(self.ctx.h, self.h, _seed(seed), first, d_out),
-              "bpp_perm_verify_slice_scalars_at", self.ctx.h)
+        proof (0 for a job over the whole batch with a replay slice).  False
+        if an asynchronous begin's replay rejected a proof."""
+        rc = self.lib.bpp_perm_verify_slice_scalars_at(self.ctx.h, self.h, _seed(seed), first, d_out)
+        if rc == 6:
+            return False
+        check(rc, "bpp_perm_verify_slice_scalars_at", self.ctx.h)
+        return True
 
     def point_bytes(self) -> int:
         """Bytes of the job's decompressed proof points (128 per point)."""

@@ -103,6 +103,7 @@ SIGNATURES = {
     "bpp_perm_verify_slice_scalars": (i32, [vp, vp, vp, vp]),
     "bpp_perm_verify_partial_gathered": (i32, [vp, vp, vp, vp, sz, vp, sz, u32, u32, vp]),
     "bpp_perm_verify_slice_scalars_at": (i32, [vp, vp, vp, sz, vp]),
+    "bpp_perm_verify_begin_dev_async": (i32, [vp, u32, sz, vp, sz, vp, vp, vp]),
     "bpp_perm_verify_slice_point_bytes": (sz, [vp]),
     "bpp_perm_verify_slice_points": (i32, [vp, vp, vp]),
     "bpp_perm_verify_partial_sharded": (i32, [vp, vp, vp, sz, vp, sz, vp, sz, vp, sz, u32, u32, vp]),

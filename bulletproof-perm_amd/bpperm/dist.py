@@ -165,24 +165,27 @@ def verify_sliced(prover, proofs, Vs, rank: int, world: int, seed: bytes, gather
     ranges = point_ranges(len(proofs), world)
     b, e = ranges[rank]
     counts = [hi - lo for lo, hi in ranges]
-    # (this rank's slice only: its upload, decompression and replay)
-    job = bpperm.VerifyJob(prover.k, proofs[b:e], Vs[b:e], prover.label, ctx=prover.ctx)
+    stride = (_slice_block_bytes(prover.k, max(counts)) + 15) // 16 * 16
+    pstride = max(counts) * _points_per_proof(prover.k) * 128
+    # (the blocks live on the library context's GPU whatever device the
+    # collectives use; ADVICE r4: not torch's current device)
+    dev = torch.device("cuda", prover.ctx.device)
+    blk = torch.zeros(stride, dtype=torch.uint8, device=dev)
+    pblk = torch.zeros(pstride, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize(dev)  # (the fills run on torch's stream, the library on its own)
+    # this rank's slice only: its upload, decompression and replay, the
+    # replay left running (asynchronous begin) while the decompressed points
+    # go out -- their all-gather (RCCL on torch's stream) overlaps the replay
+    # and the slice's scalar expansion on the library's stream
+    job = bpperm.VerifyJob(prover.k, proofs[b:e], Vs[b:e], prover.label, ctx=prover.ctx, wait=False)
     try:
         ok = job.ok
-        stride = (_slice_block_bytes(prover.k, max(counts)) + 15) // 16 * 16
-        pstride = max(counts) * _points_per_proof(prover.k) * 128
-        # (the blocks live on the library context's GPU whatever device the
-        # collectives use; ADVICE r4: not torch's current device)
-        dev = torch.device("cuda", prover.ctx.device)
-        blk = torch.zeros(stride, dtype=torch.uint8, device=dev)
-        pblk = torch.zeros(pstride, dtype=torch.uint8, device=dev)
-        torch.cuda.synchronize(dev)  # (the fills run on torch's stream, the library on its own)
         if ok:
             assert job.slice_bytes() <= stride and job.point_bytes() <= pstride
-            ok = job.slice_points(pblk.data_ptr())  # (synchronises the library's stream)
-        if ok:
-            job.slice_scalars(seed, blk.data_ptr(), first=b)
+            ok = job.slice_points(pblk.data_ptr())  # (returns once the block is complete)
         pblocks = gather(pblk)
+        if ok:
+            ok = job.slice_scalars(seed, blk.data_ptr(), first=b)  # (False: the replay rejected a proof)
         blocks = gather(blk)
         torch.cuda.synchronize(dev)
         part = bytes(128)

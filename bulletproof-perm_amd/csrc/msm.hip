@@ -127,6 +127,13 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
   // reduce 0.216-0.218 -> 0.194-0.195 ms, accumulate 0.399 -> 0.394-0.398;
   // profiles/r04_verify_k_ab.txt)
   if (rlog == RWAVE_LOG_LONE && K >= 32) K = std::max<uint32_t>(K, 48);
+  // ... and K >= 16 in any case: a window range of a large MSM (the window
+  // split's partial: config 5 over 8 GPUs is 2 windows x 520 K terms, K = 4
+  // by the round rule) otherwise spends its time closing buckets and joining
+  // lane pieces (tools/shard_model.py, rank 0's partial: 0.857 ms at K = 4,
+  // 0.377 at 16, 0.393 at 32, 0.431 at 48; 4 windows: 0.502 at K = 8, 0.421 at
+  // 16, 0.405 at 32; profiles/r05_partial_k_ab.txt)
+  if (rlog == RWAVE_LOG_LONE) K = std::max<uint32_t>(K, 16);
   if (const char* ek = getenv("BPP_MSM_ACC_K")) K = (uint32_t)std::min(128, std::max(4, atoi(ek) & ~3));  // A/B runs
   const size_t lanes = (E_max + K - 1) / K + 1;
   // a heavy bucket spans > FIX_MAX chunks, so holds > (FIX_MAX - 1) K

@@ -1326,7 +1326,16 @@ int verify_slice_scalars_dev(bpp_ctx* ctx, const bpp_verify_job& J, const uint8_
   BPP_TRY(ctx_zc_in(ctx, "vj_seed", seed, 32, &h_seed));
   BPP_TRY(verify_scalars_dev_rec(ctx, J.C, (uint32_t)J.rcount, (const uint32_t*)d_rec, h_seed, first + J.rfirst,
                                  d_out));
-  return ctx_sync(ctx);
+  BPP_TRY(ctx_sync(ctx));
+  if (J.bad_h) {  // an asynchronous begin's replay verdicts (the stream has passed them)
+    uint32_t any = 0;
+    for (size_t p = 0; p < J.rcount; ++p) any |= J.bad_h[p];
+    if (any) {
+      ctx->err = "a proof's transcript replay rejected it";
+      return BPP_ERR_VERIFY;
+    }
+  }
+  return BPP_OK;
 }
 
 // A job's decompressed proof points (bpp_perm_verify_slice_points): count x
@@ -1339,15 +1348,19 @@ int verify_slice_points_dev(bpp_ctx* ctx, const bpp_verify_job& J, void* d_out) 
     return BPP_ERR_ARG;
   }
   if (!J.count) return BPP_OK;
+  // on the decompression's own (child) stream, behind the decompression:
+  // an asynchronous begin's replay may still be running on ctx's stream
+  bpp_ctx* kid = nullptr;
+  BPP_TRY(ctx_child(ctx, VJ_CHILD, &kid));
   void *d_x = nullptr, *d_dbad = nullptr;
   BPP_TRY(ctx_ws(ctx, "vj_x", J.count * J.npt * MSM_NIELS_WORDS * 4, &d_x));
   BPP_TRY(ctx_ws(ctx, "vj_dbad", 8, &d_dbad));
   uint64_t* h_dbad = nullptr;
-  BPP_TRY(ctx_zc_out(ctx, "vj_dbad_h", 8, (uint32_t**)&h_dbad));
-  BPP_HIP(hipStreamWaitEvent(ctx->stream, ctx->vj_ev_dec, 0));
-  BPP_HIP(hipMemcpyAsync(h_dbad, d_dbad, 8, hipMemcpyDeviceToHost, ctx->stream));
-  BPP_HIP(hipMemcpyAsync(d_out, d_x, J.count * J.npt * MSM_NIELS_WORDS * 4, hipMemcpyDeviceToDevice, ctx->stream));
-  BPP_TRY(ctx_sync(ctx));
+  BPP_TRY(ctx_zc_out(kid, "sp_dbad_h", 8, (uint32_t**)&h_dbad));
+  BPP_HIP(hipStreamWaitEvent(kid->stream, ctx->vj_ev_dec, 0));
+  BPP_HIP(hipMemcpyAsync(h_dbad, d_dbad, 8, hipMemcpyDeviceToHost, kid->stream));
+  BPP_HIP(hipMemcpyAsync(d_out, d_x, J.count * J.npt * MSM_NIELS_WORDS * 4, hipMemcpyDeviceToDevice, kid->stream));
+  BPP_TRY(ctx_sync(kid));
   if (*h_dbad != ~0ull) {
     ctx->err = "undecodable proof point at index " + std::to_string(*h_dbad);
     return BPP_ERR_VERIFY;
@@ -1745,6 +1758,20 @@ int bpp_perm_verify_begin_dev(bpp_ctx* ctx, uint32_t k, size_t count, const uint
     std::unique_ptr<bpp_verify_job> job;
     BPP_TRY(verify_begin_dev(ctx, C, label, llen, count, proofs, V, job));
     if (r_out && count) memcpy(r_out, job->rs.data(), 32 * count);
+    *out = job.release();
+    return BPP_OK;
+  });
+}
+
+int bpp_perm_verify_begin_dev_async(bpp_ctx* ctx, uint32_t k, size_t count, const uint8_t* label, size_t llen,
+                                    const uint8_t* proofs, const uint8_t* V, bpp_verify_job** out) {
+  return bpp_guard(ctx, [&]() -> int {
+    if (!ctx || !out || ((!proofs || !V) && count) || (!label && llen) || k < 2 || k > (1u << 20)) return BPP_ERR_ARG;
+    *out = nullptr;
+    BPP_HIP(hipSetDevice(ctx->device));
+    const perm::Circuit C = perm::build(k);
+    std::unique_ptr<bpp_verify_job> job;
+    BPP_TRY(verify_begin_dev(ctx, C, label, llen, count, proofs, V, job, 0, SIZE_MAX, false));
     *out = job.release();
     return BPP_OK;
   });

@@ -374,12 +374,14 @@ int bpp_perm_verify_partial_gathered(bpp_ctx* ctx, const bpp_gens* g, const bpp_
 /* Window split with the upload and decompression sharded too (config 5
  * over N GPUs, "windows_sharded").  Rank r of N, slice
  * [first, first + n) of the batch:
- *   1. bpp_perm_verify_begin_dev over the slice's proofs and V only (each
- *      rank uploads, decompresses and replays 1/N of the batch);
+ *   1. bpp_perm_verify_begin_dev(_async) over the slice's proofs and V only
+ *      (each rank uploads, decompresses and replays 1/N of the batch);
  *   2. bpp_perm_verify_slice_points copies the slice's decompressed points
  *      (bpp_perm_verify_slice_point_bytes(job): n x npt records of 128 B,
  *      proof-major) to device memory d_out; BPP_ERR_VERIFY if one did not
- *      decode; synchronises ctx;
+ *      decode; returns once d_out is complete (it waits for the
+ *      decompression, not for an asynchronous begin's replay), so the point
+ *      blocks' all-gather can run beside the replay and step 3;
  *   3. bpp_perm_verify_slice_scalars_at(job, seed, first) writes the slice's
  *      scalar block as bpp_perm_verify_slice_scalars, the proofs weighted as
  *      batch proofs first + p;
@@ -391,6 +393,15 @@ int bpp_perm_verify_partial_gathered(bpp_ctx* ctx, const bpp_gens* g, const bpp_
  *      which must sit at proof offset `first` among counts[]);
  *   6. the 128-B partials are exchanged as for bpp_perm_verify_partial;
  *      a replay reject or an undecodable point on any rank vetoes the batch. */
+/* bpp_perm_verify_begin_dev without waiting for the replay (no r_out): the
+ * replay's verdicts are checked by the job's next synchronising call
+ * (bpp_perm_verify_slice_scalars(_at) and bpp_perm_verify_partial return
+ * BPP_ERR_VERIFY for a rejected proof); bpp_perm_verify_slice_points can run
+ * meanwhile (it waits for the decompression only).  Pinned input buffers
+ * (bpp_host_alloc) are read by DMA after the return: keep them until that
+ * next synchronising call; pageable ones are staged before it returns. */
+int bpp_perm_verify_begin_dev_async(bpp_ctx* ctx, uint32_t k, size_t count, const uint8_t* label, size_t llen,
+                                    const uint8_t* proofs, const uint8_t* V, bpp_verify_job** out);
 int bpp_perm_verify_slice_scalars_at(bpp_ctx* ctx, const bpp_verify_job* job, const uint8_t seed[32], size_t first,
                                      void* d_out);
 size_t bpp_perm_verify_slice_point_bytes(const bpp_verify_job* job);

@@ -264,7 +264,9 @@ def _sharded_partials(g, proofs, Vs, ranks, tamper_rank=None, equal_stride=False
     prs = [bpperm.PermProver(g, K, ctx=c) for c in ctxs]
     ranges = bdist.point_ranges(len(proofs), ranks)
     counts = [e - b for b, e in ranges]
-    jobs = [bpperm.VerifyJob(K, proofs[b:e], Vs[b:e], prs[r].label, ctx=ctxs[r]) for r, (b, e) in enumerate(ranges)]
+    # (asynchronous begins, as bpperm.dist.verify_sliced: replay verdicts come with slice_scalars)
+    jobs = [bpperm.VerifyJob(K, proofs[b:e], Vs[b:e], prs[r].label, ctx=ctxs[r], wait=False)
+            for r, (b, e) in enumerate(ranges)]
     blocks = pblocks = None
     try:
         if not all(j.ok for j in jobs):
@@ -278,7 +280,8 @@ def _sharded_partials(g, proofs, Vs, ranks, tamper_rank=None, equal_stride=False
             assert j.point_bytes() == counts[r] * bdist._points_per_proof(K) * 128
             if not j.slice_points(pblocks + r * pstride):
                 return None
-            j.slice_scalars(SEED, blocks + r * stride, first=b)
+            if not j.slice_scalars(SEED, blocks + r * stride, first=b):
+                return None
         if tamper_rank is not None:  # one rank's first point record perturbed after the fact
             at = pblocks + tamper_rank * pstride
             b0 = bytearray(ctxs[0].dtoh(at, 16))

@@ -175,6 +175,10 @@ int ctx_zc_out(bpp_ctx* ctx, const char* name, size_t bytes, uint32_t** d);
 int ctx_h2d(bpp_ctx* ctx, void* d, const void* h, size_t bytes);
 // memcpy into / out of the pinned arena, split over the host pool above 512 KB
 void ctx_stage_copy(void* dst, const void* src, size_t bytes);
+// bpp_host_alloc's pinned buffers (ctx.hip): is [p, p + n) inside one?
+void host_pinned_add(const void* p, size_t n);
+void host_pinned_remove(const void* p);
+bool host_is_pinned(const void* p, size_t n);
 // Two host buffers copied back to back into d (one staging copy).
 int ctx_h2d2(bpp_ctx* ctx, void* d, const void* h0, size_t n0, const void* h1, size_t n1);
 // Two-step form for data produced straight into the pinned arena:

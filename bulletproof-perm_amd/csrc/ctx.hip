@@ -1,3 +1,5 @@
+#include <map>
+#include <mutex>
 // Context, workspace, profiling and device-memory entry points of the C ABI.
 #include <execinfo.h>
 #include <malloc.h>
@@ -16,6 +18,41 @@
 // memcpy to / from the pinned arena, split over the copy pool above 512 KB
 // (a 2.6 MB scalar upload is ~0.25 ms on one core of the box; par.h
 // copy_threads)
+// Pinned host buffers handed out by bpp_host_alloc (start -> bytes), so that
+// an entry point can tell them from pageable memory without
+// hipPointerGetAttributes, which walks the runtime's allocation tables
+// (BPP_PIN_QUERY=1: ask the runtime as well, for memory a caller pinned
+// itself with hipHostRegister)
+static std::mutex g_pin_mu;
+static std::map<uintptr_t, size_t> g_pinned;
+void host_pinned_add(const void* p, size_t n) {
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  g_pinned[(uintptr_t)p] = n;
+}
+void host_pinned_remove(const void* p) {
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  g_pinned.erase((uintptr_t)p);
+}
+bool host_is_pinned(const void* p, size_t n) {
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    auto it = g_pinned.upper_bound((uintptr_t)p);
+    if (it != g_pinned.begin()) {
+      --it;
+      if ((uintptr_t)p >= it->first && (uintptr_t)p + n <= it->first + it->second) return true;
+    }
+  }
+  static const bool query = [] {
+    const char* e = getenv("BPP_PIN_QUERY");
+    return e && atoi(e) != 0;
+  }();
+  if (!query) return false;
+  hipPointerAttribute_t at;
+  const bool pin = hipPointerGetAttributes(&at, p) == hipSuccess && at.type == hipMemoryTypeHost;
+  (void)hipGetLastError();  // (a pageable pointer leaves an error code behind)
+  return pin;
+}
+
 void ctx_stage_copy(void* dst, const void* src, size_t bytes) {
   const size_t chunk = 128u << 10;
   if (bytes < (512u << 10)) {

@@ -1158,13 +1158,7 @@ int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label,
           evs->push_back(e);
         }
       if (!ctx->vj_ev_vrep) BPP_HIP(hipEventCreateWithFlags(&ctx->vj_ev_vrep, hipEventDisableTiming));
-      auto is_pinned = [](const void* h) {
-        hipPointerAttribute_t at;
-        const bool pin = hipPointerGetAttributes(&at, h) == hipSuccess && at.type == hipMemoryTypeHost;
-        (void)hipGetLastError();
-        return pin;
-      };
-      const bool direct = is_pinned(proofs) && is_pinned(V);
+      const bool direct = host_is_pinned(proofs, count * plen) && host_is_pinned(V, count * vbytes);
       uint8_t* stg = nullptr;
       if (!direct) BPP_TRY(ctx_h2d_stage(ctx, count * (plen + vbytes), &stg));
       auto up = [&](size_t off, const uint8_t* src, size_t n) -> int {
@@ -1220,17 +1214,11 @@ int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label,
         BPP_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         ctx->vj_ev_chunk.push_back(e);
       }
-      // proofs and V already in pinned host memory (bpp_host_alloc, or
-      // registered by the caller) go up by DMA from where they are; pageable
-      // buffers are staged through the pinned arena first (the host copy
-      // then paces the upload)
-      auto pinned = [](const void* h) {
-        hipPointerAttribute_t at;
-        const bool pin = hipPointerGetAttributes(&at, h) == hipSuccess && at.type == hipMemoryTypeHost;
-        (void)hipGetLastError();  // (a pageable pointer leaves an error code behind)
-        return pin;
-      };
-      const bool direct = pinned(proofs) && pinned(V);
+      // proofs and V already in pinned host memory (bpp_host_alloc; memory
+      // the caller registered itself with BPP_PIN_QUERY=1) go up by DMA from
+      // where they are; pageable buffers are staged through the pinned arena
+      // first (the host copy then paces the upload)
+      const bool direct = host_is_pinned(proofs, count * plen) && host_is_pinned(V, count * vbytes);
       uint8_t* stg = nullptr;
       if (!direct) BPP_TRY(ctx_h2d_stage(ctx, count * (plen + vbytes), &stg));
       static const size_t stage_piece = [] {  // (BPP_VERIFY_PIECE_KB, A/B; 0 = whole parts)

@@ -159,7 +159,11 @@ int bpp_msm_collect(bpp_ctx* ctx, uint64_t ticket, uint8_t out[32], uint8_t part
  * unchanged until collect. */
 int bpp_msm_submit_host(bpp_ctx* ctx, const void* h_scalars, const bpp_points* tbl, size_t n, uint32_t w_begin,
                         uint32_t w_end, uint64_t* ticket);
-/* Pinned (page-locked) host memory for bpp_msm_submit_host inputs. */
+/* Pinned (page-locked) host memory for bpp_msm_submit_host and
+ * bpp_perm_verify_* inputs: the library recognises these buffers (a range
+ * inside one goes up by direct DMA) from its own registry; other host memory
+ * is treated as pageable and staged (memory the caller pinned itself is
+ * also looked up in the HIP runtime when BPP_PIN_QUERY=1). */
 int bpp_host_alloc(bpp_ctx* ctx, size_t bytes, void** hptr);
 int bpp_host_free(bpp_ctx* ctx, void* hptr);
 /* Sum raw extended partial points (count x 128 bytes) and compress. */

@@ -65,8 +65,10 @@ static int upload_offsets(bpp_ctx* ctx, const std::vector<uint32_t>& off, void**
 
 int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const uint32_t* d_off, uint32_t M,
                uint32_t T, uint32_t c, uint32_t wb, uint32_t Wn, const uint32_t* d_tbl, uint32_t** d_wsum_out,
-               const uint32_t* d_tbl1, uint32_t n0, bool fb, uint32_t* terms_out, uint32_t rlog) {
+               const uint32_t* d_tbl1, uint32_t n0, bool fb, uint32_t* terms_out, uint32_t rlog,
+               uint32_t* rshift_out) {
   if (terms_out) *terms_out = 1;
+  if (rshift_out) *rshift_out = rlog + 6;
   MsmGeom g;
   g.M = M;
   g.T = T;
@@ -246,7 +248,15 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
     }
     BPP_TRY(ctx_check_launch(ctx, "k_msm_fixup_heavy"));
     if (rlog != RWAVE_LOG && rlog != RWAVE_LOG_LONE) rlog = RWAVE_LOG;
-    const uint32_t rshift = rlog + 6;
+    uint32_t rl = rlog;
+    if (rlog == RWAVE_LOG_LONE) {
+      // an MSM alone: 2^rl buckets a lane with rl <= RWAVE_LOG_LONE, as few as
+      // keep >= 512 waves in flight (a window range of the split verifier
+      // MSM, 2 x 2^14 buckets, ran k_msm_reduce_wave<3> on 64 waves: 124 us
+      // of latency chain, tools/shard_model.py) and nw <= RWAVE_NW_MAX
+      while (rl > 0 && (((size_t)nseg * g.B) >> (6 + rl)) < 512 && (g.B >> (6 + rl - 1)) <= RWAVE_NW_MAX) --rl;
+    }
+    const uint32_t rshift = rl + 6;
     if (terms_out && M == 1 && !fb && g.B >= (1u << rshift) && g.B <= ((uint32_t)RWAVE_NW_MAX << rshift)) {
       // power-of-two weights left to the host Horner (k_msm_reduce_wave)
       const uint32_t nw = g.B >> rshift;
@@ -264,15 +274,24 @@ int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, con
         hipLaunchKernelGGL(k_msm_reduce_bits<RWAVE_LOG>, dim3((unsigned)(nseg * (1 + J))), dim3(64), 0, ctx->stream,
                            (const uint32_t*)part, g, 1 + J, (uint32_t*)wsum);
       } else {
-        hipLaunchKernelGGL(k_msm_reduce_wave<RWAVE_LOG_LONE>, dim3((unsigned)(nseg * nw)), dim3(64), 0, ctx->stream,
-                           (const uint32_t*)boff, K, (const uint32_t*)head, (const uint32_t*)tail,
-                           (const uint32_t*)bsum, g, (uint32_t*)part);
-        hipLaunchKernelGGL(k_msm_reduce_bits<RWAVE_LOG_LONE>, dim3((unsigned)(nseg * (1 + J))), dim3(64), 0,
-                           ctx->stream, (const uint32_t*)part, g, 1 + J, (uint32_t*)wsum);
+        auto launch = [&](auto kw, auto kb) {
+          hipLaunchKernelGGL(kw, dim3((unsigned)(nseg * nw)), dim3(64), 0, ctx->stream, (const uint32_t*)boff, K,
+                             (const uint32_t*)head, (const uint32_t*)tail, (const uint32_t*)bsum, g, (uint32_t*)part);
+          hipLaunchKernelGGL(kb, dim3((unsigned)(nseg * (1 + J))), dim3(64), 0, ctx->stream, (const uint32_t*)part, g,
+                             1 + J, (uint32_t*)wsum);
+        };
+        static_assert(RWAVE_LOG_LONE == 3, "lone reduce shapes 0..3");
+        switch (rl) {
+          case 0: launch(k_msm_reduce_wave<0>, k_msm_reduce_bits<0>); break;
+          case 1: launch(k_msm_reduce_wave<1>, k_msm_reduce_bits<1>); break;
+          case 2: launch(k_msm_reduce_wave<2>, k_msm_reduce_bits<2>); break;
+          default: launch(k_msm_reduce_wave<3>, k_msm_reduce_bits<3>); break;
+        }
       }
 #endif
       BPP_TRY(ctx_check_launch(ctx, "k_msm_reduce_wave/bits"));
       *terms_out = 1 + J;
+      if (rshift_out) *rshift_out = rshift;
       *d_wsum_out = (uint32_t*)wsum;
       return BPP_OK;
     }
@@ -335,14 +354,14 @@ int msm_single_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx,
     return (e && atoi(e) == RWAVE_LOG) ? (uint32_t)RWAVE_LOG : (uint32_t)RWAVE_LOG_LONE;
   }();
   uint32_t* d_ws = nullptr;
-  uint32_t nterms = 1;
+  uint32_t nterms = 1, rshift = rlog + 6;
   BPP_TRY(msm_engine(ctx, d_scal, d_pidx, nullptr, 1, (uint32_t)n, c, wb, Wn, d_tbl, &d_ws, d_tbl1, n0, false,
-                     &nterms, rlog));
+                     &nterms, rlog, &rshift));
   void* h = nullptr;
   BPP_TRY(ctx_pinned(ctx, (size_t)Wn * nterms * P3_BYTES, &h));
   BPP_HIP(hipMemcpyAsync(h, d_ws, (size_t)Wn * nterms * P3_BYTES, hipMemcpyDeviceToHost, ctx->stream));
   BPP_TRY(ctx_sync_latency(ctx));
-  *out = horner_host_terms((const uint32_t*)h, Wn, nterms, c, wb, rlog + 6);
+  *out = horner_host_terms((const uint32_t*)h, Wn, nterms, c, wb, rshift);
   return BPP_OK;
 }
 

@@ -20,10 +20,12 @@ uint32_t msm_choose_c(double n_per_msm);
 int msm_engine(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t* d_pidx, const uint32_t* d_off, uint32_t M,
                uint32_t T, uint32_t c, uint32_t wb, uint32_t Wn, const uint32_t* d_tbl, uint32_t** d_wsum_out,
                const uint32_t* d_tbl1 = nullptr, uint32_t n0 = 0xffffffffu, bool fb = false,
-               uint32_t* terms_out = nullptr, uint32_t rlog = RWAVE_LOG);
+               uint32_t* terms_out = nullptr, uint32_t rlog = RWAVE_LOG, uint32_t* rshift_out = nullptr);
 // With terms_out (single MSMs only) the engine may return, per window, 1 + J
-// terms instead of one sum: the window sum is term 0 + sum_j 2^(rlog+6+j)
-// term 1+j (k_msm_reduce_wave); *terms_out = terms per window (1 = plain sums).
+// terms instead of one sum: the window sum is term 0 + sum_j 2^(rshift+j)
+// term 1+j (k_msm_reduce_wave); *terms_out = terms per window (1 = plain sums),
+// *rshift_out = rshift (rlog + 6 for the stream shape; the lone shape picks
+// its own buckets per lane).
 // Host Horner over such terms: sum_j 2^(c (wb + j)) * window_j.
 h25519::ge horner_host_terms(const uint32_t* ws_words, uint32_t Wn, uint32_t nterms, uint32_t c, uint32_t wb,
                              uint32_t rshift = RWAVE_LOG + 6);

@@ -1356,6 +1356,55 @@ int verify_slice_points_dev(bpp_ctx* ctx, const bpp_verify_job& J, void* d_out) 
   return BPP_OK;
 }
 
+// Gathered slice blocks -> one contiguous array in ONE launch (a
+// hipMemcpyAsync per slice cost ~5 us of launch gap each: 8 slices of
+// scalars took 50 us before config 5's rank MSM, tools/shard_model.py):
+// slice r's n_r elements of `ew` 16-B units sit at src + r stride + off, and
+// land at dst in slice order.
+#define GB_MAX 64
+struct GatherTab {
+  uint32_t n;                // slices
+  uint32_t pre[GB_MAX + 1];  // element prefix counts
+};
+__global__ void __launch_bounds__(256) k_gather_blocks(const uint8_t* __restrict__ src, size_t stride, size_t off,
+                                                       uint32_t ew, GatherTab tab, uint4* __restrict__ dst) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // 16-B unit
+  const size_t e = i / ew;
+  if (e >= tab.pre[tab.n]) return;
+  uint32_t lo = 0, hi = tab.n;  // slice r: pre[r] <= e < pre[r + 1]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) / 2;
+    if (tab.pre[mid] <= e) lo = mid;
+    else hi = mid;
+  }
+  const uint4* s = reinterpret_cast<const uint4*>(src + lo * stride + off);
+  dst[i] = s[(e - tab.pre[lo]) * ew + i % ew];
+}
+
+static int gather_blocks_dev(bpp_ctx* ctx, const uint8_t* src, size_t stride, size_t off, size_t elem_bytes,
+                             const size_t* counts, size_t nslices, uint8_t* dst) {
+  if (nslices > GB_MAX || elem_bytes % 16 || stride % 16 || off % 16) {
+    size_t o = 0;
+    for (size_t r = 0; r < nslices; ++r) {
+      if (counts[r])
+        BPP_HIP(hipMemcpyAsync(dst + o * elem_bytes, src + r * stride + off, counts[r] * elem_bytes,
+                               hipMemcpyDeviceToDevice, ctx->stream));
+      o += counts[r];
+    }
+    return BPP_OK;
+  }
+  GatherTab tab;
+  tab.n = (uint32_t)nslices;
+  tab.pre[0] = 0;
+  for (size_t r = 0; r < nslices; ++r) tab.pre[r + 1] = tab.pre[r] + (uint32_t)counts[r];
+  const uint32_t ew = (uint32_t)(elem_bytes / 16);
+  const size_t units = (size_t)tab.pre[nslices] * ew;
+  if (!units) return BPP_OK;
+  hipLaunchKernelGGL(k_gather_blocks, dim3((unsigned)((units + 255) / 256)), dim3(256), 0, ctx->stream, src, stride,
+                     off, ew, tab, (uint4*)dst);
+  return ctx_check_launch(ctx, "k_gather_blocks");
+}
+
 // The MSM of a sliced job over windows [wb, we) with the scalars of every
 // slice gathered (bpp_perm_verify_partial_gathered): block r (stride bytes
 // apart) holds slice r's [NG | counts[r] x npt]; the generator scalars are
@@ -1391,13 +1440,7 @@ int verify_partial_gathered_dev(bpp_ctx* ctx, const bpp_gens* G, const bpp_verif
   BPP_TRY(ctx_ws(ctx, "vj_dbad", 8, &d_dbad));
   BPP_TRY(verify_sum_blocks_dev(ctx, (uint32_t)nslices, (uint32_t)NG, (const uint32_t*)d_blocks,
                                 (uint32_t)(stride / 4), (uint32_t*)d_sv));
-  size_t off = NG;
-  for (size_t r = 0; r < nslices; ++r) {
-    if (counts[r])
-      BPP_HIP(hipMemcpyAsync((uint8_t*)d_sv + off * 32, d_blocks + r * stride + NG * 32, counts[r] * npt * 32,
-                             hipMemcpyDeviceToDevice, ctx->stream));
-    off += counts[r] * npt;
-  }
+  BPP_TRY(gather_blocks_dev(ctx, d_blocks, stride, NG * 32, npt * 32, counts, nslices, (uint8_t*)d_sv + NG * 32));
   uint64_t* h_dbad = nullptr;
   BPP_TRY(ctx_zc_out(ctx, "vj_dbad_h", 8, (uint32_t**)&h_dbad));
   BPP_HIP(hipStreamWaitEvent(ctx->stream, ctx->vj_ev_dec, 0));
@@ -1456,17 +1499,9 @@ int verify_partial_sharded_dev(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify
     BPP_TRY(ctx_ws(ctx, "vj_xg", total * npt * prec, &d));
     d_x = (const uint8_t*)d;
   }
-  size_t off = 0;
-  for (size_t r = 0; r < nslices; ++r) {
-    if (counts[r]) {
-      BPP_HIP(hipMemcpyAsync((uint8_t*)d_sv + (NG + off * npt) * 32, d_blocks + r * stride + NG * 32,
-                             counts[r] * npt * 32, hipMemcpyDeviceToDevice, ctx->stream));
-      if (!tight)
-        BPP_HIP(hipMemcpyAsync((uint8_t*)d_x + off * npt * prec, d_pblocks + r * pstride, counts[r] * npt * prec,
-                               hipMemcpyDeviceToDevice, ctx->stream));
-    }
-    off += counts[r];
-  }
+  // the slices' proof-point scalars (and, when padded, points) in proof order
+  BPP_TRY(gather_blocks_dev(ctx, d_blocks, stride, NG * 32, npt * 32, counts, nslices, (uint8_t*)d_sv + NG * 32));
+  if (!tight) BPP_TRY(gather_blocks_dev(ctx, d_pblocks, pstride, 0, npt * prec, counts, nslices, (uint8_t*)d_x));
   BPP_TRY(verify_msm(ctx, G, J.C, total, (const uint32_t*)d_sv, (const uint32_t*)d_x, wb, we, out));
   return ctx_sync(ctx);
 }

@@ -309,8 +309,7 @@ extern "C" int bpp_debug_vs_timing(unsigned long long* out, size_t n) {
 #define VK_WRX2F 15  // w_p r x^2 F
 #define VK_XU2 16    // w_p x U^2
 #define VK_U2W 17    // w_p U^2
-#define VK_RC 18     // lg values: -w_p Y prod_{k != j} u_k^2 (R_j's scalar)
-#define VK_N(lg) (VK_RC + (lg))
+#define VK_N 18      // constants a proof
 
 // k_verify_consts works on 16 lanes a proof, 4 proofs a wave, VC_W such
 // waves and one Keccak wave a workgroup.  One lane a proof (round 5's first
@@ -321,8 +320,12 @@ extern "C" int bpp_debug_vs_timing(unsigned long long* out, size_t n) {
 // lg-step loop (one lane each), the named constants in four levels of at most
 // 10 independent products (a table of (op, dst, a, b) per lane), and the
 // batch weight's SHAKE256 on the Keccak wave while the loop runs.  Values
-// travel through LDS slots (VC_*), the first VK_RC of which are the VK_*
-// outputs.
+// travel through LDS slots (VC_*), the first VK_N of which are the VK_*
+// outputs.  The proof-point scalars that are per-proof constants -- A_I,
+// A_O, S: -w F x^(1,2,3); T_k: -w F r x^k (k = 1, 3..6); L_j: -w F u_j^2;
+// R_j: -w Y prod_{k != j} u_k^2 -- are finished here too and written
+// straight to their MSM slots (sc_out[NG + p npt + m + j], canonical), so
+// k_verify_scalars is left with the gate and V columns.
 #define VC_W 2
 #define VC_P (4 * VC_W)  // proofs a workgroup
 #define VC_LGMAX 32
@@ -385,7 +388,8 @@ __constant__ uint8_t vc_load[11][2] = {{VREC_Z, VK_Z},     {VREC_Y, VK_Y},      
 __global__ void __launch_bounds__(64 * (VC_W + 1)) k_verify_consts(uint32_t count, uint32_t lg, uint64_t first,
                                                                    const uint32_t* __restrict__ seed,
                                                                    const uint32_t* __restrict__ rec,
-                                                                   uint32_t* __restrict__ kc) {
+                                                                   uint32_t* __restrict__ kc, uint32_t NG, uint32_t m,
+                                                                   uint32_t npt, uint32_t* __restrict__ sc_out) {
   __builtin_amdgcn_s_setprio(3);  // (latency chain; the decompression runs beside it)
   __shared__ __attribute__((aligned(16))) uint32_t vs[VC_P][VC_NV * 8];
   __shared__ __attribute__((aligned(16))) uint32_t ut[VC_P][VC_LGMAX * 8], u2t[VC_P][VC_LGMAX * 8],
@@ -455,16 +459,30 @@ __global__ void __launch_bounds__(64 * (VC_W + 1)) k_verify_consts(uint32_t coun
       const sc r = op == VC_MUL ? sc_mont(x, y) : op == VC_ADD ? sc_add(x, y) : op == VC_SUB ? sc_sub(x, y) : sc_neg(x);
       sc_store(V + 8 * vc_prog[lv][l][1], r);
     }
-    if (lv == 2 && live) {
-      const sc nwy = ldv(VC_T_NWY);
-      for (uint32_t j = l; j < lg; j += 16) sc_store(kc + ((size_t)p * VK_N(lg) + VK_RC + j) * 8,
-                                                     sc_mont(sc_load(pjt[g] + 8 * j), nwy));
-    }
     __syncthreads();
   }
   if (live) {
-    uint32_t* K = kc + (size_t)p * VK_N(lg) * 8;
-    for (uint32_t w = l; w < VK_RC * 8; w += 16) K[w] = V[w];
+    uint32_t* K = kc + (size_t)p * VK_N * 8;
+    for (uint32_t w = l; w < VK_N * 8; w += 16) K[w] = V[w];
+    // the proof-point scalars after V_0..V_{m-1}
+    uint32_t* out = sc_out + 8 * ((size_t)NG + (size_t)p * npt + m);
+    const sc xR = ldv(VK_X), nwtf = sc_neg(ldv(VK_WTF));
+    for (uint32_t j = l; j < 8 + 2 * lg; j += 16) {
+      sc v;
+      if (j >= 8 + lg) {
+        v = sc_mont(sc_load(pjt[g] + 8 * (j - 8 - lg)), ldv(VC_T_NWY));
+      } else {
+        if (j < 3) {
+          v = sc_pow_small(xR, j + 1, oneR);
+        } else if (j < 8) {
+          v = sc_mont(ldv(VK_R), sc_pow_small(xR, j == 3 ? 1u : j - 1, oneR));  // T1, T3, T4, T5, T6
+        } else {
+          v = sc_load(u2t[g] + 8 * (j - 8));
+        }
+        v = sc_mont(v, nwtf);
+      }
+      sc_store(out + 8 * j, sc_from_mont(v));
+    }
   }
 }
 
@@ -490,7 +508,7 @@ __global__ void __launch_bounds__(POLY_T) __attribute__((amdgpu_waves_per_eu(VS_
   const uint32_t* zp = zt + 8;       // z^(q+1)
   const uint32_t p = blockIdx.x, nrec = VREC_U + lg;
   const uint32_t* R = rec + (size_t)p * nrec * 8;
-  const uint32_t* K = kc + (size_t)p * VK_N(lg) * 8;
+  const uint32_t* K = kc + (size_t)p * VK_N * 8;
   const sc oneR = sc_one_mont();
   auto ldm = [&](uint32_t k) { return sc_to_mont(sc_load(R + 8 * k)); };
   auto ldk = [&](uint32_t k) { return sc_load(K + 8 * k); };
@@ -566,27 +584,7 @@ __global__ void __launch_bounds__(POLY_T) __attribute__((amdgpu_waves_per_eu(VS_
     if (threadIdx.x == 0) sc_store(sc_out + 8 * (pb + j), sc_from_mont(sc_neg(sc_mont(cs, wrx2fR))));
   }
   VS_T(4);
-  // A_I, A_O, S: -wt F x^(1,2,3); T_k: -wt F r x^k (k = 1, 3..6); L_j:
-  // -wt F u_j^2; R_j: -wt Y prod_{k != j} u_k^2 (k_verify_consts)
-  for (uint32_t j = threadIdx.x; j < 8 + 2 * lg; j += blockDim.x) {
-    if (j >= 8 + lg) {
-      sc_store(sc_out + 8 * (pb + m + j), sc_from_mont(ldk(VK_RC + (j - 8 - lg))));
-      continue;
-    }
-    sc v;
-    if (j < 3) {
-      const sc xR = ldk(VK_X);
-      v = xR;
-      for (uint32_t e = 0; e < j; ++e) v = sc_mont(v, xR);
-    } else if (j < 8) {
-      const uint32_t e = j == 3 ? 1u : j - 1;  // T1, T3, T4, T5, T6
-      v = sc_mont(ldk(VK_R), sc_pow_small(ldk(VK_X), e, oneR));
-    } else {
-      const sc u = ldm(VREC_U + (j - 8));
-      v = sc_mont(u, u);
-    }
-    sc_store(sc_out + 8 * (pb + m + j), sc_from_mont(sc_neg(sc_mont(v, ldk(VK_WTF)))));
-  }
+  // (A_I .. R_j: written by k_verify_consts)
   VS_T(5);
   sc_block_sum<2>(acc, red);
   VS_T(6);
@@ -925,12 +923,11 @@ int verify_scalars_dev_rec(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count,
   const size_t lds = ((size_t)C.Q + 1 + 2 * std::min(C.n_p, (uint32_t)POW_LO)) * 32 + (POLY_T / 64) * 2 * 32;
   if (C.lg > VC_LGMAX) return BPP_ERR_LEN;  // (k_verify_consts' LDS tables)
   void* d_kc = nullptr;
-  BPP_TRY(ctx_ws(ctx, "vs_kc", (size_t)count * VK_N(C.lg) * 32, &d_kc));
+  BPP_TRY(ctx_ws(ctx, "vs_kc", (size_t)count * VK_N * 32, &d_kc));
   {
     ProfScope ps(ctx, "verify_scalars");
     hipLaunchKernelGGL(k_verify_consts, dim3((count + VC_P - 1) / VC_P), dim3(64 * (VC_W + 1)), 0, ctx->stream, count,
-                       C.lg, first, seed,
-                       d_rec, (uint32_t*)d_kc);
+                       C.lg, first, seed, d_rec, (uint32_t*)d_kc, NG, C.m, npt, d_sc);
     hipLaunchKernelGGL(k_verify_scalars, dim3(count), dim3(nt), lds, ctx->stream, C.n_p, C.m, C.Q, C.lg, d_rec,
                        (const uint32_t*)d_kc, (const uint32_t*)d_cp, (const uint32_t*)d_ce, (const uint32_t*)d_c,
                        (uint32_t*)d_gen, d_sc, NG, npt);

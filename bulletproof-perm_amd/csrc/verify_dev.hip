@@ -268,6 +268,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(VD_WPE)
 k_verify_decompress(size_t i0, size_t i1, uint32_t jlo, uint32_t jn, uint32_t m, uint32_t lg, uint32_t npt,
                     const uint32_t* __restrict__ proofs, uint32_t pw, const uint32_t* __restrict__ V,
                     uint32_t* __restrict__ tbl, unsigned long long* __restrict__ bad) {
+#ifdef VD_PRIO  // (A/B: issue priority against the expansion's s_setprio(2))
+  __builtin_amdgcn_s_setprio(VD_PRIO);
+#endif
   // lane -> (proof p, point j = jlo + j' with j' < jn): the V points (jlo =
   // 0, jn = m) or the proof's own points (jlo = m) can go separately
   const size_t t = i0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -162,8 +162,8 @@ int bpp_msm_submit_host(bpp_ctx* ctx, const void* h_scalars, const bpp_points* t
 /* Pinned (page-locked) host memory for bpp_msm_submit_host and
  * bpp_perm_verify_* inputs: the library recognises these buffers (a range
  * inside one goes up by direct DMA) from its own registry; other host memory
- * is treated as pageable and staged (memory the caller pinned itself is
- * also looked up in the HIP runtime when BPP_PIN_QUERY=1). */
+ * is looked up in the HIP runtime (memory the caller pinned itself also goes
+ * by DMA) and otherwise staged as pageable. */
 int bpp_host_alloc(bpp_ctx* ctx, size_t bytes, void** hptr);
 int bpp_host_free(bpp_ctx* ctx, void* hptr);
 /* Sum raw extended partial points (count x 128 bytes) and compress. */

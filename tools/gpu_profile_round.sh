@@ -1,9 +1,12 @@
 # One GPU call per round for the judged evidence: -m gpu tests + smoke, the
 # full bench line, kernel-trace stats (MSM stream traced one MSM at a time,
 # --inflight 1, so each launch is timed alone and its average matches the
-# bench line's kernel_ms; one 256-proof batch; three config-5 batch
-# verifications), FETCH_SIZE / WRITE_SIZE PMC passes over the MSM bench, and
-# the prover and MSM SQ counter passes (gpu_pmc_prover.sh, ... msm).
+# bench line's kernel_ms; one 384-proof batch; three config-5 batch
+# verifications), FETCH_SIZE / WRITE_SIZE PMC passes over the MSM bench, the
+# config-5 timeline of one unprofiled pinned batch, the per-rank shard model
+# (tools/shard_model.py), the k_verify_scalars phase stamps (the vst
+# variant, if built), and the prover and MSM SQ counter passes
+# (gpu_pmc_prover.sh, ... msm).
 # Usage (on the box): bash tools/gpu_profile_round.sh <tag>
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -21,6 +24,10 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace_proofs -o run -
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_verify -o run --output-format csv -- python3 tools/verify_stages.py --reps 3 > $OUT/trace_verify_log.txt 2>&1 || { echo "verify trace failed"; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu --proofs-per-gpu 0 --verify-proofs 0 --no-extra --no-extra > $OUT/pmc_fetch_log.txt 2>&1 || { echo "pmc fetch failed"; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu --proofs-per-gpu 0 --verify-proofs 0 --no-extra --no-extra > $OUT/pmc_write_log.txt 2>&1 || { echo "pmc write failed"; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d $OUT/vtl -o run --output-format csv -- python3 tools/verify_stages.py --reps 3 --pinned > $OUT/vtl_log.txt 2>&1 || { echo "verify timeline failed"; exit 1; }
+python3 tools/verify_timeline.py $OUT/vtl > $OUT/verify_timeline_pinned.txt
+timeout -k 10 300 python3 tools/shard_model.py > $OUT/shard_model.json 2> $OUT/shard_model.err || { echo "shard model failed"; exit 1; }
+[ -f bulletproof-perm_amd/bpperm/variants/libbpperm_vst.so ] && { BPP_LIB=bulletproof-perm_amd/bpperm/variants/libbpperm_vst.so timeout -k 10 300 python3 tools/vs_phases.py > $OUT/vs_phases.txt 2>&1 || { echo "vs phases failed"; exit 1; }; }
 bash tools/gpu_pmc_prover.sh $TAG || exit 1
 bash tools/gpu_pmc_prover.sh $TAG msm || exit 1
 echo done

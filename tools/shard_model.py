@@ -74,6 +74,18 @@ def main():
             if rep:
                 for k, v in zip(t, (t1 - t0, t2 - t1, t3 - t2, t4 - t3)):
                     t[k].append(v * 1e3)
+        # the proof split's rank 0: its slice job and the MSM of its slice over all windows
+        t["proofs_split"] = []
+        for rep in range(a.reps + 1):
+            t0 = time.perf_counter()
+            j = bpperm.VerifyJob(a.k, proofs[b:e], Vs[b:e], pr.label, ctx=ctx, wait=False)
+            _, Wj = j.windows()
+            part_p = pr.verify_partial(j, SEED, b, 0, Wj)
+            t1 = time.perf_counter()
+            j.close()
+            assert part_p is not None
+            if rep:
+                t["proofs_split"].append((t1 - t0) * 1e3)
         med = {k: round(sorted(v)[len(v) // 2], 4) for k, v in t.items()}
         out["worlds"][world] = {"slice_proofs": counts[0], "window_range": [wb, we], "ms": med,
                                 "gather_bytes_per_rank": {"points": pstride * (world - 1), "scalars": stride * (world - 1)},

@@ -249,7 +249,9 @@ FE_INLINE ge_niels fetch_entry(const uint32_t* __restrict__ tbl, const uint32_t*
 // heavy[0]) by the lane where it starts and summed by a whole wave
 // (k_msm_fixup_heavy) instead of one lane's serial chain.
 #define FIX_MAX 8
+#ifndef ACC_T
 #define ACC_T 256
+#endif
 
 // Balanced bucket accumulation: lane l owns entries [l*K, (l+1)*K) of the
 // bucket-sorted entry array, so every lane does exactly K mixed additions

@@ -1208,7 +1208,11 @@ int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label,
         const char* e = getenv("BPP_VERIFY_CHUNKS");
         return (size_t)std::max(1, e ? atoi(e) : 4);
       }();
-      const size_t nchunk = std::min(nchunk_env, std::max<size_t>(1, count / 256));
+      // (chunks of >= 1024 proofs: a decompression launch is a per-lane
+      // latency chain of ~50-80 us however few points it has, and the
+      // launches of one stream run in turn -- a 512-proof slice in two
+      // chunks waited 0.32 ms for its points, tools/shard_model.py)
+      const size_t nchunk = std::min(nchunk_env, std::max<size_t>(1, count / 1024));
       while (ctx->vj_ev_chunk.size() < nchunk) {
         hipEvent_t e = nullptr;
         BPP_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));

@@ -1,5 +1,3 @@
-#include <map>
-#include <mutex>
 // Context, workspace, profiling and device-memory entry points of the C ABI.
 #include <execinfo.h>
 #include <malloc.h>
@@ -7,10 +5,14 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <immintrin.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 
 #include "ctx.h"
 #include "host/par.h"
@@ -53,15 +55,49 @@ bool host_is_pinned(const void* p, size_t n) {
   return pin;
 }
 
+// Non-temporal copy into the pinned arena: the arena is only read back by
+// the copy engine, so streaming stores skip the read-for-ownership of every
+// destination line (a plain memcpy moves each byte three times over the
+// memory bus, this one twice).  BPP_STAGE_NT=0 falls back to memcpy (A/B).
+static void copy_nt(uint8_t* d, const uint8_t* s, size_t n) {
+  while (n && ((uintptr_t)d & 31)) {
+    *d++ = *s++;
+    --n;
+  }
+  size_t i = 0;
+  for (; i + 128 <= n; i += 128) {
+    const __m256i a = _mm256_loadu_si256((const __m256i*)(s + i));
+    const __m256i b = _mm256_loadu_si256((const __m256i*)(s + i + 32));
+    const __m256i c = _mm256_loadu_si256((const __m256i*)(s + i + 64));
+    const __m256i e = _mm256_loadu_si256((const __m256i*)(s + i + 96));
+    _mm256_stream_si256((__m256i*)(d + i), a);
+    _mm256_stream_si256((__m256i*)(d + i + 32), b);
+    _mm256_stream_si256((__m256i*)(d + i + 64), c);
+    _mm256_stream_si256((__m256i*)(d + i + 96), e);
+  }
+  if (i < n) memcpy(d + i, s + i, n - i);
+  _mm_sfence();  // (the DMA is enqueued by this thread or after the pool's join)
+}
+
 void ctx_stage_copy(void* dst, const void* src, size_t bytes) {
+  static const bool nt = [] {
+    const char* e = getenv("BPP_STAGE_NT");
+    return !e || atoi(e) != 0;
+  }();
+  auto cp = [&](uint8_t* d, const uint8_t* s, size_t n) {
+    if (nt && n >= 4096)
+      copy_nt(d, s, n);
+    else
+      memcpy(d, s, n);
+  };
   const size_t chunk = 128u << 10;
   if (bytes < (512u << 10)) {
-    memcpy(dst, src, bytes);
+    cp((uint8_t*)dst, (const uint8_t*)src, bytes);
     return;
   }
   par::for_each_copy((bytes + chunk - 1) / chunk, [&](size_t i) {
     const size_t o = i * chunk;
-    memcpy((uint8_t*)dst + o, (const uint8_t*)src + o, std::min(chunk, bytes - o));
+    cp((uint8_t*)dst + o, (const uint8_t*)src + o, std::min(chunk, bytes - o));
   });
 }
 

@@ -1,6 +1,8 @@
 set -o pipefail
-cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; O=gpurun_out/r05s; mkdir -p $O
-timeout -k 10 300 python tools/shard_model.py --worlds 8,4,2 > $O/shard_model.json 2> $O/shard_model.err || { tail $O/shard_model.err; exit 1; }
-cat $O/shard_model.json
-timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d $O/smtr -o run --output-format csv -- python3 tools/shard_model.py --worlds 8 --reps 3 > $O/smtr_log.txt 2>&1 || { tail $O/smtr_log.txt; exit 1; }
-python3 tools/verify_timeline.py $O/smtr > $O/smtr_timeline.txt 2>&1; cat $O/smtr_timeline.txt
+cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; O=gpurun_out/r05t; mkdir -p $O
+true
+true
+for rep in 1 2; do for cfg in BPP_COPY_THREADS=4 BPP_COPY_THREADS=6 BPP_COPY_THREADS=8; do
+  env $cfg timeout -k 10 300 python bench.py --no-cpu --proofs-per-gpu 0 --no-extra --steps 10 > $O/bv.json 2> $O/bv.err || { tail $O/bv.err; exit 1; }
+  python3 -c "import json;d=json.load(open('$O/bv.json'));v=d['verify_batch'];h=d['host_scalars'];print('$cfg'.ljust(18),{k:round(x['ms_per_batch'],3) for k,x in v['splits'].items()}, 'upl', round(v['stage_ms']['verify_upload'],3), 'host lat', round(h['latency_host_scalars_ms'],3), 'pipe', round(h['pipelined']['pageable']['vs_resident_pipelined'],3))"
+done; done

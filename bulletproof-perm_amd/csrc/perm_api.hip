@@ -1131,6 +1131,8 @@ int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label,
   const bool split = split_env && dec_order == 0 && rfirst == 0 && rcount == count && count >= 256;
   uint32_t* d_stt = nullptr;
   uint32_t* h_init = nullptr;  // the shared transcript prefix, read in place (zero copy)
+  ReplayEarly early{};
+  bool use_early = false;
   if (split) {
     void* d = nullptr;
     BPP_TRY(ctx_ws(ctx, "vj_stt", count * 52 * 4, &d));
@@ -1225,11 +1227,29 @@ int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label,
       const bool direct = host_is_pinned(proofs, count * plen) && host_is_pinned(V, count * vbytes);
       uint8_t* stg = nullptr;
       if (!direct) BPP_TRY(ctx_h2d_stage(ctx, count * (plen + vbytes), &stg));
-      static const size_t stage_piece = [] {  // (BPP_VERIFY_PIECE_KB, A/B; 0 = whole parts)
+      static const size_t stage_piece = [] {  // (BPP_VERIFY_PIECE_KB, A/B; 0 = whole parts, the default)
         const char* e = getenv("BPP_VERIFY_PIECE_KB");
-        const long kb = e ? atol(e) : 1024;
+        const long kb = e ? atol(e) : 0;
         return kb > 0 ? (size_t)kb << 10 : SIZE_MAX;
       }();
+      // the first nchunk - 1 chunks' transcripts start once their bytes are
+      // up, beside the last chunk's upload (BPP_VERIFY_EARLY=0: one replay
+      // after the last copy)
+      static const bool early_env = [] {
+        const char* e = getenv("BPP_VERIFY_EARLY");
+        return !e || atoi(e) != 0;
+      }();
+      if (early_env && nchunk >= 2 && rfirst == 0 && rcount == count) {
+        bpp_ctx* kv = nullptr;
+        BPP_TRY(ctx_child(ctx, VJ_CHILD + 1, &kv));
+        if (!ctx->vj_ev_vrep) BPP_HIP(hipEventCreateWithFlags(&ctx->vj_ev_vrep, hipEventDisableTiming));
+        early = ReplayEarly{kv->stream, ctx->vj_ev_chunk[nchunk - 2], ctx->vj_ev_vrep,
+                            (uint32_t)(count * (nchunk - 1) / nchunk)};
+        use_early = true;
+        uint32_t init[52];
+        verify_init_state(C, label, llen, init);
+        BPP_TRY(ctx_zc_in(ctx, "vj_init", init, sizeof init, &h_init));
+      }
       for (size_t q = 0; q < nchunk; ++q) {
         const size_t p0 = count * q / nchunk, p1 = count * (q + 1) / nchunk;
         const size_t po = p0 * plen, pn = (p1 - p0) * plen, vo = count * plen + p0 * vbytes, vn = (p1 - p0) * vbytes;
@@ -1237,8 +1257,8 @@ int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label,
           BPP_HIP(hipMemcpyAsync((uint8_t*)d_in + po, proofs + po, pn, hipMemcpyHostToDevice, ctx->stream));
           BPP_HIP(hipMemcpyAsync((uint8_t*)d_in + vo, V + p0 * vbytes, vn, hipMemcpyHostToDevice, ctx->stream));
         } else {
-          // staged in pieces, each piece's DMA behind its host copy: the
-          // copy engine starts after one piece instead of a whole chunk
+          // (in pieces, each piece's DMA behind its host copy, with
+          // BPP_VERIFY_PIECE_KB: measured slower, r05_verify_ab.txt)
           auto staged = [&](size_t o, const uint8_t* src, size_t n) -> int {
             for (size_t a = 0; a < n; a += stage_piece) {
               const size_t b = std::min(n, a + stage_piece);
@@ -1254,6 +1274,8 @@ int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label,
         BPP_HIP(hipStreamWaitEvent(kid->stream, ctx->vj_ev_chunk[q], 0));
         BPP_TRY(verify_decompress_dev(kid, C, (uint32_t)count, d_pf, d_V, (uint32_t*)d_x,
                                       (unsigned long long*)d_dbad, (uint32_t)p0, (uint32_t)p1));
+        if (use_early && q + 2 == nchunk)
+          BPP_TRY(verify_replay_early_dev(ctx, C, (uint32_t)count, h_init, d_pf, d_V, early));
       }
       BPP_HIP(hipEventRecord(ctx->vj_ev_dec, kid->stream));
       ctx->vj_dec_pending = true;
@@ -1276,7 +1298,8 @@ int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label,
     BPP_HIP(hipEventRecord(ctx->vj_ev_in, ctx->stream));
   }
   BPP_TRY(verify_replay_dev(ctx, C, (uint32_t)rcount, h_init, d_pf + rfirst * (plen / 4),
-                            d_V + rfirst * (vbytes / 4), (uint32_t*)d_rec, h_r, h_bad, d_stt));
+                            d_V + rfirst * (vbytes / 4), (uint32_t*)d_rec, h_r, h_bad, d_stt,
+                            use_early ? &early : nullptr));
   if (dec_order == 1) {
     BPP_HIP(hipStreamWaitEvent(kid->stream, ctx->vj_ev_in, 0));
     BPP_TRY(verify_decompress_dev(kid, C, (uint32_t)count, d_pf, d_V, (uint32_t*)d_x, (unsigned long long*)d_dbad));

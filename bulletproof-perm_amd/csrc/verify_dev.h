@@ -39,9 +39,21 @@ inline uint32_t vpts_n(const perm::Circuit& C) { return C.m + 8 + 2 * C.lg; }
 // d_stt (optional): the transcripts' V parts already replayed by
 // verify_replay_v_dev into d_stt ([count][52] words); the replay then starts
 // from each proof's state there and reads only the proof bytes.
+// early (optional): proofs [0, early->split) replay on early->st once
+// early->ready has fired (their bytes are up), the rest on ctx's stream,
+// which then waits for early->done.
+struct ReplayEarly {
+  hipStream_t st;
+  hipEvent_t ready, done;
+  uint32_t split;
+};
 int verify_replay_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const uint32_t* d_init,
                       const uint32_t* d_proofs, const uint32_t* d_V, uint32_t* d_rec, uint32_t* r_out, uint32_t* bad,
-                      const uint32_t* d_stt = nullptr);
+                      const uint32_t* d_stt = nullptr, const ReplayEarly* early = nullptr);
+// The early part: launches proofs [0, e.split) on e.st behind e.ready and
+// records e.done (call it as soon as those proofs' copies are enqueued).
+int verify_replay_early_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const uint32_t* d_init,
+                            const uint32_t* d_proofs, const uint32_t* d_V, const ReplayEarly& e);
 // The V part of the transcripts of proofs [p0, p1) of a batch of `total`
 // (2k V appends, x_perm, V_2k): needs only their V bytes; leaves each
 // proof's sponge in d_stt[p] (52 words) and its x_perm challenge bytes in

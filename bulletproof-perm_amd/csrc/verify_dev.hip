@@ -333,9 +333,24 @@ int verify_replay_v_dev(bpp_ctx* ctx, hipStream_t st, const perm::Circuit& C, ui
   return ctx_check_launch(ctx, "k_verify_replay_g<V>");
 }
 
+int verify_replay_early_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const uint32_t* d_init,
+                            const uint32_t* d_proofs, const uint32_t* d_V, const ReplayEarly& e) {
+  if (!e.split || e.split >= count) return BPP_OK;
+  const uint32_t nch = 6 + C.lg;
+  void *d_ch = nullptr, *d_ok = nullptr;
+  BPP_TRY(ctx_ws(ctx, "vj_ch", ((size_t)count + 1) * nch * 64, &d_ch));
+  BPP_TRY(ctx_ws(ctx, "vj_ok", (size_t)count * 4, &d_ok));
+  // proofs [0, split) as soon as their bytes are up (e.ready): a latency
+  // chain of ~0.25-0.3 ms beside the last chunk's upload and the rest's replay
+  BPP_HIP(hipStreamWaitEvent(e.st, e.ready, 0));
+  launch_replay<0>(e.st, C, 0, e.split, count, d_init, d_proofs, d_V, (uint32_t*)d_ch, (uint32_t*)d_ok, nullptr);
+  BPP_HIP(hipEventRecord(e.done, e.st));
+  return ctx_check_launch(ctx, "k_verify_replay_g<early>");
+}
+
 int verify_replay_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, const uint32_t* d_init,
                       const uint32_t* d_proofs, const uint32_t* d_V, uint32_t* d_rec, uint32_t* r_out, uint32_t* bad,
-                      const uint32_t* d_stt) {
+                      const uint32_t* d_stt, const ReplayEarly* early) {
   if (!count) return BPP_OK;
   const uint32_t pw = (uint32_t)(perm::proof_len(C.k) / 4);
   const uint32_t nch = 6 + C.lg;
@@ -344,12 +359,19 @@ int verify_replay_dev(bpp_ctx* ctx, const perm::Circuit& C, uint32_t count, cons
   BPP_TRY(ctx_ws(ctx, "vj_ok", (size_t)count * 4, &d_ok));
   {
     ProfScope ps(ctx, "verify_replay_dev");
-    if (d_stt)
+    if (d_stt) {
       launch_replay<2>(ctx->stream, C, 0, count, count, nullptr, d_proofs, d_V, (uint32_t*)d_ch, (uint32_t*)d_ok,
                        (uint32_t*)d_stt);
-    else
+    } else if (early && early->split > 0 && early->split < count) {
+      // proofs [0, split) went on early->st already (verify_replay_early_dev);
+      // the rest here after the last copy, then the join
+      launch_replay<0>(ctx->stream, C, early->split, count, count, d_init, d_proofs, d_V, (uint32_t*)d_ch,
+                       (uint32_t*)d_ok, nullptr);
+      BPP_HIP(hipStreamWaitEvent(ctx->stream, early->done, 0));
+    } else {
       launch_replay<0>(ctx->stream, C, 0, count, count, d_init, d_proofs, d_V, (uint32_t*)d_ch, (uint32_t*)d_ok,
                        nullptr);
+    }
   }
   BPP_TRY(ctx_check_launch(ctx, "k_verify_replay_g"));
   {

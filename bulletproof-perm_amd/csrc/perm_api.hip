@@ -1232,12 +1232,15 @@ int verify_begin_dev(bpp_ctx* ctx, const perm::Circuit& C, const uint8_t* label,
         const long kb = e ? atol(e) : 0;
         return kb > 0 ? (size_t)kb << 10 : SIZE_MAX;
       }();
-      // the first nchunk - 1 chunks' transcripts start once their bytes are
-      // up, beside the last chunk's upload (BPP_VERIFY_EARLY=0: one replay
-      // after the last copy)
+      // BPP_VERIFY_EARLY=1 (A/B, off): the first nchunk - 1 chunks'
+      // transcripts start on a side stream once their bytes are up, beside
+      // the last chunk's upload.  It does not pay: a replay launch is a
+      // latency chain of ~0.26-0.28 ms however few transcripts it holds, so
+      // the last chunk's replay ends when the whole one did (1.84-1.89 vs
+      // 1.80-1.86 ms per batch, profiles/r05_verify_ab.txt)
       static const bool early_env = [] {
         const char* e = getenv("BPP_VERIFY_EARLY");
-        return !e || atoi(e) != 0;
+        return e && atoi(e) != 0;
       }();
       if (early_env && nchunk >= 2 && rfirst == 0 && rcount == count) {
         bpp_ctx* kv = nullptr;

@@ -274,12 +274,21 @@ __global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_
                                                        uint32_t* __restrict__ head, uint32_t* __restrict__ tail,
                                                        uint32_t* __restrict__ heavy) {
   // K is a multiple of 4 (msm_engine); lane of entry e = e / K
-  __shared__ __attribute__((aligned(16))) uint32_t piece[ACC_T * P3_WORDS];
   const uint32_t l = blockIdx.x * ACC_T + threadIdx.x;
   const uint32_t lane_first = blockIdx.x * ACC_T, lane_last = lane_first + ACC_T - 1;
   const uint32_t E = boff[nbuckets];
   const uint32_t i0 = l * K;
   const uint32_t i1 = min(i0 + K, E);
+#if ACC_PIECE_GLOBAL
+  // (A/B) every later piece to head[l], the owner folding this workgroup's
+  // from there after the barrier (a workgroup's waves share the CU's L1, so
+  // the barrier's release / acquire makes them visible): no LDS, so the
+  // occupancy is the VGPRs' (8 waves per SIMD at 64) instead of 4 workgroups
+  // of 40 KB per CU
+  auto park = [&](const ge_p3& v, uint32_t, uint32_t) { store_p3(head, l, v); };
+  const uint32_t* piece = head + (size_t)lane_first * P3_WORDS;
+#else
+  __shared__ __attribute__((aligned(16))) uint32_t piece[ACC_T * P3_WORDS];
   // a later piece of a bucket that started in an earlier chunk: to LDS when
   // its owner is in this workgroup and will fold it, else to head[l]
   auto park = [&](const ge_p3& v, uint32_t s, uint32_t e) {
@@ -288,6 +297,7 @@ __global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_
                                                                            : head + (size_t)l * P3_WORDS;
     store_p3(dst, 0, v);
   };
+#endif
   bool owner = false;
   uint32_t b = 0, bstart = 0, bend = 0;
   // a bucket is heavy when it ends FIX_MAX or more lanes past this one:

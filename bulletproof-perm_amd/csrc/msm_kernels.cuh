@@ -252,6 +252,9 @@ FE_INLINE ge_niels fetch_entry(const uint32_t* __restrict__ tbl, const uint32_t*
 #ifndef ACC_T
 #define ACC_T 256
 #endif
+#ifndef ACC_PARK_SPLIT
+#define ACC_PARK_SPLIT 1
+#endif
 
 // Balanced bucket accumulation: lane l owns entries [l*K, (l+1)*K) of the
 // bucket-sorted entry array, so every lane does exactly K mixed additions
@@ -291,12 +294,26 @@ __global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_
   __shared__ __attribute__((aligned(16))) uint32_t piece[ACC_T * P3_WORDS];
   // a later piece of a bucket that started in an earlier chunk: to LDS when
   // its owner is in this workgroup and will fold it, else to head[l]
+#if ACC_PARK_SPLIT
+  // the two destinations as two stores (ds_write / global_store) instead of
+  // one through a selected generic pointer, which compiled to 10
+  // flat_store_dwordx4 on every close: accumulate 0.715-0.735 vs 0.743-0.749
+  // ms at 2^20, three interleaved passes (profiles/r05_acc_park_ab.txt)
+  auto park = [&](const ge_p3& v, uint32_t s, uint32_t e) {
+    const uint32_t l0 = s / K;
+    if ((((e - 1) / K) - l0) < FIX_MAX && l0 >= lane_first)
+      store_p3(piece, threadIdx.x, v);
+    else
+      store_p3(head, l, v);
+  };
+#else
   auto park = [&](const ge_p3& v, uint32_t s, uint32_t e) {
     const uint32_t l0 = s / K;
     uint32_t* dst = ((((e - 1) / K) - l0) < FIX_MAX && l0 >= lane_first) ? piece + threadIdx.x * P3_WORDS
                                                                            : head + (size_t)l * P3_WORDS;
     store_p3(dst, 0, v);
   };
+#endif
 #endif
   bool owner = false;
   uint32_t b = 0, bstart = 0, bend = 0;

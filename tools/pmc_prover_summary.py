@@ -19,7 +19,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 KERNELS = ("k_ipa_round_dt", "k_dt_msm", "k_pedersen", "k_ipa_fold", "k_ipa_terms", "k_ipa_cross_final", "k_poly_coef", "k_poly_x",
-           "k_verify_replay_g", "k_verify_replay_post", "k_verify_weights", "k_verify_decompress",
+           "k_verify_replay_g", "k_verify_replay_post", "k_verify_consts", "k_verify_decompress",
            "k_compress_p3", "k_decompress", "k_msm_accumulate", "k_msm_reduce_wave", "k_sc_halve", "k_verify_scalars")
 
 

@@ -15,7 +15,7 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT / "bulletproof-perm_amd"))
 
 STAGES = ("verify_upload", "verify_replay", "verify_terms", "verify_replay_dev", "verify_replay_post", "verify_decompress",
-          "verify_weights", "verify_scalars", "msm_digits", "msm_scatter", "msm_accumulate", "msm_reduce")
+          "verify_scalars", "msm_digits", "msm_scatter", "msm_accumulate", "msm_reduce")
 
 
 def main():

@@ -346,10 +346,30 @@ __global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_
     // loads in the iteration that closes a run
     uint32_t nbend = boff[min(b + 2, nbuckets)];
 #endif
+#if ACC_PREFETCH
+    // (A/B) one entry ahead: the next entry's table row is requested before
+    // this entry's mixed addition, so its load latency hides behind ~5 K
+    // cycles of arithmetic instead of stalling the next iteration
+    e4 = *reinterpret_cast<const uint4*>(entries + i0);
+    uint32_t e_next = e4.x;
+    ge_niels q_next = fetch_entry_sw(tbl, tbl1, n0, e_next);
+#endif
     for (uint32_t i = i0; i < i1; ++i) {
+#if ACC_PREFETCH
+      const uint32_t e = e_next;
+      const ge_niels q_cur = q_next;
+      if (i + 1 < i1) {
+        const uint32_t j = i + 1 - i0;
+        if ((j & 3u) == 0) e4 = *reinterpret_cast<const uint4*>(entries + i + 1);
+        const uint32_t jq = j & 3u;
+        e_next = jq == 0 ? e4.x : jq == 1 ? e4.y : jq == 2 ? e4.z : e4.w;
+        q_next = fetch_entry_sw(tbl, tbl1, n0, e_next);
+      }
+#else
       if (((i - i0) & 3u) == 0) e4 = *reinterpret_cast<const uint4*>(entries + i);
       const uint32_t q = (i - i0) & 3u;
       const uint32_t e = q == 0 ? e4.x : q == 1 ? e4.y : q == 2 ? e4.z : e4.w;
+#endif
       if (i == bend) {  // close the run of bucket b
         if (bstart >= i0) {
           store_p3(bsum, b, acc);  // whole bucket inside the chunk
@@ -387,7 +407,9 @@ __global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_
         acc = ge_identity();
 #endif
       }
-#if ACC_ADDR_SWAP
+#if ACC_PREFETCH
+      acc = ge_madd_fg(acc, q_cur, (e >> 31) != 0);
+#elif ACC_ADDR_SWAP
       acc = ge_madd_fg(acc, fetch_entry_sw(tbl, tbl1, n0, e), (e >> 31) != 0);
 #else
       acc = ge_madd(acc, fetch_entry(tbl, tbl1, n0, e));

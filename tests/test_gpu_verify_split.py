@@ -300,7 +300,7 @@ def _sharded_partials(g, proofs, Vs, ranks, tamper_rank=None, equal_stride=False
             c.close()
 
 
-@pytest.mark.parametrize("ranks,n", [(4, 64), (3, 100), (8, 64)])
+@pytest.mark.parametrize("ranks,n", [(4, 64), (3, 100), (8, 64), (4, 3)])
 def test_upload_sharded_window_split(setup, ranks, n):
     """the window split with the upload, decompression,
     replay and scalar expansion all sharded by proof.  The partials add up
@@ -313,7 +313,7 @@ def test_upload_sharded_window_split(setup, ranks, n):
     if n > len(proofs):
         more, mv = pr.prove_batch(list(range(700, 700 + n - len(proofs))))
         proofs, Vs = proofs + more, Vs + mv
-    proofs, Vs = proofs[:n], Vs[:n]
+    proofs, Vs = proofs[:n], Vs[:n]  # (n = 3 over 4 ranks: rank 0's slice is empty)
     parts = _sharded_partials(g, proofs, Vs, ranks)
     assert bpperm.partials_is_identity(parts)
     assert not bpperm.partials_is_identity(parts[:-1])

@@ -41,6 +41,13 @@ struct bpp_gens {
   // (bpp_perm_prove_batch sub-batches, callers sharing one gens across
   // threads) may ask for the tables at the same time
   mutable std::mutex build_mu;
+  // bpp_ipa_prove's Q (an arbitrary point): its Niels row at d_tbl[2n + 2]
+  // and its direct-table rows at generator slot 2n + 2 of d_dt, written per
+  // call under q_mu (ipa_api.hip ipa_q_slot), so that the IPA rounds run
+  // fused over the direct tables like the prover's, whose Q is a multiple
+  // of the resident B
+  mutable std::mutex q_mu;
+  uint32_t qslot() const { return (uint32_t)(2 * n + 2); }
   uint32_t gidx(size_t i) const { return (uint32_t)i; }
   uint32_t hidx(size_t i) const { return (uint32_t)(n + i); }
   uint32_t bidx() const { return (uint32_t)(2 * n); }

@@ -154,7 +154,7 @@ static int gens_alloc(bpp_ctx* ctx, size_t n, bpp_gens** out) {
   bpp_gens* g = new bpp_gens();
   g->ctx = ctx;
   g->n = n;
-  if (hipMalloc(&g->d_tbl, (2 * n + 2) * MSM_NIELS_WORDS * 4) != hipSuccess ||
+  if (hipMalloc(&g->d_tbl, (2 * n + 3) * MSM_NIELS_WORDS * 4) != hipSuccess ||  // (+1: the Q slot, gens.h)
       hipMalloc(&g->d_fb, 2 * FB_POS * 8 * MSM_NIELS_WORDS * 4) != hipSuccess) {
     if (g->d_tbl) hipFree(g->d_tbl);
     delete g;
@@ -278,10 +278,11 @@ int gens_points(bpp_ctx* ctx, const bpp_gens* g, MsmPoints* out) {
     // narrower tables instead of exhausting HBM)
     const size_t used = g_dt_total.load();
     const size_t budget = std::min<size_t>(GENS_DT_BUDGET, used < GENS_DT_TOTAL ? GENS_DT_TOTAL - used : 0);
+    // (np + 1 generator slots: the last is bpp_ipa_prove's Q, gens.h)
     uint32_t c = 8;
-    while (c < GENS_DT_CMAX && dt_bytes(np, c + 1) <= budget) ++c;
+    while (c < GENS_DT_CMAX && dt_bytes(np + 1, c + 1) <= budget) ++c;
     uint32_t* d = nullptr;
-    if (hipMalloc(&d, dt_bytes(np, c)) != hipSuccess) {
+    if (hipMalloc(&d, dt_bytes(np + 1, c)) != hipSuccess) {
       ctx->err = "hipMalloc generator direct tables";
       return BPP_ERR_NOMEM;
     }
@@ -296,7 +297,7 @@ int gens_points(bpp_ctx* ctx, const bpp_gens* g, MsmPoints* out) {
     }
     g->d_dt = d;
     g->dt_c = c;
-    g_dt_total += dt_bytes(np, c);
+    g_dt_total += dt_bytes(np + 1, c);
   }
   *out = MsmPoints();
   out->tbl = g->d_tbl;
@@ -424,7 +425,7 @@ void bpp_gens_destroy(bpp_gens* g) {
   if (g->d_wt) hipFree(g->d_wt);
   if (g->d_dt) {
     hipFree(g->d_dt);
-    g_dt_total -= dt_bytes((uint32_t)(2 * g->n + 2), g->dt_c);
+    g_dt_total -= dt_bytes((uint32_t)(2 * g->n + 3), g->dt_c);
   }
   delete g;
 }

@@ -8,6 +8,13 @@
 #include "host/scalar.h"
 #include "msm_engine.h"
 
+// widest IPA run as one launch per round (k_ipa_round_dt; its LDS holds the
+// n + 1 terms and the round's a, b: 102 KB at n = 1024, within gfx950's 160 KB
+// per workgroup; 0 builds the four-kernel rounds everywhere, for A/B runs)
+#ifndef IPA_FUSED_NMAX
+#define IPA_FUSED_NMAX 1024
+#endif
+
 struct IpaGens {
   MsmPoints pts;                      // generators (+ window tables), extra points from n0
   uint32_t gbase = 0, hbase = 0;     // G_i at gbase + i, H_i at hbase + i

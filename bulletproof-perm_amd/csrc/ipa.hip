@@ -38,12 +38,6 @@ bool msm_use_dt(const MsmPoints& pts, uint32_t M, uint32_t T);  // msm.hip
 
 static unsigned grid_for(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
-// widest IPA run as one launch per round (k_ipa_round_dt; its LDS holds the
-// n + 1 terms and the round's a, b within 64 KB; 0 builds the four-kernel
-// rounds everywhere, for A/B runs)
-#ifndef IPA_FUSED_NMAX
-#define IPA_FUSED_NMAX 512
-#endif
 
 // All kernels run P independent instances of the same length n in lockstep
 // (a batch of proofs); per-instance arrays are [P][n] scalars, the MSM term

@@ -1,6 +1,8 @@
 // C ABI: Merlin transcript handles, vector commitments and the inner-product
 // argument (bpp_transcript_*, bpp_vec_commit, bpp_ipa_prove, bpp_ipa_verify).
 #include <cstring>
+#include <mutex>
+#include <vector>
 
 #include "ctx.h"
 #include "gens.h"
@@ -156,6 +158,58 @@ int bpp_vec_commit(bpp_ctx* ctx, const bpp_gens* g, const uint8_t blind[32], con
   });
 }
 
+}  // extern "C" (C++ helpers below)
+
+bool msm_use_dt(const MsmPoints& pts, uint32_t M, uint32_t T);  // msm.hip
+
+namespace {
+// host extended point -> the device's 128-B Niels row (y + x, y - x, 2 d x y
+// in 10 limbs at bit offsets ceil(25.5 i), ge_io.cuh store_niels)
+void niels_row_host(const h25519::ge& p, uint32_t w[MSM_NIELS_WORDS]) {
+  namespace H = h25519;
+  const H::fe zi = H::fe_invert(p.Z), x = H::fe_mul(p.X, zi), y = H::fe_mul(p.Y, zi);
+  const H::fe f[3] = {H::fe_add(y, x), H::fe_sub(y, x), H::fe_mul(H::fe_mul(x, y), H::FE_D2)};
+  for (int e = 0; e < 3; ++e) {
+    const H::fe c = H::fe_canon(f[e]);
+    for (int k = 0; k < 5; ++k) {
+      w[10 * e + 2 * k] = (uint32_t)(c.v[k] & 0x3ffffffu);
+      w[10 * e + 2 * k + 1] = (uint32_t)(c.v[k] >> 26);
+    }
+  }
+  w[30] = w[31] = 0;
+}
+
+// Q into the generators' Q slot (gens.h): its window points 2^(8u) Q, u <
+// 32, on the host (248 doublings: ~35 us, where one GPU lane's chain took
+// ~0.5 ms), their Niels rows uploaded as a window table, then Q's direct-table
+// rows built on the device into slot 2n + 2 and its Niels row into d_tbl.
+// The caller holds g->q_mu until the IPA using the slot has completed.
+int ipa_q_slot(bpp_ctx* ctx, const bpp_gens* g, const uint8_t Q[32], uint32_t dt_c) {
+  h25519::ge P;
+  if (!h25519::decode(P, Q)) {
+    ctx->err = "Q does not decode";
+    return BPP_ERR_DECOMPRESS;
+  }
+  std::vector<uint32_t> wt((size_t)FBW_W * MSM_NIELS_WORDS);
+  h25519::ge cur = P;
+  for (uint32_t u = 0; u < FBW_W; ++u) {
+    niels_row_host(cur, &wt[(size_t)u * MSM_NIELS_WORDS]);
+    for (uint32_t i = 0; i < FBW_C; ++i) cur = h25519::ge_dbl(cur);
+  }
+  void* d_wt = nullptr;
+  BPP_TRY(ctx_ws(ctx, "ipa_q_wt", wt.size() * 4, &d_wt));
+  BPP_TRY(ctx_h2d(ctx, d_wt, wt.data(), wt.size() * 4));
+  // (slot rows start after the 2n + 2 generators' rows: dt_bytes per point)
+  uint32_t* slot = g->d_dt + dt_bytes(g->qslot(), dt_c) / 4;
+  BPP_TRY(dt_build(ctx, (const uint32_t*)d_wt, 1, dt_c, slot));
+  BPP_HIP(hipMemcpyAsync(g->d_tbl + (size_t)g->qslot() * MSM_NIELS_WORDS, d_wt, MSM_NIELS_WORDS * 4,
+                         hipMemcpyDeviceToDevice, ctx->stream));
+  return BPP_OK;
+}
+}  // namespace
+
+extern "C" {
+
 int bpp_ipa_prove(bpp_ctx* ctx, const bpp_gens* g, bpp_transcript* tr, const uint8_t Q[32], const uint8_t* G_factors,
                   const uint8_t* H_factors, const uint8_t* a, const uint8_t* b, size_t n, uint8_t* L_out,
                   uint8_t* R_out, uint8_t a_out[32], uint8_t b_out[32]) {
@@ -168,13 +222,29 @@ int bpp_ipa_prove(bpp_ctx* ctx, const bpp_gens* g, bpp_transcript* tr, const uin
     BPP_TRY(upload_scalars(ctx, b, n, "ipa_in_b", &d_b));
     BPP_TRY(upload_opt(ctx, G_factors, n, "ipa_in_gf", &d_gf));
     BPP_TRY(upload_opt(ctx, H_factors, n, "ipa_in_hf", &d_hf));
-    BPP_TRY(decompress_ws(ctx, Q, 1, "ipa_q", &d_q));
     IpaGens ig;
     BPP_TRY(gens_points(ctx, g, &ig.pts));
-    BPP_TRY(msm_points_extra(ctx, &ig.pts, d_q, 1, (uint32_t)(2 * g->n + 2), "ipa_q_wt", (double)(n + 1)));
     ig.gbase = 0;
     ig.hbase = (uint32_t)g->n;
-    ig.qidx = ig.pts.n0;
+    // Q in the generators' slot when they have direct tables and the rounds
+    // can run fused (BPP_IPA_QSLOT=0: Q as an extra point, the four-kernel
+    // rounds over the generic engine)
+    static const bool qslot_env = [] {
+      const char* e = getenv("BPP_IPA_QSLOT");
+      return !e || atoi(e) != 0;
+    }();
+    std::unique_lock<std::mutex> qlock;
+    // (exactly the fused rounds' condition, ipa.hip: the slot has direct-table
+    // rows and a Niels row only, no window-table rows for the other engines)
+    if (qslot_env && n >= 2 && n <= IPA_FUSED_NMAX && msm_use_dt(ig.pts, 2, (uint32_t)(2 * n + 2))) {
+      qlock = std::unique_lock<std::mutex>(g->q_mu);
+      BPP_TRY(ipa_q_slot(ctx, g, Q, ig.pts.dt_c));
+      ig.qidx = g->qslot();
+    } else {
+      BPP_TRY(decompress_ws(ctx, Q, 1, "ipa_q", &d_q));
+      BPP_TRY(msm_points_extra(ctx, &ig.pts, d_q, 1, (uint32_t)(2 * g->n + 2), "ipa_q_wt", (double)(n + 1)));
+      ig.qidx = ig.pts.n0;
+    }
     IpaProofHost pf;
     BPP_TRY(ipa_prove_dev(ctx, tr->t, ig, (uint32_t)n, d_gf, d_hf, d_a, d_b, pf));
     for (size_t j = 0; j < pf.L.size(); ++j) {

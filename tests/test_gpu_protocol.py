@@ -120,3 +120,56 @@ def test_ipa_and_vec_commit_both_msm_engines(ctx, gens16, monkeypatch, mode):
     P = bp.msm(a + b + [bp.inner(a, b)], oG + oH + [Q])
     assert gens16.ipa_verify(bpperm.Transcript(b"ipa-fb"), n, None, None, r255.encode(P), r255.encode(Q),
                              L, R, ga, gb)
+
+
+def test_ipa_q_slot_shared_gens_two_contexts(ctx, gens16):
+    """bpp_ipa_prove writes Q into the generators' spare slot for the call
+    (gens.h qslot, under a per-set mutex): two contexts proving with
+    different Q on one generator set from two threads get their own proofs,
+    and an undecodable Q is refused (BPP_ERR_DECOMPRESS)."""
+    import ctypes as C
+    import threading
+
+    import bpperm
+    rng = Rng(900)
+    oG, oH = merlin.bulletproof_gens(16)
+    n = 16
+    cases = []
+    for i in range(4):
+        Q = rng.point()
+        a = [rng.scalar() for _ in range(n)]
+        b = [rng.scalar() for _ in range(n)]
+        want = bp.ipa_create(merlin.Transcript(b"qslot"), Q, [1] * n, [1] * n, oG, oH, a, b)
+        cases.append((r255.encode(Q), b"".join(sb(x) for x in a), b"".join(sb(x) for x in b), want))
+    ctx2 = bpperm.Context(0)
+    lib = ctx.lib
+    errs = []
+
+    def run(c, idx):
+        try:
+            for _ in range(3):
+                for i in idx:
+                    Qe, ab, bb, want = cases[i]
+                    tr = bpperm.Transcript(b"qslot")
+                    Lo, Ro = C.create_string_buffer(32 * 4), C.create_string_buffer(32 * 4)
+                    ao, bo = C.create_string_buffer(32), C.create_string_buffer(32)
+                    rc = lib.bpp_ipa_prove(c.h, gens16.h, tr.h, C.c_char_p(Qe), None, None, C.c_char_p(ab),
+                                           C.c_char_p(bb), n, Lo, Ro, ao, bo)
+                    tr.close()
+                    L = [Lo.raw[32 * k: 32 * k + 32] for k in range(4)]
+                    R = [Ro.raw[32 * k: 32 * k + 32] for k in range(4)]
+                    if rc != 0 or L != want.L or R != want.R or ao.raw != sb(want.a) or bo.raw != sb(want.b):
+                        errs.append((i, rc))
+        except Exception as e:  # (reported below)
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=run, args=(ctx, [0, 1])), threading.Thread(target=run, args=(ctx2, [2, 3]))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    ctx2.close()
+    assert errs == []
+    bad = bytes([1]) + bytes(31)  # a nonzero encoding that is not a ristretto point (odd)
+    with pytest.raises(bpperm.BppError):
+        gens16.ipa_prove(bpperm.Transcript(b"qslot"), bad, None, None, cases[0][1], cases[0][2])

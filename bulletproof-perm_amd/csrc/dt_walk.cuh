@@ -210,28 +210,42 @@ FE_INLINE void lds_store_coord(uint32_t* tl, uint32_t nslots, uint32_t j, uint32
   }
 }
 
-// Block tree in LDS (tl: blockDim.x extended points); lane 0 writes the
-// block's sum to out_p3[m].  A level of s additions runs one lane per
-// addition while 4 s exceeds the block, then four lanes per addition
-// (ge_add_quad): a narrow level's latency is one wave's instruction stream,
-// which the quads cut by ~3x (the 8-level tree was ~29 us of each 80-us IPA
-// round at 256 lanes, measured with EXP_IPA_NOTREE).
-FE_INLINE void dt_block_tree(uint32_t* tl, const ge_p3& acc, uint32_t nt, uint32_t* __restrict__ out_p3, uint32_t m) {
+// Block tree in LDS (tl: blockDim.x extended points) over `segs` segments
+// of nt / segs lanes each; lane i < segs writes segment i's sum to
+// out_p3[m0 + i * mstride].  A level of s additions per segment runs one
+// lane per addition while 4 segs s exceeds the block, then four lanes per
+// addition (ge_add_quad): a narrow level's latency is one wave's instruction
+// stream, which the quads cut by ~3x (the 8-level tree was ~29 us of each
+// 80-us IPA round at 256 lanes, measured with EXP_IPA_NOTREE).  Segments
+// side by side share the narrow levels' waves (the two-sided IPA round).
+FE_INLINE void dt_block_tree_segs(uint32_t* tl, const ge_p3& acc, uint32_t nt, uint32_t segs,
+                                  uint32_t* __restrict__ out_p3, uint32_t m0, uint32_t mstride) {
   lds_store_p3(tl, nt, threadIdx.x, acc);
   __syncthreads();
-  uint32_t p2 = 1;
-  while (p2 < nt) p2 <<= 1;
-  for (uint32_t s = p2 >> 1; s > 0; s >>= 1) {
-    if (4 * s > nt) {
-      if (threadIdx.x < s && threadIdx.x + s < nt)
-        lds_store_p3(tl, nt, threadIdx.x, ge_add(lds_load_p3(tl, nt, threadIdx.x), lds_load_p3(tl, nt, threadIdx.x + s)));
-    } else if ((threadIdx.x & ~63u) < 4 * s) {  // wave-uniform: whole waves run the DPP exchange
-      const uint32_t j = threadIdx.x >> 2, c = threadIdx.x & 3;
-      const bool live = j < s && j + s < nt;
-      const fe r = ge_add_quad(lds_load_p3(tl, nt, live ? j : 0), lds_load_p3(tl, nt, live ? j + s : 0), c);
-      if (live) lds_store_coord(tl, nt, j, c, r);
+  const uint32_t ns = nt / segs;  // lanes per segment (segs divides nt)
+  uint32_t p2 = 1, lp = 0;
+  while (p2 < ns) {
+    p2 <<= 1;
+    ++lp;
+  }
+  for (uint32_t s = p2 >> 1, l = lp - (lp ? 1u : 0u); s > 0; s >>= 1, --l) {
+    const uint32_t na = segs * s;  // additions at this level
+    if (4 * na > nt) {
+      if (threadIdx.x < na) {
+        const uint32_t g = threadIdx.x >> l, j = threadIdx.x & (s - 1u), a = g * ns + j;
+        if (j + s < ns) lds_store_p3(tl, nt, a, ge_add(lds_load_p3(tl, nt, a), lds_load_p3(tl, nt, a + s)));
+      }
+    } else if ((threadIdx.x & ~63u) < 4 * na) {  // wave-uniform: whole waves run the DPP exchange
+      const uint32_t i = threadIdx.x >> 2, c = threadIdx.x & 3;
+      const uint32_t g = i >> l, j = i & (s - 1u), a = g * ns + j;
+      const bool live = i < na && j + s < ns;
+      const fe r = ge_add_quad(lds_load_p3(tl, nt, live ? a : 0), lds_load_p3(tl, nt, live ? a + s : 0), c);
+      if (live) lds_store_coord(tl, nt, a, c, r);
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) store_p3(out_p3, m, lds_load_p3(tl, nt, 0));
+  if (threadIdx.x < segs) store_p3(out_p3, m0 + threadIdx.x * mstride, lds_load_p3(tl, nt, threadIdx.x * ns));
+}
+FE_INLINE void dt_block_tree(uint32_t* tl, const ge_p3& acc, uint32_t nt, uint32_t* __restrict__ out_p3, uint32_t m) {
+  dt_block_tree_segs(tl, acc, nt, 1, out_p3, m, 0);
 }

@@ -235,8 +235,13 @@ struct IpaRoundArgs {
   uint32_t split;   // J: blocks per L / R MSM, each walking a slice of its n + 1 terms
 };
 
+// S = sides per block: 1 (block bidx = MSM bidx / J's slice, L or R) or 2
+// (block bidx = instance bidx / J's slice, lanes [0, nt/2) walking its L and
+// [nt/2, nt) its R): the two sides share the fold and the term scalars,
+// which a pair of one-sided blocks each compute in full, and their block
+// trees run side by side (BPP_IPA_LR, large batches).
 FE_INLINE void ipa_round_body(const uint32_t* __restrict__ dt, const DtGeom& dg, uint32_t n, uint32_t TG,
-                              const IpaRoundArgs& A, uint32_t bidx, uint32_t* lds) {
+                              const IpaRoundArgs& A, uint32_t bidx, uint32_t* lds, uint32_t S) {
   const uint32_t m = A.m, lg_h = A.lg_h, fold = A.fold, init = A.init, halve = A.halve, gbase = A.gbase,
                  hbase = A.hbase, qidx = A.qidx, J = A.split;
   const uint32_t* __restrict__ am_in = A.am_in;
@@ -254,20 +259,31 @@ FE_INLINE void ipa_round_body(const uint32_t* __restrict__ dt, const DtGeom& dg,
   const uint32_t* __restrict__ b0 = A.b0;
   const uint32_t* __restrict__ gf0 = A.gf0;
   const uint32_t* __restrict__ hf0 = A.hf0;
-  uint32_t* tsc = lds;                           // (n + 1) x 8 words: halved term scalars
-  uint32_t* tgen = lds + 8 * (n + 1);            // n + 1 generator indices
-  uint32_t* sa = tgen + ((n + 1 + 3) & ~3u);     // m x 8: a (Montgomery), this round
+  const uint32_t NS = n + 1;                     // term slots per side
+  uint32_t* tsc = lds;                           // S x (n + 1) x 8 words: halved term scalars
+  uint32_t* tgen = lds + 8 * S * NS;             // S x (n + 1) generator indices
+  uint32_t* sa = tgen + ((S * NS + 3) & ~3u);    // m x 8: a (Montgomery), this round
   uint32_t* sb = sa + 8 * m;                     // m x 8: b
-  uint32_t* red = sb + 8 * m;                    // waves x 8 words
-  const uint32_t nt = blockDim.x, tid = threadIdx.x;
-  // block bidx: slice jp of J of MSM bidx / J = instance inst's L (side 0) or R
-  const uint32_t msm = bidx / J, jp = bidx - msm * J;
-  const uint32_t inst = msm >> 1, side = msm & 1u;
+  uint32_t* red = sb + 8 * m;                    // S x waves x 8 words
+  const uint32_t nt = blockDim.x, tid = threadIdx.x, nwv = (nt + 63) / 64;
+  // S = 1: block bidx is slice jp of J of MSM bidx / J = instance inst's L
+  // (side 0) or R; S = 2: slice jp of instance bidx / J, both sides
+  uint32_t inst, side0, jp;
+  if (S == 2) {
+    inst = bidx / J;
+    jp = bidx - inst * J;
+    side0 = 0;
+  } else {
+    const uint32_t msm = bidx / J;
+    jp = bidx - msm * J;
+    inst = msm >> 1;
+    side0 = msm & 1u;
+  }
   const size_t ib = (size_t)inst * n;
   // init (the first round, no fold): a, b and the generator factors come
   // from the caller's canonical arrays a0, b0, gf0, hf0 (null: all one), and
   // side 0 writes the Montgomery state that round 1 folds (k_ipa_init's work)
-  const bool writer = (fold || init) && side == 0 && jp == 0;
+  const bool writer = (fold || init) && side0 == 0 && jp == 0;
   sc um = sc_zero(), uim = sc_zero();
   if (fold) {
     um = sc_load(u + 16 * inst);
@@ -294,8 +310,8 @@ FE_INLINE void ipa_round_body(const uint32_t* __restrict__ dt, const DtGeom& dg,
     sc_store((isb ? sb : sa) + 8 * p, x);
   }
   __syncthreads();
-  // 2. term scalars: every k gives one G term and one H term, to this side
-  // or the other; item q < n is G_k, q >= n is H_{q-n}
+  // 2. term scalars: every k gives one G term and one H term, to side 0 or
+  // side 1; item q < n is G_k, q >= n is H_{q-n}
   const uint32_t h = m >> 1;
   for (uint32_t q = tid; q < 2 * n; q += nt) {
     const bool ish = q >= n;
@@ -321,52 +337,60 @@ FE_INLINE void ipa_round_body(const uint32_t* __restrict__ dt, const DtGeom& dg,
     const uint32_t r = k & (m - 1);
     const bool hi = (r & h) != 0;
     // G_k's term is on side 0 (L) for hi k, H_k's on side 0 for lo k
-    if ((hi == (side == 0)) != ish) {
+    const uint32_t side = hi != ish ? 0u : 1u;
+    if (S == 2 || side == side0) {
       const uint32_t p = r ^ h;
       const uint32_t cidx = ((k >> (lg_h + 1)) << lg_h) | (k & (h - 1));
       const sc x = sc_mont(sc_load((ish ? sb : sa) + 8 * p), f);
-      const uint32_t slot = (ish ? (n >> 1) : 0) + cidx;
+      const uint32_t slot = (S == 2 ? side * NS : 0u) + (ish ? (n >> 1) : 0) + cidx;
       sc_store(tsc + 8 * slot, halve ? sc_half(x) : x);
       tgen[slot] = (ish ? hbase : gbase) + k;
     }
   }
   // c_L = <a_lo, b_hi> (L) or c_R = <a_hi, b_lo> (R), Montgomery form
-  sc c = sc_zero();
-  for (uint32_t j = tid; j < h; j += nt)
-    c = sc_add(c, side == 0 ? sc_mont(sc_load(sa + 8 * j), sc_load(sb + 8 * (j + h)))
-                            : sc_mont(sc_load(sa + 8 * (j + h)), sc_load(sb + 8 * j)));
-  c = sc_wave_sum(c);
-  if ((tid & 63u) == 0) sc_store(red + 8 * (tid >> 6), c);
+  for (uint32_t s = 0; s < S; ++s) {
+    const uint32_t side = S == 2 ? s : side0;
+    sc c = sc_zero();
+    for (uint32_t j = tid; j < h; j += nt)
+      c = sc_add(c, side == 0 ? sc_mont(sc_load(sa + 8 * j), sc_load(sb + 8 * (j + h)))
+                              : sc_mont(sc_load(sa + 8 * (j + h)), sc_load(sb + 8 * j)));
+    c = sc_wave_sum(c);
+    if ((tid & 63u) == 0) sc_store(red + 8 * (s * nwv + (tid >> 6)), c);
+  }
   __syncthreads();
-  if (tid == 0) {
+  if (tid < S) {
     sc t = sc_zero();
-    for (uint32_t wv = 0; wv < (nt + 63) / 64; ++wv) t = sc_add(t, sc_load(red + 8 * wv));
+    for (uint32_t wv = 0; wv < nwv; ++wv) t = sc_add(t, sc_load(red + 8 * (tid * nwv + wv)));
     const sc cq = sc_mont(t, sc_load(qmul + 8 * inst));  // Montgomery c * canonical q
-    sc_store(tsc + 8 * n, halve ? sc_half(cq) : cq);
-    tgen[n] = qidx;
+    sc_store(tsc + 8 * (tid * NS + n), halve ? sc_half(cq) : cq);
+    tgen[tid * NS + n] = qidx;
   }
   __syncthreads();
   // 3. direct-table walk over the LDS terms, then the block tree (reusing LDS)
-  const uint32_t tg = tid / dg.W;
-  const DtLane ln = DtLane::make(dg, tid % dg.W);
+  const uint32_t ns = nt / S, ls = tid / ns, lt = tid - ls * ns;  // lanes per side, this lane's side
+  const uint32_t tg = lt / dg.W;
+  const DtLane ln = DtLane::make(dg, lt % dg.W);
+  const uint32_t* __restrict__ tscs = tsc + 8 * ls * NS;
+  const uint32_t* __restrict__ tgens = tgen + ls * NS;
 #ifdef EXP_IPA_NOWALK  // timing experiment only (wrong results): no walk, no tree
-  if (tid == 0) store_p3(out_p3, bidx, ge_identity());
+  if (tid < S) store_p3(out_p3, S == 2 ? (2 * inst + tid) * J + jp : bidx, ge_identity());
   return;
 #endif
-  const uint32_t t0 = (uint32_t)((uint64_t)jp * (n + 1) / J), t1 = (uint32_t)((uint64_t)(jp + 1) * (n + 1) / J);
+  const uint32_t t0 = (uint32_t)((uint64_t)jp * NS / J), t1 = (uint32_t)((uint64_t)(jp + 1) * NS / J);
   const ge_p3 acc = tg < TG ? dt_walk(dt, dg, ln, t0 + tg, t1, TG,
                                       [&](uint32_t t, uint32_t s[8], uint32_t& gen) {
-                                        const sc v = sc_load(tsc + 8 * t);
+                                        const sc v = sc_load(tscs + 8 * t);
                                         _Pragma("unroll") for (int i = 0; i < 8; ++i) s[i] = v.v[i];
-                                        gen = tgen[t];
+                                        gen = tgens[t];
                                       })
                             : ge_identity();
   __syncthreads();
 #ifdef EXP_IPA_NOTREE  // timing experiment only (wrong results): no block tree
-  if (tid == 0) store_p3(out_p3, bidx, acc);
+  if (lt == 0) store_p3(out_p3, S == 2 ? (2 * inst + ls) * J + jp : bidx, acc);
   return;
 #endif
-  dt_block_tree(lds, acc, nt, out_p3, bidx);
+  // result of side s: out_p3[(2 inst + s) J + jp] (= bidx for S = 1)
+  dt_block_tree_segs(lds, acc, nt, S, out_p3, S == 2 ? 2 * inst * J + jp : bidx, J);
 }
 
 __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
@@ -376,7 +400,7 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
     uint32_t* __restrict__ fG_out, uint32_t* __restrict__ fH_out, const uint32_t* __restrict__ u,
     const uint32_t* __restrict__ qmul, uint32_t gbase, uint32_t hbase, uint32_t qidx, uint32_t TG, uint32_t halve,
     uint32_t* __restrict__ out_p3, const uint32_t* __restrict__ a0, const uint32_t* __restrict__ b0,
-    const uint32_t* __restrict__ gf0, const uint32_t* __restrict__ hf0, uint32_t init, uint32_t J) {
+    const uint32_t* __restrict__ gf0, const uint32_t* __restrict__ hf0, uint32_t init, uint32_t J, uint32_t S) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   IpaRoundArgs A;
   A.am_in = am_in; A.bm_in = bm_in; A.fG_in = fG_in; A.fH_in = fH_in;
@@ -386,7 +410,7 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
   A.m = m; A.lg_h = lg_h; A.fold = fold; A.init = init; A.halve = halve;
   A.gbase = gbase; A.hbase = hbase; A.qidx = qidx;
   A.split = J;
-  ipa_round_body(dt, dg, n, TG, A, blockIdx.x, lds);
+  ipa_round_body(dt, dg, n, TG, A, blockIdx.x, lds, S);
 }
 
 // Several batches' rounds in one launch (BPP_IPA_MERGE, the shared-launch
@@ -407,7 +431,7 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt_multi(const uint32_t
     sb = b;
   }
   __syncthreads();
-  ipa_round_body(dt, dg, n, TG, sA, sb, lds);
+  ipa_round_body(dt, dg, n, TG, sA, sb, lds, 1);
 }
 
 // The shared-launch round scheduler (BPP_IPA_MERGE=1; an
@@ -525,8 +549,9 @@ int merger_submit(bpp_ctx* ctx, IpaMergeReq& req) {
 
 // LDS words of k_ipa_round_dt: terms + indices + a, b + wave partials, or
 // the block tree, whichever is larger
-static size_t ipa_round_lds_words(uint32_t n, uint32_t nt) {
-  const size_t prologue = 8 * (size_t)(n + 1) + ((n + 1 + 3) & ~3u) + 16 * (size_t)n + 8 * ((nt + 63) / 64);
+static size_t ipa_round_lds_words(uint32_t n, uint32_t nt, uint32_t S = 1) {
+  const size_t NS = (size_t)S * (n + 1);
+  const size_t prologue = 8 * NS + ((NS + 3) & ~(size_t)3) + 16 * (size_t)n + 8 * (size_t)S * ((nt + 63) / 64);
   return std::max(prologue, (size_t)nt * P3_WORDS);
 }
 
@@ -623,8 +648,22 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
     BPP_TRY(ctx_ws(ctx, "ipa_res", (size_t)2 * P * P3_BYTES, &d_res));
     dg = dt_geom(g.pts.dt_c);
     TG = dt_term_groups(dg.W, (double)(n + 1), 2 * P);  // as msm_multi_dt_dev for (n + 1)-term MSMs
+    static const int tg_env = [] {  // term groups per side (A/B switch)
+      const char* e = getenv("BPP_IPA_TG");
+      return e ? atoi(e) : 0;
+    }();
+    if (tg_env >= 1 && (uint32_t)tg_env * dg.W <= DT_NT_MAX) TG = (uint32_t)tg_env;
     nt = TG * dg.W;
   }
+  // Both sides of an instance in one block (ipa_round_body S = 2) for batches
+  // that fill the device with blocks anyway; BPP_IPA_LR=0 keeps one side per
+  // block (A/B switch)
+  static const bool lr_env = [] {
+    const char* e = getenv("BPP_IPA_LR");
+    return !e || atoi(e) != 0;
+  }();
+  uint32_t sides = 1;
+  if (fused && lr_env && P >= 128 && 2 * nt <= DT_NT_MAX && ipa_round_lds_words(n, 2 * nt, 2) * 4 <= 65536) sides = 2;
   // Device transcript path (an A/B experiment: see
   // DESIGN.md): the rounds run back to back on the stream -- fused MSM,
   // k_compress_p3 of L and R, k_ipa_transcript_step (Merlin + u^-1) --
@@ -713,19 +752,21 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
         BPP_HIP(hipStreamWaitEvent(ctx->stream, req.done, 0));  // (ctx_sync below then covers the round)
       } else {
         ProfScope ps(ctx, "ipa_round_dt");  // (bench.py: this kernel's own roofline)
-        hipLaunchKernelGGL(k_ipa_round_dt, dim3(2 * P * J), dim3(nt), ipa_round_lds_words(n, nt) * 4, ctx->stream,
+        hipLaunchKernelGGL(k_ipa_round_dt, dim3(2 / sides * P * J), dim3(sides * nt),
+                           ipa_round_lds_words(n, sides * nt, sides) * 4,
+                           ctx->stream,
                            g.pts.dt, dg, n, m, lg_h, round ? 1u : 0u, S[in][0], S[in][1], S[in][2], S[in][3],
                            S[round ? outs : in][0], S[round ? outs : in][1], S[round ? outs : in][2],
                            S[round ? outs : in][3], (const uint32_t*)d_u, (const uint32_t*)d_q, g.gbase, g.hbase,
                            g.qidx, TG, dev_merlin ? 0u : 1u, (uint32_t*)d_res, d_a, d_b, d_Gf, d_Hf,
-                           round ? 0u : 1u, J);
+                           round ? 0u : 1u, J, sides);
       }
       BPP_TRY(ctx_check_launch(ctx, "k_ipa_round_dt"));
       if (round) cur = outs;
       const uint64_t terms = (uint64_t)2 * P * (n + 1);
       ctx_work(ctx, "msm_terms", terms);
       ctx_work(ctx, "madds", terms * dg.W);
-      ctx_work(ctx, "padds", (uint64_t)2 * P * (nt - 1));
+      ctx_work(ctx, "padds", (uint64_t)2 * P * J * (nt - 1));
       ctx_work(ctx, "msm_launches", 1);
       ctx_work(ctx, "dt_terms", terms);
       ctx_work(ctx, "dt_madds", terms * dg.W);

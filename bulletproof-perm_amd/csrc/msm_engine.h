@@ -12,7 +12,7 @@ bool scalar_is_canonical(const uint8_t* s);
 #define RWAVE_LOG 4
 #endif
 #ifndef RWAVE_LOG_LONE
-#define RWAVE_LOG_LONE 2
+#define RWAVE_LOG_LONE 3  // (msm_kernels.cuh holds the same value; msm.hip asserts it)
 #endif
 uint32_t msm_choose_c(double n_per_msm);
 // Runs K1..K5 for M MSMs over T terms; returns the device array of M*Wn

@@ -212,14 +212,15 @@ FE_INLINE void lds_store_coord(uint32_t* tl, uint32_t nslots, uint32_t j, uint32
 
 // Block tree in LDS (tl: blockDim.x extended points) over `segs` segments
 // of nt / segs lanes each; lane i < segs writes segment i's sum to
-// out_p3[m0 + i * mstride].  A level of s additions per segment runs one
+// out_p3[m0 + i * mstride] when that index is below mend.  A level of s additions per segment runs one
 // lane per addition while 4 segs s exceeds the block, then four lanes per
 // addition (ge_add_quad): a narrow level's latency is one wave's instruction
 // stream, which the quads cut by ~3x (the 8-level tree was ~29 us of each
 // 80-us IPA round at 256 lanes, measured with EXP_IPA_NOTREE).  Segments
 // side by side share the narrow levels' waves (the two-sided IPA round).
 FE_INLINE void dt_block_tree_segs(uint32_t* tl, const ge_p3& acc, uint32_t nt, uint32_t segs,
-                                  uint32_t* __restrict__ out_p3, uint32_t m0, uint32_t mstride) {
+                                  uint32_t* __restrict__ out_p3, uint32_t m0, uint32_t mstride,
+                                  uint32_t mend = 0xffffffffu) {
   lds_store_p3(tl, nt, threadIdx.x, acc);
   __syncthreads();
   const uint32_t ns = nt / segs;  // lanes per segment (segs divides nt)
@@ -244,7 +245,8 @@ FE_INLINE void dt_block_tree_segs(uint32_t* tl, const ge_p3& acc, uint32_t nt, u
     }
     __syncthreads();
   }
-  if (threadIdx.x < segs) store_p3(out_p3, m0 + threadIdx.x * mstride, lds_load_p3(tl, nt, threadIdx.x * ns));
+  if (threadIdx.x < segs && m0 + threadIdx.x * mstride < mend)
+    store_p3(out_p3, m0 + threadIdx.x * mstride, lds_load_p3(tl, nt, threadIdx.x * ns));
 }
 FE_INLINE void dt_block_tree(uint32_t* tl, const ge_p3& acc, uint32_t nt, uint32_t* __restrict__ out_p3, uint32_t m) {
   dt_block_tree_segs(tl, acc, nt, 1, out_p3, m, 0);

@@ -908,6 +908,13 @@ static int msm_multi_dt_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t
   const double t_avg = (double)T / (double)M;
   const uint32_t TG = dt_term_groups(dg.W, t_avg, M);
   const uint32_t nt = TG * dg.W;
+  // two MSMs per block (k_dt_msm segs = 2) for launches with blocks to spare
+  // (the prover's A_I / A_O / S); BPP_DT_PAIR=0 keeps one (A/B switch)
+  static const bool pair_env = [] {
+    const char* e = getenv("BPP_DT_PAIR");
+    return !e || atoi(e) != 0;
+  }();
+  const uint32_t segs = pair_env && M >= 512 && 2 * nt <= DT_NT_MAX ? 2u : 1u;
   ctx_work(ctx, "msm_terms", T);
   ctx_work(ctx, "madds", (uint64_t)T * dg.W);
   ctx_work(ctx, "padds", (uint64_t)M * (nt - 1));
@@ -917,8 +924,9 @@ static int msm_multi_dt_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t
   ctx_work(ctx, "dt_launches", 1);
   {
     ProfScope ps(ctx, "msm_direct");
-    hipLaunchKernelGGL(k_dt_msm, dim3(M), dim3(nt), (size_t)nt * P3_BYTES, ctx->stream, pts.dt, dg, d_scal, d_pidx,
-                       (const uint32_t*)d_off, (uint32_t*)res, d_smap);
+    hipLaunchKernelGGL(k_dt_msm, dim3((M + segs - 1) / segs), dim3(segs * nt), (size_t)segs * nt * P3_BYTES,
+                       ctx->stream, pts.dt, dg, d_scal, d_pidx, (const uint32_t*)d_off, (uint32_t*)res, d_smap, segs,
+                       M);
   }
   BPP_TRY(ctx_check_launch(ctx, "k_dt_msm"));
   *d_res = (uint32_t*)res;

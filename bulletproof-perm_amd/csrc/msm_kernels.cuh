@@ -1050,32 +1050,37 @@ __global__ void __launch_bounds__(RS_FT) k_rsort_fine(const uint32_t* __restrict
 #include "sc25519.cuh"
 
 // smap (optional): term t's scalar is scalars[smap[t]] / 2 mod l (the
-// prover's halved, compacted A_I/A_O/S terms without a gather pass)
+// prover's halved, compacted A_I/A_O/S terms without a gather pass).
+// segs MSMs per block (1 or 2; M = the launch's MSM count): lanes
+// [j nt / segs, (j + 1) nt / segs) walk MSM blockIdx.x * segs + j, and the
+// segments' block trees run side by side (their narrow levels share waves).
 __global__ void __launch_bounds__(DT_NT_MAX) k_dt_msm(const uint32_t* __restrict__ dt, DtGeom dg,
                                                     const uint32_t* __restrict__ scalars,
                                                     const uint32_t* __restrict__ pidx, const uint32_t* __restrict__ off,
-                                                    uint32_t* __restrict__ out_p3, const uint32_t* __restrict__ smap) {
+                                                    uint32_t* __restrict__ out_p3, const uint32_t* __restrict__ smap,
+                                                    uint32_t segs, uint32_t M) {
   extern __shared__ uint32_t tl[];  // blockDim.x extended points (40 KB at 256 lanes)
-  const uint32_t nt = blockDim.x, TG = nt / dg.W;
-  const uint32_t m = blockIdx.x;
-  const DtLane ln = DtLane::make(dg, threadIdx.x % dg.W);
-  const uint32_t tg = threadIdx.x / dg.W;
+  const uint32_t nt = blockDim.x, ns = nt / segs, sg = threadIdx.x / ns, lt = threadIdx.x - sg * ns;
+  const uint32_t TG = ns / dg.W;
+  const uint32_t m0 = blockIdx.x * segs, m = m0 + sg;
+  const DtLane ln = DtLane::make(dg, lt % dg.W);
+  const uint32_t tg = lt / dg.W;
 #ifdef EXP_DT_NOWALK  // timing experiment only (wrong results): no walk, no tree
-  if (threadIdx.x == 0) store_p3(out_p3, m, ge_identity());
+  if (lt == 0 && m < M) store_p3(out_p3, m, ge_identity());
   return;
 #endif
-  const ge_p3 acc = tg < TG ? dt_walk(dt, dg, ln, off[m] + tg, off[m + 1], TG,
-                                      [&](uint32_t t, uint32_t s[8], uint32_t& gen) {
-                                        if (smap) {
-                                          const sc h = sc_half(sc_load(scalars + 8 * (size_t)smap[t]));
-                                          _Pragma("unroll") for (int i = 0; i < 8; ++i) s[i] = h.v[i];
-                                        } else {
-                                          load_scalar(scalars, t, s);
-                                        }
-                                        gen = pidx ? pidx[t] : t;
-                                      })
-                            : ge_identity();
-  dt_block_tree(tl, acc, nt, out_p3, m);
+  const ge_p3 acc = tg < TG && m < M ? dt_walk(dt, dg, ln, off[m] + tg, off[m + 1], TG,
+                                               [&](uint32_t t, uint32_t s[8], uint32_t& gen) {
+                                                 if (smap) {
+                                                   const sc h = sc_half(sc_load(scalars + 8 * (size_t)smap[t]));
+                                                   _Pragma("unroll") for (int i = 0; i < 8; ++i) s[i] = h.v[i];
+                                                 } else {
+                                                   load_scalar(scalars, t, s);
+                                                 }
+                                                 gen = pidx ? pidx[t] : t;
+                                               })
+                                     : ge_identity();
+  dt_block_tree_segs(tl, acc, nt, segs, out_p3, m0, 1, M);
 }
 
 // Direct tables from the window tables (wt[k * 32 + u] = 2^(8u) P_k): lane

@@ -32,12 +32,27 @@ def test_gens_match_bulletproofs_spec(gens16):
 def test_pedersen_commit_batch(gens16):
     rng = Rng(5)
     L = r255.L
-    v = [rng.scalar() for _ in range(50)] + [0, 1, L - 1, 2**252]
-    g = [rng.scalar() for _ in range(50)] + [L - 1, 0, 7, 2**252 - 1]
+    v = [rng.scalar() for _ in range(50)] + [0, 1, L - 1, 2**252, 0]
+    g = [rng.scalar() for _ in range(50)] + [L - 1, 0, 7, 2**252 - 1, 0]
     got = gens16.pedersen_commit([sb(x) for x in v], [sb(x) for x in g])
     B, Bb = merlin.pedersen_gens_default()
     want = [r255.encode(r255.msm([a, c], [B, Bb])) for a, c in zip(v, g)]
     assert got == want
+    assert got[-1] == bytes(32)  # the identity (its double-encoding W is zero)
+
+
+def test_pedersen_commit_batch_large(gens16):
+    """2 100 commitments (the 8-group kernel, 263 lanes of the batched double
+    encoding, 4 points in the last): 37 distinct pairs, identity included,
+    repeated in a scrambled order, each checked against the oracle."""
+    rng = Rng(55)
+    L = r255.L
+    pairs = [(rng.scalar(), rng.scalar()) for _ in range(33)] + [(0, 0), (3, 0), (0, L - 1), (L - 1, L - 1)]
+    order = [(i * 17 + i // 37) % len(pairs) for i in range(2100)]
+    got = gens16.pedersen_commit([sb(pairs[j][0]) for j in order], [sb(pairs[j][1]) for j in order])
+    B, Bb = merlin.pedersen_gens_default()
+    want = [r255.encode(r255.msm([a, c], [B, Bb])) for a, c in pairs]
+    assert got == [want[j] for j in order]
 
 
 def test_vec_commit(gens16):

@@ -40,23 +40,6 @@ __global__ void __launch_bounds__(64) k_fb_tables(const uint32_t* __restrict__ t
   store_niels(fb, t, ge_to_niels(acc));
 }
 
-// (l + 1) / 2 * P for P = tbl[b0] (lane 0) and tbl[b1] (lane 1): the half
-// bases B / 2 and Bb / 2 whose commitments v (B / 2) + g (Bb / 2) = C / 2
-// encode as C by the batched double encoding (k_double_encode); one lane
-// each, once per generator set (a public double-and-add chain)
-__global__ void __launch_bounds__(64) k_half_bases(const uint32_t* __restrict__ tbl, uint32_t b0, uint32_t b1,
-                                                   uint32_t* __restrict__ out) {
-  if (threadIdx.x >= 2) return;
-  constexpr uint32_t HALF_L[8] = {0x2e7ae9f7u, 0x2c09318du, 0x517bce6bu, 0x0a6f7cefu, 0, 0, 0, 0x08000000u};
-  const ge_niels P = load_niels(tbl, threadIdx.x ? b1 : b0);
-  ge_p3 acc = ge_identity();
-  for (int b = 251; b >= 0; --b) {
-    acc = ge_dbl(acc);
-    if ((HALF_L[b >> 5] >> (b & 31)) & 1u) acc = ge_madd(acc, P);
-  }
-  store_niels(out, threadIdx.x, ge_to_niels(acc));
-}
-
 // Pedersen commitments P_j = v_j * B + g_j * Bb (PedersenGens::commit,
 // weights.rs:58-61), constant time in v and gamma like the reference's
 // commit (a constant-time 2-term multiscalar_mul).
@@ -78,8 +61,6 @@ __global__ void __launch_bounds__(64) k_half_bases(const uint32_t* __restrict__ 
 // a commitment are added by k_pedersen_sum (G lanes, log2 G butterfly levels).
 // G = 8 for large batches (13 312 V commitments per 128 proofs: fewest
 // partials), G = 32 for small ones (latency: 4 additions per lane).
-// tb: the table pair, 0 = (B, Bb), 2 = (B / 2, Bb / 2) (C / 2 for the
-// batched double encoding).
 #define PED_T 256
 // v_groups: position groups that can hold nonzero digits of v (G in
 // general; 1 when a PUBLIC bound puts every v below 2^(4 P - 1), e.g. the V
@@ -93,7 +74,7 @@ __global__ void __launch_bounds__(64) k_half_bases(const uint32_t* __restrict__ 
 template <int G>
 __global__ void __launch_bounds__(PED_T) k_pedersen(const uint32_t* __restrict__ fb, const uint32_t* __restrict__ v,
                                                     const uint32_t* __restrict__ gam, size_t m, uint32_t v_groups,
-                                                    uint32_t v_npos, uint32_t* __restrict__ part, uint32_t tb) {
+                                                    uint32_t v_npos, uint32_t* __restrict__ part) {
   constexpr uint32_t PED_GPOS = FB_POS / G;    // positions per group
   constexpr uint32_t PED_ROWS = 2 * PED_GPOS * 8;  // table rows one block needs
   __shared__ __attribute__((aligned(16))) uint32_t rows[PED_ROWS * MSM_NIELS_WORDS];
@@ -102,7 +83,7 @@ __global__ void __launch_bounds__(PED_T) k_pedersen(const uint32_t* __restrict__
   for (uint32_t i = threadIdx.x; i < PED_ROWS * (MSM_NIELS_WORDS / 4); i += PED_T) {
     const uint32_t r = i / (MSM_NIELS_WORDS / 4), c = i % (MSM_NIELS_WORDS / 4);
     const uint32_t which = r / (PED_GPOS * 8), rem = r % (PED_GPOS * 8);
-    const uint32_t src = ((tb + which) * FB_POS + PED_GPOS * g) * 8 + rem;
+    const uint32_t src = (which * FB_POS + PED_GPOS * g) * 8 + rem;
     reinterpret_cast<uint4*>(rows)[i] = reinterpret_cast<const uint4*>(fb + (size_t)src * MSM_NIELS_WORDS)[c];
   }
   __syncthreads();
@@ -174,7 +155,7 @@ static int gens_alloc(bpp_ctx* ctx, size_t n, bpp_gens** out) {
   g->ctx = ctx;
   g->n = n;
   if (hipMalloc(&g->d_tbl, (2 * n + 3) * MSM_NIELS_WORDS * 4) != hipSuccess ||  // (+1: the Q slot, gens.h)
-      hipMalloc(&g->d_fb, 4 * FB_POS * 8 * MSM_NIELS_WORDS * 4) != hipSuccess) {  // (B, Bb, B / 2, Bb / 2)
+      hipMalloc(&g->d_fb, 2 * FB_POS * 8 * MSM_NIELS_WORDS * 4) != hipSuccess) {
     if (g->d_tbl) hipFree(g->d_tbl);
     delete g;
     ctx->err = "hipMalloc generators";
@@ -189,13 +170,6 @@ static int gens_finish(bpp_ctx* ctx, bpp_gens* g) {
     ProfScope ps(ctx, "fb_tables");
     hipLaunchKernelGGL(k_fb_tables, dim3(grid_for(2 * FB_POS * 8, 64)), dim3(64), 0, ctx->stream, g->d_tbl,
                        (uint32_t)(2 * g->n), (uint32_t)(2 * g->n + 1), g->d_fb);
-    // the half bases' tables after them (pedersen_dev's double encoding)
-    void* hb = nullptr;
-    BPP_TRY(ctx_ws(ctx, "half_bases", 2 * MSM_NIELS_WORDS * 4, &hb));
-    hipLaunchKernelGGL(k_half_bases, dim3(1), dim3(64), 0, ctx->stream, g->d_tbl, (uint32_t)(2 * g->n),
-                       (uint32_t)(2 * g->n + 1), (uint32_t*)hb);
-    hipLaunchKernelGGL(k_fb_tables, dim3(grid_for(2 * FB_POS * 8, 64)), dim3(64), 0, ctx->stream,
-                       (const uint32_t*)hb, 0u, 1u, g->d_fb + (size_t)2 * FB_POS * 8 * MSM_NIELS_WORDS);
   }
   BPP_TRY(ctx_check_launch(ctx, "k_fb_tables"));
   BPP_HIP(hipStreamSynchronize(ctx->stream));
@@ -239,33 +213,23 @@ int pedersen_dev(bpp_ctx* ctx, const bpp_gens* g, const uint32_t* d_v, const uin
   ctx_work(ctx, "madds", (uint64_t)(FB_POS + (v_groups == 1 ? v_npos : FB_POS)) * m);
   ctx_work(ctx, "padds", (uint64_t)(G - 1) * m);
   ctx_work(ctx, "msm_launches", 1);
-  // encodings wanted: commit C / 2 over the half bases and encode 2 (C / 2)
-  // with one field inversion per DE_K points (k_double_encode) instead of an
-  // inverse square root per point (k_compress_p3); BPP_PED_DBL=0: the latter
-  static const bool dbl_env = [] {
-    const char* e = getenv("BPP_PED_DBL");
-    return !e || atoi(e) != 0;
-  }();
-  const bool dbl = d_out_enc && dbl_env;
-  const uint32_t tb = dbl ? 2u : 0u;
   void* part = nullptr;
   BPP_TRY(ctx_ws(ctx, "ped_part", m * G * P3_BYTES, &part));
   {
     ProfScope ps(ctx, "pedersen");
     if (G == 32) {
       hipLaunchKernelGGL(k_pedersen<32>, dim3(grid_for(m, PED_T), 32), dim3(PED_T), 0, ctx->stream, g->d_fb, d_v,
-                         d_gam, m, v_groups, v_npos, (uint32_t*)part, tb);
+                         d_gam, m, v_groups, v_npos, (uint32_t*)part);
       hipLaunchKernelGGL(k_pedersen_sum<32>, dim3(grid_for(m * 32, 256)), dim3(256), 0, ctx->stream,
                          (const uint32_t*)part, m, p3);
     } else {
       hipLaunchKernelGGL(k_pedersen<8>, dim3(grid_for(m, PED_T), 8), dim3(PED_T), 0, ctx->stream, g->d_fb, d_v,
-                         d_gam, m, v_groups, v_npos, (uint32_t*)part, tb);
+                         d_gam, m, v_groups, v_npos, (uint32_t*)part);
       hipLaunchKernelGGL(k_pedersen_sum<8>, dim3(grid_for(m * 8, 256)), dim3(256), 0, ctx->stream,
                          (const uint32_t*)part, m, p3);
     }
   }
   BPP_TRY(ctx_check_launch(ctx, "k_pedersen"));
-  if (dbl) return points_double_encode_dev(ctx, p3, m, d_out_enc);
   if (d_out_enc) {
     {
       ProfScope ps(ctx, "compress");

@@ -36,9 +36,6 @@ int upload_scalars(bpp_ctx* ctx, const uint8_t* scalars, size_t n, const char* n
 int points_compress_p3(bpp_ctx* ctx, const uint32_t* d_p3, size_t n, uint8_t* out_host);
 // same, encodings left on the device (d_out: n x 32 B)
 int points_compress_p3_dev(bpp_ctx* ctx, const uint32_t* d_p3, size_t n, uint8_t* d_out);
-// Encodings of 2 P_i into d_out (n x 32 B, device or mapped host memory),
-// one field inversion per few points (k_double_encode)
-int points_double_encode_dev(bpp_ctx* ctx, const uint32_t* d_p3, size_t n, uint32_t* d_out);
 // out = encodings of 2 * P_i (host batch encoding; see points.hip)
 int points_double_encode_p3(bpp_ctx* ctx, const uint32_t* d_p3, size_t n, uint8_t* out_host);
 // same for n points already in host memory (P3 words)

@@ -71,93 +71,6 @@ __global__ void __launch_bounds__(64) k_compress_p3(const uint32_t* __restrict__
 
 static unsigned grid_for(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
-// Encodings of 2 P_i for n device points (P3 layout) on the device, the
-// batch form of encode_double_batch (host/fe64.h, whose comment derives it):
-// 2P = (eh : gf : fh : eg) with e = 2XY, f = Z^2 + dT^2, g = Y^2 + X^2,
-// h = Z^2 - dT^2 has u1 u2^2 = W^2 (a - d), W = 2 e f^2 g h T Z, so its
-// inverse square root is |INVSQRT_A_MINUS_D / W| -- rational, and the W of
-// a lane's points share ONE inversion (Montgomery's trick).  Lane l of L
-// takes points l, l + L, l + 2L, ...; the first pass parks 2P, W and the
-// running product in scr (n x 60 words), the second walks back.  ~30 field
-// multiplies a point plus a 265-multiply inversion per lane, against ~285 a
-// point for k_compress_p3's inverse square root.  W = 0 only for the
-// identity's torsion representatives, whose double encodes to zero.
-__global__ void __launch_bounds__(64) k_double_encode(const uint32_t* __restrict__ pts, size_t n, uint32_t L,
-                                                      uint32_t* __restrict__ scr, uint32_t* __restrict__ out) {
-  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
-  if (l >= L) return;
-  uint32_t* __restrict__ sw = scr + n * P3_WORDS;  // [20][n]: W, then the running product before the point
-  fe run = fe_one();
-  uint32_t cnt = 0;
-  for (size_t i = l; i < n; i += L, ++cnt) {
-    const ge_p3 p = load_p3(pts, i);
-    const fe XX = fe_sq(p.X), YY = fe_sq(p.Y), ZZ = fe_sq(p.Z), dTT = fe_mul(fe_sq(p.T), fe_const(FE_D));
-    const fe e = fe_mul(fe_add(p.X, p.X), p.Y);
-    const fe f = fe_add(ZZ, dTT), g = fe_add(YY, XX), h = fe_sub(ZZ, dTT);
-    ge_p3 q;
-    q.X = fe_mul(e, h);
-    q.Y = fe_mul(g, f);
-    q.Z = fe_mul(f, h);
-    q.T = fe_mul(e, g);
-    fe W = fe_mul(fe_mul(q.X, q.Y), fe_mul(f, fe_mul(p.T, p.Z)));
-    W = fe_add(W, W);
-    if (fe_iszero(W)) W = fe_zero();
-    store_p3(scr, i, q);
-    _Pragma("unroll") for (int k = 0; k < FE_LIMBS; ++k) {
-      sw[(size_t)k * n + i] = W.v[k];
-      sw[(size_t)(FE_LIMBS + k) * n + i] = run.v[k];
-    }
-    if (!fe_iszero(W)) run = fe_mul(run, W);
-  }
-  fe inv = fe_invert(run);
-  for (uint32_t c = cnt; c-- > 0;) {
-    const size_t i = l + (size_t)c * L;
-    fe W, acc;
-    _Pragma("unroll") for (int k = 0; k < FE_LIMBS; ++k) {
-      W.v[k] = sw[(size_t)k * n + i];
-      acc.v[k] = sw[(size_t)(FE_LIMBS + k) * n + i];
-    }
-    uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (!fe_iszero(W)) {
-      const ge_p3 q = load_p3(scr, i);
-      const fe Winv = fe_mul(inv, acc);
-      inv = fe_mul(inv, W);
-      const fe isq = fe_abs(fe_mul(fe_const(FE_INVSQRT_A_MINUS_D), Winv));
-      const fe u1 = fe_mul(fe_add(q.Z, q.Y), fe_sub(q.Z, q.Y));
-      const fe u2 = fe_mul(q.X, q.Y);
-      const fe den1 = fe_mul(isq, u1), den2 = fe_mul(isq, u2);
-      const fe z_inv = fe_mul(fe_mul(den1, den2), q.T);
-      const bool rotate = fe_isneg(fe_mul(q.T, z_inv));
-      const fe x = fe_select(q.X, fe_mul(q.Y, fe_const(FE_SQRT_M1)), rotate);
-      fe y = fe_select(q.Y, fe_mul(q.X, fe_const(FE_SQRT_M1)), rotate);
-      const fe den_inv = fe_select(den2, fe_mul(den1, fe_const(FE_INVSQRT_A_MINUS_D)), rotate);
-      y = fe_select(y, fe_neg(y), fe_isneg(fe_mul(x, z_inv)));
-      fe_store_words(w, fe_canon(fe_abs(fe_mul(den_inv, fe_sub(q.Z, y)))));
-    }
-    uint4* o = reinterpret_cast<uint4*>(out + i * 8);
-    o[0] = make_uint4(w[0], w[1], w[2], w[3]);
-    o[1] = make_uint4(w[4], w[5], w[6], w[7]);
-  }
-}
-
-int points_double_encode_dev(bpp_ctx* ctx, const uint32_t* d_p3, size_t n, uint32_t* d_out) {
-  if (!n) return BPP_OK;
-  static const uint32_t K = [] {  // points per lane (BPP_DE_K: A/B switch)
-    const char* e = getenv("BPP_DE_K");
-    const int k = e ? atoi(e) : 0;
-    return k >= 1 && k <= 256 ? (uint32_t)k : 4u;
-  }();
-  const uint32_t L = (uint32_t)((n + K - 1) / K);
-  void* scr = nullptr;
-  BPP_TRY(ctx_ws(ctx, "de_scr", n * (P3_WORDS + 2 * FE_LIMBS) * 4, &scr));
-  {
-    ProfScope ps(ctx, "compress");
-    hipLaunchKernelGGL(k_double_encode, dim3(grid_for(L, 64)), dim3(64), 0, ctx->stream, d_p3, n, L,
-                       (uint32_t*)scr, d_out);
-  }
-  return ctx_check_launch(ctx, "k_double_encode");
-}
-
 int points_compress_p3_dev(bpp_ctx* ctx, const uint32_t* d_p3, size_t n, uint8_t* d_out) {
   if (!n) return BPP_OK;
   {

@@ -1,5 +1,6 @@
 set -o pipefail
-cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; O=gpurun_out/r05kt; mkdir -p $O
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/new -o run --output-format csv -- python3 tools/prove_batch_once.py 384 > $O/new.log 2>&1 || { tail $O/new.log; exit 1; }
-BPP_IPA_LR=0 BPP_PED_DBL=0 BPP_DT_PAIR=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/old -o run --output-format csv -- python3 tools/prove_batch_once.py 384 > $O/old.log 2>&1 || { tail $O/old.log; exit 1; }
-for d in new old; do python3 tools/kstats.py -n 14 $(find $O/$d -name "*kernel_stats.csv"); done
+cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; O=gpurun_out/r05th; mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_gpu_protocol.py tests/test_gpu_config4.py tests/test_gpu_perm.py -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
+B=384 T=16 REPS=3 bash tools/ab.sh prove "BPP_TREE_HALF=1" "BPP_TREE_HALF=0" 2>&1 | tee $O/ab.txt
+for v in 1 0; do BPP_TREE_HALF=$v timeout -k 10 120 python tools/config2_once.py 20 2>&1 | tail -1; done | tee -a $O/ab.txt

@@ -1,7 +1,6 @@
 set -o pipefail
-cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; O=gpurun_out/r05p2; mkdir -p $O
-BPP_LIB=bulletproof-perm_amd/bpperm/variants/libbpperm_p2.so timeout -k 10 400 python -u -m pytest tests/test_gpu_protocol.py tests/test_gpu_config4.py tests/test_gpu_perm.py -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
-tail -2 $O/tests.log
-B=384 T=16 REPS=3 bash tools/ab.sh prove "LIB=p2" "LIB=default" 2>&1 | tee $O/ab.txt
-B=384 REPS=2 bash tools/ab.sh one "LIB=p2" "LIB=default" 2>&1 | tee -a $O/ab.txt
-for L in bulletproof-perm_amd/bpperm/variants/libbpperm_p2.so ""; do BPP_LIB=$L timeout -k 10 120 python tools/config2_once.py 20 2>&1 | tail -1; done | tee -a $O/ab.txt
+cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; O=gpurun_out/r05vs; mkdir -p $O
+for rep in 1 2; do for vs in 4 6 8; do
+  timeout -k 10 300 python bench.py --no-cpu --proofs-per-gpu 0 --no-extra --steps 10 --verify-streams $vs > $O/bv.json 2> $O/bv.err || { tail $O/bv.err; exit 1; }
+  python3 -c "import json;d=json.load(open('$O/bv.json'));v=d['verify_batch'];print('streams=$vs',{k:round(x['ms_per_batch'],3) for k,x in v['splits'].items()}, round(v['value']/1e6,3), v['rejects_tampered'])"
+done; done 2>&1 | tee $O/ab.txt

@@ -93,62 +93,6 @@ struct DtLane {
 // ahead, and the next term's 128-B table row is gathered between the two
 // halves of the current addition (the operand is dead after its first three
 // multiplies).  A zero digit adds the identity (no divergent skip).
-#ifndef DT_PIPE2
-#define DT_PIPE2 0
-#endif
-#if DT_PIPE2
-// Two rows in flight (DT_PIPE2, the default): terms alternate between two
-// row registers, and the row of term i + 2 is gathered while term i adds, so
-// a gather has one and a half additions to land instead of half of one (the
-// tables are far larger than the caches: every row is an HBM access).
-template <class Src>
-FE_INLINE ge_p3 dt_walk(const uint32_t* __restrict__ dt, const DtGeom& dg, const DtLane& ln, uint32_t t, uint32_t t1,
-                        uint32_t TG, const Src& src) {
-  ge_p3 acc = ge_identity();
-  if (t >= t1) return acc;
-  uint32_t sc[8];
-  uint32_t gen, row;
-  src(t, sc, gen);
-  bool negA, zeroA, negB = false, zeroB = true;
-  ln.row_of(dg, sc, gen, row, negA, zeroA);
-  ge_niels qa = load_niels(dt, row), qb = ge_niels_identity();
-  uint32_t tc = t + TG;
-  bool haveB = tc < t1;
-  if (haveB) {
-    src(tc, sc, gen);
-    ln.row_of(dg, sc, gen, row, negB, zeroB);
-    qb = load_niels(dt, row);
-  }
-  tc += TG;  // the next term to gather
-  if (tc < t1) src(tc, sc, gen);
-  for (;;) {
-    if (zeroA) qa = ge_niels_identity();
-    ge_madd_mid mid = ge_madd_signed_h1(acc, qa, negA);
-    const bool haveC = tc < t1;
-    if (haveC) {
-      ln.row_of(dg, sc, gen, row, negA, zeroA);
-      qa = load_niels(dt, row);
-      tc += TG;
-      if (tc < t1) src(tc, sc, gen);
-    }
-    acc = ge_madd_h2(mid);
-    if (!haveB) break;
-    if (zeroB) qb = ge_niels_identity();
-    mid = ge_madd_signed_h1(acc, qb, negB);
-    const bool haveD = tc < t1;
-    if (haveD) {
-      ln.row_of(dg, sc, gen, row, negB, zeroB);
-      qb = load_niels(dt, row);
-      tc += TG;
-      if (tc < t1) src(tc, sc, gen);
-    }
-    acc = ge_madd_h2(mid);
-    if (!haveC) break;
-    haveB = haveD;
-  }
-  return acc;
-}
-#else
 template <class Src>
 FE_INLINE ge_p3 dt_walk(const uint32_t* __restrict__ dt, const DtGeom& dg, const DtLane& ln, uint32_t t, uint32_t t1,
                         uint32_t TG, const Src& src) {
@@ -184,7 +128,6 @@ FE_INLINE ge_p3 dt_walk(const uint32_t* __restrict__ dt, const DtGeom& dg, const
   }
   return acc;
 }
-#endif
 
 // Extended points in LDS as 10 planes of 16-byte chunks (chunk i of slot j
 // at plane i, position j): consecutive lanes touch consecutive 16 B, where

@@ -15,10 +15,10 @@
 # Examples:
 #   bash tools/ab.sh msm "LIB=default" "LIB=w2"              (was ab_msm.sh)
 #   bash tools/ab.sh msmv "BPP_MSM_LONE_RLOG=2" "BPP_MSM_LONE_RLOG=4"
-#   bash tools/ab.sh full "GPU_MAX_HW_QUEUES=4" "GPU_MAX_HW_QUEUES=12"
+#   bash tools/ab.sh full "BPP_BENCH_HW_QUEUES=4" "BPP_BENCH_HW_QUEUES=8"   (bench.py sets GPU_MAX_HW_QUEUES from it)
 #   bash tools/ab.sh prove "B=256 T=16 BPP_HOST_THREADS=4" "B=384 T=11"
 #   bash tools/ab.sh prove "GPU_MAX_HW_QUEUES=8 T=12" "BPP_IPA_DEVICE_MERLIN=1"
-#   STEPS=120 bash tools/ab.sh msm "INFLIGHT=3" "INFLIGHT=4 GPU_MAX_HW_QUEUES=8"
+#   STEPS=120 bash tools/ab.sh msm "INFLIGHT=3" "INFLIGHT=4 BPP_BENCH_HW_QUEUES=12"
 #   bash tools/ab.sh msmv "BENCH_ARGS=--verify-streams=2" "BENCH_ARGS=--verify-streams=3"
 # (BENCH_ARGS: extra bench.py arguments, comma-separated)
 set -o pipefail

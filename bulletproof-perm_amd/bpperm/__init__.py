@@ -352,6 +352,60 @@ class Transcript:
         self.append_message(label, p)
 
 
+# bpp_transcript_hooks (include/bpperm.h): the caller's transcript behind C hooks
+_APPEND_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_ubyte), C.c_size_t, C.POINTER(C.c_ubyte), C.c_size_t)
+_CHALLENGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_ubyte), C.c_size_t, C.POINTER(C.c_ubyte), C.c_size_t)
+
+
+class _Hooks(C.Structure):
+    _fields_ = [("user", C.c_void_p), ("append_message", _APPEND_FN), ("challenge_bytes", _CHALLENGE_FN)]
+
+
+def transcript_hooks(tr):
+    """bpp_transcript_hooks over any object with merlin's two primitives,
+    `append_message(label, msg)` and `challenge_bytes(label, n) -> bytes`
+    (the caller keeps its own transcript, bpp_ipa_prove_cb).  An exception in
+    a hook is kept on the returned object (`.error`) and reported to the
+    library as a failed hook (BPP_ERR_CALLBACK)."""
+
+    class _H:
+        error = None
+
+    h = _H()
+
+    def _append(_u, lab, ll, msg, ml):
+        try:
+            tr.append_message(C.string_at(lab, ll), C.string_at(msg, ml) if ml else b"")
+            return 0
+        except Exception as e:  # noqa: BLE001 (reported through BPP_ERR_CALLBACK)
+            h.error = e
+            return 1
+
+    def _challenge(_u, lab, ll, out, n):
+        try:
+            b = tr.challenge_bytes(C.string_at(lab, ll), n)
+            if len(b) != n:
+                raise ValueError("challenge_bytes returned %d bytes, wanted %d" % (len(b), n))
+            C.memmove(out, b, n)
+            return 0
+        except Exception as e:  # noqa: BLE001
+            h.error = e
+            return 1
+
+    h.fa, h.fc = _APPEND_FN(_append), _CHALLENGE_FN(_challenge)  # (kept alive with h)
+    h.s = _Hooks(None, h.fa, h.fc)
+    return h
+
+
+def _tr_args(tr, lib, plain: str):
+    """(function, transcript argument, hooks holder) for a library Transcript
+    (bpp_transcript*) or a caller-owned one (hooks)."""
+    if isinstance(tr, Transcript):
+        return getattr(lib, plain), tr.h, None
+    h = transcript_hooks(tr)
+    return getattr(lib, plain + "_cb"), C.byref(h.s), h
+
+
 class Gens:
     """BulletproofGens(n, 1) + PedersenGens resident on the GPU (bpp_gens)."""
 
@@ -405,8 +459,10 @@ class Gens:
                                           len(ab) // 32, out), "bpp_vec_commit", self.ctx.h)
         return out.raw
 
-    def ipa_prove(self, tr: Transcript, Q: bytes, G_factors, H_factors, a, b):
-        """InnerProductProof::create -> (L list, R list, a, b)."""
+    def ipa_prove(self, tr, Q: bytes, G_factors, H_factors, a, b):
+        """InnerProductProof::create -> (L list, R list, a, b).  `tr`: a
+        bpperm.Transcript, or the caller's own transcript object (merlin's
+        append_message / challenge_bytes; bpp_ipa_prove_cb)."""
         ab, bb = _join(a, 32, "a"), _join(b, 32, "b")
         n = len(ab) // 32
         gf = _join(G_factors, 32, "G_factors") if G_factors is not None else None
@@ -415,20 +471,25 @@ class Gens:
         Lo = C.create_string_buffer(32 * max(lg, 1))
         Ro = C.create_string_buffer(32 * max(lg, 1))
         ao, bo = C.create_string_buffer(32), C.create_string_buffer(32)
-        check(self.ctx.lib.bpp_ipa_prove(self.ctx.h, self.h, tr.h, _buf(Q), _buf(gf) if gf else None,
-                                         _buf(hf) if hf else None, _buf(ab), _buf(bb), n, Lo, Ro, ao, bo),
-              "bpp_ipa_prove", self.ctx.h)
+        fn, targ, hooks = _tr_args(tr, self.ctx.lib, "bpp_ipa_prove")
+        rc = fn(self.ctx.h, self.h, targ, _buf(Q), _buf(gf) if gf else None, _buf(hf) if hf else None, _buf(ab),
+                _buf(bb), n, Lo, Ro, ao, bo)
+        if hooks is not None and hooks.error is not None:
+            raise hooks.error
+        check(rc, "bpp_ipa_prove", self.ctx.h)
         lraw, rraw = Lo.raw, Ro.raw
         return ([lraw[32 * i: 32 * i + 32] for i in range(lg)], [rraw[32 * i: 32 * i + 32] for i in range(lg)],
                 ao.raw, bo.raw)
 
-    def ipa_verify(self, tr: Transcript, n: int, G_factors, H_factors, P: bytes, Q: bytes, L, R, a: bytes,
+    def ipa_verify(self, tr, n: int, G_factors, H_factors, P: bytes, Q: bytes, L, R, a: bytes,
                    b: bytes) -> bool:
         gf = _join(G_factors, 32, "G_factors") if G_factors is not None else None
         hf = _join(H_factors, 32, "H_factors") if H_factors is not None else None
-        rc = self.ctx.lib.bpp_ipa_verify(self.ctx.h, self.h, tr.h, n, _buf(gf) if gf else None,
-                                         _buf(hf) if hf else None, _buf(P), _buf(Q), _buf(b"".join(L)),
-                                         _buf(b"".join(R)), _buf(a), _buf(b))
+        fn, targ, hooks = _tr_args(tr, self.ctx.lib, "bpp_ipa_verify")
+        rc = fn(self.ctx.h, self.h, targ, n, _buf(gf) if gf else None, _buf(hf) if hf else None, _buf(P), _buf(Q),
+                _buf(b"".join(L)), _buf(b"".join(R)), _buf(a), _buf(b))
+        if hooks is not None and hooks.error is not None:
+            raise hooks.error
         if rc == 6:
             return False
         check(rc, "bpp_ipa_verify", self.ctx.h)
@@ -537,21 +598,6 @@ class PermProver:
         on the host (bpp_perm_verify_begin)."""
         return VerifyJob(self.k, proofs, Vs, self.label, ctx=self.ctx if device else None)
 
-    def verify_partial_gathered(self, job: "VerifyJob", d_blocks: int, stride: int, counts: Sequence[int],
-                                w_begin: int, w_end: int) -> bytes:
-        """128-B raw partial of a sliced job's MSM over ALL its proofs, windows
-        [w_begin, w_end), from every slice's scalar block gathered at d_blocks
-        (block s at d_blocks + s * stride; bpp_perm_verify_partial_gathered).
-        None when a proof point does not decode."""
-        part = C.create_string_buffer(128)
-        cn = (C.c_size_t * max(len(counts), 1))(*counts)
-        rc = self.ctx.lib.bpp_perm_verify_partial_gathered(self.ctx.h, self.gens.h, job.h, d_blocks, stride, cn,
-                                                           len(counts), w_begin, w_end, part)
-        if rc == 6:
-            return None
-        check(rc, "bpp_perm_verify_partial_gathered", self.ctx.h)
-        return part.raw
-
     def verify_partial_sharded(self, job: "VerifyJob", first: int, d_blocks: int, stride: int, d_pblocks: int,
                                pstride: int, counts: Sequence[int], w_begin: int, w_end: int) -> bytes:
         """128-B raw partial of the whole batch's MSM over windows [w_begin,
@@ -590,11 +636,8 @@ class VerifyJob:
     verifier seed (bpp_perm_verify_scalars)."""
 
     def __init__(self, k: int, proofs: Sequence[bytes], Vs: Sequence[bytes], label: bytes = b"bp-perm",
-                 ctx: "Context | None" = None, replay: "tuple[int, int] | None" = None, wait: bool = True):
-        """replay=(first, n): a sliced device job (bpp_perm_verify_begin_dev_slice):
-        every proof uploaded and decompressed, proofs [first, first + n)
-        replayed; `r` then holds the slice's n challenges.  wait=False (a
-        device job over all its proofs): bpp_perm_verify_begin_dev_async --
+                 ctx: "Context | None" = None, wait: bool = True):
+        """wait=False (a device job): bpp_perm_verify_begin_dev_async --
         returns before the replay ends, `r` is None and a rejected proof
         surfaces as False from slice_scalars / verify_partial."""
         self.lib = _lib.load()
@@ -602,28 +645,23 @@ class VerifyJob:
         self.count = len(proofs)
         self.device = ctx is not None
         self.ctx = ctx
-        self.slice = replay
         h = C.c_void_p()
-        nr = self.count if replay is None else replay[1]
+        nr = self.count
         r = C.create_string_buffer(32 * nr + 1)
         pb, vb = _buf(b"".join(proofs)), _buf(b"".join(Vs))
         if ctx is None:
             rc = self.lib.bpp_perm_verify_begin(k, self.count, _buf(label), len(label), pb, vb, r, C.byref(h))
             name = "bpp_perm_verify_begin"
-        elif replay is None and not wait:
+        elif not wait:
             self._keep = (pb, vb)  # (pinned inputs are read after the return; these are staged, but keep them)
             rc = self.lib.bpp_perm_verify_begin_dev_async(ctx.h, k, self.count, _buf(label), len(label), pb, vb,
                                                           C.byref(h))
             name = "bpp_perm_verify_begin_dev_async"
             nr = 0
-        elif replay is None:
+        else:
             rc = self.lib.bpp_perm_verify_begin_dev(ctx.h, k, self.count, _buf(label), len(label), pb, vb, r,
                                                     C.byref(h))
             name = "bpp_perm_verify_begin_dev"
-        else:
-            rc = self.lib.bpp_perm_verify_begin_dev_slice(ctx.h, k, self.count, _buf(label), len(label), pb, vb,
-                                                          replay[0], replay[1], r, C.byref(h))
-            name = "bpp_perm_verify_begin_dev_slice"
         if rc == 6:
             self.h = None
             self.r = None
@@ -639,7 +677,7 @@ class VerifyJob:
         """The replayed slice's MSM scalars into device memory d_out
         (slice_bytes() bytes; bpp_perm_verify_slice_scalars_at), weighted from
         the batch's verifier seed; first = the batch index of the job's first
-        proof (0 for a job over the whole batch with a replay slice).  False
+        proof.  False
         if an asynchronous begin's replay rejected a proof."""
         rc = self.lib.bpp_perm_verify_slice_scalars_at(self.ctx.h, self.h, _seed(seed), first, d_out)
         if rc == 6:

@@ -22,6 +22,7 @@ ERRORS = {
     5: "BPP_ERR_DEVICE",
     6: "BPP_ERR_VERIFY",
     7: "BPP_ERR_NOMEM",
+    8: "BPP_ERR_CALLBACK",
 }
 
 vp = C.c_void_p
@@ -83,6 +84,8 @@ SIGNATURES = {
     "bpp_transcript_challenge_scalar": (i32, [vp, vp, sz, vp]),
     "bpp_ipa_prove": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, vp]),
     "bpp_ipa_verify": (i32, [vp, vp, vp, sz, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "bpp_ipa_prove_cb": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, sz, vp, vp, vp, vp]),
+    "bpp_ipa_verify_cb": (i32, [vp, vp, vp, sz, vp, vp, vp, vp, vp, vp, vp, vp]),
     "bpp_perm_proof_len": (sz, [u32]),
     "bpp_perm_prove": (i32, [vp, vp, u32, u64, vp, sz, vp, vp, vp]),
     "bpp_perm_prove_batch": (i32, [vp, vp, u32, sz, vp, vp, sz, vp, vp]),
@@ -98,10 +101,7 @@ SIGNATURES = {
     "bpp_scalar_powers": (i32, [vp, sz, vp]),
     "bpp_perm_verify_scalars": (i32, [vp, vp, sz, vp, vp]),
     "bpp_perm_verify_partial": (i32, [vp, vp, vp, vp, sz, u32, u32, vp]),
-    "bpp_perm_verify_begin_dev_slice": (i32, [vp, u32, sz, vp, sz, vp, vp, sz, sz, vp, C.POINTER(vp)]),
     "bpp_perm_verify_slice_bytes": (sz, [vp]),
-    "bpp_perm_verify_slice_scalars": (i32, [vp, vp, vp, vp]),
-    "bpp_perm_verify_partial_gathered": (i32, [vp, vp, vp, vp, sz, vp, sz, u32, u32, vp]),
     "bpp_perm_verify_slice_scalars_at": (i32, [vp, vp, vp, sz, vp]),
     "bpp_perm_verify_begin_dev_async": (i32, [vp, u32, sz, vp, sz, vp, vp, vp]),
     "bpp_perm_verify_slice_point_bytes": (sz, [vp]),

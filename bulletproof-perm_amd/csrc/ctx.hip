@@ -49,10 +49,15 @@ bool host_is_pinned(const void* p, size_t n) {
     return !e || atoi(e) != 0;
   }();
   if (!query) return false;
-  hipPointerAttribute_t at;
-  const bool pin = hipPointerGetAttributes(&at, p) == hipSuccess && at.type == hipMemoryTypeHost;
-  (void)hipGetLastError();  // (a pageable pointer leaves an error code behind)
-  return pin;
+  // both ends of [p, p + n) must be page-locked (a buffer the caller
+  // registered only in part is staged as pageable)
+  auto pinned_at = [](const void* q) {
+    hipPointerAttribute_t at;
+    const bool pin = hipPointerGetAttributes(&at, q) == hipSuccess && at.type == hipMemoryTypeHost;
+    (void)hipGetLastError();  // (a pageable pointer leaves an error code behind)
+    return pin;
+  };
+  return pinned_at(p) && (n <= 1 || pinned_at((const uint8_t*)p + n - 1));
 }
 
 // Non-temporal copy into the pinned arena: the arena is only read back by
@@ -230,6 +235,24 @@ static int stage_take(bpp_ctx* ctx, size_t bytes, uint8_t** out) {
   }
   *out = ctx->stage + ctx->stage_used;
   ctx->stage_used += need;
+  // the arena is reused after every sync: bytes handed out again no longer
+  // belong to the last wipe, so they leave its span list (what is left of a
+  // span still holds the wipe's zeros for bpp_debug_secret_residue)
+  if (!ctx->wiped.empty()) {
+    uint8_t *lo = *out, *hi = *out + need;
+    std::vector<std::pair<uint8_t*, size_t>> keep;
+    keep.reserve(ctx->wiped.size() + 1);
+    for (const auto& s : ctx->wiped) {
+      uint8_t *a = s.first, *b = s.first + s.second;
+      if (b <= lo || hi <= a) {
+        keep.push_back(s);
+        continue;
+      }
+      if (a < lo) keep.push_back({a, (size_t)(lo - a)});
+      if (hi < b) keep.push_back({hi, (size_t)(b - hi)});
+    }
+    ctx->wiped.swap(keep);
+  }
   return BPP_OK;
 }
 

@@ -29,23 +29,64 @@ struct IpaProofHost {
   hsc::Sc a, b;
 };
 
+// The transcript of ONE inner-product argument, as bulletproofs 4.0.0 drives
+// it: innerproduct_domain_sep(n) = append_message("dom-sep", "ipp v1") +
+// append_u64("n", n); per round append_point("L"), append_point("R"),
+// challenge_scalar("u") = 64 challenge bytes reduced wide
+// (transcript_protocol.rs:26-67).  Two primitives are all it needs, so a
+// caller-owned merlin::Transcript can sit behind C hooks (bpp_ipa_prove_cb);
+// a false return (a hook failed) aborts the IPA.
+struct IpaTranscript {
+  virtual ~IpaTranscript() = default;
+  virtual bool append(const char* label, const uint8_t* msg, size_t n) = 0;
+  virtual bool challenge(const char* label, uint8_t* out, size_t n) = 0;
+  bool domain_sep(uint64_t n) {
+    uint8_t le[8];
+    memcpy(le, &n, 8);
+    return append("dom-sep", (const uint8_t*)"ipp v1", 6) && append("n", le, 8);
+  }
+  bool challenge_scalar(const char* label, hsc::Sc& out) {
+    uint8_t buf[64];
+    if (!challenge(label, buf, 64)) return false;
+    out = hsc::from_wide(buf);
+    return true;
+  }
+};
+
+// The library's own Merlin behind that interface (bpp_transcript*).
+struct IpaMerlin final : IpaTranscript {
+  merlin::Transcript& t;
+  explicit IpaMerlin(merlin::Transcript& tr) : t(tr) {}
+  bool append(const char* label, const uint8_t* msg, size_t n) override {
+    t.append(label, msg, n);
+    return true;
+  }
+  bool challenge(const char* label, uint8_t* out, size_t n) override {
+    t.challenge_bytes(label, out, n);
+    return true;
+  }
+};
+
 // a, b, Gf, Hf: device arrays of n canonical scalars (Gf/Hf may be null =
-// all ones).  a and b are consumed.
-int ipa_prove_dev(bpp_ctx* ctx, merlin::Transcript& tr, const IpaGens& g, uint32_t n, const uint32_t* d_Gf,
+// all ones).  a and b are consumed.  BPP_ERR_CALLBACK when a transcript hook
+// fails.
+int ipa_prove_dev(bpp_ctx* ctx, IpaTranscript& tr, const IpaGens& g, uint32_t n, const uint32_t* d_Gf,
                   const uint32_t* d_Hf, const uint32_t* d_a, const uint32_t* d_b, IpaProofHost& out);
 
 // P instances in lockstep (one per transcript): d_a, d_b, d_Gf, d_Hf are
-// [P][n] (Gf/Hf may be null); Q_p = qmul[p] * P[g.qidx].
+// [P][n] (Gf/Hf may be null); Q_p = qmul[p] * P[g.qidx].  `one` (P = 1, trs
+// ignored): the single instance's transcript behind the generic interface.
 int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& trs, const IpaGens& g, uint32_t n,
                         const uint32_t* d_Gf, const uint32_t* d_Hf, const uint32_t* d_a, const uint32_t* d_b,
-                        const std::vector<hsc::Sc>& qmul, std::vector<IpaProofHost>& out);
+                        const std::vector<hsc::Sc>& qmul, std::vector<IpaProofHost>& out,
+                        IpaTranscript* one = nullptr);
 
 // Replays the verifier side of the transcript; returns false on malformed
-// proof (identity L/R, wrong length).  Fills u^2, u^-2 and s (bulletproofs
-// verification_scalars).
-bool ipa_verification_scalars(merlin::Transcript& tr, uint32_t n, const std::vector<Enc32>& L,
+// proof (identity L/R, wrong length) or a failed hook (*hook_failed set).
+// Fills u^2, u^-2 and s (bulletproofs verification_scalars).
+bool ipa_verification_scalars(IpaTranscript& tr, uint32_t n, const std::vector<Enc32>& L,
                               const std::vector<Enc32>& R, std::vector<hsc::Sc>& u_sq,
-                              std::vector<hsc::Sc>& uinv_sq, std::vector<hsc::Sc>& s);
+                              std::vector<hsc::Sc>& uinv_sq, std::vector<hsc::Sc>& s, bool* hook_failed = nullptr);
 
 static const hsc::Sc SC_R_MOD_L = {{0xd6ec31748d98951dULL, 0xc6ef5bf4737dcf70ULL, 0xfffffffffffffffeULL,
                                     0x0fffffffffffffffULL}};

@@ -564,6 +564,11 @@ static sc to_dev_sc(const hsc::Sc& x) {
   return r;
 }
 
+static int ipa_hook_failed(bpp_ctx* ctx) {
+  ctx->err = "ipa: a transcript hook returned an error";
+  return BPP_ERR_CALLBACK;
+}
+
 static hsc::Sc from_dev_words(const uint32_t w[8]) {
   hsc::Sc r;
   for (int i = 0; i < 4; ++i) r.v[i] = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
@@ -572,8 +577,9 @@ static hsc::Sc from_dev_words(const uint32_t w[8]) {
 
 int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& trs, const IpaGens& g, uint32_t n,
                         const uint32_t* d_Gf, const uint32_t* d_Hf, const uint32_t* d_a, const uint32_t* d_b,
-                        const std::vector<hsc::Sc>& qmul, std::vector<IpaProofHost>& out) {
-  const uint32_t P = (uint32_t)trs.size();
+                        const std::vector<hsc::Sc>& qmul, std::vector<IpaProofHost>& out,
+                        IpaTranscript* one) {
+  const uint32_t P = one ? 1u : (uint32_t)trs.size();
   if (n == 0 || (n & (n - 1))) {
     ctx->err = "ipa: n must be a power of two";
     return BPP_ERR_LEN;
@@ -587,7 +593,11 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
   if (!P) return BPP_OK;
   uint32_t lg_n = 0;
   while ((1u << lg_n) < n) ++lg_n;
-  par::for_each(P, [&](size_t p) { trs[p]->innerproduct_domain_sep(n); });
+  if (one) {
+    if (!one->domain_sep(n)) return ipa_hook_failed(ctx);
+  } else {
+    par::for_each(P, [&](size_t p) { trs[p]->innerproduct_domain_sep(n); });
+  }
   const size_t PN = (size_t)P * n, PT = (size_t)P * (2 * n + 2);
   void *am, *bm, *fG, *fH, *scal, *pidx, *part, *d_q, *d_u;
   BPP_TRY(ctx_ws(ctx, "ipa_am", PN * 32, &am));
@@ -669,7 +679,7 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
   // k_compress_p3 of L and R, k_ipa_transcript_step (Merlin + u^-1) --
   // with no host round trip; L, R and the transcripts come back at the end.
   const char* dm_env = getenv("BPP_IPA_DEVICE_MERLIN");
-  const bool dev_merlin = fused && dm_env && atoi(dm_env) != 0;
+  const bool dev_merlin = fused && !one && dm_env && atoi(dm_env) != 0;
   // Host round trip of the fused rounds without copy launches: the round
   // kernel writes L/2, R/2 straight into pinned host memory and reads the
   // challenges u, u^-1 from it (ctx_host_buf), where a device result buffer
@@ -809,6 +819,11 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
     }
     if (!dev_merlin) {
     HostScope hs(ctx, "ipa_host");
+    if (one) {  // the caller's transcript (bpp_ipa_prove_cb), one instance
+      if (!one->append("L", enc.data(), 32) || !one->append("R", enc.data() + 32, 32) ||
+          !one->challenge_scalar("u", u[0]))
+        return ipa_hook_failed(ctx);
+    } else
     // L, R appends and the u challenge of eight proofs at a time on the
     // 8-way Keccak (their transcripts are in lockstep)
     merlin::lockstep_x8(
@@ -904,25 +919,35 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
   return BPP_OK;
 }
 
-int ipa_prove_dev(bpp_ctx* ctx, merlin::Transcript& tr, const IpaGens& g, uint32_t n, const uint32_t* d_Gf,
+int ipa_prove_dev(bpp_ctx* ctx, IpaTranscript& tr, const IpaGens& g, uint32_t n, const uint32_t* d_Gf,
                   const uint32_t* d_Hf, const uint32_t* d_a, const uint32_t* d_b, IpaProofHost& out) {
   std::vector<IpaProofHost> o;
-  BPP_TRY(ipa_prove_batch_dev(ctx, {&tr}, g, n, d_Gf, d_Hf, d_a, d_b, {g.qmul}, o));
+  BPP_TRY(ipa_prove_batch_dev(ctx, {}, g, n, d_Gf, d_Hf, d_a, d_b, {g.qmul}, o, &tr));
   out = std::move(o[0]);
   return BPP_OK;
 }
 
-bool ipa_verification_scalars(merlin::Transcript& tr, uint32_t n, const std::vector<Enc32>& L,
+bool ipa_verification_scalars(IpaTranscript& tr, uint32_t n, const std::vector<Enc32>& L,
                               const std::vector<Enc32>& R, std::vector<hsc::Sc>& u_sq,
-                              std::vector<hsc::Sc>& uinv_sq, std::vector<hsc::Sc>& s) {
+                              std::vector<hsc::Sc>& uinv_sq, std::vector<hsc::Sc>& s, bool* hook_failed) {
   const size_t lg_n = L.size();
+  if (hook_failed) *hook_failed = false;
   if (lg_n >= 32 || R.size() != lg_n || n != (1u << lg_n)) return false;
-  tr.innerproduct_domain_sep(n);
+  auto failed = [&] {
+    if (hook_failed) *hook_failed = true;
+    return false;
+  };
+  if (!tr.domain_sep(n)) return failed();
   std::vector<hsc::Sc> u(lg_n);
+  static const uint8_t zero[32] = {0};
   for (size_t j = 0; j < lg_n; ++j) {
-    if (!tr.validate_and_append_point("L", L[j].data())) return false;
-    if (!tr.validate_and_append_point("R", R[j].data())) return false;
-    u[j] = tr.challenge_scalar("u");
+    // validate_and_append_point (transcript_protocol.rs:48-60): the identity
+    // encoding is a VerificationError before anything is appended
+    if (!memcmp(L[j].data(), zero, 32)) return false;
+    if (!tr.append("L", L[j].data(), 32)) return failed();
+    if (!memcmp(R[j].data(), zero, 32)) return false;
+    if (!tr.append("R", R[j].data(), 32)) return failed();
+    if (!tr.challenge_scalar("u", u[j])) return failed();
   }
   std::vector<hsc::Sc> ui = u;
   const hsc::Sc allinv = hsc::batch_invert(ui);

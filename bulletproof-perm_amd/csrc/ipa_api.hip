@@ -208,11 +208,9 @@ int ipa_q_slot(bpp_ctx* ctx, const bpp_gens* g, const uint8_t Q[32], uint32_t dt
 }
 }  // namespace
 
-extern "C" {
-
-int bpp_ipa_prove(bpp_ctx* ctx, const bpp_gens* g, bpp_transcript* tr, const uint8_t Q[32], const uint8_t* G_factors,
-                  const uint8_t* H_factors, const uint8_t* a, const uint8_t* b, size_t n, uint8_t* L_out,
-                  uint8_t* R_out, uint8_t a_out[32], uint8_t b_out[32]) {
+static int ipa_prove_api(bpp_ctx* ctx, const bpp_gens* g, IpaTranscript* tr, const uint8_t Q[32],
+                         const uint8_t* G_factors, const uint8_t* H_factors, const uint8_t* a, const uint8_t* b,
+                         size_t n, uint8_t* L_out, uint8_t* R_out, uint8_t a_out[32], uint8_t b_out[32]) {
   return bpp_guard(ctx, [&]() -> int {
     if (!ctx || !g || !tr || !Q || !a || !b || !a_out || !b_out || ((!L_out || !R_out) && n > 1)) return BPP_ERR_ARG;
     if (n == 0 || (n & (n - 1)) || n > g->n) return BPP_ERR_LEN;
@@ -246,7 +244,13 @@ int bpp_ipa_prove(bpp_ctx* ctx, const bpp_gens* g, bpp_transcript* tr, const uin
       ig.qidx = ig.pts.n0;
     }
     IpaProofHost pf;
-    BPP_TRY(ipa_prove_dev(ctx, tr->t, ig, (uint32_t)n, d_gf, d_hf, d_a, d_b, pf));
+    {
+      const int rc = ipa_prove_dev(ctx, *tr, ig, (uint32_t)n, d_gf, d_hf, d_a, d_b, pf);
+      // a failed IPA (a hook error, a device error) may leave this context's
+      // kernels queued on the Q slot: drain them before the slot's lock goes
+      if (rc != BPP_OK && qlock.owns_lock()) (void)hipStreamSynchronize(ctx->stream);
+      BPP_TRY(rc);
+    }
     for (size_t j = 0; j < pf.L.size(); ++j) {
       memcpy(L_out + 32 * j, pf.L[j].data(), 32);
       memcpy(R_out + 32 * j, pf.R[j].data(), 32);
@@ -257,9 +261,9 @@ int bpp_ipa_prove(bpp_ctx* ctx, const bpp_gens* g, bpp_transcript* tr, const uin
   });
 }
 
-int bpp_ipa_verify(bpp_ctx* ctx, const bpp_gens* g, bpp_transcript* tr, size_t n, const uint8_t* G_factors,
-                   const uint8_t* H_factors, const uint8_t P[32], const uint8_t Q[32], const uint8_t* L,
-                   const uint8_t* R, const uint8_t a[32], const uint8_t b[32]) {
+static int ipa_verify_api(bpp_ctx* ctx, const bpp_gens* g, IpaTranscript* tr, size_t n, const uint8_t* G_factors,
+                          const uint8_t* H_factors, const uint8_t P[32], const uint8_t Q[32], const uint8_t* L,
+                          const uint8_t* R, const uint8_t a[32], const uint8_t b[32]) {
   return bpp_guard(ctx, [&]() -> int {
     if (!ctx || !g || !tr || !P || !Q || !a || !b || ((!L || !R) && n > 1)) return BPP_ERR_ARG;
     if (n == 0 || (n & (n - 1)) || n > g->n) return BPP_ERR_LEN;
@@ -279,7 +283,11 @@ int bpp_ipa_verify(bpp_ctx* ctx, const bpp_gens* g, bpp_transcript* tr, size_t n
       if (H_factors && !hsc::from_canonical(hf[i], H_factors + 32 * i)) return BPP_ERR_NONCANONICAL;
     }
     std::vector<hsc::Sc> u_sq, uinv_sq, s;
-    if (!ipa_verification_scalars(tr->t, (uint32_t)n, Lv, Rv, u_sq, uinv_sq, s)) return BPP_ERR_VERIFY;
+    bool hook_failed = false;
+    if (!ipa_verification_scalars(*tr, (uint32_t)n, Lv, Rv, u_sq, uinv_sq, s, &hook_failed)) {
+      if (hook_failed) ctx->err = "ipa: a transcript hook returned an error";
+      return hook_failed ? BPP_ERR_CALLBACK : BPP_ERR_VERIFY;
+    }
     // extra points: Q, L_0.., R_0.., P
     std::vector<uint8_t> extra((2 + 2 * lg) * 32);
     memcpy(extra.data(), Q, 32);
@@ -320,6 +328,56 @@ int bpp_ipa_verify(bpp_ctx* ctx, const bpp_gens* g, bpp_transcript* tr, size_t n
     static const uint8_t zero[32] = {0};
     return memcmp(e, zero, 32) == 0 ? BPP_OK : BPP_ERR_VERIFY;
   });
+}
+
+namespace {
+// the caller's transcript behind C hooks (bpp_transcript_hooks)
+struct IpaHooks final : IpaTranscript {
+  const bpp_transcript_hooks& h;
+  explicit IpaHooks(const bpp_transcript_hooks& hooks) : h(hooks) {}
+  bool append(const char* label, const uint8_t* msg, size_t n) override {
+    return h.append_message(h.user, (const uint8_t*)label, strlen(label), msg, n) == 0;
+  }
+  bool challenge(const char* label, uint8_t* out, size_t n) override {
+    return h.challenge_bytes(h.user, (const uint8_t*)label, strlen(label), out, n) == 0;
+  }
+};
+bool hooks_ok(const bpp_transcript_hooks* h) { return h && h->append_message && h->challenge_bytes; }
+}  // namespace
+
+extern "C" {
+
+int bpp_ipa_prove_cb(bpp_ctx* ctx, const bpp_gens* g, const bpp_transcript_hooks* tr, const uint8_t Q[32],
+                     const uint8_t* G_factors, const uint8_t* H_factors, const uint8_t* a, const uint8_t* b, size_t n,
+                     uint8_t* L_out, uint8_t* R_out, uint8_t a_out[32], uint8_t b_out[32]) {
+  if (!hooks_ok(tr)) return BPP_ERR_ARG;
+  IpaHooks t(*tr);
+  return ipa_prove_api(ctx, g, &t, Q, G_factors, H_factors, a, b, n, L_out, R_out, a_out, b_out);
+}
+
+int bpp_ipa_verify_cb(bpp_ctx* ctx, const bpp_gens* g, const bpp_transcript_hooks* tr, size_t n,
+                      const uint8_t* G_factors, const uint8_t* H_factors, const uint8_t P[32], const uint8_t Q[32],
+                      const uint8_t* L, const uint8_t* R, const uint8_t a[32], const uint8_t b[32]) {
+  if (!hooks_ok(tr)) return BPP_ERR_ARG;
+  IpaHooks t(*tr);
+  return ipa_verify_api(ctx, g, &t, n, G_factors, H_factors, P, Q, L, R, a, b);
+}
+
+// the library's own Merlin behind the same code path
+int bpp_ipa_prove(bpp_ctx* ctx, const bpp_gens* g, bpp_transcript* tr, const uint8_t Q[32], const uint8_t* G_factors,
+                  const uint8_t* H_factors, const uint8_t* a, const uint8_t* b, size_t n, uint8_t* L_out,
+                  uint8_t* R_out, uint8_t a_out[32], uint8_t b_out[32]) {
+  if (!tr) return BPP_ERR_ARG;
+  IpaMerlin t(tr->t);
+  return ipa_prove_api(ctx, g, &t, Q, G_factors, H_factors, a, b, n, L_out, R_out, a_out, b_out);
+}
+
+int bpp_ipa_verify(bpp_ctx* ctx, const bpp_gens* g, bpp_transcript* tr, size_t n, const uint8_t* G_factors,
+                   const uint8_t* H_factors, const uint8_t P[32], const uint8_t Q[32], const uint8_t* L,
+                   const uint8_t* R, const uint8_t a[32], const uint8_t b[32]) {
+  if (!tr) return BPP_ERR_ARG;
+  IpaMerlin t(tr->t);
+  return ipa_verify_api(ctx, g, &t, n, G_factors, H_factors, P, Q, L, R, a, b);
 }
 
 }  // extern "C"

@@ -690,7 +690,12 @@ int bpp_partials_finish(const uint8_t* partials, size_t count, uint8_t out[32]) 
     for (size_t i = 0; i < count; ++i) {
       uint32_t w[32];
       memcpy(w, partials + 128 * i, 128);
-      acc = h25519::ge_add(acc, h25519::ge_from_words(w));
+      const h25519::ge p = h25519::ge_from_words(w);
+      // Z = 0 is no extended point (e.g. a partial a failed rank never
+      // wrote): it would absorb the sum and encode as the identity, so it
+      // is refused rather than accepted as one
+      if (h25519::fe_iszero(p.Z)) return BPP_ERR_ARG;
+      acc = h25519::ge_add(acc, p);
     }
     h25519::encode(out, acc);
     return BPP_OK;

@@ -1435,58 +1435,10 @@ static int gather_blocks_dev(bpp_ctx* ctx, const uint8_t* src, size_t stride, si
   return ctx_check_launch(ctx, "k_gather_blocks");
 }
 
-// The MSM of a sliced job over windows [wb, we) with the scalars of every
-// slice gathered (bpp_perm_verify_partial_gathered): block r (stride bytes
-// apart) holds slice r's [NG | counts[r] x npt]; the generator scalars are
-// the sum of the blocks' NG heads, the proof-point scalars the blocks' tails
-// in slice (= proof) order.
-int verify_partial_gathered_dev(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J, const uint8_t* d_blocks,
-                                size_t stride, const size_t* counts, size_t nslices, uint32_t wb, uint32_t we,
-                                h25519::ge* out) {
-  if (J.dctx != ctx || J.dgen != ctx->vjob_gen) {
-    ctx->err = "device verify job belongs to another context or was superseded by a later begin";
-    return BPP_ERR_ARG;
-  }
-  if (G->n < J.C.n_p) {
-    ctx->err = "generators shorter than the padded circuit";
-    return BPP_ERR_LEN;
-  }
-  const size_t NG = 2 * (size_t)J.C.n_p + 2, npt = J.npt, T = NG + J.count * npt;
-  size_t sum = 0;
-  bool mine = false;  // this job's replayed slice sits at its place among the blocks
-  for (size_t r = 0; r < nslices; ++r) {
-    if ((NG + counts[r] * npt) * 32 > stride) return BPP_ERR_ARG;
-    mine |= sum == J.rfirst && counts[r] == J.rcount;
-    sum += counts[r];
-  }
-  if (sum != J.count || stride % 16) return BPP_ERR_ARG;
-  if (!mine) {
-    ctx->err = "the gathered blocks do not hold this job's slice at its proof offset";
-    return BPP_ERR_ARG;
-  }
-  void *d_sv = nullptr, *d_x = nullptr, *d_dbad = nullptr;
-  BPP_TRY(ctx_ws(ctx, "pv_s", T * 32 + 32, &d_sv));
-  BPP_TRY(ctx_ws(ctx, "vj_x", J.count * npt * MSM_NIELS_WORDS * 4, &d_x));
-  BPP_TRY(ctx_ws(ctx, "vj_dbad", 8, &d_dbad));
-  BPP_TRY(verify_sum_blocks_dev(ctx, (uint32_t)nslices, (uint32_t)NG, (const uint32_t*)d_blocks,
-                                (uint32_t)(stride / 4), (uint32_t*)d_sv));
-  BPP_TRY(gather_blocks_dev(ctx, d_blocks, stride, NG * 32, npt * 32, counts, nslices, (uint8_t*)d_sv + NG * 32));
-  uint64_t* h_dbad = nullptr;
-  BPP_TRY(ctx_zc_out(ctx, "vj_dbad_h", 8, (uint32_t**)&h_dbad));
-  BPP_HIP(hipStreamWaitEvent(ctx->stream, ctx->vj_ev_dec, 0));
-  BPP_HIP(hipMemcpyAsync(h_dbad, d_dbad, 8, hipMemcpyDeviceToHost, ctx->stream));
-  BPP_TRY(verify_msm(ctx, G, J.C, J.count, (const uint32_t*)d_sv, (const uint32_t*)d_x, wb, we, out));
-  BPP_TRY(ctx_sync(ctx));
-  if (*h_dbad != ~0ull) {
-    ctx->err = "undecodable proof point at index " + std::to_string(*h_dbad);
-    return BPP_ERR_VERIFY;
-  }
-  return BPP_OK;
-}
-
 // The MSM of a sharded batch over windows [wb, we) (bpp_perm_verify_partial_sharded):
-// slice s's scalar block at d_blocks + s stride ([NG | counts[s] x npt], as
-// verify_partial_gathered_dev) and its decompressed points at d_pblocks + s
+// slice s's scalar block at d_blocks + s stride ([NG | counts[s] x npt]:
+// the generator scalars summed over the slice, then its proof-point scalars)
+// and its decompressed points at d_pblocks + s
 // pstride (counts[s] x npt Niels records, bpp_perm_verify_slice_points); J is
 // this rank's job over its own slice, batch proofs [first, first + J.count).
 int verify_partial_sharded_dev(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J, size_t first,
@@ -1548,7 +1500,7 @@ int verify_partial_dev(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job& J,
     return BPP_ERR_ARG;
   }
   if (J.rcount != J.count) {
-    ctx->err = "a sliced verify job takes bpp_perm_verify_slice_scalars / _partial_gathered";
+    ctx->err = "a partially replayed job has no whole-batch partial";
     return BPP_ERR_ARG;
   }
   if (G->n < J.C.n_p) {
@@ -1859,30 +1811,8 @@ int bpp_perm_verify_scalars(const bpp_verify_job* job, const uint8_t seed[32], s
   });
 }
 
-int bpp_perm_verify_begin_dev_slice(bpp_ctx* ctx, uint32_t k, size_t count, const uint8_t* label, size_t llen,
-                                    const uint8_t* proofs, const uint8_t* V, size_t first, size_t n, uint8_t* r_out,
-                                    bpp_verify_job** out) {
-  return bpp_guard(ctx, [&]() -> int {
-    if (!ctx || !out || ((!proofs || !V) && count) || (!label && llen) || k < 2 || k > (1u << 20) ||
-        first > count || n > count - first)
-      return BPP_ERR_ARG;
-    *out = nullptr;
-    BPP_HIP(hipSetDevice(ctx->device));
-    const perm::Circuit C = perm::build(k);
-    std::unique_ptr<bpp_verify_job> job;
-    BPP_TRY(verify_begin_dev(ctx, C, label, llen, count, proofs, V, job, first, n));
-    if (r_out && n) memcpy(r_out, job->rs.data(), 32 * n);
-    *out = job.release();
-    return BPP_OK;
-  });
-}
-
 size_t bpp_perm_verify_slice_bytes(const bpp_verify_job* job) {
   return job ? (2 * (size_t)job->C.n_p + 2 + job->rcount * job->npt) * 32 : 0;
-}
-
-int bpp_perm_verify_slice_scalars(bpp_ctx* ctx, const bpp_verify_job* job, const uint8_t seed[32], void* d_out) {
-  return bpp_perm_verify_slice_scalars_at(ctx, job, seed, 0, d_out);
 }
 
 int bpp_perm_verify_slice_scalars_at(bpp_ctx* ctx, const bpp_verify_job* job, const uint8_t seed[32], size_t first,
@@ -1927,24 +1857,6 @@ int bpp_perm_verify_partial_sharded(bpp_ctx* ctx, const bpp_gens* G, const bpp_v
   });
 }
 
-int bpp_perm_verify_partial_gathered(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job* job,
-                                     const void* d_blocks, size_t stride, const size_t* counts, size_t nslices,
-                                     uint32_t w_begin, uint32_t w_end, uint8_t partial[128]) {
-  return bpp_guard(ctx, [&]() -> int {
-    if (!ctx || !G || !job || !partial || !job->dev || (!d_blocks && nslices) || (!counts && nslices))
-      return BPP_ERR_ARG;
-    const uint32_t c = msm_choose_c((double)verify_terms(*job));
-    if (w_begin > w_end || w_end > (254 + c - 1) / c) return BPP_ERR_ARG;
-    BPP_HIP(hipSetDevice(ctx->device));
-    h25519::ge r = h25519::ge_identity();
-    if (job->count)
-      BPP_TRY(verify_partial_gathered_dev(ctx, G, *job, (const uint8_t*)d_blocks, stride, counts, nslices, w_begin,
-                                          w_end, &r));
-    h25519::ge_to_words((uint32_t*)partial, r);
-    return BPP_OK;
-  });
-}
-
 int bpp_perm_verify_partial(bpp_ctx* ctx, const bpp_gens* G, const bpp_verify_job* job, const uint8_t seed[32],
                             size_t first, uint32_t w_begin, uint32_t w_end, uint8_t partial[128]) {
   return bpp_guard(ctx, [&]() -> int {
@@ -1969,7 +1881,9 @@ void bpp_perm_verify_end(bpp_verify_job* job) { delete job; }
 int bpp_partials_is_identity(const uint8_t* partials, size_t count) {
   return bpp_guard(nullptr, [&]() -> int {
     uint8_t e[32];
-    BPP_TRY(bpp_partials_finish(partials, count, e));
+    const int rc = bpp_partials_finish(partials, count, e);
+    if (rc == BPP_ERR_ARG && partials) return BPP_ERR_VERIFY;  // a partial with Z = 0: never a pass
+    BPP_TRY(rc);
     static const uint8_t zero[32] = {0};
     return memcmp(e, zero, 32) == 0 ? BPP_OK : BPP_ERR_VERIFY;
   });

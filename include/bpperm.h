@@ -56,6 +56,7 @@ enum {
   BPP_ERR_DEVICE = 5,
   BPP_ERR_VERIFY = 6,
   BPP_ERR_NOMEM = 7,
+  BPP_ERR_CALLBACK = 8, /* a caller's transcript hook returned nonzero */
 };
 
 typedef struct bpp_ctx bpp_ctx;
@@ -166,7 +167,9 @@ int bpp_msm_submit_host(bpp_ctx* ctx, const void* h_scalars, const bpp_points* t
  * by DMA) and otherwise staged as pageable. */
 int bpp_host_alloc(bpp_ctx* ctx, size_t bytes, void** hptr);
 int bpp_host_free(bpp_ctx* ctx, void* hptr);
-/* Sum raw extended partial points (count x 128 bytes) and compress. */
+/* Sum raw extended partial points (count x 128 bytes) and compress.
+ * BPP_ERR_ARG for a partial whose Z coordinate is zero (not a point: e.g. an
+ * all-zero buffer a failed rank never wrote). */
 int bpp_partials_finish(const uint8_t* partials, size_t count, uint8_t out[32]);
 /* Host batch encoding of doubled points: out[i] = compress(2 * P_i) for raw
  * extended points P_i (count x 128 bytes), one field inversion per call
@@ -243,6 +246,37 @@ int bpp_ipa_prove(bpp_ctx* ctx, const bpp_gens* g, bpp_transcript* tr, const uin
 int bpp_ipa_verify(bpp_ctx* ctx, const bpp_gens* g, bpp_transcript* tr, size_t n, const uint8_t* G_factors,
                    const uint8_t* H_factors, const uint8_t P[32], const uint8_t Q[32], const uint8_t* L,
                    const uint8_t* R, const uint8_t a[32], const uint8_t b[32]);
+
+/* The same two calls over the CALLER's transcript (north_star: the bp-perm
+ * crate keeps its merlin::Transcript; bulletproofs'
+ * InnerProductProof::create(transcript: &mut Transcript, ..) and verify).
+ * The library never owns the transcript: it calls back, on the calling
+ * thread and in this order, exactly where bulletproofs 4.0.0 touches it
+ * (transcript_protocol.rs:26-67):
+ *   append_message("dom-sep", "ipp v1"), append_message("n", le64(n))
+ *                                  -- innerproduct_domain_sep(n)
+ *   per round j < log2(n):
+ *     append_message("L", L_j), append_message("R", R_j)
+ *                                  -- append_point / validate_and_append_point
+ *     challenge_bytes("u", 64 B)   -- challenge_scalar("u"): the library
+ *                                     reduces the 64 bytes mod l (from_bytes_mod_order_wide)
+ * Labels are exactly those byte strings (no NUL counted in llen).  The
+ * verifier refuses an identity L_j / R_j (BPP_ERR_VERIFY) before appending
+ * it, as validate_and_append_point does.  A hook returning nonzero aborts
+ * the call with BPP_ERR_CALLBACK (the transcript is then in an unspecified
+ * state).  bpp_ipa_prove / bpp_ipa_verify are these with the library's own
+ * Merlin (bpp_transcript) behind the hooks. */
+typedef struct bpp_transcript_hooks {
+  void* user;
+  int (*append_message)(void* user, const uint8_t* label, size_t llen, const uint8_t* msg, size_t mlen);
+  int (*challenge_bytes)(void* user, const uint8_t* label, size_t llen, uint8_t* out, size_t n);
+} bpp_transcript_hooks;
+int bpp_ipa_prove_cb(bpp_ctx* ctx, const bpp_gens* g, const bpp_transcript_hooks* tr, const uint8_t Q[32],
+                     const uint8_t* G_factors, const uint8_t* H_factors, const uint8_t* a, const uint8_t* b, size_t n,
+                     uint8_t* L_out, uint8_t* R_out, uint8_t a_out[32], uint8_t b_out[32]);
+int bpp_ipa_verify_cb(bpp_ctx* ctx, const bpp_gens* g, const bpp_transcript_hooks* tr, size_t n,
+                      const uint8_t* G_factors, const uint8_t* H_factors, const uint8_t P[32], const uint8_t Q[32],
+                      const uint8_t* L, const uint8_t* R, const uint8_t a[32], const uint8_t b[32]);
 
 /* ------------------------------------------- permutation proof (sound) */
 /* Arithmetic-circuit proof that the second half of v = [1..k, pi(1..k), x]
@@ -348,36 +382,6 @@ int bpp_perm_verify_scalars(const bpp_verify_job* job, const uint8_t seed[32], s
  * exchange before the MSM) sum to the identity (bpp_partials_is_identity). */
 int bpp_perm_verify_partial(bpp_ctx* ctx, const bpp_gens* g, const bpp_verify_job* job, const uint8_t seed[32],
                             size_t first, uint32_t w_begin, uint32_t w_end, uint8_t partial[128]);
-/* Window split with the per-proof work sharded by proof (config 5 over N
- * GPUs, VERDICT r3: the plain window split replays and expands every proof
- * on every rank).  Rank r of N:
- *   1. bpp_perm_verify_begin_dev_slice: uploads all `count` proofs and
- *      decompresses every proof point (the MSM's window range needs them
- *      all), but replays only proofs [first, first + n), its slice; r_out =
- *      the slice's r challenges (n x 32 B);
- *   2. (every rank holds the batch's seed, bpp_verify_seed)
- *   3. bpp_perm_verify_slice_scalars writes the slice's MSM scalars to device
- *      memory d_out (bpp_perm_verify_slice_bytes(job) bytes): the 2 n_p + 2
- *      generator scalars summed over the slice, then the slice's n x
- *      (m + 8 + 2 lg) proof-point scalars (32 B each, canonical); it
- *      synchronises ctx, so d_out is complete for a collective on return;
- *   4. the N blocks are all-gathered into one device buffer (block s at
- *      d_blocks + s * stride; RCCL all_gather of equal-size padded blocks);
- *   5. bpp_perm_verify_partial_gathered runs the MSM of ALL proofs over
- *      windows [w_begin, w_end): generator scalars = the sum of the blocks'
- *      heads, proof-point scalars = the blocks' tails in slice order (slices
- *      contiguous, in proof order, counts[s] proofs each, summing to count);
- *   6. the 128-B partials are exchanged as for bpp_perm_verify_partial.
- * A sliced job is refused by bpp_perm_verify_partial (BPP_ERR_ARG); replay
- * rejects (BPP_ERR_VERIFY from step 1) must veto the batch on every rank. */
-int bpp_perm_verify_begin_dev_slice(bpp_ctx* ctx, uint32_t k, size_t count, const uint8_t* label, size_t llen,
-                                    const uint8_t* proofs, const uint8_t* V, size_t first, size_t n, uint8_t* r_out,
-                                    bpp_verify_job** out);
-size_t bpp_perm_verify_slice_bytes(const bpp_verify_job* job);
-int bpp_perm_verify_slice_scalars(bpp_ctx* ctx, const bpp_verify_job* job, const uint8_t seed[32], void* d_out);
-int bpp_perm_verify_partial_gathered(bpp_ctx* ctx, const bpp_gens* g, const bpp_verify_job* job,
-                                     const void* d_blocks, size_t stride, const size_t* counts, size_t nslices,
-                                     uint32_t w_begin, uint32_t w_end, uint8_t partial[128]);
 /* Window split with the upload and decompression sharded too (config 5
  * over N GPUs, "windows_sharded").  Rank r of N, slice
  * [first, first + n) of the batch:
@@ -390,8 +394,11 @@ int bpp_perm_verify_partial_gathered(bpp_ctx* ctx, const bpp_gens* g, const bpp_
  *      decompression, not for an asynchronous begin's replay), so the point
  *      blocks' all-gather can run beside the replay and step 3;
  *   3. bpp_perm_verify_slice_scalars_at(job, seed, first) writes the slice's
- *      scalar block as bpp_perm_verify_slice_scalars, the proofs weighted as
- *      batch proofs first + p;
+ *      scalar block to device memory d_out (bpp_perm_verify_slice_bytes(job)
+ *      bytes): the 2 n_p + 2 generator scalars summed over the slice, then
+ *      the slice's n x (m + 8 + 2 lg) proof-point scalars (32 B each,
+ *      canonical), the proofs weighted as batch proofs first + p; it
+ *      synchronises ctx, so d_out is complete for a collective on return;
  *   4. the point blocks (pstride bytes apart) and the scalar blocks (stride
  *      apart) of all slices are all-gathered into device memory (RCCL
  *      all_gather over xGMI), slices contiguous and in proof order;
@@ -402,13 +409,16 @@ int bpp_perm_verify_partial_gathered(bpp_ctx* ctx, const bpp_gens* g, const bpp_
  *      a replay reject or an undecodable point on any rank vetoes the batch. */
 /* bpp_perm_verify_begin_dev without waiting for the replay (no r_out): the
  * replay's verdicts are checked by the job's next synchronising call
- * (bpp_perm_verify_slice_scalars(_at) and bpp_perm_verify_partial return
+ * (bpp_perm_verify_slice_scalars_at and bpp_perm_verify_partial return
  * BPP_ERR_VERIFY for a rejected proof); bpp_perm_verify_slice_points can run
- * meanwhile (it waits for the decompression only).  Pinned input buffers
- * (bpp_host_alloc) are read by DMA after the return: keep them until that
- * next synchronising call; pageable ones are staged before it returns. */
+ * meanwhile (it waits for the decompression only).  Pinned input buffers --
+ * bpp_host_alloc's and any memory the caller page-locked itself
+ * (hipHostRegister / hipHostMalloc), which the library also sends by DMA --
+ * are read after the return: keep them alive and unchanged until that next
+ * synchronising call; pageable ones are staged before it returns. */
 int bpp_perm_verify_begin_dev_async(bpp_ctx* ctx, uint32_t k, size_t count, const uint8_t* label, size_t llen,
                                     const uint8_t* proofs, const uint8_t* V, bpp_verify_job** out);
+size_t bpp_perm_verify_slice_bytes(const bpp_verify_job* job);
 int bpp_perm_verify_slice_scalars_at(bpp_ctx* ctx, const bpp_verify_job* job, const uint8_t seed[32], size_t first,
                                      void* d_out);
 size_t bpp_perm_verify_slice_point_bytes(const bpp_verify_job* job);
@@ -418,7 +428,9 @@ int bpp_perm_verify_partial_sharded(bpp_ctx* ctx, const bpp_gens* g, const bpp_v
                                     const size_t* counts, size_t nslices, uint32_t w_begin, uint32_t w_end,
                                     uint8_t partial[128]);
 void bpp_perm_verify_end(bpp_verify_job* job);
-/* BPP_OK if the partials add up to the identity, else BPP_ERR_VERIFY. */
+/* BPP_OK if the partials add up to the identity, else BPP_ERR_VERIFY (also
+ * for any partial with Z = 0, so an unwritten all-zero partial never passes;
+ * callers still exchange a per-rank ok flag). */
 int bpp_partials_is_identity(const uint8_t* partials, size_t count);
 
 #ifdef __cplusplus

@@ -13,6 +13,10 @@
  *   Merlin y; bpp_ipa_prove == config2 L, R, a, b;
  *   bpp_gens_export + bpp_msm for P; bpp_ipa_verify accepts, rejects a
  *   tampered a;
+ *   the same IPA through bpp_ipa_prove_cb / bpp_ipa_verify_cb with a
+ *   caller-owned C Merlin (merlin_min.h) behind the hooks: L, R, a, b equal
+ *   config2, the hooks are called 2 + 2 lg / lg times, a tampered a is
+ *   refused, a failing hook gives BPP_ERR_CALLBACK;
  *   bpp_perm_prove_batch_entropy (caller seeds) == oracle proofs and V;
  *   bpp_debug_secret_residue == 0; bpp_perm_verify_batch accepts, rejects a
  *   tampered proof; OS-entropy proofs verify; bpp_perm_verify (one proof).
@@ -22,6 +26,7 @@
 #include <string.h>
 
 #include "bpperm.h"
+#include "merlin_min.h"
 
 #define CHECK(c)                                              \
   do {                                                        \
@@ -63,6 +68,28 @@ static uint8_t* get(const char* name, size_t* len) {
   }
   *len = 0;
   return NULL;
+}
+
+/* bpp_transcript_hooks over the caller's transcript; fail_at > 0 makes the
+ * fail_at-th call (1-based) fail */
+struct hook_log {
+  mm_transcript* t;
+  int appends, challenges;
+  int fail_at;
+};
+static int hook_append(void* user, const uint8_t* label, size_t llen, const uint8_t* msg, size_t mlen) {
+  struct hook_log* h = (struct hook_log*)user;
+  if (h->fail_at && h->appends + h->challenges + 1 == h->fail_at) return -1;
+  ++h->appends;
+  mm_append_message(h->t, label, llen, msg, mlen);
+  return 0;
+}
+static int hook_challenge(void* user, const uint8_t* label, size_t llen, uint8_t* out, size_t n) {
+  struct hook_log* h = (struct hook_log*)user;
+  if (h->fail_at && h->appends + h->challenges + 1 == h->fail_at) return -1;
+  ++h->challenges;
+  mm_challenge_bytes(h->t, label, llen, out, n);
+  return 0;
 }
 
 int main(int argc, char** argv) {
@@ -161,6 +188,45 @@ int main(int argc, char** argv) {
     const int rc = bpp_ipa_verify(ctx, g, tv, n, NULL, hf, P, Q, Lo, Ro, av, b);
     CHECK(rc == (tamper ? BPP_ERR_VERIFY : BPP_OK));
     bpp_transcript_destroy(tv);
+  }
+
+  /* ---- the same IPA over the CALLER's transcript (bpp_ipa_prove_cb): an
+   * independent C Merlin (merlin_min.h) behind the hooks, as the Rust crate's
+   * merlin::Transcript would be; A and y go through it before the IPA */
+  {
+    mm_transcript ct;
+    struct hook_log lg0 = {&ct, 0, 0, 0};
+    bpp_transcript_hooks hk = {&lg0, hook_append, hook_challenge};
+    mm_new(&ct, (const uint8_t*)"config2", 7);
+    mm_append_message(&ct, (const uint8_t*)"A", 1, A, 32);
+    uint8_t ywide[64];
+    mm_challenge_bytes(&ct, (const uint8_t*)"y", 1, ywide, 64); /* (y itself comes with the inputs) */
+    uint8_t Lc[32 * 16], Rc[32 * 16], ac[32], bc[32];
+    CHECK(lg <= 16);
+    CHECK(bpp_ipa_prove_cb(ctx, g, &hk, Q, NULL, hf, aL, aR, n, Lc, Rc, ac, bc) == BPP_OK);
+    CHECK(memcmp(Lc, wL, 32 * lg) == 0 && memcmp(Rc, wR, 32 * lg) == 0);
+    CHECK(memcmp(ac, wa, 32) == 0 && memcmp(bc, wb, 32) == 0);
+    /* dom-sep, n, then L, R, u per round */
+    CHECK(lg0.appends == 2 + 2 * lg && lg0.challenges == lg);
+    for (int tamper = 0; tamper < 2; ++tamper) {
+      mm_transcript cv;
+      struct hook_log lv = {&cv, 0, 0, 0};
+      bpp_transcript_hooks hv = {&lv, hook_append, hook_challenge};
+      mm_new(&cv, (const uint8_t*)"config2", 7);
+      mm_append_message(&cv, (const uint8_t*)"A", 1, A, 32);
+      mm_challenge_bytes(&cv, (const uint8_t*)"y", 1, ywide, 64);
+      uint8_t av[32];
+      memcpy(av, ac, 32);
+      av[0] ^= (uint8_t)tamper;
+      CHECK(bpp_ipa_verify_cb(ctx, g, &hv, n, NULL, hf, P, Q, Lc, Rc, av, bc) == (tamper ? BPP_ERR_VERIFY : BPP_OK));
+    }
+    /* a hook that fails aborts the call */
+    mm_transcript cf;
+    struct hook_log lf = {&cf, 0, 0, 3};
+    bpp_transcript_hooks hf2 = {&lf, hook_append, hook_challenge};
+    mm_new(&cf, (const uint8_t*)"config2", 7);
+    CHECK(bpp_ipa_prove_cb(ctx, g, &hf2, Q, NULL, hf, aL, aR, n, Lc, Rc, ac, bc) == BPP_ERR_CALLBACK);
+    CHECK(bpp_ipa_prove_cb(ctx, g, NULL, Q, NULL, hf, aL, aR, n, Lc, Rc, ac, bc) == BPP_ERR_ARG);
   }
   bpp_gens_destroy(g);
 

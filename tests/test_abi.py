@@ -110,3 +110,33 @@ def test_scalar_helpers_match_python():
         bpperm.scalar_invert(bytes(32))
     with pytest.raises(BppError):
         bpperm.scalar_powers(L.to_bytes(32, "little"), 3)
+
+
+def test_partials_refuse_unwritten_partial():
+    """a 128-B partial whose Z is zero (an all-zero buffer a failed
+    rank never wrote) absorbed the sum and encoded as the identity, so one
+    such partial made bpp_partials_is_identity accept any batch.  It is now
+    refused: bpp_partials_finish -> BPP_ERR_ARG, bpp_partials_is_identity ->
+    BPP_ERR_VERIFY.  Host-only entry points (no GPU)."""
+    from bpperm import _lib
+    from oracle import ristretto as r255
+    lib = ctypes.CDLL(str(_lib.LIB_PATH))
+    P = r255.ed_mul(12345, r255.BASEPOINT)
+    Pn = r255.ed_neg(P)
+    raw = r255.raw_point_bytes
+    zero = bytes(128)
+    out = ctypes.create_string_buffer(32)
+
+    def is_id(*parts):
+        b = b"".join(parts)
+        return lib.bpp_partials_is_identity(ctypes.c_char_p(b), ctypes.c_size_t(len(parts)))
+
+    assert is_id(raw(r255.IDENTITY)) == 0
+    assert is_id(raw(P), raw(Pn)) == 0
+    assert is_id(raw(P)) == 6
+    assert is_id(zero) == 6
+    assert is_id(raw(P), raw(Pn), zero) == 6
+    assert is_id(zero, raw(P), raw(Pn)) == 6
+    assert lib.bpp_partials_finish(ctypes.c_char_p(zero), ctypes.c_size_t(1), out) == 1
+    assert lib.bpp_partials_finish(ctypes.c_char_p(raw(P)), ctypes.c_size_t(1), out) == 0
+    assert out.raw == r255.encode(P)

@@ -22,3 +22,16 @@ def test_c_caller_through_header(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.strip() == "ok"
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="gcc not installed")
+def test_c_caller_transcript_kat(tmp_path):
+    """tests/c/merlin_min.h -- the caller-owned transcript abi_gpu.c puts
+    behind bpp_transcript_hooks -- reproduces merlin's "simple transcript"
+    known answer, so the GPU test's transcript is an independent Merlin."""
+    exe = tmp_path / "merlin_kat"
+    r = subprocess.run(["gcc", "-std=c11", "-O1", "-Wall", "-Werror", str(ROOT / "tests" / "c" / "merlin_kat.c"),
+                        "-o", str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=30)
+    assert r.stdout.strip() == "d5a21972d0d5fe320c0d263fac7fffb8145aa640af6e9bca177c03c7efcf0615"

@@ -5,7 +5,10 @@ over gloo (BPP_DIST_BACKEND=gloo stands in for RCCL, which needs one GPU per
 rank).  Asserts the 2-rank MSM (2^20 pairs per rank, bucket windows split)
 equals the C-port golden for world 2 (tests/golden/bench_msm.json), the
 proofs of both ranks verify, and both config-5 splits (windows, proofs)
-accept the batch and reject a tampered one."""
+accept the batch and reject a tampered one; config 5's single 2^22-term MSM
+with its windows split over the two ranks equals the world-4 golden; and
+config 4 as one job (proofs sharded over the ranks, one batch verification
+by the proof split) verifies and refuses a tampered proof."""
 import json
 import os
 import socket
@@ -33,7 +36,7 @@ def test_bench_two_ranks_gloo(tmp_path):
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
            "--gpus", "2", "--steps", "4", "--warmup", "1", "--log2n", "20", "--no-cpu",
            "--proofs-per-gpu", "64", "--proof-streams", "2", "--proof-steps", "2",
-           "--verify-proofs", "512", "--verify-steps", "1"]
+           "--verify-proofs", "512", "--verify-steps", "1", "--job-proofs", "256", "--job-reps", "1"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
@@ -46,3 +49,11 @@ def test_bench_two_ranks_gloo(tmp_path):
     assert set(v["splits"]) == {"windows", "windows_sharded", "proofs"}
     assert all(s["all_verified"] for s in v["splits"].values())
     assert v["rejects_tampered"] is True
+    # config 5's one 2^22-term MSM, windows split over the two ranks (strong)
+    m = d["msm_2e22"]
+    assert m["n_gpus"] == 2 and m["pairs"] == 1 << 22 and m["scaling"] == "strong"
+    assert m["result_ok"] is True
+    # config 4 as one job: 256 proofs over the two ranks, one batch verification
+    j = d["proofs"]["job"]
+    assert j["proofs"] == 256 and j["proofs_per_rank"] == 128 and j["n_gpus"] == 2
+    assert j["all_verified"] is True and j["rejects_tampered"] is True

@@ -175,9 +175,13 @@ def test_entropy_batch_leaves_no_secret_bytes(ctx, gens, monkeypatch, k, streams
             g.close()
 
 
-def test_entropy_wipe_after_staging_arena_growth(gens):
+@pytest.mark.parametrize("where", ["fresh", "shared"])
+def test_entropy_wipe_after_staging_arena_growth(gens, where):
     """VERDICT r4 item 5 (the round-4 segfault, fixed in ctx.hip stage_take),
-    on a fresh context so that its pinned staging arena starts at 16 MB: a
+    on a fresh context, so that its pinned staging arena starts at 16 MB, and
+    on the session's long-lived context, whose arena earlier tests grew and
+    reuse (the staged scalars of a later MSM land on the
+    last wipe's spans; stage_take now drops reused bytes from them).  A
     test-hook batch records secret spans in the arena and leaves them; one
     staging request larger than the arena (19.2 MB of host scalars for
     bpp_msm_table) frees and replaces it; the next production batch's
@@ -193,7 +197,7 @@ def test_entropy_wipe_after_staging_arena_growth(gens):
         sc[31::32] = bytes(n)  # < 2^248: canonical
         return bytes(sc)
 
-    ctx2 = bpperm.Context(gens.ctx.device)
+    ctx2 = bpperm.Context(gens.ctx.device) if where == "fresh" else gens.ctx
     n, big = 600_000, 800_000
     tbl = ctx2.from_uniform(hashlib.shake_256(b"arena-growth").digest(64 * big))  # (direct copy, no staging)
     try:
@@ -207,7 +211,10 @@ def test_entropy_wipe_after_staging_arena_growth(gens):
         assert ctx2.secret_residue() == 0
         e2, ve2 = pr.prove_batch_entropy(5)
         assert ctx2.secret_residue() == 0
+        ctx2.msm_table(host_scalars(1000), tbl, 1000)  # arena reused, no growth: random bytes over the spans
+        assert ctx2.secret_residue() == 0
         assert pr.verify_batch(proofs + e + e2, Vs + ve + ve2)
     finally:
         tbl.close()
-        ctx2.close()
+        if ctx2 is not gens.ctx:
+            ctx2.close()

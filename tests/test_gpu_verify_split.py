@@ -153,105 +153,6 @@ def test_device_scalars_match_host_expansion(setup, ctx):
     job.close()
 
 
-def _sliced_partials(g, proofs, Vs, ranks, tamper_rank=None):
-    """The sharded window split (bpperm.dist.verify_sliced) rehearsed on one
-    GPU: one context per rank (its sliced job stays valid), r and the scalar
-    blocks gathered by concatenation in rank order (device memory from the
-    library: torch's own HIP runtime is not initialised in this process)."""
-    import bpperm
-    from bpperm import dist as bdist
-    ctxs = [bpperm.Context(0) for _ in range(ranks)]
-    prs = [bpperm.PermProver(g, K, ctx=c) for c in ctxs]
-    ranges = bdist.point_ranges(len(proofs), ranks)
-    counts = [e - b for b, e in ranges]
-    jobs = [bpperm.VerifyJob(K, proofs, Vs, prs[r].label, ctx=ctxs[r], replay=(b, e - b))
-            for r, (b, e) in enumerate(ranges)]
-    try:
-        if not all(j.ok for j in jobs):
-            return None
-        stride = (bdist._slice_block_bytes(K, max(counts)) + 15) // 16 * 16
-        blocks = ctxs[0].dev_alloc(ranks * stride)
-        ctxs[0].htod(blocks, bytes(ranks * stride))
-        for r, j in enumerate(jobs):
-            assert j.slice_bytes() == bdist._slice_block_bytes(K, counts[r])
-            j.slice_scalars(SEED, blocks + r * stride)
-        if tamper_rank is not None:  # one rank's generator block perturbed after the fact
-            at = blocks + tamper_rank * stride
-            b0 = bytearray(ctxs[0].dtoh(at, 16))
-            b0[0] ^= 1
-            ctxs[0].htod(at, bytes(b0))
-        W = jobs[0].windows()[1]
-        return [prs[r].verify_partial_gathered(jobs[r], blocks, stride, counts, wb, we)
-                for r, (wb, we) in enumerate(bdist.window_ranges(W, ranks))]
-    finally:
-        for j in jobs:
-            j.close()
-        for c in ctxs:
-            c.close()
-
-
-@pytest.mark.parametrize("ranks,n", [(4, 64), (3, 100), (8, 64)])
-def test_sharded_window_split(setup, ranks, n):
-    """the window split with replay and scalar expansion sharded
-    by proof.  The ranks' window partials add up to the identity exactly when
-    the batch verifies, and to the same element as the plain window split's;
-    a tampered proof or a perturbed scalar block is rejected; a sliced job is
-    refused by bpp_perm_verify_partial; blocks gathered out of slice order are
-    refused."""
-    import bpperm
-    g, pr, proofs, Vs = setup
-    if n > len(proofs):
-        more, mv = pr.prove_batch(list(range(700, 700 + n - len(proofs))))
-        proofs, Vs = proofs + more, Vs + mv
-    proofs, Vs = proofs[:n], Vs[:n]
-    parts = _sliced_partials(g, proofs, Vs, ranks)
-    assert bpperm.partials_is_identity(parts)
-    assert not bpperm.partials_is_identity(parts[:-1])
-    bad = list(proofs)
-    b = bytearray(bad[n // 2])
-    b[40] ^= 1  # A_O's encoding: the replay rejects it or its point decodes to another
-    bad[n // 2] = bytes(b)
-    tp = _sliced_partials(g, bad, Vs, ranks)
-    assert tp is None or None in tp or not bpperm.partials_is_identity(tp)
-    badV = list(Vs)
-    v = bytearray(badV[1])
-    v[33] ^= 2
-    badV[1] = bytes(v)
-    tv = _sliced_partials(g, proofs, badV, ranks)
-    assert tv is None or None in tv or not bpperm.partials_is_identity(tv)
-    assert not bpperm.partials_is_identity(_sliced_partials(g, proofs, Vs, ranks, tamper_rank=ranks - 1))
-    job = bpperm.VerifyJob(K, proofs, Vs, pr.label, ctx=pr.ctx, replay=(0, n // 2))
-    with pytest.raises(bpperm.BppError):
-        pr.verify_partial(job, SEED, 0, 0, 1)
-    job.close()
-
-
-def test_gathered_blocks_out_of_order_refused(setup):
-    """bpp_perm_verify_partial_gathered checks that the job's own
-    slice sits at its proof offset among the gathered blocks: counts listed
-    in another order are an argument error, not a silent rejection."""
-    import bpperm
-    from bpperm import dist as bdist
-    g, pr, proofs, Vs = setup
-    ranges = bdist.point_ranges(len(proofs), 3)
-    counts = [e - b for b, e in ranges]
-    assert counts == [21, 21, 22]
-    b, e = ranges[0]
-    job = bpperm.VerifyJob(K, proofs, Vs, pr.label, ctx=pr.ctx, replay=(b, e - b))
-    stride = (bdist._slice_block_bytes(K, max(counts)) + 15) // 16 * 16
-    blocks = pr.ctx.dev_alloc(3 * stride)
-    try:
-        pr.ctx.htod(blocks, bytes(3 * stride))
-        job.slice_scalars(SEED, blocks)
-        W = job.windows()[1]
-        # the job's slice is proofs [0, 21); counts [22, 21, 21] put 22 there
-        with pytest.raises(bpperm.BppError):
-            pr.verify_partial_gathered(job, blocks, stride, counts[::-1], 0, W)
-    finally:
-        pr.ctx.dev_free(blocks)
-        job.close()
-
-
 def _sharded_partials(g, proofs, Vs, ranks, tamper_rank=None, equal_stride=False):
     """The upload-sharded window split (bpperm.dist.verify_sliced, VERDICT r4
     item 2) rehearsed on one GPU: one context per rank, each job over its
@@ -337,8 +238,7 @@ def test_upload_sharded_window_split(setup, ranks, n):
 
 def test_sharded_blocks_out_of_order_refused(setup):
     """bpp_perm_verify_partial_sharded checks that the job's slice sits at
-    its proof offset among the gathered blocks, and refuses a sliced-replay
-    job (those take bpp_perm_verify_partial_gathered)."""
+    its proof offset among the gathered blocks."""
     import bpperm
     from bpperm import dist as bdist
     g, pr, proofs, Vs = setup
@@ -351,7 +251,6 @@ def test_sharded_blocks_out_of_order_refused(setup):
     pstride = max(counts) * bdist._points_per_proof(K) * 128
     blocks = pr.ctx.dev_alloc(3 * stride)
     pblocks = pr.ctx.dev_alloc(3 * pstride)
-    sliced = None
     try:
         pr.ctx.htod(blocks, bytes(3 * stride))
         pr.ctx.htod(pblocks, bytes(3 * pstride))
@@ -362,12 +261,7 @@ def test_sharded_blocks_out_of_order_refused(setup):
             pr.verify_partial_sharded(job, 0, blocks, stride, pblocks, pstride, counts[::-1], 0, W)
         with pytest.raises(bpperm.BppError):  # the slice claimed at offset 5 (no slice starts there)
             pr.verify_partial_sharded(job, 5, blocks, stride, pblocks, pstride, counts, 0, W)
-        sliced = bpperm.VerifyJob(K, proofs, Vs, pr.label, ctx=pr.ctx, replay=(0, 21))
-        with pytest.raises(bpperm.BppError):
-            pr.verify_partial_sharded(sliced, 0, blocks, stride, pblocks, pstride, counts, 0, W)
     finally:
         pr.ctx.dev_free(blocks)
         pr.ctx.dev_free(pblocks)
-        if sliced is not None:
-            sliced.close()
         job.close()

@@ -913,11 +913,15 @@ static int msm_multi_dt_dev(bpp_ctx* ctx, const uint32_t* d_scal, const uint32_t
   const double t_avg = (double)T / (double)M;
   const uint32_t TG = dt_term_groups(dg.W, t_avg, M);
   const uint32_t nt = TG * dg.W;
-  // two MSMs per block (k_dt_msm segs = 2) for launches with blocks to spare
-  // (the prover's A_I / A_O / S); BPP_DT_PAIR=0 keeps one (A/B switch)
+  // two MSMs per block (k_dt_msm segs = 2, BPP_DT_PAIR=1) for launches with
+  // blocks to spare, an A/B switch, off: round 6 re-ran the A/B at the bench's
+  // prover shape (384 x 32 in flight, 8 queues): proofs/s equal (363-365 K
+  // vs 364-366 K), but one MSM per block issues more (k_dt_msm VALU issue
+  // 0.359 vs 0.314, wait_any 0.368 vs 0.456) and misses the UTCL1 less (5.2 %
+  // vs 8.3 % of requests); profiles/r06_dt_pair_ab.txt, r06_tlb_prover.json
   static const bool pair_env = [] {
     const char* e = getenv("BPP_DT_PAIR");
-    return !e || atoi(e) != 0;
+    return e && atoi(e) != 0;
   }();
   const uint32_t segs = pair_env && M >= 512 && 2 * nt <= DT_NT_MAX ? 2u : 1u;
   ctx_work(ctx, "msm_terms", T);

@@ -255,6 +255,9 @@ FE_INLINE ge_niels fetch_entry(const uint32_t* __restrict__ tbl, const uint32_t*
 #ifndef ACC_PARK_SPLIT
 #define ACC_PARK_SPLIT 1
 #endif
+#ifndef ACC_PARK_PRE
+#define ACC_PARK_PRE 1
+#endif
 
 // Balanced bucket accumulation: lane l owns entries [l*K, (l+1)*K) of the
 // bucket-sorted entry array, so every lane does exactly K mixed additions
@@ -294,7 +297,20 @@ __global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_
   __shared__ __attribute__((aligned(16))) uint32_t piece[ACC_T * P3_WORDS];
   // a later piece of a bucket that started in an earlier chunk: to LDS when
   // its owner is in this workgroup and will fold it, else to head[l]
-#if ACC_PARK_SPLIT
+#if ACC_PARK_SPLIT && ACC_PARK_PRE
+  // Only a lane's FIRST run can park (its bucket started in an earlier
+  // chunk), so where it parks is decided once before the loop (park_lds0)
+  // instead of by two divisions by the runtime K inside the divergent close
+  // path, which the whole wave executed whenever any lane closed its first
+  // run.  Two destinations as two stores (ds_write / global_store), as below.
+  bool park_lds0 = false;
+  auto park = [&](const ge_p3& v, uint32_t, uint32_t) {
+    if (park_lds0)
+      store_p3(piece, threadIdx.x, v);
+    else
+      store_p3(head, l, v);
+  };
+#elif ACC_PARK_SPLIT
   // the two destinations as two stores (ds_write / global_store) instead of
   // one through a selected generic pointer, which compiled to 10
   // flat_store_dwordx4 on every close: accumulate 0.715-0.735 vs 0.743-0.749
@@ -328,6 +344,12 @@ __global__ void __launch_bounds__(ACC_T) ACC_ATTR k_msm_accumulate(const uint32_
     b = bucket_of(boff, nbuckets, i0);
     bstart = boff[b];
     bend = boff[b + 1];
+#if ACC_PARK_SPLIT && ACC_PARK_PRE && !ACC_PIECE_GLOBAL
+    if (bstart < i0) {
+      const uint32_t l0 = bstart / K;
+      park_lds0 = (((bend - 1) / K) - l0) < FIX_MAX && l0 >= lane_first;
+    }
+#endif
     // the lane where a bucket starts lists it if it is heavy
 #ifndef ACC_HEAVY_DIV
     if (bstart == i0 && bend - 1 >= heavy_lim) heavy[1 + atomicAdd(&heavy[0], 1u)] = b;

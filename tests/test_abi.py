@@ -140,3 +140,13 @@ def test_partials_refuse_unwritten_partial():
     assert lib.bpp_partials_finish(ctypes.c_char_p(zero), ctypes.c_size_t(1), out) == 1
     assert lib.bpp_partials_finish(ctypes.c_char_p(raw(P)), ctypes.c_size_t(1), out) == 0
     assert out.raw == r255.encode(P)
+
+
+def test_integration_lists_every_export():
+    """INTEGRATION.md §5 lists every export the header
+    declares (and no retired one)."""
+    sec = (ROOT / "INTEGRATION.md").read_text().split("## 5.")[1]
+    syms = declared_symbols()
+    assert [s for s in syms if f"`{s}`" not in sec] == []
+    for gone in ("bpp_perm_verify_begin_dev_slice", "bpp_perm_verify_partial_gathered"):
+        assert gone not in syms

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--k", type=int, default=52)
     ap.add_argument("--worlds", default="1,2,4,8")
+    ap.add_argument("--no-proof-split", action="store_true",
+                    help="skip the proof split's rank 0 (a trace then ends with the sharded partial)")
     a = ap.parse_args()
     import bpperm
     from bpperm import dist as bdist
@@ -76,7 +78,7 @@ def main():
                     t[k].append(v * 1e3)
         # the proof split's rank 0: its slice job and the MSM of its slice over all windows
         t["proofs_split"] = []
-        for rep in range(a.reps + 1):
+        for rep in range(0 if a.no_proof_split else a.reps + 1):
             t0 = time.perf_counter()
             j = bpperm.VerifyJob(a.k, proofs[b:e], Vs[b:e], pr.label, ctx=ctx, wait=False)
             _, Wj = j.windows()
@@ -86,7 +88,7 @@ def main():
             assert part_p is not None
             if rep:
                 t["proofs_split"].append((t1 - t0) * 1e3)
-        med = {k: round(sorted(v)[len(v) // 2], 4) for k, v in t.items()}
+        med = {k: round(sorted(v)[len(v) // 2], 4) for k, v in t.items() if v}
         out["worlds"][world] = {"slice_proofs": counts[0], "window_range": [wb, we], "ms": med,
                                 "gather_bytes_per_rank": {"points": pstride * (world - 1), "scalars": stride * (world - 1)},
                                 "partial_nonzero": part != bytes(128)}

@@ -1,4 +1,6 @@
 set -o pipefail
-cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; O=gpurun_out/r05m; mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.txt 2>&1 || { tail -30 $O/gpu_tests.txt; exit 1; }
-tail -1 $O/gpu_tests.txt
+cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; O=gpurun_out/r06e; mkdir -p $O
+bash tools/gpu_r06.sh r06e tests bench || exit 1
+timeout -k 10 120 python3 tools/prove_phases.py 32 8 > $O/phases32.txt 2>&1 || { tail $O/phases32.txt; exit 1; }
+timeout -k 10 120 python3 tools/prove_phases.py 128 8 > $O/phases128.txt 2>&1 || { tail $O/phases128.txt; exit 1; }
+cat $O/phases32.txt $O/phases128.txt

@@ -248,11 +248,13 @@ class Context:
         return [raw[32 * i: 32 * i + 32] for i in range(count)]
 
 
-def host_tuning(malloc: bool = True):
+def host_tuning(malloc: bool = True, hw_queues: bool = False):
     """Opt-in process-wide host tuning (bpp_host_tuning): BPP_TUNE_MALLOC
     fixes glibc's mmap threshold and disables heap trimming (the prover's
-    per-batch host vectors stay in the arenas)."""
-    check(_lib.load().bpp_host_tuning(1 if malloc else 0), "bpp_host_tuning")
+    per-batch host vectors stay in the arenas); BPP_TUNE_HW_QUEUES asks HIP
+    for 8 hardware queues (GPU_MAX_HW_QUEUES=8 unless set; effective only
+    before anything in the process initialises HIP)."""
+    check(_lib.load().bpp_host_tuning((1 if malloc else 0) | (2 if hw_queues else 0)), "bpp_host_tuning")
 
 
 def host_pool_threads() -> int:

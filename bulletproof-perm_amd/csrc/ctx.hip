@@ -414,14 +414,22 @@ extern "C" {
 // the pad, tools/hostprof + prove_inflight_exp.py).  This changes the allocator policy
 // of the whole host process, so it is opt-in (bench.py asks for it); loading
 // the library changes nothing.
+// BPP_TUNE_HW_QUEUES: HIP's hardware queues per process come from
+// GPU_MAX_HW_QUEUES, read once when the HIP runtime starts; a prover with
+// many batches in flight (one context and stream each) measured +2.5 % on 8
+// queues over HIP's default 4 (368 vs 359 K proofs/s, profiles/
+// r05_hw_queues_ab.txt).  The flag sets GPU_MAX_HW_QUEUES=8 unless the
+// caller set it, so it only takes effect before anything in the process
+// initialises HIP.
 int bpp_host_tuning(uint32_t flags) {
   return bpp_guard(nullptr, [&]() -> int {
-    if (flags & ~(uint32_t)BPP_TUNE_MALLOC) return BPP_ERR_ARG;
+    if (flags & ~(uint32_t)(BPP_TUNE_MALLOC | BPP_TUNE_HW_QUEUES)) return BPP_ERR_ARG;
     if (flags & BPP_TUNE_MALLOC) {
       mallopt(M_MMAP_THRESHOLD, 64 << 20);
       mallopt(M_TRIM_THRESHOLD, 1 << 30);
       mallopt(M_TOP_PAD, 64 << 20);
     }
+    if (flags & BPP_TUNE_HW_QUEUES) setenv("GPU_MAX_HW_QUEUES", "8", 0);
     return BPP_OK;
   });
 }

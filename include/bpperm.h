@@ -90,8 +90,14 @@ void bpp_ctx_work_reset(bpp_ctx* ctx);
  * trimming and pads arena growth by 64 MB, which keeps the prover's
  * per-batch host vectors in the arenas
  * (measured in a host profile of 8 batches in flight).
+ * BPP_TUNE_HW_QUEUES asks HIP for 8 hardware queues per process
+ * (GPU_MAX_HW_QUEUES=8 unless the caller set it): a prover keeping many
+ * batches in flight, one context and stream each, needs more than HIP's
+ * default 4.  HIP reads the variable once, when it starts, so this flag must
+ * come before the first bpp_ctx_create and any other HIP use in the process.
  * BPP_ERR_ARG for unknown flags. */
 #define BPP_TUNE_MALLOC 1u
+#define BPP_TUNE_HW_QUEUES 2u
 int bpp_host_tuning(uint32_t flags);
 /* Threads of the library's host pool (transcripts, scalar bookkeeping),
  * calling threads included: BPP_HOST_THREADS, else a quarter of this

@@ -150,3 +150,26 @@ def test_integration_lists_every_export():
     assert [s for s in syms if f"`{s}`" not in sec] == []
     for gone in ("bpp_perm_verify_begin_dev_slice", "bpp_perm_verify_partial_gathered"):
         assert gone not in syms
+
+
+def test_host_tuning_hw_queues_flag():
+    """bpp_host_tuning(BPP_TUNE_HW_QUEUES) sets GPU_MAX_HW_QUEUES=8 for the
+    process unless the caller set it (a production prover's queue count,
+    VERDICT r5 weak 8); unknown flags are refused.  In a child process: the
+    variable is process-wide."""
+    import subprocess
+    import sys
+    code = ("import ctypes, os, sys; sys.path.insert(0, %r); from bpperm import _lib; "
+            "lib = ctypes.CDLL(str(_lib.LIB_PATH)); "
+            "assert lib.bpp_host_tuning(ctypes.c_uint32(4)) == 1; "
+            "assert lib.bpp_host_tuning(ctypes.c_uint32(2)) == 0; "
+            "libc = ctypes.CDLL(None); libc.getenv.restype = ctypes.c_char_p; "
+            "print(libc.getenv(b'GPU_MAX_HW_QUEUES').decode())") % str(ROOT / "bulletproof-perm_amd")
+    import os
+    env = {k: v for k, v in os.environ.items() if k != "GPU_MAX_HW_QUEUES"}
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip() == "8"
+    env["GPU_MAX_HW_QUEUES"] = "4"
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=60)
+    assert r.stdout.strip() == "4"  # the caller's own setting wins

@@ -31,6 +31,9 @@ struct bpp_ctx {
   uint8_t* stage = nullptr;
   size_t stage_cap = 0, stage_used = 0;
   hipEvent_t sync_ev = nullptr;  // ctx_sync's completion event
+  // > 0: ctx_sync spins this many us before it sleeps (SyncSpin, for the
+  // latency-bound callers: one IPA, small prover batches); 0 = sleep at once
+  unsigned sync_spin_us = 0;
   // profiling
   bool prof = false;
   struct Pend {
@@ -206,6 +209,17 @@ int ctx_sync(bpp_ctx* ctx);
 // spin_us first (a 5 us nanosleep sleeps ~55 us under the default timer
 // slack, and these calls wait on the GPU twice or three times per result).
 int ctx_sync_latency(bpp_ctx* ctx, unsigned spin_us = 400);
+// Scoped latency mode: ctx_sync on ctx spins `us` before sleeping while the
+// guard lives (a 5-us nanosleep oversleeps by the 50-us default timer slack,
+// which a chain of short kernels and host steps pays at every sync).
+struct SyncSpin {
+  bpp_ctx* c;
+  unsigned old;
+  SyncSpin(bpp_ctx* ctx, unsigned us) : c(ctx), old(ctx->sync_spin_us) { ctx->sync_spin_us = us; }
+  ~SyncSpin() { c->sync_spin_us = old; }
+  SyncSpin(const SyncSpin&) = delete;
+  SyncSpin& operator=(const SyncSpin&) = delete;
+};
 // i-th child context of ctx (created on first use, destroyed with ctx).
 int ctx_child(bpp_ctx* ctx, size_t i, bpp_ctx** out);
 

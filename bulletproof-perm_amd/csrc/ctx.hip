@@ -180,6 +180,7 @@ int ctx_zc_in(bpp_ctx* ctx, const char* name, const void* h, size_t bytes, uint3
 // with or without a 15 us spin first, measured within noise (105-117 K vs
 // 101-120 K proofs/s at 12 in flight).
 int ctx_sync(bpp_ctx* ctx) {
+  if (ctx->sync_spin_us) return ctx_sync_latency(ctx, ctx->sync_spin_us);
   if (!ctx->sync_ev) BPP_HIP(hipEventCreateWithFlags(&ctx->sync_ev, hipEventDisableTiming));
   BPP_HIP(hipEventRecord(ctx->sync_ev, ctx->stream));
   for (hipError_t r; (r = hipEventQuery(ctx->sync_ev)) != hipSuccess;) {

@@ -46,6 +46,17 @@ int decompress_ws(bpp_ctx* ctx, const uint8_t* enc, size_t count, const char* na
   return BPP_OK;
 }
 
+// One commitment or one IPA is a chain of short kernels and host steps:
+// its syncs spin before sleeping (SyncSpin; BPP_IPA_SPIN_US, 0 = sleep at
+// once as the throughput paths do)
+static unsigned ipa_spin_us() {
+  static const unsigned v = [] {
+    const char* e = getenv("BPP_IPA_SPIN_US");
+    return e ? (unsigned)std::max(0, atoi(e)) : 400u;
+  }();
+  return v;
+}
+
 static int upload_opt(bpp_ctx* ctx, const uint8_t* s, size_t n, const char* name, uint32_t** d) {
   if (!s) {
     *d = nullptr;
@@ -124,6 +135,7 @@ int bpp_vec_commit(bpp_ctx* ctx, const bpp_gens* g, const uint8_t blind[32], con
   return bpp_guard(ctx, [&]() -> int {
     if (!ctx || !g || !blind || !a || !out) return BPP_ERR_ARG;
     if (n > g->n) return BPP_ERR_LEN;
+    SyncSpin spin(ctx, ipa_spin_us());
     BPP_HIP(hipSetDevice(ctx->device));
     const size_t T = 1 + n + (b ? n : 0);
     std::vector<uint8_t> sc(T * 32);
@@ -214,6 +226,7 @@ static int ipa_prove_api(bpp_ctx* ctx, const bpp_gens* g, IpaTranscript* tr, con
   return bpp_guard(ctx, [&]() -> int {
     if (!ctx || !g || !tr || !Q || !a || !b || !a_out || !b_out || ((!L_out || !R_out) && n > 1)) return BPP_ERR_ARG;
     if (n == 0 || (n & (n - 1)) || n > g->n) return BPP_ERR_LEN;
+    SyncSpin spin(ctx, ipa_spin_us());
     BPP_HIP(hipSetDevice(ctx->device));
     uint32_t *d_a, *d_b, *d_gf, *d_hf, *d_q;
     BPP_TRY(upload_scalars(ctx, a, n, "ipa_in_a", &d_a));
@@ -267,6 +280,7 @@ static int ipa_verify_api(bpp_ctx* ctx, const bpp_gens* g, IpaTranscript* tr, si
   return bpp_guard(ctx, [&]() -> int {
     if (!ctx || !g || !tr || !P || !Q || !a || !b || ((!L || !R) && n > 1)) return BPP_ERR_ARG;
     if (n == 0 || (n & (n - 1)) || n > g->n) return BPP_ERR_LEN;
+    SyncSpin spin(ctx, ipa_spin_us());
     BPP_HIP(hipSetDevice(ctx->device));
     uint32_t lg = 0;
     while ((1u << lg) < n) ++lg;

@@ -332,6 +332,15 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
   const size_t P = seeds.size();
   Ps.resize(P);
   if (!P) return BPP_OK;
+  // A small batch is a latency chain (a config-4 job's sub-batches): its
+  // syncs spin before sleeping; the throughput shape (384 proofs, 32 in
+  // flight) keeps the sleeping wait that frees the host cores
+  // (BPP_SPIN_BATCH = the largest batch that spins, 0 = none)
+  static const size_t spin_batch = [] {
+    const char* e = getenv("BPP_SPIN_BATCH");
+    return e ? (size_t)std::max(0, atoi(e)) : (size_t)128;
+  }();
+  SyncSpin spin(ctx, P <= spin_batch ? 300u : ctx->sync_spin_us);
   // (a plain reference: pool workers must reach THIS thread's states, a
   // thread_local named inside their lambdas would be their own)
   std::vector<std::unique_ptr<ProverState>>& S = prover_states_tl();
@@ -1732,6 +1741,15 @@ int bpp_perm_verify_batch(bpp_ctx* ctx, const bpp_gens* G, uint32_t k, size_t co
   return bpp_guard(ctx, [&]() -> int {
     if (!ctx || !G || ((!proofs || !V) && count) || (!label && llen) || k < 2 || k > (1u << 20)) return BPP_ERR_ARG;
     if (!count) return BPP_OK;
+    // (BPP_VERIFY_SPIN_US > 0: its syncs spin before sleeping, an A/B
+    // switch, off: the verifier's waits already spin where they sit on the
+    // critical path (ctx_sync_latency), and 300 us measured within noise,
+    // profiles/r06_sync_spin_ab.txt)
+    static const unsigned vspin = [] {
+      const char* e = getenv("BPP_VERIFY_SPIN_US");
+      return e ? (unsigned)std::max(0, atoi(e)) : 0u;
+    }();
+    SyncSpin spin(ctx, vspin ? vspin : ctx->sync_spin_us);
     BPP_HIP(hipSetDevice(ctx->device));
     const perm::Circuit C = perm::build(k);
     return verify_batch(ctx, G, C, label, llen, count, proofs, V);

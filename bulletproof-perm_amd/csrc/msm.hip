@@ -879,9 +879,20 @@ int dt_build(bpp_ctx* ctx, const uint32_t* d_wt, uint32_t npts, uint32_t c, uint
     ctx->err = "dt_build: table too large";
     return BPP_ERR_LEN;
   }
+  // 4 rows a lane (k_dt_build_n: one double-and-add and one inversion per 4
+  // rows; BPP_DT_BUILD_RPL=1 keeps one row a lane, an A/B switch)
+  static const int rpl = [] {
+    const char* e = getenv("BPP_DT_BUILD_RPL");
+    return e ? atoi(e) : 4;
+  }();
   {
     ProfScope ps(ctx, "dt_tables");
-    hipLaunchKernelGGL(k_dt_build, dim3(grid_for(rows, 64)), dim3(64), 0, ctx->stream, d_wt, npts, g, d_dt);
+    if (rpl == 4 && g.H % 4 == 0)
+      hipLaunchKernelGGL(k_dt_build_n<4>, dim3(grid_for(rows / 4, 64)), dim3(64), 0, ctx->stream, d_wt, npts, g, d_dt);
+    else if (rpl == 2)
+      hipLaunchKernelGGL(k_dt_build_n<2>, dim3(grid_for(rows / 2, 64)), dim3(64), 0, ctx->stream, d_wt, npts, g, d_dt);
+    else
+      hipLaunchKernelGGL(k_dt_build, dim3(grid_for(rows, 64)), dim3(64), 0, ctx->stream, d_wt, npts, g, d_dt);
   }
   return ctx_check_launch(ctx, "k_dt_build");
 }

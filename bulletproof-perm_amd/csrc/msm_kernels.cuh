@@ -1126,6 +1126,47 @@ __global__ void __launch_bounds__(64) k_dt_build(const uint32_t* __restrict__ wt
   store_niels(dt, (uint32_t)i, ge_to_niels(R));
 }
 
+// The same rows, RPL consecutive digits per lane: d0 * Q by double-and-add,
+// then d0 + 1 .. d0 + RPL - 1 by one addition each, and the RPL inverses of Z
+// by one field inversion (Montgomery's trick).  A lane's chain -- not the row
+// count -- sets a table build's time (one wave per SIMD or less: the Q slot
+// of bpp_ipa_prove builds 20 x 4096 rows per call), and this chain is ~1/RPL
+// of RPL separate double-and-adds and inversions.
+template <int RPL>
+__global__ void __launch_bounds__(64) k_dt_build_n(const uint32_t* __restrict__ wt, uint32_t ngen, DtGeom dg,
+                                                   uint32_t* __restrict__ dt) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // lane: rows [RPL t, RPL t + RPL)
+  const size_t i0 = t * RPL;
+  if (i0 >= (size_t)ngen * dg.W * dg.H) return;
+  const uint32_t d0 = (uint32_t)(i0 & (dg.H - 1)) + 1u;  // (H is a multiple of RPL: one window per lane)
+  const size_t kw = i0 >> (dg.c - 1);
+  const uint32_t k = (uint32_t)(kw / dg.W), w = (uint32_t)(kw % dg.W);
+  const uint32_t bit = dg.c * w;
+  ge_p3 Q = ge_from_niels(load_niels(wt, k * 32u + (bit >> 3)));
+  for (uint32_t r = 0; r < (bit & 7u); ++r) Q = ge_dbl(Q);
+  ge_p3 R[RPL];
+  R[0] = Q;
+  const int top = 31 - __clz(d0);
+  for (int b = top - 1; b >= 0; --b) {
+    R[0] = ge_dbl(R[0]);
+    if ((d0 >> b) & 1u) R[0] = ge_add(R[0], Q);
+  }
+  _Pragma("unroll") for (int j = 1; j < RPL; ++j) R[j] = ge_add(R[j - 1], Q);
+  fe pre[RPL];
+  fe run = R[0].Z;
+  pre[0] = fe_one();
+  _Pragma("unroll") for (int j = 1; j < RPL; ++j) {
+    pre[j] = run;
+    run = fe_mul(run, R[j].Z);
+  }
+  fe inv = fe_invert(run);
+  _Pragma("unroll") for (int j = RPL - 1; j >= 0; --j) {
+    const fe zi = j ? fe_mul(inv, pre[j]) : inv;
+    if (j) inv = fe_mul(inv, R[j].Z);
+    store_niels(dt, (uint32_t)(i0 + j), ge_niels_from_affine(fe_mul(R[j].X, zi), fe_mul(R[j].Y, zi)));
+  }
+}
+
 // One wave per heavy bucket: lane j sums pieces j, j+64, ... of the bucket's
 // chunk sequence, then a 6-level shuffle tree.  Blocks past heavy[0] exit.
 __global__ void __launch_bounds__(64) k_msm_fixup_heavy(const uint32_t* __restrict__ boff, uint32_t K,

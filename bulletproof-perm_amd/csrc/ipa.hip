@@ -289,6 +289,118 @@ FE_INLINE void ipa_round_body(const uint32_t* __restrict__ dt, const DtGeom& dg,
     um = sc_load(u + 16 * inst);
     uim = sc_load(u + 16 * inst + 8);
   }
+#ifndef IPA_SPLIT_PROLOGUE
+#define IPA_SPLIT_PROLOGUE 1
+#endif
+  if (IPA_SPLIT_PROLOGUE && J > 1) {
+    // A split round (J blocks per MSM: small batches, config 2): each block
+    // computes only what its slice needs -- the term scalars of its n / J
+    // slots per side, its J-th of the next state's writes and of the cross
+    // product -- instead of every block folding the whole state and forming
+    // all 2n term scalars (28 of a config-2 round's 64 us, EXP_IPA_NOWALK).
+    // The Q term rides in every block with that block's share of
+    // c = <a_lo, b_hi> (resp. <a_hi, b_lo>): the host adds the J partials,
+    // and sum_jp c^(jp) Q = c Q.
+    const uint32_t h = m >> 1;
+    const uint32_t* __restrict__ gf0p = A.gf0;
+    const uint32_t* __restrict__ hf0p = A.hf0;
+    auto cur_ab = [&](bool isb, uint32_t p) -> sc {  // element p of this round's a or b (Montgomery)
+      const uint32_t* in = isb ? bm_in : am_in;
+      if (fold)
+        return sc_add(sc_mont(sc_load(in + 8 * (ib + p)), isb ? uim : um),
+                      sc_mont(sc_load(in + 8 * (ib + p + m)), isb ? um : uim));
+      if (init) return sc_to_mont(sc_load((isb ? b0 : a0) + 8 * (ib + p)));
+      return sc_load(in + 8 * (ib + p));
+    };
+    auto factor = [&](bool ish, uint32_t k) -> sc {  // generator k's factor this round (canonical)
+      sc f;
+      if (init) {
+        const uint32_t* r = ish ? hf0p : gf0p;
+        if (r) {
+          f = sc_load(r + 8 * (ib + k));
+        } else {
+          f = sc_zero();
+          f.v[0] = 1;
+        }
+      } else {
+        f = sc_load((ish ? fH_in : fG_in) + 8 * (ib + k));
+      }
+      if (fold) {
+        const bool hi_prev = (k & (2 * m - 1)) & m;
+        f = sc_mont(f, hi_prev != ish ? um : uim);
+      }
+      return f;
+    };
+    // (i) this block's share of the next state (the side-0 blocks of S = 1)
+    if ((fold || init) && (S == 2 || side0 == 0)) {
+      const uint32_t q0 = (uint32_t)((uint64_t)jp * 2 * m / J), q1 = (uint32_t)((uint64_t)(jp + 1) * 2 * m / J);
+      for (uint32_t q = q0 + tid; q < q1; q += nt) {
+        const bool isb = q >= m;
+        const uint32_t p = isb ? q - m : q;
+        sc_store((isb ? bm_out : am_out) + 8 * (ib + p), cur_ab(isb, p));
+      }
+      const uint32_t f0 = (uint32_t)((uint64_t)jp * 2 * n / J), f1 = (uint32_t)((uint64_t)(jp + 1) * 2 * n / J);
+      for (uint32_t q = f0 + tid; q < f1; q += nt) {
+        const bool ish = q >= n;
+        const uint32_t k = ish ? q - n : q;
+        sc_store((ish ? fH_out : fG_out) + 8 * (ib + k), factor(ish, k));
+      }
+    }
+    // (ii) the slice's term scalars: side slots [t0, t1) of [0, n) (G terms
+    // below n / 2, H terms above), local slot cnt = the Q term
+    const uint32_t t0 = (uint32_t)((uint64_t)jp * n / J), t1 = (uint32_t)((uint64_t)(jp + 1) * n / J);
+    const uint32_t cnt = t1 - t0, CS = cnt + 1;
+    uint32_t* tsl = lds;                            // S x CS x 8 words
+    uint32_t* tgl = lds + 8 * S * CS;               // S x CS
+    uint32_t* redl = tgl + ((S * CS + 3) & ~3u);    // S x waves x 8 words
+    for (uint32_t q = tid; q < S * cnt; q += nt) {
+      const uint32_t s = q / cnt, slot = t0 + (q - s * cnt);
+      const uint32_t side = S == 2 ? s : side0;
+      const bool ish = slot >= (n >> 1);
+      const uint32_t cidx = slot - (ish ? (n >> 1) : 0u);
+      const bool hi = ish != (side == 0);  // G_k on side 0 for hi k, H_k for lo k
+      const uint32_t k = ((cidx >> lg_h) << (lg_h + 1)) | (hi ? h : 0u) | (cidx & (h - 1));
+      const uint32_t p = (k & (m - 1)) ^ h;
+      const sc x = sc_mont(cur_ab(ish, p), factor(ish, k));
+      sc_store(tsl + 8 * (s * CS + (slot - t0)), halve ? sc_half(x) : x);
+      tgl[s * CS + (slot - t0)] = (ish ? hbase : gbase) + k;
+    }
+    // (iii) this block's share of the cross product
+    const uint32_t j0 = (uint32_t)((uint64_t)jp * h / J), j1 = (uint32_t)((uint64_t)(jp + 1) * h / J);
+    for (uint32_t s = 0; s < S; ++s) {
+      const uint32_t side = S == 2 ? s : side0;
+      sc c = sc_zero();
+      for (uint32_t j = j0 + tid; j < j1; j += nt)
+        c = sc_add(c, side == 0 ? sc_mont(cur_ab(false, j), cur_ab(true, j + h))
+                                : sc_mont(cur_ab(false, j + h), cur_ab(true, j)));
+      c = sc_wave_sum(c);
+      if ((tid & 63u) == 0) sc_store(redl + 8 * (s * nwv + (tid >> 6)), c);
+    }
+    __syncthreads();
+    if (tid < S) {
+      sc t = sc_zero();
+      for (uint32_t wv = 0; wv < nwv; ++wv) t = sc_add(t, sc_load(redl + 8 * (tid * nwv + wv)));
+      const sc cq = sc_mont(t, sc_load(qmul + 8 * inst));
+      sc_store(tsl + 8 * (tid * CS + cnt), halve ? sc_half(cq) : cq);
+      tgl[tid * CS + cnt] = qidx;
+    }
+    __syncthreads();
+    const uint32_t ns = nt / S, ls = tid / ns, lt = tid - ls * ns;
+    const uint32_t tg = lt / dg.W;
+    const DtLane ln = DtLane::make(dg, lt % dg.W);
+    const uint32_t* __restrict__ tscs = tsl + 8 * ls * CS;
+    const uint32_t* __restrict__ tgens = tgl + ls * CS;
+    const ge_p3 acc = tg < TG ? dt_walk(dt, dg, ln, tg, CS, TG,
+                                        [&](uint32_t t, uint32_t sv[8], uint32_t& gen) {
+                                          const sc v = sc_load(tscs + 8 * t);
+                                          _Pragma("unroll") for (int i = 0; i < 8; ++i) sv[i] = v.v[i];
+                                          gen = tgens[t];
+                                        })
+                              : ge_identity();
+    __syncthreads();
+    dt_block_tree_segs(lds, acc, nt, S, out_p3, S == 2 ? 2 * inst * J + jp : bidx, J);
+    return;
+  }
   // 1. a, b of this round (length m) into LDS: item q < m is a_q, q >= m is
   // b_{q-m} (one vector per lane, so a fold costs a lane two multiplies, not
   // four, while 2 m <= blockDim)

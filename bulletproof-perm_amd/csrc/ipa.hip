@@ -810,7 +810,10 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
   // J blocks per L / R MSM when the batch is small (config 2: P = 1, two
   // blocks of one wave per SIMD walking ~64 of the 1025 terms per lane in a
   // row): each block walks a slice of the terms and the host adds the J
-  // partials before it encodes (zero-copy path only; BPP_IPA_SPLIT overrides)
+  // partials before it encodes (zero-copy path only; BPP_IPA_SPLIT overrides).
+  // Since each block folds only its own slice (IPA_SPLIT_PROLOGUE) a slice
+  // may be as short as one term per lane group: config 2 J = 16 1.10-1.13 ms,
+  // 32 1.06, 64 1.10 (profiles/r06_ipa_jsweep.txt)
   uint32_t J = 1;
   if (zc && nt) {
     static const int split_env = [] {
@@ -820,7 +823,14 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
     if (split_env >= 1) {
       J = (uint32_t)split_env;
     } else if (split_env < 0) {
-      while (J < 16 && 2 * P * (2 * J) <= 512 && (n + 1) / (2 * J) >= 2 * TG) J *= 2;
+#ifndef IPA_J_MAX
+#define IPA_J_MAX 32
+#endif
+#ifndef IPA_J_SLICE_TG
+#define IPA_J_SLICE_TG (IPA_SPLIT_PROLOGUE ? 1 : 2)
+#endif
+      const uint32_t per_slice = IPA_J_SLICE_TG * TG;
+      while (J < IPA_J_MAX && 2 * P * (2 * J) <= 512 && (n + 1) / (2 * J) >= per_slice) J *= 2;
     }
   }
   uint32_t* h_uw = nullptr;  // zc: the challenges' device words, in place

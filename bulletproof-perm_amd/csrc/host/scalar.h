@@ -263,13 +263,50 @@ static inline Sc invert(const Sc& a) {
   return pow(a, e);
 }
 
+// a^-1 mod l by the binary extended Euclidean algorithm, in time that depends
+// on a: only for public values (the inner-product argument's challenges u,
+// which the transcript publishes).  Invariants x1 a = u, x2 a = v (mod l);
+// each step halves an even one of u, v (and its x mod l) or subtracts the
+// smaller odd one from the larger.  ~3x fewer 64-bit operations than
+// invert's 250 squarings (config 2 spends one per IPA round on the host).
+// a != 0 mod l.
+static inline Sc invert_vartime(const Sc& a) {
+  auto shr1 = [](Sc s) {
+    for (int i = 0; i < 3; ++i) s.v[i] = (s.v[i] >> 1) | (s.v[i + 1] << 63);
+    s.v[3] >>= 1;
+    return s;
+  };
+  auto is_one = [](const Sc& s) { return s.v[0] == 1 && (s.v[1] | s.v[2] | s.v[3]) == 0; };
+  Sc u = a, v = L, x1 = one(), x2 = zero();
+  while (!is_one(u) && !is_one(v)) {
+    while (!(u.v[0] & 1)) {
+      u = shr1(u);
+      x1 = half(x1);
+    }
+    while (!(v.v[0] & 1)) {
+      v = shr1(v);
+      x2 = half(x2);
+    }
+    if (is_one(u) || is_one(v)) break;
+    if (geq(u, v)) {
+      u = sub_raw(u, v, nullptr);
+      x1 = sub(x1, x2);
+    } else {
+      v = sub_raw(v, u, nullptr);
+      x2 = sub(x2, x1);
+    }
+  }
+  return is_one(u) ? x1 : x2;
+}
+
 // Montgomery's trick; returns the inverse of the product.  Zero inputs
 // are not allowed (dalek batch_invert has the same precondition).
 // One Montgomery product per step on canonical values: acc_i = prod_{j<i}
 // x_j R^-i, inv_{i+1} = acc_{i+1}^-1 = prod_{j<=i} x_j^-1 R^(i+1), so
 // mont(inv_{i+1}, acc_i) = x_i^-1 and mont(inv_{i+1}, x_i) = inv_i: 3n
 // products + one inversion (the canonical-product form took 6n).
-static inline Sc batch_invert(std::vector<Sc>& xs, bool want_allinv = true) {
+// vartime: the one inversion by invert_vartime (public inputs only).
+static inline Sc batch_invert(std::vector<Sc>& xs, bool want_allinv = true, bool vartime = false) {
   const size_t n = xs.size();
   std::vector<Sc> pref(n);
   Sc acc = one();
@@ -277,7 +314,7 @@ static inline Sc batch_invert(std::vector<Sc>& xs, bool want_allinv = true) {
     pref[i] = acc;
     acc = mont(acc, xs[i]);
   }
-  Sc inv = invert(acc);  // prod x^-1 R^n
+  Sc inv = vartime ? invert_vartime(acc) : invert(acc);  // prod x^-1 R^n
   Sc allinv = zero();
   if (want_allinv) {  // prod x^-1 = inv R^-n
     allinv = inv;

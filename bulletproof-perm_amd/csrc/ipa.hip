@@ -189,6 +189,17 @@ __global__ void __launch_bounds__(256) k_ipa_fold(uint32_t n, uint32_t lg_n, uin
   }
 }
 
+// The J partials of a split round's L / R (block b = MSM b, lane j = partial
+// b J + j, J a power of two <= 64) summed by dt_block_tree_segs' tree and
+// written to out[b] (pinned host memory) -- the host then encodes 2P points
+// instead of adding 2P (J - 1) first.
+__global__ void __launch_bounds__(64) k_ipa_jsum(const uint32_t* __restrict__ part, uint32_t J,
+                                                uint32_t* __restrict__ out) {
+  extern __shared__ uint32_t lds[];
+  const ge_p3 p = load_p3(part, (size_t)blockIdx.x * J + threadIdx.x);
+  dt_block_tree_segs(lds, p, J, 1, out, blockIdx.x, 0);
+}
+
 // The last fold of the fused path, for element 0 only (the proof's a, b):
 // out[p] = (a_0 u + a_1 u^-1, b_0 u^-1 + b_1 u), Montgomery words, written
 // in place into pinned host memory -- one launch where k_ipa_fold over all n
@@ -833,14 +844,27 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
       while (J < IPA_J_MAX && 2 * P * (2 * J) <= 512 && (n + 1) / (2 * J) >= per_slice) J *= 2;
     }
   }
+  // the J partials of each L / R summed on the device (k_ipa_jsum, one
+  // block per MSM, a 5-level tree for J = 32) rather than by 2 (J - 1) host
+  // additions between the rounds: an A/B switch, off (BPP_IPA_JSUM=1 on).
+  // Config 2 measured 1.10-1.11 ms with it against 1.03-1.04 without: the
+  // host's 62 additions take ~6.5 us a round, the extra launch and its tree
+  // ~13 us of the round's wait (profiles/r06_ipa_jsum_ab.txt)
+  static const bool jsum_env = [] {
+    const char* e = getenv("BPP_IPA_JSUM");
+    return e && atoi(e) != 0;
+  }();
+  const bool dev_jsum = zc && !merge && J > 1 && J <= 64 && (J & (J - 1)) == 0 && jsum_env;
+  void* d_part = nullptr;  // dev_jsum: the round kernel's J partials per MSM
   uint32_t* h_uw = nullptr;  // zc: the challenges' device words, in place
   if (zc) {
     void *hr = nullptr, *hu = nullptr;
-    BPP_TRY(ctx_host_buf(ctx, "ipa_res_h", (size_t)2 * P * J * P3_BYTES, &hr));
+    BPP_TRY(ctx_host_buf(ctx, "ipa_res_h", (size_t)2 * P * (dev_jsum ? 1 : J) * P3_BYTES, &hr));
     BPP_TRY(ctx_host_buf(ctx, "ipa_u_h", (size_t)P * 64, &hu));
     d_res = hr;
     d_u = hu;
     h_uw = (uint32_t*)hu;
+    if (dev_jsum) BPP_TRY(ctx_ws(ctx, "ipa_part", (size_t)2 * P * J * P3_BYTES, &d_part));
   }
   void *d_states = nullptr, *d_lr = nullptr;
   if (dev_merlin) {
@@ -890,8 +914,11 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
                            g.pts.dt, dg, n, m, lg_h, round ? 1u : 0u, S[in][0], S[in][1], S[in][2], S[in][3],
                            S[round ? outs : in][0], S[round ? outs : in][1], S[round ? outs : in][2],
                            S[round ? outs : in][3], (const uint32_t*)d_u, (const uint32_t*)d_q, g.gbase, g.hbase,
-                           g.qidx, TG, dev_merlin ? 0u : 1u, (uint32_t*)d_res, d_a, d_b, d_Gf, d_Hf,
-                           round ? 0u : 1u, J, sides);
+                           g.qidx, TG, dev_merlin ? 0u : 1u, (uint32_t*)(dev_jsum ? d_part : d_res), d_a, d_b,
+                           d_Gf, d_Hf, round ? 0u : 1u, J, sides);
+        if (dev_jsum)
+          hipLaunchKernelGGL(k_ipa_jsum, dim3(2 * P), dim3(J), (size_t)J * P3_BYTES, ctx->stream,
+                             (const uint32_t*)d_part, J, (uint32_t*)d_res);
       }
       BPP_TRY(ctx_check_launch(ctx, "k_ipa_round_dt"));
       if (round) cur = outs;
@@ -912,8 +939,11 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
         BPP_TRY(ipa_transcript_step_dev(ctx, P, (uint8_t*)d_states, lr, (uint32_t*)d_u));
       } else if (zc) {
         HostScope hs(ctx, "ipa_msm");
-        BPP_TRY(ctx_sync(ctx));  // the kernel's L/2, R/2 are in host memory now
-        BPP_TRY(points_double_encode_host(ctx, (const uint32_t*)d_res, 2 * (size_t)P, enc.data(), J));
+        {
+          HostScope hw(ctx, "ipa_wait");
+          BPP_TRY(ctx_sync(ctx));  // the kernel's L/2, R/2 are in host memory now
+        }
+        BPP_TRY(points_double_encode_host(ctx, (const uint32_t*)d_res, 2 * (size_t)P, enc.data(), dev_jsum ? 1 : J));
       } else {
         HostScope hs(ctx, "ipa_msm");
         BPP_TRY(points_double_encode_p3(ctx, (const uint32_t*)d_res, 2 * (size_t)P, enc.data()));
@@ -975,7 +1005,10 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
       out[p].R.push_back(Re);
     }
     ui = u;
-    hsc::batch_invert(ui, false);
+    {
+      HostScope hi(ctx, "ipa_uinv");
+      hsc::batch_invert(ui, false, true);  // (u: public challenges)
+    }
     uint32_t* uwp = zc ? h_uw : uw.data();  // (zc: the device reads them in place)
     for (uint32_t p = 0; p < P; ++p) {  // device Montgomery forms u R, u^-1 R
       const sc um = to_dev_sc(hsc::to_mont(u[p]));
@@ -1072,7 +1105,7 @@ bool ipa_verification_scalars(IpaTranscript& tr, uint32_t n, const std::vector<E
     if (!tr.challenge_scalar("u", u[j])) return failed();
   }
   std::vector<hsc::Sc> ui = u;
-  const hsc::Sc allinv = hsc::batch_invert(ui);
+  const hsc::Sc allinv = hsc::batch_invert(ui, true, true);  // (u: public challenges)
   u_sq.resize(lg_n);
   uinv_sq.resize(lg_n);
   for (size_t j = 0; j < lg_n; ++j) {

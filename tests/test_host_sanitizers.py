@@ -49,3 +49,18 @@ def test_from_wide_fast_path_matches_montgomery_form(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "mismatches: 0" in r.stdout, (r.stdout + r.stderr)[-2000:]
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not installed")
+def test_invert_vartime_matches_fermat(tmp_path):
+    """hsc::invert_vartime (binary extended Euclid, the IPA challenges'
+    inversions) equals hsc::invert (a^(l-2)) on ~200 K random, sparse and
+    edge scalars, and batch_invert's vartime form equals its constant-time
+    form, under UBSan."""
+    exe = tmp_path / "invert"
+    cmd = ["g++", "-std=c++17", "-O2", "-g", "-march=x86-64-v3", "-fsanitize=undefined", "-fno-sanitize-recover=all",
+           "-I", str(CSRC), str(ROOT / "tests" / "c" / "invert_check.cpp"), "-o", str(exe)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "mismatches: 0" in r.stdout, (r.stdout + r.stderr)[-2000:]

@@ -335,27 +335,36 @@ static inline Sc inner_product(const std::vector<Sc>& a, const std::vector<Sc>& 
   return mont(r, R2);
 }
 
-// (1, x, x^2, ..., x^{n-1})
-static inline std::vector<Sc> powers(const Sc& x, size_t n) {
-  std::vector<Sc> r(n);
+// r[i] = r[0] x^i from r[0] (canonical or Montgomery form alike: mont by xR
+// multiplies by x): four interleaved chains r[i] = r[i-4] x^4 after the
+// first four, so four independent products overlap in the core's pipeline
+// instead of one chain of n dependent ones (2^10 powers ~3x faster)
+static inline void powers_fill(std::vector<Sc>& r, Sc c, const Sc& x) {
+  const size_t n = r.size();
   const Sc xR = to_mont(x);
-  Sc c = one();
-  for (size_t i = 0; i < n; ++i) {
+  size_t i = 0;
+  for (; i < n && i < 4; ++i) {
     r[i] = c;
     c = mont(c, xR);
   }
+  if (i == n) return;
+  Sc x4 = mont(x, xR);   // x^2
+  x4 = mont(x4, x4);     // x^4 R^-1 ... (mont(a, a) = a^2 R^-1)
+  x4 = mont(x4, R3);     // x^4 R
+  for (; i < n; ++i) r[i] = mont(r[i - 4], x4);
+}
+
+// (1, x, x^2, ..., x^{n-1})
+static inline std::vector<Sc> powers(const Sc& x, size_t n) {
+  std::vector<Sc> r(n);
+  powers_fill(r, one(), x);
   return r;
 }
 
 // (R, xR, x^2 R, ...): Montgomery forms of the powers, for mulm
 static inline std::vector<Sc> powers_mont(const Sc& x, size_t n) {
   std::vector<Sc> r(n);
-  const Sc xR = to_mont(x);
-  Sc c = to_mont(one());
-  for (size_t i = 0; i < n; ++i) {
-    r[i] = c;
-    c = mont(c, xR);
-  }
+  powers_fill(r, to_mont(one()), x);
   return r;
 }
 

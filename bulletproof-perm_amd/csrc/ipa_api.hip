@@ -57,6 +57,38 @@ static unsigned ipa_spin_us() {
   return v;
 }
 
+// Canonical host scalars into the pinned buffer `name`, which the kernels
+// read in place (null s: *d = null, all ones); a non-canonical scalar fails
+// with its index before anything is queued.
+static int zc_scalars(bpp_ctx* ctx, const uint8_t* s, size_t n, const char* name, uint32_t** d) {
+  *d = nullptr;
+  if (!s) return BPP_OK;
+  for (size_t i = 0; i < n; ++i)
+    if (!scalar_is_canonical(s + 32 * i)) {
+      ctx->err = "non-canonical scalar at index " + std::to_string(i);
+      return BPP_ERR_NONCANONICAL;
+    }
+  BPP_TRY(ctx_zc_out(ctx, name, 32 * n + 32, d));
+  memcpy(*d, s, 32 * n);
+  memset((uint8_t*)*d + 32 * n, 0, 32);
+  return BPP_OK;
+}
+
+// Zeroes the pinned copies of the witness (a, b) when the call returns,
+// error paths included (after their drain): no secret residue in pinned
+// host memory once bpp_ipa_prove(_cb) is back.
+struct IpaZcWipe {
+  bpp_ctx* ctx;
+  std::vector<std::pair<void*, size_t>> spans;
+  explicit IpaZcWipe(bpp_ctx* c) : ctx(c) {}
+  void add(void* p, size_t n) {
+    if (p) spans.emplace_back(p, n);
+  }
+  ~IpaZcWipe() {
+    for (auto& sp : spans) memset(sp.first, 0, sp.second);  // (persistent buffers: not a dead store)
+  }
+};
+
 static int upload_opt(bpp_ctx* ctx, const uint8_t* s, size_t n, const char* name, uint32_t** d) {
   if (!s) {
     *d = nullptr;
@@ -244,10 +276,6 @@ static int ipa_prove_api(bpp_ctx* ctx, const bpp_gens* g, IpaTranscript* tr, con
     SyncSpin spin(ctx, ipa_spin_us());
     BPP_HIP(hipSetDevice(ctx->device));
     uint32_t *d_a, *d_b, *d_gf, *d_hf, *d_q;
-    BPP_TRY(upload_scalars(ctx, a, n, "ipa_in_a", &d_a));
-    BPP_TRY(upload_scalars(ctx, b, n, "ipa_in_b", &d_b));
-    BPP_TRY(upload_opt(ctx, G_factors, n, "ipa_in_gf", &d_gf));
-    BPP_TRY(upload_opt(ctx, H_factors, n, "ipa_in_hf", &d_hf));
     IpaGens ig;
     BPP_TRY(gens_points(ctx, g, &ig.pts));
     ig.gbase = 0;
@@ -262,21 +290,48 @@ static int ipa_prove_api(bpp_ctx* ctx, const bpp_gens* g, IpaTranscript* tr, con
     std::unique_lock<std::mutex> qlock;
     // (exactly the fused rounds' condition, ipa.hip: the slot has direct-table
     // rows and a Niels row only, no window-table rows for the other engines)
-    if (qslot_env && n >= 2 && n <= IPA_FUSED_NMAX && msm_use_dt(ig.pts, 2, (uint32_t)(2 * n + 2))) {
+    const bool qslot =
+        qslot_env && n >= 2 && n <= IPA_FUSED_NMAX && msm_use_dt(ig.pts, 2, (uint32_t)(2 * n + 2));
+    // the fused path: Q's table build is queued first, and a, b and the
+    // factors are read in place by round 0 from pinned host memory (each
+    // element once) -- the inputs' staging copies and H2D enqueues, ~40 us
+    // of host time, run beside the build instead of before it
+    bool zc_in = false;
+    if (qslot) {
       qlock = std::unique_lock<std::mutex>(g->q_mu);
       BPP_TRY(ipa_q_slot(ctx, g, Q, ig.pts.dt_c));
       ig.qidx = g->qslot();
+      static const bool zc_env = [] {
+        const char* e = getenv("BPP_IPA_ZC_IN");
+        return !e || atoi(e) != 0;
+      }();
+      zc_in = zc_env;
     } else {
       BPP_TRY(decompress_ws(ctx, Q, 1, "ipa_q", &d_q));
       BPP_TRY(msm_points_extra(ctx, &ig.pts, d_q, 1, (uint32_t)(2 * g->n + 2), "ipa_q_wt", (double)(n + 1)));
       ig.qidx = ig.pts.n0;
     }
+    IpaZcWipe wipe(ctx);
+    if (zc_in) {
+      BPP_TRY(zc_scalars(ctx, a, n, "ipa_zc_a", &d_a));
+      wipe.add(d_a, 32 * n);
+      BPP_TRY(zc_scalars(ctx, b, n, "ipa_zc_b", &d_b));
+      wipe.add(d_b, 32 * n);
+      BPP_TRY(zc_scalars(ctx, G_factors, n, "ipa_zc_gf", &d_gf));
+      BPP_TRY(zc_scalars(ctx, H_factors, n, "ipa_zc_hf", &d_hf));
+    } else {
+      BPP_TRY(upload_scalars(ctx, a, n, "ipa_in_a", &d_a));
+      BPP_TRY(upload_scalars(ctx, b, n, "ipa_in_b", &d_b));
+      BPP_TRY(upload_opt(ctx, G_factors, n, "ipa_in_gf", &d_gf));
+      BPP_TRY(upload_opt(ctx, H_factors, n, "ipa_in_hf", &d_hf));
+    }
     IpaProofHost pf;
     {
       const int rc = ipa_prove_dev(ctx, *tr, ig, (uint32_t)n, d_gf, d_hf, d_a, d_b, pf);
       // a failed IPA (a hook error, a device error) may leave this context's
-      // kernels queued on the Q slot: drain them before the slot's lock goes
-      if (rc != BPP_OK && qlock.owns_lock()) (void)hipStreamSynchronize(ctx->stream);
+      // kernels queued on the Q slot or reading the pinned inputs: drain them
+      // before the slot's lock goes and the inputs are wiped
+      if (rc != BPP_OK && (qlock.owns_lock() || zc_in)) (void)hipStreamSynchronize(ctx->stream);
       BPP_TRY(rc);
     }
     for (size_t j = 0; j < pf.L.size(); ++j) {

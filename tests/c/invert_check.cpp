@@ -50,6 +50,24 @@ int main() {
   ys = xs;
   const hsc::Sc pa = hsc::batch_invert(xs, true, false), pb = hsc::batch_invert(ys, true, true);
   if (xs != ys || pa != pb) ++bad, puts("batch_invert vartime mismatch");
+  // powers / powers_mont (four interleaved chains) against one chain of mul
+  for (int t = 0; t < 40; ++t) {
+    const hsc::Sc x = t == 0 ? hsc::one() : t == 1 ? hsc::zero() : xs[t % xs.size()];
+    const size_t n = t < 20 ? (size_t)t : 1024 + t;
+    const std::vector<hsc::Sc> p = hsc::powers(x, n), pm = hsc::powers_mont(x, n);
+    hsc::Sc c = hsc::one();
+    for (size_t i = 0; i < n; ++i) {
+      if (p[i] != c || pm[i] != hsc::to_mont(c)) {
+        if (bad++ < 5) printf("powers mismatch t=%d i=%zu\n", t, i);
+        break;
+      }
+      c = hsc::mul(c, x);
+    }
+  }
+  const auto tp0 = std::chrono::steady_clock::now();
+  for (int i = 0; i < 200; ++i) xs[0].v[0] ^= hsc::powers(xs[1], 1024)[1023].v[0] & 1;
+  const auto tp1 = std::chrono::steady_clock::now();
+  printf("powers(1024) %.2f us\n", std::chrono::duration<double, std::micro>(tp1 - tp0).count() / 200);
   const auto t0 = std::chrono::steady_clock::now();
   hsc::Sc acc = xs[0];
   for (int i = 0; i < 20000; ++i) acc = hsc::add(hsc::invert_vartime(acc), hsc::one());

@@ -243,7 +243,7 @@ std::vector<Proof>& proofs_tl();
 // by each sub-batch thread on its child context (BPP_PROVE_STREAMS > 1).
 static const char* const kSecretWs[] = {"pb_rng_in", "pb_gamma", "mt_s",  "pv_v",   "pv_g",    "pv_gx",  "poly_vec",
                                         "poly_hf",   "pf_l",     "pf_r",  "ipa_am", "ipa_bm",  "ipa_am1", "ipa_bm1"};
-static const char* const kSecretHost[] = {"pp_v", "pp_g"};
+static const char* const kSecretHost[] = {"pp_v", "pp_g", "ipa_zc_a", "ipa_zc_b"};  // (ipa_zc_*: bpp_ipa_prove zeroes them itself)
 // The device workspaces of kSecretWs zeroed by ONE launch (blockIdx.y = span)
 // instead of one hipMemsetAsync (a fill kernel each) per workspace.
 #define WIPE_MAX 16

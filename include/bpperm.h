@@ -243,7 +243,11 @@ int bpp_scalar_powers(const uint8_t x[32], size_t n, uint8_t* out);
  * compressed points each; G_factors / H_factors may be NULL (all ones).
  * Q may be any point: it is written into g's spare generator slot for the
  * call (BPP_ERR_DECOMPRESS if it does not decode), so concurrent
- * bpp_ipa_prove calls on one g (from several contexts) run one at a time. */
+ * bpp_ipa_prove calls on one g (from several contexts) run one at a time.
+ * On that path the kernels read a, b and the factors in place from ctx's
+ * pinned host buffers (copied in at the call; the copies of a and b are
+ * zeroed before it returns, on error paths too); the folded a, b stay in
+ * ctx's device workspaces (the entropy prover's wipe zeroes them). */
 int bpp_ipa_prove(bpp_ctx* ctx, const bpp_gens* g, bpp_transcript* tr, const uint8_t Q[32], const uint8_t* G_factors,
                   const uint8_t* H_factors, const uint8_t* a, const uint8_t* b, size_t n, uint8_t* L_out,
                   uint8_t* R_out, uint8_t a_out[32], uint8_t b_out[32]);

@@ -632,7 +632,7 @@ int prove_batch(bpp_ctx* ctx, const bpp_gens* G, const perm::Circuit& C, const s
           ch[3 * p + 2] = st.tr.challenge_scalar("z");
         });
     std::vector<Sc> yinv = ys;
-    hsc::batch_invert(yinv, false);
+    hsc::batch_invert(yinv, false, true);  // (y: public challenges)
     for (size_t p = 0; p < P; ++p) ch[3 * p + 1] = yinv[p];
     BPP_TRY(poly_coef_dev(ctx, C, (uint32_t)P, d_s, per, d_gamma, ch, tco));
     for (size_t p = 0; p < P; ++p) {

@@ -359,6 +359,23 @@ static inline void encode_double_batch_auto(const ge* pts, size_t n, uint8_t* ou
     encode_double_batch(pts, n, out);
 }
 
+// out[i] = in[i J] + ... + in[i J + J - 1] (i < n): eight additions per
+// AVX-512 IFMA vector (host/encode_x8.cpp) when the CPU has IFMA and
+// BPP_HOST_IFMA is not 0, else one chain per point
+void ge_sum_x8(const ge* in, size_t n, uint32_t J, ge* out);
+static inline void ge_sum_auto(const ge* in, size_t n, uint32_t J, ge* out) {
+  const char* e = getenv("BPP_HOST_IFMA");
+  if (J >= 4 && encode_x8_available() && !(e && e[0] == '0')) {
+    ge_sum_x8(in, n, J, out);
+    return;
+  }
+  for (size_t i = 0; i < n; ++i) {
+    ge t = in[i * J];
+    for (uint32_t j = 1; j < J; ++j) t = ge_add(t, in[i * J + j]);
+    out[i] = t;
+  }
+}
+
 static inline bool decode(ge& out, const uint8_t in[32]) {
   fe s = fe_from_bytes(in);
   uint8_t chk[32];

@@ -297,43 +297,52 @@ static int ipa_prove_api(bpp_ctx* ctx, const bpp_gens* g, IpaTranscript* tr, con
     // element once) -- the inputs' staging copies and H2D enqueues, ~40 us
     // of host time, run beside the build instead of before it
     bool zc_in = false;
-    if (qslot) {
-      qlock = std::unique_lock<std::mutex>(g->q_mu);
-      BPP_TRY(ipa_q_slot(ctx, g, Q, ig.pts.dt_c));
-      ig.qidx = g->qslot();
-      static const bool zc_env = [] {
-        const char* e = getenv("BPP_IPA_ZC_IN");
-        return !e || atoi(e) != 0;
-      }();
-      zc_in = zc_env;
-    } else {
-      BPP_TRY(decompress_ws(ctx, Q, 1, "ipa_q", &d_q));
-      BPP_TRY(msm_points_extra(ctx, &ig.pts, d_q, 1, (uint32_t)(2 * g->n + 2), "ipa_q_wt", (double)(n + 1)));
-      ig.qidx = ig.pts.n0;
-    }
-    IpaZcWipe wipe(ctx);
-    if (zc_in) {
-      BPP_TRY(zc_scalars(ctx, a, n, "ipa_zc_a", &d_a));
-      wipe.add(d_a, 32 * n);
-      BPP_TRY(zc_scalars(ctx, b, n, "ipa_zc_b", &d_b));
-      wipe.add(d_b, 32 * n);
-      BPP_TRY(zc_scalars(ctx, G_factors, n, "ipa_zc_gf", &d_gf));
-      BPP_TRY(zc_scalars(ctx, H_factors, n, "ipa_zc_hf", &d_hf));
-    } else {
-      BPP_TRY(upload_scalars(ctx, a, n, "ipa_in_a", &d_a));
-      BPP_TRY(upload_scalars(ctx, b, n, "ipa_in_b", &d_b));
-      BPP_TRY(upload_opt(ctx, G_factors, n, "ipa_in_gf", &d_gf));
-      BPP_TRY(upload_opt(ctx, H_factors, n, "ipa_in_hf", &d_hf));
-    }
+    IpaZcWipe wipe(ctx);  // (destroyed before qlock: the drain below runs first)
     IpaProofHost pf;
-    {
-      const int rc = ipa_prove_dev(ctx, *tr, ig, (uint32_t)n, d_gf, d_hf, d_a, d_b, pf);
-      // a failed IPA (a hook error, a device error) may leave this context's
-      // kernels queued on the Q slot or reading the pinned inputs: drain them
-      // before the slot's lock goes and the inputs are wiped
-      if (rc != BPP_OK && (qlock.owns_lock() || zc_in)) (void)hipStreamSynchronize(ctx->stream);
-      BPP_TRY(rc);
+    auto body = [&]() -> int {
+      if (qslot) {
+        qlock = std::unique_lock<std::mutex>(g->q_mu);
+        BPP_TRY(ipa_q_slot(ctx, g, Q, ig.pts.dt_c));
+        ig.qidx = g->qslot();
+        static const bool zc_env = [] {
+          const char* e = getenv("BPP_IPA_ZC_IN");
+          return !e || atoi(e) != 0;
+        }();
+        zc_in = zc_env;
+      } else {
+        BPP_TRY(decompress_ws(ctx, Q, 1, "ipa_q", &d_q));
+        BPP_TRY(msm_points_extra(ctx, &ig.pts, d_q, 1, (uint32_t)(2 * g->n + 2), "ipa_q_wt", (double)(n + 1)));
+        ig.qidx = ig.pts.n0;
+      }
+      if (zc_in) {
+        BPP_TRY(zc_scalars(ctx, a, n, "ipa_zc_a", &d_a));
+        wipe.add(d_a, 32 * n);
+        BPP_TRY(zc_scalars(ctx, b, n, "ipa_zc_b", &d_b));
+        wipe.add(d_b, 32 * n);
+        BPP_TRY(zc_scalars(ctx, G_factors, n, "ipa_zc_gf", &d_gf));
+        BPP_TRY(zc_scalars(ctx, H_factors, n, "ipa_zc_hf", &d_hf));
+      } else {
+        BPP_TRY(upload_scalars(ctx, a, n, "ipa_in_a", &d_a));
+        BPP_TRY(upload_scalars(ctx, b, n, "ipa_in_b", &d_b));
+        BPP_TRY(upload_opt(ctx, G_factors, n, "ipa_in_gf", &d_gf));
+        BPP_TRY(upload_opt(ctx, H_factors, n, "ipa_in_hf", &d_hf));
+      }
+      return ipa_prove_dev(ctx, *tr, ig, (uint32_t)n, d_gf, d_hf, d_a, d_b, pf);
+    };
+    int rc;
+    try {
+      rc = body();
+    } catch (const std::bad_alloc&) {
+      rc = BPP_ERR_NOMEM;
+    } catch (...) {
+      rc = BPP_ERR_DEVICE;
     }
+    // a failed call (a non-canonical input, a hook error, a device error)
+    // may leave this context's kernels queued on the Q slot (its build is
+    // queued first) or reading the pinned inputs: drain them before the
+    // slot's lock goes and the inputs are wiped
+    if (rc != BPP_OK && (qlock.owns_lock() || zc_in)) (void)hipStreamSynchronize(ctx->stream);
+    BPP_TRY(rc);
     for (size_t j = 0; j < pf.L.size(); ++j) {
       memcpy(L_out + 32 * j, pf.L[j].data(), 32);
       memcpy(R_out + 32 * j, pf.R[j].data(), 32);

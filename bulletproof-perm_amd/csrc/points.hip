@@ -108,10 +108,12 @@ int points_double_encode_host(bpp_ctx* ctx, const uint32_t* raw, size_t n, uint8
   par::for_each(chunks, [&](size_t c) {
     const size_t b = n * c / chunks, e = n * (c + 1) / chunks;
     std::vector<h25519::ge> pts(e - b);
-    for (size_t i = b; i < e; ++i) {
-      pts[i - b] = h25519::ge_from_dev(raw + i * J * P3_WORDS);
-      for (uint32_t j = 1; j < J; ++j)
-        pts[i - b] = h25519::ge_add(pts[i - b], h25519::ge_from_dev(raw + (i * J + j) * P3_WORDS));
+    if (J == 1) {
+      for (size_t i = b; i < e; ++i) pts[i - b] = h25519::ge_from_dev(raw + i * P3_WORDS);
+    } else {  // the J partials of each point summed eight additions a vector (ge_sum_auto)
+      std::vector<h25519::ge> parts((e - b) * J);
+      for (size_t k = 0; k < parts.size(); ++k) parts[k] = h25519::ge_from_dev(raw + (b * J + k) * P3_WORDS);
+      h25519::ge_sum_auto(parts.data(), e - b, J, pts.data());
     }
     h25519::encode_double_batch_auto(pts.data(), e - b, out_host + 32 * b);
   });

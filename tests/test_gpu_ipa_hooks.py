@@ -141,6 +141,36 @@ def test_ipa_cb_hook_failure_aborts(ctx, gens16):
     assert len(L) == 3 and tr.log == expected_log(n, L, R)
 
 
+def test_ipa_prove_noncanonical_input_then_exact(ctx, gens16):
+    """A non-canonical a, b or factor fails bpp_ipa_prove with
+    BPP_ERR_NONCANONICAL after Q's table build was queued (the call drains it
+    before releasing the Q slot); the next call, with another Q, equals the
+    oracle's proof."""
+    import bpperm
+    rng = Rng(91)
+    n = 16
+    oG, oH = merlin.bulletproof_gens(16)
+    a = [rng.scalar() for _ in range(n)]
+    b = [rng.scalar() for _ in range(n)]
+    hf = [rng.scalar() for _ in range(n)]
+    bad = (r255.L + 3).to_bytes(32, "little")
+    for which in range(3):
+        aa = [sb(x) for x in a]
+        bb = [sb(x) for x in b]
+        hh = [sb(x) for x in hf]
+        (aa, bb, hh)[which][5] = bad
+        with pytest.raises(bpperm.BppError) as ei:
+            gens16.ipa_prove(bpperm.Transcript(b"nc"), r255.encode(rng.point()), None, hh, aa, bb)
+        assert ei.value.name == "BPP_ERR_NONCANONICAL"
+    Q = rng.point()
+    want = bp.ipa_create(merlin.Transcript(b"nc"), Q, [1] * n, hf, oG[:n], oH[:n], a, b)
+    tr = bpperm.Transcript(b"nc")
+    L, R, ga, gb = gens16.ipa_prove(tr, r255.encode(Q), None, [sb(x) for x in hf], [sb(x) for x in a],
+                                    [sb(x) for x in b])
+    tr.close()
+    assert L == want.L and R == want.R and ga == sb(want.a) and gb == sb(want.b)
+
+
 def test_config2_ipa_through_caller_transcript(ctx):
     """Config 2 (n = 2^10 commitment + IPA) with the caller's transcript
     behind the hooks from the first message on: A appended and y drawn by the

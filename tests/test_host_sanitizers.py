@@ -64,3 +64,19 @@ def test_invert_vartime_matches_fermat(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "mismatches: 0" in r.stdout, (r.stdout + r.stderr)[-2000:]
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not installed")
+def test_ge_sum_x8_matches_scalar_chain(tmp_path):
+    """h25519::ge_sum_x8 (the IPA split rounds' J-partial sums on AVX-512
+    IFMA) encodes to the same bytes as one scalar ge_add chain per point, for
+    n = 1..64 points of J = 2..64 terms (identity terms included), under
+    UBSan; skipped inside the program on a CPU without IFMA."""
+    exe = tmp_path / "ge_sum"
+    cmd = ["g++", "-std=c++17", "-O2", "-g", "-march=x86-64-v3", "-fsanitize=undefined", "-fno-sanitize-recover=all",
+           "-I", str(CSRC), str(ROOT / "tests" / "c" / "ge_sum_check.cpp"), str(CSRC / "host" / "encode_x8.cpp"),
+           "-o", str(exe)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "mismatches: 0" in r.stdout, (r.stdout + r.stderr)[-2000:]

@@ -189,14 +189,19 @@ int bpp_vec_commit(bpp_ctx* ctx, const bpp_gens* g, const uint8_t blind[32], con
     MsmPoints pts;
     BPP_TRY(gens_points(ctx, g, &pts));
     // one long MSM alone runs as one block (one wave per SIMD walking ~T/16
-    // terms per lane in a row): cut it into J slices, J blocks side by side,
-    // and add the J results here (config 2's 2049 terms: 16 slices)
-    const uint32_t J = (uint32_t)std::max<size_t>(1, std::min<size_t>(16, T / 128));
+    // terms per lane in a row): cut it into J slices of >= 32 terms, J blocks
+    // side by side, and add the J results here (ge_sum_auto) -- config 2's
+    // 2049 terms: BPP_VC_SPLIT caps J (default 16)
+    static const size_t vc_split = [] {
+      const char* e = getenv("BPP_VC_SPLIT");
+      return (size_t)std::max(1, e ? atoi(e) : 16);
+    }();
+    const uint32_t J = (uint32_t)std::max<size_t>(1, std::min<size_t>(vc_split, T / 32));
     std::vector<uint32_t> off(J + 1);
     for (uint32_t j = 0; j <= J; ++j) off[j] = (uint32_t)((uint64_t)T * j / J);
     BPP_TRY(msm_multi(ctx, d_s, (const uint32_t*)d_i, off, pts, res));
-    h25519::ge acc = res[0];
-    for (uint32_t j = 1; j < J; ++j) acc = h25519::ge_add(acc, res[j]);
+    h25519::ge acc;
+    h25519::ge_sum_auto(res.data(), 1, J, &acc);
     h25519::encode(out, acc);
     return BPP_OK;
   });

@@ -191,10 +191,11 @@ int bpp_vec_commit(bpp_ctx* ctx, const bpp_gens* g, const uint8_t blind[32], con
     // one long MSM alone runs as one block (one wave per SIMD walking ~T/16
     // terms per lane in a row): cut it into J slices of >= 32 terms, J blocks
     // side by side, and add the J results here (ge_sum_auto) -- config 2's
-    // 2049 terms: BPP_VC_SPLIT caps J (default 16)
+    // 2049 terms: BPP_VC_SPLIT caps J (default 64; config 2 at 16 / 32 / 64
+    // slices 1.016-1.024 / 0.996-1.004 / 0.979-0.996 ms, r06_vc_split_ab.txt)
     static const size_t vc_split = [] {
       const char* e = getenv("BPP_VC_SPLIT");
-      return (size_t)std::max(1, e ? atoi(e) : 16);
+      return (size_t)std::max(1, e ? atoi(e) : 64);
     }();
     const uint32_t J = (uint32_t)std::max<size_t>(1, std::min<size_t>(vc_split, T / 32));
     std::vector<uint32_t> off(J + 1);

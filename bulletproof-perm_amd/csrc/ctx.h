@@ -34,6 +34,12 @@ struct bpp_ctx {
   // > 0: ctx_sync spins this many us before it sleeps (SyncSpin, for the
   // latency-bound callers: one IPA, small prover batches); 0 = sleep at once
   unsigned sync_spin_us = 0;
+  // kernel -> host completion flag (ctx_done_flag): a device ticket counter
+  // the last block of a launch resets, a coherent pinned word it then writes
+  // with the launch's tag, and the tag counter
+  uint32_t* done_ticket = nullptr;
+  uint32_t* done_word = nullptr;
+  uint32_t done_tag = 0;
   // profiling
   bool prof = false;
   struct Pend {
@@ -212,6 +218,18 @@ int ctx_sync_latency(bpp_ctx* ctx, unsigned spin_us = 400);
 // Scoped latency mode: ctx_sync on ctx spins `us` before sleeping while the
 // guard lives (a 5-us nanosleep oversleeps by the 50-us default timer slack,
 // which a chain of short kernels and host steps pays at every sync).
+// The completion flag of the next launch (latency paths): *ticket (device,
+// zero between launches) and *word (coherent pinned host memory) for a
+// kernel that ends with done_signal(ticket, word, *tag); ctx_wait_flag then
+// waits for it -- ~6 us of a kernel -> host round trip where an event record
+// and query took ~12.5 (tools/ubench/flagpoll).
+int ctx_done_flag(bpp_ctx* ctx, uint32_t** ticket, uint32_t** word, uint32_t* tag);
+// Waits for *word == tag: spins up to the context's sync_spin_us, then falls
+// back to ctx_sync (which reports a failed launch) and resets the ticket if
+// the flag never came (a launch cut short), so the flag is only ever a
+// shortcut.  Clears nothing ctx_sync would (zc_live, the stage arena).
+int ctx_wait_flag(bpp_ctx* ctx, const uint32_t* word, uint32_t tag);
+
 struct SyncSpin {
   bpp_ctx* c;
   unsigned old;

@@ -216,6 +216,40 @@ int ctx_sync_latency(bpp_ctx* ctx, unsigned spin_us) {
   return BPP_OK;
 }
 
+int ctx_done_flag(bpp_ctx* ctx, uint32_t** ticket, uint32_t** word, uint32_t* tag) {
+  if (!ctx->done_ticket) {
+    BPP_HIP(hipMalloc(&ctx->done_ticket, 4));
+    BPP_HIP(hipMemsetAsync(ctx->done_ticket, 0, 4, ctx->stream));
+  }
+  if (!ctx->done_word) {
+    BPP_HIP(hipHostMalloc((void**)&ctx->done_word, 64, hipHostMallocCoherent));
+    __atomic_store_n(ctx->done_word, 0u, __ATOMIC_RELEASE);
+  }
+  if (++ctx->done_tag == 0) ++ctx->done_tag;  // (0: never a live tag)
+  *ticket = ctx->done_ticket;
+  *word = ctx->done_word;
+  *tag = ctx->done_tag;
+  return BPP_OK;
+}
+
+int ctx_wait_flag(bpp_ctx* ctx, const uint32_t* word, uint32_t tag) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const auto cap = std::chrono::microseconds(ctx->sync_spin_us);
+  while (__atomic_load_n(word, __ATOMIC_ACQUIRE) != tag) {
+    if (std::chrono::steady_clock::now() - t0 >= cap) {
+      BPP_TRY(ctx_sync(ctx));  // the launch has ended (or failed: reported here)
+      if (__atomic_load_n(word, __ATOMIC_ACQUIRE) != tag) {
+        // a launch that ended without its flag (none should): the results
+        // are complete after the sync; re-zero the ticket for the next one
+        BPP_HIP(hipMemsetAsync(ctx->done_ticket, 0, 4, ctx->stream));
+      }
+      return BPP_OK;
+    }
+    __builtin_ia32_pause();
+  }
+  return BPP_OK;
+}
+
 static int stage_take(bpp_ctx* ctx, size_t bytes, uint8_t** out) {
   const size_t need = (bytes + 255) & ~(size_t)255;
   if (ctx->stage_used + need > ctx->stage_cap) {
@@ -505,6 +539,8 @@ void bpp_ctx_destroy(bpp_ctx* ctx) {
   }
   for (auto e : ctx->ev_pool) hipEventDestroy(e);
   if (ctx->sync_ev) hipEventDestroy(ctx->sync_ev);
+  if (ctx->done_ticket) hipFree(ctx->done_ticket);
+  if (ctx->done_word) hipHostFree(ctx->done_word);
   if (ctx->up_sc) hipFree(ctx->up_sc);
   for (auto e : ctx->up_ev)
     if (e) hipEventDestroy(e);

@@ -516,6 +516,23 @@ FE_INLINE void ipa_round_body(const uint32_t* __restrict__ dt, const DtGeom& dg,
   dt_block_tree_segs(lds, acc, nt, S, out_p3, S == 2 ? 2 * inst * J + jp : bidx, J);
 }
 
+// The launch's completion flag (ctx_done_flag / ctx_wait_flag): after the
+// block's results are stored (all by wave 0, whose thread 0 runs this),
+// each block counts itself on the device ticket behind a system-scope
+// release; the last one re-zeroes the ticket and writes the tag to the
+// host's word.  Vector atomics and stores only.
+FE_INLINE void done_signal(uint32_t* ticket, uint32_t* word, uint32_t tag) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    if (atomicAdd(ticket, 1u) == gridDim.x - 1) {
+      atomicExch(ticket, 0u);
+      __threadfence_system();
+      __hip_atomic_store(word, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
     const uint32_t* __restrict__ dt, DtGeom dg, uint32_t n, uint32_t m, uint32_t lg_h, uint32_t fold,
     const uint32_t* __restrict__ am_in, const uint32_t* __restrict__ bm_in, const uint32_t* __restrict__ fG_in,
@@ -523,7 +540,8 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
     uint32_t* __restrict__ fG_out, uint32_t* __restrict__ fH_out, const uint32_t* __restrict__ u,
     const uint32_t* __restrict__ qmul, uint32_t gbase, uint32_t hbase, uint32_t qidx, uint32_t TG, uint32_t halve,
     uint32_t* __restrict__ out_p3, const uint32_t* __restrict__ a0, const uint32_t* __restrict__ b0,
-    const uint32_t* __restrict__ gf0, const uint32_t* __restrict__ hf0, uint32_t init, uint32_t J, uint32_t S) {
+    const uint32_t* __restrict__ gf0, const uint32_t* __restrict__ hf0, uint32_t init, uint32_t J, uint32_t S,
+    uint32_t* done_ticket, uint32_t* done_word, uint32_t done_tag) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   IpaRoundArgs A;
   A.am_in = am_in; A.bm_in = bm_in; A.fG_in = fG_in; A.fH_in = fH_in;
@@ -534,6 +552,7 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
   A.gbase = gbase; A.hbase = hbase; A.qidx = qidx;
   A.split = J;
   ipa_round_body(dt, dg, n, TG, A, blockIdx.x, lds, S);
+  if (done_word) done_signal(done_ticket, done_word, done_tag);
 }
 
 // Several batches' rounds in one launch (BPP_IPA_MERGE, the shared-launch
@@ -856,6 +875,17 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
   }();
   const bool dev_jsum = zc && !merge && J > 1 && J <= 64 && (J & (J - 1)) == 0 && jsum_env;
   void* d_part = nullptr;  // dev_jsum: the round kernel's J partials per MSM
+  // one IPA alone (bpp_ipa_prove: P = 1 on a spinning context) waits for
+  // each round through the kernel's completion flag instead of an event
+  // (ctx_wait_flag; BPP_IPA_FLAG=0 off): config 2 0.92-0.95 vs 0.96-0.99 ms.
+  // Not for prover batches: with 8 sub-batches in flight the busy flag
+  // waits cost the config-4 job 7.5-9.1 vs 7.0-7.2 ms (r06_ipa_flag_ab.txt)
+  static const bool flag_env = [] {
+    const char* e = getenv("BPP_IPA_FLAG");
+    return !e || atoi(e) != 0;
+  }();
+  const bool use_flag = zc && !merge && !dev_jsum && P == 1 && ctx->sync_spin_us > 0 && flag_env;
+  uint32_t *done_ticket = nullptr, *done_word = nullptr, done_tag = 0;
   uint32_t* h_uw = nullptr;  // zc: the challenges' device words, in place
   if (zc) {
     void *hr = nullptr, *hu = nullptr;
@@ -908,6 +938,7 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
         BPP_HIP(hipStreamWaitEvent(ctx->stream, req.done, 0));  // (ctx_sync below then covers the round)
       } else {
         ProfScope ps(ctx, "ipa_round_dt");  // (bench.py: this kernel's own roofline)
+        if (use_flag) BPP_TRY(ctx_done_flag(ctx, &done_ticket, &done_word, &done_tag));
         hipLaunchKernelGGL(k_ipa_round_dt, dim3(2 / sides * P * J), dim3(sides * nt),
                            ipa_round_lds_words(n, sides * nt, sides) * 4,
                            ctx->stream,
@@ -915,7 +946,8 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
                            S[round ? outs : in][0], S[round ? outs : in][1], S[round ? outs : in][2],
                            S[round ? outs : in][3], (const uint32_t*)d_u, (const uint32_t*)d_q, g.gbase, g.hbase,
                            g.qidx, TG, dev_merlin ? 0u : 1u, (uint32_t*)(dev_jsum ? d_part : d_res), d_a, d_b,
-                           d_Gf, d_Hf, round ? 0u : 1u, J, sides);
+                           d_Gf, d_Hf, round ? 0u : 1u, J, sides, done_ticket, use_flag ? done_word : nullptr,
+                           done_tag);
         if (dev_jsum)
           hipLaunchKernelGGL(k_ipa_jsum, dim3(2 * P), dim3(J), (size_t)J * P3_BYTES, ctx->stream,
                              (const uint32_t*)d_part, J, (uint32_t*)d_res);
@@ -941,7 +973,11 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
         HostScope hs(ctx, "ipa_msm");
         {
           HostScope hw(ctx, "ipa_wait");
-          BPP_TRY(ctx_sync(ctx));  // the kernel's L/2, R/2 are in host memory now
+          // the kernel's L/2, R/2 are in host memory now
+          if (use_flag && !merge)
+            BPP_TRY(ctx_wait_flag(ctx, done_word, done_tag));
+          else
+            BPP_TRY(ctx_sync(ctx));
         }
         BPP_TRY(points_double_encode_host(ctx, (const uint32_t*)d_res, 2 * (size_t)P, enc.data(), dev_jsum ? 1 : J));
       } else {

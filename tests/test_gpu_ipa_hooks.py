@@ -211,3 +211,18 @@ def test_config2_ipa_through_caller_transcript(ctx):
             assert g.ipa_verify(tv, n, None, hf, P, Q, L, R, av, b) == (tamper == 0)
     finally:
         g.close()
+
+
+def test_config2_flag_wait_fallback_subprocess():
+    """The rounds' completion-flag wait with a 1-us spin budget
+    (BPP_IPA_SPIN_US=1): every round falls back to the event wait after the
+    flag spin, and config 2 still equals its golden (bench_config2's check),
+    in a child process so the environment is read fresh."""
+    import os
+    import subprocess
+    root = Path(__file__).resolve().parent.parent
+    env = dict(os.environ, BPP_IPA_SPIN_US="1")
+    r = subprocess.run([sys.executable, str(root / "tools" / "config2_once.py"), "3"], capture_output=True, text=True,
+                       timeout=180, env=env, cwd=str(root))
+    assert r.returncode == 0, (r.stdout + r.stderr)[-2000:]
+    assert r.stdout.strip().split()[-1] == "True", r.stdout[-500:]

@@ -95,8 +95,8 @@ struct DtLane {
 // multiplies).  A zero digit adds the identity (no divergent skip).
 template <class Src>
 FE_INLINE ge_p3 dt_walk(const uint32_t* __restrict__ dt, const DtGeom& dg, const DtLane& ln, uint32_t t, uint32_t t1,
-                        uint32_t TG, const Src& src) {
-  ge_p3 acc = ge_identity();
+                        uint32_t TG, const Src& src, const ge_p3& acc0 = ge_identity()) {
+  ge_p3 acc = acc0;  // (a lane's starting point: the identity, or an extra term's point)
   if (t >= t1) return acc;
   uint32_t sc[8];
   uint32_t gen;

@@ -20,6 +20,10 @@ struct IpaGens {
   uint32_t gbase = 0, hbase = 0;     // G_i at gbase + i, H_i at hbase + i
   uint32_t qidx = 0;                 // Q = qmul * P[qidx]
   hsc::Sc qmul = hsc::one();
+  // non-null: Q given as its 253 doublings 2^j Q (device P3 rows) instead of
+  // a generator: the fused rounds add c Q bit by bit, one lane per bit, into
+  // the block tree (no per-call Q table; qidx / qmul unused)
+  const uint32_t* qpow = nullptr;
 };
 
 typedef std::array<uint8_t, 32> Enc32;

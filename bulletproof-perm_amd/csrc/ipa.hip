@@ -244,13 +244,33 @@ struct IpaRoundArgs {
   uint32_t m, lg_h, fold, init, halve, gbase, hbase, qidx;
   uint32_t blocks;  // 2 P J (k_ipa_round_dt_multi)
   uint32_t split;   // J: blocks per L / R MSM, each walking a slice of its n + 1 terms
+  const uint32_t* qpow;  // IpaGens::qpow (null: Q's term walked from its table rows)
 };
+
+// c Q for the Q term's scalar c (8 canonical words in LDS) with Q given as
+// qpow[j] = 2^j Q: lane lt of a side's ns lanes owns bits b = lt, lt + ns,
+// ... < 253.  Its first bit's point (2^lt Q or the identity) is where the
+// lane's walk starts (dt_walk's acc0: no extra addition, the load overlaps
+// the walk's first row), further bits (ns < 253 only) are added after, and
+// the block tree sums the lanes -- where a per-call direct table for Q cost
+// a 152-us build (bpp_ipa_prove, config 2).
+FE_INLINE bool q_bit(const uint32_t* qsc, uint32_t b) { return (qsc[b >> 5] >> (b & 31)) & 1u; }
+FE_INLINE ge_p3 q_bits_first(const uint32_t* __restrict__ qpow, const uint32_t* qsc, uint32_t lt) {
+  return lt < 253 && q_bit(qsc, lt) ? load_p3(qpow, lt) : ge_identity();
+}
+FE_INLINE ge_p3 q_bits_rest(ge_p3 acc, const uint32_t* __restrict__ qpow, const uint32_t* qsc, uint32_t lt,
+                            uint32_t ns) {
+  for (uint32_t b = lt + ns; b < 253; b += ns)
+    if (q_bit(qsc, b)) acc = ge_add(acc, load_p3(qpow, b));
+  return acc;
+}
 
 // S = sides per block: 1 (block bidx = MSM bidx / J's slice, L or R) or 2
 // (block bidx = instance bidx / J's slice, lanes [0, nt/2) walking its L and
 // [nt/2, nt) its R): the two sides share the fold and the term scalars,
 // which a pair of one-sided blocks each compute in full, and their block
 // trees run side by side (BPP_IPA_LR, large batches).
+template <bool QP>  // QP: Q by its doublings (A.qpow), a separate instantiation (VGPRs)
 FE_INLINE void ipa_round_body(const uint32_t* __restrict__ dt, const DtGeom& dg, uint32_t n, uint32_t TG,
                               const IpaRoundArgs& A, uint32_t bidx, uint32_t* lds, uint32_t S) {
   const uint32_t m = A.m, lg_h = A.lg_h, fold = A.fold, init = A.init, halve = A.halve, gbase = A.gbase,
@@ -401,13 +421,16 @@ FE_INLINE void ipa_round_body(const uint32_t* __restrict__ dt, const DtGeom& dg,
     const DtLane ln = DtLane::make(dg, lt % dg.W);
     const uint32_t* __restrict__ tscs = tsl + 8 * ls * CS;
     const uint32_t* __restrict__ tgens = tgl + ls * CS;
-    const ge_p3 acc = tg < TG ? dt_walk(dt, dg, ln, tg, CS, TG,
-                                        [&](uint32_t t, uint32_t sv[8], uint32_t& gen) {
-                                          const sc v = sc_load(tscs + 8 * t);
-                                          _Pragma("unroll") for (int i = 0; i < 8; ++i) sv[i] = v.v[i];
-                                          gen = tgens[t];
-                                        })
-                              : ge_identity();
+    // (QP: every slice adds its own share of c Q by bits, slot cnt not walked)
+    const ge_p3 acc0 = QP ? q_bits_first(A.qpow, tscs + 8 * cnt, lt) : ge_identity();
+    ge_p3 acc = tg < TG ? dt_walk(dt, dg, ln, tg, QP ? cnt : CS, TG,
+                                  [&](uint32_t t, uint32_t sv[8], uint32_t& gen) {
+                                    const sc v = sc_load(tscs + 8 * t);
+                                    _Pragma("unroll") for (int i = 0; i < 8; ++i) sv[i] = v.v[i];
+                                    gen = tgens[t];
+                                  }, acc0)
+                        : acc0;
+    if (QP && ns < 253) acc = q_bits_rest(acc, A.qpow, tscs + 8 * cnt, lt, ns);
     __syncthreads();
     dt_block_tree_segs(lds, acc, nt, S, out_p3, S == 2 ? 2 * inst * J + jp : bidx, J);
     return;
@@ -500,13 +523,17 @@ FE_INLINE void ipa_round_body(const uint32_t* __restrict__ dt, const DtGeom& dg,
   return;
 #endif
   const uint32_t t0 = (uint32_t)((uint64_t)jp * NS / J), t1 = (uint32_t)((uint64_t)(jp + 1) * NS / J);
-  const ge_p3 acc = tg < TG ? dt_walk(dt, dg, ln, t0 + tg, t1, TG,
-                                      [&](uint32_t t, uint32_t s[8], uint32_t& gen) {
-                                        const sc v = sc_load(tscs + 8 * t);
-                                        _Pragma("unroll") for (int i = 0; i < 8; ++i) s[i] = v.v[i];
-                                        gen = tgens[t];
-                                      })
-                            : ge_identity();
+  // (QP: the Q term, slot n, is added by bits in the slice holding it)
+  const bool qhere = QP && t1 > n;
+  const ge_p3 acc0 = qhere ? q_bits_first(A.qpow, tscs + 8 * n, lt) : ge_identity();
+  ge_p3 acc = tg < TG ? dt_walk(dt, dg, ln, t0 + tg, QP ? min(t1, n) : t1, TG,
+                                [&](uint32_t t, uint32_t s[8], uint32_t& gen) {
+                                  const sc v = sc_load(tscs + 8 * t);
+                                  _Pragma("unroll") for (int i = 0; i < 8; ++i) s[i] = v.v[i];
+                                  gen = tgens[t];
+                                }, acc0)
+                      : acc0;
+  if (qhere && ns < 253) acc = q_bits_rest(acc, A.qpow, tscs + 8 * n, lt, ns);
   __syncthreads();
 #ifdef EXP_IPA_NOTREE  // timing experiment only (wrong results): no block tree
   if (lt == 0) store_p3(out_p3, S == 2 ? (2 * inst + ls) * J + jp : bidx, acc);
@@ -533,6 +560,7 @@ FE_INLINE void done_signal(uint32_t* ticket, uint32_t* word, uint32_t tag) {
   }
 }
 
+template <bool QP>
 __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
     const uint32_t* __restrict__ dt, DtGeom dg, uint32_t n, uint32_t m, uint32_t lg_h, uint32_t fold,
     const uint32_t* __restrict__ am_in, const uint32_t* __restrict__ bm_in, const uint32_t* __restrict__ fG_in,
@@ -541,7 +569,7 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
     const uint32_t* __restrict__ qmul, uint32_t gbase, uint32_t hbase, uint32_t qidx, uint32_t TG, uint32_t halve,
     uint32_t* __restrict__ out_p3, const uint32_t* __restrict__ a0, const uint32_t* __restrict__ b0,
     const uint32_t* __restrict__ gf0, const uint32_t* __restrict__ hf0, uint32_t init, uint32_t J, uint32_t S,
-    uint32_t* done_ticket, uint32_t* done_word, uint32_t done_tag) {
+    const uint32_t* __restrict__ qpow, uint32_t* done_ticket, uint32_t* done_word, uint32_t done_tag) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   IpaRoundArgs A;
   A.am_in = am_in; A.bm_in = bm_in; A.fG_in = fG_in; A.fH_in = fH_in;
@@ -551,7 +579,8 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
   A.m = m; A.lg_h = lg_h; A.fold = fold; A.init = init; A.halve = halve;
   A.gbase = gbase; A.hbase = hbase; A.qidx = qidx;
   A.split = J;
-  ipa_round_body(dt, dg, n, TG, A, blockIdx.x, lds, S);
+  A.qpow = qpow;
+  ipa_round_body<QP>(dt, dg, n, TG, A, blockIdx.x, lds, S);
   if (done_word) done_signal(done_ticket, done_word, done_tag);
 }
 
@@ -573,7 +602,7 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt_multi(const uint32_t
     sb = b;
   }
   __syncthreads();
-  ipa_round_body(dt, dg, n, TG, sA, sb, lds, 1);
+  ipa_round_body<false>(dt, dg, n, TG, sA, sb, lds, 1);  // (the merged launches never carry qpow)
 }
 
 // The shared-launch round scheduler (BPP_IPA_MERGE=1; an
@@ -781,6 +810,10 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
   // tables: the state (a, b, fG, fH) alternates between two sets so that a
   // round's blocks read the previous state while side 0 writes the next.
   const bool fused = n >= 2 && n <= IPA_FUSED_NMAX && !g.pts.tbl1 && msm_use_dt(g.pts, 2 * P, (uint32_t)PT);
+  if (g.qpow && !fused) {  // (only the fused rounds add Q by its doublings)
+    ctx->err = "ipa: Q as doublings needs the fused direct-table rounds";
+    return BPP_ERR_ARG;
+  }
   if (!fused) {  // (the fused first round converts the inputs itself)
     hipLaunchKernelGGL(k_ipa_init, dim3(grid_for(PN, 256)), dim3(256), 0, ctx->stream, n, P, d_a, d_b, d_Gf, d_Hf,
                        (uint32_t*)am, (uint32_t*)bm, (uint32_t*)fG, (uint32_t*)fH);
@@ -836,7 +869,7 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
     const char* e = getenv("BPP_IPA_MERGE");
     return e && atoi(e) != 0;
   }();
-  const bool merge = merge_env && zc;
+  const bool merge = merge_env && zc && !g.qpow;
   // J blocks per L / R MSM when the batch is small (config 2: P = 1, two
   // blocks of one wave per SIMD walking ~64 of the 1025 terms per lane in a
   // row): each block walks a slice of the terms and the host adds the J
@@ -926,6 +959,7 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
         A.gbase = g.gbase; A.hbase = g.hbase; A.qidx = g.qidx;
         A.blocks = 2 * P * J;
         A.split = J;
+        A.qpow = g.qpow;
         req.dt = g.pts.dt;
         req.dg = dg;
         req.n = n;
@@ -939,15 +973,16 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
       } else {
         ProfScope ps(ctx, "ipa_round_dt");  // (bench.py: this kernel's own roofline)
         if (use_flag) BPP_TRY(ctx_done_flag(ctx, &done_ticket, &done_word, &done_tag));
-        hipLaunchKernelGGL(k_ipa_round_dt, dim3(2 / sides * P * J), dim3(sides * nt),
+        hipLaunchKernelGGL(g.qpow ? k_ipa_round_dt<true> : k_ipa_round_dt<false>, dim3(2 / sides * P * J),
+                           dim3(sides * nt),
                            ipa_round_lds_words(n, sides * nt, sides) * 4,
                            ctx->stream,
                            g.pts.dt, dg, n, m, lg_h, round ? 1u : 0u, S[in][0], S[in][1], S[in][2], S[in][3],
                            S[round ? outs : in][0], S[round ? outs : in][1], S[round ? outs : in][2],
                            S[round ? outs : in][3], (const uint32_t*)d_u, (const uint32_t*)d_q, g.gbase, g.hbase,
                            g.qidx, TG, dev_merlin ? 0u : 1u, (uint32_t*)(dev_jsum ? d_part : d_res), d_a, d_b,
-                           d_Gf, d_Hf, round ? 0u : 1u, J, sides, done_ticket, use_flag ? done_word : nullptr,
-                           done_tag);
+                           d_Gf, d_Hf, round ? 0u : 1u, J, sides, g.qpow, done_ticket,
+                           use_flag ? done_word : nullptr, done_tag);
         if (dev_jsum)
           hipLaunchKernelGGL(k_ipa_jsum, dim3(2 * P), dim3(J), (size_t)J * P3_BYTES, ctx->stream,
                              (const uint32_t*)d_part, J, (uint32_t*)d_res);

@@ -271,6 +271,40 @@ int ipa_q_slot(bpp_ctx* ctx, const bpp_gens* g, const uint8_t Q[32], uint32_t dt
                          hipMemcpyDeviceToDevice, ctx->stream));
   return BPP_OK;
 }
+// host extended point -> the device's P3 row (40 words: X, Y, Z, T in 10
+// limbs at bit offsets ceil(25.5 i), ge_io.cuh load_p3; canonical limbs)
+void p3_row_host(const h25519::ge& p, uint32_t w[P3_WORDS]) {
+  const h25519::fe* c = &p.X;
+  for (int e = 0; e < 4; ++e) {
+    const h25519::fe f = h25519::fe_canon(c[e]);
+    for (int k = 0; k < 5; ++k) {
+      w[10 * e + 2 * k] = (uint32_t)(f.v[k] & 0x3ffffffu);
+      w[10 * e + 2 * k + 1] = (uint32_t)(f.v[k] >> 26);
+    }
+  }
+}
+
+// Q as its doublings 2^j Q, j < 253, in device memory (IpaGens::qpow): the
+// fused rounds add c Q bit by bit inside their block trees, so no per-call
+// table is built for Q and g's Q slot (and its lock) is not used.  253
+// doublings on the host (the Q slot's window points took 248 of them).
+int ipa_q_powers(bpp_ctx* ctx, const uint8_t Q[32], const uint32_t** d_out) {
+  h25519::ge P;
+  if (!h25519::decode(P, Q)) {
+    ctx->err = "Q does not decode";
+    return BPP_ERR_DECOMPRESS;
+  }
+  std::vector<uint32_t> rows((size_t)253 * P3_WORDS);
+  for (uint32_t j = 0; j < 253; ++j) {
+    p3_row_host(P, &rows[(size_t)j * P3_WORDS]);
+    P = h25519::ge_dbl(P);
+  }
+  void* d = nullptr;
+  BPP_TRY(ctx_ws(ctx, "ipa_qpow", rows.size() * 4, &d));
+  BPP_TRY(ctx_h2d(ctx, d, rows.data(), rows.size() * 4));
+  *d_out = (const uint32_t*)d;
+  return BPP_OK;
+}
 }  // namespace
 
 static int ipa_prove_api(bpp_ctx* ctx, const bpp_gens* g, IpaTranscript* tr, const uint8_t Q[32],
@@ -305,11 +339,22 @@ static int ipa_prove_api(bpp_ctx* ctx, const bpp_gens* g, IpaTranscript* tr, con
     bool zc_in = false;
     IpaZcWipe wipe(ctx);  // (destroyed before qlock: the drain below runs first)
     IpaProofHost pf;
+    // Q in the fused rounds: by its doublings (IpaGens::qpow, default) or in
+    // g's Q slot with a per-call direct table (BPP_IPA_QPOW=0)
+    static const bool qpow_env = [] {
+      const char* e = getenv("BPP_IPA_QPOW");
+      return !e || atoi(e) != 0;
+    }();
     auto body = [&]() -> int {
       if (qslot) {
-        qlock = std::unique_lock<std::mutex>(g->q_mu);
-        BPP_TRY(ipa_q_slot(ctx, g, Q, ig.pts.dt_c));
-        ig.qidx = g->qslot();
+        if (qpow_env) {
+          BPP_TRY(ipa_q_powers(ctx, Q, &ig.qpow));
+          ig.qidx = 0;  // (unused with qpow)
+        } else {
+          qlock = std::unique_lock<std::mutex>(g->q_mu);
+          BPP_TRY(ipa_q_slot(ctx, g, Q, ig.pts.dt_c));
+          ig.qidx = g->qslot();
+        }
         static const bool zc_env = [] {
           const char* e = getenv("BPP_IPA_ZC_IN");
           return !e || atoi(e) != 0;

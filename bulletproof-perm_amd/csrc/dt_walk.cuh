@@ -85,6 +85,24 @@ struct DtLane {
     neg = d < 0;
     row = (gen * W + w) * H + (zero ? 0u : ad - 1u);
   }
+  // (VQ walks) a virtual term gen = 2^31 | v: lane w adds row qrow0 + b,
+  // b = v W + w, when bit b of the term's scalar is set -- the 253 doublings
+  // 2^b Q of a point with no direct table, as Niels rows from qrow0
+  FE_INLINE void row_of_q(const uint32_t sc[8], uint32_t gen, uint32_t qrow0, uint32_t& row, bool& neg,
+                          bool& zero) const {
+    const uint32_t b = (gen & 0xffffu) * W + w;
+    zero = b >= 253u || !((sel8(sc, b >> 5) >> (b & 31)) & 1u);
+    neg = false;
+    row = qrow0 + (b < 253u ? b : 0u);
+  }
+  template <bool VQ>
+  FE_INLINE void row_any(const DtGeom& g, const uint32_t sc[8], uint32_t gen, uint32_t qrow0, uint32_t& row,
+                         bool& neg, bool& zero) const {
+    if (VQ && (gen >> 31))
+      row_of_q(sc, gen, qrow0, row, neg, zero);
+    else
+      row_of(g, sc, gen, row, neg, zero);
+  }
 };
 
 // One lane's walk over terms t, t + TG, ... < t1 (src(t, s, gen) supplies
@@ -93,9 +111,10 @@ struct DtLane {
 // ahead, and the next term's 128-B table row is gathered between the two
 // halves of the current addition (the operand is dead after its first three
 // multiplies).  A zero digit adds the identity (no divergent skip).
-template <class Src>
+// VQ: terms may be virtual (DtLane::row_of_q, rows from qrow0).
+template <bool VQ = false, class Src>
 FE_INLINE ge_p3 dt_walk(const uint32_t* __restrict__ dt, const DtGeom& dg, const DtLane& ln, uint32_t t, uint32_t t1,
-                        uint32_t TG, const Src& src, const ge_p3& acc0 = ge_identity()) {
+                        uint32_t TG, const Src& src, const ge_p3& acc0 = ge_identity(), uint32_t qrow0 = 0) {
   ge_p3 acc = acc0;  // (a lane's starting point: the identity, or an extra term's point)
   if (t >= t1) return acc;
   uint32_t sc[8];
@@ -107,7 +126,7 @@ FE_INLINE ge_p3 dt_walk(const uint32_t* __restrict__ dt, const DtGeom& dg, const
   if (tn < t1) src(tn, scn, genn);
   uint32_t row;
   bool neg, zero;
-  ln.row_of(dg, sc, gen, row, neg, zero);
+  ln.row_any<VQ>(dg, sc, gen, qrow0, row, neg, zero);
   ge_niels q = load_niels(dt, row);
   for (;;) {
     if (zero) q = ge_niels_identity();
@@ -116,7 +135,7 @@ FE_INLINE ge_p3 dt_walk(const uint32_t* __restrict__ dt, const DtGeom& dg, const
     bool neg2 = false, zero2 = false;
     if (more) {
       uint32_t row2;
-      ln.row_of(dg, scn, genn, row2, neg2, zero2);
+      ln.row_any<VQ>(dg, scn, genn, qrow0, row2, neg2, zero2);
       q = load_niels(dt, row2);
       tn += TG;
       if (tn < t1) src(tn, scn, genn);

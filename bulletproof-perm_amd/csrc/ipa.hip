@@ -245,31 +245,15 @@ struct IpaRoundArgs {
   uint32_t blocks;  // 2 P J (k_ipa_round_dt_multi)
   uint32_t split;   // J: blocks per L / R MSM, each walking a slice of its n + 1 terms
   const uint32_t* qpow;  // IpaGens::qpow (null: Q's term walked from its table rows)
+  uint32_t qrow0;        // qpow's first row as a row of dt (the virtual terms' rows)
 };
 
-// c Q for the Q term's scalar c (8 canonical words in LDS) with Q given as
-// qpow[j] = 2^j Q: lane lt of a side's ns lanes owns bits b = lt, lt + ns,
-// ... < 253.  Its first bit's point (2^lt Q or the identity) is where the
-// lane's walk starts (dt_walk's acc0: no extra addition, the load overlaps
-// the walk's first row), further bits (ns < 253 only) are added after, and
-// the block tree sums the lanes -- where a per-call direct table for Q cost
-// a 152-us build (bpp_ipa_prove, config 2).
-FE_INLINE bool q_bit(const uint32_t* qsc, uint32_t b) { return (qsc[b >> 5] >> (b & 31)) & 1u; }
-FE_INLINE ge_p3 q_bits_first(const uint32_t* __restrict__ qpow, const uint32_t* qsc, uint32_t lt) {
-  return lt < 253 && q_bit(qsc, lt) ? load_p3(qpow, lt) : ge_identity();
-}
-FE_INLINE ge_p3 q_bits_rest(ge_p3 acc, const uint32_t* __restrict__ qpow, const uint32_t* qsc, uint32_t lt,
-                            uint32_t ns) {
-  for (uint32_t b = lt + ns; b < 253; b += ns)
-    if (q_bit(qsc, b)) acc = ge_add(acc, load_p3(qpow, b));
-  return acc;
-}
-
-// S = sides per block: 1 (block bidx = MSM bidx / J's slice, L or R) or 2
-// (block bidx = instance bidx / J's slice, lanes [0, nt/2) walking its L and
-// [nt/2, nt) its R): the two sides share the fold and the term scalars,
-// which a pair of one-sided blocks each compute in full, and their block
-// trees run side by side (BPP_IPA_LR, large batches).
+// QP (IpaGens::qpow): c Q for the Q term's scalar c with Q given as its 253
+// doublings 2^j Q, Niels rows inside dt from row qrow0 (no per-call direct
+// table for Q, whose build cost 152 us of bpp_ipa_prove in config 2): the
+// Q term becomes V = ceil(253 / W) virtual terms carrying c, and lane w of
+// virtual term v adds 2^(vW + w) Q when that bit of c is set
+// (DtLane::row_of_q) -- walked like any other term.
 template <bool QP>  // QP: Q by its doublings (A.qpow), a separate instantiation (VGPRs)
 FE_INLINE void ipa_round_body(const uint32_t* __restrict__ dt, const DtGeom& dg, uint32_t n, uint32_t TG,
                               const IpaRoundArgs& A, uint32_t bidx, uint32_t* lds, uint32_t S) {
@@ -290,7 +274,8 @@ FE_INLINE void ipa_round_body(const uint32_t* __restrict__ dt, const DtGeom& dg,
   const uint32_t* __restrict__ b0 = A.b0;
   const uint32_t* __restrict__ gf0 = A.gf0;
   const uint32_t* __restrict__ hf0 = A.hf0;
-  const uint32_t NS = n + 1;                     // term slots per side
+  const uint32_t VQ = QP ? (253u + dg.W - 1) / dg.W : 1u;  // Q term slots: 1, or QP's V virtual terms
+  const uint32_t NS = n + VQ;                    // term slots per side
   uint32_t* tsc = lds;                           // S x (n + 1) x 8 words: halved term scalars
   uint32_t* tgen = lds + 8 * S * NS;             // S x (n + 1) generator indices
   uint32_t* sa = tgen + ((S * NS + 3) & ~3u);    // m x 8: a (Montgomery), this round
@@ -380,7 +365,7 @@ FE_INLINE void ipa_round_body(const uint32_t* __restrict__ dt, const DtGeom& dg,
     // (ii) the slice's term scalars: side slots [t0, t1) of [0, n) (G terms
     // below n / 2, H terms above), local slot cnt = the Q term
     const uint32_t t0 = (uint32_t)((uint64_t)jp * n / J), t1 = (uint32_t)((uint64_t)(jp + 1) * n / J);
-    const uint32_t cnt = t1 - t0, CS = cnt + 1;
+    const uint32_t cnt = t1 - t0, CS = cnt + VQ;
     uint32_t* tsl = lds;                            // S x CS x 8 words
     uint32_t* tgl = lds + 8 * S * CS;               // S x CS
     uint32_t* redl = tgl + ((S * CS + 3) & ~3u);    // S x waves x 8 words
@@ -408,12 +393,13 @@ FE_INLINE void ipa_round_body(const uint32_t* __restrict__ dt, const DtGeom& dg,
       if ((tid & 63u) == 0) sc_store(redl + 8 * (s * nwv + (tid >> 6)), c);
     }
     __syncthreads();
-    if (tid < S) {
+    if (tid < S * VQ) {  // (QP: the same scalar in each of the V virtual terms)
+      const uint32_t s = tid / VQ, v = tid - s * VQ;
       sc t = sc_zero();
-      for (uint32_t wv = 0; wv < nwv; ++wv) t = sc_add(t, sc_load(redl + 8 * (tid * nwv + wv)));
+      for (uint32_t wv = 0; wv < nwv; ++wv) t = sc_add(t, sc_load(redl + 8 * (s * nwv + wv)));
       const sc cq = sc_mont(t, sc_load(qmul + 8 * inst));
-      sc_store(tsl + 8 * (tid * CS + cnt), halve ? sc_half(cq) : cq);
-      tgl[tid * CS + cnt] = qidx;
+      sc_store(tsl + 8 * (s * CS + cnt + v), halve ? sc_half(cq) : cq);
+      tgl[s * CS + cnt + v] = QP ? 0x80000000u | v : qidx;
     }
     __syncthreads();
     const uint32_t ns = nt / S, ls = tid / ns, lt = tid - ls * ns;
@@ -421,16 +407,15 @@ FE_INLINE void ipa_round_body(const uint32_t* __restrict__ dt, const DtGeom& dg,
     const DtLane ln = DtLane::make(dg, lt % dg.W);
     const uint32_t* __restrict__ tscs = tsl + 8 * ls * CS;
     const uint32_t* __restrict__ tgens = tgl + ls * CS;
-    // (QP: every slice adds its own share of c Q by bits, slot cnt not walked)
-    const ge_p3 acc0 = QP ? q_bits_first(A.qpow, tscs + 8 * cnt, lt) : ge_identity();
-    ge_p3 acc = tg < TG ? dt_walk(dt, dg, ln, tg, QP ? cnt : CS, TG,
-                                  [&](uint32_t t, uint32_t sv[8], uint32_t& gen) {
-                                    const sc v = sc_load(tscs + 8 * t);
-                                    _Pragma("unroll") for (int i = 0; i < 8; ++i) sv[i] = v.v[i];
-                                    gen = tgens[t];
-                                  }, acc0)
-                        : acc0;
-    if (QP && ns < 253) acc = q_bits_rest(acc, A.qpow, tscs + 8 * cnt, lt, ns);
+    // (QP: every slice walks its own share of c Q as the V virtual terms)
+    const ge_p3 acc = tg < TG ? dt_walk<QP>(dt, dg, ln, tg, CS, TG,
+                                            [&](uint32_t t, uint32_t sv[8], uint32_t& gen) {
+                                              const sc v = sc_load(tscs + 8 * t);
+                                              _Pragma("unroll") for (int i = 0; i < 8; ++i) sv[i] = v.v[i];
+                                              gen = tgens[t];
+                                            },
+                                            ge_identity(), A.qrow0)
+                              : ge_identity();
     __syncthreads();
     dt_block_tree_segs(lds, acc, nt, S, out_p3, S == 2 ? 2 * inst * J + jp : bidx, J);
     return;
@@ -504,12 +489,13 @@ FE_INLINE void ipa_round_body(const uint32_t* __restrict__ dt, const DtGeom& dg,
     if ((tid & 63u) == 0) sc_store(red + 8 * (s * nwv + (tid >> 6)), c);
   }
   __syncthreads();
-  if (tid < S) {
+  if (tid < S * VQ) {  // (QP: the same scalar in each of the V virtual terms)
+    const uint32_t s = tid / VQ, v = tid - s * VQ;
     sc t = sc_zero();
-    for (uint32_t wv = 0; wv < nwv; ++wv) t = sc_add(t, sc_load(red + 8 * (tid * nwv + wv)));
+    for (uint32_t wv = 0; wv < nwv; ++wv) t = sc_add(t, sc_load(red + 8 * (s * nwv + wv)));
     const sc cq = sc_mont(t, sc_load(qmul + 8 * inst));  // Montgomery c * canonical q
-    sc_store(tsc + 8 * (tid * NS + n), halve ? sc_half(cq) : cq);
-    tgen[tid * NS + n] = qidx;
+    sc_store(tsc + 8 * (s * NS + n + v), halve ? sc_half(cq) : cq);
+    tgen[s * NS + n + v] = QP ? 0x80000000u | v : qidx;
   }
   __syncthreads();
   // 3. direct-table walk over the LDS terms, then the block tree (reusing LDS)
@@ -523,17 +509,14 @@ FE_INLINE void ipa_round_body(const uint32_t* __restrict__ dt, const DtGeom& dg,
   return;
 #endif
   const uint32_t t0 = (uint32_t)((uint64_t)jp * NS / J), t1 = (uint32_t)((uint64_t)(jp + 1) * NS / J);
-  // (QP: the Q term, slot n, is added by bits in the slice holding it)
-  const bool qhere = QP && t1 > n;
-  const ge_p3 acc0 = qhere ? q_bits_first(A.qpow, tscs + 8 * n, lt) : ge_identity();
-  ge_p3 acc = tg < TG ? dt_walk(dt, dg, ln, t0 + tg, QP ? min(t1, n) : t1, TG,
-                                [&](uint32_t t, uint32_t s[8], uint32_t& gen) {
-                                  const sc v = sc_load(tscs + 8 * t);
-                                  _Pragma("unroll") for (int i = 0; i < 8; ++i) s[i] = v.v[i];
-                                  gen = tgens[t];
-                                }, acc0)
-                      : acc0;
-  if (qhere && ns < 253) acc = q_bits_rest(acc, A.qpow, tscs + 8 * n, lt, ns);
+  const ge_p3 acc = tg < TG ? dt_walk<QP>(dt, dg, ln, t0 + tg, t1, TG,
+                                          [&](uint32_t t, uint32_t s[8], uint32_t& gen) {
+                                            const sc v = sc_load(tscs + 8 * t);
+                                            _Pragma("unroll") for (int i = 0; i < 8; ++i) s[i] = v.v[i];
+                                            gen = tgens[t];
+                                          },
+                                          ge_identity(), A.qrow0)
+                            : ge_identity();
   __syncthreads();
 #ifdef EXP_IPA_NOTREE  // timing experiment only (wrong results): no block tree
   if (lt == 0) store_p3(out_p3, S == 2 ? (2 * inst + ls) * J + jp : bidx, acc);
@@ -580,6 +563,7 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
   A.gbase = gbase; A.hbase = hbase; A.qidx = qidx;
   A.split = J;
   A.qpow = qpow;
+  A.qrow0 = qpow ? (uint32_t)((size_t)(qpow - dt) / MSM_NIELS_WORDS) : 0u;  // (qpow lies inside dt)
   ipa_round_body<QP>(dt, dg, n, TG, A, blockIdx.x, lds, S);
   if (done_word) done_signal(done_ticket, done_word, done_tag);
 }
@@ -720,8 +704,8 @@ int merger_submit(bpp_ctx* ctx, IpaMergeReq& req) {
 
 // LDS words of k_ipa_round_dt: terms + indices + a, b + wave partials, or
 // the block tree, whichever is larger
-static size_t ipa_round_lds_words(uint32_t n, uint32_t nt, uint32_t S = 1) {
-  const size_t NS = (size_t)S * (n + 1);
+static size_t ipa_round_lds_words(uint32_t n, uint32_t nt, uint32_t S = 1, uint32_t vq = 1) {
+  const size_t NS = (size_t)S * (n + vq);  // (vq: the Q term's slots, ipa_round_body VQ)
   const size_t prologue = 8 * NS + ((NS + 3) & ~(size_t)3) + 16 * (size_t)n + 8 * (size_t)S * ((nt + 63) / 64);
   return std::max(prologue, (size_t)nt * P3_WORDS);
 }
@@ -960,6 +944,7 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
         A.blocks = 2 * P * J;
         A.split = J;
         A.qpow = g.qpow;
+        A.qrow0 = 0;  // (merged launches never carry qpow: merge is off with it)
         req.dt = g.pts.dt;
         req.dg = dg;
         req.n = n;
@@ -975,7 +960,7 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
         if (use_flag) BPP_TRY(ctx_done_flag(ctx, &done_ticket, &done_word, &done_tag));
         hipLaunchKernelGGL(g.qpow ? k_ipa_round_dt<true> : k_ipa_round_dt<false>, dim3(2 / sides * P * J),
                            dim3(sides * nt),
-                           ipa_round_lds_words(n, sides * nt, sides) * 4,
+                           ipa_round_lds_words(n, sides * nt, sides, g.qpow ? (253u + dg.W - 1) / dg.W : 1u) * 4,
                            ctx->stream,
                            g.pts.dt, dg, n, m, lg_h, round ? 1u : 0u, S[in][0], S[in][1], S[in][2], S[in][3],
                            S[round ? outs : in][0], S[round ? outs : in][1], S[round ? outs : in][2],

@@ -9,6 +9,7 @@
 #include "ge_io.cuh"
 #include "ipa.h"
 #include "msm_engine.h"
+#include "host/par.h"
 
 struct bpp_transcript {
   merlin::Transcript t;
@@ -271,38 +272,46 @@ int ipa_q_slot(bpp_ctx* ctx, const bpp_gens* g, const uint8_t Q[32], uint32_t dt
                          hipMemcpyDeviceToDevice, ctx->stream));
   return BPP_OK;
 }
-// host extended point -> the device's P3 row (40 words: X, Y, Z, T in 10
-// limbs at bit offsets ceil(25.5 i), ge_io.cuh load_p3; canonical limbs)
-void p3_row_host(const h25519::ge& p, uint32_t w[P3_WORDS]) {
-  const h25519::fe* c = &p.X;
-  for (int e = 0; e < 4; ++e) {
-    const h25519::fe f = h25519::fe_canon(c[e]);
-    for (int k = 0; k < 5; ++k) {
-      w[10 * e + 2 * k] = (uint32_t)(f.v[k] & 0x3ffffffu);
-      w[10 * e + 2 * k + 1] = (uint32_t)(f.v[k] >> 26);
-    }
-  }
-}
-
-// Q as its doublings 2^j Q, j < 253, in device memory (IpaGens::qpow): the
-// fused rounds add c Q bit by bit inside their block trees, so no per-call
-// table is built for Q and g's Q slot (and its lock) is not used.  253
-// doublings on the host (the Q slot's window points took 248 of them).
-int ipa_q_powers(bpp_ctx* ctx, const uint8_t Q[32], const uint32_t** d_out) {
+// Q as its doublings 2^j Q, j < 253 (IpaGens::qpow): 253 doublings on the
+// host (the window points of a Q-slot table took 248), their Z inverses by
+// one field inversion, and the 253 Niels rows written over the start of g's
+// Q slot (the caller holds g->q_mu until the IPA has completed).  The fused
+// rounds then add c Q bit by bit (ipa.hip q_bits_*, DtLane::row_of_q): no
+// direct table is built for Q, where its build was 152 us of config 2.
+int ipa_q_powers(bpp_ctx* ctx, const bpp_gens* g, const uint8_t Q[32], uint32_t dt_c, const uint32_t** d_out) {
   h25519::ge P;
   if (!h25519::decode(P, Q)) {
     ctx->err = "Q does not decode";
     return BPP_ERR_DECOMPRESS;
   }
-  std::vector<uint32_t> rows((size_t)253 * P3_WORDS);
-  for (uint32_t j = 0; j < 253; ++j) {
-    p3_row_host(P, &rows[(size_t)j * P3_WORDS]);
+  constexpr uint32_t NB = 253;
+  std::vector<h25519::ge> pts(NB);
+  for (uint32_t j = 0; j < NB; ++j) {
+    pts[j] = P;
     P = h25519::ge_dbl(P);
   }
-  void* d = nullptr;
-  BPP_TRY(ctx_ws(ctx, "ipa_qpow", rows.size() * 4, &d));
-  BPP_TRY(ctx_h2d(ctx, d, rows.data(), rows.size() * 4));
-  *d_out = (const uint32_t*)d;
+  // the Niels rows in four chunks on the pool, one field inversion per chunk
+  // (Montgomery's trick): ~3/4 of the conversion's ~30 us off this thread
+  std::vector<uint32_t> rows((size_t)NB * MSM_NIELS_WORDS);
+  constexpr uint32_t NCH = 4;
+  par::for_each(NCH, [&](size_t c) {
+    const uint32_t j0 = (uint32_t)(NB * c / NCH), j1 = (uint32_t)(NB * (c + 1) / NCH);
+    std::vector<h25519::fe> pre(j1 - j0);
+    h25519::fe run = h25519::fe_one();
+    for (uint32_t j = j0; j < j1; ++j) {
+      pre[j - j0] = run;
+      run = h25519::fe_mul(run, pts[j].Z);  // (Z is never zero for a decoded point)
+    }
+    h25519::fe inv = h25519::fe_invert(run);
+    for (uint32_t j = j1; j-- > j0;) {
+      const h25519::fe zi = h25519::fe_mul(inv, pre[j - j0]);
+      inv = h25519::fe_mul(inv, pts[j].Z);
+      niels_row_host(pts[j], zi, &rows[(size_t)j * MSM_NIELS_WORDS]);
+    }
+  });
+  uint32_t* slot = g->d_dt + dt_bytes(g->qslot(), dt_c) / 4;
+  BPP_TRY(ctx_h2d(ctx, slot, rows.data(), rows.size() * 4));
+  *d_out = slot;
   return BPP_OK;
 }
 }  // namespace
@@ -347,14 +356,12 @@ static int ipa_prove_api(bpp_ctx* ctx, const bpp_gens* g, IpaTranscript* tr, con
     }();
     auto body = [&]() -> int {
       if (qslot) {
-        if (qpow_env) {
-          BPP_TRY(ipa_q_powers(ctx, Q, &ig.qpow));
-          ig.qidx = 0;  // (unused with qpow)
-        } else {
-          qlock = std::unique_lock<std::mutex>(g->q_mu);
+        qlock = std::unique_lock<std::mutex>(g->q_mu);
+        if (qpow_env)
+          BPP_TRY(ipa_q_powers(ctx, g, Q, ig.pts.dt_c, &ig.qpow));
+        else
           BPP_TRY(ipa_q_slot(ctx, g, Q, ig.pts.dt_c));
-          ig.qidx = g->qslot();
-        }
+        ig.qidx = g->qslot();
         static const bool zc_env = [] {
           const char* e = getenv("BPP_IPA_ZC_IN");
           return !e || atoi(e) != 0;

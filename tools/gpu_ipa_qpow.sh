@@ -1,6 +1,6 @@
 # round 6: Q as its doublings in the fused IPA rounds (BPP_IPA_QPOW, default on) vs the per-call Q-slot table -- parity, config 2 A/B, a trace
 set -o pipefail
-cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; O=gpurun_out/r06qp2; mkdir -p $O
+cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; O=gpurun_out/r06qp4; mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_gpu_ipa_hooks.py tests/test_gpu_protocol.py tests/test_golden_protocol.py tests/test_gpu_config4.py tests/test_gpu_perm.py tests/test_gpu_abi_c.py tests/test_gpu_compat.py tests/test_gpu_merlin.py -m gpu -x -v --timeout 200 --timeout-method thread > $O/tests.txt 2>&1 || { tail -40 $O/tests.txt; exit 1; }
 tail -1 $O/tests.txt
 BPP_IPA_QPOW=0 timeout -k 10 300 python -u -m pytest tests/test_gpu_ipa_hooks.py tests/test_gpu_protocol.py -m gpu -x -q --timeout 200 --timeout-method thread > $O/tests_qslot.txt 2>&1 || { tail -40 $O/tests_qslot.txt; exit 1; }

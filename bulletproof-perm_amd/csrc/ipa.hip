@@ -407,6 +407,10 @@ FE_INLINE void ipa_round_body(const uint32_t* __restrict__ dt, const DtGeom& dg,
     const DtLane ln = DtLane::make(dg, lt % dg.W);
     const uint32_t* __restrict__ tscs = tsl + 8 * ls * CS;
     const uint32_t* __restrict__ tgens = tgl + ls * CS;
+#ifdef EXP_IPA_NOWALK  // timing experiment only (wrong results): no walk, no tree
+    if (tid < S) store_p3(out_p3, (S == 2 ? 2 * inst * J + jp : bidx) + tid * J, ge_identity());
+    return;
+#endif
     // (QP: every slice walks its own share of c Q as the V virtual terms)
     const ge_p3 acc = tg < TG ? dt_walk<QP>(dt, dg, ln, tg, CS, TG,
                                             [&](uint32_t t, uint32_t sv[8], uint32_t& gen) {
@@ -417,6 +421,10 @@ FE_INLINE void ipa_round_body(const uint32_t* __restrict__ dt, const DtGeom& dg,
                                             ge_identity(), A.qrow0)
                               : ge_identity();
     __syncthreads();
+#ifdef EXP_IPA_NOTREE  // timing experiment only (wrong results): no block tree
+    if (lt == 0) store_p3(out_p3, (S == 2 ? 2 * inst * J + jp : bidx) + ls * J, acc);
+    return;
+#endif
     dt_block_tree_segs(lds, acc, nt, S, out_p3, S == 2 ? 2 * inst * J + jp : bidx, J);
     return;
   }

@@ -246,6 +246,8 @@ struct IpaRoundArgs {
   uint32_t split;   // J: blocks per L / R MSM, each walking a slice of its n + 1 terms
   const uint32_t* qpow;  // IpaGens::qpow (null: Q's term walked from its table rows)
   uint32_t qrow0;        // qpow's first row as a row of dt (the virtual terms' rows)
+  uint32_t *done_ticket, *done_word;  // the launch's completion flag (null: none)
+  uint32_t done_tag;
 };
 
 // QP (IpaGens::qpow): c Q for the Q term's scalar c with Q given as its 253
@@ -254,6 +256,23 @@ struct IpaRoundArgs {
 // Q term becomes V = ceil(253 / W) virtual terms carrying c, and lane w of
 // virtual term v adds 2^(vW + w) Q when that bit of c is set
 // (DtLane::row_of_q) -- walked like any other term.
+// The launch's completion flag (ctx_done_flag / ctx_wait_flag): after the
+// block's results are stored (all by wave 0, whose thread 0 runs this),
+// each block counts itself on the device ticket behind a system-scope
+// release; the last one re-zeroes the ticket and writes the tag to the
+// host's word.  Vector atomics and stores only.
+FE_INLINE void done_signal(uint32_t* ticket, uint32_t* word, uint32_t tag) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    if (atomicAdd(ticket, 1u) == gridDim.x - 1) {
+      atomicExch(ticket, 0u);
+      __threadfence_system();
+      __hip_atomic_store(word, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 template <bool QP>  // QP: Q by its doublings (A.qpow), a separate instantiation (VGPRs)
 FE_INLINE void ipa_round_body(const uint32_t* __restrict__ dt, const DtGeom& dg, uint32_t n, uint32_t TG,
                               const IpaRoundArgs& A, uint32_t bidx, uint32_t* lds, uint32_t S) {
@@ -347,21 +366,6 @@ FE_INLINE void ipa_round_body(const uint32_t* __restrict__ dt, const DtGeom& dg,
       }
       return f;
     };
-    // (i) this block's share of the next state (the side-0 blocks of S = 1)
-    if ((fold || init) && (S == 2 || side0 == 0)) {
-      const uint32_t q0 = (uint32_t)((uint64_t)jp * 2 * m / J), q1 = (uint32_t)((uint64_t)(jp + 1) * 2 * m / J);
-      for (uint32_t q = q0 + tid; q < q1; q += nt) {
-        const bool isb = q >= m;
-        const uint32_t p = isb ? q - m : q;
-        sc_store((isb ? bm_out : am_out) + 8 * (ib + p), cur_ab(isb, p));
-      }
-      const uint32_t f0 = (uint32_t)((uint64_t)jp * 2 * n / J), f1 = (uint32_t)((uint64_t)(jp + 1) * 2 * n / J);
-      for (uint32_t q = f0 + tid; q < f1; q += nt) {
-        const bool ish = q >= n;
-        const uint32_t k = ish ? q - n : q;
-        sc_store((ish ? fH_out : fG_out) + 8 * (ib + k), factor(ish, k));
-      }
-    }
     // (ii) the slice's term scalars: side slots [t0, t1) of [0, n) (G terms
     // below n / 2, H terms above), local slot cnt = the Q term
     const uint32_t t0 = (uint32_t)((uint64_t)jp * n / J), t1 = (uint32_t)((uint64_t)(jp + 1) * n / J);
@@ -426,6 +430,25 @@ FE_INLINE void ipa_round_body(const uint32_t* __restrict__ dt, const DtGeom& dg,
     return;
 #endif
     dt_block_tree_segs(lds, acc, nt, S, out_p3, S == 2 ? 2 * inst * J + jp : bidx, J);
+    if (A.done_word) done_signal(A.done_ticket, A.done_word, A.done_tag);
+    // (i) this block's share of the next state (the side-0 blocks of S = 1),
+    // written after the block's L / R partial and the completion flag: the
+    // next round reads it only after this launch has ended, so its loads and
+    // multiplies overlap the host's round step instead of preceding it
+    if ((fold || init) && (S == 2 || side0 == 0)) {
+      const uint32_t q0 = (uint32_t)((uint64_t)jp * 2 * m / J), q1 = (uint32_t)((uint64_t)(jp + 1) * 2 * m / J);
+      for (uint32_t q = q0 + tid; q < q1; q += nt) {
+        const bool isb = q >= m;
+        const uint32_t p = isb ? q - m : q;
+        sc_store((isb ? bm_out : am_out) + 8 * (ib + p), cur_ab(isb, p));
+      }
+      const uint32_t f0 = (uint32_t)((uint64_t)jp * 2 * n / J), f1 = (uint32_t)((uint64_t)(jp + 1) * 2 * n / J);
+      for (uint32_t q = f0 + tid; q < f1; q += nt) {
+        const bool ish = q >= n;
+        const uint32_t k = ish ? q - n : q;
+        sc_store((ish ? fH_out : fG_out) + 8 * (ib + k), factor(ish, k));
+      }
+    }
     return;
   }
   // 1. a, b of this round (length m) into LDS: item q < m is a_q, q >= m is
@@ -532,23 +555,7 @@ FE_INLINE void ipa_round_body(const uint32_t* __restrict__ dt, const DtGeom& dg,
 #endif
   // result of side s: out_p3[(2 inst + s) J + jp] (= bidx for S = 1)
   dt_block_tree_segs(lds, acc, nt, S, out_p3, S == 2 ? 2 * inst * J + jp : bidx, J);
-}
-
-// The launch's completion flag (ctx_done_flag / ctx_wait_flag): after the
-// block's results are stored (all by wave 0, whose thread 0 runs this),
-// each block counts itself on the device ticket behind a system-scope
-// release; the last one re-zeroes the ticket and writes the tag to the
-// host's word.  Vector atomics and stores only.
-FE_INLINE void done_signal(uint32_t* ticket, uint32_t* word, uint32_t tag) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence_system();
-    if (atomicAdd(ticket, 1u) == gridDim.x - 1) {
-      atomicExch(ticket, 0u);
-      __threadfence_system();
-      __hip_atomic_store(word, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
+  if (A.done_word) done_signal(A.done_ticket, A.done_word, A.done_tag);
 }
 
 template <bool QP>
@@ -572,8 +579,10 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
   A.split = J;
   A.qpow = qpow;
   A.qrow0 = qpow ? (uint32_t)((size_t)(qpow - dt) / MSM_NIELS_WORDS) : 0u;  // (qpow lies inside dt)
+  A.done_ticket = done_ticket;
+  A.done_word = done_word;
+  A.done_tag = done_tag;
   ipa_round_body<QP>(dt, dg, n, TG, A, blockIdx.x, lds, S);
-  if (done_word) done_signal(done_ticket, done_word, done_tag);
 }
 
 // Several batches' rounds in one launch (BPP_IPA_MERGE, the shared-launch
@@ -953,6 +962,8 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
         A.split = J;
         A.qpow = g.qpow;
         A.qrow0 = 0;  // (merged launches never carry qpow: merge is off with it)
+        A.done_ticket = A.done_word = nullptr;
+        A.done_tag = 0;
         req.dt = g.pts.dt;
         req.dg = dg;
         req.n = n;

@@ -248,6 +248,15 @@ struct IpaRoundArgs {
   uint32_t qrow0;        // qpow's first row as a row of dt (the virtual terms' rows)
   uint32_t *done_ticket, *done_word;  // the launch's completion flag (null: none)
   uint32_t done_tag;
+  // P = 1: the challenge's words u R, u^-1 R by value (kernel arguments)
+  // instead of a load from pinned host memory at the head of the round
+  uint32_t u1;
+  sc u1m, u1im;
+};
+
+// u R, u^-1 R of a one-instance round, passed by value (IpaRoundArgs::u1)
+struct IpaU1 {
+  uint32_t w[16];
 };
 
 // QP (IpaGens::qpow): c Q for the Q term's scalar c with Q given as its 253
@@ -321,8 +330,8 @@ FE_INLINE void ipa_round_body(const uint32_t* __restrict__ dt, const DtGeom& dg,
   const bool writer = (fold || init) && side0 == 0 && jp == 0;
   sc um = sc_zero(), uim = sc_zero();
   if (fold) {
-    um = sc_load(u + 16 * inst);
-    uim = sc_load(u + 16 * inst + 8);
+    um = A.u1 ? A.u1m : sc_load(u + 16 * inst);
+    uim = A.u1 ? A.u1im : sc_load(u + 16 * inst + 8);
   }
 #ifndef IPA_SPLIT_PROLOGUE
 #define IPA_SPLIT_PROLOGUE 1
@@ -567,7 +576,8 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
     const uint32_t* __restrict__ qmul, uint32_t gbase, uint32_t hbase, uint32_t qidx, uint32_t TG, uint32_t halve,
     uint32_t* __restrict__ out_p3, const uint32_t* __restrict__ a0, const uint32_t* __restrict__ b0,
     const uint32_t* __restrict__ gf0, const uint32_t* __restrict__ hf0, uint32_t init, uint32_t J, uint32_t S,
-    const uint32_t* __restrict__ qpow, uint32_t* done_ticket, uint32_t* done_word, uint32_t done_tag) {
+    const uint32_t* __restrict__ qpow, uint32_t* done_ticket, uint32_t* done_word, uint32_t done_tag,
+    uint32_t u1, IpaU1 u1w) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   IpaRoundArgs A;
   A.am_in = am_in; A.bm_in = bm_in; A.fG_in = fG_in; A.fH_in = fH_in;
@@ -582,6 +592,11 @@ __global__ void __launch_bounds__(DT_NT_MAX) k_ipa_round_dt(
   A.done_ticket = done_ticket;
   A.done_word = done_word;
   A.done_tag = done_tag;
+  A.u1 = u1;
+  _Pragma("unroll") for (int i = 0; i < 8; ++i) {
+    A.u1m.v[i] = u1w.w[i];
+    A.u1im.v[i] = u1w.w[8 + i];
+  }
   ipa_round_body<QP>(dt, dg, n, TG, A, blockIdx.x, lds, S);
 }
 
@@ -964,6 +979,7 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
         A.qrow0 = 0;  // (merged launches never carry qpow: merge is off with it)
         A.done_ticket = A.done_word = nullptr;
         A.done_tag = 0;
+        A.u1 = 0;
         req.dt = g.pts.dt;
         req.dg = dg;
         req.n = n;
@@ -977,6 +993,17 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
       } else {
         ProfScope ps(ctx, "ipa_round_dt");  // (bench.py: this kernel's own roofline)
         if (use_flag) BPP_TRY(ctx_done_flag(ctx, &done_ticket, &done_word, &done_tag));
+        // one instance: its u words as kernel arguments (the host wrote them
+        // after the last round; BPP_IPA_U_ARG=0: read in place).  Config 2
+        // best of four 0.795 vs 0.804 ms, within the run-to-run noise
+        // (r06_ipa_uarg_ab.txt)
+        static const bool u1_env = [] {
+          const char* e = getenv("BPP_IPA_U_ARG");
+          return !e || atoi(e) != 0;
+        }();
+        const bool u1 = P == 1 && zc && round > 0 && u1_env;
+        IpaU1 u1w{};
+        if (u1) memcpy(u1w.w, h_uw, sizeof u1w.w);
         hipLaunchKernelGGL(g.qpow ? k_ipa_round_dt<true> : k_ipa_round_dt<false>, dim3(2 / sides * P * J),
                            dim3(sides * nt),
                            ipa_round_lds_words(n, sides * nt, sides, g.qpow ? (253u + dg.W - 1) / dg.W : 1u) * 4,
@@ -986,7 +1013,7 @@ int ipa_prove_batch_dev(bpp_ctx* ctx, const std::vector<merlin::Transcript*>& tr
                            S[round ? outs : in][3], (const uint32_t*)d_u, (const uint32_t*)d_q, g.gbase, g.hbase,
                            g.qidx, TG, dev_merlin ? 0u : 1u, (uint32_t*)(dev_jsum ? d_part : d_res), d_a, d_b,
                            d_Gf, d_Hf, round ? 0u : 1u, J, sides, g.qpow, done_ticket,
-                           use_flag ? done_word : nullptr, done_tag);
+                           use_flag ? done_word : nullptr, done_tag, u1 ? 1u : 0u, u1w);
         if (dev_jsum)
           hipLaunchKernelGGL(k_ipa_jsum, dim3(2 * P), dim3(J), (size_t)J * P3_BYTES, ctx->stream,
                              (const uint32_t*)d_part, J, (uint32_t*)d_res);
